@@ -1,0 +1,95 @@
+"""ctypes binding of libnbx.so (include/nbx.h).
+
+The product path has NO CPU fallback: every op goes through this library and
+raises if it is missing or if a tensor is not on a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnbx.so")
+ABI_VERSION = 1
+MAX_LAYERS = 64
+
+c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double,
+                                     ctypes.c_void_p, ctypes.c_size_t)
+
+
+class SegnnLayer(ctypes.Structure):
+    _fields_ = [(n, c_p) for n in (
+        "node_pre_s_t", "node_pre_v_t", "msg1_amf", "msg1_bias", "msg2_s_t", "msg2_v_t", "msg2_bias",
+        "upd1_s_t", "upd1_v_t", "upd1_bias", "upd2_s_t", "upd2_v_t", "upd2_bias",
+        "msg_bn_weight", "msg_bn_bias", "msg_bn_running_mean", "msg_bn_running_var",
+        "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var")]
+
+
+class SegnnWeights(ctypes.Structure):
+    _fields_ = [("mul", c_i32), ("num_layers", c_i32), ("training", c_i32), ("bn_eps", c_f),
+                ("bn_momentum", c_f)] + [(n, c_p) for n in (
+                    "emb", "emb_bias", "pp1_s_t", "pp1_v_t", "pp1_bias", "pp2")] + [
+                ("layers", SegnnLayer * MAX_LAYERS)]
+
+
+_SIGNATURES = {
+    "nbx_abi_version": (ctypes.c_int, []),
+    "nbx_last_error": (ctypes.c_char_p, []),
+    "nbx_fc_edge_index": (ctypes.c_int, [c_i64, c_i64, c_p, c_p]),
+    "nbx_knn_edge_index": (ctypes.c_int, [c_p, c_i32, c_i64, c_i64, c_i64, c_p, c_p]),
+    "nbx_gravity_acceleration": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_d, c_d, c_p, c_p]),
+    "nbx_gravity_sample": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_d, c_d, c_d,
+                                          c_p, c_p, c_p, c_p]),
+    "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
+    "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
+                                         c_p, c_sz, c_p]),
+    "nbx_segnn_forward_timed": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
+                                               c_p, c_sz, c_p, ctypes.POINTER(c_f), ctypes.POINTER(c_i32),
+                                               ctypes.POINTER(c_d), ctypes.POINTER(c_f)]),
+    "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
+                                         c_p, c_p, c_p, c_sz, c_p]),
+}
+
+_lib = None
+
+
+class NbxError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libnbx.so (once).  Raises NbxError if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NbxError(f"HIP extension not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype, fn.argtypes = res, args
+        if handle.nbx_abi_version() != ABI_VERSION:
+            raise NbxError("libnbx ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise NbxError(f"{what}: {lib().nbx_last_error().decode()} (code {rc})")
+
+
+def dev_ptr(t: torch.Tensor, dtype=None) -> int:
+    """Device pointer of a contiguous HIP tensor (raises on CPU tensors: no fallback)."""
+    if not t.is_cuda:
+        raise NbxError("nbx ops run on the HIP device only; got a CPU tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise NbxError(f"expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise NbxError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,149 @@
+// A20-A22 — GravitySim softened-gravity leapfrog (datasets/nbody/dataset/synthetic_sim.py:305-420), fp64.
+//
+// Layout: one thread per body, floor(256/N) systems per 256-thread workgroup
+// (one system per workgroup when N > 256).  The current positions of the
+// workgroup's systems live in LDS; the whole T-step KDK loop runs inside the
+// kernel, so HBM only sees the initial state, the sampled frames and the final
+// state.  Per step each body does N softened interactions (FP64 VALU bound).
+#include "nbx_internal.h"
+
+namespace {
+
+// a_i = G * sum_j ((x_j - x_i) * r^-3) * m_j, r^2 = |x_j - x_i|^2 + eps^2 (synthetic_sim.py:318-340)
+__device__ inline void accel_from_lds(const double* __restrict__ sp, const double* __restrict__ sm, int N, int i,
+                                      double G, double soft2, double& ax, double& ay, double& az) {
+    const double xi = sp[3 * i], yi = sp[3 * i + 1], zi = sp[3 * i + 2];
+    double sx = 0.0, sy = 0.0, sz = 0.0;
+    for (int j = 0; j < N; ++j) {
+        const double dx = sp[3 * j] - xi, dy = sp[3 * j + 1] - yi, dz = sp[3 * j + 2] - zi;
+        const double r2 = dx * dx + dy * dy + dz * dz + soft2;
+        const double inv = r2 > 0.0 ? 1.0 / (r2 * sqrt(r2)) : r2;
+        const double mj = sm[j];
+        sx += (dx * inv) * mj;
+        sy += (dy * inv) * mj;
+        sz += (dz * inv) * mj;
+    }
+    ax = G * sx;
+    ay = G * sy;
+    az = G * sz;
+}
+
+__global__ void gravity_accel_kernel(const double* __restrict__ pos, const double* __restrict__ mass, int64_t S, int N,
+                                     int spb, double G, double soft2, double* __restrict__ acc) {
+    extern __shared__ double lds[];
+    double* sp = lds;                 // [spb][N][3]
+    double* sm = lds + 3 * spb * N;   // [spb][N]
+    const int local = threadIdx.x / N, i = threadIdx.x % N;
+    const int64_t s = (int64_t)blockIdx.x * spb + local;
+    const bool live = local < spb && s < S;
+    if (live) {
+        for (int c = 0; c < 3; ++c) sp[(local * N + i) * 3 + c] = pos[(s * N + i) * 3 + c];
+        sm[local * N + i] = mass[s * N + i];
+    }
+    __syncthreads();
+    if (!live) return;
+    double ax, ay, az;
+    accel_from_lds(sp + local * N * 3, sm + local * N, N, i, G, soft2, ax, ay, az);
+    acc[(s * N + i) * 3 + 0] = ax;
+    acc[(s * N + i) * 3 + 1] = ay;
+    acc[(s * N + i) * 3 + 2] = az;
+}
+
+__global__ void gravity_sample_kernel(double* __restrict__ pos, double* __restrict__ vel,
+                                      const double* __restrict__ mass, int64_t S, int N, int spb, int64_t T,
+                                      int64_t freq, double dt, double G, double soft2, double* __restrict__ pos_save,
+                                      double* __restrict__ vel_save, double* __restrict__ force_save) {
+    extern __shared__ double lds[];
+    double* sp = lds;
+    double* sm = lds + 3 * spb * N;
+    const int local = threadIdx.x / N, i = threadIdx.x % N;
+    const int64_t s = (int64_t)blockIdx.x * spb + local;
+    const bool live = local < spb && s < S;
+    const int64_t Ts = T / freq;
+    double x = 0, y = 0, z = 0, vx = 0, vy = 0, vz = 0, m = 0;
+    if (live) {
+        x = pos[(s * N + i) * 3 + 0];
+        y = pos[(s * N + i) * 3 + 1];
+        z = pos[(s * N + i) * 3 + 2];
+        vx = vel[(s * N + i) * 3 + 0];
+        vy = vel[(s * N + i) * 3 + 1];
+        vz = vel[(s * N + i) * 3 + 2];
+        m = mass[s * N + i];
+        sp[(local * N + i) * 3 + 0] = x;
+        sp[(local * N + i) * 3 + 1] = y;
+        sp[(local * N + i) * 3 + 2] = z;
+        sm[local * N + i] = m;
+    }
+    __syncthreads();
+    double ax = 0, ay = 0, az = 0;
+    if (live) accel_from_lds(sp + local * N * 3, sm + local * N, N, i, G, soft2, ax, ay, az);
+    const double hdt = dt / 2.0;
+    int64_t c = 0;
+    for (int64_t t = 0; t < T; ++t) {
+        if (live && t % freq == 0) {
+            const int64_t o = ((s * Ts + c) * N + i) * 3;
+            pos_save[o] = x; pos_save[o + 1] = y; pos_save[o + 2] = z;
+            vel_save[o] = vx; vel_save[o + 1] = vy; vel_save[o + 2] = vz;
+            force_save[o] = ax * m; force_save[o + 1] = ay * m; force_save[o + 2] = az * m;
+            ++c;
+        }
+        // (1/2) kick, drift
+        vx += ax * hdt; vy += ay * hdt; vz += az * hdt;
+        x += vx * dt; y += vy * dt; z += vz * dt;
+        __syncthreads();  // everyone finished reading the previous positions
+        if (live) {
+            sp[(local * N + i) * 3 + 0] = x;
+            sp[(local * N + i) * 3 + 1] = y;
+            sp[(local * N + i) * 3 + 2] = z;
+        }
+        __syncthreads();
+        if (live) accel_from_lds(sp + local * N * 3, sm + local * N, N, i, G, soft2, ax, ay, az);
+        // (1/2) kick
+        vx += ax * hdt; vy += ay * hdt; vz += az * hdt;
+    }
+    if (live) {
+        pos[(s * N + i) * 3 + 0] = x; pos[(s * N + i) * 3 + 1] = y; pos[(s * N + i) * 3 + 2] = z;
+        vel[(s * N + i) * 3 + 0] = vx; vel[(s * N + i) * 3 + 1] = vy; vel[(s * N + i) * 3 + 2] = vz;
+    }
+}
+
+void launch_geometry(int64_t N, int& spb, int& threads) {
+    if (N <= 256) {
+        spb = (int)(256 / N);
+        threads = ((spb * (int)N + 63) / 64) * 64;
+    } else {
+        spb = 1;
+        threads = (int)(((N + 63) / 64) * 64);
+    }
+}
+
+}  // namespace
+
+extern "C" int nbx_gravity_acceleration(const double* pos, const double* mass, int64_t S, int64_t N, double G,
+                                        double softening, double* acc, void* stream) {
+    NBX_CHECK_ARG(S >= 0 && N >= 1 && N <= 1024, "nbx_gravity_acceleration: need 1 <= N <= 1024");
+    if (S == 0) return NBX_OK;
+    int spb, threads;
+    launch_geometry(N, spb, threads);
+    const size_t lds = sizeof(double) * 4 * spb * N;
+    hipLaunchKernelGGL(gravity_accel_kernel, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
+                       (hipStream_t)stream, pos, mass, S, (int)N, spb, G, softening * softening, acc);
+    NBX_LAUNCH_CHECK("gravity_accel_kernel");
+    return NBX_OK;
+}
+
+extern "C" int nbx_gravity_sample(double* pos, double* vel, const double* mass, int64_t S, int64_t N, int64_t T,
+                                  int64_t sample_freq, double dt, double G, double softening, double* pos_save,
+                                  double* vel_save, double* force_save, void* stream) {
+    NBX_CHECK_ARG(S >= 0 && N >= 1 && N <= 1024, "nbx_gravity_sample: need 1 <= N <= 1024");
+    NBX_CHECK_ARG(sample_freq > 0 && T >= 0 && T % sample_freq == 0, "nbx_gravity_sample: T %% sample_freq != 0");
+    if (S == 0) return NBX_OK;
+    int spb, threads;
+    launch_geometry(N, spb, threads);
+    const size_t lds = sizeof(double) * 4 * spb * N;
+    hipLaunchKernelGGL(gravity_sample_kernel, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
+                       (hipStream_t)stream, pos, vel, mass, S, (int)N, spb, T, sample_freq, dt, G,
+                       softening * softening, pos_save, vel_save, force_save);
+    NBX_LAUNCH_CHECK("gravity_sample_kernel");
+    return NBX_OK;
+}

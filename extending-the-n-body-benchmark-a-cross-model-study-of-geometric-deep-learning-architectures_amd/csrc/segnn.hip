@@ -1,0 +1,651 @@
+// SEGNN forward + device-resident self-feed rollout (fp32).
+//
+// Reference: models/segnn/segnn.py:17-304, models/segnn/o3_building_blocks.py:10-278,
+// helper_scripts/infer_self_feed.py:99-194.  Math restated in DESIGN.md §SEGNN.
+//
+// Data layout in HBM (V = B*N nodes, E = V*(N-1) edges, M = mul):
+//   X    [4][V][M]   node features, plane 0 = 0e channels, planes 1..3 = x/y/z of 1o channels
+//   NA   [V][4]      node attribute (1, na_x, na_y, na_z)  (na_0 forced to 1: catch_isolated_nodes)
+//   EG   [E][8]      per edge (dst-major): rhat xyz, |rel|, m_src*m_dst
+//   edges are enumerated dst-major: e = dst*(N-1) + q, src = the q-th other node of the system,
+//   so the N-1 messages into a node are contiguous (aggregation without atomics).
+// Every O(3) tensor product with l <= 1 is split into a "scalar-row" GEMM
+// [x_s | x_v.y] -> [s | t] and a "vector-row" GEMM x_v[:,k] -> v (one row per
+// component); the constants of e3nn's path normalisation, the SEGNN rescale and
+// the spherical-harmonic prefactors are folded into the packed weights.
+// The x_i / x_j halves of message_layer_1 are linear in node features, so they
+// are computed once per node (node_pre GEMM) and combined per edge.
+#include <vector>
+
+#include "gemm_f32.h"
+#include "nbx_internal.h"
+
+namespace {
+
+using nbx::kC_SIGMOID;
+using nbx::kC_SILU;
+using nbx::kSH_C1;
+
+__device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
+__device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Elementwise kernels use block (32, 8): threadIdx.x = channel within a 32-chunk,
+// threadIdx.y = row lane; a block covers ROWS_PER_BLOCK rows x 32 channels.
+constexpr int EW_X = 32, EW_Y = 8, ROWS_PER_BLOCK = 64;
+
+// ---------------------------------------------------------------- featurise
+// O3Transform (o3_building_blocks.py:231-278) + catch_isolated_nodes (segnn.py:136-148)
+__global__ void featurize_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
+                                 const float* __restrict__ mass, int64_t V, int N, float* __restrict__ NA,
+                                 float* __restrict__ X0, float* __restrict__ EG) {
+    const int64_t node = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (node >= V) return;
+    const int64_t b = node / N;
+    const int d = (int)(node - b * N);
+    const float px = pos[3 * node], py = pos[3 * node + 1], pz = pos[3 * node + 2];
+    const float vx = vel[3 * node], vy = vel[3 * node + 1], vz = vel[3 * node + 2];
+    const float m = mass[node];
+    float sx = 0.f, sy = 0.f, sz = 0.f;
+    for (int q = 0; q < N - 1; ++q) {
+        const int64_t s = b * N + (q < d ? q : q + 1);
+        const float rx = pos[3 * s] - px, ry = pos[3 * s + 1] - py, rz = pos[3 * s + 2] - pz;
+        const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+        const float den = fmaxf(dist, 1e-12f);
+        const float hx = rx / den, hy = ry / den, hz = rz / den;
+        float* eg = EG + (node * (N - 1) + q) * 8;
+        eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s] * m;
+        sx += kSH_C1 * hx; sy += kSH_C1 * hy; sz += kSH_C1 * hz;
+    }
+    const float cnt = (float)(N - 1 > 0 ? N - 1 : 1);
+    const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
+    const float vden = fmaxf(vn, 1e-12f);
+    NA[4 * node + 0] = 1.0f;
+    NA[4 * node + 1] = sx / cnt + kSH_C1 * (vx / vden);
+    NA[4 * node + 2] = sy / cnt + kSH_C1 * (vy / vden);
+    NA[4 * node + 3] = sz / cnt + kSH_C1 * (vz / vden);
+    const float mp = (px + py + pz) / 3.0f;  // pos.mean(1): mean over xyz (reference quirk)
+    float* x0 = X0 + 8 * node;
+    x0[0] = px - mp; x0[1] = py - mp; x0[2] = pz - mp;
+    x0[3] = vx; x0[4] = vy; x0[5] = vz; x0[6] = vn; x0[7] = 0.f;
+}
+
+// embedding_layer: O3TensorProduct(2x1o+1x0e -> hidden, node attrs) (segnn.py:69-71,170)
+__global__ void embed_kernel(const float* __restrict__ X0, const float* __restrict__ NA,
+                             const float* __restrict__ emb, const float* __restrict__ emb_b, int64_t V, int M,
+                             float* __restrict__ X) {
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    if (w >= M) return;
+    const float a0 = emb[w], a1 = emb[M + w], b0 = emb[2 * M + w], b1 = emb[3 * M + w];
+    const float c = emb[4 * M + w], dd = emb[5 * M + w], bias = emb_b[w];
+    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+        const float* x0 = X0 + 8 * n;
+        const float* na = NA + 4 * n;
+        const float u0n = x0[0] * na[1] + x0[1] * na[2] + x0[2] * na[3];
+        const float u1n = x0[3] * na[1] + x0[4] * na[2] + x0[5] * na[3];
+        X[n * M + w] = b0 * u0n + b1 * u1n + c * x0[6] + bias;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) X[((1 + k) * V + n) * M + w] = a0 * x0[k] + a1 * x0[3 + k] + dd * x0[6] * na[1 + k];
+    }
+}
+
+// ---------------------------------------------------------------- message
+// message_layer_1 per (edge, channel) from the per-node precomputation NP
+// NP rows: [V scalar rows | 3V vector rows] x 6M columns:
+//   scalar row  [P_dst(2M) | R_dst(M) | P_src(2M) | R_src(M)]
+//   vector row  [Q_dst(2M) | S_dst(M) | Q_src(2M) | S_src(M)]
+// then Gate -> M1S [E][2M] = [m_s | m_v . rhat], M1V [3][E][M] = m_v
+__global__ void msg1_kernel(const float* __restrict__ NP, const float* __restrict__ EG,
+                            const float* __restrict__ amfw, const float* __restrict__ bias, int64_t V, int N, int M,
+                            float* __restrict__ M1S, float* __restrict__ M1V) {
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    if (w >= M) return;
+    const int64_t E = V * (N - 1);
+    const int ld = 6 * M;
+    const float ea0 = amfw[w], eg0 = amfw[M + w], et0 = amfw[2 * M + w];
+    const float ea1 = amfw[3 * M + w], eg1 = amfw[4 * M + w], et1 = amfw[5 * M + w];
+    const float ba = bias[w], bg = bias[M + w];
+    for (int64_t e = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; e < E && e < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; e += EW_Y) {
+        const int64_t dn = e / (N - 1);
+        const int q = (int)(e - dn * (N - 1));
+        const int64_t b = dn / N;
+        const int d = (int)(dn - b * N);
+        const int64_t sn = b * N + (q < d ? q : q + 1);
+        const float* eg = EG + e * 8;
+        const float hx = eg[0], hy = eg[1], hz = eg[2], dist = eg[3], pm = eg[4];
+        const float* sd = NP + dn * ld;
+        const float* ss = NP + sn * ld;
+        float sa = sd[w] + ss[3 * M + w] + ea0 * dist + ea1 * pm + ba;
+        float sg = sd[M + w] + ss[4 * M + w] + eg0 * dist + eg1 * pm + bg;
+        const float t = sd[2 * M + w] + ss[5 * M + w] + et0 * dist + et1 * pm;
+        float v[3];
+        const float hk[3] = {hx, hy, hz};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float* vd = NP + ((1 + k) * V + dn) * ld;
+            const float* vs = NP + ((1 + k) * V + sn) * ld;
+            sa += hk[k] * (vd[w] + vs[3 * M + w]);
+            sg += hk[k] * (vd[M + w] + vs[4 * M + w]);
+            v[k] = hk[k] * t + vd[2 * M + w] + vs[5 * M + w];
+        }
+        const float g = kC_SIGMOID * sigmoid_f(sg);
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float mv = g * v[k];
+            M1V[((int64_t)k * E + e) * M + w] = mv;
+            dot += mv * hk[k];
+        }
+        M1S[e * 2 * M + w] = kC_SILU * silu_f(sa);
+        M1S[e * 2 * M + M + w] = dot;
+    }
+}
+
+// message_layer_2 epilogue: bias + Gate, aggregation over the N-1 in-edges
+// (aggr="add" at edge_index[1]) and per-block BatchNorm partial sums
+// (sum m_s, sum m_s^2, sum |m_v|^2) in fp64.
+__global__ void msg2_epi_kernel(const float* __restrict__ G2S, const float* __restrict__ G2V,
+                                const float* __restrict__ EG, const float* __restrict__ bias, int64_t V, int N, int M,
+                                float* __restrict__ AGG, double* __restrict__ partial) {
+    __shared__ double red[3][EW_Y][EW_X];
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    const int64_t E = V * (N - 1);
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if (w < M) {
+        const float ba = bias[w], bg = bias[M + w];
+        for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+            float as = 0.f, av0 = 0.f, av1 = 0.f, av2 = 0.f;
+            for (int q = 0; q < N - 1; ++q) {
+                const int64_t e = n * (N - 1) + q;
+                const float* g = G2S + e * 3 * M;
+                const float* eg = EG + e * 8;
+                const float ms = kC_SILU * silu_f(g[w] + ba);
+                const float gg = kC_SIGMOID * sigmoid_f(g[M + w] + bg);
+                const float t = g[2 * M + w];
+                const float m0 = gg * (eg[0] * t + G2V[(0 * E + e) * M + w]);
+                const float m1 = gg * (eg[1] * t + G2V[(1 * E + e) * M + w]);
+                const float m2 = gg * (eg[2] * t + G2V[(2 * E + e) * M + w]);
+                as += ms; av0 += m0; av1 += m1; av2 += m2;
+                s1 += (double)ms;
+                s2 += (double)ms * (double)ms;
+                s3 += (double)m0 * m0 + (double)m1 * m1 + (double)m2 * m2;
+            }
+            AGG[n * M + w] = as;
+            AGG[(1 * V + n) * M + w] = av0;
+            AGG[(2 * V + n) * M + w] = av1;
+            AGG[(3 * V + n) * M + w] = av2;
+        }
+    }
+    red[0][threadIdx.y][threadIdx.x] = s1;
+    red[1][threadIdx.y][threadIdx.x] = s2;
+    red[2][threadIdx.y][threadIdx.x] = s3;
+    __syncthreads();
+    if (threadIdx.y < 3 && w < M) {
+        double acc = 0.0;
+        for (int y = 0; y < EW_Y; ++y) acc += red[threadIdx.y][y][threadIdx.x];
+        partial[((int64_t)blockIdx.x * 3 + threadIdx.y) * M + w] = acc;
+    }
+}
+
+// e3nn BatchNorm (train mode) finalisation: one 64-lane group per channel
+// reduces the per-block partials in a fixed order, then computes
+// scale/shift and the running-stat update r <- (1-m) r + m * batch_stat.
+// coef layout: [0..2M) scale (0e then 1o channels), [2M..3M) shift (0e).
+__global__ void bn_finalize_kernel(const double* __restrict__ partial, int nblk, double count, int M, int training,
+                                   float eps, float momentum, const float* __restrict__ weight,
+                                   const float* __restrict__ bias, float* __restrict__ rmean,
+                                   float* __restrict__ rvar, float* __restrict__ coef) {
+    const int group = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (group >= 2 * M) return;
+    const bool scalar = group < M;
+    const int c = scalar ? group : group - M;
+    double a = 0.0, b = 0.0;
+    if (training) {
+        for (int i = lane; i < nblk; i += 64) {
+            if (scalar) {
+                a += partial[((int64_t)i * 3 + 0) * M + c];
+                b += partial[((int64_t)i * 3 + 1) * M + c];
+            } else {
+                a += partial[((int64_t)i * 3 + 2) * M + c];
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+        }
+    }
+    if (lane != 0) return;
+    if (scalar) {
+        double mu, var;
+        if (training) {
+            mu = a / count;
+            var = b / count - mu * mu;
+            if (var < 0.0) var = 0.0;
+            rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mu;
+            rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)var;
+        } else {
+            mu = rmean[c];
+            var = rvar[c];
+        }
+        const float sc = (float)(1.0 / sqrt(var + (double)eps)) * weight[c];
+        coef[c] = sc;
+        coef[2 * M + c] = bias[c] - sc * (float)mu;
+    } else {
+        double n;
+        if (training) {
+            n = a / (3.0 * count);
+            rvar[M + c] = (1.0f - momentum) * rvar[M + c] + momentum * (float)n;
+        } else {
+            n = rvar[M + c];
+        }
+        coef[M + c] = (float)(1.0 / sqrt(n + (double)eps)) * weight[M + c];
+    }
+}
+
+// ---------------------------------------------------------------- update
+// message BatchNorm applied to the aggregate (BN is affine per channel, so
+// sum_j BN(m_ij) = scale * sum_j m_ij + deg * shift), then the update_layer_1
+// GEMM inputs: U1S [V][4M] = [x_s | a_s | x_v.na | a_v.na], U1V [3][V][2M] = [x_v[:,k] | a_v[:,k]]
+__global__ void upd_pre_kernel(const float* __restrict__ X, const float* __restrict__ AGG,
+                               const float* __restrict__ NA, const float* __restrict__ coef, float deg, int64_t V,
+                               int M, float* __restrict__ U1S, float* __restrict__ U1V) {
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    if (w >= M) return;
+    const float sc_s = coef[w], sc_v = coef[M + w], sh = coef[2 * M + w] * deg;
+    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+        const float* na = NA + 4 * n;
+        const float xs = X[n * M + w];
+        const float as = sc_s * AGG[n * M + w] + sh;
+        float xdot = 0.f, adot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float xv = X[((1 + k) * V + n) * M + w];
+            const float av = sc_v * AGG[((1 + k) * V + n) * M + w];
+            xdot += xv * na[1 + k];
+            adot += av * na[1 + k];
+            U1V[((int64_t)k * V + n) * 2 * M + w] = xv;
+            U1V[((int64_t)k * V + n) * 2 * M + M + w] = av;
+        }
+        float* u = U1S + n * 4 * M;
+        u[w] = xs; u[M + w] = as; u[2 * M + w] = xdot; u[3 * M + w] = adot;
+    }
+}
+
+// Gate epilogue of a (scalar-row [s(2M) | t(M)], vector-row v) TP with node
+// attributes: h_s = c*SiLU(s+b), h_v = c*sigmoid(g+b) (na_k t + v);
+// writes the next TP's inputs U2S [V][2M] = [h_s | h_v.na], U2V [3][V][M] = h_v.
+__global__ void node_gate_kernel(const float* __restrict__ GS, const float* __restrict__ GV,
+                                 const float* __restrict__ NA, const float* __restrict__ bias, int64_t V, int M,
+                                 float* __restrict__ U2S, float* __restrict__ U2V) {
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    if (w >= M) return;
+    const float ba = bias[w], bg = bias[M + w];
+    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+        const float* g = GS + n * 3 * M;
+        const float* na = NA + 4 * n;
+        const float hs = kC_SILU * silu_f(g[w] + ba);
+        const float gg = kC_SIGMOID * sigmoid_f(g[M + w] + bg);
+        const float t = g[2 * M + w];
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float hv = gg * (na[1 + k] * t + GV[((int64_t)k * V + n) * M + w]);
+            U2V[((int64_t)k * V + n) * M + w] = hv;
+            dot += hv * na[1 + k];
+        }
+        U2S[n * 2 * M + w] = hs;
+        U2S[n * 2 * M + M + w] = dot;
+    }
+}
+
+// update_layer_2 epilogue + residual x += update (segnn.py:300-303) + feature
+// BatchNorm partial sums of the new x.
+__global__ void upd2_epi_kernel(const float* __restrict__ GS, const float* __restrict__ GV,
+                                const float* __restrict__ NA, const float* __restrict__ bias, int64_t V, int M,
+                                float* __restrict__ X, double* __restrict__ partial) {
+    __shared__ double red[3][EW_Y][EW_X];
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if (w < M) {
+        const float b = bias[w];
+        for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+            const float* g = GS + n * 2 * M;
+            const float* na = NA + 4 * n;
+            const float xs = X[n * M + w] + (g[w] + b);
+            X[n * M + w] = xs;
+            s1 += (double)xs;
+            s2 += (double)xs * xs;
+            const float t = g[M + w];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float* xp = X + ((1 + k) * V + n) * M + w;
+                const float xv = *xp + (na[1 + k] * t + GV[((int64_t)k * V + n) * M + w]);
+                *xp = xv;
+                s3 += (double)xv * xv;
+            }
+        }
+    }
+    red[0][threadIdx.y][threadIdx.x] = s1;
+    red[1][threadIdx.y][threadIdx.x] = s2;
+    red[2][threadIdx.y][threadIdx.x] = s3;
+    __syncthreads();
+    if (threadIdx.y < 3 && w < M) {
+        double acc = 0.0;
+        for (int y = 0; y < EW_Y; ++y) acc += red[threadIdx.y][y][threadIdx.x];
+        partial[((int64_t)blockIdx.x * 3 + threadIdx.y) * M + w] = acc;
+    }
+}
+
+// feature BatchNorm apply (in place on X)
+__global__ void bn_apply_kernel(float* __restrict__ X, const float* __restrict__ coef, int64_t V, int M) {
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    if (w >= M) return;
+    const float sc_s = coef[w], sc_v = coef[M + w], sh = coef[2 * M + w];
+    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+        X[n * M + w] = sc_s * X[n * M + w] + sh;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) X[((1 + k) * V + n) * M + w] *= sc_v;
+    }
+}
+
+// pre_pool1 inputs from X: U2S [V][2M] = [x_s | x_v.na], U2V = x_v (a view of X planes 1..3)
+__global__ void pp_pre_kernel(const float* __restrict__ X, const float* __restrict__ NA, int64_t V, int M,
+                              float* __restrict__ U2S) {
+    const int w = blockIdx.y * EW_X + threadIdx.x;
+    if (w >= M) return;
+    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
+        const float* na = NA + 4 * n;
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dot += X[((1 + k) * V + n) * M + w] * na[1 + k];
+        U2S[n * 2 * M + w] = X[n * M + w];
+        U2S[n * 2 * M + M + w] = dot;
+    }
+}
+
+// pre_pool2: O3TensorProduct(hidden -> 2x1o, node attrs); one wave per node,
+// lanes stride over channels, shuffle reduction.  out [V][6] = (c0 xyz, c1 xyz).
+__global__ void pp2_kernel(const float* __restrict__ H2S, const float* __restrict__ H2V,
+                           const float* __restrict__ NA, const float* __restrict__ W, int64_t V, int M,
+                           float* __restrict__ out) {
+    const int64_t n = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (n >= V) return;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // t0, t1, v0xyz, v1xyz
+    for (int u = lane; u < M; u += 64) {
+        const float hs = H2S[n * 2 * M + u];
+        acc[0] += W[u] * hs;
+        acc[1] += W[M + u] * hs;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float hv = H2V[((int64_t)k * V + n) * M + u];
+            acc[2 + k] += W[2 * M + u] * hv;
+            acc[5 + k] += W[3 * M + u] * hv;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off);
+    if (lane == 0) {
+        const float* na = NA + 4 * n;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            out[6 * n + k] = na[1 + k] * acc[0] + acc[2 + k];
+            out[6 * n + 3 + k] = na[1 + k] * acc[1] + acc[5 + k];
+        }
+    }
+}
+
+// self-feed state update (infer_self_feed.py:182-194, target pos_dt+vel) and trajectory write
+__global__ void rollout_update_kernel(float* __restrict__ pos, float* __restrict__ vel, const float* __restrict__ out,
+                                      int64_t V, int N, int64_t frame, int64_t num_frames,
+                                      float* __restrict__ traj_pos, float* __restrict__ traj_vel) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= V * 3) return;
+    const int64_t node = i / 3;
+    const int k = (int)(i - node * 3);
+    float p = pos[i], v = vel[i];
+    if (frame > 0) {
+        p = p + out[6 * node + k];
+        v = out[6 * node + 3 + k];
+        pos[i] = p;
+        vel[i] = v;
+    }
+    const int64_t b = node / N, d = node - b * N;
+    const int64_t o = ((b * num_frames + frame) * N + d) * 3 + k;
+    traj_pos[o] = p;
+    traj_vel[o] = v;
+}
+
+// ---------------------------------------------------------------- host side
+struct Workspace {
+    float *X, *NA, *X0, *EG, *NP, *M1S, *M1V, *G2S, *G2V, *AGG, *U1S, *U1V, *G3S, *G3V, *U2S, *U2V, *G4S, *G4V, *coef_msg,
+        *coef_feat, *out;
+    double* partial;
+    size_t bytes;
+};
+
+size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
+    const int64_t V = B * N, E = V * (N - 1);
+    const int64_t nblk = nbx::ceil_div(V > 0 ? V : 1, ROWS_PER_BLOCK);
+    size_t off = 0;
+    auto take = [&](size_t n_elems, size_t elem) -> void* {
+        off = (off + 255) & ~size_t(255);
+        void* p = base ? (void*)((char*)base + off) : nullptr;
+        off += n_elems * elem;
+        return p;
+    };
+    Workspace w;
+    w.partial = (double*)take(nblk * 3 * M, 8);
+    w.X = (float*)take(4 * V * M, 4);
+    w.NA = (float*)take(4 * V, 4);
+    w.X0 = (float*)take(8 * V, 4);
+    w.EG = (float*)take(8 * E, 4);
+    w.NP = (float*)take(4 * V * 6 * M, 4);
+    w.M1S = (float*)take(E * 2 * M, 4);
+    w.M1V = (float*)take(3 * E * M, 4);
+    w.G2S = (float*)take(E * 3 * M, 4);
+    w.G2V = (float*)take(3 * E * M, 4);
+    w.AGG = (float*)take(4 * V * M, 4);
+    w.U1S = (float*)take(V * 4 * M, 4);
+    w.U1V = (float*)take(3 * V * 2 * M, 4);
+    w.G3S = (float*)take(V * 3 * M, 4);
+    w.G3V = (float*)take(3 * V * M, 4);
+    w.U2S = (float*)take(V * 2 * M, 4);
+    w.U2V = (float*)take(3 * V * M, 4);
+    w.G4S = (float*)take(V * 3 * M, 4);
+    w.G4V = (float*)take(3 * V * M, 4);
+    w.coef_msg = (float*)take(3 * M, 4);
+    w.coef_feat = (float*)take(3 * M, 4);
+    w.out = (float*)take(6 * V, 4);
+    w.bytes = (off + 255) & ~size_t(255);
+    if (ws) *ws = w;
+    return w.bytes;
+}
+
+int check_weights(const nbx_segnn_weights* w) {
+    NBX_CHECK_ARG(w != nullptr, "segnn: null weights");
+    NBX_CHECK_ARG(w->mul > 0 && w->mul % 4 == 0, "segnn: mul must be a positive multiple of 4 (got %d)", w->mul);
+    NBX_CHECK_ARG(w->num_layers >= 0 && w->num_layers <= NBX_SEGNN_MAX_LAYERS, "segnn: bad num_layers %d",
+                  w->num_layers);
+    return NBX_OK;
+}
+
+dim3 ew_grid(int64_t rows, int M) {
+    return dim3((unsigned)nbx::ceil_div(rows > 0 ? rows : 1, ROWS_PER_BLOCK), (unsigned)nbx::ceil_div(M, EW_X));
+}
+
+// Optional per-launch timing of the GEMM kernel (nbx_segnn_forward_timed):
+// an event pair around every gemm_f32 launch on the launch stream.
+struct GemmTiming {
+    std::vector<hipEvent_t> ev;
+    double flops = 0.0;
+    int launches = 0;
+};
+
+int timed_gemm(const nbx::GemmProb* probs, int np, hipStream_t st, GemmTiming* tm) {
+    if (!tm) return nbx::gemm_f32(probs, np, st);
+    hipEvent_t a, b;
+    NBX_HIP(hipEventCreate(&a));
+    NBX_HIP(hipEventCreate(&b));
+    tm->ev.push_back(a);
+    tm->ev.push_back(b);
+    NBX_HIP(hipEventRecord(a, st));
+    if (int rc = nbx::gemm_f32(probs, np, st)) return rc;
+    NBX_HIP(hipEventRecord(b, st));
+    for (int i = 0; i < np; ++i) tm->flops += 2.0 * probs[i].M * (double)probs[i].N * probs[i].K;
+    tm->launches += 1;
+    return NBX_OK;
+}
+
+int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass, int64_t B,
+                 int64_t N, float* out, const Workspace& ws, hipStream_t st, GemmTiming* tm = nullptr) {
+    using nbx::make_prob;
+    const int M = w->mul;
+    const int64_t V = B * N, E = V * (N - 1);
+    const int iV = (int)V, iE = (int)E;
+    const dim3 ewb(EW_X, EW_Y);
+    const int nblk = (int)nbx::ceil_div(V, ROWS_PER_BLOCK);
+
+    hipLaunchKernelGGL(featurize_kernel, dim3((unsigned)nbx::ceil_div(V, 256)), dim3(256), 0, st, pos, vel, mass, V,
+                       (int)N, ws.NA, ws.X0, ws.EG);
+    hipLaunchKernelGGL(embed_kernel, ew_grid(V, M), ewb, 0, st, ws.X0, ws.NA, w->emb, w->emb_bias, V, M, ws.X);
+    NBX_LAUNCH_CHECK("embed");
+
+    for (int l = 0; l < w->num_layers; ++l) {
+        const nbx_segnn_layer& L = w->layers[l];
+        if (N > 1) {
+            // node precomputation of message_layer_1 (x_i / x_j halves)
+            nbx::GemmProb np[2] = {
+                make_prob(ws.X, M, L.node_pre_s_t, M, ws.NP, 6 * M, iV, 6 * M, M),
+                make_prob(ws.X + V * M, M, L.node_pre_v_t, M, ws.NP + V * 6 * M, 6 * M, 3 * iV, 6 * M, M)};
+            if (int rc = timed_gemm(np, 2, st, tm)) return rc;
+            hipLaunchKernelGGL(msg1_kernel, ew_grid(E, M), ewb, 0, st, ws.NP, ws.EG, L.msg1_amf, L.msg1_bias, V,
+                               (int)N, M, ws.M1S, ws.M1V);
+            NBX_LAUNCH_CHECK("msg1");
+            nbx::GemmProb m2[2] = {make_prob(ws.M1S, 2 * M, L.msg2_s_t, 2 * M, ws.G2S, 3 * M, iE, 3 * M, 2 * M),
+                                   make_prob(ws.M1V, M, L.msg2_v_t, M, ws.G2V, M, 3 * iE, M, M)};
+            if (int rc = timed_gemm(m2, 2, st, tm)) return rc;
+        }
+        hipLaunchKernelGGL(msg2_epi_kernel, ew_grid(V, M), ewb, 0, st, ws.G2S, ws.G2V, ws.EG, L.msg2_bias, V,
+                           (int)N, M, ws.AGG, ws.partial);
+        NBX_LAUNCH_CHECK("msg2_epi");
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
+                           nblk, (double)E, M, w->training, w->bn_eps, w->bn_momentum, L.msg_bn_weight,
+                           L.msg_bn_bias, L.msg_bn_running_mean, L.msg_bn_running_var, ws.coef_msg);
+        NBX_LAUNCH_CHECK("bn_finalize(msg)");
+        hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg,
+                           (float)(N - 1), V, M, ws.U1S, ws.U1V);
+        NBX_LAUNCH_CHECK("upd_pre");
+        nbx::GemmProb u1[2] = {make_prob(ws.U1S, 4 * M, L.upd1_s_t, 4 * M, ws.G3S, 3 * M, iV, 3 * M, 4 * M),
+                               make_prob(ws.U1V, 2 * M, L.upd1_v_t, 2 * M, ws.G3V, M, 3 * iV, M, 2 * M)};
+        if (int rc = timed_gemm(u1, 2, st, tm)) return rc;
+        hipLaunchKernelGGL(node_gate_kernel, ew_grid(V, M), ewb, 0, st, ws.G3S, ws.G3V, ws.NA, L.upd1_bias, V, M,
+                           ws.U2S, ws.U2V);
+        NBX_LAUNCH_CHECK("upd1_gate");
+        nbx::GemmProb u2[2] = {make_prob(ws.U2S, 2 * M, L.upd2_s_t, 2 * M, ws.G4S, 2 * M, iV, 2 * M, 2 * M),
+                               make_prob(ws.U2V, M, L.upd2_v_t, M, ws.G4V, M, 3 * iV, M, M)};
+        if (int rc = timed_gemm(u2, 2, st, tm)) return rc;
+        hipLaunchKernelGGL(upd2_epi_kernel, ew_grid(V, M), ewb, 0, st, ws.G4S, ws.G4V, ws.NA, L.upd2_bias, V, M, ws.X,
+                           ws.partial);
+        NBX_LAUNCH_CHECK("upd2_epi");
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
+                           nblk, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
+                           L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat);
+        hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M);
+        NBX_LAUNCH_CHECK("bn_apply");
+    }
+    // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)
+    hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA, V, M, ws.U2S);
+    nbx::GemmProb p1[2] = {make_prob(ws.U2S, 2 * M, w->pp1_s_t, 2 * M, ws.G3S, 3 * M, iV, 3 * M, 2 * M),
+                           make_prob(ws.X + V * M, M, w->pp1_v_t, M, ws.G3V, M, 3 * iV, M, M)};
+    if (int rc = timed_gemm(p1, 2, st, tm)) return rc;
+    hipLaunchKernelGGL(node_gate_kernel, ew_grid(V, M), ewb, 0, st, ws.G3S, ws.G3V, ws.NA, w->pp1_bias, V, M, ws.U2S,
+                       ws.U2V);
+    hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,
+                       w->pp2, V, M, out);
+    NBX_LAUNCH_CHECK("pre_pool2");
+    return NBX_OK;
+}
+
+int prepare(const nbx_segnn_weights* w, int64_t B, int64_t N, void* workspace, size_t bytes, Workspace* ws) {
+    if (int rc = check_weights(w)) return rc;
+    NBX_CHECK_ARG(B >= 1 && N >= 1, "segnn: need B >= 1 and N >= 1");
+    NBX_CHECK_ARG(B * N * (N > 1 ? N - 1 : 1) < (int64_t)1 << 30, "segnn: graph too large");
+    const size_t need = carve(ws, workspace, B, N, w->mul);
+    if (bytes < need || workspace == nullptr) {
+        nbx::set_error("segnn: workspace too small (%zu < %zu bytes)", bytes, need);
+        return NBX_E_WORKSPACE;
+    }
+    return NBX_OK;
+}
+
+}  // namespace
+
+extern "C" int nbx_segnn_workspace_bytes(int64_t B, int64_t N, int32_t mul, size_t* bytes) {
+    NBX_CHECK_ARG(bytes != nullptr && B >= 1 && N >= 1 && mul > 0, "nbx_segnn_workspace_bytes: bad arguments");
+    *bytes = carve(nullptr, nullptr, B, N, mul);
+    return NBX_OK;
+}
+
+extern "C" int nbx_segnn_forward(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
+                                 int64_t B, int64_t N, float* out, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+    Workspace ws;
+    if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    return forward_impl(w, pos, vel, mass, B, N, out, ws, (hipStream_t)stream);
+}
+
+extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass, int64_t B,
+                                 int64_t N, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+    Workspace ws;
+    if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    NBX_CHECK_ARG(num_frames >= 1, "nbx_segnn_rollout: num_frames must be >= 1");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t V = B * N;
+    const unsigned ub = (unsigned)nbx::ceil_div(V * 3, 256);
+    hipLaunchKernelGGL(rollout_update_kernel, dim3(ub), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
+                       num_frames, traj_pos, traj_vel);
+    NBX_LAUNCH_CHECK("rollout_update");
+    for (int64_t f = 1; f < num_frames; ++f) {
+        if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st)) return rc;
+        hipLaunchKernelGGL(rollout_update_kernel, dim3(ub), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, f,
+                           num_frames, traj_pos, traj_vel);
+        NBX_LAUNCH_CHECK("rollout_update");
+    }
+    return NBX_OK;
+}
+
+extern "C" int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* pos, const float* vel,
+                                       const float* mass, int64_t B, int64_t N, float* out, void* workspace,
+                                       size_t workspace_bytes, void* stream, float* gemm_ms, int32_t* gemm_launches,
+                                       double* gemm_flops, float* total_ms) {
+    Workspace ws;
+    if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    GemmTiming tm;
+    hipEvent_t t0, t1;
+    NBX_HIP(hipEventCreate(&t0));
+    NBX_HIP(hipEventCreate(&t1));
+    NBX_HIP(hipEventRecord(t0, st));
+    int rc = forward_impl(w, pos, vel, mass, B, N, out, ws, st, &tm);
+    NBX_HIP(hipEventRecord(t1, st));
+    NBX_HIP(hipEventSynchronize(t1));
+    float acc = 0.f;
+    for (size_t i = 0; i + 1 < tm.ev.size(); i += 2) {
+        float ms = 0.f;
+        NBX_HIP(hipEventElapsedTime(&ms, tm.ev[i], tm.ev[i + 1]));
+        acc += ms;
+    }
+    float tot = 0.f;
+    NBX_HIP(hipEventElapsedTime(&tot, t0, t1));
+    for (hipEvent_t e : tm.ev) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (rc) return rc;
+    if (gemm_ms) *gemm_ms = acc;
+    if (gemm_launches) *gemm_launches = tm.launches;
+    if (gemm_flops) *gemm_flops = tm.flops;
+    if (total_ms) *total_ms = tot;
+    return NBX_OK;
+}

@@ -1,0 +1,42 @@
+"""Drop-in for utils/build_fully_connected_graph.py, edge indices built on the device
+by libnbx (bit-exact with the reference)."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_cache = {}
+
+
+def fc_edge_index(batch_size: int, num_nodes: int, device) -> torch.Tensor:
+    """_build_fully_connected_edge_index (build_fully_connected_graph.py:4-20).
+    Cached per (B, N, device): the pattern is a pure function of the sizes."""
+    device = torch.device(device)
+    key = (int(batch_size), int(num_nodes), device)
+    ei = _cache.get(key)
+    if ei is None:
+        E = batch_size * num_nodes * (num_nodes - 1)
+        ei = torch.empty(2, E, dtype=torch.int64, device=device)
+        _lib.check(_lib.lib().nbx_fc_edge_index(batch_size, num_nodes, _lib.dev_ptr(ei), _lib.stream_ptr(device)),
+                   "nbx_fc_edge_index")
+        _cache[key] = ei
+    return ei
+
+
+def build_graph_with_knn(loc, batch_size, num_nodes, device, num_neighbors):
+    """build_graph_with_knn (build_fully_connected_graph.py:23-80)."""
+    num_nodes = int(num_nodes)
+    k = num_nodes - 1 if num_neighbors is None else int(num_neighbors)
+    if k >= num_nodes:
+        raise ValueError("Graph cannot have more neighbors than there are nodes in simulation - 1")
+    if k == num_nodes - 1:
+        return fc_edge_index(batch_size, num_nodes, device)
+    loc = loc.reshape(batch_size * num_nodes, -1).contiguous()
+    if loc.dtype not in (torch.float32, torch.float64):
+        raise TypeError("loc must be fp32 or fp64")
+    ei = torch.empty(2, batch_size * num_nodes * k, dtype=torch.int64, device=loc.device)
+    _lib.check(_lib.lib().nbx_knn_edge_index(_lib.dev_ptr(loc), 0 if loc.dtype == torch.float32 else 1,
+                                             batch_size, num_nodes, k, _lib.dev_ptr(ei), _lib.stream_ptr(loc.device)),
+               "nbx_knn_edge_index")
+    return ei.to(device)

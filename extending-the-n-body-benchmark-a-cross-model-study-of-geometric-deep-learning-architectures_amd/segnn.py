@@ -1,0 +1,317 @@
+"""SEGNN — drop-in for models/segnn/segnn.py::SEGNN with a fused HIP forward.
+
+Module tree, parameter names, shapes, init ranges and state_dict keys follow the
+reference (segnn.py:17-304, o3_building_blocks.py:10-203, e3nn BatchNorm), so a
+reference checkpoint loads into this class.  ``forward(graph)`` runs O3Transform +
+catch_isolated_nodes + the SEGNN forward (fp32) inside libnbx (csrc/segnn.hip);
+``rollout`` runs the whole self-feed loop device-resident.
+
+Native scope (anything else raises NotImplementedError): task="node", norm="batch",
+lmax_h = lmax_attr = 1, input 2x1o+1x0e, output 2x1o, additional message
+irreps 2x0e, fully-connected systems of equal size.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .o3 import FullyConnectedTensorProduct, Irreps, weight_balanced_irreps
+
+SH_C0 = 1.0 / math.sqrt(4.0 * math.pi)
+SH_C1 = math.sqrt(3.0 / (4.0 * math.pi))
+INV_SQRT3 = 1.0 / math.sqrt(3.0)
+
+
+class O3TensorProduct(nn.Module):
+    """o3_building_blocks.py:10-167: e3nn FCTP + sqrt(fan_in) rescale + 0e biases.
+    Init: e3nn randn, then U(-1/sqrt(fan_in), +) per instruction block and bias."""
+
+    def __init__(self, irreps_in1, irreps_out, irreps_in2=None, tp_rescale=True):
+        super().__init__()
+        self.irreps_in1 = Irreps(irreps_in1)
+        self.irreps_out = Irreps(irreps_out)
+        self.irreps_in2_provided = irreps_in2 is not None
+        self.irreps_in2 = Irreps(irreps_in2) if irreps_in2 is not None else Irreps("1x0e")
+        self.tp_rescale = tp_rescale
+        self.tp = FullyConnectedTensorProduct(self.irreps_in1, self.irreps_in2, self.irreps_out)
+        fan_in = {}
+        for ins in self.tp.instructions:
+            fan_in[ins.i_out] = fan_in.get(ins.i_out, 0) + ins.shape[0] * ins.shape[1]
+        self.fan_in = fan_in
+        bias_slots = [io for io, (m, ir) in enumerate(self.irreps_out) if ir.l == 0]
+        with torch.no_grad():
+            for w, ins in zip(self.tp.weight_views(), self.tp.instructions):
+                k = 1.0 / math.sqrt(fan_in[ins.i_out]) if tp_rescale else 1.0
+                w.uniform_(-k, k)
+            biases = []
+            for io in bias_slots:
+                k = 1.0 / math.sqrt(fan_in[io])
+                biases.append(torch.zeros(self.irreps_out[io][0]).uniform_(-k, k))
+        self.biases = nn.Parameter(torch.cat(biases)) if biases else None
+
+    def forward(self, *a):  # pragma: no cover
+        raise NotImplementedError("O3 tensor products run fused inside the SEGNN HIP kernels")
+
+
+class O3TensorProductSwishGate(O3TensorProduct):
+    """o3_building_blocks.py:170-203: TP to (scalars + gates + gated).simplify()."""
+
+    def __init__(self, irreps_in1, irreps_out, irreps_in2=None):
+        irreps_out = Irreps(irreps_out)
+        scalars = Irreps([irreps_out[0]])
+        gates = Irreps(f"{irreps_out.num_irreps - scalars.num_irreps}x0e")
+        gated = Irreps(irreps_out[1:])
+        super().__init__(irreps_in1, (scalars + gates + gated).simplify(), irreps_in2)
+        self.irreps_gated = gated
+
+
+class BatchNorm(nn.Module):
+    """e3nn.nn.BatchNorm parameter/buffer layout (affine, reduce="mean",
+    normalization="component", eps=1e-5, momentum=0.1)."""
+
+    def __init__(self, irreps, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.irreps = Irreps(irreps)
+        self.eps, self.momentum = eps, momentum
+        n_scalar = sum(m for m, ir in self.irreps if ir.l == 0 and ir.p == 1)
+        self.weight = nn.Parameter(torch.ones(self.irreps.num_irreps))
+        self.bias = nn.Parameter(torch.zeros(n_scalar))
+        self.register_buffer("running_mean", torch.zeros(n_scalar))
+        self.register_buffer("running_var", torch.ones(self.irreps.num_irreps))
+
+
+class SEGNNLayer(nn.Module):
+    """segnn.py:192-304 (PyG MessagePassing, aggr="add", node_dim=-2)."""
+
+    def __init__(self, input_irreps, hidden_irreps, output_irreps, edge_attr_irreps, node_attr_irreps,
+                 norm=None, additional_message_irreps=None):
+        super().__init__()
+        self.hidden_irreps = hidden_irreps
+        msg_in = (input_irreps + input_irreps + additional_message_irreps).simplify()
+        upd_in = (input_irreps + hidden_irreps).simplify()
+        self.message_layer_1 = O3TensorProductSwishGate(msg_in, hidden_irreps, edge_attr_irreps)
+        self.message_layer_2 = O3TensorProductSwishGate(hidden_irreps, hidden_irreps, edge_attr_irreps)
+        self.update_layer_1 = O3TensorProductSwishGate(upd_in, hidden_irreps, node_attr_irreps)
+        self.update_layer_2 = O3TensorProduct(hidden_irreps, hidden_irreps, node_attr_irreps)
+        self.norm = norm
+        self.feature_norm = self.message_norm = None
+        if norm == "batch":
+            self.feature_norm = BatchNorm(hidden_irreps)
+            self.message_norm = BatchNorm(hidden_irreps)
+        elif norm is not None:
+            raise NotImplementedError(f"SEGNN norm={norm!r} is outside the native path")
+
+
+class SEGNN(nn.Module):
+    """Steerable E(3) equivariant message passing network (segnn.py:14-189)."""
+
+    def __init__(self, input_irreps="2x1o + 1x0e", hidden_features=64, lmax_h=1, lmax_attr=1, num_layers=4,
+                 output_irreps="2x1o", norm="batch", pool="avg", task="node", additional_message_irreps="2x0e",
+                 training_args=None):
+        super().__init__()
+        if task != "node" or lmax_h != 1 or lmax_attr != 1 or norm != "batch":
+            raise NotImplementedError("native SEGNN supports task='node', norm='batch', lmax_h = lmax_attr = 1")
+        self.hidden_features, self.lmax_h, self.lmax_attr, self.num_layers = hidden_features, lmax_h, lmax_attr, num_layers
+        self.node_attr_irreps = Irreps.spherical_harmonics(lmax_attr)
+        hidden_irreps = weight_balanced_irreps(hidden_features, self.node_attr_irreps, lmax_h)
+        self.edge_attr_irreps = Irreps.spherical_harmonics(lmax_attr)
+        self.hidden_irreps, self.task, self.norm, self.pool = hidden_irreps, task, norm, pool
+        self.additional_message_irreps = Irreps(additional_message_irreps)
+        self.training_args = training_args
+        input_irreps, output_irreps = Irreps(input_irreps), Irreps(output_irreps)
+        if str(input_irreps) != "2x1o+1x0e" or str(output_irreps) != "2x1o" or \
+                str(self.additional_message_irreps) != "2x0e":
+            raise NotImplementedError("native SEGNN expects 2x1o+1x0e -> 2x1o with 2x0e message features")
+        self.embedding_layer = O3TensorProduct(input_irreps, hidden_irreps, self.node_attr_irreps)
+        self.layers = nn.ModuleList([
+            SEGNNLayer(hidden_irreps, hidden_irreps, hidden_irreps, self.edge_attr_irreps, self.node_attr_irreps,
+                       norm=norm, additional_message_irreps=self.additional_message_irreps)
+            for _ in range(num_layers)])
+        self.pre_pool1 = O3TensorProductSwishGate(hidden_irreps, hidden_irreps, self.node_attr_irreps)
+        self.pre_pool2 = O3TensorProduct(hidden_irreps, output_irreps, self.node_attr_irreps)
+        self.mul = hidden_irreps[0][0]
+        if str(hidden_irreps) != f"{self.mul}x0e+{self.mul}x1o" or self.mul % 4:
+            raise NotImplementedError(f"hidden irreps {hidden_irreps} outside the native path (mul % 4 == 0)")
+        self._packed = None
+        self._ws = None
+        self._warned_dtype = False
+
+    # ------------------------------------------------------------ reference API
+    def get_model_size(self):
+        return self.hidden_features
+
+    def get_serializable_attributes(self):
+        return {
+            "hidden_features": self.hidden_features, "lmax_h": self.lmax_h, "lmax_attr": self.lmax_attr,
+            "node_attr_irreps": str(self.node_attr_irreps), "num_layers": self.num_layers,
+            "input_irreps": str(self.embedding_layer.irreps_in1), "hidden_irreps": str(self.hidden_irreps),
+            "output_irreps": str(self.pre_pool2.irreps_out), "edge_attr_irreps": str(self.edge_attr_irreps),
+            "norm": self.norm, "pool": None, "task": self.task,
+            "additional_message_irreps": str(self.additional_message_irreps),
+            "training_args": self.training_args, "num_params": sum(p.numel() for p in self.parameters()),
+        }
+
+    # ------------------------------------------------------------ weight packing
+    def _param_version(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters()) + \
+            tuple((b.data_ptr(), b.dtype) for b in self.buffers())
+
+    def packed_matrices(self, device="cpu", dtype=torch.float32):
+        """The e3nn parameters re-packed into the fp32 GEMM operands of include/nbx.h
+        (M = mul, c0/c1 = SH prefactors, s3 = 1/sqrt 3; derivation in DESIGN.md §SEGNN).
+        Matrices named *_t are [N_out][K_in]."""
+        M = self.mul
+        f32 = dict(device=device, dtype=dtype)
+
+        def views(tpmod):
+            return [w.detach().to(**f32)[:, 0, :] for w in tpmod.tp.weight_views()]   # [mul1, mul_out]
+
+        def T(x):
+            return x.t().contiguous()
+
+        def vec(x):
+            return x.detach().to(**f32).contiguous()
+
+        z = torch.zeros(M, M, **f32)
+        P = {}
+        Wa, Wb, Wc, Wd = views(self.embedding_layer)
+        P["emb"] = vec(torch.stack([Wa[0], Wa[1], Wb[0] * INV_SQRT3, Wb[1] * INV_SQRT3, Wc[0], Wd[0]]))
+        P["emb_bias"] = vec(self.embedding_layer.biases)
+        for li, layer in enumerate(self.layers):
+            p = f"layers.{li}."
+            WA0, WA1, WB0, WB1, WC0, WC1, WD0, WD1, WE0, WE1 = views(layer.message_layer_1)
+            P[p + "node_pre_s_t"] = T(torch.cat([SH_C0 * WA0, SH_C1 * WA1, SH_C0 * WC0, SH_C1 * WC1], 1))
+            P[p + "node_pre_v_t"] = T(torch.cat([SH_C1 * INV_SQRT3 * WB1, SH_C0 * WB0,
+                                                 SH_C1 * INV_SQRT3 * WD1, SH_C0 * WD0], 1))
+            P[p + "msg1_amf"] = vec(torch.cat([SH_C0 * WE0, SH_C1 * WE1], 1))
+            P[p + "msg1_bias"] = vec(layer.message_layer_1.biases)
+            W1, W2, W3, W4 = views(layer.message_layer_2)
+            P[p + "msg2_s_t"] = T(torch.cat([torch.cat([SH_C0 * W1, SH_C1 * INV_SQRT3 * W4], 0),
+                                             torch.cat([SH_C1 * W2, z], 0)], 1))
+            P[p + "msg2_v_t"] = T(SH_C0 * W3)
+            P[p + "msg2_bias"] = vec(layer.message_layer_2.biases)
+            Xs0, Xs1, Xv0, Xv1, As0, As1, Av0, Av1 = views(layer.update_layer_1)
+            P[p + "upd1_s_t"] = T(torch.cat([torch.cat([Xs0, As0, INV_SQRT3 * Xv1, INV_SQRT3 * Av1], 0),
+                                             torch.cat([Xs1, As1, z, z], 0)], 1))
+            P[p + "upd1_v_t"] = T(torch.cat([Xv0, Av0], 0))
+            P[p + "upd1_bias"] = vec(layer.update_layer_1.biases)
+            U1, U2, U3, U4 = views(layer.update_layer_2)
+            P[p + "upd2_s_t"] = T(torch.cat([torch.cat([U1, INV_SQRT3 * U4], 0), torch.cat([U2, z], 0)], 1))
+            P[p + "upd2_v_t"] = T(U3)
+            P[p + "upd2_bias"] = vec(layer.update_layer_2.biases)
+            for name, bn in (("msg", layer.message_norm), ("feat", layer.feature_norm)):
+                P[p + f"{name}_bn_weight"] = vec(bn.weight)
+                P[p + f"{name}_bn_bias"] = vec(bn.bias)
+        P1, P2, P3, P4 = views(self.pre_pool1)
+        P["pp1_s_t"] = T(torch.cat([torch.cat([P1, INV_SQRT3 * P4], 0), torch.cat([P2, z], 0)], 1))
+        P["pp1_v_t"] = T(P3)
+        P["pp1_bias"] = vec(self.pre_pool1.biases)
+        Ws, Wv = views(self.pre_pool2)
+        P["pp2"] = vec(torch.stack([Ws[:, 0], Ws[:, 1], Wv[:, 0], Wv[:, 1]]))
+        return P
+
+    def pack_weights(self, device):
+        """Build the nbx_segnn_weights struct (device pointers) from packed_matrices."""
+        P = self.packed_matrices(device)
+        W = _lib.SegnnWeights()
+        W.mul, W.num_layers, W.bn_eps, W.bn_momentum = self.mul, self.num_layers, 1e-5, 0.1
+        for k in ("emb", "emb_bias", "pp1_s_t", "pp1_v_t", "pp1_bias", "pp2"):
+            setattr(W, k, P[k].data_ptr())
+        for li, layer in enumerate(self.layers):
+            L = W.layers[li]
+            for name, _ in L._fields_:
+                key = f"layers.{li}.{name}"
+                if key in P:
+                    setattr(L, name, P[key].data_ptr())
+            for name, bn in (("msg", layer.message_norm), ("feat", layer.feature_norm)):
+                # running stats are updated IN PLACE by the kernels: point at the module's buffers
+                for stat in ("running_mean", "running_var"):
+                    buf = getattr(bn, stat)
+                    if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
+                        raise _lib.NbxError("BatchNorm running stats must be contiguous fp32 on the device")
+                    setattr(L, f"{name}_bn_{stat}", buf.data_ptr())
+        self._packed = (self._param_version(), W, P)
+        return W
+
+    def _weights(self, device):
+        if self._packed is None or self._packed[0] != self._param_version():
+            self.pack_weights(device)
+        W = self._packed[1]
+        W.training = 1 if self.training else 0
+        return W
+
+    def _workspace(self, B, N, device):
+        nbytes = _lib.c_sz()
+        _lib.check(_lib.lib().nbx_segnn_workspace_bytes(B, N, self.mul, nbytes), "segnn workspace")
+        if self._ws is None or self._ws.numel() < nbytes.value or self._ws.device != device:
+            self._ws = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def _check_params(self, device):
+        for p in self.parameters():
+            if not p.is_cuda:
+                raise _lib.NbxError("SEGNN HIP path: move the model to the HIP device first")
+
+    # ------------------------------------------------------------ forward
+    @staticmethod
+    def infer_system_size(num_nodes: int, num_edges: int):
+        if num_nodes == 0:
+            raise ValueError("empty graph")
+        n = num_edges // num_nodes + 1
+        if num_edges != num_nodes * (n - 1) or num_nodes % n:
+            raise NotImplementedError("native SEGNN needs fully-connected systems of equal size")
+        return num_nodes // n, n
+
+    def forward(self, graph):
+        """graph: pos [V,3], vel [V,3], mass [V,1], edge_index (fully connected,
+        utils/build_fully_connected_graph.py order).  Returns [V, 6] in the
+        graph's dtype; computes in fp32."""
+        pos = graph.pos
+        device = pos.device
+        V = pos.shape[0]
+        edge_index = graph.edge_index
+        if getattr(graph, "nbx_system_size", None) is not None:
+            N = int(graph.nbx_system_size)
+            B = V // N
+        else:
+            B, N = self.infer_system_size(V, edge_index.shape[1])
+            from .graph import fc_edge_index
+            if not torch.equal(edge_index.to(device), fc_edge_index(B, N, device)):
+                raise NotImplementedError("native SEGNN needs the fully-connected edge_index of "
+                                          "build_graph_with_knn (num_neighbors = N-1)")
+        out_dtype = pos.dtype
+        if out_dtype != torch.float32 and not self._warned_dtype:
+            warnings.warn("SEGNN HIP path computes in fp32; inputs are cast", stacklevel=2)
+            self._warned_dtype = True
+        self._check_params(device)
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
+        p, v, m = f(pos), f(graph.vel), f(graph.mass.reshape(-1))
+        out = torch.empty(V, 6, device=device, dtype=torch.float32)
+        W = self._weights(device)
+        ws = self._workspace(B, N, device)
+        _lib.check(_lib.lib().nbx_segnn_forward(
+            W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(out),
+            _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_forward")
+        return out.to(out_dtype)
+
+    @torch.no_grad()
+    def rollout(self, loc, vel, mass, num_frames: int):
+        """Device-resident self-feed (infer_self_feed.py:99-194, target pos_dt+vel).
+        loc/vel [B,N,3], mass [B,N,1] -> (traj_loc, traj_vel) [B, num_frames, N, 3] fp32."""
+        device = loc.device
+        self._check_params(device)
+        B, N, _ = loc.shape
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
+        p, v, m = f(loc), f(vel), f(mass.reshape(B * N))
+        tp = torch.empty(B, num_frames, N, 3, device=device, dtype=torch.float32)
+        tv = torch.empty_like(tp)
+        W = self._weights(device)
+        ws = self._workspace(B, N, device)
+        _lib.check(_lib.lib().nbx_segnn_rollout(
+            W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames, _lib.dev_ptr(tp),
+            _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_rollout")
+        return tp, tv

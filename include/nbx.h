@@ -1,0 +1,156 @@
+/*
+ * nbx.h — C ABI of the MI355X-native N-body hot path (libnbx.so).
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t passed
+ * as `void*`; nothing here owns memory (callers allocate outputs and the
+ * workspace).  Return value: 0 on success, otherwise a nonzero code; the message
+ * is available from nbx_last_error() (thread-local).  Launches are asynchronous
+ * on `stream` unless stated otherwise and never synchronise the device, so a
+ * caller may capture them into a hipGraph.
+ *
+ * Each declaration cites the reference interface (file:line, paths relative to
+ * the reference repository) whose behaviour it reproduces.  The reference is
+ * pure Python; the binding a maintainer would add is shown in INTEGRATION.md.
+ */
+#ifndef NBX_H
+#define NBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NBX_ABI_VERSION 1
+
+#define NBX_OK 0
+#define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
+#define NBX_E_UNSUPPORTED 2 /* configuration outside the native path */
+#define NBX_E_HIP 3        /* HIP runtime error (message has details) */
+#define NBX_E_WORKSPACE 4  /* workspace too small */
+
+int nbx_abi_version(void);
+const char* nbx_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * A1 — graph builder.
+ * Replaces utils/build_fully_connected_graph.py:4-20 (_build_fully_connected_edge_index)
+ * and the fully-connected branch of build_graph_with_knn (:23-40).
+ * edge_index: int64 [2, B*N*(N-1)], row-major over i then j != i, system offset b*N.
+ * Bit-exact with the reference.
+ */
+int nbx_fc_edge_index(int64_t batch_size, int64_t num_nodes, int64_t* edge_index, void* stream);
+
+/* kNN branch of build_graph_with_knn (:42-80): per system, the k nearest other
+ * nodes by Euclidean distance in ascending order (index order breaks ties);
+ * edge_index = [i, neighbour] + b*N, int64 [2, B*N*k].  loc fp32 [B*N, 3]
+ * (dtype 0) or fp64 (dtype 1).  Returns NBX_E_INVAL if k >= N (the reference
+ * raises ValueError), requires N <= 64. */
+int nbx_knn_edge_index(const void* loc, int32_t dtype, int64_t batch_size, int64_t num_nodes, int64_t k,
+                       int64_t* edge_index, void* stream);
+
+/* ------------------------------------------------------------------------
+ * A20-A22 — GravitySim ground-truth integrator (fp64).
+ * Replaces datasets/nbody/dataset/synthetic_sim.py:318-340 (compute_acceleration).
+ * pos [S,N,3], mass [S,N]; acc [S,N,3] = G * sum_j m_j (x_j - x_i)(|x_j-x_i|^2+eps^2)^-1.5
+ */
+int nbx_gravity_acceleration(const double* pos, const double* mass, int64_t num_systems, int64_t num_nodes,
+                             double G, double softening, double* acc, void* stream);
+
+/* Replaces synthetic_sim.py:383-408 (the sample_trajectory KDK loop, noise_var=0):
+ * from initial (pos, vel) [S,N,3] run T kick-drift-kick steps of size dt,
+ * saving (pos, vel, acc*mass) every sample_freq steps BEFORE stepping into
+ * pos_save/vel_save/force_save [S, T/sample_freq, N, 3].  pos/vel are
+ * overwritten with the final state.  The whole loop runs inside one kernel per
+ * system tile (state in LDS).  Requires T % sample_freq == 0, N <= 1024. */
+int nbx_gravity_sample(double* pos, double* vel, const double* mass, int64_t num_systems, int64_t num_nodes,
+                       int64_t T, int64_t sample_freq, double dt, double G, double softening,
+                       double* pos_save, double* vel_save, double* force_save, void* stream);
+
+/* ------------------------------------------------------------------------
+ * SEGNN (models/segnn/segnn.py:17-304, o3_building_blocks.py:10-278) — fp32.
+ *
+ * Native scope: task="node", norm="batch", lmax_h = lmax_attr = 1, input irreps
+ * 2x1o+1x0e, output 2x1o, additional message irreps 2x0e, fully-connected
+ * systems of N nodes.  Hidden irreps are mul x 0e + mul x 1o (mul % 4 == 0).
+ *
+ * Weights are the reference's e3nn parameters re-packed once on the device by
+ * the host module (see the package's segnn.py::pack_weights for the exact
+ * formulas).  Matrices named *_t are stored transposed, [N_out][K_in], row-major.
+ */
+#define NBX_SEGNN_MAX_LAYERS 64
+
+typedef struct nbx_segnn_layer {
+    const float* node_pre_s_t; /* [6*mul][mul]  x_s -> [P_dst(2mul) R_dst(mul) P_src(2mul) R_src(mul)] */
+    const float* node_pre_v_t; /* [6*mul][mul]  x_v[:,k] -> [Q_dst(2mul) S_dst(mul) Q_src(2mul) S_src(mul)] */
+    const float* msg1_amf;     /* [2][3*mul]    amf (dist, m_i m_j) -> [s(2mul) t(mul)] */
+    const float* msg1_bias;    /* [2*mul] */
+    const float* msg2_s_t;     /* [3*mul][2*mul] [m_s | m_v.rhat] -> [s(2mul) t(mul)] */
+    const float* msg2_v_t;     /* [mul][mul]     m_v[:,k] -> v */
+    const float* msg2_bias;    /* [2*mul] */
+    const float* upd1_s_t;     /* [3*mul][4*mul] [x_s a_s x_v.na a_v.na] -> [s(2mul) t(mul)] */
+    const float* upd1_v_t;     /* [mul][2*mul]   [x_v[:,k] a_v[:,k]] -> v */
+    const float* upd1_bias;    /* [2*mul] */
+    const float* upd2_s_t;     /* [2*mul][2*mul] [h_s | h_v.na] -> [s(mul) t(mul)] */
+    const float* upd2_v_t;     /* [mul][mul] */
+    const float* upd2_bias;    /* [mul] */
+    /* e3nn BatchNorm(hidden): weight [2mul], bias [mul], running_mean [mul],
+       running_var [2mul]; running stats are updated in place in train mode. */
+    const float* msg_bn_weight;
+    const float* msg_bn_bias;
+    float* msg_bn_running_mean;
+    float* msg_bn_running_var;
+    const float* feat_bn_weight;
+    const float* feat_bn_bias;
+    float* feat_bn_running_mean;
+    float* feat_bn_running_var;
+} nbx_segnn_layer;
+
+typedef struct nbx_segnn_weights {
+    int32_t mul;        /* hidden multiplicity: hidden irreps = mul x 0e + mul x 1o */
+    int32_t num_layers; /* <= NBX_SEGNN_MAX_LAYERS */
+    int32_t training;   /* 1: BatchNorm uses batch statistics (the reference rollout), 0: running stats */
+    float bn_eps;       /* 1e-5 */
+    float bn_momentum;  /* 0.1 */
+    const float* emb;      /* [6][mul]: W_a[0], W_a[1], W_b[0]/sqrt3, W_b[1]/sqrt3, W_c, W_d */
+    const float* emb_bias; /* [mul] */
+    const float* pp1_s_t;  /* [3*mul][2*mul] pre_pool1 (gate TP, node attrs) */
+    const float* pp1_v_t;  /* [mul][mul] */
+    const float* pp1_bias; /* [2*mul] */
+    const float* pp2;      /* [2][2][mul]: (s->1o, v->1o) x (out channel 0, 1) */
+    nbx_segnn_layer layers[NBX_SEGNN_MAX_LAYERS];
+} nbx_segnn_weights;
+
+/* Bytes of device workspace nbx_segnn_forward / nbx_segnn_rollout need. */
+int nbx_segnn_workspace_bytes(int64_t batch_size, int64_t num_nodes, int32_t mul, size_t* bytes);
+
+/* O3Transform + catch_isolated_nodes + SEGNN.forward in one call
+ * (infer_self_feed.py:115-130 graph build and model(graph)).
+ * pos/vel [B*N,3], mass [B*N] fp32 -> out [B*N, 6] = (2x1o: delta-pos, vel). */
+int nbx_segnn_forward(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
+                      int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
+/* Diagnostic variant of nbx_segnn_forward used by bench.py: records a HIP event
+ * pair around every launch of the dominant GEMM kernel on `stream`, synchronises
+ * at the end (so it is NOT graph-capturable) and reports the summed GEMM time,
+ * the number of GEMM launches, their executed FLOPs (2*M*N*K summed) and the
+ * whole forward's time. */
+int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
+                            int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
+                            void* stream, float* gemm_ms, int32_t* gemm_launches, double* gemm_flops, float* total_ms);
+
+/* Device-resident self-feed rollout (helper_scripts/infer_self_feed.py:99-194,
+ * target "pos_dt+vel", force zeroed, mass constant): starting from pos/vel
+ * [B,N,3] it runs num_frames-1 model steps; traj_pos/traj_vel [B, num_frames, N, 3]
+ * receive frame 0 = the initial state and frame t = the state after t steps.
+ * pos/vel are updated to the final state.  No host synchronisation inside. */
+int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass,
+                      int64_t batch_size, int64_t num_nodes, int64_t num_frames,
+                      float* traj_pos, float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NBX_H */

@@ -1,0 +1,67 @@
+"""The C-ABI library loads and exports every entry point include/nbx.h declares
+(CPU-only: no compute call touches a device)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "nbx.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(nbx_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    import nbody_amd._lib as lib
+    if not os.path.exists(lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return lib.lib()
+
+
+def test_header_declares_the_path():
+    syms = declared_symbols()
+    for s in ["nbx_fc_edge_index", "nbx_knn_edge_index", "nbx_gravity_acceleration", "nbx_gravity_sample",
+              "nbx_segnn_forward", "nbx_segnn_rollout", "nbx_segnn_workspace_bytes", "nbx_last_error"]:
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(L):
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_abi_version_and_host_only_calls(L):
+    import nbody_amd._lib as lib
+    assert L.nbx_abi_version() == lib.ABI_VERSION
+    n = lib.c_sz()
+    assert L.nbx_segnn_workspace_bytes(1024, 5, 96, ctypes.byref(n)) == 0
+    assert n.value > 100 * 2 ** 20
+    # argument validation happens before any device call and reports through nbx_last_error
+    assert L.nbx_fc_edge_index(-1, 5, None, None) == 1
+    assert b"bad sizes" in L.nbx_last_error()
+    assert L.nbx_knn_edge_index(None, 0, 1, 5, 5, None, None) == 1
+    assert b"more neighbors" in L.nbx_last_error()
+
+
+def test_struct_layout_matches_header():
+    """ctypes mirror of nbx_segnn_weights has the C layout (pointer-aligned)."""
+    import nbody_amd._lib as lib
+    layer_ptrs = 21
+    assert ctypes.sizeof(lib.SegnnLayer) == layer_ptrs * 8
+    head = 3 * 4 + 2 * 4   # mul, num_layers, training, bn_eps, bn_momentum
+    head = (head + 7) // 8 * 8
+    assert ctypes.sizeof(lib.SegnnWeights) == head + 6 * 8 + lib.MAX_LAYERS * layer_ptrs * 8
+
+
+def test_product_fails_loudly_without_device():
+    """No CPU fallback: the HIP-only ops raise on CPU tensors."""
+    import torch
+
+    import nbody_amd._lib as lib
+    with pytest.raises(lib.NbxError):
+        lib.dev_ptr(torch.zeros(3))
