@@ -130,7 +130,7 @@ def main():
         elapsed = float(t.item())
     finite = bool(torch.isfinite(tp).all().item())
 
-    # live roofline of the dominant kernel (gemm_f32_kernel): HIP events around
+    # live roofline of the dominant kernel (tp_fused_kernel): HIP events around
     # every GEMM launch of a few forwards on the launch stream
     V, E, M = B * N, B * N * (N - 1), model.mul
     p32 = loc_d.reshape(-1, 3).contiguous()
@@ -179,7 +179,7 @@ def main():
                    "bn_mode": "batch statistics per rank (reference train-mode rollout)"},
         "trajectory_steps_per_s": round(value * B, 1),
         "survey_formulation_tflops": round(value * SURVEY_GFLOP_PER_STEP / 1e3, 3),
-        "roofline": {"bound": "mfma", "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)",
+        "roofline": {"bound": "mfma", "kernel": "tp_fused_kernel (v_mfma_f32_32x32x2_f32, weight-stationary)",
                      "achieved": round(achieved_tflops, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                      "avg_launch_us": round(avg_launch_s * 1e6, 3),

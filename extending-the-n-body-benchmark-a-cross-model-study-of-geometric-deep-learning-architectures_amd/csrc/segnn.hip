@@ -6,19 +6,25 @@
 // Data layout in HBM (V = B*N nodes, E = V*(N-1) edges, M = mul):
 //   X    [4][V][M]   node features, plane 0 = 0e channels, planes 1..3 = x/y/z of 1o channels
 //   NA   [V][4]      node attribute (1, na_x, na_y, na_z)  (na_0 forced to 1: catch_isolated_nodes)
-//   EG   [E][8]      per edge (dst-major): rhat xyz, |rel|, m_src*m_dst
-//   edges are enumerated dst-major: e = dst*(N-1) + q, src = the q-th other node of the system,
-//   so the N-1 messages into a node are contiguous (aggregation without atomics).
+//   EG   [Ep][8]     per edge slot (dst-major): rhat xyz, |rel|, m_src*m_dst
+//   edges are enumerated dst-major in G = next_pow2(N-1) slots per destination:
+//   slot e = dst*G + q, q < N-1 is the edge from the q-th other node of the system,
+//   q >= N-1 is padding (zero rows, masked).  A node's messages are then G
+//   consecutive rows, i.e. registers of one lane in the MFMA accumulator tile,
+//   and aggregate without atomics (Ep = V*G; G = 4 at N = 5: no padding).
 // Every O(3) tensor product with l <= 1 is split into a "scalar-row" GEMM
 // [x_s | x_v.y] -> [s | t] and a "vector-row" GEMM x_v[:,k] -> v (one row per
 // component); the constants of e3nn's path normalisation, the SEGNN rescale and
 // the spherical-harmonic prefactors are folded into the packed weights.
 // The x_i / x_j halves of message_layer_1 are linear in node features, so they
 // are computed once per node (node_pre GEMM) and combined per edge.
+#include <algorithm>
+#include <cstring>
 #include <vector>
 
-#include "gemm_f32.h"
 #include "nbx_internal.h"
+#include "tp16.h"
+#include "tp_fused.h"
 
 namespace {
 
@@ -31,12 +37,12 @@ __device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Elementwise kernels use block (32, 8): threadIdx.x = channel within a 32-chunk,
 // threadIdx.y = row lane; a block covers ROWS_PER_BLOCK rows x 32 channels.
-constexpr int EW_X = 32, EW_Y = 8, ROWS_PER_BLOCK = 64;
+constexpr int EW_X = 32, EW_Y = 8, ROWS_PER_BLOCK = 16;
 
 // ---------------------------------------------------------------- featurise
 // O3Transform (o3_building_blocks.py:231-278) + catch_isolated_nodes (segnn.py:136-148)
 __global__ void featurize_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
-                                 const float* __restrict__ mass, int64_t V, int N, float* __restrict__ NA,
+                                 const float* __restrict__ mass, int64_t V, int N, int G, float* __restrict__ NA,
                                  float* __restrict__ X0, float* __restrict__ EG) {
     const int64_t node = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (node >= V) return;
@@ -52,9 +58,13 @@ __global__ void featurize_kernel(const float* __restrict__ pos, const float* __r
         const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
         const float den = fmaxf(dist, 1e-12f);
         const float hx = rx / den, hy = ry / den, hz = rz / den;
-        float* eg = EG + (node * (N - 1) + q) * 8;
+        float* eg = EG + (node * G + q) * 8;
         eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s] * m;
         sx += kSH_C1 * hx; sy += kSH_C1 * hy; sz += kSH_C1 * hz;
+    }
+    for (int q = N - 1; q < G; ++q) {
+        float* eg = EG + (node * G + q) * 8;
+        eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
     }
     const float cnt = (float)(N - 1 > 0 ? N - 1 : 1);
     const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
@@ -95,18 +105,24 @@ __global__ void embed_kernel(const float* __restrict__ X0, const float* __restri
 //   vector row  [Q_dst(2M) | S_dst(M) | Q_src(2M) | S_src(M)]
 // then Gate -> M1S [E][2M] = [m_s | m_v . rhat], M1V [3][E][M] = m_v
 __global__ void msg1_kernel(const float* __restrict__ NP, const float* __restrict__ EG,
-                            const float* __restrict__ amfw, const float* __restrict__ bias, int64_t V, int N, int M,
-                            float* __restrict__ M1S, float* __restrict__ M1V) {
+                            const float* __restrict__ amfw, const float* __restrict__ bias, int64_t V, int N, int G,
+                            int M, float* __restrict__ M1S, float* __restrict__ M1V) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
-    const int64_t E = V * (N - 1);
+    const int64_t E = V * G;
     const int ld = 6 * M;
     const float ea0 = amfw[w], eg0 = amfw[M + w], et0 = amfw[2 * M + w];
     const float ea1 = amfw[3 * M + w], eg1 = amfw[4 * M + w], et1 = amfw[5 * M + w];
     const float ba = bias[w], bg = bias[M + w];
     for (int64_t e = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; e < E && e < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; e += EW_Y) {
-        const int64_t dn = e / (N - 1);
-        const int q = (int)(e - dn * (N - 1));
+        const int64_t dn = e / G;
+        const int q = (int)(e - dn * G);
+        if (q >= N - 1) {  // padding slot
+            M1S[e * 2 * M + w] = 0.f;
+            M1S[e * 2 * M + M + w] = 0.f;
+            for (int k = 0; k < 3; ++k) M1V[((int64_t)k * E + e) * M + w] = 0.f;
+            continue;
+        }
         const int64_t b = dn / N;
         const int d = (int)(dn - b * N);
         const int64_t sn = b * N + (q < d ? q : q + 1);
@@ -140,57 +156,11 @@ __global__ void msg1_kernel(const float* __restrict__ NP, const float* __restric
     }
 }
 
-// message_layer_2 epilogue: bias + Gate, aggregation over the N-1 in-edges
-// (aggr="add" at edge_index[1]) and per-block BatchNorm partial sums
-// (sum m_s, sum m_s^2, sum |m_v|^2) in fp64.
-__global__ void msg2_epi_kernel(const float* __restrict__ G2S, const float* __restrict__ G2V,
-                                const float* __restrict__ EG, const float* __restrict__ bias, int64_t V, int N, int M,
-                                float* __restrict__ AGG, double* __restrict__ partial) {
-    __shared__ double red[3][EW_Y][EW_X];
-    const int w = blockIdx.y * EW_X + threadIdx.x;
-    const int64_t E = V * (N - 1);
-    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    if (w < M) {
-        const float ba = bias[w], bg = bias[M + w];
-        for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
-            float as = 0.f, av0 = 0.f, av1 = 0.f, av2 = 0.f;
-            for (int q = 0; q < N - 1; ++q) {
-                const int64_t e = n * (N - 1) + q;
-                const float* g = G2S + e * 3 * M;
-                const float* eg = EG + e * 8;
-                const float ms = kC_SILU * silu_f(g[w] + ba);
-                const float gg = kC_SIGMOID * sigmoid_f(g[M + w] + bg);
-                const float t = g[2 * M + w];
-                const float m0 = gg * (eg[0] * t + G2V[(0 * E + e) * M + w]);
-                const float m1 = gg * (eg[1] * t + G2V[(1 * E + e) * M + w]);
-                const float m2 = gg * (eg[2] * t + G2V[(2 * E + e) * M + w]);
-                as += ms; av0 += m0; av1 += m1; av2 += m2;
-                s1 += (double)ms;
-                s2 += (double)ms * (double)ms;
-                s3 += (double)m0 * m0 + (double)m1 * m1 + (double)m2 * m2;
-            }
-            AGG[n * M + w] = as;
-            AGG[(1 * V + n) * M + w] = av0;
-            AGG[(2 * V + n) * M + w] = av1;
-            AGG[(3 * V + n) * M + w] = av2;
-        }
-    }
-    red[0][threadIdx.y][threadIdx.x] = s1;
-    red[1][threadIdx.y][threadIdx.x] = s2;
-    red[2][threadIdx.y][threadIdx.x] = s3;
-    __syncthreads();
-    if (threadIdx.y < 3 && w < M) {
-        double acc = 0.0;
-        for (int y = 0; y < EW_Y; ++y) acc += red[threadIdx.y][y][threadIdx.x];
-        partial[((int64_t)blockIdx.x * 3 + threadIdx.y) * M + w] = acc;
-    }
-}
-
 // e3nn BatchNorm (train mode) finalisation: one 64-lane group per channel
-// reduces the per-block partials in a fixed order, then computes
+// reduces the per-wave partials of the fused TP kernel in a fixed order, then computes
 // scale/shift and the running-stat update r <- (1-m) r + m * batch_stat.
 // coef layout: [0..2M) scale (0e then 1o channels), [2M..3M) shift (0e).
-__global__ void bn_finalize_kernel(const double* __restrict__ partial, int nblk, double count, int M, int training,
+__global__ void bn_finalize_kernel(const double* __restrict__ partial, int wpc, int cw, double count, int M, int training,
                                    float eps, float momentum, const float* __restrict__ weight,
                                    const float* __restrict__ bias, float* __restrict__ rmean,
                                    float* __restrict__ rvar, float* __restrict__ coef) {
@@ -200,12 +170,14 @@ __global__ void bn_finalize_kernel(const double* __restrict__ partial, int nblk,
     const int c = scalar ? group : group - M;
     double a = 0.0, b = 0.0;
     if (training) {
-        for (int i = lane; i < nblk; i += 64) {
+        // partial layout of the fused TP kernels: [chunk][wave][3][cw], cw = chunk width (16 or 32)
+        const double* p = partial + (size_t)(c / cw) * wpc * 3 * cw + (c % cw);
+        for (int i = lane; i < wpc; i += 64) {
             if (scalar) {
-                a += partial[((int64_t)i * 3 + 0) * M + c];
-                b += partial[((int64_t)i * 3 + 1) * M + c];
+                a += p[(size_t)i * 3 * cw];
+                b += p[(size_t)i * 3 * cw + cw];
             } else {
-                a += partial[((int64_t)i * 3 + 2) * M + c];
+                a += p[(size_t)i * 3 * cw + 2 * cw];
             }
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -267,71 +239,6 @@ __global__ void upd_pre_kernel(const float* __restrict__ X, const float* __restr
         }
         float* u = U1S + n * 4 * M;
         u[w] = xs; u[M + w] = as; u[2 * M + w] = xdot; u[3 * M + w] = adot;
-    }
-}
-
-// Gate epilogue of a (scalar-row [s(2M) | t(M)], vector-row v) TP with node
-// attributes: h_s = c*SiLU(s+b), h_v = c*sigmoid(g+b) (na_k t + v);
-// writes the next TP's inputs U2S [V][2M] = [h_s | h_v.na], U2V [3][V][M] = h_v.
-__global__ void node_gate_kernel(const float* __restrict__ GS, const float* __restrict__ GV,
-                                 const float* __restrict__ NA, const float* __restrict__ bias, int64_t V, int M,
-                                 float* __restrict__ U2S, float* __restrict__ U2V) {
-    const int w = blockIdx.y * EW_X + threadIdx.x;
-    if (w >= M) return;
-    const float ba = bias[w], bg = bias[M + w];
-    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
-        const float* g = GS + n * 3 * M;
-        const float* na = NA + 4 * n;
-        const float hs = kC_SILU * silu_f(g[w] + ba);
-        const float gg = kC_SIGMOID * sigmoid_f(g[M + w] + bg);
-        const float t = g[2 * M + w];
-        float dot = 0.f;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float hv = gg * (na[1 + k] * t + GV[((int64_t)k * V + n) * M + w]);
-            U2V[((int64_t)k * V + n) * M + w] = hv;
-            dot += hv * na[1 + k];
-        }
-        U2S[n * 2 * M + w] = hs;
-        U2S[n * 2 * M + M + w] = dot;
-    }
-}
-
-// update_layer_2 epilogue + residual x += update (segnn.py:300-303) + feature
-// BatchNorm partial sums of the new x.
-__global__ void upd2_epi_kernel(const float* __restrict__ GS, const float* __restrict__ GV,
-                                const float* __restrict__ NA, const float* __restrict__ bias, int64_t V, int M,
-                                float* __restrict__ X, double* __restrict__ partial) {
-    __shared__ double red[3][EW_Y][EW_X];
-    const int w = blockIdx.y * EW_X + threadIdx.x;
-    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    if (w < M) {
-        const float b = bias[w];
-        for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
-            const float* g = GS + n * 2 * M;
-            const float* na = NA + 4 * n;
-            const float xs = X[n * M + w] + (g[w] + b);
-            X[n * M + w] = xs;
-            s1 += (double)xs;
-            s2 += (double)xs * xs;
-            const float t = g[M + w];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float* xp = X + ((1 + k) * V + n) * M + w;
-                const float xv = *xp + (na[1 + k] * t + GV[((int64_t)k * V + n) * M + w]);
-                *xp = xv;
-                s3 += (double)xv * xv;
-            }
-        }
-    }
-    red[0][threadIdx.y][threadIdx.x] = s1;
-    red[1][threadIdx.y][threadIdx.x] = s2;
-    red[2][threadIdx.y][threadIdx.x] = s3;
-    __syncthreads();
-    if (threadIdx.y < 3 && w < M) {
-        double acc = 0.0;
-        for (int y = 0; y < EW_Y; ++y) acc += red[threadIdx.y][y][threadIdx.x];
-        partial[((int64_t)blockIdx.x * 3 + threadIdx.y) * M + w] = acc;
     }
 }
 
@@ -417,16 +324,46 @@ __global__ void rollout_update_kernel(float* __restrict__ pos, float* __restrict
 }
 
 // ---------------------------------------------------------------- host side
+int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+struct Dims {
+    int64_t B, N, V, G, Ep;  // Ep = V * G padded edge slots
+    int M, chunks;
+};
+
+Dims dims_of(int64_t B, int64_t N, int M) {
+    Dims d;
+    d.B = B; d.N = N; d.V = B * N;
+    d.G = N > 1 ? next_pow2((int)(N - 1)) : 1;
+    d.Ep = d.V * d.G;
+    d.M = M;
+    d.chunks = (M + 31) / 32;
+    return d;
+}
+
+// Upper bound of waves per chunk over every fused launch (partials buffer size).
+// Upper bound of (chunks x waves per chunk x 3 x chunk width) over every fused
+// launch: the BN partial-sum buffer size in doubles.
+int64_t partial_doubles(const Dims& d) {
+    const int64_t tiles = (std::max(d.Ep, d.V) + 15) / 16;
+    const int64_t waves = std::min<int64_t>(tiles, 2 * 256 * 8);  // <= 2 blocks/CU x 8 waves per group
+    const int64_t chunks16 = (d.M + 15) / 16;
+    return std::max<int64_t>(1, (chunks16 + 1) * (waves + 8)) * 3 * 32;
+}
+
 struct Workspace {
-    float *X, *NA, *X0, *EG, *NP, *M1S, *M1V, *G2S, *G2V, *AGG, *U1S, *U1V, *G3S, *G3V, *U2S, *U2V, *G4S, *G4V, *coef_msg,
-        *coef_feat, *out;
+    float *X, *NA, *X0, *EG, *NP, *M1S, *M1V, *AGG, *U1S, *U1V, *U2S, *U2V, *coef_msg, *coef_feat, *out;
     double* partial;
     size_t bytes;
 };
 
 size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
-    const int64_t V = B * N, E = V * (N - 1);
-    const int64_t nblk = nbx::ceil_div(V > 0 ? V : 1, ROWS_PER_BLOCK);
+    const Dims d = dims_of(B, N, M);
+    const int64_t V = d.V, Ep = d.Ep;
     size_t off = 0;
     auto take = [&](size_t n_elems, size_t elem) -> void* {
         off = (off + 255) & ~size_t(255);
@@ -435,25 +372,19 @@ size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
         return p;
     };
     Workspace w;
-    w.partial = (double*)take(nblk * 3 * M, 8);
+    w.partial = (double*)take((size_t)partial_doubles(d), 8);
     w.X = (float*)take(4 * V * M, 4);
     w.NA = (float*)take(4 * V, 4);
     w.X0 = (float*)take(8 * V, 4);
-    w.EG = (float*)take(8 * E, 4);
+    w.EG = (float*)take(8 * Ep, 4);
     w.NP = (float*)take(4 * V * 6 * M, 4);
-    w.M1S = (float*)take(E * 2 * M, 4);
-    w.M1V = (float*)take(3 * E * M, 4);
-    w.G2S = (float*)take(E * 3 * M, 4);
-    w.G2V = (float*)take(3 * E * M, 4);
+    w.M1S = (float*)take(Ep * 2 * M, 4);
+    w.M1V = (float*)take(3 * Ep * M, 4);
     w.AGG = (float*)take(4 * V * M, 4);
     w.U1S = (float*)take(V * 4 * M, 4);
     w.U1V = (float*)take(3 * V * 2 * M, 4);
-    w.G3S = (float*)take(V * 3 * M, 4);
-    w.G3V = (float*)take(3 * V * M, 4);
     w.U2S = (float*)take(V * 2 * M, 4);
     w.U2V = (float*)take(3 * V * M, 4);
-    w.G4S = (float*)take(V * 3 * M, 4);
-    w.G4V = (float*)take(3 * V * M, 4);
     w.coef_msg = (float*)take(3 * M, 4);
     w.coef_feat = (float*)take(3 * M, 4);
     w.out = (float*)take(6 * V, 4);
@@ -474,93 +405,165 @@ dim3 ew_grid(int64_t rows, int M) {
     return dim3((unsigned)nbx::ceil_div(rows > 0 ? rows : 1, ROWS_PER_BLOCK), (unsigned)nbx::ceil_div(M, EW_X));
 }
 
-// Optional per-launch timing of the GEMM kernel (nbx_segnn_forward_timed):
-// an event pair around every gemm_f32 launch on the launch stream.
-struct GemmTiming {
+// Optional per-launch timing of the dominant kernel (nbx_segnn_forward_timed):
+// an event pair around every tp_fused launch on the launch stream.
+struct KernelTiming {
     std::vector<hipEvent_t> ev;
     double flops = 0.0;
     int launches = 0;
 };
 
-int timed_gemm(const nbx::GemmProb* probs, int np, hipStream_t st, GemmTiming* tm) {
-    if (!tm) return nbx::gemm_f32(probs, np, st);
+template <int NS, int NV, int EPI>
+int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    p.NS = NS;
+    p.NV = NV;
+    p.epi = EPI;
+    nbx::tp_geometry(p);
+    if (!tm) return nbx::tp_launch<NS, NV, EPI>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
     NBX_HIP(hipEventCreate(&b));
     tm->ev.push_back(a);
     tm->ev.push_back(b);
     NBX_HIP(hipEventRecord(a, st));
-    if (int rc = nbx::gemm_f32(probs, np, st)) return rc;
+    if (int rc = nbx::tp_launch<NS, NV, EPI>(p, st)) return rc;
     NBX_HIP(hipEventRecord(b, st));
-    for (int i = 0; i < np; ++i) tm->flops += 2.0 * probs[i].M * (double)probs[i].N * probs[i].K;
+    double k = 0;
+    for (int j = 0; j < NS; ++j) k += p.K[j];
+    k += NV ? 3.0 * p.Kv : 0.0;
+    tm->flops += 2.0 * p.rows * 32.0 * p.chunks * k;  // executed MACs x 2 (incl. channel padding)
     tm->launches += 1;
     return NBX_OK;
 }
 
+template <int NS, int NV, int EPI, int CG>
+int run_tp16(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG>(p, st);
+    hipEvent_t a, b;
+    NBX_HIP(hipEventCreate(&a));
+    NBX_HIP(hipEventCreate(&b));
+    tm->ev.push_back(a);
+    tm->ev.push_back(b);
+    NBX_HIP(hipEventRecord(a, st));
+    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG>(p, st)) return rc;
+    NBX_HIP(hipEventRecord(b, st));
+    double k = 0;
+    for (int j = 0; j < NS; ++j) k += p.K[j];
+    k += NV ? 3.0 * p.Kv : 0.0;
+    tm->flops += 2.0 * p.rows * 16.0 * p.chunks * k;
+    tm->launches += 1;
+    return NBX_OK;
+}
+
+nbx::TpProb tp_base(int rows, const Dims& d) {
+    nbx::TpProb p;
+    memset(&p, 0, sizeof(p));
+    p.rows = rows;
+    p.M = d.M;
+    p.chunks = d.chunks;
+    return p;
+}
+
 int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass, int64_t B,
-                 int64_t N, float* out, const Workspace& ws, hipStream_t st, GemmTiming* tm = nullptr) {
-    using nbx::make_prob;
+                 int64_t N, float* out, const Workspace& ws, hipStream_t st, KernelTiming* tm = nullptr) {
     const int M = w->mul;
-    const int64_t V = B * N, E = V * (N - 1);
-    const int iV = (int)V, iE = (int)E;
+    const Dims d = dims_of(B, N, M);
+    const int64_t V = d.V, Ep = d.Ep;
     const dim3 ewb(EW_X, EW_Y);
-    const int nblk = (int)nbx::ceil_div(V, ROWS_PER_BLOCK);
 
     hipLaunchKernelGGL(featurize_kernel, dim3((unsigned)nbx::ceil_div(V, 256)), dim3(256), 0, st, pos, vel, mass, V,
-                       (int)N, ws.NA, ws.X0, ws.EG);
+                       (int)N, (int)d.G, ws.NA, ws.X0, ws.EG);
     hipLaunchKernelGGL(embed_kernel, ew_grid(V, M), ewb, 0, st, ws.X0, ws.NA, w->emb, w->emb_bias, V, M, ws.X);
     NBX_LAUNCH_CHECK("embed");
 
     for (int l = 0; l < w->num_layers; ++l) {
         const nbx_segnn_layer& L = w->layers[l];
         if (N > 1) {
-            // node precomputation of message_layer_1 (x_i / x_j halves)
-            nbx::GemmProb np[2] = {
-                make_prob(ws.X, M, L.node_pre_s_t, M, ws.NP, 6 * M, iV, 6 * M, M),
-                make_prob(ws.X + V * M, M, L.node_pre_v_t, M, ws.NP + V * 6 * M, 6 * M, 3 * iV, 6 * M, M)};
-            if (int rc = timed_gemm(np, 2, st, tm)) return rc;
-            hipLaunchKernelGGL(msg1_kernel, ew_grid(E, M), ewb, 0, st, ws.NP, ws.EG, L.msg1_amf, L.msg1_bias, V,
-                               (int)N, M, ws.M1S, ws.M1V);
+            // message_layer_1, x_i / x_j halves once per node (plain fused GEMM, 96-column chunks)
+            for (int part = 0; part < 2; ++part) {
+                nbx::TpProb p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
+                p.As = ws.X + (part ? V * M : 0);
+                p.lda_s = M;
+                p.Bs = part ? L.node_pre_v_t : L.node_pre_s_t;
+                p.ldb_s = M;
+                p.K[0] = p.K[1] = p.K[2] = M;
+                p.chunks = (6 * M + 47) / 48;  // 48-column chunks (3 sub-tiles of 16)
+                p.C = ws.NP + (part ? V * 6 * M : 0);
+                p.ldc = 6 * M;
+                p.ncols = 6 * M;
+                if (int rc = run_tp16<3, 0, nbx::TP_PLAIN, 2>(p, st, tm)) return rc;
+            }
+            hipLaunchKernelGGL(msg1_kernel, ew_grid(Ep, M), ewb, 0, st, ws.NP, ws.EG, L.msg1_amf, L.msg1_bias, V,
+                               (int)N, (int)d.G, M, ws.M1S, ws.M1V);
             NBX_LAUNCH_CHECK("msg1");
-            nbx::GemmProb m2[2] = {make_prob(ws.M1S, 2 * M, L.msg2_s_t, 2 * M, ws.G2S, 3 * M, iE, 3 * M, 2 * M),
-                                   make_prob(ws.M1V, M, L.msg2_v_t, M, ws.G2V, M, 3 * iE, M, M)};
-            if (int rc = timed_gemm(m2, 2, st, tm)) return rc;
         }
-        hipLaunchKernelGGL(msg2_epi_kernel, ew_grid(V, M), ewb, 0, st, ws.G2S, ws.G2V, ws.EG, L.msg2_bias, V,
-                           (int)N, M, ws.AGG, ws.partial);
-        NBX_LAUNCH_CHECK("msg2_epi");
+        int wpc_msg = 1, cw_msg = 16;
+        {
+            // message_layer_2 + gate + aggregation + message-BN partial sums
+            nbx::TpProb p = tp_base((int)Ep, d);
+            p.As = ws.M1S; p.lda_s = 2 * M; p.Bs = L.msg2_s_t; p.ldb_s = 2 * M;
+            p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
+            p.Av = ws.M1V; p.lda_v = M; p.plane_stride = Ep * M; p.Bv = L.msg2_v_t; p.ldb_v = M; p.Kv = M;
+            p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G; p.valid_per_group = (int)(N - 1);
+            p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
+            if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
+                if (int rc = run_tp<3, 1, nbx::TP_MSG>(p, st, tm)) return rc;
+                wpc_msg = p.waves_per_chunk;
+                cw_msg = 32;
+            } else {
+                NBX_HIP(hipMemsetAsync(ws.AGG, 0, sizeof(float) * 4 * V * M, st));
+                NBX_HIP(hipMemsetAsync(ws.partial, 0, sizeof(double) * 48 * ((M + 15) / 16), st));
+            }
+        }
         hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
-                           nblk, (double)E, M, w->training, w->bn_eps, w->bn_momentum, L.msg_bn_weight,
-                           L.msg_bn_bias, L.msg_bn_running_mean, L.msg_bn_running_var, ws.coef_msg);
+                           wpc_msg, cw_msg, (double)(V * (N - 1) > 0 ? V * (N - 1) : 1), M, w->training, w->bn_eps,
+                           w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
+                           L.msg_bn_running_var, ws.coef_msg);
         NBX_LAUNCH_CHECK("bn_finalize(msg)");
         hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg,
                            (float)(N - 1), V, M, ws.U1S, ws.U1V);
         NBX_LAUNCH_CHECK("upd_pre");
-        nbx::GemmProb u1[2] = {make_prob(ws.U1S, 4 * M, L.upd1_s_t, 4 * M, ws.G3S, 3 * M, iV, 3 * M, 4 * M),
-                               make_prob(ws.U1V, 2 * M, L.upd1_v_t, 2 * M, ws.G3V, M, 3 * iV, M, 2 * M)};
-        if (int rc = timed_gemm(u1, 2, st, tm)) return rc;
-        hipLaunchKernelGGL(node_gate_kernel, ew_grid(V, M), ewb, 0, st, ws.G3S, ws.G3V, ws.NA, L.upd1_bias, V, M,
-                           ws.U2S, ws.U2V);
-        NBX_LAUNCH_CHECK("upd1_gate");
-        nbx::GemmProb u2[2] = {make_prob(ws.U2S, 2 * M, L.upd2_s_t, 2 * M, ws.G4S, 2 * M, iV, 2 * M, 2 * M),
-                               make_prob(ws.U2V, M, L.upd2_v_t, M, ws.G4V, M, 3 * iV, M, M)};
-        if (int rc = timed_gemm(u2, 2, st, tm)) return rc;
-        hipLaunchKernelGGL(upd2_epi_kernel, ew_grid(V, M), ewb, 0, st, ws.G4S, ws.G4V, ws.NA, L.upd2_bias, V, M, ws.X,
-                           ws.partial);
-        NBX_LAUNCH_CHECK("upd2_epi");
+        {
+            // update_layer_1 + gate -> inputs of update_layer_2
+            nbx::TpProb p = tp_base((int)V, d);
+            p.As = ws.U1S; p.lda_s = 4 * M; p.Bs = L.upd1_s_t; p.ldb_s = 4 * M;
+            p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M;
+            p.Av = ws.U1V; p.lda_v = 2 * M; p.plane_stride = V * 2 * M; p.Bv = L.upd1_v_t; p.ldb_v = 2 * M;
+            p.Kv = 2 * M;
+            p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
+            p.chunks = (M + 15) / 16;
+            if (int rc = run_tp16<3, 1, nbx::TP_GATE_NODE, 1>(p, st, tm)) return rc;
+        }
+        int wpc_feat;
+        {
+            // update_layer_2 + residual + feature-BN partial sums
+            nbx::TpProb p = tp_base((int)V, d);
+            p.As = ws.U2S; p.lda_s = 2 * M; p.Bs = L.upd2_s_t; p.ldb_s = 2 * M;
+            p.K[0] = 2 * M; p.K[1] = M;
+            p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Bv = L.upd2_v_t; p.ldb_v = M; p.Kv = M;
+            p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
+            p.partial = ws.partial;
+            p.chunks = (M + 15) / 16;
+            if (int rc = run_tp16<2, 1, nbx::TP_RESID, 2>(p, st, tm)) return rc;
+            wpc_feat = p.waves_per_chunk;
+        }
         hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
-                           nblk, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
+                           wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
                            L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat);
         hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M);
         NBX_LAUNCH_CHECK("bn_apply");
     }
     // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)
-    hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA, V, M, ws.U2S);
-    nbx::GemmProb p1[2] = {make_prob(ws.U2S, 2 * M, w->pp1_s_t, 2 * M, ws.G3S, 3 * M, iV, 3 * M, 2 * M),
-                           make_prob(ws.X + V * M, M, w->pp1_v_t, M, ws.G3V, M, 3 * iV, M, M)};
-    if (int rc = timed_gemm(p1, 2, st, tm)) return rc;
-    hipLaunchKernelGGL(node_gate_kernel, ew_grid(V, M), ewb, 0, st, ws.G3S, ws.G3V, ws.NA, w->pp1_bias, V, M, ws.U2S,
-                       ws.U2V);
+    hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA, V, M, ws.U1S);
+    {
+        nbx::TpProb p = tp_base((int)V, d);
+        p.As = ws.U1S; p.lda_s = 2 * M; p.Bs = w->pp1_s_t; p.ldb_s = 2 * M;
+        p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
+        p.Av = ws.X + V * M; p.lda_v = M; p.plane_stride = V * M; p.Bv = w->pp1_v_t; p.ldb_v = M; p.Kv = M;
+        p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
+        p.chunks = (M + 15) / 16;
+        if (int rc = run_tp16<3, 1, nbx::TP_GATE_NODE, 2>(p, st, tm)) return rc;
+    }
     hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,
                        w->pp2, V, M, out);
     NBX_LAUNCH_CHECK("pre_pool2");
@@ -570,7 +573,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
 int prepare(const nbx_segnn_weights* w, int64_t B, int64_t N, void* workspace, size_t bytes, Workspace* ws) {
     if (int rc = check_weights(w)) return rc;
     NBX_CHECK_ARG(B >= 1 && N >= 1, "segnn: need B >= 1 and N >= 1");
-    NBX_CHECK_ARG(B * N * (N > 1 ? N - 1 : 1) < (int64_t)1 << 30, "segnn: graph too large");
+    NBX_CHECK_ARG(N <= 33, "segnn: native path supports systems of at most 33 nodes (got %lld)", (long long)N);
+    NBX_CHECK_ARG(B * N * 32 < (int64_t)1 << 30, "segnn: graph too large");
     const size_t need = carve(ws, workspace, B, N, w->mul);
     if (bytes < need || workspace == nullptr) {
         nbx::set_error("segnn: workspace too small (%zu < %zu bytes)", bytes, need);
@@ -623,7 +627,7 @@ extern "C" int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* 
     Workspace ws;
     if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     hipStream_t st = (hipStream_t)stream;
-    GemmTiming tm;
+    KernelTiming tm;
     hipEvent_t t0, t1;
     NBX_HIP(hipEventCreate(&t0));
     NBX_HIP(hipEventCreate(&t1));

@@ -1,0 +1,359 @@
+// Fine-grained variant of the fused tensor-product kernel: v_mfma_f32_16x16x4_f32,
+// 16-row tiles, CG chunks of 16 output channels per wave.
+//
+// Same contract as tp_fused.h (TpProb, epilogues), but the weight chunks are
+// 16 channels wide (B rows stored [chunks16][NS][16][K]) so node-row problems
+// (V = B*N rows) spread over ~4x more waves, and accumulators are 4 registers
+// per tile, which keeps 4 waves per SIMD resident.
+//   16x16x4 f32 fragments: A lane l -> A[row = l & 15][k = l >> 4], B -> B[k = l >> 4][col = l & 15],
+//   C register j -> row 4 (l >> 4) + j, col l & 15.  Dependent-issue latency is 40 cycles, so
+//   the MFMAs of a k-step are issued round-robin over the (NS + 3 NV) x CG accumulators.
+// Inside a 32-deep K chunk lane quarter qd supplies k = 8 qd + s at step s (permuted, same sum).
+#pragma once
+#include "tp_fused.h"
+
+namespace nbx {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ inline float f4get(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
+
+template <int NS, int NV, int EPI, int CG>
+__global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int NT = NS + NV;  // B sub-tiles per chunk
+    const int cgroup = blockIdx.x / P.blocks_per_chunk;   // group of CG 16-channel chunks
+    const int blk = blockIdx.x - cgroup * P.blocks_per_chunk;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
+    const int nchunks16 = P.chunks;                        // total 16-channel chunks
+
+    int pit[NT], sub_off[NT];
+    int stride_g = 0;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        pit[j] = tp_pitch(j < NS ? P.K[j] : P.Kv);
+        sub_off[j] = stride_g;
+        stride_g += 16 * pit[j];
+    }
+    // ---- stage CG chunks of weights in LDS
+#pragma unroll
+    for (int g = 0; g < CG; ++g) {
+        const int ch = cgroup * CG + g;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const bool vec = j == NS;
+            const int K = vec ? P.Kv : P.K[j];
+            const int pitch = pit[j];
+            const int q4 = pitch / 4;
+            float* dst = &lds[g * stride_g + sub_off[j]];
+            const float* src = vec ? P.Bv + (size_t)ch * 16 * P.ldb_v : P.Bs + ((size_t)ch * NS + j) * 16 * P.ldb_s;
+            const int ld = vec ? P.ldb_v : P.ldb_s;
+            for (int i = t; i < 16 * q4; i += T16_THREADS) {
+                const int row = i / q4, kq = (i - row * q4) * 4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ch < nchunks16 && kq < K) v = *reinterpret_cast<const float4*>(src + (size_t)row * ld + kq);
+                *reinterpret_cast<float4*>(dst + row * pitch + kq) = v;
+            }
+        }
+    }
+    __syncthreads();
+
+    const int ks_chunks = (P.K[0] + 31) >> 5;
+    const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
+    const int n_chunks = ks_chunks + 3 * kv_chunks;
+    const int row_tiles = (P.rows + 15) >> 4;
+    const int wstride = P.blocks_per_chunk * T16_WAVES;
+    const int wid = blk * T16_WAVES + wave;
+
+    double st0[CG], st1[CG], st2[CG];
+#pragma unroll
+    for (int g = 0; g < CG; ++g) st0[g] = st1[g] = st2[g] = 0.0;
+
+    auto load_a = [&](int rt, int i, float4 (&a)[2]) {
+        const int row = rt * 16 + c16;
+        const float* base;
+        int k0;
+        bool ok = row < P.rows;
+        if (i < ks_chunks) {
+            base = P.As + (size_t)row * P.lda_s;
+            k0 = i * 32;
+            ok = ok && k0 + 8 * qd < P.K[0];
+        } else {
+            const int v = i - ks_chunks, plane = v / kv_chunks;
+            k0 = (v - plane * kv_chunks) * 32;
+            base = P.Av + plane * P.plane_stride + (size_t)row * P.lda_v;
+            ok = ok && k0 + 8 * qd < P.Kv;
+        }
+        const float* p = base + k0 + 8 * qd;
+        a[0] = ok ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a[1] = ok ? *reinterpret_cast<const float4*>(p + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+
+    // A chunks are prefetched two ahead (cur <- nxt <- nx2); (lrt, li) = next chunk to load
+    int rt = wid;
+    if (rt < row_tiles) {
+        float4 cur[2], nxt[2], nx2[2];
+        int lrt = rt, li = 0;
+        auto advance = [&]() {
+            if (++li >= n_chunks) {
+                li = 0;
+                lrt += wstride;
+            }
+        };
+        load_a(lrt, li, cur);
+        advance();
+        if (lrt < row_tiles) load_a(lrt, li, nxt);
+        advance();
+        while (true) {
+            floatx4 acc[CG][NS + 3 * NV];
+#pragma unroll
+            for (int g = 0; g < CG; ++g)
+#pragma unroll
+                for (int j = 0; j < NS + 3 * NV; ++j) acc[g][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            const int next_rt = rt + wstride;
+            for (int i = 0; i < n_chunks; ++i) {
+                if (lrt < row_tiles) load_a(lrt, li, nx2);
+                advance();
+                const float av[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+                if (i < ks_chunks) {
+                    const int k0 = i * 32;
+                    float4 b[CG][NS][2];
+#pragma unroll
+                    for (int g = 0; g < CG; ++g)
+#pragma unroll
+                        for (int j = 0; j < NS; ++j) {
+                            if (k0 >= P.K[j]) continue;
+                            const float* bp = &lds[g * stride_g + sub_off[j] + c16 * pit[j] + k0 + 8 * qd];
+                            b[g][j][0] = *reinterpret_cast<const float4*>(bp);
+                            b[g][j][1] = *reinterpret_cast<const float4*>(bp + 4);
+                        }
+#pragma unroll
+                    for (int s = 0; s < 8; ++s) {
+#pragma unroll
+                        for (int g = 0; g < CG; ++g)
+#pragma unroll
+                            for (int j = 0; j < NS; ++j) {
+                                if (k0 >= P.K[j]) continue;
+                                const float bv = f4get(b[g][j][s >> 2], s & 3);
+                                acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv, acc[g][j], 0, 0, 0);
+                            }
+                    }
+                } else if (NV) {
+                    const int v = i - ks_chunks, plane = v / kv_chunks;
+                    const int k0 = (v - plane * kv_chunks) * 32;
+                    float4 b[CG][2];
+#pragma unroll
+                    for (int g = 0; g < CG; ++g) {
+                        const float* bp = &lds[g * stride_g + sub_off[NS] + c16 * pit[NS] + k0 + 8 * qd];
+                        b[g][0] = *reinterpret_cast<const float4*>(bp);
+                        b[g][1] = *reinterpret_cast<const float4*>(bp + 4);
+                    }
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) {
+                        if (pl != plane) continue;
+#pragma unroll
+                        for (int s = 0; s < 8; ++s)
+#pragma unroll
+                            for (int g = 0; g < CG; ++g) {
+                                const float bv = f4get(b[g][s >> 2], s & 3);
+                                acc[g][NS + pl] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv, acc[g][NS + pl], 0, 0, 0);
+                            }
+                    }
+                }
+                cur[0] = nxt[0];
+                cur[1] = nxt[1];
+                nxt[0] = nx2[0];
+                nxt[1] = nx2[1];
+            }
+
+            // ------------------------------------------------------------ epilogue
+            const int row0 = rt * 16 + 4 * qd;   // rows of registers 0..3: row0 + jj
+#pragma unroll
+            for (int g = 0; g < CG; ++g) {
+                const int ch = (cgroup * CG + g) * 16 + c16;
+                const int M = P.M;
+                if constexpr (EPI == TP_PLAIN) {
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) {
+                        const int col = ((cgroup * CG + g) * NS + j) * 16 + c16;
+                        if (col < P.ncols)
+#pragma unroll
+                            for (int jj = 0; jj < 4; ++jj)
+                                if (row0 + jj < P.rows) P.C[(size_t)(row0 + jj) * P.ldc + col] = acc[g][j][jj];
+                    }
+                } else if constexpr (EPI == TP_MSG) {
+                    const bool live = ch < M;
+                    const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
+                    float ms[4], m0[4], m1[4], m2[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int row = row0 + jj;
+                        const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group;
+                        const float* gm = P.geom + (size_t)(row < P.rows ? row : 0) * 8;
+                        const float s = kC_SILU * tp_silu(acc[g][0][jj] + ba);
+                        const float gg = kC_SIGMOID * tp_sigmoid(acc[g][1][jj] + bg);
+                        const float tt = acc[g][2][jj];
+                        ms[jj] = ok ? s : 0.f;
+                        m0[jj] = ok ? gg * (gm[0] * tt + acc[g][NS + 0][jj]) : 0.f;
+                        m1[jj] = ok ? gg * (gm[1] * tt + acc[g][NS + 1][jj]) : 0.f;
+                        m2[jj] = ok ? gg * (gm[2] * tt + acc[g][NS + 2][jj]) : 0.f;
+                        st0[g] += (double)ms[jj];
+                        st1[g] += (double)ms[jj] * ms[jj];
+                        st2[g] += (double)m0[jj] * m0[jj] + (double)m1[jj] * m1[jj] + (double)m2[jj] * m2[jj];
+                    }
+                    const int G = P.group;
+                    auto put = [&](int row, float a0, float a1, float a2, float a3) {
+                        if (live && row < P.rows) {
+                            const size_t o = (size_t)(row / G) * M + ch;
+                            P.out_s[o] = a0;
+                            P.out_v[o] = a1;
+                            P.out_v[P.out_plane + o] = a2;
+                            P.out_v[2 * P.out_plane + o] = a3;
+                        }
+                    };
+                    if (G <= 4) {
+#pragma unroll
+                        for (int s0 = 0; s0 < 4; ++s0) {
+                            if (s0 % G) continue;
+                            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (s0 + u >= 4 || u >= G) continue;
+                                a0 += ms[s0 + u]; a1 += m0[s0 + u]; a2 += m1[s0 + u]; a3 += m2[s0 + u];
+                            }
+                            put(row0 + s0, a0, a1, a2, a3);
+                        }
+                    } else {  // G = 8 or 16: lanes qd and qd^1 (^2) hold the other rows of the group
+                        float a0 = ms[0] + ms[1] + ms[2] + ms[3], a1 = m0[0] + m0[1] + m0[2] + m0[3];
+                        float a2 = m1[0] + m1[1] + m1[2] + m1[3], a3 = m2[0] + m2[1] + m2[2] + m2[3];
+                        a0 += __shfl_xor(a0, 16); a1 += __shfl_xor(a1, 16);
+                        a2 += __shfl_xor(a2, 16); a3 += __shfl_xor(a3, 16);
+                        if (G == 16) {
+                            a0 += __shfl_xor(a0, 32); a1 += __shfl_xor(a1, 32);
+                            a2 += __shfl_xor(a2, 32); a3 += __shfl_xor(a3, 32);
+                        }
+                        if ((qd & (G / 4 - 1)) == 0) put(row0, a0, a1, a2, a3);
+                    }
+                } else if constexpr (EPI == TP_GATE_NODE) {
+                    const bool live = ch < M;
+                    const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int row = row0 + jj;
+                        if (!live || row >= P.rows) continue;
+                        const float* na = P.geom + (size_t)row * 4;
+                        const float hs = kC_SILU * tp_silu(acc[g][0][jj] + ba);
+                        const float gg = kC_SIGMOID * tp_sigmoid(acc[g][1][jj] + bg);
+                        const float tt = acc[g][2][jj];
+                        const float h0 = gg * (na[1] * tt + acc[g][NS + 0][jj]);
+                        const float h1 = gg * (na[2] * tt + acc[g][NS + 1][jj]);
+                        const float h2 = gg * (na[3] * tt + acc[g][NS + 2][jj]);
+                        P.out_s[(size_t)row * 2 * M + ch] = hs;
+                        P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
+                        P.out_v[(size_t)row * M + ch] = h0;
+                        P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
+                        P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
+                    }
+                } else if constexpr (EPI == TP_RESID) {
+                    const bool live = ch < M;
+                    const float b = live ? P.bias[ch] : 0.f;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int row = row0 + jj;
+                        if (!live || row >= P.rows) continue;
+                        const float* na = P.geom + (size_t)row * 4;
+                        const float tt = acc[g][1][jj];
+                        float* xs = P.out_s + (size_t)row * M + ch;
+                        const float s = *xs + (acc[g][0][jj] + b);
+                        *xs = s;
+                        float* x0 = P.out_v + (size_t)row * M + ch;
+                        float* x1 = x0 + P.out_plane;
+                        float* x2 = x1 + P.out_plane;
+                        const float v0 = *x0 + (na[1] * tt + acc[g][NS + 0][jj]);
+                        const float v1 = *x1 + (na[2] * tt + acc[g][NS + 1][jj]);
+                        const float v2 = *x2 + (na[3] * tt + acc[g][NS + 2][jj]);
+                        *x0 = v0; *x1 = v1; *x2 = v2;
+                        st0[g] += (double)s;
+                        st1[g] += (double)s * s;
+                        st2[g] += (double)v0 * v0 + (double)v1 * v1 + (double)v2 * v2;
+                    }
+                }
+            }
+            rt = next_rt;
+            if (rt >= row_tiles) break;
+        }
+    }
+    if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
+        // reduce the 8 waves of the block in LDS (the weights are no longer needed), one
+        // partial row per block: layout [chunk16][block][3][16]
+        __syncthreads();
+        double* red = reinterpret_cast<double*>(lds);   // [CG][3][8 waves][16]
+#pragma unroll
+        for (int g = 0; g < CG; ++g) {
+            double a = st0[g], b = st1[g], c = st2[g];
+            a += __shfl_xor(a, 16); b += __shfl_xor(b, 16); c += __shfl_xor(c, 16);
+            a += __shfl_xor(a, 32); b += __shfl_xor(b, 32); c += __shfl_xor(c, 32);
+            if (qd == 0) {
+                red[((g * 3 + 0) * T16_WAVES + wave) * 16 + c16] = a;
+                red[((g * 3 + 1) * T16_WAVES + wave) * 16 + c16] = b;
+                red[((g * 3 + 2) * T16_WAVES + wave) * 16 + c16] = c;
+            }
+        }
+        __syncthreads();
+        if (t < CG * 3 * 16) {
+            const int g = t / 48, st = (t / 16) % 3, c = t % 16;
+            double acc = 0.0;
+            for (int w = 0; w < T16_WAVES; ++w) acc += red[((g * 3 + st) * T16_WAVES + w) * 16 + c];
+            const int ch16 = cgroup * CG + g;
+            if (ch16 < nchunks16) P.partial[((size_t)ch16 * P.blocks_per_chunk + blk) * 48 + st * 16 + c] = acc;
+        }
+    }
+}
+
+template <int CG>
+inline int tp16_lds_floats(const TpProb& p) {
+    auto pitch = [](int K) { return ((K + 31) & ~31) + 4; };
+    int n = 0;
+    for (int j = 0; j < p.NS; ++j) n += 16 * pitch(p.K[j]);
+    if (p.NV) n += 16 * pitch(p.Kv);
+    return n * CG;
+}
+
+// p.chunks = number of 16-channel chunks; grid = ceil(chunks / CG) groups x blocks_per_chunk
+template <int NS, int NV, int EPI, int CG>
+int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
+    p.NS = NS;
+    p.NV = NV;
+    p.epi = EPI;
+    if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
+    p.lds_floats = tp16_lds_floats<CG>(p);
+    const size_t lds = (size_t)p.lds_floats * 4;
+    if (lds > 160 * 1024) {
+        set_error("tp16: weight chunk group needs %zu bytes of LDS (> 160 KiB)", lds);
+        return NBX_E_UNSUPPORTED;
+    }
+    const int groups = (p.chunks + CG - 1) / CG;
+    int per_cu = (int)((160 * 1024) / lds);
+    if (per_cu > 2) per_cu = 2;
+    if (per_cu < 1) per_cu = 1;
+    const int row_tiles = (p.rows + 15) / 16;
+    int bpc = (num_cus * per_cu + groups - 1) / groups;
+    const int max_bpc = (row_tiles + T16_WAVES - 1) / T16_WAVES;
+    if (bpc > max_bpc) bpc = max_bpc;
+    if (bpc < 1) bpc = 1;
+    p.blocks_per_chunk = bpc;
+    p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
+    static bool attr_set = false;
+    if (!attr_set) {
+        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG>), dim3(groups * bpc), dim3(T16_THREADS), lds, st, p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
+}  // namespace nbx

@@ -1,0 +1,402 @@
+// Weight-stationary fused O(3) tensor-product kernel (fp32 MFMA) for SEGNN.
+//
+// Every l <= 1 tensor product of the path is a pair of GEMMs on the same rows:
+//   scalar part  A_S[row, K_S] x B_S -> NS sub-tiles of 32 output columns (e.g. s, gate, t)
+//   vector part  A_V[k][row, K_V] x B_V -> 1 sub-tile per component plane k = 0..2
+// for one 32-channel "chunk" of the output.  A block owns one chunk: its slices
+// of B_S / B_V are loaded into LDS once and stay there while the block's waves
+// stream 32-row tiles of A straight from global memory (register double
+// buffering, no barrier in the main loop).  A wave keeps the whole chunk of its
+// 32 rows in accumulators (NS + 3 tiles of v_mfma_f32_32x32x2_f32), so the
+// epilogue - SiLU/sigmoid gate, aggregation over a node's incoming edges,
+// BatchNorm partial sums, residual update - runs in registers.
+//
+// MFMA 32x32x2 f32 fragment maps (cdna_hip_programming.md §3):
+//   A: lane l holds A[row = l & 31][k = l >> 5];  B: B[k = l >> 5][col = l & 31]
+//   C: col = l & 31, row = (j & 3) + 8 (j >> 2) + 4 (l >> 5), j = register 0..15
+// Inside every 32-deep K chunk the K order is permuted so that a lane reads 16
+// consecutive k (lane half h supplies k = 16h + s at MFMA step s for both
+// operands: the sum is unchanged).
+#pragma once
+#include "nbx_internal.h"
+
+namespace nbx {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3 };
+
+struct TpProb {
+    // scalar part: NS sub-tiles, sub-tile j uses the first K_j columns of its B rows
+    const float* As;   // [rows][lda_s]
+    const float* Bs;   // [chunks][NS][32][ldb_s]
+    int lda_s, ldb_s, NS;
+    int K[3];
+    // vector part (NV = 1: three planes, NV = 0: none)
+    const float* Av;   // plane k, row r at Av + k * plane_stride + r * lda_v
+    const float* Bv;   // [chunks][32][ldb_v]
+    long plane_stride;
+    int lda_v, ldb_v, Kv, NV;
+    int rows, chunks, M;  // M = real channels (epilogue mask)
+    int epi;
+    // PLAIN: C[row][chunk*NS*32 + 32 j + col]
+    float* C;
+    int ldc, ncols;
+    // epilogue operands
+    const float* bias;   // gate: [2M] (s, gate); resid: [M]
+    const float* geom;   // MSG: per-edge [rows][8] (rhat xyz ...); GATE_NODE/RESID: node attrs [rows][4]
+    int group;           // MSG: edges per destination (power of two <= 32)
+    int valid_per_group; // MSG: real edges per destination (<= group)
+    float* out_s;        // MSG: AGG plane 0 [nodes][M]; GATE_NODE: U2S [rows][2M]; RESID: X plane 0
+    float* out_v;        // MSG: AGG planes 1..3; GATE_NODE: U2V planes; RESID: X planes 1..3
+    long out_plane;      // stride between output planes (elements)
+    double* partial;     // MSG / RESID: [chunks][waves_per_chunk][3][32] fp64 BN partial sums
+    int waves_per_chunk;
+    // grid geometry (set by the launcher)
+    int blocks_per_chunk;
+    int lds_floats;
+};
+
+constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
+
+__device__ inline float tp_silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ inline float tp_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ inline int tp_pitch(int K) { return ((K + 31) & ~31) + 4; }
+
+template <int NS, int NV, int EPI>
+__global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int chunk = blockIdx.x / P.blocks_per_chunk;
+    const int blk = blockIdx.x - chunk * P.blocks_per_chunk;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+
+    // ---- stage this chunk's weights in LDS (zero-padded to 32-deep K chunks)
+    int off[NS + 1];
+    int pit[NS + 1];
+    {
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            off[j] = o;
+            pit[j] = tp_pitch(P.K[j]);
+            o += 32 * pit[j];
+        }
+        off[NS] = o;
+        pit[NS] = tp_pitch(P.Kv);
+    }
+#pragma unroll
+    for (int j = 0; j < NS + NV; ++j) {
+        const bool vec = j == NS;
+        const int K = vec ? P.Kv : P.K[j];
+        const int pitch = pit[j];
+        const int ld = vec ? P.ldb_v : P.ldb_s;
+        const int q4 = pitch / 4;  // float4 per LDS row (incl. pad)
+        for (int i = t; i < 32 * q4; i += TP_THREADS) {
+            const int row = i / q4, kq = (i - row * q4) * 4;
+            // scalar-part B rows are stored 16-channel interleaved: [chunks16][NS][16][K]
+            const float* src = vec ? P.Bv + ((size_t)chunk * 32 + row) * P.ldb_v
+                                   : P.Bs + (((size_t)(2 * chunk + (row >> 4)) * NS + j) * 16 + (row & 15)) * P.ldb_s;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (kq < K) v = *reinterpret_cast<const float4*>(src + kq);
+            *reinterpret_cast<float4*>(&lds[off[j] + row * pitch + kq]) = v;
+        }
+    }
+    __syncthreads();
+
+    const int ks_chunks = (P.K[0] + 31) >> 5;            // K_S = K[0] (sub-tile 0 uses all of it)
+    const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
+    const int n_chunks = ks_chunks + 3 * kv_chunks;      // A chunks per row tile
+    const int row_tiles = (P.rows + 31) >> 5;
+    const int wstride = P.blocks_per_chunk * TP_WAVES;
+    const int wid = blk * TP_WAVES + wave;               // wave index within this chunk
+
+    double st0 = 0.0, st1 = 0.0, st2 = 0.0;              // BN partial sums for column r
+
+    // A-chunk loader: chunk i of a row tile -> 16 floats per lane (4 x dwordx4)
+    auto load_a = [&](int rt, int i, float4 (&a)[4]) {
+        const int row = rt * 32 + r;
+        const float* base;
+        int k0;
+        bool ok = row < P.rows;
+        if (i < ks_chunks) {
+            base = P.As + (size_t)row * P.lda_s;
+            k0 = i * 32;
+            ok = ok && k0 + 16 * h < P.K[0];
+        } else {
+            const int v = i - ks_chunks, plane = v / kv_chunks;
+            k0 = (v - plane * kv_chunks) * 32;
+            base = P.Av + plane * P.plane_stride + (size_t)row * P.lda_v;
+            ok = ok && k0 + 16 * h < P.Kv;
+        }
+        const float* p = base + k0 + 16 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            a[q] = ok ? *reinterpret_cast<const float4*>(p + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+
+    int rt = wid;
+    if (rt >= row_tiles) goto done;
+    {
+        float4 cur[4], nxt[4];
+        load_a(rt, 0, cur);
+        while (true) {
+            floatx16 acc[NS + 3 * NV];
+#pragma unroll
+            for (int j = 0; j < NS + 3 * NV; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+            const int next_rt = rt + wstride;
+            for (int i = 0; i < n_chunks; ++i) {
+                // prefetch the next A chunk (possibly the next row tile's first)
+                if (i + 1 < n_chunks) load_a(rt, i + 1, nxt);
+                else if (next_rt < row_tiles) load_a(next_rt, 0, nxt);
+                if (i < ks_chunks) {
+                    const int k0 = i * 32;
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) {
+                        if (k0 >= P.K[j]) continue;
+                        const float* bp = &lds[off[j] + r * pit[j] + k0 + 16 * h];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * q);
+                            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4.x, acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4.y, acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4.z, acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4.w, acc[j], 0, 0, 0);
+                        }
+                    }
+                } else if (NV) {
+                    const int v = i - ks_chunks, plane = v / kv_chunks;
+                    const int k0 = (v - plane * kv_chunks) * 32;
+                    const float* bp = &lds[off[NS] + r * pit[NS] + k0 + 16 * h];
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) {
+                        if (pl != plane) continue;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * q);
+                            acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4.x, acc[NS + pl], 0, 0, 0);
+                            acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4.y, acc[NS + pl], 0, 0, 0);
+                            acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4.z, acc[NS + pl], 0, 0, 0);
+                            acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4.w, acc[NS + pl], 0, 0, 0);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+            }
+
+            // ------------------------------------------------------------ epilogue
+            const int ch = chunk * 32 + r;          // output channel of this lane's column
+            const int row0 = rt * 32;
+            if constexpr (EPI == TP_PLAIN) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    const int col = (chunk * NS + j) * 32 + r;
+                    if (col < P.ncols) {
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) {
+                            const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                            if (row < P.rows) P.C[(size_t)row * P.ldc + col] = acc[j][e];
+                        }
+                    }
+                }
+            } else if constexpr (EPI == TP_MSG) {
+                // rows are edges, dst-major, `group` (power of two) slots per destination
+                const int M = P.M;
+                const bool live = ch < M;
+                const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
+                float ms[16], mv0[16], mv1[16], mv2[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group;
+                    const float* g = P.geom + (size_t)(row < P.rows ? row : 0) * 8;
+                    const float s = kC_SILU * tp_silu(acc[0][e] + ba);
+                    const float gg = kC_SIGMOID * tp_sigmoid(acc[1][e] + bg);
+                    const float tt = acc[2][e];
+                    ms[e] = ok ? s : 0.f;
+                    mv0[e] = ok ? gg * (g[0] * tt + acc[NS + 0][e]) : 0.f;
+                    mv1[e] = ok ? gg * (g[1] * tt + acc[NS + 1][e]) : 0.f;
+                    mv2[e] = ok ? gg * (g[2] * tt + acc[NS + 2][e]) : 0.f;
+                    st0 += (double)ms[e];
+                    st1 += (double)ms[e] * ms[e];
+                    st2 += (double)mv0[e] * mv0[e] + (double)mv1[e] * mv1[e] + (double)mv2[e] * mv2[e];
+                }
+                // aggregate the `group` consecutive rows of each destination (all indices
+                // compile-time so the per-row arrays stay in registers)
+                const int G = P.group;
+                auto put = [&](int row, float a0, float a1, float a2, float a3) {
+                    if (live && row < P.rows) {
+                        const size_t o = (size_t)(row / G) * M + ch;
+                        P.out_s[o] = a0;
+                        P.out_v[o] = a1;
+                        P.out_v[P.out_plane + o] = a2;
+                        P.out_v[2 * P.out_plane + o] = a3;
+                    }
+                };
+                if (G <= 4) {
+#pragma unroll
+                    for (int e0 = 0; e0 < 16; e0 += 4) {
+#pragma unroll
+                        for (int s0 = 0; s0 < 4; ++s0) {
+                            if (s0 % G) continue;
+                            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (s0 + u >= 4 || u >= G) continue;
+                                a0 += ms[e0 + s0 + u]; a1 += mv0[e0 + s0 + u];
+                                a2 += mv1[e0 + s0 + u]; a3 += mv2[e0 + s0 + u];
+                            }
+                            put(row0 + s0 + 8 * (e0 >> 2) + 4 * h, a0, a1, a2, a3);
+                        }
+                    }
+                } else {
+                    // 8/16/32-row groups: (h, e&3) covers 8 rows, e>>2 selects the 8-row block
+                    float b0[4], b1[4], b2[4], b3[4];
+#pragma unroll
+                    for (int b8 = 0; b8 < 4; ++b8) {
+                        b0[b8] = ms[4 * b8] + ms[4 * b8 + 1] + ms[4 * b8 + 2] + ms[4 * b8 + 3];
+                        b1[b8] = mv0[4 * b8] + mv0[4 * b8 + 1] + mv0[4 * b8 + 2] + mv0[4 * b8 + 3];
+                        b2[b8] = mv1[4 * b8] + mv1[4 * b8 + 1] + mv1[4 * b8 + 2] + mv1[4 * b8 + 3];
+                        b3[b8] = mv2[4 * b8] + mv2[4 * b8 + 1] + mv2[4 * b8 + 2] + mv2[4 * b8 + 3];
+                        b0[b8] += __shfl_xor(b0[b8], 32); b1[b8] += __shfl_xor(b1[b8], 32);
+                        b2[b8] += __shfl_xor(b2[b8], 32); b3[b8] += __shfl_xor(b3[b8], 32);
+                    }
+                    const int nb = G / 8;
+#pragma unroll
+                    for (int gb = 0; gb < 4; ++gb) {
+                        if (gb % nb) continue;
+                        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+                        for (int b8 = 0; b8 < 4; ++b8) {
+                            if (b8 < gb || b8 >= gb + nb) continue;
+                            a0 += b0[b8]; a1 += b1[b8]; a2 += b2[b8]; a3 += b3[b8];
+                        }
+                        if (h == 0) put(row0 + 8 * gb, a0, a1, a2, a3);
+                    }
+                }
+            } else if constexpr (EPI == TP_GATE_NODE) {
+                // rows are nodes; writes the next TP's inputs [h_s | h_v . na] and h_v planes
+                const int M = P.M;
+                const bool live = ch < M;
+                const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (!live || row >= P.rows) continue;
+                    const float* na = P.geom + (size_t)row * 4;
+                    const float hs = kC_SILU * tp_silu(acc[0][e] + ba);
+                    const float gg = kC_SIGMOID * tp_sigmoid(acc[1][e] + bg);
+                    const float tt = acc[2][e];
+                    const float h0 = gg * (na[1] * tt + acc[NS + 0][e]);
+                    const float h1 = gg * (na[2] * tt + acc[NS + 1][e]);
+                    const float h2 = gg * (na[3] * tt + acc[NS + 2][e]);
+                    P.out_s[(size_t)row * 2 * M + ch] = hs;
+                    P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
+                    P.out_v[(size_t)row * M + ch] = h0;
+                    P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
+                    P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
+                }
+            } else if constexpr (EPI == TP_RESID) {
+                // rows are nodes: x += update (update_layer_2 output), BN partial sums of the new x
+                const int M = P.M;
+                const bool live = ch < M;
+                const float b = live ? P.bias[ch] : 0.f;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (!live || row >= P.rows) continue;
+                    const float* na = P.geom + (size_t)row * 4;
+                    const float tt = acc[1][e];
+                    float* xs = P.out_s + (size_t)row * M + ch;
+                    const float s = *xs + (acc[0][e] + b);
+                    *xs = s;
+                    float* x0 = P.out_v + (size_t)row * M + ch;
+                    float* x1 = x0 + P.out_plane;
+                    float* x2 = x1 + P.out_plane;
+                    const float v0 = *x0 + (na[1] * tt + acc[NS + 0][e]);
+                    const float v1 = *x1 + (na[2] * tt + acc[NS + 1][e]);
+                    const float v2 = *x2 + (na[3] * tt + acc[NS + 2][e]);
+                    *x0 = v0; *x1 = v1; *x2 = v2;
+                    st0 += (double)s;
+                    st1 += (double)s * s;
+                    st2 += (double)v0 * v0 + (double)v1 * v1 + (double)v2 * v2;
+                }
+            }
+            rt = next_rt;
+            if (rt >= row_tiles) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+        }
+    }
+done:
+    if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
+        // reduce the block's waves in LDS: one partial row per block, layout [chunk][block][3][32]
+        __syncthreads();
+        double* red = reinterpret_cast<double*>(lds);   // [3][TP_WAVES][32]
+        st0 += __shfl_xor(st0, 32);
+        st1 += __shfl_xor(st1, 32);
+        st2 += __shfl_xor(st2, 32);
+        if (h == 0) {
+            red[(0 * TP_WAVES + wave) * 32 + r] = st0;
+            red[(1 * TP_WAVES + wave) * 32 + r] = st1;
+            red[(2 * TP_WAVES + wave) * 32 + r] = st2;
+        }
+        __syncthreads();
+        if (t < 96) {
+            const int st = t / 32, c = t % 32;
+            double acc = 0.0;
+            for (int w = 0; w < TP_WAVES; ++w) acc += red[(st * TP_WAVES + w) * 32 + c];
+            P.partial[((size_t)chunk * P.blocks_per_chunk + blk) * 96 + st * 32 + c] = acc;
+        }
+    }
+}
+
+inline int tp_lds_floats(const TpProb& p) {
+    auto pitch = [](int K) { return ((K + 31) & ~31) + 4; };
+    int n = 0;
+    for (int j = 0; j < p.NS; ++j) n += 32 * pitch(p.K[j]);
+    if (p.NV) n += 32 * pitch(p.Kv);
+    return n;
+}
+
+// Grid: `blocks_per_chunk` blocks per 32-channel chunk, chosen to fill the CUs
+// (as many blocks per CU as the LDS footprint allows) without idle waves.
+inline void tp_geometry(TpProb& p, int num_cus = 256) {
+    p.lds_floats = tp_lds_floats(p);
+    const int lds_bytes = p.lds_floats * 4;
+    int per_cu = (160 * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
+    if (per_cu < 1) per_cu = 1;
+    if (per_cu > 2) per_cu = 2;  // 8-wave blocks: at most 16 waves / CU
+    const int row_tiles = (p.rows + 31) / 32;
+    int bpc = (num_cus * per_cu + p.chunks - 1) / p.chunks;
+    const int max_bpc = (row_tiles + TP_WAVES - 1) / TP_WAVES;
+    if (bpc > max_bpc) bpc = max_bpc;
+    if (bpc < 1) bpc = 1;
+    p.blocks_per_chunk = bpc;
+    p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
+}
+
+template <int NS, int NV, int EPI>
+int tp_launch(const TpProb& p, hipStream_t st) {
+    if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
+    const size_t lds = (size_t)p.lds_floats * 4;
+    if (lds > 160 * 1024) {
+        set_error("tp_fused: weight chunk needs %zu bytes of LDS (> 160 KiB)", lds);
+        return NBX_E_UNSUPPORTED;
+    }
+    static bool attr_set = false;  // per instantiation
+    if (!attr_set) {
+        NBX_HIP(hipFuncSetAttribute((const void*)tp_fused_kernel<NS, NV, EPI>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((tp_fused_kernel<NS, NV, EPI>), dim3(p.chunks * p.blocks_per_chunk), dim3(TP_THREADS), lds, st,
+                       p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
+}  // namespace nbx

@@ -214,9 +214,32 @@ class SEGNN(nn.Module):
         P["pp2"] = vec(torch.stack([Ws[:, 0], Ws[:, 1], Wv[:, 0], Wv[:, 1]]))
         return P
 
+    # gate / update TPs whose scalar-row matrix is stored chunk-interleaved on the
+    # device: name -> number of 32-column sub-tiles per 32-channel chunk
+    _INTERLEAVED = {"msg2_s_t": 3, "upd1_s_t": 3, "upd2_s_t": 2, "pp1_s_t": 3}
+    _CHUNK_PADDED = ("msg2_v_t", "upd1_v_t", "upd2_v_t", "pp1_v_t")
+
+    @staticmethod
+    def device_layout(name: str, mat: torch.Tensor, mul: int) -> torch.Tensor:
+        """Layout of include/nbx.h for the fused TP kernels: channels are padded to
+        Mp = 32*ceil(M/32); [parts*M][K] scalar-row matrices become
+        [Mp/16][parts][16][K] (channel c of part j at row (c//16)*parts*16 + 16j + c%16,
+        zero rows for padded channels); vector-row matrices [M][K] are padded to [Mp][K]."""
+        base = name.rsplit(".", 1)[-1]
+        mp = 32 * ((mul + 31) // 32)
+        if base in SEGNN._INTERLEAVED:
+            parts = SEGNN._INTERLEAVED[base]
+            K = mat.shape[1]
+            x = torch.nn.functional.pad(mat.reshape(parts, mul, K), (0, 0, 0, mp - mul))
+            c16 = mp // 16
+            return x.reshape(parts, c16, 16, K).permute(1, 0, 2, 3).reshape(c16 * parts * 16, K).contiguous()
+        if base in SEGNN._CHUNK_PADDED:
+            return torch.nn.functional.pad(mat, (0, 0, 0, mp - mul)).contiguous()
+        return mat
+
     def pack_weights(self, device):
         """Build the nbx_segnn_weights struct (device pointers) from packed_matrices."""
-        P = self.packed_matrices(device)
+        P = {k: self.device_layout(k, v, self.mul) for k, v in self.packed_matrices(device).items()}
         W = _lib.SegnnWeights()
         W.mul, W.num_layers, W.bn_eps, W.bn_momentum = self.mul, self.num_layers, 1e-5, 0.1
         for k in ("emb", "emb_bias", "pp1_s_t", "pp1_v_t", "pp1_bias", "pp2"):

@@ -23,6 +23,10 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py --steps 100 --warmup 10 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o segnn \
                -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o segnn \
+               -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o segnn \
+               -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
   esac
 done
 echo done
