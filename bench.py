@@ -36,20 +36,6 @@ FP32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vec
 SURVEY_GFLOP_PER_STEP = 67.73          # algorithmic work of the reference formulation
 
 
-def useful_gemm_flops(V, E, M, layers):
-    """Useful (non-zero-block) MACs x2 of the dominant GEMM kernel per forward, i.e.
-    the O(3) tensor-product contractions of the factorised formulation
-    (DESIGN.md §Measurement)."""
-    per_layer = (
-        2 * V * M * 6 * M + 2 * 3 * V * M * 6 * M                    # node_pre (message_layer_1 halves)
-        + 2 * E * (2 * M * 2 * M + M * M) + 2 * 3 * E * M * M       # message_layer_2
-        + 2 * V * (4 * M * 2 * M + 2 * M * M) + 2 * 3 * V * 2 * M * M  # update_layer_1
-        + 2 * V * (2 * M * M + M * M) + 2 * 3 * V * M * M           # update_layer_2
-    )
-    pre_pool1 = 2 * V * (2 * M * 2 * M + M * M) + 2 * 3 * V * M * M
-    return layers * per_layer + pre_pool1
-
-
 def initial_states(B, N, seed0):
     from nbody_amd.gravity import GravitySim
     sim = GravitySim(n_balls=N, interaction_strength=2, dt=0.01, softening=0.2, device="cpu")
@@ -130,34 +116,50 @@ def main():
         elapsed = float(t.item())
     finite = bool(torch.isfinite(tp).all().item())
 
-    # live roofline of the dominant kernel (tp_fused_kernel): HIP events around
-    # every GEMM launch of a few forwards on the launch stream
-    V, E, M = B * N, B * N * (N - 1), model.mul
+    # live roofline of the dominant kernel: HIP events around every launch of the
+    # fused tensor-product kernels of a few forwards, on the launch stream, split by kind
+    V, M = B * N, model.mul
     p32 = loc_d.reshape(-1, 3).contiguous()
     v32 = vel_d.reshape(-1, 3).contiguous()
     m32 = mass_d.reshape(-1).contiguous()
     out = torch.empty(V, 6, device=device)
     W = model._weights(device)
     ws = model._workspace(B, N, device)
-    g_ms, g_n, g_fl, tot = _lib.c_f(), _lib.c_i32(), _lib.c_d(), _lib.c_f()
-    reps, gemm_ms, gemm_launches, fwd_ms = 5, 0.0, 0, 0.0
+    kms, kn, kfl, tot = (_lib.c_f * 4)(), (_lib.c_i32 * 4)(), (_lib.c_d * 4)(), _lib.c_f()
+    reps = 5
+    ms_k, n_k, fl_k, fwd_ms = [0.0] * 4, [0] * 4, [0.0] * 4, 0.0
     for _ in range(reps):
         _lib.check(_lib.lib().nbx_segnn_forward_timed(
             W, _lib.dev_ptr(p32), _lib.dev_ptr(v32), _lib.dev_ptr(m32), B, N, _lib.dev_ptr(out), _lib.dev_ptr(ws),
-            ws.numel(), _lib.stream_ptr(device), g_ms, g_n, g_fl, tot), "forward_timed")
-        gemm_ms += g_ms.value
-        gemm_launches += g_n.value
+            ws.numel(), _lib.stream_ptr(device), kms, kn, kfl, tot), "forward_timed")
+        for k in range(4):
+            ms_k[k] += kms[k]
+            n_k[k] += kn[k]
+            fl_k[k] += kfl[k]
         fwd_ms += tot.value
-    useful = useful_gemm_flops(V, E, M, LAYERS)
-    avg_launch_s = gemm_ms / gemm_launches / 1e3
-    useful_per_launch = useful / (gemm_launches / reps)
-    achieved_tflops = useful_per_launch / avg_launch_s / 1e12
+    # rocprofv3 names of the four fused TP launch kinds (csrc/segnn.hip::forward_impl)
+    names = ["void nbx::tp16_kernel<3, 0, 0, 2>(nbx::TpProb)", "void nbx::tp_fused_kernel<3, 1, 1>(nbx::TpProb)",
+             "void nbx::tp16_kernel<3, 1, 2, 1>(nbx::TpProb)", "void nbx::tp16_kernel<2, 1, 3, 2>(nbx::TpProb)"]
+    roles = ["message_layer_1 node halves", "message_layer_2 + gate + aggregation + BN sums",
+             "update_layer_1 + gate (pre_pool1 uses CG=2)", "update_layer_2 + residual + BN sums"]
+    per_kind = {}
+    for k in range(4):
+        if n_k[k]:
+            avg_s = ms_k[k] / n_k[k] / 1e3
+            fl = fl_k[k] / n_k[k]
+            per_kind[names[k]] = {"role": roles[k], "avg_launch_us": round(avg_s * 1e6, 3), "gflop_per_launch": round(fl / 1e9, 4),
+                                  "tflops": round(fl / avg_s / 1e12, 3), "share_of_forward": round(ms_k[k] / fwd_ms, 3)}
+    dom = max(range(4), key=lambda k: ms_k[k])
+    dom_avg_s = ms_k[dom] / n_k[dom] / 1e3
+    dom_flops = fl_k[dom] / n_k[dom]
+    achieved_tflops = dom_flops / dom_avg_s / 1e12
+    fused_share = sum(ms_k) / fwd_ms
 
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_gemm_f32.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_tp_kernels.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            traffic = json.load(f)["kernels"].get(names[dom], {}).get("hbm_bytes_per_launch")
 
     steps_per_s_rank = a.steps / elapsed
     value = steps_per_s_rank * world
@@ -179,13 +181,11 @@ def main():
                    "bn_mode": "batch statistics per rank (reference train-mode rollout)"},
         "trajectory_steps_per_s": round(value * B, 1),
         "survey_formulation_tflops": round(value * SURVEY_GFLOP_PER_STEP / 1e3, 3),
-        "roofline": {"bound": "mfma", "kernel": "tp_fused_kernel (v_mfma_f32_32x32x2_f32, weight-stationary)",
-                     "achieved": round(achieved_tflops, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": round(achieved_tflops, 3),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "avg_launch_us": round(avg_launch_s * 1e6, 3),
-                     "useful_gflop_per_launch": round(useful_per_launch / 1e9, 4),
-                     "executed_gflop_per_launch": round(g_fl.value / g_n.value / 1e9, 4),
-                     "gemm_share_of_forward": round(gemm_ms / fwd_ms, 3)},
+                     "avg_launch_us": round(dom_avg_s * 1e6, 3), "gflop_per_launch": round(dom_flops / 1e9, 4),
+                     "fused_tp_share_of_forward": round(fused_share, 3), "per_kind": per_kind},
         "finite": finite,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

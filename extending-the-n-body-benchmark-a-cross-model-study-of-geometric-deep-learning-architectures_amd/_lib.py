@@ -46,8 +46,7 @@ _SIGNATURES = {
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),
     "nbx_segnn_forward_timed": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
-                                               c_p, c_sz, c_p, ctypes.POINTER(c_f), ctypes.POINTER(c_i32),
-                                               ctypes.POINTER(c_d), ctypes.POINTER(c_f)]),
+                                               c_p, c_sz, c_p, c_f * 4, c_i32 * 4, c_d * 4, ctypes.POINTER(c_f)]),
     "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
                                          c_p, c_p, c_p, c_sz, c_p]),
 }

@@ -407,10 +407,12 @@ dim3 ew_grid(int64_t rows, int M) {
 
 // Optional per-launch timing of the dominant kernel (nbx_segnn_forward_timed):
 // an event pair around every tp_fused launch on the launch stream.
+// Kinds: 0 = TP_PLAIN (node_pre), 1 = TP_MSG, 2 = TP_GATE_NODE, 3 = TP_RESID.
 struct KernelTiming {
     std::vector<hipEvent_t> ev;
-    double flops = 0.0;
-    int launches = 0;
+    std::vector<int> kind;
+    double flops[4] = {0, 0, 0, 0};
+    int launches[4] = {0, 0, 0, 0};
 };
 
 template <int NS, int NV, int EPI>
@@ -431,8 +433,9 @@ int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
     k += NV ? 3.0 * p.Kv : 0.0;
-    tm->flops += 2.0 * p.rows * 32.0 * p.chunks * k;  // executed MACs x 2 (incl. channel padding)
-    tm->launches += 1;
+    tm->kind.push_back(EPI);
+    tm->flops[EPI] += 2.0 * p.rows * 32.0 * p.chunks * k;  // executed MACs x 2 (incl. channel padding)
+    tm->launches[EPI] += 1;
     return NBX_OK;
 }
 
@@ -450,8 +453,9 @@ int run_tp16(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
     k += NV ? 3.0 * p.Kv : 0.0;
-    tm->flops += 2.0 * p.rows * 16.0 * p.chunks * k;
-    tm->launches += 1;
+    tm->kind.push_back(EPI);
+    tm->flops[EPI] += 2.0 * p.rows * 16.0 * p.chunks * k;
+    tm->launches[EPI] += 1;
     return NBX_OK;
 }
 
@@ -622,8 +626,8 @@ extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* 
 
 extern "C" int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* pos, const float* vel,
                                        const float* mass, int64_t B, int64_t N, float* out, void* workspace,
-                                       size_t workspace_bytes, void* stream, float* gemm_ms, int32_t* gemm_launches,
-                                       double* gemm_flops, float* total_ms) {
+                                       size_t workspace_bytes, void* stream, float* kind_ms, int32_t* kind_launches,
+                                       double* kind_flops, float* total_ms) {
     Workspace ws;
     if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     hipStream_t st = (hipStream_t)stream;
@@ -635,11 +639,11 @@ extern "C" int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* 
     int rc = forward_impl(w, pos, vel, mass, B, N, out, ws, st, &tm);
     NBX_HIP(hipEventRecord(t1, st));
     NBX_HIP(hipEventSynchronize(t1));
-    float acc = 0.f;
+    float acc[4] = {0, 0, 0, 0};
     for (size_t i = 0; i + 1 < tm.ev.size(); i += 2) {
         float ms = 0.f;
         NBX_HIP(hipEventElapsedTime(&ms, tm.ev[i], tm.ev[i + 1]));
-        acc += ms;
+        acc[tm.kind[i / 2]] += ms;
     }
     float tot = 0.f;
     NBX_HIP(hipEventElapsedTime(&tot, t0, t1));
@@ -647,9 +651,11 @@ extern "C" int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* 
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
     if (rc) return rc;
-    if (gemm_ms) *gemm_ms = acc;
-    if (gemm_launches) *gemm_launches = tm.launches;
-    if (gemm_flops) *gemm_flops = tm.flops;
+    for (int k = 0; k < 4; ++k) {
+        if (kind_ms) kind_ms[k] = acc[k];
+        if (kind_launches) kind_launches[k] = tm.launches[k];
+        if (kind_flops) kind_flops[k] = tm.flops[k];
+    }
     if (total_ms) *total_ms = tot;
     return NBX_OK;
 }

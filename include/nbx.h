@@ -133,13 +133,14 @@ int nbx_segnn_forward(const nbx_segnn_weights* w, const float* pos, const float*
                       void* stream);
 
 /* Diagnostic variant of nbx_segnn_forward used by bench.py: records a HIP event
- * pair around every launch of the dominant GEMM kernel on `stream`, synchronises
- * at the end (so it is NOT graph-capturable) and reports the summed GEMM time,
- * the number of GEMM launches, their executed FLOPs (2*M*N*K summed) and the
- * whole forward's time. */
+ * pair around every launch of the fused tensor-product kernels on `stream`,
+ * synchronises at the end (so it is NOT graph-capturable) and reports, per
+ * kernel kind (0 node_pre, 1 edge message, 2 gated node TP, 3 residual node TP),
+ * the summed time (ms), the launch count and the executed FLOPs (2*MACs), plus
+ * the whole forward's time.  Arrays have 4 entries. */
 int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
                             int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
-                            void* stream, float* gemm_ms, int32_t* gemm_launches, double* gemm_flops, float* total_ms);
+                            void* stream, float* kind_ms, int32_t* kind_launches, double* kind_flops, float* total_ms);
 
 /* Device-resident self-feed rollout (helper_scripts/infer_self_feed.py:99-194,
  * target "pos_dt+vel", force zeroed, mass constant): starting from pos/vel

@@ -26,7 +26,8 @@ for s in $STEPS; do
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o segnn \
                -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o segnn \
-               -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+               -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
+           python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_tp_kernels.json ;;
   esac
 done
 echo done
