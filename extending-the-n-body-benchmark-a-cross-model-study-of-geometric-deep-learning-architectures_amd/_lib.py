@@ -34,6 +34,25 @@ class SegnnWeights(ctypes.Structure):
                 ("layers", SegnnLayer * MAX_LAYERS)]
 
 
+EGNN_MAX_LAYERS = 64
+
+
+class EgnnLayer(ctypes.Structure):
+    _fields_ = [("e0_t", c_p), ("e0_b", c_p), ("e1_t", c_p), ("e1_b", c_p), ("c0_t", c_p), ("c0_b", c_p),
+                ("c1_w", c_p), ("v0_t", c_p), ("v0_b", c_p), ("v1_w", c_p), ("v1_b", c_f), ("n0_t", c_p),
+                ("n0_b", c_p), ("n1_t", c_p), ("n1_b", c_p)]
+
+
+class EgnnHead(ctypes.Structure):
+    _fields_ = [(n, c_p) for n in ("w0_t", "b0", "w1_t", "b1", "w2_t", "b2")]
+
+
+class EgnnWeights(ctypes.Structure):
+    _fields_ = [(n, c_i32) for n in ("hidden", "num_layers", "num_heads", "recurrent", "norm_diff", "use_tanh")] + [
+        ("coords_weight", c_f), ("emb_t", c_p), ("emb_b", c_p), ("heads", EgnnHead * 2),
+        ("layers", EgnnLayer * EGNN_MAX_LAYERS)]
+
+
 _SIGNATURES = {
     "nbx_abi_version": (ctypes.c_int, []),
     "nbx_last_error": (ctypes.c_char_p, []),
@@ -47,6 +66,11 @@ _SIGNATURES = {
                                          c_p, c_sz, c_p]),
     "nbx_segnn_forward_timed": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                                c_p, c_sz, c_p, c_f * 4, c_i32 * 4, c_d * 4, ctypes.POINTER(c_f)]),
+    "nbx_egnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
+    "nbx_egnn_forward": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_sz,
+                                        c_p]),
+    "nbx_egnn_rollout": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p,
+                                        c_p, c_sz, c_p]),
     "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
                                          c_p, c_p, c_p, c_sz, c_p]),
 }

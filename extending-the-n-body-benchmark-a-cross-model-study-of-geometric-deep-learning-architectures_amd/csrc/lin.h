@@ -1,0 +1,236 @@
+// Generic weight-stationary fp32 linear layer on CDNA4 matrix cores:
+//   Y[row, n] = epilogue( sum_k A[row, k] * Wt[n, k] )
+// where A is the concatenation along K of up to 3 segments, each optionally
+// gathered through a per-row index (EGNN edge inputs [h_row | h_col | radial, attrs]).
+//
+// A block owns NT x 32 output columns: that slice of Wt is staged in LDS once
+// (zero-padded, pitch = 32k + 4 floats) and its 8 waves stream 32-row tiles of A
+// from global memory (3-deep register prefetch, no barrier in the main loop)
+// through v_mfma_f32_32x32x2_f32.  Epilogues: bias, activation (SiLU / exact
+// GELU / tanh), optional residual "Y = R + s (.) act(...)" and optional
+// accumulate of a per-row dot product with a vector (EGNN's 128 -> 1 heads).
+// Fragment maps and the in-chunk K permutation are those of tp_fused.h.
+#pragma once
+#include "nbx_internal.h"
+
+namespace nbx {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+enum LinAct : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
+
+struct LinSeg {
+    const float* ptr;   // segment base
+    const int64_t* idx; // optional row gather index (row -> source row), else identity
+    int ld;             // row stride (floats)
+    int K;              // padded width (multiple of 32) occupied in the concatenated K
+    int Kvalid;         // real columns (multiple of 4); the rest reads as zero
+};
+
+struct LinProb {
+    LinSeg seg[3];
+    int nseg;
+    int rows, N, Ktot;  // Ktot = sum of seg[].K
+    const float* Wt;    // [N][ldw]  (columns of the concatenated K)
+    int ldw;
+    const float* bias;  // [N] or null
+    float* Y;           // [rows][ldy] (may be null when only the row dot is wanted)
+    int ldy;
+    const float* resid; // optional residual R [rows][ldr] (may alias Y)
+    int ldr;
+    const float* scale; // optional per-column scale s (layer_scale)
+    const float* dotw;  // optional: rowdot[row] += sum_n act(...)[n] * dotw[n]
+    float* rowdot;      // [rows] accumulated with atomics across column blocks (zero it first)
+    int blocks_per_chunk;
+    int chunks;         // ceil(N / (NT*32))
+};
+
+constexpr int LIN_WAVES = 8, LIN_THREADS = 64 * LIN_WAVES;
+
+__device__ inline float lin_act(float x, int act) {
+    switch (act) {
+        case ACT_SILU: return x / (1.0f + __expf(-x));
+        case ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+        case ACT_TANH: return tanhf(x);
+        default: return x;
+    }
+}
+
+template <int NT, int ACT>
+__global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int chunk = blockIdx.x / P.blocks_per_chunk;
+    const int blk = blockIdx.x - chunk * P.blocks_per_chunk;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+    const int pitch = ((P.Ktot + 31) & ~31) + 4;
+    const int n0 = chunk * NT * 32;
+
+    // ---- stage Wt[n0 : n0 + NT*32, :] in LDS
+    {
+        const int q4 = pitch / 4;
+        for (int i = t; i < NT * 32 * q4; i += LIN_THREADS) {
+            const int row = i / q4, kq = (i - row * q4) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n0 + row < P.N && kq < P.Ktot)
+                v = *reinterpret_cast<const float4*>(P.Wt + (size_t)(n0 + row) * P.ldw + kq);
+            *reinterpret_cast<float4*>(&lds[row * pitch + kq]) = v;
+        }
+    }
+    __syncthreads();
+
+    const int n_chunks = P.Ktot >> 5;
+    const int row_tiles = (P.rows + 31) >> 5;
+    const int wstride = P.blocks_per_chunk * LIN_WAVES;
+
+    // A chunk loader: 32-deep K chunk i of row tile rt -> 16 floats per lane
+    auto load_a = [&](int rt, int i, float4 (&a)[4]) {
+        const int row = rt * 32 + r;
+        int k0 = i * 32, s = 0;
+        while (s < P.nseg - 1 && k0 >= P.seg[s].K) {
+            k0 -= P.seg[s].K;
+            ++s;
+        }
+        const LinSeg& S = P.seg[s];
+        const int kk = k0 + 16 * h;
+        bool ok = row < P.rows;
+        int64_t src = row;
+        if (ok && S.idx) src = S.idx[row];
+        const float* p = S.ptr + (size_t)src * S.ld + kk;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            a[q] = (ok && kk + 4 * q < S.Kvalid) ? *reinterpret_cast<const float4*>(p + 4 * q)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+
+    int rt = blk * LIN_WAVES + wave;
+    if (rt >= row_tiles) return;
+    float4 cur[4], nxt[4], nx2[4];
+    int lrt = rt, li = 0;
+    auto advance = [&]() {
+        if (++li >= n_chunks) {
+            li = 0;
+            lrt += wstride;
+        }
+    };
+    load_a(lrt, li, cur);
+    advance();
+    if (lrt < row_tiles) load_a(lrt, li, nxt);
+    advance();
+    while (true) {
+        floatx16 acc[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+        for (int i = 0; i < n_chunks; ++i) {
+            if (lrt < row_tiles) load_a(lrt, li, nx2);
+            advance();
+            const int k0 = i * 32;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float4 b4[NT];
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    b4[j] = *reinterpret_cast<const float4*>(&lds[(32 * j + r) * pitch + k0 + 16 * h + 4 * q]);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4[j].x, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4[j].y, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4[j].z, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4[j].w, acc[j], 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                cur[q] = nxt[q];
+                nxt[q] = nx2[q];
+            }
+        }
+        // ---- epilogue: col = n0 + 32 j + r; row = rt*32 + (e&3) + 8(e>>2) + 4h
+        float dot[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dot[e] = 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int col = n0 + 32 * j + r;
+            const bool live = col < P.N;
+            const float b = (live && P.bias) ? P.bias[col] : 0.f;
+            const float sc = (live && P.scale) ? P.scale[col] : 1.f;
+            const float dw = (live && P.dotw) ? P.dotw[col] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                float y = lin_act(acc[j][e] + b, ACT);
+                dot[e] += y * dw;
+                if (live && row < P.rows && P.Y) {
+                    if (P.resid) y = P.resid[(size_t)row * P.ldr + col] + sc * y;
+                    P.Y[(size_t)row * P.ldy + col] = y;
+                }
+            }
+        }
+        if (P.dotw) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                float v = dot[e];
+                for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);  // sum over the 32 columns
+                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (r == 0 && row < P.rows) atomicAdd(&P.rowdot[row], v);
+            }
+        }
+        rt += wstride;
+        if (rt >= row_tiles) break;
+    }
+}
+
+template <int NT, int ACT>
+int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
+    if (p.rows <= 0 || p.N <= 0) return NBX_OK;
+    if (p.Ktot % 32) {
+        set_error("lin: Ktot must be a multiple of 32 (got %d)", p.Ktot);
+        return NBX_E_INVAL;
+    }
+    const size_t lds = (size_t)NT * 32 * ((((p.Ktot + 31) & ~31) + 4)) * 4;
+    if (lds > 160 * 1024) {
+        set_error("lin: weight slice needs %zu bytes of LDS", lds);
+        return NBX_E_UNSUPPORTED;
+    }
+    p.chunks = (p.N + NT * 32 - 1) / (NT * 32);
+    int per_cu = (int)((160 * 1024) / lds);
+    if (per_cu > 2) per_cu = 2;
+    if (per_cu < 1) per_cu = 1;
+    const int row_tiles = (p.rows + 31) / 32;
+    int bpc = (num_cus * per_cu + p.chunks - 1) / p.chunks;
+    const int max_bpc = (row_tiles + LIN_WAVES - 1) / LIN_WAVES;
+    if (bpc > max_bpc) bpc = max_bpc;
+    if (bpc < 1) bpc = 1;
+    p.blocks_per_chunk = bpc;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((lin_kernel<NT, ACT>), dim3(p.chunks * bpc), dim3(LIN_THREADS), lds, st, p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
+inline LinProb lin_dense(const float* A, int lda, int K, int rows, const float* Wt, int ldw, int N, const float* bias,
+                         float* Y, int ldy) {
+    LinProb p;
+    memset(&p, 0, sizeof(p));
+    p.seg[0] = LinSeg{A, nullptr, lda, (K + 31) & ~31, K};
+    p.nseg = 1;
+    p.rows = rows;
+    p.N = N;
+    p.Ktot = (K + 31) & ~31;
+    p.Wt = Wt;
+    p.ldw = ldw;
+    p.bias = bias;
+    p.Y = Y;
+    p.ldy = ldy;
+    return p;
+}
+
+}  // namespace nbx

@@ -1,0 +1,233 @@
+"""EGNNMultiChannel — drop-in for models/egnn_mc/egnn_mc.py with a HIP forward.
+
+Module tree, parameter names/shapes and initialisation order follow the
+reference (egnn_mc.py:45-306), so ``torch.manual_seed(s)`` gives the same
+weights and reference checkpoints load.  ``forward(graph)`` takes the rollout /
+dataloader graph (pos, vel, mass, fully-connected edge_index) and runs the
+preprocessing of dataloaders/egnn_mc_n_body_dataloader.py:8-56 plus the model
+in libnbx (csrc/egnn.hip); ``rollout`` runs the self-feed loop device-resident.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+from torch import nn
+
+from . import _lib
+
+__all__ = ["EGNNMultiChannel"]
+
+
+def _make_activation(name: str):
+    name = name.lower()
+    if name == "silu":
+        return nn.SiLU
+    if name == "relu":
+        return nn.ReLU
+    if name in {"leaky_relu", "lrelu"}:
+        return lambda: nn.LeakyReLU(negative_slope=0.2)
+    raise ValueError(f"Unsupported activation '{name}'.")
+
+
+class _EGNNMessageBlock(nn.Module):
+    """egnn_mc.py:45-130 (parameter container; the arithmetic runs in csrc/egnn.hip)."""
+
+    def __init__(self, node_input_dim, node_output_dim, hidden_edge_dim, hidden_node_dim, hidden_coord_dim, *,
+                 edge_attr_dim=0, act_factory=nn.SiLU, coords_weight=1.0, recurrent=True, attention=False,
+                 norm_diff=False, tanh=False, num_vectors_in=1, num_vectors_out=1):
+        super().__init__()
+        self.coords_weight, self.recurrent, self.attention = coords_weight, recurrent, attention
+        self.norm_diff, self.tanh = norm_diff, tanh
+        self.num_vectors_in, self.num_vectors_out = num_vectors_in, num_vectors_out
+        edge_input_dim = node_input_dim * 2 + num_vectors_in + edge_attr_dim
+        self.edge_mlp = nn.Sequential(nn.Linear(edge_input_dim, hidden_edge_dim), act_factory(),
+                                      nn.Linear(hidden_edge_dim, hidden_edge_dim), act_factory())
+        self.node_mlp = nn.Sequential(nn.Linear(hidden_edge_dim + node_input_dim, hidden_node_dim), act_factory(),
+                                      nn.Linear(hidden_node_dim, node_output_dim))
+        coord_layers = [nn.Linear(hidden_edge_dim, hidden_coord_dim), act_factory(),
+                        nn.Linear(hidden_coord_dim, num_vectors_in * num_vectors_out, bias=False)]
+        nn.init.xavier_uniform_(coord_layers[-1].weight, gain=0.001)
+        if tanh:
+            coord_layers.append(nn.Tanh())
+        self.coord_mlp = nn.Sequential(*coord_layers)
+        self.coord_mlp_vel = nn.Sequential(nn.Linear(node_input_dim, hidden_coord_dim), act_factory(),
+                                           nn.Linear(hidden_coord_dim, num_vectors_in * num_vectors_out))
+        if attention:
+            self.att_mlp = nn.Sequential(nn.Linear(hidden_edge_dim, 1), nn.Sigmoid())
+
+
+class _VectorHead(nn.Module):
+    def __init__(self, input_dim, hidden_dim, act_factory):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(input_dim, hidden_dim), act_factory(), nn.Linear(hidden_dim, hidden_dim),
+                                 act_factory(), nn.Linear(hidden_dim, 3))
+
+
+class EGNNMultiChannel(nn.Module):
+    """EGNN variant with learnable vector heads for multiple targets (egnn_mc.py:211-306)."""
+
+    def __init__(self, *, node_input_dim: int = 2, edge_attr_dim: int = 3, hidden_node_dim: int = 128,
+                 hidden_edge_dim: int = 128, hidden_coord_dim: int = 128, num_layers: int = 4,
+                 target_names: Sequence[str] | None = None, activation: str = "silu", coords_weight: float = 1.0,
+                 recurrent: bool = True, norm_diff: bool = False, tanh: bool = False, device="cpu"):
+        super().__init__()
+        if target_names is None or len(target_names) == 0:
+            raise ValueError("EGNNMultiChannel requires at least one target.")
+        self.device = torch.device(device)
+        self.target_names = tuple(target_names)
+        self.hidden_node_dim, self.num_layers = hidden_node_dim, num_layers
+        self.activation, self.coords_weight, self.recurrent = activation, coords_weight, recurrent
+        self.norm_diff, self.use_tanh = norm_diff, tanh
+        act_factory = _make_activation(activation)
+        self.embedding = nn.Linear(node_input_dim, hidden_node_dim)
+        self.layers = nn.ModuleList([
+            _EGNNMessageBlock(hidden_node_dim, hidden_node_dim, hidden_edge_dim, hidden_node_dim, hidden_coord_dim,
+                              edge_attr_dim=edge_attr_dim, act_factory=act_factory, coords_weight=coords_weight,
+                              recurrent=recurrent, attention=False, norm_diff=norm_diff, tanh=tanh)
+            for _ in range(num_layers)])
+        head_input_dim = hidden_node_dim + 6
+        self.heads = nn.ModuleList([_VectorHead(head_input_dim, hidden_node_dim, act_factory)
+                                    for _ in self.target_names])
+        native = (activation == "silu" and node_input_dim == 2 and edge_attr_dim == 4
+                  and hidden_node_dim == hidden_edge_dim == hidden_coord_dim and hidden_node_dim % 4 == 0
+                  and hidden_node_dim <= 128 and len(self.target_names) <= 2)
+        self._native_reason = None if native else (
+            "native EGNN-MC needs SiLU, node_input_dim 2, edge_attr_dim 4, equal hidden dims (<=128, %4), <=2 heads")
+        self._packed = None
+        self._ws = None
+        self.to(self.device)
+
+    def get_serializable_attributes(self):
+        return {"hidden_node_dim": self.hidden_node_dim, "num_layers": self.num_layers,
+                "target_names": list(self.target_names), "num_params": sum(p.numel() for p in self.parameters())}
+
+    def get_model_size(self):
+        return self.hidden_node_dim
+
+    # ------------------------------------------------------------ packing
+    def _version(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def packed_matrices(self, device, dtype=torch.float32):
+        """nn.Linear weights [out][in] with each input segment zero-padded to a
+        multiple of 32 columns (include/nbx.h, EGNN-MC section)."""
+        H = self.hidden_node_dim
+        kp = (H + 31) // 32 * 32
+        f = dict(device=device, dtype=dtype)
+
+        def pad_cols(w, segs):
+            """segs: list of (width, padded width) covering w's columns in order."""
+            out, c = [], 0
+            for width, padded in segs:
+                part = w[:, c:c + width].to(**f)
+                out.append(torch.nn.functional.pad(part, (0, padded - width)))
+                c += width
+            return torch.cat(out, 1).contiguous()
+
+        def vec(t):
+            return t.detach().to(**f).contiguous()
+
+        P = {"emb_t": pad_cols(self.embedding.weight.detach(), [(2, 32)]), "emb_b": vec(self.embedding.bias)}
+        for i, L in enumerate(self.layers):
+            p = f"layers.{i}."
+            P[p + "e0_t"] = pad_cols(L.edge_mlp[0].weight.detach(), [(H, kp), (H, kp), (5, 32)])
+            P[p + "e0_b"] = vec(L.edge_mlp[0].bias)
+            P[p + "e1_t"] = pad_cols(L.edge_mlp[2].weight.detach(), [(H, kp)])
+            P[p + "e1_b"] = vec(L.edge_mlp[2].bias)
+            P[p + "c0_t"] = pad_cols(L.coord_mlp[0].weight.detach(), [(H, kp)])
+            P[p + "c0_b"] = vec(L.coord_mlp[0].bias)
+            P[p + "c1_w"] = vec(L.coord_mlp[2].weight.reshape(-1))
+            P[p + "v0_t"] = pad_cols(L.coord_mlp_vel[0].weight.detach(), [(H, kp)])
+            P[p + "v0_b"] = vec(L.coord_mlp_vel[0].bias)
+            P[p + "v1_w"] = vec(L.coord_mlp_vel[2].weight.reshape(-1))
+            P[p + "v1_b"] = vec(L.coord_mlp_vel[2].bias)
+            P[p + "n0_t"] = pad_cols(L.node_mlp[0].weight.detach(), [(H, kp), (H, kp)])
+            P[p + "n0_b"] = vec(L.node_mlp[0].bias)
+            P[p + "n1_t"] = pad_cols(L.node_mlp[2].weight.detach(), [(H, kp)])
+            P[p + "n1_b"] = vec(L.node_mlp[2].bias)
+        for t, head in enumerate(self.heads):
+            p = f"heads.{t}."
+            P[p + "w0_t"] = pad_cols(head.net[0].weight.detach(), [(H, kp), (6, 32)])
+            P[p + "b0"] = vec(head.net[0].bias)
+            P[p + "w1_t"] = pad_cols(head.net[2].weight.detach(), [(H, kp)])
+            P[p + "b1"] = vec(head.net[2].bias)
+            P[p + "w2_t"] = pad_cols(head.net[4].weight.detach(), [(H, kp)])
+            P[p + "b2"] = vec(head.net[4].bias)
+        return P
+
+    def pack_weights(self, device):
+        P = self.packed_matrices(device)
+        W = _lib.EgnnWeights()
+        W.hidden, W.num_layers, W.num_heads = self.hidden_node_dim, self.num_layers, len(self.heads)
+        W.recurrent, W.norm_diff, W.use_tanh = int(self.recurrent), int(self.norm_diff), int(self.use_tanh)
+        W.coords_weight = float(self.coords_weight)
+        W.emb_t, W.emb_b = P["emb_t"].data_ptr(), P["emb_b"].data_ptr()
+        for i in range(self.num_layers):
+            L = W.layers[i]
+            for name, _ in L._fields_:
+                if name == "v1_b":
+                    L.v1_b = float(P[f"layers.{i}.v1_b"].item())
+                else:
+                    setattr(L, name, P[f"layers.{i}.{name}"].data_ptr())
+        for t in range(len(self.heads)):
+            for name, _ in W.heads[t]._fields_:
+                setattr(W.heads[t], name, P[f"heads.{t}.{name}"].data_ptr())
+        self._packed = (self._version(), W, P)
+        return W
+
+    def _weights(self, device):
+        if self._native_reason:
+            raise NotImplementedError(self._native_reason)
+        if self._packed is None or self._packed[0] != self._version():
+            self.pack_weights(device)
+        return self._packed[1]
+
+    def _workspace(self, B, N, device):
+        n = _lib.c_sz()
+        _lib.check(_lib.lib().nbx_egnn_workspace_bytes(B, N, self.hidden_node_dim, n), "egnn workspace")
+        if self._ws is None or self._ws.numel() < n.value or self._ws.device != device:
+            self._ws = torch.empty(n.value, dtype=torch.uint8, device=device)
+        return self._ws
+
+    # ------------------------------------------------------------ forward
+    def forward(self, graph):
+        pos = graph.pos
+        device = pos.device
+        V = pos.shape[0]
+        N = getattr(graph, "nbx_system_size", None)
+        if N is None:
+            from .segnn import SEGNN
+            B, N = SEGNN.infer_system_size(V, graph.edge_index.shape[1])
+            from .graph import fc_edge_index
+            if not torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device)):
+                raise NotImplementedError("native EGNN-MC needs the fully-connected edge_index")
+        else:
+            N = int(N)
+            B = V // N
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
+        mass = getattr(graph, "mass", None)
+        m = f(mass.reshape(-1)) if mass is not None else torch.ones(V, device=device)
+        p, v = f(pos), f(graph.vel)
+        out = torch.empty(V, 3 * len(self.heads), device=device, dtype=torch.float32)
+        W = self._weights(device)
+        ws = self._workspace(B, N, device)
+        _lib.check(_lib.lib().nbx_egnn_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                               _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
+                                               _lib.stream_ptr(device)), "nbx_egnn_forward")
+        return out.to(pos.dtype)
+
+    @torch.no_grad()
+    def rollout(self, loc, vel, mass, num_frames: int):
+        device = loc.device
+        B, N, _ = loc.shape
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
+        p, v, m = f(loc), f(vel), f(mass.reshape(B * N))
+        tp = torch.empty(B, num_frames, N, 3, device=device, dtype=torch.float32)
+        tv = torch.empty_like(tp)
+        W = self._weights(device)
+        ws = self._workspace(B, N, device)
+        _lib.check(_lib.lib().nbx_egnn_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                               num_frames, _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
+                                               ws.numel(), _lib.stream_ptr(device)), "nbx_egnn_rollout")
+        return tp, tv

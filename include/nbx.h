@@ -151,6 +151,64 @@ int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* vel, const 
                       int64_t batch_size, int64_t num_nodes, int64_t num_frames,
                       float* traj_pos, float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
 
+
+/* ------------------------------------------------------------------------
+ * EGNN-MC (models/egnn_mc/egnn_mc.py:45-295 with the preprocessing of
+ * dataloaders/egnn_mc_n_body_dataloader.py:8-56) — fp32.
+ *
+ * Native scope: SiLU activation, num_vectors_in = num_vectors_out = 1, attention
+ * off, hidden_node_dim = hidden_edge_dim = hidden_coord_dim = hidden <= 128,
+ * node_input_dim 2, edge_attr_dim 4, fully-connected systems.  Linear weights
+ * are stored as W [out][K] (nn.Linear layout) with K zero-padded per input
+ * segment to a multiple of 32; `Kp = ceil32(hidden)`:
+ *   e0_t [hidden][2 Kp + 32]  (h_row | h_col | radial, edge_attr[4], 0...)
+ *   n0_t [hidden][2 Kp]       (h | mean edge features)
+ *   w0_t [hidden][Kp + 32]    (h | coord - pos, vel, 0...)
+ *   emb_t [hidden][32]        (|vel|, mass, 0...)
+ *   other *_t [out][Kp]; c1_w / v1_w [hidden] (the 128 -> 1 linears).
+ */
+#define NBX_EGNN_MAX_LAYERS 64
+
+typedef struct nbx_egnn_layer {
+    const float* e0_t; const float* e0_b;  /* edge_mlp.0 */
+    const float* e1_t; const float* e1_b;  /* edge_mlp.2 */
+    const float* c0_t; const float* c0_b;  /* coord_mlp.0 */
+    const float* c1_w;                     /* coord_mlp.2 (no bias) */
+    const float* v0_t; const float* v0_b;  /* coord_mlp_vel.0 */
+    const float* v1_w; float v1_b;         /* coord_mlp_vel.2 */
+    const float* n0_t; const float* n0_b;  /* node_mlp.0 */
+    const float* n1_t; const float* n1_b;  /* node_mlp.2 */
+} nbx_egnn_layer;
+
+typedef struct nbx_egnn_head {
+    const float* w0_t; const float* b0;   /* net.0 */
+    const float* w1_t; const float* b1;   /* net.2 */
+    const float* w2_t; const float* b2;   /* net.4 (-> 3) */
+} nbx_egnn_head;
+
+typedef struct nbx_egnn_weights {
+    int32_t hidden, num_layers, num_heads, recurrent, norm_diff, use_tanh;
+    float coords_weight;
+    const float* emb_t; const float* emb_b;
+    nbx_egnn_head heads[2];
+    nbx_egnn_layer layers[NBX_EGNN_MAX_LAYERS];
+} nbx_egnn_weights;
+
+int nbx_egnn_workspace_bytes(int64_t batch_size, int64_t num_nodes, int32_t hidden, size_t* bytes);
+
+/* preprocess_batch + EGNNMultiChannel.forward: pos/vel [B*N,3], mass [B*N] ->
+ * out [B*N, 3*num_heads] (heads in target order, e.g. pos_dt | vel). */
+int nbx_egnn_forward(const nbx_egnn_weights* w, const float* pos, const float* vel, const float* mass,
+                     int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+/* Device-resident self-feed rollout with the EGNN-MC branch of
+ * infer_self_feed.py:161-194 (two heads: pos_dt, vel); same contract as
+ * nbx_segnn_rollout. */
+int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
+                     int64_t num_nodes, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                     size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

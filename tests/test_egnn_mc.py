@@ -1,0 +1,130 @@
+"""EGNN-MC: host module vs reference (init, state_dict), packed-operand emulation
+on CPU, and the HIP path vs the reference golden vectors on the GPU.
+Tolerance for the fp32 HIP path: max |gpu - ref| <= 1e-4 * max|ref| + 1e-6 per
+forward; rollouts with the horizon-scaled budget of test_gpu_segnn."""
+import numpy as np
+import pytest
+import torch
+
+import nbody_amd.egnn_mc as E
+import nbody_amd.graph as G
+from oracle import egnn_mc as oe
+from oracle.graph import fc_edge_index
+
+
+def make(hidden=32, layers=2, dtype=torch.float64):
+    torch.manual_seed(0)
+    return E.EGNNMultiChannel(node_input_dim=2, edge_attr_dim=4, hidden_node_dim=hidden, hidden_edge_dim=hidden,
+                              hidden_coord_dim=hidden, num_layers=layers, target_names=("pos_dt", "vel"),
+                              activation="silu", coords_weight=1.0, recurrent=True, norm_diff=True,
+                              tanh=True).to(dtype)
+
+
+def test_init_and_state_dict_match_reference(golden):
+    g = golden("egnn_mc")
+    ref = {k[len("f64/param/"):]: g[k] for k in g.files if k.startswith("f64/param/")}
+    sd = make().state_dict()
+    assert set(sd) == set(ref)
+    for k, v in ref.items():
+        np.testing.assert_array_equal(sd[k].numpy(), v)
+
+
+def emulate(model, pos, vel, mass, B, N):
+    """numpy mirror of csrc/egnn.hip driven by the packed (padded) operands."""
+    P = {k: v.double().numpy() for k, v in model.packed_matrices("cpu", torch.float64).items()}
+    H = model.hidden_node_dim
+    kp = (H + 31) // 32 * 32
+    silu = lambda x: x / (1 + np.exp(-x))
+    ei = fc_edge_index(B, N)
+    row, col = ei
+    V = B * N
+    x4 = np.zeros((V, 32)); x4[:, 0] = np.linalg.norm(vel, axis=1); x4[:, 1] = mass
+    d = pos[row] - pos[col]
+    d2 = (d ** 2).sum(1)
+    dh = d / np.maximum(np.sqrt(d2), 1e-12)[:, None]
+    ea = np.stack([mass[row] * mass[col], (vel[row] * dh).sum(1), (vel[col] * dh).sum(1), d2], 1)
+    h = x4 @ P["emb_t"].T + P["emb_b"]
+    coord = pos.copy()
+    pad = lambda a, w: np.pad(a, ((0, 0), (0, w - a.shape[1])))
+    for i in range(model.num_layers):
+        p = f"layers.{i}."
+        diff = coord[row] - coord[col]
+        rad = (diff ** 2).sum(1, keepdims=True)
+        diff = diff / np.maximum(np.sqrt(rad), 1.0)
+        a = np.concatenate([pad(h[row], kp), pad(h[col], kp), pad(np.concatenate([rad, ea], 1), 32)], 1)
+        ef = silu(silu(a @ P[p + "e0_t"].T + P[p + "e0_b"]) @ P[p + "e1_t"].T + P[p + "e1_b"])
+        c = np.tanh(silu(ef @ P[p + "c0_t"].T + P[p + "c0_b"]) @ P[p + "c1_w"])
+        trans = np.clip(diff * c[:, None], -100, 100).reshape(V, N - 1, 3).mean(1)
+        cv = silu(h @ P[p + "v0_t"].T + P[p + "v0_b"]) @ P[p + "v1_w"] + P[p + "v1_b"]
+        agg = ef.reshape(V, N - 1, H).mean(1)
+        nh = silu(np.concatenate([pad(h, kp), pad(agg, kp)], 1) @ P[p + "n0_t"].T + P[p + "n0_b"])
+        h = h + nh @ P[p + "n1_t"].T + P[p + "n1_b"]
+        coord = coord + trans + cv[:, None] * vel
+    hin = np.concatenate([pad(h, kp), pad(np.concatenate([coord - pos, vel], 1), 32)], 1)
+    outs = []
+    for t in range(2):
+        p = f"heads.{t}."
+        y = silu(silu(hin @ P[p + "w0_t"].T + P[p + "b0"]) @ P[p + "w1_t"].T + P[p + "b1"])
+        outs.append(y @ P[p + "w2_t"].T + P[p + "b2"])
+    return np.concatenate(outs, 1)
+
+
+def test_packed_emulation_matches_reference(golden):
+    g = golden("egnn_mc")
+    model = make()
+    loc, vel, mass = g["loc"].reshape(-1, 3), g["vel"].reshape(-1, 3), g["mass"].reshape(-1)
+    got = emulate(model, loc, vel, mass, 4, 5)
+    np.testing.assert_allclose(got, g["f64/pred"], rtol=1e-10, atol=1e-12)
+
+
+class Graph:
+    pass
+
+
+@pytest.mark.gpu
+def test_gpu_forward_matches_reference(hip_device, golden):
+    g = golden("egnn_mc")
+    model = make(dtype=torch.float32).to(hip_device)
+    gr = Graph()
+    gr.pos = torch.tensor(g["loc"].reshape(-1, 3), dtype=torch.float32, device=hip_device)
+    gr.vel = torch.tensor(g["vel"].reshape(-1, 3), dtype=torch.float32, device=hip_device)
+    gr.mass = torch.tensor(g["mass"].reshape(-1, 1), dtype=torch.float32, device=hip_device)
+    gr.edge_index = G.fc_edge_index(4, 5, hip_device)
+    out = model(gr).double().cpu().numpy()
+    ref = g["f64/pred"]
+    assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_matches_reference(hip_device, golden):
+    g = golden("egnn_mc")
+    model = make(dtype=torch.float32).to(hip_device)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = model.rollout(t(g["loc"]), t(g["vel"]), t(g["mass"]), 10)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    rl, rv = g["f64/roll_loc"], g["f64/roll_vel"]
+    for k in range(10):
+        tol = 1e-4 * (k + 1)
+        assert np.abs(tp[:, k] - rl[:, k]).max() <= tol * np.abs(rl[:, k]).max() + 1e-6
+        assert np.abs(tv[:, k] - rv[:, k]).max() <= tol * np.abs(rv[:, k]).max() + 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N,hidden,layers", [(64, 5, 128, 6), (3, 7, 64, 2), (2, 2, 32, 1)])
+def test_gpu_forward_matches_oracle(hip_device, B, N, hidden, layers):
+    """C1 shape (B=64, 6 x 128) and edge cases vs the numpy oracle."""
+    model = make(hidden, layers, torch.float32).to(hip_device)
+    params = {k: v.double().cpu().numpy() for k, v in model.state_dict().items()}
+    rng = np.random.default_rng(1)
+    pos, vel = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3))
+    mass = np.ones((B * N, 1))
+    ei = fc_edge_index(B, N)
+    x, ea = oe.preprocess(pos, vel, mass, ei)
+    ref = oe.forward(params, x, pos, vel, ei, ea, layers)
+    gr = Graph()
+    gr.pos = torch.tensor(pos, dtype=torch.float32, device=hip_device)
+    gr.vel = torch.tensor(vel, dtype=torch.float32, device=hip_device)
+    gr.mass = torch.tensor(mass, dtype=torch.float32, device=hip_device)
+    gr.edge_index = G.fc_edge_index(B, N, hip_device)
+    out = model(gr).double().cpu().numpy()
+    assert np.abs(out - ref).max() <= 2e-4 * np.abs(ref).max() + 1e-6
