@@ -53,6 +53,21 @@ class EgnnWeights(ctypes.Structure):
         ("layers", EgnnLayer * EGNN_MAX_LAYERS)]
 
 
+PONITA_MAX_LAYERS = 64
+
+
+class PonitaLayer(ctypes.Structure):
+    _fields_ = [(n, c_p) for n in ("kernel_t", "conv_bias", "norm_w", "norm_b", "lin1_t", "lin1_b", "lin2_t",
+                                   "lin2_b", "layer_scale", "readout_w", "readout_b")]
+
+
+class PonitaWeights(ctypes.Structure):
+    _fields_ = [(n, c_i32) for n in ("hidden", "basis_dim", "widening", "num_layers", "num_ori")] + [
+        (n, c_p) for n in ("ori_grid", "basis1_t", "basis1_b", "basis2_t", "basis2_b", "fbasis1_t", "fbasis1_b",
+                           "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w")] + [
+        ("layers", PonitaLayer * PONITA_MAX_LAYERS)]
+
+
 _SIGNATURES = {
     "nbx_abi_version": (ctypes.c_int, []),
     "nbx_last_error": (ctypes.c_char_p, []),
@@ -73,6 +88,12 @@ _SIGNATURES = {
                                         c_p, c_sz, c_p]),
     "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
                                          c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_ponita_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_i64, c_i64,
+                                                  ctypes.POINTER(c_sz)]),
+    "nbx_ponita_forward": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,
+                                          c_p, c_sz, c_p]),
+    "nbx_ponita_rollout": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
+                                          c_p, c_p, c_p, c_sz, c_p]),
 }
 
 _lib = None

@@ -13,6 +13,7 @@
 #include <cstring>
 
 #include "lin.h"
+#include "rollout_state.h"
 #include "nbx_internal.h"
 
 namespace {
@@ -116,26 +117,6 @@ __global__ void egnn_headin_kernel(const float* __restrict__ coord, const float*
         HX[8 * v + 3 + k] = vel[3 * v + k];
     }
     HX[8 * v + 6] = HX[8 * v + 7] = 0.f;
-}
-
-__global__ void egnn_state_kernel(float* __restrict__ pos, float* __restrict__ vel, const float* __restrict__ out,
-                                  int64_t V, int N, int64_t frame, int64_t num_frames, float* __restrict__ tp,
-                                  float* __restrict__ tv) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= V * 3) return;
-    const int64_t node = i / 3;
-    const int k = (int)(i - node * 3);
-    float p = pos[i], v = vel[i];
-    if (frame > 0) {
-        p = p + out[6 * node + k];
-        v = out[6 * node + 3 + k];
-        pos[i] = p;
-        vel[i] = v;
-    }
-    const int64_t b = node / N, d = node - b * N;
-    const int64_t o = ((b * num_frames + frame) * N + d) * 3 + k;
-    tp[o] = p;
-    tv[o] = v;
 }
 
 struct EgnnWs {
@@ -305,11 +286,11 @@ extern "C" int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* ve
     NBX_CHECK_ARG(num_frames >= 1 && w->num_heads == 2, "nbx_egnn_rollout: needs 2 heads (pos_dt, vel), frames >= 1");
     hipStream_t st = (hipStream_t)stream;
     const int64_t V = B * N;
-    hipLaunchKernelGGL(egnn_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
+    hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
                        num_frames, traj_pos, traj_vel);
     for (int64_t f = 1; f < num_frames; ++f) {
         if (int rc = egnn_forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st)) return rc;
-        hipLaunchKernelGGL(egnn_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, f,
+        hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, f,
                            num_frames, traj_pos, traj_vel);
     }
     NBX_LAUNCH_CHECK("egnn rollout");

@@ -9,6 +9,8 @@
 // through v_mfma_f32_32x32x2_f32.  Epilogues: bias, activation (SiLU / exact
 // GELU / tanh), optional residual "Y = R + s (.) act(...)" and optional
 // accumulate of a per-row dot product with a vector (EGNN's 128 -> 1 heads).
+// LIN_CONV instead multiplies each output by a gathered source feature and sums
+// groups of G consecutive rows in registers (PONITA's message aggregation).
 // Fragment maps and the in-chunk K permutation are those of tp_fused.h.
 #pragma once
 #include "nbx_internal.h"
@@ -18,6 +20,7 @@ namespace nbx {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 enum LinAct : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
+enum LinEpi : int { LIN_STORE = 0, LIN_CONV = 1 };
 
 struct LinSeg {
     const float* ptr;   // segment base
@@ -41,6 +44,13 @@ struct LinProb {
     const float* scale; // optional per-column scale s (layer_scale)
     const float* dotw;  // optional: rowdot[row] += sum_n act(...)[n] * dotw[n]
     float* rowdot;      // [rows] accumulated with atomics across column blocks (zero it first)
+    // LIN_CONV (PONITA FiberBundleConv spatial part on a fully-connected graph): rows are
+    // (d, o, q) with G >= N-1 edge slots q per (node d, orientation o), slot q < N-1 holding the
+    // message from src(d, q) = system base + (q < d ? q : q + 1);
+    // Y[(d*O + o), n] = sum_q acc[(d, o, q), n] * X[(src(d, q)*O + o), n]
+    int conv_G, conv_O, conv_nodes;  // slots per (d,o) (power of two <= 32), orientations, N
+    const float* conv_x;             // [V*O][ldx]
+    int conv_ldx;
     int blocks_per_chunk;
     int chunks;         // ceil(N / (NT*32))
 };
@@ -56,7 +66,7 @@ __device__ inline float lin_act(float x, int act) {
     }
 }
 
-template <int NT, int ACT>
+template <int NT, int ACT, int EPI = LIN_STORE>
 __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int chunk = blockIdx.x / P.blocks_per_chunk;
@@ -148,34 +158,89 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
             }
         }
         // ---- epilogue: col = n0 + 32 j + r; row = rt*32 + (e&3) + 8(e>>2) + 4h
-        float dot[16];
+        if constexpr (EPI == LIN_CONV) {
+            const int G = P.conv_G, O = P.conv_O;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) dot[e] = 0.f;
+            for (int j = 0; j < NT; ++j) {
+                const int col = n0 + 32 * j + r;
+                const bool live = col < P.N;
+                float m[16];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int col = n0 + 32 * j + r;
-            const bool live = col < P.N;
-            const float b = (live && P.bias) ? P.bias[col] : 0.f;
-            const float sc = (live && P.scale) ? P.scale[col] : 1.f;
-            const float dw = (live && P.dotw) ? P.dotw[col] : 0.f;
+                for (int e = 0; e < 16; ++e) {
+                    const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    const int q = row % G, dq = row / G, d = dq / O, o = dq - d * O;
+                    float v = 0.f;
+                    if (live && row < P.rows && q < P.conv_nodes - 1) {
+                        const int dl = d % P.conv_nodes;
+                        const int64_t src = (int64_t)(d - dl) + (q < dl ? q : q + 1);
+                        v = acc[j][e] * P.conv_x[((size_t)src * O + o) * P.conv_ldx + col];
+                    }
+                    m[e] = v;
+                }
+                auto put = [&](int row, float a) {
+                    if (live && row < P.rows) P.Y[(size_t)(row / G) * P.ldy + col] = a;
+                };
+                if (G <= 4) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                float y = lin_act(acc[j][e] + b, ACT);
-                dot[e] += y * dw;
-                if (live && row < P.rows && P.Y) {
-                    if (P.resid) y = P.resid[(size_t)row * P.ldr + col] + sc * y;
-                    P.Y[(size_t)row * P.ldy + col] = y;
+                    for (int e0 = 0; e0 < 16; e0 += 4)
+#pragma unroll
+                        for (int s0 = 0; s0 < 4; ++s0) {
+                            if (s0 % G) continue;
+                            float a = 0.f;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (s0 + u < 4 && u < G) a += m[e0 + s0 + u];
+                            put(rt * 32 + s0 + 8 * (e0 >> 2) + 4 * h, a);
+                        }
+                } else {
+                    float b8[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        b8[k] = m[4 * k] + m[4 * k + 1] + m[4 * k + 2] + m[4 * k + 3];
+                        b8[k] += __shfl_xor(b8[k], 32);
+                    }
+                    const int nb = G / 8;
+#pragma unroll
+                    for (int gb = 0; gb < 4; ++gb) {
+                        if (gb % nb) continue;
+                        float a = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            if (k >= gb && k < gb + nb) a += b8[k];
+                        if (h == 0) put(rt * 32 + 8 * gb, a);
+                    }
                 }
             }
-        }
-        if (P.dotw) {
+        } else {
+            float dot[16];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                float v = dot[e];
-                for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);  // sum over the 32 columns
-                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (r == 0 && row < P.rows) atomicAdd(&P.rowdot[row], v);
+            for (int e = 0; e < 16; ++e) dot[e] = 0.f;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int col = n0 + 32 * j + r;
+                const bool live = col < P.N;
+                const float b = (live && P.bias) ? P.bias[col] : 0.f;
+                const float sc = (live && P.scale) ? P.scale[col] : 1.f;
+                const float dw = (live && P.dotw) ? P.dotw[col] : 0.f;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    float y = lin_act(acc[j][e] + b, ACT);
+                    dot[e] += y * dw;
+                    if (live && row < P.rows && P.Y) {
+                        if (P.resid) y = P.resid[(size_t)row * P.ldr + col] + sc * y;
+                        P.Y[(size_t)row * P.ldy + col] = y;
+                    }
+                }
+            }
+            if (P.dotw) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    float v = dot[e];
+                    for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);  // sum over the 32 columns
+                    const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (r == 0 && row < P.rows) atomicAdd(&P.rowdot[row], v);
+                }
             }
         }
         rt += wstride;
@@ -183,7 +248,7 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     }
 }
 
-template <int NT, int ACT>
+template <int NT, int ACT, int EPI = LIN_STORE>
 int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     if (p.rows <= 0 || p.N <= 0) return NBX_OK;
     if (p.Ktot % 32) {
@@ -207,11 +272,11 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     p.blocks_per_chunk = bpc;
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
+        NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT, EPI>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((lin_kernel<NT, ACT>), dim3(p.chunks * bpc), dim3(LIN_THREADS), lds, st, p);
+    hipLaunchKernelGGL((lin_kernel<NT, ACT, EPI>), dim3(p.chunks * bpc), dim3(LIN_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

@@ -1,0 +1,369 @@
+"""PONITA_NBODY — drop-in for models/ponita/ponita_nbody.py with a HIP forward.
+
+Module tree, parameter names and initialisation order follow the reference
+(ponita_nbody.py:12-80, models/ponita_pg.py:59-127, nn/conv.py:65-101,
+nn/convnext.py:4-16), including the S2 orientation grid drawn by repulsion at
+construction (geometry/rotation.py:916-1010, geometry/repulsion.py:31-90) and the
+two LazyLinear layers materialised at the first forward, so ``torch.manual_seed(s)``
+gives the reference's grid and weights and reference checkpoints load.  Unlike the
+reference, the grid is a persistent buffer (``model.ori_grid``): a checkpoint
+written here carries it; loading a reference checkpoint (which has none) keeps
+the grid of the constructed model, exactly as the reference does.
+
+``forward(graph)`` takes the rollout / dataloader graph (x = mass, vec = vel,
+pos, fully-connected edge_index; infer_self_feed.py:131-147,
+dataloaders/ponita_n_body_dataloader.py:8-38) and runs the whole model in libnbx
+(csrc/ponita.hip).  The first training-mode forward performs the one-time
+FiberBundleConv "callibrate" weight rescaling (conv.py:115-117,134-140) from
+moments the HIP path returns.  ``rollout`` runs the self-feed loop device-resident.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from . import _lib
+
+__all__ = ["PONITA_NBODY", "PonitaFiberBundle", "uniform_grid_s2"]
+
+
+# ------------------------------------------------------------------ S2 grid
+def _spherical_to_euclid(g):
+    x = g.new_empty((*g.shape[:-1], 3))
+    beta, gamma = g[..., 0], g[..., 1]
+    x[..., 0] = torch.sin(beta) * torch.cos(gamma)
+    x[..., 1] = torch.sin(beta) * torch.sin(gamma)
+    x[..., 2] = torch.cos(beta)
+    return x
+
+
+def _euclid_to_spherical(x):
+    g = x.new_empty((*x.shape[:-1], 2))
+    g[..., 0] = torch.acos(x[..., 2])
+    g[..., 1] = torch.atan2(x[..., 1], x[..., 0])
+    return g
+
+
+def _geodesic_distance_s2(r1, r2, eps: float = 1e-7):
+    return torch.acos(torch.clamp((r1 * r2).sum(-1), -1 + eps, 1 - eps))
+
+
+def uniform_grid_s2(n: int, steps: int = 100, step_size: float = 0.1, alpha: float = 0.001) -> torch.Tensor:
+    """rotation.py:946-1010 with parameterization 'euclidean': a random S2 grid
+    (random_s2, rotation.py:916-929) relaxed by Coulomb repulsion under SGD with
+    annealed gradient noise (repulsion.py:31-90).  Consumes the global RNG in the
+    same order as the reference."""
+    x = torch.randn((n, 3))
+    grid = _euclid_to_spherical(x / torch.linalg.norm(x, dim=-1, keepdim=True))
+    with torch.enable_grad():
+        grid.requires_grad = True
+        opt = torch.optim.SGD([grid], lr=step_size)
+        for epoch in range(steps):
+            opt.zero_grad(set_to_none=True)
+            e = _spherical_to_euclid(grid)
+            dists = _geodesic_distance_s2(e[:, None], e).sort(dim=-1)[0][:, 1:]
+            energy = (dists / math.pi) ** (-2)
+            energy.mean().backward()
+            grid.grad += (steps - epoch) / steps * alpha * torch.randn(grid.grad.shape)
+            opt.step()
+        grid.requires_grad = False
+    return _spherical_to_euclid(grid.detach())
+
+
+# ------------------------------------------------------------------ modules
+class PolynomialFeatures(nn.Module):
+    """nn/embedding.py:4-15 (parameter-free; its arithmetic is in po_attr_kernel)."""
+
+    def __init__(self, degree):
+        super().__init__()
+        self.degree = degree
+
+
+class FiberBundleConv(nn.Module):
+    """nn/conv.py:65-101: separable depth-wise conv parameters + the callibrated flag."""
+
+    def __init__(self, channels, attr_dim):
+        super().__init__()
+        self.kernel = nn.Linear(attr_dim, channels, bias=False)
+        self.fiber_kernel = nn.Linear(attr_dim, channels, bias=False)
+        self.bias = nn.Parameter(torch.empty(channels))
+        self.bias.data.zero_()
+        self.register_buffer("callibrated", torch.tensor(False))
+
+
+class ConvNext(nn.Module):
+    """nn/convnext.py:4-16."""
+
+    def __init__(self, channels, conv, layer_scale=1e-6, widening_factor=4):
+        super().__init__()
+        self.conv = conv
+        self.act_fn = nn.GELU()
+        self.linear_1 = nn.Linear(channels, widening_factor * channels)
+        self.linear_2 = nn.Linear(widening_factor * channels, channels)
+        if layer_scale is not None:
+            self.layer_scale = nn.Parameter(torch.ones(channels) * layer_scale)
+        else:
+            self.register_buffer("layer_scale", None)
+        self.norm = nn.LayerNorm(channels)
+
+
+class PonitaFiberBundle(nn.Module):
+    """models/ponita_pg.py:56-127 (fibre-bundle variant, task_level 'node')."""
+
+    def __init__(self, input_dim, hidden_dim, output_dim, num_layers, output_dim_vec=0, radius=None, num_ori=20,
+                 basis_dim=None, degree=3, widening_factor=4, layer_scale=None, multiple_readouts=True):
+        super().__init__()
+        self.output_dim, self.output_dim_vec = output_dim, output_dim_vec
+        self.hidden_dim, self.num_ori, self.degree, self.radius = hidden_dim, num_ori, degree, radius
+        self.widening_factor = widening_factor
+        # PositionOrientationGraph(num_ori) draws the grid at construction (position_orientation_graph.py:31-32)
+        self.register_buffer("ori_grid", uniform_grid_s2(num_ori))
+        basis_dim = hidden_dim if basis_dim is None else basis_dim
+        self.basis_dim = basis_dim
+        self.basis_fn = nn.Sequential(PolynomialFeatures(degree), nn.LazyLinear(hidden_dim), nn.GELU(),
+                                      nn.Linear(hidden_dim, basis_dim), nn.GELU())
+        self.fiber_basis_fn = nn.Sequential(PolynomialFeatures(degree), nn.LazyLinear(hidden_dim), nn.GELU(),
+                                            nn.Linear(hidden_dim, basis_dim), nn.GELU())
+        self.x_embedder = nn.Linear(input_dim, hidden_dim, False)
+        self.interaction_layers = nn.ModuleList()
+        self.read_out_layers = nn.ModuleList()
+        for i in range(num_layers):
+            conv = FiberBundleConv(hidden_dim, basis_dim)
+            self.interaction_layers.append(ConvNext(hidden_dim, conv, layer_scale=layer_scale,
+                                                    widening_factor=widening_factor))
+            if multiple_readouts or i == num_layers - 1:
+                self.read_out_layers.append(nn.Linear(hidden_dim, output_dim + output_dim_vec))
+            else:
+                self.read_out_layers.append(None)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        # reference checkpoints do not carry the grid: keep the constructed one
+        key = prefix + "ori_grid"
+        if key not in state_dict:
+            state_dict[key] = self.ori_grid
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+
+    def materialize(self):
+        """LazyLinear(hidden) of both basis MLPs, in forward order (basis_fn first),
+        initialised on the CPU generator in the model dtype as the reference's first
+        forward does (in_features = 14 and 3 for degree 3 and 2 / 1 invariants)."""
+        ref = self.x_embedder.weight
+        for seq, n_inv in ((self.basis_fn, 2), (self.fiber_basis_fn, 1)):
+            lazy = seq[1]
+            if isinstance(lazy, nn.modules.lazy.LazyModuleMixin) and lazy.has_uninitialized_params():
+                fan_in = sum(n_inv ** k for k in range(1, self.degree + 1))
+                lin = nn.Linear(fan_in, lazy.out_features, dtype=ref.dtype)
+                seq[1] = lin.to(ref.device)
+
+
+class PONITA_NBODY(nn.Module):
+    """ponita_nbody.py:9-116.  ``forward(graph) -> [B*N, 6]`` (pos_dt | vel)."""
+
+    def __init__(self, lr=1e-3, weight_decay=1e-5, warmup=10, layer_scale=1e-6, train_augm=False, hidden_dim=64,
+                 layers=4, radius=None, num_ori=20, basis_dim=128, degree=3, widening_factor=4,
+                 multiple_readouts=True, in_channels_scalar=1, in_channels_vec=1, out_channels_scalar=0,
+                 out_channels_vec=2):
+        super().__init__()
+        self.lr, self.weight_decay, self.warmup = lr, weight_decay, warmup
+        self.layer_scale, self.train_augm = layer_scale, train_augm
+        self.hidden_dim, self.layers, self.radius, self.num_ori = hidden_dim, layers, radius, num_ori
+        self.basis_dim, self.degree, self.widening_factor = basis_dim, degree, widening_factor
+        self.multiple_readouts = multiple_readouts
+        self.in_channels_scalar, self.in_channels_vec = in_channels_scalar, in_channels_vec
+        self.out_channels_scalar, self.out_channels_vec = out_channels_scalar, out_channels_vec
+        if layer_scale == 0.0:
+            layer_scale = None
+        self.model = PonitaFiberBundle(in_channels_scalar + in_channels_vec, hidden_dim, out_channels_scalar, layers,
+                                       output_dim_vec=out_channels_vec, radius=radius, num_ori=num_ori,
+                                       basis_dim=basis_dim, degree=degree, widening_factor=widening_factor,
+                                       layer_scale=layer_scale, multiple_readouts=multiple_readouts)
+        bd = hidden_dim if basis_dim is None else basis_dim
+        native = (in_channels_scalar == 1 and in_channels_vec == 1 and out_channels_scalar == 0
+                  and out_channels_vec == 2 and radius is None and degree == 3 and hidden_dim in (32, 64, 128)
+                  and bd % 4 == 0 and bd <= 1024 and 1 <= num_ori <= 24 and widening_factor * hidden_dim <= 1024
+                  and 1 <= layers <= _lib.PONITA_MAX_LAYERS)
+        self._native_reason = None if native else (
+            "native PONITA needs x = mass, vec = vel, 2 vector outputs, radius None, degree 3, hidden in "
+            "{32, 64, 128}, basis_dim % 4 == 0, num_ori <= 24, widening * hidden <= 1024")
+        self._packed = None
+        self._ws = None
+
+    def get_serializable_attributes(self):
+        return {"lr": self.lr, "weight_decay": self.weight_decay, "warmup": self.warmup,
+                "layer_scale": self.layer_scale, "train_augm": self.train_augm, "hidden_dim": self.hidden_dim,
+                "layers": self.layers, "radius": self.radius, "num_ori": self.num_ori, "basis_dim": self.basis_dim,
+                "degree": self.degree, "widening_factor": self.widening_factor,
+                "multiple_readouts": self.multiple_readouts}
+
+    def get_model_size(self):
+        return self.hidden_dim
+
+    # ------------------------------------------------------------ packing
+    def _version(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters()) + (
+            self.model.ori_grid.data_ptr(), self.model.ori_grid._version)
+
+    def packed_matrices(self, device, dtype=torch.float32):
+        """nn.Linear weights [out][K] with K zero-padded to a multiple of 32
+        (include/nbx.h, PONITA section)."""
+        m = self.model
+        m.materialize()
+        f = dict(device=device, dtype=dtype)
+        kp = lambda k: (k + 31) // 32 * 32
+
+        def pad(w):
+            w = w.detach().to(**f)
+            return nn.functional.pad(w, (0, kp(w.shape[1]) - w.shape[1])).contiguous()
+
+        vec = lambda t: t.detach().to(**f).contiguous()
+        P = {"ori_grid": vec(m.ori_grid), "embed_w": vec(m.x_embedder.weight),
+             "basis1_t": pad(m.basis_fn[1].weight), "basis1_b": vec(m.basis_fn[1].bias),
+             "basis2_t": pad(m.basis_fn[3].weight), "basis2_b": vec(m.basis_fn[3].bias),
+             "fbasis1_t": pad(m.fiber_basis_fn[1].weight), "fbasis1_b": vec(m.fiber_basis_fn[1].bias),
+             "fbasis2_t": pad(m.fiber_basis_fn[3].weight), "fbasis2_b": vec(m.fiber_basis_fn[3].bias),
+             "fiber_t": pad(torch.cat([L.conv.fiber_kernel.weight.detach() for L in m.interaction_layers], 0))}
+        for i, (L, R) in enumerate(zip(m.interaction_layers, m.read_out_layers)):
+            p = f"layers.{i}."
+            P[p + "kernel_t"] = pad(L.conv.kernel.weight)
+            P[p + "conv_bias"] = vec(L.conv.bias)
+            P[p + "norm_w"], P[p + "norm_b"] = vec(L.norm.weight), vec(L.norm.bias)
+            P[p + "lin1_t"], P[p + "lin1_b"] = pad(L.linear_1.weight), vec(L.linear_1.bias)
+            P[p + "lin2_t"], P[p + "lin2_b"] = pad(L.linear_2.weight), vec(L.linear_2.bias)
+            if L.layer_scale is not None:
+                P[p + "layer_scale"] = vec(L.layer_scale)
+            if R is not None:
+                P[p + "readout_w"], P[p + "readout_b"] = vec(R.weight), vec(R.bias)
+        return P
+
+    def pack_weights(self, device):
+        P = self.packed_matrices(device)
+        m = self.model
+        W = _lib.PonitaWeights()
+        W.hidden, W.basis_dim, W.widening = m.hidden_dim, m.basis_dim, m.widening_factor
+        W.num_layers, W.num_ori = len(m.interaction_layers), m.num_ori
+        for name in ("ori_grid", "basis1_t", "basis1_b", "basis2_t", "basis2_b", "fbasis1_t", "fbasis1_b",
+                     "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w"):
+            setattr(W, name, P[name].data_ptr())
+        for i in range(W.num_layers):
+            L = W.layers[i]
+            for name, _ in L._fields_:
+                t = P.get(f"layers.{i}.{name}")
+                setattr(L, name, t.data_ptr() if t is not None else None)
+        self._packed = (self._version(), W, P)
+        return W
+
+    def _weights(self, device):
+        if self._native_reason:
+            raise NotImplementedError(self._native_reason)
+        self.model.materialize()
+        if self._packed is None or self._packed[0] != self._version():
+            self.pack_weights(device)
+        return self._packed[1]
+
+    def _workspace(self, W, B, N, device):
+        n = _lib.c_sz()
+        _lib.check(_lib.lib().nbx_ponita_workspace_bytes(W, B, N, n), "ponita workspace")
+        if self._ws is None or self._ws.numel() < n.value or self._ws.device != device:
+            self._ws = None
+            self._ws = torch.empty(n.value, dtype=torch.uint8, device=device)
+        return self._ws
+
+    # ------------------------------------------------------------ calibration
+    def _needs_callibration(self):
+        return self.training and any(not bool(L.conv.callibrated) for L in self.model.interaction_layers)
+
+    @torch.no_grad()
+    def _callibrate(self, moments, n):
+        """FiberBundleConv.callibrate (conv.py:134-140) from per-layer (sum, sum sq)
+        of the layer input, x_1 and x_2: unbiased std as torch's Tensor.std()."""
+        mom = moments.double().cpu().view(-1, 3, 2)
+        std = torch.sqrt((mom[:, :, 1] - mom[:, :, 0] ** 2 / n) / (n - 1))
+        for i, L in enumerate(self.model.interaction_layers):
+            if bool(L.conv.callibrated):
+                continue
+            s_in, s_1, s_2 = (float(v) for v in std[i])
+            L.conv.kernel.weight.data = L.conv.kernel.weight.data * s_in / s_1
+            L.conv.fiber_kernel.weight.data = L.conv.fiber_kernel.weight.data * s_1 / s_2
+            L.conv.callibrated = ~L.conv.callibrated
+
+    # ------------------------------------------------------------ forward
+    def forward(self, graph):
+        pos = graph.pos
+        device = pos.device
+        V = pos.shape[0]
+        N = getattr(graph, "nbx_system_size", None)
+        if N is None:
+            from .segnn import SEGNN
+            B, N = SEGNN.infer_system_size(V, graph.edge_index.shape[1])
+            from .graph import fc_edge_index
+            if not torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device)):
+                raise NotImplementedError("native PONITA needs the fully-connected edge_index")
+        else:
+            N = int(N)
+            B = V // N
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
+        x = getattr(graph, "x", None)
+        if x is None:
+            x = graph.mass
+        m = f(x.reshape(V))
+        vel = graph.vec if getattr(graph, "vec", None) is not None else graph.vel
+        p, v = f(pos), f(vel.reshape(V, 3))
+        out = torch.empty(V, 6, device=device, dtype=torch.float32)
+        W = self._weights(device)
+        ws = self._workspace(W, B, N, device)
+        calib = self._needs_callibration()
+        mom = torch.zeros(6 * W.num_layers, dtype=torch.float64, device=device) if calib else None
+        _lib.check(_lib.lib().nbx_ponita_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                 _lib.dev_ptr(out), _lib.dev_ptr(mom) if calib else None,
+                                                 _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                   "nbx_ponita_forward")
+        if calib:
+            self._callibrate(mom, V * self.num_ori * self.hidden_dim)
+        return out.to(pos.dtype)
+
+    @torch.no_grad()
+    def rollout(self, loc, vel, mass, num_frames: int):
+        """Self-feed loop (infer_self_feed.py:131-147,182-194) device-resident:
+        loc/vel [B,N,3], mass [B,N,1] -> trajectories [B, T, N, 3] each, frame 0 =
+        the initial state.  A model still owing its one-time calibration runs one
+        calibrating forward on the initial state first, as the reference's first
+        step would."""
+        device = loc.device
+        B, N, _ = loc.shape
+        f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
+        p, v, m = f(loc), f(vel), f(mass.reshape(B * N))
+        if self._needs_callibration():
+            g = type("G", (), {})()
+            g.pos, g.vec, g.x, g.nbx_system_size = p.reshape(-1, 3), v.reshape(-1, 1, 3), m.reshape(-1, 1), N
+            g.edge_index = None
+            first = self.forward(g)
+        else:
+            first = None
+        tp = torch.empty(B, num_frames, N, 3, device=device, dtype=torch.float32)
+        tv = torch.empty_like(tp)
+        W = self._weights(device)
+        ws = self._workspace(W, B, N, device)
+        if first is None:
+            _lib.check(_lib.lib().nbx_ponita_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                     num_frames, _lib.dev_ptr(tp), _lib.dev_ptr(tv),
+                                                     _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                       "nbx_ponita_rollout")
+            return tp, tv
+        # frame 1 came from the calibrating forward; the rest from the calibrated weights
+        tp[:, 0], tv[:, 0] = p, v
+        if num_frames == 1:
+            return tp, tv
+        p = p + first[:, :3].reshape(B, N, 3)
+        v = first[:, 3:].reshape(B, N, 3).contiguous()
+        rp = torch.empty(B, num_frames - 1, N, 3, device=device, dtype=torch.float32)
+        rv = torch.empty_like(rp)
+        _lib.check(_lib.lib().nbx_ponita_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                 num_frames - 1, _lib.dev_ptr(rp), _lib.dev_ptr(rv),
+                                                 _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                   "nbx_ponita_rollout")
+        tp[:, 1:], tv[:, 1:] = rp, rv
+        return tp, tv

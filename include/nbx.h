@@ -209,6 +209,65 @@ int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* vel, const fl
                      int64_t num_nodes, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * PONITA fibre bundle (models/ponita/ponita_nbody.py:9-95,
+ * models/ponita/models/ponita_pg.py:56-192, nn/conv.py:65-140,
+ * nn/convnext.py:4-32, transforms/, geometry/invariants.py:9-51) — fp32.
+ *
+ * Scope: num_ori orientations on S2 (<= 24), hidden C in {32, 64, 128},
+ * basis_dim % 4 == 0, degree 3, in = (mass, vel), out = 2 vector channels,
+ * radius None (identity window), fully-connected systems.  Weights as
+ * W [out][K] with K zero-padded to a multiple of 32 (`Kp(x) = ceil32(x)`):
+ *   basis1_t / fbasis1_t [C][32]        (14 / 3 polynomial features valid)
+ *   basis2_t / fbasis2_t [Bk][Kp(C)]    (Bk = basis_dim)
+ *   fiber_t  [L*C][Kp(Bk)]              (conv.fiber_kernel of every layer, stacked)
+ *   kernel_t [C][Kp(Bk)]; lin1_t [4C][Kp(C)]; lin2_t [C][Kp(4C)]
+ *   embed_w  [C][2] (x_embedder, no bias); readout_w [2][C].
+ * The orientation grid ori_grid [O][3] is an input like any weight (the
+ * reference draws it from the RNG at construction and does not persist it).
+ */
+#define NBX_PONITA_MAX_LAYERS 64
+
+typedef struct nbx_ponita_layer {
+    const float* kernel_t;            /* conv.kernel (no bias) */
+    const float* conv_bias;           /* conv.bias [C] */
+    const float* norm_w; const float* norm_b;   /* LayerNorm(C), eps 1e-5 */
+    const float* lin1_t; const float* lin1_b;   /* linear_1 -> GELU */
+    const float* lin2_t; const float* lin2_b;   /* linear_2 */
+    const float* layer_scale;         /* [C] or NULL */
+    const float* readout_w; const float* readout_b;  /* read_out_layers[i] or NULL */
+} nbx_ponita_layer;
+
+typedef struct nbx_ponita_weights {
+    int32_t hidden, basis_dim, widening, num_layers, num_ori;
+    const float* ori_grid;
+    const float* basis1_t; const float* basis1_b;
+    const float* basis2_t; const float* basis2_b;
+    const float* fbasis1_t; const float* fbasis1_b;
+    const float* fbasis2_t; const float* fbasis2_b;
+    const float* fiber_t;
+    const float* embed_w;
+    nbx_ponita_layer layers[NBX_PONITA_MAX_LAYERS];
+} nbx_ponita_weights;
+
+int nbx_ponita_workspace_bytes(const nbx_ponita_weights* w, int64_t batch_size, int64_t num_nodes, size_t* bytes);
+
+/* PONITA_NBODY.forward on the graph of infer_self_feed.py:131-147
+ * (x = mass, vec = vel, rel_pos = pos[src] - pos[dst]): out [B*N, 6].
+ * calib_moments: NULL, or a device buffer of num_layers*6 doubles that receives per layer
+ * (sum, sum of squares) of the layer input, x_1 and x_2 (before the bias) — the
+ * statistics FiberBundleConv.callibrate (conv.py:115-117,134-140) needs on the first
+ * training-mode forward; the caller rescales the weights. */
+int nbx_ponita_forward(const nbx_ponita_weights* w, const float* pos, const float* vel, const float* mass,
+                       int64_t batch_size, int64_t num_nodes, float* out, double* calib_moments, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* Device-resident self-feed rollout with the PONITA branch of
+ * infer_self_feed.py:131-147,182-194; same contract as nbx_segnn_rollout. */
+int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
+                       int64_t num_nodes, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,257 @@
+"""PONITA: host module vs reference (grid, init, state_dict), packed-operand
+emulation on CPU, and the HIP path vs the reference golden vectors and the
+numpy oracle on the GPU.
+
+Tolerance for the fp32 HIP path: max |gpu - ref| <= 1e-4 * max|ref| + 1e-6 per
+forward on the golden case, 2e-4 * max|ref| + 1e-6 vs the oracle at larger
+shapes; rollouts with a budget growing linearly with the horizon; calibrated
+weights to 1e-5 relative (fp32 std()s)."""
+import numpy as np
+import pytest
+import torch
+
+import nbody_amd.graph as G
+import nbody_amd.ponita as P
+from oracle import ponita as op
+from oracle.graph import fc_edge_index
+from oracle.rollout import ponita_step
+from oracle.rollout import rollout as oracle_rollout
+from scipy.special import erf
+
+
+def make(hidden=32, layers=2, dtype=torch.float32, **kw):
+    torch.manual_seed(0)
+    m = P.PONITA_NBODY(hidden_dim=hidden, layers=layers, lr=1e-3, **kw).to(dtype)
+    m.model.materialize()
+    return m
+
+
+def ref_params(g, tag):
+    pre = tag + "/param/"
+    return {k[len(pre):]: g[k] for k in g.files if k.startswith(pre)}
+
+
+def load_golden(model, g, tag, device="cpu"):
+    sd = {k: torch.from_numpy(np.array(v)) for k, v in ref_params(g, tag).items()}
+    model.load_state_dict(sd, strict=True)
+    model.model.ori_grid.copy_(torch.from_numpy(g[tag + "/ori_grid"]))
+    return model.to(device)
+
+
+@pytest.mark.parametrize("tag,dtype", [("f32", torch.float32), ("f64", torch.float64)])
+def test_grid_and_init_match_reference(golden, tag, dtype):
+    """Same RNG consumption as the reference: S2 repulsion grid, Linear inits and
+    the lazily materialised basis layers bit-exact; conv kernels differ from the
+    fixture only by the one-time calibration factor (a per-tensor constant)."""
+    g = golden("ponita")
+    m = make(dtype=dtype)
+    np.testing.assert_array_equal(m.model.ori_grid.numpy(), g[tag + "/ori_grid"])
+    sd = m.state_dict()
+    ref = ref_params(g, tag)
+    assert set(sd) == set(ref) | {"model.ori_grid"}
+    for k, v in ref.items():
+        a = sd[k].numpy()
+        if k.endswith("conv.kernel.weight") or k.endswith("conv.fiber_kernel.weight"):
+            r = v / a
+            assert np.ptp(r) <= 1e-6 * np.abs(r).max()
+        elif k.endswith("callibrated"):
+            assert not a and v
+        else:
+            np.testing.assert_array_equal(a, v, err_msg=k)
+
+
+def test_reference_checkpoint_loads_and_keeps_grid(golden):
+    g = golden("ponita")
+    m = make()
+    grid = m.model.ori_grid.clone()
+    ref = {k: torch.from_numpy(np.array(v)) for k, v in ref_params(g, "f32").items()}
+    m.load_state_dict(ref, strict=True)          # no ori_grid key: constructed grid kept
+    assert torch.equal(m.model.ori_grid, grid)
+    sd = m.state_dict()
+    sd["model.ori_grid"] = torch.zeros_like(grid)
+    m.load_state_dict(sd)
+    assert torch.count_nonzero(m.model.ori_grid) == 0
+
+
+def test_native_restrictions_are_loud():
+    m = make(hidden=48)
+    with pytest.raises(NotImplementedError):
+        m._weights("cpu")
+
+
+def gelu(x):
+    return 0.5 * x * (1.0 + erf(x / np.sqrt(2.0)))
+
+
+def emulate(model, pos, vel, mass, B, N):
+    """numpy mirror of csrc/ponita.hip driven by the packed (padded) operands:
+    destination-major edge slots, orientation-major fibre rows."""
+    Pm = {k: v.double().numpy() for k, v in model.packed_matrices("cpu", torch.float64).items()}
+    ori = Pm["ori_grid"]
+    O, C = ori.shape[0], model.hidden_dim
+    V = B * N
+    L = len(model.model.interaction_layers)
+    src = np.array([[(d // N) * N + (q if q < d % N else q + 1) for q in range(N - 1)] for d in range(V)])
+    rel = pos[src] - pos[:, None, :]                                        # [V, N-1, 3]
+    a = np.einsum("vqk,ok->voq", rel, ori)
+    b = np.linalg.norm(rel[:, None] - a[..., None] * ori[None, :, None], axis=-1)
+    p1 = np.stack([a, b], -1)
+    p2 = (p1[..., :, None] * p1[..., None, :]).reshape(p1.shape[:-1] + (4,))
+    p3 = (p2[..., :, None] * p1[..., None, :]).reshape(p1.shape[:-1] + (8,))
+    P16 = np.concatenate([p1, p2, p3, np.zeros(p1.shape[:-1] + (18,))], -1)  # padded to 32
+    kb = gelu(gelu(P16 @ Pm["basis1_t"].T + Pm["basis1_b"]) @ Pm["basis2_t"].T[:C] + Pm["basis2_b"])
+    s = ori @ ori.T
+    fp = np.zeros((O, O, 32))
+    fp[..., 0], fp[..., 1], fp[..., 2] = s, s * s, s * s * s
+    fkb = gelu(gelu(fp @ Pm["fbasis1_t"].T + Pm["fbasis1_b"]) @ Pm["fbasis2_t"].T[:C] + Pm["fbasis2_b"])
+    Bk = fkb.shape[-1]
+    fk = fkb @ Pm["fiber_t"].T[:Bk]                                           # [O, O, L*C]
+    x = mass.reshape(V, 1, 1) * Pm["embed_w"][:, 0] + np.einsum("vk,ok->vo", vel, ori)[..., None] * Pm["embed_w"][:, 1]
+    ro = 0.0
+    nro = 0
+    for i in range(L):
+        p = f"layers.{i}."
+        k = kb @ Pm[p + "kernel_t"].T[:Bk]                                    # [V, O, N-1, C]
+        x1 = (k * x[src].transpose(0, 2, 1, 3)).sum(2)
+        y = np.einsum("voc,opc->vpc", x1, fk[..., i * C:(i + 1) * C]) / O + Pm[p + "conv_bias"]
+        mu = y.mean(-1, keepdims=True)
+        var = ((y - mu) ** 2).mean(-1, keepdims=True)
+        xn = (y - mu) / np.sqrt(var + 1e-5) * Pm[p + "norm_w"] + Pm[p + "norm_b"]
+        h = gelu(xn @ Pm[p + "lin1_t"].T[:C] + Pm[p + "lin1_b"])
+        x = x + Pm.get(p + "layer_scale", 1.0) * (h @ Pm[p + "lin2_t"].T[:h.shape[-1]] + Pm[p + "lin2_b"])
+        if p + "readout_w" in Pm:
+            ro = ro + x @ Pm[p + "readout_w"].T + Pm[p + "readout_b"]
+            nro += 1
+    return np.einsum("voc,ok->vck", ro / nro, ori).reshape(V, 6) / O
+
+
+def test_packed_emulation_matches_reference(golden):
+    g = golden("ponita")
+    m = load_golden(make(dtype=torch.float64), g, "f64")
+    got = emulate(m, g["loc"].reshape(-1, 3), g["vel"].reshape(-1, 3), g["mass"].reshape(-1), 4, 5)
+    np.testing.assert_allclose(got, g["f64/pred"], rtol=1e-10, atol=1e-12)
+
+
+# ------------------------------------------------------------------ GPU
+class Graph:
+    pass
+
+
+def gpu_graph(pos, vel, mass, B, N, device):
+    gr = Graph()
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
+    gr.pos = t(pos).reshape(-1, 3)
+    gr.vec = t(vel).reshape(-1, 1, 3)
+    gr.x = t(mass).reshape(-1, 1)
+    gr.edge_index = G.fc_edge_index(B, N, device)
+    gr.rel_pos = gr.pos[gr.edge_index[0]] - gr.pos[gr.edge_index[1]]
+    return gr
+
+
+@pytest.mark.gpu
+def test_gpu_forward_matches_reference(hip_device, golden):
+    g = golden("ponita")
+    m = load_golden(make(), g, "f32", hip_device)
+    with torch.no_grad():
+        out = m(gpu_graph(g["loc"], g["vel"], g["mass"], 4, 5, hip_device)).double().cpu().numpy()
+    ref = g["f32/pred"]
+    assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_first_forward_calibrates_like_reference(hip_device, golden):
+    """Fresh seeded model: the first training-mode forward rescales conv.kernel /
+    conv.fiber_kernel exactly as the reference's did when the fixture was made."""
+    g = golden("ponita")
+    m = make().to(hip_device)
+    assert m.training
+    with torch.no_grad():
+        m(gpu_graph(g["loc"], g["vel"], g["mass"], 4, 5, hip_device))
+    sd = m.state_dict()
+    for k, v in ref_params(g, "f32").items():
+        a = sd[k].cpu().numpy()
+        if k.endswith("callibrated"):
+            assert bool(a)
+        else:
+            np.testing.assert_allclose(a, v, rtol=1e-5, atol=1e-7, err_msg=k)
+    with torch.no_grad():
+        out = m(gpu_graph(g["loc"], g["vel"], g["mass"], 4, 5, hip_device)).double().cpu().numpy()
+    ref = g["f32/pred"]
+    assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_matches_reference(hip_device, golden):
+    g = golden("ponita")
+    m = load_golden(make(), g, "f32", hip_device)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = m.rollout(t(g["loc"]), t(g["vel"]), t(g["mass"]), 10)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    rl, rv = g["f32/roll_loc"], g["f32/roll_vel"]
+    for k in range(10):
+        tol = 1e-4 * (k + 1)
+        assert np.abs(tp[:, k] - rl[:, k]).max() <= tol * np.abs(rl[:, k]).max() + 1e-6
+        assert np.abs(tv[:, k] - rv[:, k]).max() <= tol * np.abs(rv[:, k]).max() + 1e-6
+
+
+def oracle_params(model):
+    return {k: t.double().cpu().numpy() for k, t in model.state_dict().items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N,hidden,layers,num_ori", [(64, 5, 128, 6, 20), (3, 2, 32, 1, 20), (2, 9, 64, 2, 12),
+                                                       (1, 20, 32, 2, 24)])
+def test_gpu_forward_matches_oracle(hip_device, B, N, hidden, layers, num_ori):
+    """C3 architecture (6 x 128, 20 orientations) and edge cases: N = 2 (one edge
+    per node), N = 9 (G = 8 slots), N = 20 (19 of 32 slots live)."""
+    m = make(hidden, layers, num_ori=num_ori).to(hip_device)
+    m.eval()                                    # no calibration: compare the constructed weights
+    rng = np.random.default_rng(1)
+    pos, vel = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3))
+    mass = rng.uniform(0.5, 1.5, (B * N, 1))
+    ei = fc_edge_index(B, N)
+    ref = op.forward(oracle_params(m), mass, vel[:, None, :], ei, pos[ei[0]] - pos[ei[1]],
+                     m.model.ori_grid.double().cpu().numpy(), layers)
+    with torch.no_grad():
+        out = m(gpu_graph(pos, vel, mass, B, N, hip_device)).double().cpu().numpy()
+    assert np.abs(out - ref).max() <= 2e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_matches_oracle(hip_device):
+    B, N, T = 16, 5, 6
+    m = make(64, 3).to(hip_device)
+    m.eval()
+    rng = np.random.default_rng(2)
+    loc, vel = rng.standard_normal((B, N, 3)), rng.standard_normal((B, N, 3)) * 0.1
+    mass = np.ones((B, N, 1))
+    params = oracle_params(m)
+    grid = m.model.ori_grid.double().cpu().numpy()
+    rl, rv = oracle_rollout(ponita_step(params, grid, 3), loc, vel, np.zeros_like(loc), mass, T)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = m.rollout(t(loc), t(vel), t(mass), T)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    mse = ((tp - rl) ** 2).mean() + ((tv - rv) ** 2).mean()
+    assert mse <= 1e-5
+    for k in range(T):
+        tol = 2e-4 * (k + 1)
+        assert np.abs(tp[:, k] - rl[:, k]).max() <= tol * np.abs(rl[:, k]).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_equals_repeated_forward(hip_device):
+    B, N, T = 8, 5, 4
+    m = make(32, 2).to(hip_device)
+    m.eval()
+    rng = np.random.default_rng(3)
+    loc = torch.tensor(rng.standard_normal((B, N, 3)), dtype=torch.float32, device=hip_device)
+    vel = torch.tensor(rng.standard_normal((B, N, 3)), dtype=torch.float32, device=hip_device)
+    mass = torch.ones(B, N, 1, device=hip_device)
+    tp, tv = m.rollout(loc, vel, mass, T)
+    p, v = loc.reshape(-1, 3), vel.reshape(-1, 3)
+    for k in range(1, T):
+        with torch.no_grad():
+            out = m(gpu_graph(p.cpu().numpy(), v.cpu().numpy(), mass.cpu().numpy(), B, N, hip_device))
+        p, v = p + out[:, :3], out[:, 3:]
+        assert torch.equal(tp[:, k].reshape(-1, 3), p)
+        assert torch.equal(tv[:, k].reshape(-1, 3), v)
