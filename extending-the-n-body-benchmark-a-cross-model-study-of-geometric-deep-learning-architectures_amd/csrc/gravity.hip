@@ -107,6 +107,37 @@ __global__ void gravity_sample_kernel(double* __restrict__ pos, double* __restri
     }
 }
 
+// Trainer._compute_nbody_energies (trainer.py:888-927) per (system, frame):
+// kinetic = 0.5 sum v^2 (unit masses), potential = -G sum_{i<j} 1/sqrt(|x_i - x_j|^2 + eps^2)
+// (a zero distance with eps = 0 contributes 0, like the reference's inv_r > 0 mask).
+__global__ void nbody_energy_kernel(const double* __restrict__ loc, const double* __restrict__ vel, int64_t F, int N,
+                                    double G, double soft2, double* __restrict__ kin, double* __restrict__ pot) {
+    const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    const double* x = loc + f * N * 3;
+    const double* v = vel + f * N * 3;
+    double k = 0.0;
+    for (int i = 0; i < 3 * N; ++i) k += v[i] * v[i];
+    double s = 0.0;
+    for (int i = 0; i < N; ++i)
+        for (int j = i + 1; j < N; ++j) {
+            const double dx = x[3 * j] - x[3 * i], dy = x[3 * j + 1] - x[3 * i + 1], dz = x[3 * j + 2] - x[3 * i + 2];
+            const double r = sqrt(dx * dx + dy * dy + dz * dz + soft2);
+            s += r > 0.0 ? 1.0 / r : 0.0;
+        }
+    kin[f] = 0.5 * k;
+    pot[f] = -G * s;
+}
+
+// out[t] = mean over systems b of x[b, t]
+__global__ void batch_mean_kernel(const double* __restrict__ x, int64_t B, int64_t T, double* __restrict__ out) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    double s = 0.0;
+    for (int64_t b = 0; b < B; ++b) s += x[b * T + t];
+    out[t] = s / (double)B;
+}
+
 void launch_geometry(int64_t N, int& spb, int& threads) {
     if (N <= 256) {
         spb = (int)(256 / N);
@@ -145,5 +176,25 @@ extern "C" int nbx_gravity_sample(double* pos, double* vel, const double* mass, 
                        (hipStream_t)stream, pos, vel, mass, S, (int)N, spb, T, sample_freq, dt, G,
                        softening * softening, pos_save, vel_save, force_save);
     NBX_LAUNCH_CHECK("gravity_sample_kernel");
+    return NBX_OK;
+}
+
+extern "C" int nbx_nbody_energies(const double* loc, const double* vel, int64_t B, int64_t T, int64_t N, double G,
+                                  double softening, double* kinetic, double* potential, double* mean_kinetic,
+                                  double* mean_potential, void* stream) {
+    NBX_CHECK_ARG(B >= 0 && T >= 0 && N >= 1 && N <= 4096, "nbx_nbody_energies: bad shape");
+    NBX_CHECK_ARG(kinetic && potential, "nbx_nbody_energies: kinetic/potential outputs required");
+    const int64_t F = B * T;
+    if (F == 0) return NBX_OK;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(nbody_energy_kernel, dim3((unsigned)nbx::ceil_div(F, 256)), dim3(256), 0, st, loc, vel, F,
+                       (int)N, G, softening * softening, kinetic, potential);
+    if (mean_kinetic)
+        hipLaunchKernelGGL(batch_mean_kernel, dim3((unsigned)nbx::ceil_div(T, 256)), dim3(256), 0, st, kinetic, B, T,
+                           mean_kinetic);
+    if (mean_potential)
+        hipLaunchKernelGGL(batch_mean_kernel, dim3((unsigned)nbx::ceil_div(T, 256)), dim3(256), 0, st, potential, B,
+                           T, mean_potential);
+    NBX_LAUNCH_CHECK("nbody_energy_kernel");
     return NBX_OK;
 }

@@ -98,6 +98,34 @@ class GravitySim:
             o += np.random.randn(Ts, self.n_balls, self.dim) * self.noise_var
         return out[0], out[1], out[2], mass
 
+    def sample_trajectory_batch(self, batch_size, T=10000, sample_freq=10, seeds=None):
+        """``batch_size`` independent ``sample_trajectory`` calls integrated in one launch.
+        Each trajectory consumes the legacy RNG exactly as the reference's does
+        (seed -> initial conditions -> observation noise; the integration itself draws
+        nothing), so trajectory i equals ``sample_trajectory(random_seed=seeds[i])``.
+        ``seeds=None`` means OS entropy per trajectory, like the reference dataset."""
+        if seeds is None:
+            seeds = [None] * batch_size
+        if len(seeds) != batch_size:
+            raise ValueError("need one seed per trajectory")
+        Ts = T // sample_freq
+        ics, noise = [], []
+        for s in seeds:
+            pos, vel, mass = self.initial_conditions(s)
+            ics.append((pos, vel, mass))
+            noise.append([np.random.randn(Ts, self.n_balls, self.dim) * self.noise_var for _ in range(3)])
+        pos = np.stack([p for p, _, _ in ics])
+        vel = np.stack([v for _, v, _ in ics])
+        mass = np.stack([m for _, _, m in ics])
+        ps, vs, fs = (t.cpu().numpy() for t in self.sample_trajectories(pos, vel, mass, T, sample_freq))
+        out = []
+        for i in range(batch_size):
+            traj = [ps[i], vs[i], fs[i]]
+            for o, n in zip(traj, noise[i]):
+                o += n
+            out.append((traj[0], traj[1], traj[2], ics[i][2]))
+        return out
+
     def _energy(self, pos, vel, mass, G):
         """synthetic_sim.py:450-473 (host numpy, evaluation only)."""
         KE = 0.5 * np.sum(np.sum(mass * vel ** 2))

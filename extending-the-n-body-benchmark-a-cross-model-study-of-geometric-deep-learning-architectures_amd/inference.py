@@ -1,0 +1,216 @@
+"""Self-feed rollout API — drop-in for helper_scripts/infer_self_feed.py:20-254
+(``run_inference``), the self_feed.py names the trainer imports (``SelfFeedError``,
+``MACROS_DIR_NAME``, self_feed.py:25-40) and Trainer.run_self_feed's energy
+post-processing (trainer.py:888-1010).
+
+``run_inference`` keeps the reference's signature, seeding, dataset handling,
+truncation, output arrays ([2, B, T, N, 3]: ground truth, prediction) and
+``.npy`` file layout, but the rollout itself is ONE device-resident call
+(``model.rollout``): graph, features, forward and state update stay in HBM for all
+T-1 steps and the trajectory comes back to the host once, instead of a Python
+loop with a device->host copy per step.  Models compute in fp32 on the device;
+the returned predictions are cast to the dataset precision like the reference's.
+Macro plotting (``plot_macros``) is outside the native scope and is ignored with
+a warning.
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import warnings
+from datetime import datetime
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dataloaders import get_device
+from .dataset import GravityDatasetOtf
+
+__all__ = ["run_inference", "SelfFeedError", "MACROS_DIR_NAME", "STEPS_TO_RETURN_MULTIPLIER", "nbody_energies",
+           "get_dataset_metadata_path", "load_dataset_from_metadata_file", "SelfFeedTrainer"]
+
+MACROS_DIR_NAME = "visualize_macros"
+STEPS_TO_RETURN_MULTIPLIER = 100
+NATIVE_MODEL_TYPES = ("segnn", "ponita", "egnn_mc")
+
+
+class SelfFeedError(RuntimeError):
+    """self_feed.py:29-40."""
+
+    def __init__(self, steps_survived: int):
+        super().__init__(f"Self-feed failed after {steps_survived} steps")
+        self.steps_survived = steps_survived
+
+
+def get_dataset_metadata_path(path):
+    """utils/nbody_utils.py:1452-1488: <highest run dir named YYYY-MM-DD_HH-MM-SS>/nbody_small_dataset/metadata.json."""
+    current = os.path.abspath(path)
+    pattern = re.compile(r"\d{4}-\d{2}-\d{2}_\d{2}-\d{2}-\d{2}")
+    run_root = None
+    while True:
+        if pattern.match(os.path.basename(current)):
+            run_root = current
+        parent = os.path.dirname(current)
+        if parent == current:
+            break
+        current = parent
+    if run_root is None:
+        raise FileNotFoundError("Run directory root not found")
+    return os.path.join(run_root, "nbody_small_dataset", "metadata.json")
+
+
+_DATASET_ARGS = ("dataset_name", "target", "path", "batch_size", "sim_length", "sample_freq", "noise_var",
+                 "num_nodes", "vel_norm", "interaction_strength", "dt", "softening", "double_precision",
+                 "center_of_mass", "lmax_attr", "use_cached", "cache_data")
+
+
+def load_dataset_from_metadata_file(metadata_file_path, n_bodies=None, device=None, metadata=None):
+    """datasets/nbody/visualization_utils.py:1438-1452: keep only constructor
+    arguments (so the saved ``n_balls`` is NOT applied — num_nodes falls back to 5
+    unless ``n_bodies`` is given, as in the reference)."""
+    if metadata is None:
+        with open(metadata_file_path) as f:
+            metadata = json.load(f)
+    kw = {k: metadata[k] for k in _DATASET_ARGS if k in metadata}
+    if n_bodies is not None:
+        kw["num_nodes"] = n_bodies
+    return GravityDatasetOtf(device=device, **kw)
+
+
+def nbody_energies(loc, vel, G, softening, device=None):
+    """Trainer._compute_nbody_energies (trainer.py:888-927) on the device:
+    loc/vel [B, T, N, 3] -> dict of batch-mean potential / kinetic / total [T] (numpy)."""
+    device = device or get_device()
+    l = torch.as_tensor(np.asarray(loc), dtype=torch.float64).to(device).contiguous()
+    v = torch.as_tensor(np.asarray(vel), dtype=torch.float64).to(device).contiguous()
+    B, T, N, _ = l.shape
+    kin = torch.empty(B, T, dtype=torch.float64, device=device)
+    pot = torch.empty_like(kin)
+    mk = torch.empty(T, dtype=torch.float64, device=device)
+    mp = torch.empty_like(mk)
+    _lib.check(_lib.lib().nbx_nbody_energies(_lib.dev_ptr(l), _lib.dev_ptr(v), B, T, N, float(G), float(softening),
+                                             _lib.dev_ptr(kin), _lib.dev_ptr(pot), _lib.dev_ptr(mk), _lib.dev_ptr(mp),
+                                             _lib.stream_ptr(device)), "nbx_nbody_energies")
+    mk, mp = mk.cpu().numpy(), mp.cpu().numpy()
+    return {"potential": mp, "kinetic": mk, "total": mp + mk}
+
+
+@torch.no_grad()
+def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=None, print_step=True, n_bodies=None,
+                  plot_macros=False, num_neighbors=None, device=None, max_rollout_steps=None, dataset=None):
+    """infer_self_feed.py:20-254.  Returns ``(trajectories_save_dir,
+    combined_locations [2,B,T,N,3], combined_velocities [2,B,T,N,3])``.
+
+    The dataset comes from ``dataset`` if given, else from the run's metadata file
+    (``model_path``), else from the dataloader's dataset attributes."""
+    torch.manual_seed(42)
+    if device is None:
+        device = get_device()
+    device = torch.device(device)
+    if model_type not in NATIVE_MODEL_TYPES:
+        raise ValueError(f"model_type {model_type!r} has no native rollout (native: {NATIVE_MODEL_TYPES})")
+    if dataset is None:
+        meta = None
+        if model_path is not None:
+            try:
+                meta_path = get_dataset_metadata_path(model_path)
+                if os.path.exists(meta_path):
+                    with open(meta_path) as f:
+                        meta = json.load(f)
+            except FileNotFoundError:
+                meta = None
+        if meta is None:
+            if dataloader is None:
+                raise FileNotFoundError("no dataset metadata next to model_path and no dataloader given")
+            meta = dataloader.dataset.get_serializable_attributes()
+            meta.setdefault("num_nodes", meta.get("n_balls"))
+            if n_bodies is None:
+                n_bodies = meta["num_nodes"]
+        dataset = load_dataset_from_metadata_file(None, n_bodies=n_bodies, device=device, metadata=meta)
+    if model is None:
+        raise NotImplementedError("pass the model instance (checkpoint loading: model.load_state_dict)")
+    model = model.double() if dataset.double_precision else model.float()
+
+    batch_size = dataset.batch_size
+    batch_data, _ = dataset.get_ground_truth_trajectories(batch_size=batch_size)
+    loc_actual, vel_actual, force_actual, mass_actual = [torch.from_numpy(np.array(d)) for d in zip(*batch_data)]
+    output_dims = loc_actual.shape[-1]
+    n_nodes = loc_actual.shape[-2]
+    num_neighbors = num_neighbors if num_neighbors is not None else n_nodes - 1
+    if num_neighbors != n_nodes - 1:
+        raise NotImplementedError("the native rollout runs fully-connected systems (num_neighbors = N - 1)")
+    num_steps = loc_actual.shape[1]
+    if max_rollout_steps is not None:
+        try:
+            max_rollout_steps = int(max_rollout_steps)
+            if max_rollout_steps > 0:
+                num_steps = min(num_steps, max_rollout_steps)
+                loc_actual = loc_actual[:, :num_steps]
+                vel_actual = vel_actual[:, :num_steps]
+        except Exception as e:  # reference: print and keep the full length
+            print(e)
+    print(f"Number of steps to generate: {num_steps}")
+
+    dtype = torch.float64 if dataset.double_precision else torch.float32
+    loc0 = loc_actual[:, 0].to(device=device, dtype=dtype)
+    vel0 = vel_actual[:, 0].to(device=device, dtype=dtype)
+    mass0 = mass_actual.reshape(batch_size, n_nodes, 1).to(device=device, dtype=dtype)
+    if print_step:
+        print(f"Predicting {num_steps - 1} steps for {batch_size} simulations (device-resident rollout)")
+    tp, tv = model.rollout(loc0, vel0, mass0, num_steps)
+    print("Finished prediction for all simulations")
+    loc_pred = tp.to(dtype).cpu().numpy()
+    vel_pred = tv.to(dtype).cpu().numpy()
+    steps_in_actual = loc_actual.shape[1]
+    loc_actual = loc_actual.view(batch_size, steps_in_actual, n_nodes, output_dims).numpy()
+    vel_actual = vel_actual.view(batch_size, steps_in_actual, n_nodes, output_dims).numpy()
+    combined_locations = np.stack([loc_actual, loc_pred], axis=0)
+    combined_velocities = np.stack([vel_actual, vel_pred], axis=0)
+
+    if not save_dir:
+        base = os.path.dirname(model_path) if model_path else "."
+        save_dir = f"{base}/generated_trajectories/{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}"
+    os.makedirs(save_dir, exist_ok=True)
+    if plot_macros:
+        warnings.warn("plot_macros is outside the native rollout scope; skipped")
+    out_dir = os.path.join(save_dir, "trajectories_data")
+    os.makedirs(out_dir, exist_ok=True)
+    for i in range(batch_size):
+        np.save(os.path.join(out_dir, f"loc_actual_sim_{i}.npy"), loc_actual[i])
+        np.save(os.path.join(out_dir, f"loc_pred_sim_{i}.npy"), loc_pred[i])
+        np.save(os.path.join(out_dir, f"vel_actual_sim_{i}.npy"), vel_actual[i])
+        np.save(os.path.join(out_dir, f"vel_pred_sim_{i}.npy"), vel_pred[i])
+    print(f"Saved actual and predicted trajectories for all simulations to {out_dir}")
+    return out_dir, combined_locations, combined_velocities
+
+
+class SelfFeedTrainer:
+    """The self-feed half of trainer.Trainer (trainer.py:929-1010): ``run_self_feed``
+    rolls the model out with ``run_inference`` and computes the energy series on the
+    device.  Training itself is outside the native path."""
+
+    def __init__(self, model, train_dataloader, validation_dataloader=None, args=None, save_dir_path="."):
+        self.model, self.dataloader, self.args = model, train_dataloader, args
+        self.save_dir_path = save_dir_path
+        self.step_count = 1
+        self.device = train_dataloader.device if train_dataloader is not None else get_device()
+        self.last_energies = None
+
+    def _compute_nbody_energies(self, loc, vel, G, softening):
+        return nbody_energies(loc, vel, G, softening, self.device)
+
+    def run_self_feed(self):
+        print(f"Running self feed (epoch {self.step_count - 1})")
+        max_steps = getattr(self.args, "self_feed_limit_steps", None)
+        _, locs, vels = run_inference(model_type=self.args.model_type, dataloader=self.dataloader,
+                                      model_path=None, model=self.model,
+                                      save_dir=f"{self.save_dir_path}/checkpoints/{self.step_count}",
+                                      print_step=True, device=self.device, max_rollout_steps=max_steps)
+        steps = locs.shape[2] - 1
+        sim = self.dataloader.dataset.simulation
+        G, soft = float(sim.interaction_strength), float(sim.softening)
+        self.last_energies = {"simulation": self._compute_nbody_energies(locs[0], vels[0], G, soft),
+                              "self_feed": self._compute_nbody_energies(locs[1], vels[1], G, soft)}
+        return steps

@@ -68,6 +68,13 @@ int nbx_gravity_sample(double* pos, double* vel, const double* mass, int64_t num
                        int64_t T, int64_t sample_freq, double dt, double G, double softening,
                        double* pos_save, double* vel_save, double* force_save, void* stream);
 
+/* Trainer._compute_nbody_energies (trainer.py:888-927) on the device: loc/vel
+ * [B, T, N, 3] fp64 -> kinetic/potential [B, T] per frame (unit masses) and, when
+ * the pointers are non-NULL, their means over the B systems [T]. */
+int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size, int64_t num_frames,
+                       int64_t num_nodes, double G, double softening, double* kinetic, double* potential,
+                       double* mean_kinetic, double* mean_potential, void* stream);
+
 /* ------------------------------------------------------------------------
  * SEGNN (models/segnn/segnn.py:17-304, o3_building_blocks.py:10-278) — fp32.
  *

@@ -1,0 +1,204 @@
+"""Plugin registry, dataloaders, GravityDatasetOtf cache format and the
+run_inference host logic (CPU); the device halves (ground truth, energies,
+end-to-end rollout through the registry) are the @gpu tests at the bottom."""
+import hashlib
+import json
+import os
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+import nbody_amd.dataset as D
+import nbody_amd.inference as I
+from nbody_amd.data import Batch, Data
+from nbody_amd.registry import create_model, load_class_from_args, parse_args
+from oracle.energy import nbody_energies as oracle_energies
+
+
+# ------------------------------------------------------------------ registry
+def test_parse_args_defaults_and_overrides():
+    args, cfg = parse_args(["--model_type", "ponita", "--dataloader_type", "ponita_nbody",
+                            "--model.num_layers", "3", "--dataloader.batch_size=16",
+                            "--dataloader.gravity_dataset.num_atoms", "7"])
+    assert args.model.class_path == "nbody_amd.ponita.PONITA_NBODY"
+    assert (args.num_layers, args.batch_size, args.num_atoms) == (3, 16, 7)
+    assert args.learning_rate == 0.5            # the trainer section shadows the model's, as in the reference
+    assert cfg["models"]["ponita"]["num_layers"] == 3
+    assert args.dataloader.class_path.endswith("PonitaNBodyDataLoader")
+
+
+def test_parse_args_rejects_unknown_plugins_and_bad_class_paths(tmp_path):
+    with pytest.raises(ValueError):
+        parse_args(["--model_type", "equiformer_v2"])
+    with pytest.raises(Exception):
+        parse_args(["--model.class_path", "nbody_amd.nope.Missing"])
+
+
+@pytest.mark.parametrize("model_type,dl,cls,check", [
+    ("segnn", "segnn_nbody", "SEGNN", lambda m: sum(p.numel() for p in m.parameters()) == 1947552),
+    ("ponita", "ponita_nbody", "PONITA_NBODY", lambda m: m.hidden_dim == 128 and m.layers == 6),
+    ("egnn_mc", "egnn_mc_nbody", "EGNNMultiChannel", lambda m: m.target_names == ("pos_dt", "vel")),
+])
+def test_create_model(model_type, dl, cls, check):
+    args, _ = parse_args(["--model_type", model_type, "--dataloader_type", dl])
+    torch.manual_seed(0)
+    m = create_model(args)
+    assert type(m).__name__ == cls and check(m)
+    assert load_class_from_args(args, "dataloader").__name__.lower().startswith(model_type.replace("_", ""))
+
+
+def test_segnn_needs_segnn_dataloader():
+    args, _ = parse_args(["--model_type", "segnn", "--dataloader_type", "ponita_nbody"])
+    with pytest.raises(ValueError):
+        create_model(args)
+
+
+# ------------------------------------------------------------------ data / dataset
+def test_batch_from_data_list():
+    ds = [Data(pos=torch.randn(3, 3), mass=torch.ones(3, 1)) for _ in range(4)]
+    b = Batch.from_data_list(ds)
+    assert b.pos.shape == (12, 3) and b.num_graphs == 4
+    assert torch.equal(b.batch, torch.arange(4).repeat_interleave(3))
+
+
+def fake_trajectories(B, T, N, seed=0):
+    rng = np.random.default_rng(seed)
+    return [(rng.standard_normal((T, N, 3)), rng.standard_normal((T, N, 3)), rng.standard_normal((T, N, 3)),
+             np.ones((N, 1))) for _ in range(B)]
+
+
+@pytest.fixture
+def fake_sim(monkeypatch):
+    calls = []
+
+    def sample(self, batch_size, T=10000, sample_freq=10, seeds=None):
+        calls.append((batch_size, T, sample_freq))
+        return fake_trajectories(batch_size, T // sample_freq, self.n_balls, seed=len(calls))
+    monkeypatch.setattr(D.GravitySim, "sample_trajectory_batch", sample)
+    return calls
+
+
+def test_cache_folder_name_is_reference_hash(tmp_path, fake_sim):
+    ds = D.GravityDatasetOtf(batch_size=3, sim_length=100, num_nodes=5, device="cpu",
+                             data_path=str(tmp_path / "saved_simulations"))
+    ref = {"dataset_name": "nbody_small", "target": "pos_dt+vel", "batch_size": 3, "sim_length": 100,
+           "sample_freq": 10, "noise_var": 0, "num_nodes": 5, "vel_norm": 1e-16, "interaction_strength": 2,
+           "dt": 0.01, "softening": 0.2, "double_precision": False, "center_of_mass": False, "lmax_attr": 1}
+    assert ds.cached_folder_name == hashlib.sha256(json.dumps(ref, sort_keys=True).encode()).hexdigest()
+    files = os.listdir(tmp_path / "saved_simulations" / ds.cached_folder_name)
+    assert files == ["0.pkl"]
+
+
+def test_cache_roundtrip_and_getitem_targets(tmp_path, fake_sim):
+    kw = dict(batch_size=2, sim_length=50, num_nodes=4, device="cpu", data_path=str(tmp_path / "s"))
+    ds = D.GravityDatasetOtf(**kw)                       # generates + caches 0.pkl
+    ds2 = D.GravityDatasetOtf(use_cached=True, **kw)     # loads it back through the restricted unpickler
+    assert len(fake_sim) == 1
+    a, b = ds.data_queue[0], ds2.data_queue[0]
+    for ta, tb in zip(a, b):
+        for xa, xb in zip(ta, tb):
+            np.testing.assert_array_equal(xa, xb)
+    import random
+    random.seed(3)
+    loc, vel, force, mass, y = ds2[0]
+    assert loc.shape == (2, 4, 3) and mass.shape == (2, 4, 1) and y.shape == (2, 4, 6)
+    L = np.array([t[0] for t in b])
+    Vv = np.array([t[1] for t in b])
+    f0 = [f for f in range(4) if np.array_equal(L[:, f], loc.numpy())][0]
+    np.testing.assert_array_equal(y.numpy(), np.concatenate([L[:, f0 + 1] - L[:, f0], Vv[:, f0 + 1]], 2))
+    assert f0 not in ds2.unused_indices_queue[0]
+
+
+def test_cache_loader_refuses_code(tmp_path):
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("echo pwned",))
+    p = tmp_path / "0.pkl"
+    with open(p, "wb") as f:
+        pickle.dump([Evil()], f)
+    with pytest.raises(pickle.UnpicklingError):
+        D.load_cached_simulations(str(p))
+
+
+# ------------------------------------------------------------------ run_inference host logic
+def test_metadata_path_and_self_feed_error(tmp_path):
+    run = tmp_path / "2024-09-26_14-33-13" / "checkpoints" / "3"
+    run.mkdir(parents=True)
+    assert I.get_dataset_metadata_path(str(run)) == str(tmp_path / "2024-09-26_14-33-13" / "nbody_small_dataset"
+                                                        / "metadata.json")
+    with pytest.raises(FileNotFoundError):
+        I.get_dataset_metadata_path(str(tmp_path))
+    e = I.SelfFeedError(7)
+    assert e.steps_survived == 7 and isinstance(e, RuntimeError)
+    assert I.MACROS_DIR_NAME == "visualize_macros"
+
+
+class _ConstModel(torch.nn.Module):
+    """CPU stand-in exposing the rollout contract (pos += 0.1, vel = -vel)."""
+
+    def rollout(self, loc, vel, mass, T):
+        tp, tv = [loc], [vel]
+        for _ in range(T - 1):
+            tp.append(tp[-1] + 0.1)
+            tv.append(-tv[-1])
+        return torch.stack(tp, 1), torch.stack(tv, 1)
+
+
+def test_run_inference_layout(tmp_path, fake_sim):
+    ds = D.GravityDatasetOtf(batch_size=2, sim_length=60, num_nodes=3, device="cpu", data_path=str(tmp_path / "s"),
+                             double_precision=True)
+    out_dir, locs, vels = I.run_inference("segnn", None, model=_ConstModel(), save_dir=str(tmp_path / "o"),
+                                          device="cpu", max_rollout_steps=4, dataset=ds)
+    assert locs.shape == (2, 2, 4, 3, 3) and vels.shape == locs.shape and locs.dtype == np.float64
+    np.testing.assert_allclose(locs[1][:, 3] - locs[1][:, 0], 0.3)
+    np.testing.assert_array_equal(locs[0][:, 0], locs[1][:, 0])
+    names = sorted(os.listdir(out_dir))
+    assert names == sorted(f"{k}_{w}_sim_{i}.npy" for k in ("loc", "vel") for w in ("actual", "pred")
+                           for i in range(2))
+    np.testing.assert_array_equal(np.load(os.path.join(out_dir, "loc_pred_sim_1.npy")), locs[1][1])
+    with pytest.raises(ValueError):
+        I.run_inference("painn", None, model=_ConstModel(), dataset=ds, device="cpu")
+
+
+def test_energy_oracle_small_case():
+    loc = np.array([[[[0, 0, 0], [3, 4, 0]]]], dtype=float)
+    vel = np.array([[[[1, 0, 0], [0, 2, 0]]]], dtype=float)
+    e = oracle_energies(loc, vel, G=2.0, softening=0.0)
+    assert e["kinetic"][0] == pytest.approx(2.5) and e["potential"][0] == pytest.approx(-2.0 / 5.0)
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_gpu_energies_match_oracle(hip_device):
+    rng = np.random.default_rng(0)
+    loc, vel = rng.standard_normal((6, 11, 7, 3)), rng.standard_normal((6, 11, 7, 3))
+    got = I.nbody_energies(loc, vel, 2.0, 0.2, hip_device)
+    ref = oracle_energies(loc, vel, 2.0, 0.2)
+    for k in ("potential", "kinetic", "total"):
+        np.testing.assert_allclose(got[k], ref[k], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_trajectory_batch_equals_single_trajectories(hip_device):
+    from nbody_amd.gravity import GravitySim
+    sim = GravitySim(n_balls=5, interaction_strength=2, dt=0.01, softening=0.2, device=hip_device)
+    batch = sim.sample_trajectory_batch(3, 200, 10, seeds=[4, 5, 6])
+    for s, traj in zip([4, 5, 6], batch):
+        single = sim.sample_trajectory(200, 10, random_seed=s)
+        for a, b in zip(traj, single):
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_self_feed_cli_through_registry(hip_device, tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    from nbody_amd.self_feed import main
+    s = main(["--limit_steps", "5", "--save_dir", str(tmp_path / "sf"), "--model_type", "segnn",
+              "--dataloader_type", "segnn_nbody", "--model.hidden_features", "32", "--model.num_layers", "2",
+              "--dataloader.batch_size", "4"])
+    assert s["steps_survived"] == 4
+    assert np.isfinite(s["energy_drift_self_feed"])
+    files = os.listdir(tmp_path / "sf" / "checkpoints" / "1" / "trajectories_data")
+    assert len(files) == 16
