@@ -1,18 +1,25 @@
 #!/usr/bin/env python
 """Headline benchmark: SEGNN self-feed rollout steps/sec (BASELINE.json, config C2).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model segnn|ponita|egnn_mc|gravity]
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
-Workload (per rank): SEGNN lmax_h=1, hidden_features=192, 6 layers, N=5 bodies,
-batch B=1024 systems, fp32, train-mode BatchNorm (the reference rollout never
-calls model.eval()).  A "step" = one self-feed model step for the whole batch:
-featurise -> SEGNN forward -> state update -> trajectory frame write, all
-device-resident (infer_self_feed.py:99-194).  Initial states = frame 0 of
-GravitySim(N=5) trajectories with seeds rank*B .. rank*B+B-1; weights from
-torch.manual_seed(0).  Multi-GPU: every rank runs its own B=1024 batch (the
-reference configuration, BatchNorm statistics per rank), "weak" scaling; the
+Default (the driver's line) — C2: SEGNN lmax_h=1, hidden_features=192, 6 layers,
+N=5 bodies, batch B=1024 systems per rank, fp32, train-mode BatchNorm (the
+reference rollout never calls model.eval()).  A "step" = one self-feed model step
+for the whole batch: featurise -> SEGNN forward -> state update -> trajectory
+frame write, all device-resident (infer_self_feed.py:99-194).  Initial states =
+frame 0 of GravitySim(N=5) trajectories with seeds rank*B .. rank*B+B-1; weights
+from torch.manual_seed(0).  Multi-GPU: every rank runs its own B=1024 batch (the
+reference configuration; BatchNorm statistics per rank), "weak" scaling; the
 final states are all-gathered over RCCL inside the timed region.
+
+Secondary configurations (not the headline; same JSON shape):
+  --model ponita   C3: PONITA hidden 128, 6 layers, 20 orientations, basis 128, N=5,
+                   global batch 4096 sharded over the ranks ("strong" scaling).
+  --model egnn_mc  C1: EGNN-MC 6 x 128, N=5, batch 64 per rank ("weak").
+  --model gravity  C5: ground-truth integrator, 10 000 systems x N=100, --steps
+                   KDK steps (sample_freq 10), systems sharded over the ranks ("strong").
 
 Prints ONE JSON line (rank 0).
 """
@@ -33,6 +40,7 @@ sys.path.insert(0, ROOT)
 HIDDEN, LAYERS, NBODY, BATCH = 192, 6, 5, 1024
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+FP64_VALU_PEAK_TFLOPS = 78.6           # MI355X spec; no f64 MFMA used by the integrator
 SURVEY_GFLOP_PER_STEP = 67.73          # algorithmic work of the reference formulation
 
 
@@ -47,7 +55,24 @@ def initial_states(B, N, seed0):
     return loc, vel, np.ones((B, N, 1))
 
 
-def cpu_baseline(loc, vel, mass, steps=1):
+def blas_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def timed_region(fn, device, P):
+    """barrier + sync on both sides, MAX over ranks."""
+    torch.cuda.synchronize(device)
+    P.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    out = fn()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    return out, P.max_over_ranks(elapsed, device)
+
+
+# ---------------------------------------------------------------- C2 SEGNN (headline)
+def cpu_baseline_segnn(loc, vel, mass, steps=1):
     """The CPU oracle (numpy fp64 restatement of the reference SEGNN path) timed on
     the host cores on a bounded sample: `steps` self-feed steps of the full B=1024
     batch."""
@@ -58,67 +83,37 @@ def cpu_baseline(loc, vel, mass, steps=1):
     t0 = time.perf_counter()
     rollout(segnn_step(om, params), loc, vel, np.zeros_like(loc), mass, steps + 1)
     dt = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = blas_threads()
     return {"value": steps / dt, "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": f"{steps} self-feed step(s) of the B={loc.shape[0]} N={loc.shape[1]} batch, numpy fp64 oracle "
                       f"(oracle/segnn.py), BLAS threads={threads}, {dt:.2f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=BATCH)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=1)
-    a = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local)
-
+def bench_segnn(a, rank, world, device, P):
     import nbody_amd.segnn as S
     from nbody_amd import _lib
 
-    B, N = a.batch, NBODY
+    B, N = a.batch or BATCH, NBODY
     torch.manual_seed(0)
     model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS, lmax_h=1).to(device).float().train()
     loc, vel, mass = initial_states(B, N, rank * B)
     loc_d = torch.tensor(loc, dtype=torch.float32, device=device)
     vel_d = torch.tensor(vel, dtype=torch.float32, device=device)
     mass_d = torch.tensor(mass, dtype=torch.float32, device=device)
-
-    # warmup (also packs weights / allocates the workspace)
-    if a.warmup > 0:
+    if a.warmup > 0:  # also packs weights / allocates the workspace
         model.rollout(loc_d, vel_d, mass_d, a.warmup + 1)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
-    final = torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous()
-    if dist:
-        gathered = [torch.empty_like(final) for _ in range(world)]
-        dist.all_gather(gathered, final)
-    torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    def work():
+        tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
+        final = torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous()
+        P.all_gather_shards(final)
+        return tp
+    tp, elapsed = timed_region(work, device, P)
     finite = bool(torch.isfinite(tp).all().item())
 
     # live roofline of the dominant kernel: HIP events around every launch of the
     # fused tensor-product kernels of a few forwards, on the launch stream, split by kind
-    V, M = B * N, model.mul
+    V = B * N
     p32 = loc_d.reshape(-1, 3).contiguous()
     v32 = vel_d.reshape(-1, 3).contiguous()
     m32 = mass_d.reshape(-1).contiguous()
@@ -147,34 +142,20 @@ def main():
         if n_k[k]:
             avg_s = ms_k[k] / n_k[k] / 1e3
             fl = fl_k[k] / n_k[k]
-            per_kind[names[k]] = {"role": roles[k], "avg_launch_us": round(avg_s * 1e6, 3), "gflop_per_launch": round(fl / 1e9, 4),
-                                  "tflops": round(fl / avg_s / 1e12, 3), "share_of_forward": round(ms_k[k] / fwd_ms, 3)}
+            per_kind[names[k]] = {"role": roles[k], "avg_launch_us": round(avg_s * 1e6, 3),
+                                  "gflop_per_launch": round(fl / 1e9, 4), "tflops": round(fl / avg_s / 1e12, 3),
+                                  "share_of_forward": round(ms_k[k] / fwd_ms, 3)}
     dom = max(range(4), key=lambda k: ms_k[k])
     dom_avg_s = ms_k[dom] / n_k[dom] / 1e3
     dom_flops = fl_k[dom] / n_k[dom]
     achieved_tflops = dom_flops / dom_avg_s / 1e12
-    fused_share = sum(ms_k) / fwd_ms
-
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_tp_kernels.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f)["kernels"].get(names[dom], {}).get("hbm_bytes_per_launch")
-
-    steps_per_s_rank = a.steps / elapsed
-    value = steps_per_s_rank * world
+    traffic = pmc_traffic(names[dom])
+    value = a.steps / elapsed * world
     result = {
         "metric": "self-feed rollout steps/sec, SEGNN N=5 batch=1024",
-        "value": round(value, 3),
-        "unit": "steps/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(1e3 * elapsed / a.steps, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "fp32",
+        "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights)",
         "config": {"workload": "C2: SEGNN lmax_h=1 hidden=192 layers=6, N=5, batch=1024 per GPU, self-feed rollout",
                    "model": "SEGNN", "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}",
@@ -185,15 +166,251 @@ def main():
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                      "avg_launch_us": round(dom_avg_s * 1e6, 3), "gflop_per_launch": round(dom_flops / 1e9, 4),
-                     "fused_tp_share_of_forward": round(fused_share, 3), "per_kind": per_kind},
+                     "fused_tp_share_of_forward": round(sum(ms_k) / fwd_ms, 3), "per_kind": per_kind},
         "finite": finite,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(loc, vel, mass, a.cpu_steps)
+        result["cpu_baseline"] = cpu_baseline_segnn(loc, vel, mass, a.cpu_steps)
+    return result
+
+
+def pmc_traffic(kernel_name):
+    pmc = os.path.join(ROOT, "profiles", "pmc_tp_kernels.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            return json.load(f)["kernels"].get(kernel_name, {}).get("hbm_bytes_per_launch")
+    return None
+
+
+# ---------------------------------------------------------------- C3 PONITA
+PONITA_KIND_NAMES = ["void nbx::lin_kernel<4, 0, 1>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0>(nbx::LinProb)",
+                     "void nbx::lin_kernel<2, 0, 0>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0>(nbx::LinProb)",
+                     "void (anonymous namespace)::po_fiber_ln_kernel<20, 4>(...)"]
+PONITA_KIND_ROLES = ["FiberBundleConv spatial kernel GEMM + gather/aggregate epilogue", "ConvNext linear_1 + GELU",
+                     "ConvNext linear_2 + layer_scale + residual", "kernel basis MLP (2 GEMMs)",
+                     "fibre conv + bias + LayerNorm"]
+
+
+def bench_ponita(a, rank, world, device, P):
+    from nbody_amd import _lib
+    from nbody_amd.ponita import PONITA_NBODY
+
+    B_glob, N = a.batch or 4096, 5
+    start, B = P.shard_range(B_glob, rank, world)
+    torch.manual_seed(0)
+    model = PONITA_NBODY(hidden_dim=128, layers=6, num_ori=20, basis_dim=128, degree=3).to(device)
+    loc, vel, mass = initial_states(B, N, start)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    loc_d, vel_d, mass_d = t(loc), t(vel), t(mass)
+    model.rollout(loc_d, vel_d, mass_d, max(a.warmup, 1) + 1)     # includes the one-time calibration
+
+    def work():
+        tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
+        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous(), B_glob)
+        return tp
+    tp, elapsed = timed_region(work, device, P)
+    finite = bool(torch.isfinite(tp).all().item())
+
+    W = model._weights(device)
+    ws = model._workspace(W, B, N, device)
+    p32, v32, m32 = loc_d.reshape(-1, 3), vel_d.reshape(-1, 3), mass_d.reshape(-1)
+    out = torch.empty(B * N, 6, device=device)
+    kms, kn, kfl, kby, tot = (_lib.c_f * 8)(), (_lib.c_i32 * 8)(), (_lib.c_d * 8)(), (_lib.c_d * 8)(), _lib.c_f()
+    acc = np.zeros((4, 8))
+    fwd = 0.0
+    for _ in range(3):
+        _lib.check(_lib.lib().nbx_ponita_forward_timed(W, _lib.dev_ptr(p32), _lib.dev_ptr(v32), _lib.dev_ptr(m32),
+                                                       B, N, _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
+                                                       _lib.stream_ptr(device), kms, kn, kfl, kby, tot),
+                   "nbx_ponita_forward_timed")
+        acc += np.array([list(kms), list(kn), list(kfl), list(kby)])
+        fwd += tot.value
+    per_kind = {}
+    for k in range(5):
+        if acc[1, k]:
+            s = acc[0, k] / acc[1, k] / 1e3
+            per_kind[PONITA_KIND_ROLES[k]] = {
+                "kernel": PONITA_KIND_NAMES[k], "avg_launch_us": round(s * 1e6, 2),
+                "tflops": round(acc[2, k] / acc[1, k] / s / 1e12, 3),
+                "gbs": round(acc[3, k] / acc[1, k] / s / 1e9, 1), "share_of_forward": round(acc[0, k] / fwd, 3)}
+    dom = max(range(5), key=lambda k: acc[0, k])
+    dom_s = acc[0, dom] / acc[1, dom] / 1e3
+    if dom == 4:
+        ach = acc[3, dom] / acc[1, dom] / dom_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4)}
+    else:
+        ach = acc[2, dom] / acc[1, dom] / dom_s / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
+    roof.update({"traffic": pmc_traffic(PONITA_KIND_NAMES[dom]), "kernel": PONITA_KIND_NAMES[dom],
+                 "role": PONITA_KIND_ROLES[dom], "avg_launch_us": round(dom_s * 1e6, 2), "per_kind": per_kind})
+    value = a.steps / elapsed
+    result = {
+        "metric": "self-feed rollout steps/sec, PONITA N=5 batch=4096", "value": round(value, 3), "unit": "steps/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights, calibrated)",
+        "config": {"workload": "C3: PONITA hidden=128 layers=6 num_ori=20 basis_dim=128 degree=3, N=5, "
+                               f"global batch {B_glob} sharded over {world} GPU(s)", "model": "PONITA",
+                   "global_batch": B_glob, "seq_len": a.steps, "parallelism": f"dp{world}"},
+        "trajectory_steps_per_s": round(value * B_glob, 1),
+        "algorithmic_tflops": round(value * fwd_flops(acc) / 1e12, 3),
+        "roofline": roof, "finite": finite}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_ponita(model, B_glob)
+    return result
+
+
+def fwd_flops(acc):
+    n_fwd = 3
+    return acc[2, :5].sum() / n_fwd
+
+
+def cpu_baseline_ponita(model, B_glob, B_s=64):
+    from oracle import ponita as op
+    from oracle.graph import fc_edge_index
+    params = {k: v.double().cpu().numpy() for k, v in model.state_dict().items()}
+    grid = model.model.ori_grid.double().cpu().numpy()
+    loc, vel, mass = initial_states(B_s, 5, 0)
+    pos, v, m = loc.reshape(-1, 3), vel.reshape(-1, 3), mass.reshape(-1, 1)
+    ei = fc_edge_index(B_s, 5)
+    t0 = time.perf_counter()
+    op.forward(params, m, v[:, None, :], ei, pos[ei[0]] - pos[ei[1]], grid, 6)
+    dt = time.perf_counter() - t0
+    threads = blas_threads()
+    return {"value": 1.0 / (dt * B_glob / B_s), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"1 forward of B={B_s} systems with the numpy fp64 oracle (oracle/ponita.py), {dt:.2f} s, "
+                      f"scaled x{B_glob // B_s} to the B={B_glob} batch; BLAS threads={threads}"}
+
+
+# ---------------------------------------------------------------- C1 EGNN-MC
+def bench_egnn(a, rank, world, device, P):
+    from nbody_amd.egnn_mc import EGNNMultiChannel
+    B, N = a.batch or 64, 5
+    torch.manual_seed(0)
+    model = EGNNMultiChannel(node_input_dim=2, edge_attr_dim=4, hidden_node_dim=128, hidden_edge_dim=128,
+                             hidden_coord_dim=128, num_layers=6, target_names=("pos_dt", "vel"), norm_diff=True,
+                             tanh=True, device=device)
+    loc, vel, mass = initial_states(B, N, rank * B)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    loc_d, vel_d, mass_d = t(loc), t(vel), t(mass)
+    model.rollout(loc_d, vel_d, mass_d, max(a.warmup, 1) + 1)
+
+    def work():
+        tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
+        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
+        return tp
+    tp, elapsed = timed_region(work, device, P)
+    value = a.steps / elapsed * world
+    result = {
+        "metric": "self-feed rollout steps/sec, EGNN-MC N=5 batch=64", "value": round(value, 3), "unit": "steps/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights)",
+        "config": {"workload": "C1: EGNN-MC 6 x 128, norm_diff, tanh, N=5, batch 64 per GPU", "model": "EGNN-MC",
+                   "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "launch", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                     "note": "C1 is launch/latency bound (SURVEY §8d): ~60 launches per step on 1280 edges"},
+        "finite": bool(torch.isfinite(tp).all().item())}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle.rollout import egnn_mc_step, rollout
+        params = {k: v.double().cpu().numpy() for k, v in model.state_dict().items()}
+        steps = 20
+        t0 = time.perf_counter()
+        rollout(egnn_mc_step(params, 6), loc, vel, np.zeros_like(loc), mass, steps + 1)
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": steps / dt, "unit": "steps/s", "cores": blas_threads(), "kind": "port",
+                                  "sample": f"{steps} self-feed steps of the B={B} batch, numpy fp64 oracle "
+                                            f"(oracle/egnn_mc.py), {dt:.2f} s"}
+    return result
+
+
+# ---------------------------------------------------------------- C5 integrator
+def bench_gravity(a, rank, world, device, P):
+    from nbody_amd.gravity import GravitySim
+    S_glob, N, freq = a.batch or 10000, 100, 10
+    T = max(freq, a.steps - a.steps % freq)
+    start, S = P.shard_range(S_glob, rank, world)
+    sim = GravitySim(n_balls=N, interaction_strength=2, dt=0.01, softening=0.2, device=device)
+    rng = np.random.default_rng(start)
+    pos = rng.standard_normal((S, N, 3)) * np.cbrt(N / 5)
+    vel = rng.standard_normal((S, N, 3))
+    vel -= vel.mean(1, keepdims=True)
+    mass = np.ones((S, N, 1))
+    sim.sample_trajectories(pos, vel, mass, max(freq, a.warmup - a.warmup % freq), freq)
+
+    def work():
+        ps, vs, fs = sim.sample_trajectories(pos, vel, mass, T, freq)
+        P.all_gather_shards(ps[:, -1].contiguous(), S_glob)
+        return ps
+    ps, elapsed = timed_region(work, device, P)
+    inter = float(S_glob) * N * N * T
+    flops = 23.0 * inter        # per pair: 3 sub, 3 fma (r2), +eps, sqrt, mul, div, 3 fma (acc) ~ 23 FP64 ops
+    ach = flops / elapsed / world / 1e12
+    result = {
+        "metric": "ground-truth integrator steps/sec, 10000 systems x N=100", "value": round(T / elapsed, 3),
+        "unit": "steps/s", "n_gpus": world, "steps": T, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / T, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (GravitySim-style initial conditions)",
+        "config": {"workload": f"C5: GravitySim KDK, {S_glob} systems x N={N}, dt=0.01, G=2, softening=0.2, "
+                               f"sample_freq={freq}", "model": "GravitySim", "global_batch": S_glob, "seq_len": T,
+                   "parallelism": f"dp{world}"},
+        "pair_interactions_per_s": round(inter / elapsed, 1),
+        "roofline": {"bound": "valu_f64", "achieved": round(ach, 3), "peak": FP64_VALU_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(ach / FP64_VALU_PEAK_TFLOPS, 4), "traffic": None,
+                     "flops_per_pair": 23},
+        "finite": bool(torch.isfinite(ps).all().item())}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_gravity(T, freq, S_glob)
+    return result
+
+
+def cpu_baseline_gravity(T, freq, S_glob, S_s=4, T_s=2000):
+    import ctypes
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "liboracle_gravity.so"))
+    N = 100
+    rng = np.random.default_rng(0)
+    pos = rng.standard_normal((S_s, N, 3))
+    vel = rng.standard_normal((S_s, N, 3))
+    mass = np.ones((S_s, N))
+    outs = [np.zeros((S_s, T_s // freq, N, 3)) for _ in range(3)]
+    Pp = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    t0 = time.perf_counter()
+    lib.oracle_gravity_sample(ctypes.c_int64(S_s), ctypes.c_int64(N), ctypes.c_int64(T_s), ctypes.c_int64(freq),
+                              ctypes.c_double(0.01), ctypes.c_double(2.0), ctypes.c_double(0.2), Pp(pos), Pp(vel),
+                              Pp(mass), *[Pp(o) for o in outs])
+    dt = time.perf_counter() - t0
+    return {"value": T_s / (dt * S_glob / S_s), "unit": "steps/s", "cores": 1, "kind": "port",
+            "sample": f"{S_s} systems x {T_s} steps with the C oracle (oracle/gravity.c, 1 core), {dt:.2f} s, "
+                      f"scaled to {S_glob} systems"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--model", default="segnn", choices=["segnn", "ponita", "egnn_mc", "gravity"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    a = ap.parse_args()
+    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "gravity": (1000, 100)}
+    a.steps = a.steps if a.steps is not None else defaults[a.model][0]
+    a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
+
+    from nbody_amd import parallel as P
+    rank, world, device = P.init_from_env()
+    fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "gravity": bench_gravity}[a.model]
+    result = fn(a, rank, world, device, P)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if dist:
-        dist.barrier()
+    P.barrier()
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

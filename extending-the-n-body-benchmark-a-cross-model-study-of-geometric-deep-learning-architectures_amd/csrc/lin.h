@@ -159,24 +159,29 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
         }
         // ---- epilogue: col = n0 + 32 j + r; row = rt*32 + (e&3) + 8(e>>2) + 4h
         if constexpr (EPI == LIN_CONV) {
-            const int G = P.conv_G, O = P.conv_O;
+            const int G = P.conv_G, O = P.conv_O, NN = P.conv_nodes;
+            // gathered source row offset of each accumulator row (-1: padded slot / past the end),
+            // shared by all NT column sub-tiles
+            int xoff[16];  // host guarantees V*O*ldx < 2^31
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int q = row & (G - 1), dq = row / G, d = dq / O, o = dq - d * O;
+                const int dl = d % NN;
+                xoff[e] = (row < P.rows && q < NN - 1)
+                              ? ((d - dl + (q < dl ? q : q + 1)) * O + o) * P.conv_ldx
+                              : -1;
+            }
 #pragma unroll
             for (int j = 0; j < NT; ++j) {
                 const int col = n0 + 32 * j + r;
                 const bool live = col < P.N;
+                float xv[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) xv[e] = (live && xoff[e] >= 0) ? P.conv_x[xoff[e] + col] : 0.f;
                 float m[16];
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                    const int q = row % G, dq = row / G, d = dq / O, o = dq - d * O;
-                    float v = 0.f;
-                    if (live && row < P.rows && q < P.conv_nodes - 1) {
-                        const int dl = d % P.conv_nodes;
-                        const int64_t src = (int64_t)(d - dl) + (q < dl ? q : q + 1);
-                        v = acc[j][e] * P.conv_x[((size_t)src * O + o) * P.conv_ldx + col];
-                    }
-                    m[e] = v;
-                }
+                for (int e = 0; e < 16; ++e) m[e] = acc[j][e] * xv[e];
                 auto put = [&](int row, float a) {
                     if (live && row < P.rows) P.Y[(size_t)(row / G) * P.ldy + col] = a;
                 };

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "launch_timer.h"
 #include "lin.h"
 #include "nbx_internal.h"
 #include "rollout_state.h"
@@ -126,61 +127,75 @@ __global__ void po_moments_kernel(const float* __restrict__ x, int64_t n, double
     }
 }
 
-// Depthwise fibre convolution + conv bias + LayerNorm (convnext.py:18-19):
-//   y[d,p,c] = sum_o X1[d,o,c] * FK[o,p,c] / O + bias[c];  XN = LN_c(y)
-// Thread (p, 4 channels) keeps FK[:, p, c..c+3] in registers for all nodes it visits;
-// the C/4 lanes of one p reduce the LayerNorm moments with shuffles.
-__global__ __launch_bounds__(768) void po_fiber_ln_kernel(const float* __restrict__ X1, const float* __restrict__ FK,
-                                                           int ldfk, const float* __restrict__ cbias,
-                                                           const float* __restrict__ nw, const float* __restrict__ nb,
-                                                           int64_t V, int O, int C, float* __restrict__ XN,
-                                                           double* __restrict__ mom) {
+// Depthwise fibre convolution + conv bias + LayerNorm (conv.py:121-124, convnext.py:18):
+//   y[d,p,c] = sum_o X1[d,o,c] * FK[o,p,c] / O + bias[c];  XN[d,p] = LN_c(y[d,p])
+// Block (x: node groups, y: orientation range [p0, p0+PR)) keeps FK[:, p0:p0+PR, :] in LDS.
+// A thread owns (node, 4 channels): it loads X1[d, :, c..c+3] once (coalesced rows) and
+// produces its channels of every p in the range; the C/4 lanes of a node reduce the
+// LayerNorm moments with shuffles.  X1 is re-read once per orientation range (O/PR times,
+// from L2 / MALL), FK never leaves LDS.
+constexpr int PO_FIB_THREADS = 512;
+
+template <int OMAX, int MINW>
+__global__ __launch_bounds__(PO_FIB_THREADS, MINW) void po_fiber_ln_kernel(
+    const float* __restrict__ X1, const float* __restrict__ FK, int ldfk, const float* __restrict__ cbias,
+    const float* __restrict__ nw, const float* __restrict__ nb, int64_t V, int O, int C, int PR,
+    float* __restrict__ XN, double* __restrict__ mom) {
+    extern __shared__ __attribute__((aligned(16))) float fks[];
     __shared__ double red[16];
-    const int CG = C >> 2;
-    const int t = threadIdx.x, p = t / CG, cg = t - p * CG, c = 4 * cg;
-    const bool active = p < O;
-    float4 fk[PO_OMAX];
-#pragma unroll
-    for (int o = 0; o < PO_OMAX; ++o)
-        fk[o] = (active && o < O) ? *reinterpret_cast<const float4*>(FK + (size_t)(o * O + p) * ldfk + c)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 cb = active ? *reinterpret_cast<const float4*>(cbias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 w4 = active ? *reinterpret_cast<const float4*>(nw + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 b4 = active ? *reinterpret_cast<const float4*>(nb + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int CG = C >> 2, npi = PO_FIB_THREADS / CG;
+    const int t = threadIdx.x, ns = t / CG, cg = t - ns * CG, c = 4 * cg;
+    const int p0 = blockIdx.y * PR, pn = min(PR, O - p0);
+    // FK slice -> LDS [o][pl][C]
+    for (int i = t; i < O * pn * CG; i += PO_FIB_THREADS) {
+        const int o = i / (pn * CG), r = i - o * pn * CG, pl = r / CG, q = r - pl * CG;
+        *reinterpret_cast<float4*>(&fks[(o * PR + pl) * C + 4 * q]) =
+            *reinterpret_cast<const float4*>(FK + (size_t)(o * O + p0 + pl) * ldfk + 4 * q);
+    }
+    __syncthreads();
+    const float4 cb = *reinterpret_cast<const float4*>(cbias + c);
+    const float4 w4 = *reinterpret_cast<const float4*>(nw + c);
+    const float4 b4 = *reinterpret_cast<const float4*>(nb + c);
     const float invO = 1.0f / (float)O, invC = 1.0f / (float)C;
     double s1 = 0.0, s2 = 0.0;
-    for (int64_t d = blockIdx.x; d < V; d += gridDim.x) {
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (active) {
-            const float* x1 = X1 + (size_t)d * O * C + c;
+    for (int64_t d0 = (int64_t)blockIdx.x * npi; d0 < V; d0 += (int64_t)gridDim.x * npi) {
+        const int64_t d = d0 + ns;
+        const bool active = d < V;
+        float4 x[OMAX];
+        const float* x1 = X1 + (size_t)(active ? d : 0) * O * C + c;
 #pragma unroll
-            for (int o = 0; o < PO_OMAX; ++o) {
+        for (int o = 0; o < OMAX; ++o)
+            x[o] = (o < O) ? *reinterpret_cast<const float4*>(x1 + (size_t)o * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int pl = 0; pl < pn; ++pl) {
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int o = 0; o < OMAX; ++o) {
                 if (o < O) {
-                    const float4 x = *reinterpret_cast<const float4*>(x1 + (size_t)o * C);
-                    a.x += x.x * fk[o].x;
-                    a.y += x.y * fk[o].y;
-                    a.z += x.z * fk[o].z;
-                    a.w += x.w * fk[o].w;
+                    const float4 f = *reinterpret_cast<const float4*>(&fks[(o * PR + pl) * C + c]);
+                    a.x += x[o].x * f.x;
+                    a.y += x[o].y * f.y;
+                    a.z += x[o].z * f.z;
+                    a.w += x[o].w * f.w;
                 }
             }
+            a.x *= invO; a.y *= invO; a.z *= invO; a.w *= invO;
+            if (mom && active) {
+                s1 += (double)a.x + (double)a.y + (double)a.z + (double)a.w;
+                s2 += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+            }
+            const float y0 = a.x + cb.x, y1 = a.y + cb.y, y2 = a.z + cb.z, y3 = a.w + cb.w;
+            float s = y0 + y1 + y2 + y3;
+            for (int off = CG >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off);
+            const float mu = s * invC;
+            const float e0 = y0 - mu, e1 = y1 - mu, e2 = y2 - mu, e3 = y3 - mu;
+            float v = e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+            for (int off = CG >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            const float rs = 1.0f / sqrtf(v * invC + 1e-5f);
+            if (active)
+                *reinterpret_cast<float4*>(XN + ((size_t)d * O + p0 + pl) * C + c) =
+                    make_float4(e0 * rs * w4.x + b4.x, e1 * rs * w4.y + b4.y, e2 * rs * w4.z + b4.z,
+                                e3 * rs * w4.w + b4.w);
         }
-        a.x *= invO; a.y *= invO; a.z *= invO; a.w *= invO;
-        if (mom && active) {
-            s1 += (double)a.x + (double)a.y + (double)a.z + (double)a.w;
-            s2 += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
-        }
-        const float y0 = a.x + cb.x, y1 = a.y + cb.y, y2 = a.z + cb.z, y3 = a.w + cb.w;
-        float s = y0 + y1 + y2 + y3;
-        for (int off = CG >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        const float mu = s * invC;
-        const float e0 = y0 - mu, e1 = y1 - mu, e2 = y2 - mu, e3 = y3 - mu;
-        float v = e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
-        for (int off = CG >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        const float rs = 1.0f / sqrtf(v * invC + 1e-5f);
-        if (active)
-            *reinterpret_cast<float4*>(XN + ((size_t)d * O + p) * C + c) =
-                make_float4(e0 * rs * w4.x + b4.x, e1 * rs * w4.y + b4.y, e2 * rs * w4.z + b4.z,
-                            e3 * rs * w4.w + b4.w);
     }
     if (mom) {
         s1 = block_sum_double(s1, red);
@@ -294,12 +309,18 @@ int lin_auto(nbx::LinProb& p, hipStream_t st) {
     return nbx::lin_launch<1, ACT, EPI>(p, st);
 }
 
+// launch kinds of nbx_ponita_forward_timed
+enum PoKind : int { PK_CONV = 0, PK_LIN1 = 1, PK_LIN2 = 2, PK_BASIS = 3, PK_FIBER = 4 };
+
 int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* vel, const float* mass,
-                    const PoDims& d, float* out, double* mom, const PoWs& ws, hipStream_t st) {
+                    const PoDims& d, float* out, double* mom, const PoWs& ws, hipStream_t st,
+                    nbx::LaunchTimer* tm = nullptr) {
     using nbx::LinProb;
     const int O = d.O, C = d.C, Bk = d.Bk, L = d.L;
     const int64_t VO = d.V * O;
     const int OO = O * O;
+    const double Ev = (double)VO * (double)(d.N - 1);  // real (edge, orientation) rows
+    const double f4 = 4.0;
     // ---- invariants, kernel bases (shared by all layers), lift
     hipLaunchKernelGGL(po_attr_kernel, dim3(g1(d.R)), dim3(256), 0, st, pos, w->ori_grid, d.R, (int)d.N, O, (int)d.G,
                        ws.P16);
@@ -309,9 +330,13 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
     NBX_LAUNCH_CHECK("ponita prep");
     {
         LinProb p = nbx::lin_dense(ws.P16, 16, 16, (int)d.R, w->basis1_t, 32, C, w->basis1_b, ws.B1H1, C);
-        if (int rc = lin_auto<nbx::ACT_GELU>(p, st)) return rc;
+        if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * 14 * C, Ev * f4 * (16 + C),
+                                [&] { return lin_auto<nbx::ACT_GELU>(p, st); }))
+            return rc;
         LinProb q = nbx::lin_dense(ws.B1H1, C, C, (int)d.R, w->basis2_t, kp(C), Bk, w->basis2_b, ws.KB, Bk);
-        if (int rc = lin_auto<nbx::ACT_GELU>(q, st)) return rc;
+        if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * C * Bk, Ev * f4 * (C + Bk),
+                                [&] { return lin_auto<nbx::ACT_GELU>(q, st); }))
+            return rc;
         LinProb f1 = nbx::lin_dense(ws.FP, 4, 4, OO, w->fbasis1_t, 32, C, w->fbasis1_b, ws.FB1, C);
         if (int rc = lin_auto<nbx::ACT_GELU>(f1, st)) return rc;
         LinProb f2 = nbx::lin_dense(ws.FB1, C, C, OO, w->fbasis2_t, kp(C), Bk, w->fbasis2_b, ws.FKB, Bk);
@@ -332,25 +357,40 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             p.conv_nodes = (int)d.N;
             p.conv_x = ws.X;
             p.conv_ldx = C;
-            if (int rc = lin_auto<nbx::ACT_NONE, nbx::LIN_CONV>(p, st)) return rc;
+            if (int rc = nbx::timed(tm, st, PK_CONV, 2.0 * Ev * Bk * C + 2.0 * Ev * C,
+                                    Ev * f4 * Bk + (double)VO * C * f4 * 2,
+                                    [&] { return lin_auto<nbx::ACT_NONE, nbx::LIN_CONV>(p, st); }))
+                return rc;
         }
         if (mom)
             hipLaunchKernelGGL(po_moments_kernel, dim3(512), dim3(256), 0, st, ws.X1, VO * C, mom + 6 * l + 2);
         {
-            const int threads = ((O * (C / 4) + 63) / 64) * 64;
-            const int grid = (int)std::min<int64_t>(d.V, 2048);
-            hipLaunchKernelGGL(po_fiber_ln_kernel, dim3(grid), dim3(threads), 0, st, ws.X1, ws.FK + (size_t)l * C,
-                               L * C, Ly.conv_bias, Ly.norm_w, Ly.norm_b, d.V, O, C, ws.XN,
-                               mom ? mom + 6 * l + 4 : nullptr);
+            const int PR = std::max(1, std::min(O, (int)((64 * 1024) / ((size_t)O * C * 4))));
+            const int R = (O + PR - 1) / PR;
+            const int npi = PO_FIB_THREADS / (C / 4);
+            const int gx = (int)std::min<int64_t>((d.V + npi - 1) / npi, std::max(1, 1024 / R));
+            const size_t lds = (size_t)O * PR * C * 4;
+            auto kern = O <= 20 ? po_fiber_ln_kernel<20, 4> : po_fiber_ln_kernel<PO_OMAX, 2>;
+            if (int rc = nbx::timed(tm, st, PK_FIBER, 2.0 * VO * O * C, (double)VO * C * f4 * 2, [&] {
+                    hipLaunchKernelGGL(kern, dim3(gx, R), dim3(PO_FIB_THREADS), lds, st, ws.X1,
+                                       ws.FK + (size_t)l * C, L * C, Ly.conv_bias, Ly.norm_w, Ly.norm_b, d.V, O, C,
+                                       PR, ws.XN, mom ? mom + 6 * l + 4 : nullptr);
+                    return (int)NBX_OK;
+                }))
+                return rc;
         }
         {   // ConvNext MLP with the residual in the epilogue
             LinProb p = nbx::lin_dense(ws.XN, C, C, (int)VO, Ly.lin1_t, kp(C), d.mlp, Ly.lin1_b, ws.B1H1, d.mlp);
-            if (int rc = lin_auto<nbx::ACT_GELU>(p, st)) return rc;
+            if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * VO * C * d.mlp, (double)VO * f4 * (C + d.mlp),
+                                    [&] { return lin_auto<nbx::ACT_GELU>(p, st); }))
+                return rc;
             LinProb q = nbx::lin_dense(ws.B1H1, d.mlp, d.mlp, (int)VO, Ly.lin2_t, kp(d.mlp), C, Ly.lin2_b, ws.X, C);
             q.resid = ws.X;
             q.ldr = C;
             q.scale = Ly.layer_scale;
-            if (int rc = lin_auto<nbx::ACT_NONE>(q, st)) return rc;
+            if (int rc = nbx::timed(tm, st, PK_LIN2, 2.0 * VO * C * d.mlp, (double)VO * f4 * (d.mlp + 2 * C),
+                                    [&] { return lin_auto<nbx::ACT_NONE>(q, st); }))
+                return rc;
         }
         if (Ly.readout_w) {
             const int64_t thr = VO * (C / 4);
@@ -379,7 +419,8 @@ int po_prepare(const nbx_ponita_weights* w, int64_t B, int64_t N, void* ws_ptr, 
     NBX_CHECK_ARG(w->num_ori >= 1 && w->num_ori <= PO_OMAX, "ponita: num_ori must be 1..24");
     NBX_CHECK_ARG(B >= 1 && N >= 2 && N <= 33, "ponita: need B >= 1 and 2 <= N <= 33");
     *dims = po_dims(w, B, N);
-    NBX_CHECK_ARG(dims->R < ((int64_t)1 << 31), "ponita: B*N*num_ori*G exceeds 2^31 rows");
+    NBX_CHECK_ARG(dims->R < ((int64_t)1 << 31) && dims->V * dims->O * std::max(dims->C, dims->mlp) < ((int64_t)1 << 31),
+                  "ponita: B*N*num_ori*max(G, 4*hidden) exceeds 2^31");
     const size_t need = po_carve(ws, ws_ptr, *dims);
     if (!ws_ptr || bytes < need) {
         nbx::set_error("ponita: workspace too small (%zu < %zu bytes)", bytes, need);
@@ -403,6 +444,35 @@ extern "C" int nbx_ponita_forward(const nbx_ponita_weights* w, const float* pos,
     PoWs ws;
     if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
     return po_forward_impl(w, pos, vel, mass, d, out, calib_moments, ws, (hipStream_t)stream);
+}
+
+extern "C" int nbx_ponita_forward_timed(const nbx_ponita_weights* w, const float* pos, const float* vel,
+                                        const float* mass, int64_t B, int64_t N, float* out, void* workspace,
+                                        size_t workspace_bytes, void* stream, float kind_ms[8],
+                                        int32_t kind_launches[8], double kind_flops[8], double kind_bytes[8],
+                                        float* total_ms) {
+    PoDims d;
+    PoWs ws;
+    if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    nbx::LaunchTimer tm;
+    hipEvent_t a, b;
+    NBX_HIP(hipEventCreate(&a));
+    NBX_HIP(hipEventCreate(&b));
+    NBX_HIP(hipEventRecord(a, st));
+    int rc = po_forward_impl(w, pos, vel, mass, d, out, nullptr, ws, st, &tm);
+    NBX_HIP(hipEventRecord(b, st));
+    if (!rc) rc = tm.collect(kind_ms);
+    NBX_HIP(hipEventSynchronize(b));
+    NBX_HIP(hipEventElapsedTime(total_ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (int k = 0; k < 8; ++k) {
+        kind_launches[k] = tm.launches[k];
+        kind_flops[k] = tm.flops[k];
+        kind_bytes[k] = tm.bytes[k];
+    }
+    return rc;
 }
 
 extern "C" int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass, int64_t B,

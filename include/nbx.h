@@ -269,6 +269,15 @@ int nbx_ponita_forward(const nbx_ponita_weights* w, const float* pos, const floa
                        int64_t batch_size, int64_t num_nodes, float* out, double* calib_moments, void* workspace,
                        size_t workspace_bytes, void* stream);
 
+/* nbx_ponita_forward with HIP events around the main launches, on `stream`:
+ * per kind k (0 spatial conv, 1 ConvNext linear_1, 2 linear_2, 3 basis MLP,
+ * 4 fibre conv + LayerNorm) the summed kernel time, launch count and the
+ * algorithmic flops / bytes; total_ms = the whole forward. */
+int nbx_ponita_forward_timed(const nbx_ponita_weights* w, const float* pos, const float* vel, const float* mass,
+                             int64_t batch_size, int64_t num_nodes, float* out, void* workspace,
+                             size_t workspace_bytes, void* stream, float kind_ms[8], int32_t kind_launches[8],
+                             double kind_flops[8], double kind_bytes[8], float* total_ms);
+
 /* Device-resident self-feed rollout with the PONITA branch of
  * infer_self_feed.py:131-147,182-194; same contract as nbx_segnn_rollout. */
 int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,

@@ -31,12 +31,16 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--ponita_B", type=int, default=4096)
+    ap.add_argument("--only", default="ponita,egnn")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    torch.manual_seed(0)
-    m = PONITA_NBODY(hidden_dim=128, layers=6).to(dev)
-    m.eval()
-    run("ponita_C3", m, a.ponita_B, 5, a.frames, dev)
+    if "ponita" in a.only:
+        torch.manual_seed(0)
+        m = PONITA_NBODY(hidden_dim=128, layers=6).to(dev)
+        m.eval()
+        run("ponita_C3", m, a.ponita_B, 5, a.frames, dev)
+    if "egnn" not in a.only:
+        raise SystemExit(0)
     torch.manual_seed(0)
     e = EGNNMultiChannel(node_input_dim=2, edge_attr_dim=4, hidden_node_dim=128, hidden_edge_dim=128,
                          hidden_coord_dim=128, num_layers=6, target_names=("pos_dt", "vel"), norm_diff=True,
