@@ -19,6 +19,7 @@
 // The x_i / x_j halves of message_layer_1 are linear in node features, so they
 // are computed once per node (node_pre GEMM) and combined per edge.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -439,16 +440,16 @@ int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     return NBX_OK;
 }
 
-template <int NS, int NV, int EPI, int CG>
-int run_tp16(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
-    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG>(p, st);
+template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS>
+int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
     NBX_HIP(hipEventCreate(&b));
     tm->ev.push_back(a);
     tm->ev.push_back(b);
     NBX_HIP(hipEventRecord(a, st));
-    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG>(p, st)) return rc;
+    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st)) return rc;
     NBX_HIP(hipEventRecord(b, st));
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
@@ -457,6 +458,14 @@ int run_tp16(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     tm->flops[EPI] += 2.0 * p.rows * 16.0 * p.chunks * k;
     tm->launches[EPI] += 1;
     return NBX_OK;
+}
+
+// KS > 1 splits each row tile's K loop over KS waves of the block (partials folded through
+// LDS before the epilogue).  Measured on MI355X at C2: it pays only for update_layer_2
+// (30 -> 24 us); the other node TPs lose to the extra block rounds.
+template <int NS, int NV, int EPI, int CG, int KS = 1>
+int run_tp16(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    return run_tp16_w<NS, NV, EPI, CG, 8, 3, KS>(p, st, tm);
 }
 
 nbx::TpProb tp_base(int rows, const Dims& d) {
@@ -548,7 +557,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
             p.chunks = (M + 15) / 16;
-            if (int rc = run_tp16<2, 1, nbx::TP_RESID, 2>(p, st, tm)) return rc;
+            if (int rc = run_tp16<2, 1, nbx::TP_RESID, 2, 2>(p, st, tm)) return rc;
             wpc_feat = p.waves_per_chunk;
         }
         hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,

@@ -10,6 +10,9 @@
 //   the MFMAs of a k-step are issued round-robin over the (NS + 3 NV) x CG accumulators.
 // Inside a 32-deep K chunk lane quarter qd supplies k = 8 qd + s at step s (permuted, same sum).
 #pragma once
+#include <cstdlib>
+#include <type_traits>
+
 #include "tp_fused.h"
 
 namespace nbx {
@@ -20,13 +23,18 @@ __device__ inline float f4get(const float4& v, int i) { return i == 0 ? v.x : i 
 
 constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
 
-template <int NS, int NV, int EPI, int CG>
-__global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
+__global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P) {
+    constexpr int THREADS = 64 * WAVES;
+    constexpr int TW = WAVES / KS;            // row-tile slots per block; KS waves split each tile's K
+    static_assert(WAVES % KS == 0, "KS must divide WAVES");
+    constexpr int NACC = CG * (NS + 3 * NV);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int NT = NS + NV;  // B sub-tiles per chunk
     const int cgroup = blockIdx.x / P.blocks_per_chunk;   // group of CG 16-channel chunks
     const int blk = blockIdx.x - cgroup * P.blocks_per_chunk;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
+    const int slice = wave % KS, tslot = wave / KS;
     const int nchunks16 = P.chunks;                        // total 16-channel chunks
 
     int pit[NT], sub_off[NT];
@@ -37,35 +45,15 @@ __global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
         sub_off[j] = stride_g;
         stride_g += 16 * pit[j];
     }
-    // ---- stage CG chunks of weights in LDS
-#pragma unroll
-    for (int g = 0; g < CG; ++g) {
-        const int ch = cgroup * CG + g;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const bool vec = j == NS;
-            const int K = vec ? P.Kv : P.K[j];
-            const int pitch = pit[j];
-            const int q4 = pitch / 4;
-            float* dst = &lds[g * stride_g + sub_off[j]];
-            const float* src = vec ? P.Bv + (size_t)ch * 16 * P.ldb_v : P.Bs + ((size_t)ch * NS + j) * 16 * P.ldb_s;
-            const int ld = vec ? P.ldb_v : P.ldb_s;
-            for (int i = t; i < 16 * q4; i += T16_THREADS) {
-                const int row = i / q4, kq = (i - row * q4) * 4;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (ch < nchunks16 && kq < K) v = *reinterpret_cast<const float4*>(src + (size_t)row * ld + kq);
-                *reinterpret_cast<float4*>(dst + row * pitch + kq) = v;
-            }
-        }
-    }
-    __syncthreads();
-
     const int ks_chunks = (P.K[0] + 31) >> 5;
     const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
     const int n_chunks = ks_chunks + 3 * kv_chunks;
+    const int c_lo = slice * n_chunks / KS, c_hi = (slice + 1) * n_chunks / KS;   // this wave's K chunks
     const int row_tiles = (P.rows + 15) >> 4;
-    const int wstride = P.blocks_per_chunk * T16_WAVES;
-    const int wid = blk * T16_WAVES + wave;
+    const int wstride = P.blocks_per_chunk * TW;
+    const int wid = blk * TW + tslot;
+    // iterations are uniform across the block (split-K waves meet at barriers)
+    const int iters = (row_tiles - blk * TW + wstride - 1) / wstride;
 
     double st0[CG], st1[CG], st2[CG];
 #pragma unroll
@@ -91,54 +79,120 @@ __global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
         a[1] = ok ? *reinterpret_cast<const float4*>(p + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     };
 
-    // A chunks are prefetched two ahead (cur <- nxt <- nx2); (lrt, li) = next chunk to load
+    // A chunks are prefetched PF-1 ahead through pf[]; (lrt, li) = next chunk to load.
+    // The first loads are issued before the weight staging so both latencies overlap.
     int rt = wid;
-    if (rt < row_tiles) {
-        float4 cur[2], nxt[2], nx2[2];
-        int lrt = rt, li = 0;
-        auto advance = [&]() {
-            if (++li >= n_chunks) {
-                li = 0;
-                lrt += wstride;
+    const bool has_work = rt < row_tiles && c_hi > c_lo;
+    float4 pf[PF][2];   // pf[0] = chunk being consumed, pf[1..PF-1] = loads in flight
+    int lrt = rt, li = c_lo;
+    auto advance = [&]() {
+        if (++li >= c_hi) {
+            li = c_lo;
+            lrt += wstride;
+        }
+    };
+    if (has_work) {
+        load_a(lrt, li, pf[0]);
+        advance();
+#pragma unroll
+        for (int s = 1; s < PF - 1; ++s) {
+            if (lrt < row_tiles) load_a(lrt, li, pf[s]);
+            advance();
+        }
+    }
+
+    // ---- stage CG chunks of weights in LDS, SB float4 loads in flight per thread
+    {
+        int per_g = 0;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) per_g += 16 * (pit[j] / 4);
+        const int total = CG * per_g;
+        constexpr int SB = 8;
+        for (int base = t; base < total; base += SB * THREADS) {
+            float4 v[SB];
+            int dst[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = base + u * THREADS;
+                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                dst[u] = -1;
+                if (i < total) {
+                    const int g = i / per_g;
+                    int r = i - g * per_g;
+                    const int ch = cgroup * CG + g;
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        const int q4 = pit[j] / 4, n = 16 * q4;
+                        if (r >= 0 && r < n) {
+                            const bool vec = j == NS;
+                            const int K = vec ? P.Kv : P.K[j];
+                            const int row = r / q4, kq = (r - row * q4) * 4;
+                            const float* src = vec ? P.Bv + (size_t)ch * 16 * P.ldb_v
+                                                   : P.Bs + ((size_t)ch * NS + j) * 16 * P.ldb_s;
+                            const int ld = vec ? P.ldb_v : P.ldb_s;
+                            if (ch < nchunks16 && kq < K)
+                                v[u] = *reinterpret_cast<const float4*>(src + (size_t)row * ld + kq);
+                            dst[u] = g * stride_g + sub_off[j] + row * pit[j] + kq;
+                        }
+                        r -= n;
+                    }
+                }
             }
-        };
-        load_a(lrt, li, cur);
-        advance();
-        if (lrt < row_tiles) load_a(lrt, li, nxt);
-        advance();
-        while (true) {
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+                if (dst[u] >= 0) *reinterpret_cast<float4*>(&lds[dst[u]]) = v[u];
+        }
+    }
+    __syncthreads();
+
+    float* kred = lds + P.lds_floats - (KS > 1 ? TW * (KS - 1) * NACC * 4 * 64 : 0);  // split-K partials
+    for (int it = 0; it < iters; ++it) {
+        {
             floatx4 acc[CG][NS + 3 * NV];
 #pragma unroll
             for (int g = 0; g < CG; ++g)
 #pragma unroll
                 for (int j = 0; j < NS + 3 * NV; ++j) acc[g][j] = floatx4{0.f, 0.f, 0.f, 0.f};
             const int next_rt = rt + wstride;
-            for (int i = 0; i < n_chunks; ++i) {
-                if (lrt < row_tiles) load_a(lrt, li, nx2);
+            for (int i = (rt < row_tiles ? c_lo : c_hi); i < c_hi; ++i) {
+                if (lrt < row_tiles) load_a(lrt, li, pf[PF - 1]);
                 advance();
-                const float av[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+                const float av[8] = {pf[0][0].x, pf[0][0].y, pf[0][0].z, pf[0][0].w,
+                                     pf[0][1].x, pf[0][1].y, pf[0][1].z, pf[0][1].w};
                 if (i < ks_chunks) {
                     const int k0 = i * 32;
-                    float4 b[CG][NS][2];
-#pragma unroll
-                    for (int g = 0; g < CG; ++g)
-#pragma unroll
-                        for (int j = 0; j < NS; ++j) {
-                            if (k0 >= P.K[j]) continue;
-                            const float* bp = &lds[g * stride_g + sub_off[j] + c16 * pit[j] + k0 + 8 * qd];
-                            b[g][j][0] = *reinterpret_cast<const float4*>(bp);
-                            b[g][j][1] = *reinterpret_cast<const float4*>(bp + 4);
-                        }
-#pragma unroll
-                    for (int s = 0; s < 8; ++s) {
+                    // sub-tiles are ordered by K descending (checked at launch): the first `na`
+                    // are live at this k0.  Dispatch to a compile-time count so the B fragments
+                    // are read in one batch and the MFMAs interleave over independent accumulators.
+                    auto step = [&](auto na_c) {
+                        constexpr int NA = decltype(na_c)::value;
+                        float4 b[CG][NA][2];
 #pragma unroll
                         for (int g = 0; g < CG; ++g)
 #pragma unroll
-                            for (int j = 0; j < NS; ++j) {
-                                if (k0 >= P.K[j]) continue;
-                                const float bv = f4get(b[g][j][s >> 2], s & 3);
-                                acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv, acc[g][j], 0, 0, 0);
+                            for (int j = 0; j < NA; ++j) {
+                                const float* bp = &lds[g * stride_g + sub_off[j] + c16 * pit[j] + k0 + 8 * qd];
+                                b[g][j][0] = *reinterpret_cast<const float4*>(bp);
+                                b[g][j][1] = *reinterpret_cast<const float4*>(bp + 4);
                             }
+#pragma unroll
+                        for (int s = 0; s < 8; ++s)
+#pragma unroll
+                            for (int g = 0; g < CG; ++g)
+#pragma unroll
+                                for (int j = 0; j < NA; ++j)
+                                    acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                        av[s], f4get(b[g][j][s >> 2], s & 3), acc[g][j], 0, 0, 0);
+                    };
+                    int na = 0;
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) na += k0 < P.K[j] ? 1 : 0;
+                    if (na >= NS) step(std::integral_constant<int, NS>{});
+                    else if constexpr (NS >= 2) {
+                        if (na == NS - 1) step(std::integral_constant<int, NS - 1>{});
+                        else if constexpr (NS >= 3) {
+                            if (na == NS - 2) step(std::integral_constant<int, NS - 2>{});
+                        }
                     }
                 } else if (NV) {
                     const int v = i - ks_chunks, plane = v / kv_chunks;
@@ -162,16 +216,43 @@ __global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
                             }
                     }
                 }
-                cur[0] = nxt[0];
-                cur[1] = nxt[1];
-                nxt[0] = nx2[0];
-                nxt[1] = nx2[1];
+#pragma unroll
+                for (int s = 0; s < PF - 1; ++s) {
+                    pf[s][0] = pf[s + 1][0];
+                    pf[s][1] = pf[s + 1][1];
+                }
+            }
+
+            if constexpr (KS > 1) {   // fold the K slices into slice 0 through LDS
+                __syncthreads();
+                if (slice > 0) {
+                    float* dst = kred + ((tslot * (KS - 1) + slice - 1) * NACC) * 256;
+#pragma unroll
+                    for (int g = 0; g < CG; ++g)
+#pragma unroll
+                        for (int j = 0; j < NS + 3 * NV; ++j)
+                            *reinterpret_cast<floatx4*>(dst + (g * (NS + 3 * NV) + j) * 256 + 4 * lane) = acc[g][j];
+                }
+                __syncthreads();
+                if (slice == 0) {
+#pragma unroll
+                    for (int s2 = 1; s2 < KS; ++s2) {
+                        const float* src = kred + ((tslot * (KS - 1) + s2 - 1) * NACC) * 256;
+#pragma unroll
+                        for (int g = 0; g < CG; ++g)
+#pragma unroll
+                            for (int j = 0; j < NS + 3 * NV; ++j)
+                                acc[g][j] += *reinterpret_cast<const floatx4*>(src + (g * (NS + 3 * NV) + j) * 256 +
+                                                                              4 * lane);
+                    }
+                }
             }
 
             // ------------------------------------------------------------ epilogue
             const int row0 = rt * 16 + 4 * qd;   // rows of registers 0..3: row0 + jj
 #pragma unroll
             for (int g = 0; g < CG; ++g) {
+                if (slice != 0 || rt >= row_tiles) break;
                 const int ch = (cgroup * CG + g) * 16 + c16;
                 const int M = P.M;
                 if constexpr (EPI == TP_PLAIN) {
@@ -282,7 +363,6 @@ __global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
                 }
             }
             rt = next_rt;
-            if (rt >= row_tiles) break;
         }
     }
     if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
@@ -296,16 +376,16 @@ __global__ __launch_bounds__(T16_THREADS, 2) void tp16_kernel(const TpProb P) {
             a += __shfl_xor(a, 16); b += __shfl_xor(b, 16); c += __shfl_xor(c, 16);
             a += __shfl_xor(a, 32); b += __shfl_xor(b, 32); c += __shfl_xor(c, 32);
             if (qd == 0) {
-                red[((g * 3 + 0) * T16_WAVES + wave) * 16 + c16] = a;
-                red[((g * 3 + 1) * T16_WAVES + wave) * 16 + c16] = b;
-                red[((g * 3 + 2) * T16_WAVES + wave) * 16 + c16] = c;
+                red[((g * 3 + 0) * WAVES + wave) * 16 + c16] = a;
+                red[((g * 3 + 1) * WAVES + wave) * 16 + c16] = b;
+                red[((g * 3 + 2) * WAVES + wave) * 16 + c16] = c;
             }
         }
         __syncthreads();
         if (t < CG * 3 * 16) {
             const int g = t / 48, st = (t / 16) % 3, c = t % 16;
             double acc = 0.0;
-            for (int w = 0; w < T16_WAVES; ++w) acc += red[((g * 3 + st) * T16_WAVES + w) * 16 + c];
+            for (int w = 0; w < WAVES; ++w) acc += red[((g * 3 + st) * WAVES + w) * 16 + c];
             const int ch16 = cgroup * CG + g;
             if (ch16 < nchunks16) P.partial[((size_t)ch16 * P.blocks_per_chunk + blk) * 48 + st * 16 + c] = acc;
         }
@@ -322,13 +402,19 @@ inline int tp16_lds_floats(const TpProb& p) {
 }
 
 // p.chunks = number of 16-channel chunks; grid = ceil(chunks / CG) groups x blocks_per_chunk
-template <int NS, int NV, int EPI, int CG>
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
 int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     p.NS = NS;
     p.NV = NV;
     p.epi = EPI;
     if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
+    for (int j = 1; j < NS; ++j)
+        if (p.K[j] > p.K[j - 1]) {
+            set_error("tp16: scalar sub-tile K must be non-increasing");
+            return NBX_E_INVAL;
+        }
     p.lds_floats = tp16_lds_floats<CG>(p);
+    if (KS > 1) p.lds_floats += (WAVES / KS) * (KS - 1) * CG * (NS + 3 * NV) * 4 * 64;
     const size_t lds = (size_t)p.lds_floats * 4;
     if (lds > 160 * 1024) {
         set_error("tp16: weight chunk group needs %zu bytes of LDS (> 160 KiB)", lds);
@@ -336,22 +422,22 @@ int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     }
     const int groups = (p.chunks + CG - 1) / CG;
     int per_cu = (int)((160 * 1024) / lds);
-    if (per_cu > 2) per_cu = 2;
+    if (per_cu > 16 / WAVES) per_cu = 16 / WAVES;
     if (per_cu < 1) per_cu = 1;
     const int row_tiles = (p.rows + 15) / 16;
     int bpc = (num_cus * per_cu + groups - 1) / groups;
-    const int max_bpc = (row_tiles + T16_WAVES - 1) / T16_WAVES;
+    const int max_bpc = (row_tiles + WAVES / KS - 1) / (WAVES / KS);
     if (bpc > max_bpc) bpc = max_bpc;
     if (bpc < 1) bpc = 1;
     p.blocks_per_chunk = bpc;
     p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG>,
+        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG>), dim3(groups * bpc), dim3(T16_THREADS), lds, st, p);
+    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS>), dim3(groups * bpc), dim3(64 * WAVES), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }
