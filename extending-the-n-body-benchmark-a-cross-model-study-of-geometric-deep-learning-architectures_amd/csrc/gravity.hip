@@ -9,19 +9,23 @@
 
 namespace {
 
-// a_i = G * sum_j ((x_j - x_i) * r^-3) * m_j, r^2 = |x_j - x_i|^2 + eps^2 (synthetic_sim.py:318-340)
-__device__ inline void accel_from_lds(const double* __restrict__ sp, const double* __restrict__ sm, int N, int i,
+// a_i = G * sum_j ((x_j - x_i) * r^-3) * m_j, r^2 = |x_j - x_i|^2 + eps^2 (synthetic_sim.py:318-340).
+// Bodies sit in LDS as (x, y, z, m) double4 (two broadcast ds_read_b128 per partner);
+// r^-3 = rsqrt(r^2)^3 with the correctly-rounded-to-1-ulp OCML fp64 rsqrt instead of a
+// sqrt + divide (the reference's pow(r^2, -1.5) is itself ulp-different from both).
+__device__ inline void accel_from_lds(const double4* __restrict__ sp, int N, double xi, double yi, double zi,
                                       double G, double soft2, double& ax, double& ay, double& az) {
-    const double xi = sp[3 * i], yi = sp[3 * i + 1], zi = sp[3 * i + 2];
     double sx = 0.0, sy = 0.0, sz = 0.0;
+#pragma unroll 4
     for (int j = 0; j < N; ++j) {
-        const double dx = sp[3 * j] - xi, dy = sp[3 * j + 1] - yi, dz = sp[3 * j + 2] - zi;
+        const double4 p = sp[j];
+        const double dx = p.x - xi, dy = p.y - yi, dz = p.z - zi;
         const double r2 = dx * dx + dy * dy + dz * dz + soft2;
-        const double inv = r2 > 0.0 ? 1.0 / (r2 * sqrt(r2)) : r2;
-        const double mj = sm[j];
-        sx += (dx * inv) * mj;
-        sy += (dy * inv) * mj;
-        sz += (dz * inv) * mj;
+        const double ri = rsqrt(r2);
+        const double w = r2 > 0.0 ? (ri * ri * ri) * p.w : 0.0;
+        sx += dx * w;
+        sy += dy * w;
+        sz += dz * w;
     }
     ax = G * sx;
     ay = G * sy;
@@ -30,20 +34,21 @@ __device__ inline void accel_from_lds(const double* __restrict__ sp, const doubl
 
 __global__ void gravity_accel_kernel(const double* __restrict__ pos, const double* __restrict__ mass, int64_t S, int N,
                                      int spb, double G, double soft2, double* __restrict__ acc) {
-    extern __shared__ double lds[];
-    double* sp = lds;                 // [spb][N][3]
-    double* sm = lds + 3 * spb * N;   // [spb][N]
+    extern __shared__ double4 lds4[];   // [spb][N] (x, y, z, m)
     const int local = threadIdx.x / N, i = threadIdx.x % N;
     const int64_t s = (int64_t)blockIdx.x * spb + local;
     const bool live = local < spb && s < S;
+    double x = 0, y = 0, z = 0;
     if (live) {
-        for (int c = 0; c < 3; ++c) sp[(local * N + i) * 3 + c] = pos[(s * N + i) * 3 + c];
-        sm[local * N + i] = mass[s * N + i];
+        x = pos[(s * N + i) * 3 + 0];
+        y = pos[(s * N + i) * 3 + 1];
+        z = pos[(s * N + i) * 3 + 2];
+        lds4[local * N + i] = make_double4(x, y, z, mass[s * N + i]);
     }
     __syncthreads();
     if (!live) return;
     double ax, ay, az;
-    accel_from_lds(sp + local * N * 3, sm + local * N, N, i, G, soft2, ax, ay, az);
+    accel_from_lds(lds4 + local * N, N, x, y, z, G, soft2, ax, ay, az);
     acc[(s * N + i) * 3 + 0] = ax;
     acc[(s * N + i) * 3 + 1] = ay;
     acc[(s * N + i) * 3 + 2] = az;
@@ -53,14 +58,13 @@ __global__ void gravity_sample_kernel(double* __restrict__ pos, double* __restri
                                       const double* __restrict__ mass, int64_t S, int N, int spb, int64_t T,
                                       int64_t freq, double dt, double G, double soft2, double* __restrict__ pos_save,
                                       double* __restrict__ vel_save, double* __restrict__ force_save) {
-    extern __shared__ double lds[];
-    double* sp = lds;
-    double* sm = lds + 3 * spb * N;
+    extern __shared__ double4 lds4[];   // [spb][N] (x, y, z, m)
     const int local = threadIdx.x / N, i = threadIdx.x % N;
     const int64_t s = (int64_t)blockIdx.x * spb + local;
     const bool live = local < spb && s < S;
     const int64_t Ts = T / freq;
     double x = 0, y = 0, z = 0, vx = 0, vy = 0, vz = 0, m = 0;
+    double4* sp = lds4 + (live ? local * N : 0);
     if (live) {
         x = pos[(s * N + i) * 3 + 0];
         y = pos[(s * N + i) * 3 + 1];
@@ -69,14 +73,11 @@ __global__ void gravity_sample_kernel(double* __restrict__ pos, double* __restri
         vy = vel[(s * N + i) * 3 + 1];
         vz = vel[(s * N + i) * 3 + 2];
         m = mass[s * N + i];
-        sp[(local * N + i) * 3 + 0] = x;
-        sp[(local * N + i) * 3 + 1] = y;
-        sp[(local * N + i) * 3 + 2] = z;
-        sm[local * N + i] = m;
+        sp[i] = make_double4(x, y, z, m);
     }
     __syncthreads();
     double ax = 0, ay = 0, az = 0;
-    if (live) accel_from_lds(sp + local * N * 3, sm + local * N, N, i, G, soft2, ax, ay, az);
+    if (live) accel_from_lds(sp, N, x, y, z, G, soft2, ax, ay, az);
     const double hdt = dt / 2.0;
     int64_t c = 0;
     for (int64_t t = 0; t < T; ++t) {
@@ -91,13 +92,9 @@ __global__ void gravity_sample_kernel(double* __restrict__ pos, double* __restri
         vx += ax * hdt; vy += ay * hdt; vz += az * hdt;
         x += vx * dt; y += vy * dt; z += vz * dt;
         __syncthreads();  // everyone finished reading the previous positions
-        if (live) {
-            sp[(local * N + i) * 3 + 0] = x;
-            sp[(local * N + i) * 3 + 1] = y;
-            sp[(local * N + i) * 3 + 2] = z;
-        }
+        if (live) sp[i] = make_double4(x, y, z, m);
         __syncthreads();
-        if (live) accel_from_lds(sp + local * N * 3, sm + local * N, N, i, G, soft2, ax, ay, az);
+        if (live) accel_from_lds(sp, N, x, y, z, G, soft2, ax, ay, az);
         // (1/2) kick
         vx += ax * hdt; vy += ay * hdt; vz += az * hdt;
     }
@@ -138,14 +135,22 @@ __global__ void batch_mean_kernel(const double* __restrict__ x, int64_t B, int64
     out[t] = s / (double)B;
 }
 
+// Systems per workgroup: the count (up to 1024 threads) that wastes the fewest lanes of
+// the last wave, smallest on ties; e.g. N = 100 -> 10 systems = 1000 of 1024 lanes busy.
 void launch_geometry(int64_t N, int& spb, int& threads) {
-    if (N <= 256) {
-        spb = (int)(256 / N);
-        threads = ((spb * (int)N + 63) / 64) * 64;
-    } else {
-        spb = 1;
-        threads = (int)(((N + 63) / 64) * 64);
+    if (N > 1024) N = 1024;
+    int best = 1;
+    double best_u = 0.0;
+    for (int s = 1; s * N <= 1024; ++s) {
+        const int th = ((s * (int)N + 63) / 64) * 64;
+        const double u = (double)(s * N) / th;
+        if (u > best_u + 1e-9) {
+            best_u = u;
+            best = s;
+        }
     }
+    spb = best;
+    threads = ((spb * (int)N + 63) / 64) * 64;
 }
 
 }  // namespace
@@ -156,7 +161,7 @@ extern "C" int nbx_gravity_acceleration(const double* pos, const double* mass, i
     if (S == 0) return NBX_OK;
     int spb, threads;
     launch_geometry(N, spb, threads);
-    const size_t lds = sizeof(double) * 4 * spb * N;
+    const size_t lds = sizeof(double4) * spb * N;
     hipLaunchKernelGGL(gravity_accel_kernel, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
                        (hipStream_t)stream, pos, mass, S, (int)N, spb, G, softening * softening, acc);
     NBX_LAUNCH_CHECK("gravity_accel_kernel");
@@ -171,7 +176,7 @@ extern "C" int nbx_gravity_sample(double* pos, double* vel, const double* mass, 
     if (S == 0) return NBX_OK;
     int spb, threads;
     launch_geometry(N, spb, threads);
-    const size_t lds = sizeof(double) * 4 * spb * N;
+    const size_t lds = sizeof(double4) * spb * N;
     hipLaunchKernelGGL(gravity_sample_kernel, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
                        (hipStream_t)stream, pos, vel, mass, S, (int)N, spb, T, sample_freq, dt, G,
                        softening * softening, pos_save, vel_save, force_save);

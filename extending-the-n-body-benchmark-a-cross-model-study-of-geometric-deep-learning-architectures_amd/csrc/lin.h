@@ -92,50 +92,73 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     const int row_tiles = (P.rows + 31) >> 5;
     const int wstride = P.blocks_per_chunk * LIN_WAVES;
 
-    // A chunk loader: 32-deep K chunk i of row tile rt -> 16 floats per lane
-    auto load_a = [&](int rt, int i, float4 (&a)[4]) {
+    // Segment table hoisted into (scalar) registers: the hot loop never indexes the kernel
+    // argument array (a dynamic P.seg[s] is an s_load, and its lgkmcnt wait would also drain
+    // the LDS reads in flight).
+    const int nseg = P.nseg;
+    const float* sp0 = P.seg[0].ptr;
+    const float* sp1 = nseg > 1 ? P.seg[1].ptr : sp0;
+    const float* sp2 = nseg > 2 ? P.seg[2].ptr : sp1;
+    const int64_t* si0 = P.seg[0].idx;
+    const int64_t* si1 = nseg > 1 ? P.seg[1].idx : nullptr;
+    const int64_t* si2 = nseg > 2 ? P.seg[2].idx : nullptr;
+    const int sl0 = P.seg[0].ld, sl1 = nseg > 1 ? P.seg[1].ld : 0, sl2 = nseg > 2 ? P.seg[2].ld : 0;
+    const int kv0 = P.seg[0].Kvalid, kv1 = nseg > 1 ? P.seg[1].Kvalid : 0, kv2 = nseg > 2 ? P.seg[2].Kvalid : 0;
+    const int ce0 = P.seg[0].K >> 5;                               // chunk ends of segments 0 and 1
+    const int ce1 = ce0 + (nseg > 1 ? P.seg[1].K >> 5 : 0);
+
+    // per-tile source rows of the (up to 3) segments; gathered segments read their index once
+    // per tile.  Plain scalars (no struct / reference captures) keep them in registers.
+    auto tile_rows = [&](int rt, int64_t& s0, int64_t& s1, int64_t& s2, bool& ok) {
         const int row = rt * 32 + r;
-        int k0 = i * 32, s = 0;
-        while (s < P.nseg - 1 && k0 >= P.seg[s].K) {
-            k0 -= P.seg[s].K;
-            ++s;
-        }
-        const LinSeg& S = P.seg[s];
+        ok = row < P.rows;
+        const int64_t rr = ok ? row : 0;
+        s0 = si0 ? si0[rr] : rr;
+        s1 = si1 ? si1[rr] : rr;
+        s2 = si2 ? si2[rr] : rr;
+    };
+    // A chunk loader: 32-deep K chunk i of a tile -> 16 floats per lane
+    auto load_a = [&](int64_t s0, int64_t s1, int64_t s2, bool ok, int i, float4 (&a)[4]) {
+        // segment select by arithmetic (a ternary chain gets turned into a scratch lookup table)
+        const int g1 = i >= ce0 ? 1 : 0, g2 = i >= ce1 ? 1 : 0;
+        const int k0 = (i - g1 * ce0 - g2 * (ce1 - ce0)) * 32;
+        const float* base = sp0 + g1 * (sp1 - sp0) + g2 * (sp2 - sp1);
+        const int64_t src = s0 + g1 * (s1 - s0) + g2 * (s2 - s1);
+        const int ld = sl0 + g1 * (sl1 - sl0) + g2 * (sl2 - sl1);
+        const int kvalid = kv0 + g1 * (kv1 - kv0) + g2 * (kv2 - kv1);
         const int kk = k0 + 16 * h;
-        bool ok = row < P.rows;
-        int64_t src = row;
-        if (ok && S.idx) src = S.idx[row];
-        const float* p = S.ptr + (size_t)src * S.ld + kk;
+        // Buffer loads with hardware bounds checking: invalid lanes get an out-of-range offset and
+        // read zeros, so every load is issued unconditionally (exec-masked branches around the
+        // loads would make the in-flight count unknown to the waitcnt pass and force vmcnt(0)
+        // at every use).  Segments are < 2 GiB (checked by lin_launch).
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFF0, 0x00020000);
+        const uint32_t off = (uint32_t)(((size_t)src * ld + kk) * 4);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            a[q] = (ok && kk + 4 * q < S.Kvalid) ? *reinterpret_cast<const float4*>(p + 4 * q)
-                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < 4; ++q) {
+            const bool v = ok && kk + 4 * q < kvalid;
+            a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, v ? off + 16 * q : 0x7FFFFFF0u, 0, 0));
+        }
     };
 
     int rt = blk * LIN_WAVES + wave;
     if (rt >= row_tiles) return;
-    float4 cur[4], nxt[4], nx2[4];
-    int lrt = rt, li = 0;
-    auto advance = [&]() {
-        if (++li >= n_chunks) {
-            li = 0;
-            lrt += wstride;
-        }
-    };
-    load_a(lrt, li, cur);
-    advance();
-    if (lrt < row_tiles) load_a(lrt, li, nxt);
-    advance();
+    // A is double-buffered with the two buffers' roles fixed by an unroll-by-2 of the chunk
+    // loop (bA <- even chunks, bB <- odd chunks), the next tile's chunk 0 always landing in bA
+    // during the current tile's last chunk.  No register move ever reads a load still in
+    // flight, so the waitcnt pass waits only for the chunk about to be consumed (a
+    // cur <- nxt <- nx2 shuffle would force vmcnt(0) on every chunk).
+    float4 bA[4], bB[4];
+    int64_t r0, r1, r2;
+    bool rok;
+    tile_rows(rt, r0, r1, r2, rok);
+    load_a(r0, r1, r2, rok, 0, bA);
     while (true) {
         floatx16 acc[NT];
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-        for (int i = 0; i < n_chunks; ++i) {
-            if (lrt < row_tiles) load_a(lrt, li, nx2);
-            advance();
-            const int k0 = i * 32;
+        auto consume = [&](const float4 (&cur)[4], int k0) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float4 b4[NT];
@@ -151,10 +174,30 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
 #pragma unroll
                 for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4[j].w, acc[j], 0, 0, 0);
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                cur[q] = nxt[q];
-                nxt[q] = nx2[q];
+        };
+        const int nrt = rt + wstride;       // next tile of this wave
+        int i = 0;
+        int64_t n0r, n1r, n2r;              // next tile's source rows
+        bool nok = false;
+        // sched_barrier keeps each prefetch issued ahead of the MFMAs that follow it
+        for (; i + 1 < n_chunks; i += 2) {
+            load_a(r0, r1, r2, rok, i + 1, bB);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(bA, i * 32);
+            if (i + 2 < n_chunks) {
+                load_a(r0, r1, r2, rok, i + 2, bA);
+            } else if (nrt < row_tiles) {
+                tile_rows(nrt, n0r, n1r, n2r, nok);
+                load_a(n0r, n1r, n2r, nok, 0, bA);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            consume(bB, (i + 1) * 32);
+        }
+        if (i < n_chunks) {                 // odd chunk count: the last chunk sits in bA
+            consume(bA, i * 32);
+            if (nrt < row_tiles) {
+                tile_rows(nrt, n0r, n1r, n2r, nok);
+                load_a(n0r, n1r, n2r, nok, 0, bA);
             }
         }
         // ---- epilogue: col = n0 + 32 j + r; row = rt*32 + (e&3) + 8(e>>2) + 4h
@@ -250,6 +293,7 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
         }
         rt += wstride;
         if (rt >= row_tiles) break;
+        r0 = n0r; r1 = n1r; r2 = n2r; rok = nok;
     }
 }
 
@@ -260,6 +304,11 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
         set_error("lin: Ktot must be a multiple of 32 (got %d)", p.Ktot);
         return NBX_E_INVAL;
     }
+    for (int s = 0; s < p.nseg; ++s)   // buffer-load offsets are 32-bit, OOB sentinel at 2 GiB
+        if (!p.seg[s].idx && (double)p.rows * p.seg[s].ld * 4.0 >= 2147483632.0) {
+            set_error("lin: segment %d spans >= 2 GiB", s);
+            return NBX_E_UNSUPPORTED;
+        }
     const size_t lds = (size_t)NT * 32 * ((((p.Ktot + 31) & ~31) + 4)) * 4;
     if (lds > 160 * 1024) {
         set_error("lin: weight slice needs %zu bytes of LDS", lds);

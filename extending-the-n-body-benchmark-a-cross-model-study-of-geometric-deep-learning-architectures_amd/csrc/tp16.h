@@ -59,47 +59,36 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P) {
 #pragma unroll
     for (int g = 0; g < CG; ++g) st0[g] = st1[g] = st2[g] = 0.0;
 
+    // A loads are bounds-checked buffer loads: an invalid lane gets an out-of-range offset and
+    // reads zeros, so every load issues unconditionally and the waitcnt pass can count them
+    // (conditional loads would force vmcnt(0) at each use).  Buffers are < 2 GiB (launch check).
+    const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void*)P.As, (short)0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(NV ? P.Av : P.As), (short)0, 0x7FFFFFF0, 0x00020000);
     auto load_a = [&](int rt, int i, float4 (&a)[2]) {
+        // branch-free: both the scalar- and the vector-chunk offsets are computed and selected,
+        // so one pair of loads is issued from one code path
         const int row = rt * 16 + c16;
-        const float* base;
-        int k0;
-        bool ok = row < P.rows;
-        if (i < ks_chunks) {
-            base = P.As + (size_t)row * P.lda_s;
-            k0 = i * 32;
-            ok = ok && k0 + 8 * qd < P.K[0];
-        } else {
-            const int v = i - ks_chunks, plane = v / kv_chunks;
-            k0 = (v - plane * kv_chunks) * 32;
-            base = P.Av + plane * P.plane_stride + (size_t)row * P.lda_v;
-            ok = ok && k0 + 8 * qd < P.Kv;
-        }
-        const float* p = base + k0 + 8 * qd;
-        a[0] = ok ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
-        a[1] = ok ? *reinterpret_cast<const float4*>(p + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool rok = row < P.rows;
+        const bool sc = !NV || i < ks_chunks;                      // wave-uniform
+        const int v = sc ? 0 : i - ks_chunks;
+        const int plane = NV ? v / kv_chunks : 0;
+        const int k = (sc ? i * 32 : (v - plane * kv_chunks) * 32) + 8 * qd;
+        const bool ok = rok && k < (sc ? P.K[0] : P.Kv);
+        const size_t eo = sc ? (size_t)row * P.lda_s + k
+                             : (size_t)plane * P.plane_stride + (size_t)row * P.lda_v + k;
+        const uint32_t off = ok ? (uint32_t)(eo * 4) : 0x7FFFFFF0u;
+        const __amdgpu_buffer_rsrc_t rs = sc ? rsS : rsV;
+        a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
     };
 
-    // A chunks are prefetched PF-1 ahead through pf[]; (lrt, li) = next chunk to load.
-    // The first loads are issued before the weight staging so both latencies overlap.
+    // A is double-buffered with fixed roles (bA <- even chunks of a tile's K range, bB <- odd
+    // ones, the next tile's first chunk always into bA): no register move ever reads a load in
+    // flight.  The first load is issued before the weight staging so both latencies overlap.
     int rt = wid;
-    const bool has_work = rt < row_tiles && c_hi > c_lo;
-    float4 pf[PF][2];   // pf[0] = chunk being consumed, pf[1..PF-1] = loads in flight
-    int lrt = rt, li = c_lo;
-    auto advance = [&]() {
-        if (++li >= c_hi) {
-            li = c_lo;
-            lrt += wstride;
-        }
-    };
-    if (has_work) {
-        load_a(lrt, li, pf[0]);
-        advance();
-#pragma unroll
-        for (int s = 1; s < PF - 1; ++s) {
-            if (lrt < row_tiles) load_a(lrt, li, pf[s]);
-            advance();
-        }
-    }
+    float4 bA[2], bB[2];
+    if (rt < row_tiles && c_hi > c_lo) load_a(rt, c_lo, bA);
 
     // ---- stage CG chunks of weights in LDS, SB float4 loads in flight per thread
     {
@@ -154,11 +143,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P) {
 #pragma unroll
                 for (int j = 0; j < NS + 3 * NV; ++j) acc[g][j] = floatx4{0.f, 0.f, 0.f, 0.f};
             const int next_rt = rt + wstride;
-            for (int i = (rt < row_tiles ? c_lo : c_hi); i < c_hi; ++i) {
-                if (lrt < row_tiles) load_a(lrt, li, pf[PF - 1]);
-                advance();
-                const float av[8] = {pf[0][0].x, pf[0][0].y, pf[0][0].z, pf[0][0].w,
-                                     pf[0][1].x, pf[0][1].y, pf[0][1].z, pf[0][1].w};
+            auto chunk = [&](const float4 (&cb)[2], int i) {
+                const float av[8] = {cb[0].x, cb[0].y, cb[0].z, cb[0].w, cb[1].x, cb[1].y, cb[1].z, cb[1].w};
                 if (i < ks_chunks) {
                     const int k0 = i * 32;
                     // sub-tiles are ordered by K descending (checked at launch): the first `na`
@@ -216,10 +202,22 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P) {
                             }
                     }
                 }
-#pragma unroll
-                for (int s = 0; s < PF - 1; ++s) {
-                    pf[s][0] = pf[s + 1][0];
-                    pf[s][1] = pf[s + 1][1];
+            };
+            if (rt < row_tiles) {
+                int i = c_lo;
+                // sched_barrier keeps each prefetch issued ahead of the MFMAs that follow it
+                for (; i + 1 < c_hi; i += 2) {
+                    load_a(rt, i + 1, bB);
+                    __builtin_amdgcn_sched_barrier(0);
+                    chunk(bA, i);
+                    if (i + 2 < c_hi) load_a(rt, i + 2, bA);
+                    else if (next_rt < row_tiles) load_a(next_rt, c_lo, bA);
+                    __builtin_amdgcn_sched_barrier(0);
+                    chunk(bB, i + 1);
+                }
+                if (i < c_hi) {   // odd chunk count: the last chunk sits in bA
+                    chunk(bA, i);
+                    if (next_rt < row_tiles) load_a(next_rt, c_lo, bA);
                 }
             }
 
