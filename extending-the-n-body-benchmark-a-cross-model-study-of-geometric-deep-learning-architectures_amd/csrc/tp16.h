@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P) {
         const bool rok = row < P.rows;
         const bool sc = !NV || i < ks_chunks;                      // wave-uniform
         const int v = sc ? 0 : i - ks_chunks;
-        const int plane = NV ? v / kv_chunks : 0;
+        const int plane = NV ? v / (kv_chunks > 0 ? kv_chunks : 1) : 0;
         const int k = (sc ? i * 32 : (v - plane * kv_chunks) * 32) + 8 * qd;
         const bool ok = rok && k < (sc ? P.K[0] : P.Kv);
         const size_t eo = sc ? (size_t)row * P.lda_s + k
@@ -406,6 +406,11 @@ int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     p.NV = NV;
     p.epi = EPI;
     if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
+    if ((double)p.rows * p.lda_s * 4.0 >= 2147483632.0 ||
+        (p.NV && ((double)p.plane_stride * 3 + (double)p.rows * p.lda_v) * 4.0 >= 2147483632.0)) {
+        set_error("tp: A operand spans >= 2 GiB (32-bit buffer offsets)");
+        return NBX_E_UNSUPPORTED;
+    }
     for (int j = 1; j < NS; ++j)
         if (p.K[j] > p.K[j - 1]) {
             set_error("tp16: scalar sub-tile K must be non-increasing");

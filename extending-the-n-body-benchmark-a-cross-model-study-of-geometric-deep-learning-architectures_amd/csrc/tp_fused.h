@@ -113,33 +113,36 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
 
     double st0 = 0.0, st1 = 0.0, st2 = 0.0;              // BN partial sums for column r
 
-    // A-chunk loader: chunk i of a row tile -> 16 floats per lane (4 x dwordx4)
+    // A-chunk loader: chunk i of a row tile -> 16 floats per lane (4 x dwordx4).  Bounds-checked
+    // buffer loads, branch-free (invalid lanes read zeros through an out-of-range offset), so
+    // the waitcnt pass can count the loads in flight.  Buffers are < 2 GiB (launch check).
+    const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void*)P.As, (short)0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(NV ? P.Av : P.As), (short)0, 0x7FFFFFF0, 0x00020000);
     auto load_a = [&](int rt, int i, float4 (&a)[4]) {
         const int row = rt * 32 + r;
-        const float* base;
-        int k0;
-        bool ok = row < P.rows;
-        if (i < ks_chunks) {
-            base = P.As + (size_t)row * P.lda_s;
-            k0 = i * 32;
-            ok = ok && k0 + 16 * h < P.K[0];
-        } else {
-            const int v = i - ks_chunks, plane = v / kv_chunks;
-            k0 = (v - plane * kv_chunks) * 32;
-            base = P.Av + plane * P.plane_stride + (size_t)row * P.lda_v;
-            ok = ok && k0 + 16 * h < P.Kv;
-        }
-        const float* p = base + k0 + 16 * h;
+        const bool rok = row < P.rows;
+        const bool sc = !NV || i < ks_chunks;                      // wave-uniform
+        const int v = sc ? 0 : i - ks_chunks;
+        const int plane = NV ? v / (kv_chunks > 0 ? kv_chunks : 1) : 0;
+        const int k = (sc ? i * 32 : (v - plane * kv_chunks) * 32) + 16 * h;
+        const bool ok = rok && k < (sc ? P.K[0] : P.Kv);
+        const size_t eo = sc ? (size_t)row * P.lda_s + k
+                             : (size_t)plane * P.plane_stride + (size_t)row * P.lda_v + k;
+        const uint32_t off = ok ? (uint32_t)(eo * 4) : 0x7FFFFFF0u;
+        const __amdgpu_buffer_rsrc_t rs = sc ? rsS : rsV;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            a[q] = ok ? *reinterpret_cast<const float4*>(p + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+            a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 * q : off, 0, 0));
     };
 
     int rt = wid;
     if (rt >= row_tiles) goto done;
     {
-        float4 cur[4], nxt[4];
-        load_a(rt, 0, cur);
+        // A double-buffered with fixed roles (bA <- even chunks, bB <- odd, the next tile's
+        // chunk 0 always into bA): no register move reads a load still in flight
+        float4 bA[4], bB[4];
+        load_a(rt, 0, bA);
         while (true) {
             floatx16 acc[NS + 3 * NV];
 #pragma unroll
@@ -147,10 +150,7 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
             const int next_rt = rt + wstride;
-            for (int i = 0; i < n_chunks; ++i) {
-                // prefetch the next A chunk (possibly the next row tile's first)
-                if (i + 1 < n_chunks) load_a(rt, i + 1, nxt);
-                else if (next_rt < row_tiles) load_a(next_rt, 0, nxt);
+            auto chunk_mma = [&](const float4 (&cur)[4], int i) {
                 if (i < ks_chunks) {
                     const int k0 = i * 32;
 #pragma unroll
@@ -183,8 +183,20 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
                         }
                     }
                 }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+            };
+            int i = 0;
+            for (; i + 1 < n_chunks; i += 2) {
+                load_a(rt, i + 1, bB);
+                __builtin_amdgcn_sched_barrier(0);
+                chunk_mma(bA, i);
+                if (i + 2 < n_chunks) load_a(rt, i + 2, bA);
+                else if (next_rt < row_tiles) load_a(next_rt, 0, bA);
+                __builtin_amdgcn_sched_barrier(0);
+                chunk_mma(bB, i + 1);
+            }
+            if (i < n_chunks) {   // odd chunk count: the last chunk sits in bA
+                chunk_mma(bA, i);
+                if (next_rt < row_tiles) load_a(next_rt, 0, bA);
             }
 
             // ------------------------------------------------------------ epilogue
@@ -327,8 +339,6 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
             }
             rt = next_rt;
             if (rt >= row_tiles) break;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
         }
     }
 done:
@@ -382,6 +392,11 @@ inline void tp_geometry(TpProb& p, int num_cus = 256) {
 template <int NS, int NV, int EPI>
 int tp_launch(const TpProb& p, hipStream_t st) {
     if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
+    if ((double)p.rows * p.lda_s * 4.0 >= 2147483632.0 ||
+        (p.NV && ((double)p.plane_stride * 3 + (double)p.rows * p.lda_v) * 4.0 >= 2147483632.0)) {
+        set_error("tp: A operand spans >= 2 GiB (32-bit buffer offsets)");
+        return NBX_E_UNSUPPORTED;
+    }
     const size_t lds = (size_t)p.lds_floats * 4;
     if (lds > 160 * 1024) {
         set_error("tp_fused: weight chunk needs %zu bytes of LDS (> 160 KiB)", lds);
