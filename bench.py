@@ -133,9 +133,9 @@ def bench_segnn(a, rank, world, device, P):
             fl_k[k] += kfl[k]
         fwd_ms += tot.value
     # rocprofv3 names of the four fused TP launch kinds (csrc/segnn.hip::forward_impl)
-    names = ["void nbx::tp16_kernel<3, 0, 0, 2, 8, 3, 1>(nbx::TpProb)", "void nbx::tp_fused_kernel<3, 1, 1>(nbx::TpProb)",
-             "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1>(nbx::TpProb)",
-             "void nbx::tp16_kernel<2, 1, 3, 2, 8, 3, 2>(nbx::TpProb)"]
+    names = ["void nbx::tp16_kernel<3, 0, 0, 2, 8, 3, 1, true>(nbx::TpProb, nbx::TpProb, int)", "void nbx::tp_fused_kernel<3, 1, 1>(nbx::TpProb)",
+             "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false>(nbx::TpProb, nbx::TpProb, int)",
+             "void nbx::tp16_kernel<2, 1, 3, 2, 8, 3, 2, false>(nbx::TpProb, nbx::TpProb, int)"]
     roles = ["message_layer_1 node halves", "message_layer_2 + gate + aggregation + BN sums",
              "update_layer_1 + gate (pre_pool1 uses CG=2)", "update_layer_2 + residual + BN sums"]
     per_kind = {}

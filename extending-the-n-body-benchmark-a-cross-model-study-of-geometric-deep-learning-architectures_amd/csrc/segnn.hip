@@ -460,6 +460,28 @@ int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     return NBX_OK;
 }
 
+template <int NS, int NV, int EPI, int CG>
+int run_tp16_pair(nbx::TpProb& p0, nbx::TpProb& p1, hipStream_t st, KernelTiming* tm) {
+    if (!tm) return nbx::tp16_launch2<NS, NV, EPI, CG, 8, 3, 1>(p0, p1, st);
+    hipEvent_t a, b;
+    NBX_HIP(hipEventCreate(&a));
+    NBX_HIP(hipEventCreate(&b));
+    tm->ev.push_back(a);
+    tm->ev.push_back(b);
+    NBX_HIP(hipEventRecord(a, st));
+    if (int rc = nbx::tp16_launch2<NS, NV, EPI, CG, 8, 3, 1>(p0, p1, st)) return rc;
+    NBX_HIP(hipEventRecord(b, st));
+    for (const nbx::TpProb* p : {&p0, &p1}) {
+        double k = 0;
+        for (int j = 0; j < NS; ++j) k += p->K[j];
+        k += NV ? 3.0 * p->Kv : 0.0;
+        tm->flops[EPI] += 2.0 * p->rows * 16.0 * p->chunks * k;
+    }
+    tm->kind.push_back(EPI);
+    tm->launches[EPI] += 1;
+    return NBX_OK;
+}
+
 // KS > 1 splits each row tile's K loop over KS waves of the block (partials folded through
 // LDS before the epilogue).  Measured on MI355X at C2: it pays only for update_layer_2
 // (30 -> 24 us); the other node TPs lose to the extra block rounds.
@@ -493,8 +515,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         const nbx_segnn_layer& L = w->layers[l];
         if (N > 1) {
             // message_layer_1, x_i / x_j halves once per node (plain fused GEMM, 96-column chunks)
+            // scalar rows (X plane 0) and vector rows (planes 1-3) share one launch
+            nbx::TpProb pp[2];
             for (int part = 0; part < 2; ++part) {
-                nbx::TpProb p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
+                nbx::TpProb& p = pp[part];
+                p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
                 p.As = ws.X + (part ? V * M : 0);
                 p.lda_s = M;
                 p.Bs = part ? L.node_pre_v_t : L.node_pre_s_t;
@@ -504,8 +529,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 p.C = ws.NP + (part ? V * 6 * M : 0);
                 p.ldc = 6 * M;
                 p.ncols = 6 * M;
-                if (int rc = run_tp16<3, 0, nbx::TP_PLAIN, 2>(p, st, tm)) return rc;
             }
+            if (int rc = run_tp16_pair<3, 0, nbx::TP_PLAIN, 2>(pp[0], pp[1], st, tm)) return rc;
             hipLaunchKernelGGL(msg1_kernel, ew_grid(Ep, M), ewb, 0, st, ws.NP, ws.EG, L.msg1_amf, L.msg1_bias, V,
                                (int)N, (int)d.G, M, ws.M1S, ws.M1V);
             NBX_LAUNCH_CHECK("msg1");

@@ -10,6 +10,7 @@
 //   the MFMAs of a k-step are issued round-robin over the (NS + 3 NV) x CG accumulators.
 // Inside a 32-deep K chunk lane quarter qd supplies k = 8 qd + s at step s (permuted, same sum).
 #pragma once
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -23,16 +24,21 @@ __device__ inline float f4get(const float4& v, int i) { return i == 0 ? v.x : i 
 
 constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
 
-template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
-__global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P) {
+// Two independent problems of the same shape class can share one launch (P0 for blocks below
+// `split`, P1 above): node_pre's scalar-row and vector-row GEMMs fill the chip together.
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, bool DUAL = false>
+__global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
+    const bool second = DUAL && (int)blockIdx.x >= split;
+    const TpProb& P = second ? P1 : P0;
+    const int bidx = second ? (int)blockIdx.x - split : (int)blockIdx.x;
     constexpr int THREADS = 64 * WAVES;
     constexpr int TW = WAVES / KS;            // row-tile slots per block; KS waves split each tile's K
     static_assert(WAVES % KS == 0, "KS must divide WAVES");
     constexpr int NACC = CG * (NS + 3 * NV);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int NT = NS + NV;  // B sub-tiles per chunk
-    const int cgroup = blockIdx.x / P.blocks_per_chunk;   // group of CG 16-channel chunks
-    const int blk = blockIdx.x - cgroup * P.blocks_per_chunk;
+    const int cgroup = bidx / P.blocks_per_chunk;   // group of CG 16-channel chunks
+    const int blk = bidx - cgroup * P.blocks_per_chunk;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
     const int slice = wave % KS, tslot = wave / KS;
     const int nchunks16 = P.chunks;                        // total 16-channel chunks
@@ -399,12 +405,13 @@ inline int tp16_lds_floats(const TpProb& p) {
     return n * CG;
 }
 
-// p.chunks = number of 16-channel chunks; grid = ceil(chunks / CG) groups x blocks_per_chunk
-template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
-int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
+// geometry of one problem: fills p.lds_floats / blocks_per_chunk, returns the block count
+template <int NS, int NV, int EPI, int CG, int WAVES, int KS>
+int tp16_geom(TpProb& p, int num_cus, int* blocks) {
     p.NS = NS;
     p.NV = NV;
     p.epi = EPI;
+    *blocks = 0;
     if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
     if ((double)p.rows * p.lda_s * 4.0 >= 2147483632.0 ||
         (p.NV && ((double)p.plane_stride * 3 + (double)p.rows * p.lda_v) * 4.0 >= 2147483632.0)) {
@@ -434,15 +441,41 @@ int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     if (bpc < 1) bpc = 1;
     p.blocks_per_chunk = bpc;
     p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
+    *blocks = groups * bpc;
+    return NBX_OK;
+}
+
+template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, bool DUAL>
+int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
+    if (b0 + b1 == 0) return NBX_OK;
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS>,
+        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS>), dim3(groups * bpc), dim3(64 * WAVES), lds, st, p);
+    const size_t lds = (size_t)std::max(b0 ? p0.lds_floats : 0, b1 ? p1.lds_floats : 0) * 4;
+    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL>), dim3(b0 + b1), dim3(64 * WAVES), lds, st,
+                       p0, p1, b0);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
+}
+
+// p.chunks = number of 16-channel chunks; grid = ceil(chunks / CG) groups x blocks_per_chunk
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
+int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
+    int b = 0;
+    if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p, num_cus, &b)) return rc;
+    return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, false>(p, p, b, 0, st);
+}
+
+// two independent problems in one launch (same template shape)
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
+int tp16_launch2(TpProb& p0, TpProb& p1, hipStream_t st, int num_cus = 256) {
+    int b0 = 0, b1 = 0;
+    if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p0, num_cus, &b0)) return rc;
+    if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p1, num_cus, &b1)) return rc;
+    return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, true>(p0, p1, b0, b1, st);
 }
 
 }  // namespace nbx
