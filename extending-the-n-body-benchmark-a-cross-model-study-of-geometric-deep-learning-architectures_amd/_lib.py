@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libnbx.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_LAYERS = 64
 
 c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double,
@@ -21,8 +21,8 @@ c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_fl
 
 class SegnnLayer(ctypes.Structure):
     _fields_ = [(n, c_p) for n in (
-        "node_pre_s_t", "node_pre_v_t", "msg1_amf", "msg1_bias", "msg2_s_t", "msg2_v_t", "msg2_bias",
-        "upd1_s_t", "upd1_v_t", "upd1_bias", "upd2_s_t", "upd2_v_t", "upd2_bias",
+        "node_pre_s_img", "node_pre_v_img", "msg1_amf", "msg1_bias", "msg2_img", "msg2_bias",
+        "upd1_img", "upd1_bias", "upd2_img", "upd2_bias",
         "msg_bn_weight", "msg_bn_bias", "msg_bn_running_mean", "msg_bn_running_var",
         "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var")]
 
@@ -30,7 +30,7 @@ class SegnnLayer(ctypes.Structure):
 class SegnnWeights(ctypes.Structure):
     _fields_ = [("mul", c_i32), ("num_layers", c_i32), ("training", c_i32), ("bn_eps", c_f),
                 ("bn_momentum", c_f)] + [(n, c_p) for n in (
-                    "emb", "emb_bias", "pp1_s_t", "pp1_v_t", "pp1_bias", "pp2")] + [
+                    "emb", "emb_bias", "pp1_img", "pp1_bias", "pp2")] + [
                 ("layers", SegnnLayer * MAX_LAYERS)]
 
 

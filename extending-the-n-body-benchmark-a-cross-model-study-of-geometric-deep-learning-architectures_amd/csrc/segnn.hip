@@ -416,20 +416,20 @@ struct KernelTiming {
     int launches[4] = {0, 0, 0, 0};
 };
 
-template <int NS, int NV, int EPI>
+template <int NS, int NV, int EPI, int WAVES = nbx::TP_WAVES, int D = 2>
 int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     p.NS = NS;
     p.NV = NV;
     p.epi = EPI;
-    nbx::tp_geometry(p);
-    if (!tm) return nbx::tp_launch<NS, NV, EPI>(p, st);
+    nbx::tp_geometry(p, WAVES);
+    if (!tm) return nbx::tp_launch<NS, NV, EPI, WAVES, D>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
     NBX_HIP(hipEventCreate(&b));
     tm->ev.push_back(a);
     tm->ev.push_back(b);
     NBX_HIP(hipEventRecord(a, st));
-    if (int rc = nbx::tp_launch<NS, NV, EPI>(p, st)) return rc;
+    if (int rc = nbx::tp_launch<NS, NV, EPI, WAVES, D>(p, st)) return rc;
     NBX_HIP(hipEventRecord(b, st));
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
@@ -440,8 +440,91 @@ int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     return NBX_OK;
 }
 
+// Tuning switch for A/B runs on the GPU box (NBX_MSG_VARIANT=<waves>x<depth>, e.g. 8x3);
+// the default is the measured best.
+int msg_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NBX_MSG_VARIANT");
+        const char* x = e ? strchr(e, 'x') : nullptr;
+        v = x ? atoi(e) * 10 + atoi(x + 1) : 83;
+    }
+    return v;
+}
+
+// NBX_TP_DEBUG: per-wave phase clocks scratch buffer (tuning only)
+unsigned long long* tp_dbg_buf(hipStream_t st) {
+    static unsigned long long* dbg = nullptr;
+    if (!dbg && hipMalloc(&dbg, sizeof(unsigned long long) * 4 * 65536) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 4 * 65536, st) != hipSuccess) return nullptr;
+    return dbg;
+}
+
+// NBX_TP_DEBUG=1: per-wave phase clocks of the message kernel printed to stderr (tuning only)
+int tp_debug_dump(const nbx::TpProb& p, hipStream_t st, int waves) {
+    const int n = p.chunks * p.blocks_per_chunk * waves;
+    std::vector<unsigned long long> h((size_t)n * 4);
+    NBX_HIP(hipStreamSynchronize(st));
+    NBX_HIP(hipMemcpy(h.data(), p.dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull, t3 = 0;
+    double s01 = 0, s12 = 0, s23 = 0;
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) {
+        const unsigned long long* d = &h[(size_t)i * 4];
+        if (!d[3]) continue;
+        t0 = std::min(t0, d[0]);
+        t3 = std::max(t3, d[3]);
+        if (d[2]) { s01 += d[1] - d[0]; s12 += d[2] - d[1]; s23 += d[3] - d[2]; ++cnt; }
+    }
+    fprintf(stderr, "tp_debug waves=%d span=%llu stage=%.0f loop=%.0f epi=%.0f (avg clocks)\n", cnt, t3 - t0,
+            s01 / std::max(cnt, 1), s12 / std::max(cnt, 1), s23 / std::max(cnt, 1));
+    return NBX_OK;
+}
+
+template <int NS, int NV, int EPI>
+int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
+    if (debug) {
+        p.dbg = tp_dbg_buf(st);
+        int rc = run_tp<NS, NV, EPI, 8, 3>(p, st, tm);
+        if (rc) return rc;
+        return tp_debug_dump(p, st, 8);
+    }
+    switch (msg_variant()) {
+        case 82: return run_tp<NS, NV, EPI, 8, 2>(p, st, tm);
+        case 84: return run_tp<NS, NV, EPI, 8, 4>(p, st, tm);
+        default: return run_tp<NS, NV, EPI, 8, 3>(p, st, tm);
+    }
+}
+
+
+int tp16_debug_dump(const unsigned long long* dbg, int n, hipStream_t st, const char* label) {
+    std::vector<unsigned long long> h((size_t)n * 4);
+    NBX_HIP(hipStreamSynchronize(st));
+    NBX_HIP(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    double s01 = 0, s12 = 0, s23 = 0;
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) {
+        const unsigned long long* d = &h[(size_t)i * 4];
+        if (!d[1]) continue;
+        s01 += d[1] - d[0]; s12 += d[2]; s23 += d[3]; ++cnt;
+    }
+    fprintf(stderr, "tp_debug %s waves=%d/%d stage=%.0f loop=%.0f epi=%.0f (avg clocks per wave, loop/epi summed over its tiles)\n", label, cnt, n,
+            s01 / std::max(cnt, 1), s12 / std::max(cnt, 1), s23 / std::max(cnt, 1));
+    return NBX_OK;
+}
+
 template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS>
 int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
+    if (debug) {
+        p.dbg = tp_dbg_buf(st);
+        if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st)) return rc;
+        int n = ((p.chunks + CG - 1) / CG) * p.blocks_per_chunk * WAVES;
+        char lab[32];
+        snprintf(lab, sizeof lab, "tp16<%d,%d,%d,%d,KS%d>", NS, NV, EPI, CG, KS);
+        return tp16_debug_dump(p.dbg, n, st, lab);
+    }
     if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
@@ -462,6 +545,13 @@ int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
 
 template <int NS, int NV, int EPI, int CG>
 int run_tp16_pair(nbx::TpProb& p0, nbx::TpProb& p1, hipStream_t st, KernelTiming* tm) {
+    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
+    if (debug) {
+        p0.dbg = p1.dbg = tp_dbg_buf(st);
+        if (int rc = nbx::tp16_launch2<NS, NV, EPI, CG, 8, 3, 1>(p0, p1, st)) return rc;
+        const int n = ((p0.chunks + CG - 1) / CG) * p0.blocks_per_chunk * 8;   // first problem's blocks
+        return tp16_debug_dump(p0.dbg, n, st, "tp16 node_pre pair (scalar-row part)");
+    }
     if (!tm) return nbx::tp16_launch2<NS, NV, EPI, CG, 8, 3, 1>(p0, p1, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
@@ -522,8 +612,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
                 p.As = ws.X + (part ? V * M : 0);
                 p.lda_s = M;
-                p.Bs = part ? L.node_pre_v_t : L.node_pre_s_t;
-                p.ldb_s = M;
+                p.B = part ? L.node_pre_v_img : L.node_pre_s_img;
                 p.K[0] = p.K[1] = p.K[2] = M;
                 p.chunks = (6 * M + 47) / 48;  // 48-column chunks (3 sub-tiles of 16)
                 p.C = ws.NP + (part ? V * 6 * M : 0);
@@ -539,13 +628,13 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         {
             // message_layer_2 + gate + aggregation + message-BN partial sums
             nbx::TpProb p = tp_base((int)Ep, d);
-            p.As = ws.M1S; p.lda_s = 2 * M; p.Bs = L.msg2_s_t; p.ldb_s = 2 * M;
+            p.As = ws.M1S; p.lda_s = 2 * M; p.B = L.msg2_img;
             p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
-            p.Av = ws.M1V; p.lda_v = M; p.plane_stride = Ep * M; p.Bv = L.msg2_v_t; p.ldb_v = M; p.Kv = M;
+            p.Av = ws.M1V; p.lda_v = M; p.plane_stride = Ep * M; p.Kv = M;
             p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G; p.valid_per_group = (int)(N - 1);
             p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
             if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
-                if (int rc = run_tp<3, 1, nbx::TP_MSG>(p, st, tm)) return rc;
+                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm)) return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
             } else {
@@ -564,9 +653,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         {
             // update_layer_1 + gate -> inputs of update_layer_2
             nbx::TpProb p = tp_base((int)V, d);
-            p.As = ws.U1S; p.lda_s = 4 * M; p.Bs = L.upd1_s_t; p.ldb_s = 4 * M;
+            p.As = ws.U1S; p.lda_s = 4 * M; p.B = L.upd1_img;
             p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M;
-            p.Av = ws.U1V; p.lda_v = 2 * M; p.plane_stride = V * 2 * M; p.Bv = L.upd1_v_t; p.ldb_v = 2 * M;
+            p.Av = ws.U1V; p.lda_v = 2 * M; p.plane_stride = V * 2 * M;
             p.Kv = 2 * M;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
@@ -576,9 +665,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         {
             // update_layer_2 + residual + feature-BN partial sums
             nbx::TpProb p = tp_base((int)V, d);
-            p.As = ws.U2S; p.lda_s = 2 * M; p.Bs = L.upd2_s_t; p.ldb_s = 2 * M;
+            p.As = ws.U2S; p.lda_s = 2 * M; p.B = L.upd2_img;
             p.K[0] = 2 * M; p.K[1] = M;
-            p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Bv = L.upd2_v_t; p.ldb_v = M; p.Kv = M;
+            p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
             p.chunks = (M + 15) / 16;
@@ -595,9 +684,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA, V, M, ws.U1S);
     {
         nbx::TpProb p = tp_base((int)V, d);
-        p.As = ws.U1S; p.lda_s = 2 * M; p.Bs = w->pp1_s_t; p.ldb_s = 2 * M;
+        p.As = ws.U1S; p.lda_s = 2 * M; p.B = w->pp1_img;
         p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
-        p.Av = ws.X + V * M; p.lda_v = M; p.plane_stride = V * M; p.Bv = w->pp1_v_t; p.ldb_v = M; p.Kv = M;
+        p.Av = ws.X + V * M; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
         if (int rc = run_tp16<3, 1, nbx::TP_GATE_NODE, 2>(p, st, tm)) return rc;

@@ -43,16 +43,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
     const int slice = wave % KS, tslot = wave / KS;
     const int nchunks16 = P.chunks;                        // total 16-channel chunks
 
-    int pit[NT], sub_off[NT];
-    int stride_g = 0;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        pit[j] = tp_pitch(j < NS ? P.K[j] : P.Kv);
-        sub_off[j] = stride_g;
-        stride_g += 16 * pit[j];
-    }
+    int sub_off[NS + 1];
+    tp_img_offsets<NS>(P, 16, sub_off);
+    const int stride_g = P.img_floats;                    // one 16-channel chunk image
     const int ks_chunks = (P.K[0] + 31) >> 5;
     const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
+    const float kv_inv = 1.0f / (float)(kv_chunks > 0 ? kv_chunks : 1);
     const int n_chunks = ks_chunks + 3 * kv_chunks;
     const int c_lo = slice * n_chunks / KS, c_hi = (slice + 1) * n_chunks / KS;   // this wave's K chunks
     const int row_tiles = (P.rows + 15) >> 4;
@@ -78,7 +74,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
         const bool rok = row < P.rows;
         const bool sc = !NV || i < ks_chunks;                      // wave-uniform
         const int v = sc ? 0 : i - ks_chunks;
-        const int plane = NV ? v / (kv_chunks > 0 ? kv_chunks : 1) : 0;
+        const int plane = NV ? tp_udiv_small(v, kv_inv) : 0;
         const int k = (sc ? i * 32 : (v - plane * kv_chunks) * 32) + 8 * qd;
         const bool ok = rok && k < (sc ? P.K[0] : P.Kv);
         const size_t eo = sc ? (size_t)row * P.lda_s + k
@@ -92,53 +88,19 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
     // A is double-buffered with fixed roles (bA <- even chunks of a tile's K range, bB <- odd
     // ones, the next tile's first chunk always into bA): no register move ever reads a load in
     // flight.  The first load is issued before the weight staging so both latencies overlap.
+    const unsigned long long c_start = P.dbg ? clock64() : 0ull;
+    unsigned long long c_loop = 0ull, c_epi = 0ull, c_mark = 0ull;   // per-phase sums over tiles
     int rt = wid;
     float4 bA[2], bB[2];
     if (rt < row_tiles && c_hi > c_lo) load_a(rt, c_lo, bA);
 
-    // ---- stage CG chunks of weights in LDS, SB float4 loads in flight per thread
-    {
-        int per_g = 0;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) per_g += 16 * (pit[j] / 4);
-        const int total = CG * per_g;
-        constexpr int SB = 8;
-        for (int base = t; base < total; base += SB * THREADS) {
-            float4 v[SB];
-            int dst[SB];
-#pragma unroll
-            for (int u = 0; u < SB; ++u) {
-                const int i = base + u * THREADS;
-                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                dst[u] = -1;
-                if (i < total) {
-                    const int g = i / per_g;
-                    int r = i - g * per_g;
-                    const int ch = cgroup * CG + g;
-#pragma unroll
-                    for (int j = 0; j < NT; ++j) {
-                        const int q4 = pit[j] / 4, n = 16 * q4;
-                        if (r >= 0 && r < n) {
-                            const bool vec = j == NS;
-                            const int K = vec ? P.Kv : P.K[j];
-                            const int row = r / q4, kq = (r - row * q4) * 4;
-                            const float* src = vec ? P.Bv + (size_t)ch * 16 * P.ldb_v
-                                                   : P.Bs + ((size_t)ch * NS + j) * 16 * P.ldb_s;
-                            const int ld = vec ? P.ldb_v : P.ldb_s;
-                            if (ch < nchunks16 && kq < K)
-                                v[u] = *reinterpret_cast<const float4*>(src + (size_t)row * ld + kq);
-                            dst[u] = g * stride_g + sub_off[j] + row * pit[j] + kq;
-                        }
-                        r -= n;
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < SB; ++u)
-                if (dst[u] >= 0) *reinterpret_cast<float4*>(&lds[dst[u]]) = v[u];
-        }
-    }
+    // ---- stage the CG chunk images of this group in LDS (LDS-DMA, verbatim copy; the image
+    // array holds a multiple of 4 chunks, so a group never runs past it)
+    tp_dma_image<WAVES>(P.B + (size_t)cgroup * CG * P.img_floats, lds, CG * P.img_floats);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const unsigned long long c_staged = P.dbg ? clock64() : 0ull;
+    c_mark = c_staged;
 
     float* kred = lds + P.lds_floats - (KS > 1 ? TW * (KS - 1) * NACC * 4 * 64 : 0);  // split-K partials
     for (int it = 0; it < iters; ++it) {
@@ -163,9 +125,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                         for (int g = 0; g < CG; ++g)
 #pragma unroll
                             for (int j = 0; j < NA; ++j) {
-                                const float* bp = &lds[g * stride_g + sub_off[j] + c16 * pit[j] + k0 + 8 * qd];
+                                const float* bp = &lds[g * stride_g + sub_off[j] + i * 512 + 4 * lane];
                                 b[g][j][0] = *reinterpret_cast<const float4*>(bp);
-                                b[g][j][1] = *reinterpret_cast<const float4*>(bp + 4);
+                                b[g][j][1] = *reinterpret_cast<const float4*>(bp + 256);
                             }
 #pragma unroll
                         for (int s = 0; s < 8; ++s)
@@ -187,14 +149,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                         }
                     }
                 } else if (NV) {
-                    const int v = i - ks_chunks, plane = v / kv_chunks;
-                    const int k0 = (v - plane * kv_chunks) * 32;
+                    const int v = i - ks_chunks, plane = tp_udiv_small(v, kv_inv);
+                    const int kc = v - plane * kv_chunks;
                     float4 b[CG][2];
 #pragma unroll
                     for (int g = 0; g < CG; ++g) {
-                        const float* bp = &lds[g * stride_g + sub_off[NS] + c16 * pit[NS] + k0 + 8 * qd];
+                        const float* bp = &lds[g * stride_g + sub_off[NS] + kc * 512 + 4 * lane];
                         b[g][0] = *reinterpret_cast<const float4*>(bp);
-                        b[g][1] = *reinterpret_cast<const float4*>(bp + 4);
+                        b[g][1] = *reinterpret_cast<const float4*>(bp + 256);
                     }
 #pragma unroll
                     for (int pl = 0; pl < 3; ++pl) {
@@ -252,6 +214,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                 }
             }
 
+            if (P.dbg) { const unsigned long long c = clock64(); c_loop += c - c_mark; c_mark = c; }
             // ------------------------------------------------------------ epilogue
             const int row0 = rt * 16 + 4 * qd;   // rows of registers 0..3: row0 + jj
 #pragma unroll
@@ -289,9 +252,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                         st2[g] += (double)m0[jj] * m0[jj] + (double)m1[jj] * m1[jj] + (double)m2[jj] * m2[jj];
                     }
                     const int G = P.group;
+                    const int lg = __builtin_ctz((unsigned)G);
                     auto put = [&](int row, float a0, float a1, float a2, float a3) {
                         if (live && row < P.rows) {
-                            const size_t o = (size_t)(row / G) * M + ch;
+                            const size_t o = (size_t)(row >> lg) * M + ch;
                             P.out_s[o] = a0;
                             P.out_v[o] = a1;
                             P.out_v[P.out_plane + o] = a2;
@@ -366,8 +330,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                     }
                 }
             }
+            if (P.dbg) { const unsigned long long c = clock64(); c_epi += c - c_mark; c_mark = c; }
             rt = next_rt;
         }
+    }
+    if (P.dbg && lane == 0) {
+        unsigned long long* d = P.dbg + ((size_t)bidx * WAVES + wave) * 4;
+        // [start, staged, sum over tiles of the K loop, sum over tiles of the epilogue]
+        d[0] = c_start; d[1] = c_staged; d[2] = c_loop; d[3] = c_epi;
     }
     if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
         // reduce the 8 waves of the block in LDS (the weights are no longer needed), one
@@ -397,13 +367,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
 }
 
 template <int CG>
-inline int tp16_lds_floats(const TpProb& p) {
-    auto pitch = [](int K) { return ((K + 31) & ~31) + 4; };
-    int n = 0;
-    for (int j = 0; j < p.NS; ++j) n += 16 * pitch(p.K[j]);
-    if (p.NV) n += 16 * pitch(p.Kv);
-    return n * CG;
-}
+inline int tp16_lds_floats(const TpProb& p) { return tp_img_floats(p, 16) * CG; }
 
 // geometry of one problem: fills p.lds_floats / blocks_per_chunk, returns the block count
 template <int NS, int NV, int EPI, int CG, int WAVES, int KS>
@@ -423,6 +387,7 @@ int tp16_geom(TpProb& p, int num_cus, int* blocks) {
             set_error("tp16: scalar sub-tile K must be non-increasing");
             return NBX_E_INVAL;
         }
+    p.img_floats = tp_img_floats(p, 16);
     p.lds_floats = tp16_lds_floats<CG>(p);
     if (KS > 1) p.lds_floats += (WAVES / KS) * (KS - 1) * CG * (NS + 3 * NV) * 4 * 64;
     const size_t lds = (size_t)p.lds_floats * 4;

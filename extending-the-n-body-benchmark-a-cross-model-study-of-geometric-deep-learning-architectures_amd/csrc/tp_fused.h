@@ -27,16 +27,18 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3 };
 
 struct TpProb {
-    // scalar part: NS sub-tiles, sub-tile j uses the first K_j columns of its B rows
+    // scalar part: NS sub-tiles, sub-tile j contracts the first K_j columns of A
     const float* As;   // [rows][lda_s]
-    const float* Bs;   // [chunks][NS][32][ldb_s]
-    int lda_s, ldb_s, NS;
+    int lda_s, NS;
     int K[3];
     // vector part (NV = 1: three planes, NV = 0: none)
     const float* Av;   // plane k, row r at Av + k * plane_stride + r * lda_v
-    const float* Bv;   // [chunks][32][ldb_v]
     long plane_stride;
-    int lda_v, ldb_v, Kv, NV;
+    int lda_v, Kv, NV;
+    // weights: MFMA-fragment-ordered LDS image, [chunks][img_floats] (include/nbx.h
+    // "TP operand images"); a block copies its chunk's image into LDS verbatim
+    const float* B;
+    int img_floats;
     int rows, chunks, M;  // M = real channels (epilogue mask)
     int epi;
     // PLAIN: C[row][chunk*NS*32 + 32 j + col]
@@ -55,76 +57,79 @@ struct TpProb {
     // grid geometry (set by the launcher)
     int blocks_per_chunk;
     int lds_floats;
+    unsigned long long* dbg;  // optional per-wave phase clocks [waves][4] (tuning only)
 };
 
 constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
 
-__device__ inline float tp_silu(float x) { return x / (1.0f + __expf(-x)); }
-__device__ inline float tp_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp) instead of the IEEE division sequence
+__device__ inline float tp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ inline float tp_silu(float x) { return x * tp_sigmoid(x); }
 
-__device__ inline int tp_pitch(int K) { return ((K + 31) & ~31) + 4; }
+// exact floor(a / b) for 0 <= a, b < 2^10 given inv = 1/b: one multiply instead of
+// the ~20-instruction integer division sequence
+__device__ inline int tp_udiv_small(int a, float inv) { return (int)(((float)a + 0.5f) * inv); }
 
-template <int NS, int NV, int EPI>
-__global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P) {
+// LDS-DMA copy of a weight image (nfloats a multiple of 256): one 1 KiB global_load_lds_dwordx4
+// per wave-instruction, no VGPRs, all pieces in flight at once.  The caller drains with
+// s_waitcnt vmcnt(0) + a barrier before reading the LDS.
+template <int WAVES>
+__device__ inline void tp_dma_image(const float* src, float* lds, int nfloats) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pieces = nfloats >> 8;
+    for (int p = wave; p < pieces; p += WAVES)
+        __builtin_amdgcn_global_load_lds((const void*)(src + p * 256 + lane * 4),
+                                         (__attribute__((address_space(3))) void*)(lds + p * 256), 16, 0, 0);
+}
+
+// offset (floats) of each sub-tile block inside one chunk image: KC = ceil(K/32) blocks of
+// 32 x cw floats per sub-tile, scalar sub-tiles first, then the vector sub-tile
+template <int NS>
+__device__ inline void tp_img_offsets(const TpProb& P, int cw, int (&off)[NS + 1]) {
+    int o = 0;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        off[j] = o;
+        o += ((P.K[j] + 31) >> 5) * 32 * cw;
+    }
+    off[NS] = o;
+}
+
+template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2>
+__global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(const TpProb P) {
+    constexpr int THREADS = 64 * WAVES;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int chunk = blockIdx.x / P.blocks_per_chunk;
     const int blk = blockIdx.x - chunk * P.blocks_per_chunk;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
 
-    // ---- stage this chunk's weights in LDS (zero-padded to 32-deep K chunks)
     int off[NS + 1];
-    int pit[NS + 1];
-    {
-        int o = 0;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            off[j] = o;
-            pit[j] = tp_pitch(P.K[j]);
-            o += 32 * pit[j];
-        }
-        off[NS] = o;
-        pit[NS] = tp_pitch(P.Kv);
-    }
-#pragma unroll
-    for (int j = 0; j < NS + NV; ++j) {
-        const bool vec = j == NS;
-        const int K = vec ? P.Kv : P.K[j];
-        const int pitch = pit[j];
-        const int ld = vec ? P.ldb_v : P.ldb_s;
-        const int q4 = pitch / 4;  // float4 per LDS row (incl. pad)
-        for (int i = t; i < 32 * q4; i += TP_THREADS) {
-            const int row = i / q4, kq = (i - row * q4) * 4;
-            // scalar-part B rows are stored 16-channel interleaved: [chunks16][NS][16][K]
-            const float* src = vec ? P.Bv + ((size_t)chunk * 32 + row) * P.ldb_v
-                                   : P.Bs + (((size_t)(2 * chunk + (row >> 4)) * NS + j) * 16 + (row & 15)) * P.ldb_s;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (kq < K) v = *reinterpret_cast<const float4*>(src + kq);
-            *reinterpret_cast<float4*>(&lds[off[j] + row * pitch + kq]) = v;
-        }
-    }
-    __syncthreads();
+    tp_img_offsets<NS>(P, 32, off);
 
     const int ks_chunks = (P.K[0] + 31) >> 5;            // K_S = K[0] (sub-tile 0 uses all of it)
     const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
+    const float kv_inv = 1.0f / (float)(kv_chunks > 0 ? kv_chunks : 1);
     const int n_chunks = ks_chunks + 3 * kv_chunks;      // A chunks per row tile
+    const int nc_pad = (n_chunks + D - 1) / D * D;       // chunk stream padded to the ring depth
     const int row_tiles = (P.rows + 31) >> 5;
-    const int wstride = P.blocks_per_chunk * TP_WAVES;
-    const int wid = blk * TP_WAVES + wave;               // wave index within this chunk
+    const int wstride = P.blocks_per_chunk * WAVES;
+    const int wid = blk * WAVES + wave;                  // wave index within this chunk
 
     double st0 = 0.0, st1 = 0.0, st2 = 0.0;              // BN partial sums for column r
 
     // A-chunk loader: chunk i of a row tile -> 16 floats per lane (4 x dwordx4).  Bounds-checked
-    // buffer loads, branch-free (invalid lanes read zeros through an out-of-range offset), so
-    // the waitcnt pass can count the loads in flight.  Buffers are < 2 GiB (launch check).
+    // buffer loads, branch-free (invalid lanes, padding chunks and tiles past the end read zeros
+    // through an out-of-range offset), so every load issues unconditionally and the waitcnt pass
+    // can count the loads in flight.  Buffers are < 2 GiB (launch check).
     const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void*)P.As, (short)0, 0x7FFFFFF0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV =
         __builtin_amdgcn_make_buffer_rsrc((void*)(NV ? P.Av : P.As), (short)0, 0x7FFFFFF0, 0x00020000);
     auto load_a = [&](int rt, int i, float4 (&a)[4]) {
         const int row = rt * 32 + r;
-        const bool rok = row < P.rows;
+        const bool rok = row < P.rows && i < n_chunks;
         const bool sc = !NV || i < ks_chunks;                      // wave-uniform
         const int v = sc ? 0 : i - ks_chunks;
-        const int plane = NV ? v / (kv_chunks > 0 ? kv_chunks : 1) : 0;
+        const int plane = NV ? tp_udiv_small(v, kv_inv) : 0;
         const int k = (sc ? i * 32 : (v - plane * kv_chunks) * 32) + 16 * h;
         const bool ok = rok && k < (sc ? P.K[0] : P.Kv);
         const size_t eo = sc ? (size_t)row * P.lda_s + k
@@ -136,13 +141,24 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
             a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 * q : off, 0, 0));
     };
 
+    // A ring of D chunk buffers with fixed roles: chunk i of a tile always lives in buf[i % D]
+    // (the stream is padded to a multiple of D), and the load for chunk i + D - 1 is issued
+    // before the MFMAs of chunk i.  The first D - 1 loads go out before the weight staging.
+    const unsigned long long c_start = P.dbg ? clock64() : 0ull;
     int rt = wid;
+    float4 buf[D][4];
+#pragma unroll
+    for (int u = 0; u < D - 1; ++u) load_a(rt, u, buf[u]);
+
+    // ---- stage this chunk's weight image in LDS (LDS-DMA, verbatim copy)
+    tp_dma_image<WAVES>(P.B + (size_t)chunk * P.img_floats, lds, P.img_floats);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long c_staged = P.dbg ? clock64() : 0ull;
+    unsigned long long c_loop = 0ull;
+
     if (rt >= row_tiles) goto done;
     {
-        // A double-buffered with fixed roles (bA <- even chunks, bB <- odd, the next tile's
-        // chunk 0 always into bA): no register move reads a load still in flight
-        float4 bA[4], bB[4];
-        load_a(rt, 0, bA);
         while (true) {
             floatx16 acc[NS + 3 * NV];
 #pragma unroll
@@ -150,32 +166,39 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
             const int next_rt = rt + wstride;
+            // MSG: this tile's edge geometry (rhat) is fetched now and parked in LDS before the
+            // epilogue, so the epilogue reads it without global-memory latency
+            float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (EPI == TP_MSG) {
+                const int grow = rt * 32 + r;
+                if (h == 0 && grow < P.rows) gq = *reinterpret_cast<const float4*>(P.geom + (size_t)grow * 8);
+            }
             auto chunk_mma = [&](const float4 (&cur)[4], int i) {
                 if (i < ks_chunks) {
                     const int k0 = i * 32;
 #pragma unroll
                     for (int j = 0; j < NS; ++j) {
                         if (k0 >= P.K[j]) continue;
-                        const float* bp = &lds[off[j] + r * pit[j] + k0 + 16 * h];
+                        const float* bp = &lds[off[j] + i * 1024 + 4 * lane];
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
-                            const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * q);
+                            const float4 b4 = *reinterpret_cast<const float4*>(bp + 256 * q);
                             acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4.x, acc[j], 0, 0, 0);
                             acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4.y, acc[j], 0, 0, 0);
                             acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4.z, acc[j], 0, 0, 0);
                             acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4.w, acc[j], 0, 0, 0);
                         }
                     }
-                } else if (NV) {
-                    const int v = i - ks_chunks, plane = v / kv_chunks;
-                    const int k0 = (v - plane * kv_chunks) * 32;
-                    const float* bp = &lds[off[NS] + r * pit[NS] + k0 + 16 * h];
+                } else if (NV && i < n_chunks) {
+                    const int v = i - ks_chunks, plane = tp_udiv_small(v, kv_inv);
+                    const int kc = v - plane * kv_chunks;
+                    const float* bp = &lds[off[NS] + kc * 1024 + 4 * lane];
 #pragma unroll
                     for (int pl = 0; pl < 3; ++pl) {
                         if (pl != plane) continue;
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
-                            const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * q);
+                            const float4 b4 = *reinterpret_cast<const float4*>(bp + 256 * q);
                             acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4.x, acc[NS + pl], 0, 0, 0);
                             acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4.y, acc[NS + pl], 0, 0, 0);
                             acc[NS + pl] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4.z, acc[NS + pl], 0, 0, 0);
@@ -184,21 +207,21 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
                     }
                 }
             };
-            int i = 0;
-            for (; i + 1 < n_chunks; i += 2) {
-                load_a(rt, i + 1, bB);
-                __builtin_amdgcn_sched_barrier(0);
-                chunk_mma(bA, i);
-                if (i + 2 < n_chunks) load_a(rt, i + 2, bA);
-                else if (next_rt < row_tiles) load_a(next_rt, 0, bA);
-                __builtin_amdgcn_sched_barrier(0);
-                chunk_mma(bB, i + 1);
-            }
-            if (i < n_chunks) {   // odd chunk count: the last chunk sits in bA
-                chunk_mma(bA, i);
-                if (next_rt < row_tiles) load_a(next_rt, 0, bA);
+            for (int i0 = 0; i0 < nc_pad; i0 += D) {
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    // prefetch chunk i0 + u + D - 1 (wrapping into the next tile) into the buffer
+                    // the previous step consumed
+                    int pi = i0 + u + D - 1, prt = rt;
+                    if (pi >= nc_pad) { pi -= nc_pad; prt = next_rt; }
+                    load_a(prt, pi, buf[(u + D - 1) % D]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    chunk_mma(buf[u], i0 + u);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
 
+            if (P.dbg) c_loop = clock64();
             // ------------------------------------------------------------ epilogue
             const int ch = chunk * 32 + r;          // output channel of this lane's column
             const int row0 = rt * 32;
@@ -219,29 +242,38 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
                 const int M = P.M;
                 const bool live = ch < M;
                 const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
+                float4* gl = reinterpret_cast<float4*>(lds + P.lds_floats) + wave * 32;   // [32 rows] rhat
+                if (h == 0) gl[r] = gq;
+                __builtin_amdgcn_wave_barrier();
                 float ms[16], mv0[16], mv1[16], mv2[16];
+                float f0 = 0.f, f1 = 0.f, f2 = 0.f;   // per-tile BN partials (16 rows), fp64 across tiles
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
-                    const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
+                    const int row = row0 + rr;
                     const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group;
-                    const float* g = P.geom + (size_t)(row < P.rows ? row : 0) * 8;
+                    const float4 g = gl[rr];
                     const float s = kC_SILU * tp_silu(acc[0][e] + ba);
                     const float gg = kC_SIGMOID * tp_sigmoid(acc[1][e] + bg);
                     const float tt = acc[2][e];
                     ms[e] = ok ? s : 0.f;
-                    mv0[e] = ok ? gg * (g[0] * tt + acc[NS + 0][e]) : 0.f;
-                    mv1[e] = ok ? gg * (g[1] * tt + acc[NS + 1][e]) : 0.f;
-                    mv2[e] = ok ? gg * (g[2] * tt + acc[NS + 2][e]) : 0.f;
-                    st0 += (double)ms[e];
-                    st1 += (double)ms[e] * ms[e];
-                    st2 += (double)mv0[e] * mv0[e] + (double)mv1[e] * mv1[e] + (double)mv2[e] * mv2[e];
+                    mv0[e] = ok ? gg * (g.x * tt + acc[NS + 0][e]) : 0.f;
+                    mv1[e] = ok ? gg * (g.y * tt + acc[NS + 1][e]) : 0.f;
+                    mv2[e] = ok ? gg * (g.z * tt + acc[NS + 2][e]) : 0.f;
+                    f0 += ms[e];
+                    f1 += ms[e] * ms[e];
+                    f2 += mv0[e] * mv0[e] + mv1[e] * mv1[e] + mv2[e] * mv2[e];
                 }
+                st0 += (double)f0;
+                st1 += (double)f1;
+                st2 += (double)f2;
                 // aggregate the `group` consecutive rows of each destination (all indices
                 // compile-time so the per-row arrays stay in registers)
                 const int G = P.group;
+                const int lg = __builtin_ctz((unsigned)G);
                 auto put = [&](int row, float a0, float a1, float a2, float a3) {
                     if (live && row < P.rows) {
-                        const size_t o = (size_t)(row / G) * M + ch;
+                        const size_t o = (size_t)(row >> lg) * M + ch;
                         P.out_s[o] = a0;
                         P.out_v[o] = a1;
                         P.out_v[P.out_plane + o] = a2;
@@ -342,54 +374,61 @@ __global__ __launch_bounds__(TP_THREADS, 2) void tp_fused_kernel(const TpProb P)
         }
     }
 done:
+    if (P.dbg && lane == 0) {
+        unsigned long long* d = P.dbg + ((size_t)blockIdx.x * WAVES + wave) * 4;
+        d[0] = c_start; d[1] = c_staged; d[2] = c_loop; d[3] = clock64();
+    }
     if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
         // reduce the block's waves in LDS: one partial row per block, layout [chunk][block][3][32]
         __syncthreads();
-        double* red = reinterpret_cast<double*>(lds);   // [3][TP_WAVES][32]
+        double* red = reinterpret_cast<double*>(lds);   // [3][WAVES][32]
         st0 += __shfl_xor(st0, 32);
         st1 += __shfl_xor(st1, 32);
         st2 += __shfl_xor(st2, 32);
         if (h == 0) {
-            red[(0 * TP_WAVES + wave) * 32 + r] = st0;
-            red[(1 * TP_WAVES + wave) * 32 + r] = st1;
-            red[(2 * TP_WAVES + wave) * 32 + r] = st2;
+            red[(0 * WAVES + wave) * 32 + r] = st0;
+            red[(1 * WAVES + wave) * 32 + r] = st1;
+            red[(2 * WAVES + wave) * 32 + r] = st2;
         }
         __syncthreads();
         if (t < 96) {
             const int st = t / 32, c = t % 32;
             double acc = 0.0;
-            for (int w = 0; w < TP_WAVES; ++w) acc += red[(st * TP_WAVES + w) * 32 + c];
+            for (int w = 0; w < WAVES; ++w) acc += red[(st * WAVES + w) * 32 + c];
             P.partial[((size_t)chunk * P.blocks_per_chunk + blk) * 96 + st * 32 + c] = acc;
         }
     }
 }
 
-inline int tp_lds_floats(const TpProb& p) {
-    auto pitch = [](int K) { return ((K + 31) & ~31) + 4; };
+// floats of one chunk image (cw = channels per chunk: 32 here, 16 for tp16)
+inline int tp_img_floats(const TpProb& p, int cw) {
     int n = 0;
-    for (int j = 0; j < p.NS; ++j) n += 32 * pitch(p.K[j]);
-    if (p.NV) n += 32 * pitch(p.Kv);
+    for (int j = 0; j < p.NS; ++j) n += ((p.K[j] + 31) / 32) * 32 * cw;
+    if (p.NV) n += ((p.Kv + 31) / 32) * 32 * cw;
     return n;
 }
 
+inline int tp_lds_floats(const TpProb& p) { return tp_img_floats(p, 32); }
+
 // Grid: `blocks_per_chunk` blocks per 32-channel chunk, chosen to fill the CUs
 // (as many blocks per CU as the LDS footprint allows) without idle waves.
-inline void tp_geometry(TpProb& p, int num_cus = 256) {
+inline void tp_geometry(TpProb& p, int waves = TP_WAVES, int num_cus = 256) {
+    p.img_floats = tp_img_floats(p, 32);
     p.lds_floats = tp_lds_floats(p);
     const int lds_bytes = p.lds_floats * 4;
     int per_cu = (160 * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
     if (per_cu < 1) per_cu = 1;
-    if (per_cu > 2) per_cu = 2;  // 8-wave blocks: at most 16 waves / CU
+    if (per_cu > 16 / waves) per_cu = 16 / waves > 0 ? 16 / waves : 1;  // at most 16 waves / CU
     const int row_tiles = (p.rows + 31) / 32;
     int bpc = (num_cus * per_cu + p.chunks - 1) / p.chunks;
-    const int max_bpc = (row_tiles + TP_WAVES - 1) / TP_WAVES;
+    const int max_bpc = (row_tiles + waves - 1) / waves;
     if (bpc > max_bpc) bpc = max_bpc;
     if (bpc < 1) bpc = 1;
     p.blocks_per_chunk = bpc;
     p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
 }
 
-template <int NS, int NV, int EPI>
+template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2>
 int tp_launch(const TpProb& p, hipStream_t st) {
     if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
     if ((double)p.rows * p.lda_s * 4.0 >= 2147483632.0 ||
@@ -397,19 +436,19 @@ int tp_launch(const TpProb& p, hipStream_t st) {
         set_error("tp: A operand spans >= 2 GiB (32-bit buffer offsets)");
         return NBX_E_UNSUPPORTED;
     }
-    const size_t lds = (size_t)p.lds_floats * 4;
+    const size_t lds = (size_t)p.lds_floats * 4 + (EPI == TP_MSG ? (size_t)WAVES * 32 * 16 : 0);
     if (lds > 160 * 1024) {
         set_error("tp_fused: weight chunk needs %zu bytes of LDS (> 160 KiB)", lds);
         return NBX_E_UNSUPPORTED;
     }
     static bool attr_set = false;  // per instantiation
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp_fused_kernel<NS, NV, EPI>,
+        NBX_HIP(hipFuncSetAttribute((const void*)tp_fused_kernel<NS, NV, EPI, WAVES, D>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((tp_fused_kernel<NS, NV, EPI>), dim3(p.chunks * p.blocks_per_chunk), dim3(TP_THREADS), lds, st,
-                       p);
+    hipLaunchKernelGGL((tp_fused_kernel<NS, NV, EPI, WAVES, D>), dim3(p.chunks * p.blocks_per_chunk), dim3(64 * WAVES),
+                       lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

@@ -214,35 +214,72 @@ class SEGNN(nn.Module):
         P["pp2"] = vec(torch.stack([Ws[:, 0], Ws[:, 1], Wv[:, 0], Wv[:, 1]]))
         return P
 
-    # gate / update TPs whose scalar-row matrix is stored chunk-interleaved on the
-    # device: name -> number of 32-column sub-tiles per 32-channel chunk
-    _INTERLEAVED = {"msg2_s_t": 3, "upd1_s_t": 3, "upd2_s_t": 2, "pp1_s_t": 3}
-    _CHUNK_PADDED = ("msg2_v_t", "upd1_v_t", "upd2_v_t", "pp1_v_t")
+    # ------------------------------------------------------------ LDS images (include/nbx.h)
+    @staticmethod
+    def frag_image(subs, vec, cw: int, chunks: int) -> torch.Tensor:
+        """MFMA-fragment-ordered weight image of one TP (include/nbx.h "TP operand
+        images"): `subs` = [(W_j [rows][>=K_j], K_j)] scalar sub-tiles, `vec` = (W_v, K_v) or
+        None; row c of every matrix is output channel c of that part.  Returns
+        [chunks][F] fp32, chunk = `cw` channels of every part, zero-filled past K and
+        past the real rows."""
+        blocks = []
+        for W, K in list(subs) + ([vec] if vec is not None else []):
+            kc = (K + 31) // 32
+            X = torch.zeros(chunks * cw, kc * 32, dtype=W.dtype, device=W.device)
+            n = min(W.shape[0], chunks * cw)
+            X[:n, :K] = W[:n, :K]
+            if cw == 16:   # [c][16][kc][qd 4][half 2][e 4] -> [c][kc][half][qd][16][e]
+                X = X.reshape(chunks, 16, kc, 4, 2, 4).permute(0, 2, 4, 3, 1, 5)
+            else:          # [c][32][kc][h 2][q 4][e 4] -> [c][kc][q][h][32][e]
+                X = X.reshape(chunks, 32, kc, 2, 4, 4).permute(0, 2, 4, 3, 1, 5)
+            blocks.append(X.reshape(chunks, -1))
+        return torch.cat(blocks, 1).contiguous()
 
     @staticmethod
-    def device_layout(name: str, mat: torch.Tensor, mul: int) -> torch.Tensor:
-        """Layout of include/nbx.h for the fused TP kernels: channels are padded to
-        Mp = 32*ceil(M/32); [parts*M][K] scalar-row matrices become
-        [Mp/16][parts][16][K] (channel c of part j at row (c//16)*parts*16 + 16j + c%16,
-        zero rows for padded channels); vector-row matrices [M][K] are padded to [Mp][K]."""
-        base = name.rsplit(".", 1)[-1]
-        mp = 32 * ((mul + 31) // 32)
-        if base in SEGNN._INTERLEAVED:
-            parts = SEGNN._INTERLEAVED[base]
-            K = mat.shape[1]
-            x = torch.nn.functional.pad(mat.reshape(parts, mul, K), (0, 0, 0, mp - mul))
-            c16 = mp // 16
-            return x.reshape(parts, c16, 16, K).permute(1, 0, 2, 3).reshape(c16 * parts * 16, K).contiguous()
-        if base in SEGNN._CHUNK_PADDED:
-            return torch.nn.functional.pad(mat, (0, 0, 0, mp - mul)).contiguous()
-        return mat
+    def tp_images(P: dict, mul: int) -> dict:
+        """packed_matrices -> the device images the kernels stage (msg2: 32-channel
+        chunks for the 32x32 message kernel; every node TP: 16-channel chunks, the
+        chunk count padded to a multiple of 4 so any channel-group size <= 4 divides it)."""
+        M = mul
+        c16 = -(-M // 16)
+        c16 = -(-c16 // 4) * 4
+        c32 = -(-M // 32)
+        img = SEGNN.frag_image
+        out = {}
+        for key in list(P):
+            pre, base = (key.rsplit(".", 1) + [""])[:2] if "." in key else ("", key)
+            pre = pre + "." if pre else ""
+            if base in ("node_pre_s_t", "node_pre_v_t"):
+                B = P[key]                                    # [6M][M]: 48-column chunks of 3 x 16
+                n48 = -(-6 * M // 48)
+                n48p = -(-n48 // 4) * 4
+                B = torch.nn.functional.pad(B, (0, 0, 0, n48p * 48 - 6 * M)).reshape(n48p, 3, 16, M)
+                subs = [(B[:, j].reshape(n48p * 16, M), M) for j in range(3)]
+                out[pre + base[:-2] + "_img"] = img(subs, None, 16, n48p)
+            elif base in ("msg2_s_t", "upd1_s_t", "upd2_s_t", "pp1_s_t"):
+                stem = base[:-4]
+                S, V = P[key], P[pre + stem + "_v_t"]
+                K = S.shape[1]
+                parts = S.shape[0] // M
+                # the last part (t, 0e -> 1o path) only contracts the first half of K
+                Ks = [K] * (parts - 1) + [K // 2]
+                subs = [(S[j * M:(j + 1) * M], Ks[j]) for j in range(parts)]
+                if stem == "msg2":
+                    out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 32, c32)
+                else:
+                    out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 16, c16)
+            elif base.endswith("_v_t"):
+                continue
+            else:
+                out[key] = P[key]
+        return out
 
     def pack_weights(self, device):
         """Build the nbx_segnn_weights struct (device pointers) from packed_matrices."""
-        P = {k: self.device_layout(k, v, self.mul) for k, v in self.packed_matrices(device).items()}
+        P = self.tp_images(self.packed_matrices(device), self.mul)
         W = _lib.SegnnWeights()
         W.mul, W.num_layers, W.bn_eps, W.bn_momentum = self.mul, self.num_layers, 1e-5, 0.1
-        for k in ("emb", "emb_bias", "pp1_s_t", "pp1_v_t", "pp1_bias", "pp2"):
+        for k in ("emb", "emb_bias", "pp1_img", "pp1_bias", "pp2"):
             setattr(W, k, P[k].data_ptr())
         for li, layer in enumerate(self.layers):
             L = W.layers[li]

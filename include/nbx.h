@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 1
+#define NBX_ABI_VERSION 2
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -83,24 +83,36 @@ int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size,
  * systems of N nodes.  Hidden irreps are mul x 0e + mul x 1o (mul % 4 == 0).
  *
  * Weights are the reference's e3nn parameters re-packed once on the device by
- * the host module (see the package's segnn.py::pack_weights for the exact
+ * the host module (see the package's segnn.py::packed_matrices for the exact
  * formulas).  Matrices named *_t are stored transposed, [N_out][K_in], row-major.
+ *
+ * TP operand images (*_img; built by segnn.py::tp_images).  Every O(3) tensor
+ * product is a scalar-row GEMM with sub-tiles j (output part j: s, gate, t;
+ * contraction length K_j) plus, for the gate/update TPs, a vector-row GEMM
+ * (length Kv).  Its image is [chunks][F] fp32, one chunk = CW output channels of
+ * every part, copied verbatim into LDS by the kernel:
+ *   F = (sum_j KC_j + KC_v) * 32 * CW,  KC = ceil(K / 32);
+ *   inside a chunk: the sub-tile blocks j = 0.. then the vector block, each
+ *   [KC][32 * CW] in MFMA fragment order, zero past K and past the real channels:
+ *     CW = 16 (v_mfma_f32_16x16x4_f32): [half 2][qd 4][c 16][e 4] = W[c][32 kc + 8 qd + 4 half + e]
+ *     CW = 32 (v_mfma_f32_32x32x2_f32): [q 4][h 2][c 32][e 4]     = W[c][32 kc + 16 h + 4 q + e]
+ *   so lane l of a wave reads 16 contiguous bytes per ds_read_b128 (bank-conflict free).
+ * msg2_img uses CW = 32 with ceil(mul/32) chunks; every other image CW = 16 with
+ * ceil(.../16) chunks rounded up to a multiple of 4.  node_pre: NS = 3 parts of 16
+ * columns per chunk = output columns [48 c + 16 j, 48 c + 16 j + 16) of the *_t matrix.
  */
 #define NBX_SEGNN_MAX_LAYERS 64
 
 typedef struct nbx_segnn_layer {
-    const float* node_pre_s_t; /* [6*mul][mul]  x_s -> [P_dst(2mul) R_dst(mul) P_src(2mul) R_src(mul)] */
-    const float* node_pre_v_t; /* [6*mul][mul]  x_v[:,k] -> [Q_dst(2mul) S_dst(mul) Q_src(2mul) S_src(mul)] */
+    const float* node_pre_s_img; /* image of [6*mul][mul] x_s -> [P_dst(2mul) R_dst(mul) P_src(2mul) R_src(mul)] */
+    const float* node_pre_v_img; /* image of [6*mul][mul] x_v[:,k] -> [Q_dst(2mul) S_dst(mul) Q_src(2mul) S_src(mul)] */
     const float* msg1_amf;     /* [2][3*mul]    amf (dist, m_i m_j) -> [s(2mul) t(mul)] */
     const float* msg1_bias;    /* [2*mul] */
-    const float* msg2_s_t;     /* [3*mul][2*mul] [m_s | m_v.rhat] -> [s(2mul) t(mul)] */
-    const float* msg2_v_t;     /* [mul][mul]     m_v[:,k] -> v */
+    const float* msg2_img;     /* parts of [3*mul][2*mul] [m_s | m_v.rhat] -> [s | gate | t] + [mul][mul] m_v[:,k] -> v */
     const float* msg2_bias;    /* [2*mul] */
-    const float* upd1_s_t;     /* [3*mul][4*mul] [x_s a_s x_v.na a_v.na] -> [s(2mul) t(mul)] */
-    const float* upd1_v_t;     /* [mul][2*mul]   [x_v[:,k] a_v[:,k]] -> v */
+    const float* upd1_img;     /* [3*mul][4*mul] [x_s a_s x_v.na a_v.na] -> [s | gate | t] + [mul][2*mul] -> v */
     const float* upd1_bias;    /* [2*mul] */
-    const float* upd2_s_t;     /* [2*mul][2*mul] [h_s | h_v.na] -> [s(mul) t(mul)] */
-    const float* upd2_v_t;     /* [mul][mul] */
+    const float* upd2_img;     /* [2*mul][2*mul] [h_s | h_v.na] -> [s | t] + [mul][mul] -> v */
     const float* upd2_bias;    /* [mul] */
     /* e3nn BatchNorm(hidden): weight [2mul], bias [mul], running_mean [mul],
        running_var [2mul]; running stats are updated in place in train mode. */
@@ -122,8 +134,7 @@ typedef struct nbx_segnn_weights {
     float bn_momentum;  /* 0.1 */
     const float* emb;      /* [6][mul]: W_a[0], W_a[1], W_b[0]/sqrt3, W_b[1]/sqrt3, W_c, W_d */
     const float* emb_bias; /* [mul] */
-    const float* pp1_s_t;  /* [3*mul][2*mul] pre_pool1 (gate TP, node attrs) */
-    const float* pp1_v_t;  /* [mul][mul] */
+    const float* pp1_img;  /* pre_pool1 (gate TP, node attrs): [3*mul][2*mul] + [mul][mul] */
     const float* pp1_bias; /* [2*mul] */
     const float* pp2;      /* [2][2][mul]: (s->1o, v->1o) x (out channel 0, 1) */
     nbx_segnn_layer layers[NBX_SEGNN_MAX_LAYERS];

@@ -15,7 +15,8 @@ declare -A PASSES=(
   [write]="WRITE_SIZE"
   [l2]="TCC_HIT_sum TCC_MISS_sum"
 )
-for p in sq lds fetch write l2; do
+timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
+for p in sq fetch write l2 lds; do
   echo "[$(date +%T)] pass $p: ${PASSES[$p]}"
   timeout -s KILL 120 rocprofv3 --pmc ${PASSES[$p]} --output-format csv -d gpurun_out/pmc/$p -o run \
       -- python bench.py $ARGS > gpurun_out/pmc/$p.log 2>&1
