@@ -48,14 +48,29 @@ def test_abi_version_and_host_only_calls(L):
     assert b"more neighbors" in L.nbx_last_error()
 
 
+def _struct_fields(name):
+    """(field names, pointer count) of `typedef struct name {...} name;` in include/nbx.h."""
+    import re
+    txt = open(os.path.join(ROOT, "include", "nbx.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), txt, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"(\w+)\s*(?:\[[^\]]*\])?;", body)
+    ptrs = len(re.findall(r"\*\s*\w+;", body))
+    return fields, ptrs
+
+
 def test_struct_layout_matches_header():
-    """ctypes mirror of nbx_segnn_weights has the C layout (pointer-aligned)."""
+    """ctypes mirror of nbx_segnn_weights has the C layout: same fields, same order,
+    pointer-aligned sizes."""
     import nbody_amd._lib as lib
-    layer_ptrs = 21
+    lf, layer_ptrs = _struct_fields("nbx_segnn_layer")
+    assert [f for f, _ in lib.SegnnLayer._fields_] == lf
     assert ctypes.sizeof(lib.SegnnLayer) == layer_ptrs * 8
+    wf, w_ptrs = _struct_fields("nbx_segnn_weights")
+    assert [f for f, _ in lib.SegnnWeights._fields_] == wf
     head = 3 * 4 + 2 * 4   # mul, num_layers, training, bn_eps, bn_momentum
     head = (head + 7) // 8 * 8
-    assert ctypes.sizeof(lib.SegnnWeights) == head + 6 * 8 + lib.MAX_LAYERS * layer_ptrs * 8
+    assert ctypes.sizeof(lib.SegnnWeights) == head + w_ptrs * 8 + lib.MAX_LAYERS * layer_ptrs * 8
 
 
 def test_product_fails_loudly_without_device():
