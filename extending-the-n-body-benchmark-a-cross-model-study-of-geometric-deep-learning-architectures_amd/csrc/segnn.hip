@@ -26,6 +26,7 @@
 #include "nbx_internal.h"
 #include "tp16.h"
 #include "tp_fused.h"
+#include "msg_pre.h"
 
 namespace {
 
@@ -416,20 +417,20 @@ struct KernelTiming {
     int launches[4] = {0, 0, 0, 0};
 };
 
-template <int NS, int NV, int EPI, int WAVES = nbx::TP_WAVES, int D = 2>
+template <int NS, int NV, int EPI, int WAVES = nbx::TP_WAVES, int D = 2, class SK = nbx::DynSK>
 int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     p.NS = NS;
     p.NV = NV;
     p.epi = EPI;
     nbx::tp_geometry(p, WAVES);
-    if (!tm) return nbx::tp_launch<NS, NV, EPI, WAVES, D>(p, st);
+    if (!tm) return nbx::tp_launch<NS, NV, EPI, WAVES, D, SK>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
     NBX_HIP(hipEventCreate(&b));
     tm->ev.push_back(a);
     tm->ev.push_back(b);
     NBX_HIP(hipEventRecord(a, st));
-    if (int rc = nbx::tp_launch<NS, NV, EPI, WAVES, D>(p, st)) return rc;
+    if (int rc = nbx::tp_launch<NS, NV, EPI, WAVES, D, SK>(p, st)) return rc;
     NBX_HIP(hipEventRecord(b, st));
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
@@ -439,6 +440,33 @@ int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     tm->launches[EPI] += 1;
     return NBX_OK;
 }
+
+// The node TPs run a fully unrolled K loop when their chunk counts match one of the static
+// schedules compiled here (the C2 width mul = 96 and mul = 32), else the run-time-shaped loop.
+// NBX_STATIC=0 forces the run-time loop (A/B only).
+bool static_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NBX_STATIC");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
+template <class SK>
+bool sk_matches(const nbx::TpProb& p, int NS, int NV) {
+    auto kc = [](int K) { return (K + 31) / 32; };
+    return kc(p.K[0]) == SK::K0 && (NS < 2 || kc(p.K[1]) == SK::K1) && (NS < 3 || kc(p.K[2]) == SK::K2) &&
+           (NV ? kc(p.Kv) : 0) == SK::KV;
+}
+
+// K chunk schedules per TP at mul = 96 and mul = 32
+using SK_UPD1 = nbx::StatSK<12, 12, 6, 6>;
+using SK_UPD1_32 = nbx::StatSK<4, 4, 2, 2>;
+using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
+using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
+using SK_GATE = nbx::StatSK<6, 6, 3, 3>;     // pre_pool1 (and message_layer_2's shape)
+using SK_GATE_32 = nbx::StatSK<2, 2, 1, 1>;
 
 // Tuning switch for A/B runs on the GPU box (NBX_MSG_VARIANT=<waves>x<depth>, e.g. 8x3);
 // the default is the measured best.
@@ -490,6 +518,11 @@ int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
         if (rc) return rc;
         return tp_debug_dump(p, st, 8);
     }
+    // message_layer_2 at mul = 96 / 32: fully unrolled static chunk schedule
+    if (static_enabled()) {
+        if (sk_matches<SK_GATE>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_GATE>(p, st, tm);
+        if (sk_matches<SK_GATE_32>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_GATE_32>(p, st, tm);
+    }
     switch (msg_variant()) {
         case 82: return run_tp<NS, NV, EPI, 8, 2>(p, st, tm);
         case 84: return run_tp<NS, NV, EPI, 8, 4>(p, st, tm);
@@ -514,25 +547,25 @@ int tp16_debug_dump(const unsigned long long* dbg, int n, hipStream_t st, const 
     return NBX_OK;
 }
 
-template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS>
+template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, class SK = nbx::DynSK>
 int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
     if (debug) {
         p.dbg = tp_dbg_buf(st);
-        if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st)) return rc;
+        if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK>(p, st)) return rc;
         int n = ((p.chunks + CG - 1) / CG) * p.blocks_per_chunk * WAVES;
         char lab[32];
         snprintf(lab, sizeof lab, "tp16<%d,%d,%d,%d,KS%d>", NS, NV, EPI, CG, KS);
         return tp16_debug_dump(p.dbg, n, st, lab);
     }
-    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st);
+    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
     NBX_HIP(hipEventCreate(&b));
     tm->ev.push_back(a);
     tm->ev.push_back(b);
     NBX_HIP(hipEventRecord(a, st));
-    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS>(p, st)) return rc;
+    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK>(p, st)) return rc;
     NBX_HIP(hipEventRecord(b, st));
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
@@ -540,6 +573,37 @@ int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     tm->kind.push_back(EPI);
     tm->flops[EPI] += 2.0 * p.rows * 16.0 * p.chunks * k;
     tm->launches[EPI] += 1;
+    return NBX_OK;
+}
+
+int run_msg_pre(nbx::MsgPreProb& p, hipStream_t st, KernelTiming* tm) {
+    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
+    if (debug) {
+        p.dbg = tp_dbg_buf(st);
+        if (int rc = nbx::msg_pre_launch(p, st)) return rc;
+        const int n = p.chunks * p.per_chunk * 8;
+        std::vector<unsigned long long> h((size_t)n * 4);
+        NBX_HIP(hipStreamSynchronize(st));
+        NBX_HIP(hipMemcpy(h.data(), p.dbg, h.size() * 8, hipMemcpyDeviceToHost));
+        double s[4] = {0, 0, 0, 0};
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < 4; ++k) s[k] += (double)h[(size_t)i * 4 + k];
+        fprintf(stderr, "tp_debug msg_pre waves=%d slabs=%d per_chunk=%d stage=%.0f gemm=%.0f ex=%.0f edge=%.0f\n", n,
+                p.n_slabs, p.per_chunk, s[0] / n, s[1] / n, s[2] / n, s[3] / n);
+        return NBX_OK;
+    }
+    if (!tm) return nbx::msg_pre_launch(p, st);
+    hipEvent_t a, b;
+    NBX_HIP(hipEventCreate(&a));
+    NBX_HIP(hipEventCreate(&b));
+    tm->ev.push_back(a);
+    tm->ev.push_back(b);
+    NBX_HIP(hipEventRecord(a, st));
+    if (int rc = nbx::msg_pre_launch(p, st)) return rc;
+    NBX_HIP(hipEventRecord(b, st));
+    tm->kind.push_back(nbx::TP_PLAIN);   // reported as the message_layer_1 kind
+    tm->flops[nbx::TP_PLAIN] += 2.0 * 4.0 * p.V * p.M * 6.0 * p.M;   // the node GEMM's useful MACs x 2
+    tm->launches[nbx::TP_PLAIN] += 1;
     return NBX_OK;
 }
 
@@ -575,9 +639,11 @@ int run_tp16_pair(nbx::TpProb& p0, nbx::TpProb& p1, hipStream_t st, KernelTiming
 // KS > 1 splits each row tile's K loop over KS waves of the block (partials folded through
 // LDS before the epilogue).  Measured on MI355X at C2: it pays only for update_layer_2
 // (30 -> 24 us); the other node TPs lose to the extra block rounds.
-template <int NS, int NV, int EPI, int CG, int KS = 1>
-int run_tp16(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
-    return run_tp16_w<NS, NV, EPI, CG, 8, 3, KS>(p, st, tm);
+template <int NS, int NV, int EPI, int CG, int KS, class SK, class... Rest>
+int run_tp16_try(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
+    if (static_enabled() && sk_matches<SK>(p, NS, NV)) return run_tp16_w<NS, NV, EPI, CG, 8, 3, KS, SK>(p, st, tm);
+    if constexpr (sizeof...(Rest) > 0) return run_tp16_try<NS, NV, EPI, CG, KS, Rest...>(p, st, tm);
+    else return run_tp16_w<NS, NV, EPI, CG, 8, 3, KS, nbx::DynSK>(p, st, tm);
 }
 
 nbx::TpProb tp_base(int rows, const Dims& d) {
@@ -603,23 +669,38 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
 
     for (int l = 0; l < w->num_layers; ++l) {
         const nbx_segnn_layer& L = w->layers[l];
-        if (N > 1) {
-            // message_layer_1, x_i / x_j halves once per node (plain fused GEMM, 96-column chunks)
-            // scalar rows (X plane 0) and vector rows (planes 1-3) share one launch
-            nbx::TpProb pp[2];
-            for (int part = 0; part < 2; ++part) {
-                nbx::TpProb& p = pp[part];
-                p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
-                p.As = ws.X + (part ? V * M : 0);
-                p.lda_s = M;
-                p.B = part ? L.node_pre_v_img : L.node_pre_s_img;
-                p.K[0] = p.K[1] = p.K[2] = M;
-                p.chunks = (6 * M + 47) / 48;  // 48-column chunks (3 sub-tiles of 16)
-                p.C = ws.NP + (part ? V * 6 * M : 0);
-                p.ldc = 6 * M;
-                p.ncols = 6 * M;
+        if (N > 1 && nbx::msg_pre_group((int)N) > 0 && M <= 128) {
+            // message_layer_1: node precomputation + edge combination + gate in one kernel
+            nbx::MsgPreProb mp;
+            memset(&mp, 0, sizeof(mp));
+            mp.X = ws.X; mp.Simg = L.node_pre_s_img; mp.Vimg = L.node_pre_v_img; mp.EG = ws.EG;
+            mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V;
+            mp.V = V; mp.N = (int)N; mp.G = (int)d.G; mp.M = M; mp.NG = nbx::msg_pre_group((int)N);
+            if (int rc = run_msg_pre(mp, st, tm)) return rc;
+        } else if (N > 1) {
+            // systems larger than a 16-row tile: node precomputation (plain GEMM, part-major
+            // columns of NP: parts 0-2 and 3-5 of the 6-part image in two paired launches), then
+            // the per-edge combination
+            const int KC = (M + 31) / 32, F6 = 6 * KC * 512;
+            for (int half = 0; half < 2; ++half) {
+                nbx::TpProb pp[2];
+                for (int part = 0; part < 2; ++part) {
+                    nbx::TpProb& p = pp[part];
+                    p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
+                    p.As = ws.X + (part ? V * M : 0);
+                    p.lda_s = M;
+                    p.B = (part ? L.node_pre_v_img : L.node_pre_s_img) + half * 3 * KC * 512;
+                    p.img_stride = F6;
+                    p.K[0] = p.K[1] = p.K[2] = M;
+                    p.chunks = (M + 15) / 16;
+                    p.col_part_stride = M;
+                    p.col_part0 = 3 * half;
+                    p.C = ws.NP + (part ? V * 6 * M : 0);
+                    p.ldc = 6 * M;
+                    p.ncols = 6 * M;
+                }
+                if (int rc = run_tp16_pair<3, 0, nbx::TP_PLAIN, 2>(pp[0], pp[1], st, tm)) return rc;
             }
-            if (int rc = run_tp16_pair<3, 0, nbx::TP_PLAIN, 2>(pp[0], pp[1], st, tm)) return rc;
             hipLaunchKernelGGL(msg1_kernel, ew_grid(Ep, M), ewb, 0, st, ws.NP, ws.EG, L.msg1_amf, L.msg1_bias, V,
                                (int)N, (int)d.G, M, ws.M1S, ws.M1V);
             NBX_LAUNCH_CHECK("msg1");
@@ -659,7 +740,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.Kv = 2 * M;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
-            if (int rc = run_tp16<3, 1, nbx::TP_GATE_NODE, 1>(p, st, tm)) return rc;
+            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 1, SK_UPD1, SK_UPD1_32>(p, st, tm)) return rc;
         }
         int wpc_feat;
         {
@@ -671,7 +752,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
             p.chunks = (M + 15) / 16;
-            if (int rc = run_tp16<2, 1, nbx::TP_RESID, 2, 2>(p, st, tm)) return rc;
+            if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             wpc_feat = p.waves_per_chunk;
         }
         hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
@@ -689,7 +770,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.Av = ws.X + V * M; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
-        if (int rc = run_tp16<3, 1, nbx::TP_GATE_NODE, 2>(p, st, tm)) return rc;
+        if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 2, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
     }
     hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,
                        w->pp2, V, M, out);

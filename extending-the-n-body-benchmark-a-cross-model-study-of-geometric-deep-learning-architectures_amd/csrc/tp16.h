@@ -26,7 +26,8 @@ constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
 
 // Two independent problems of the same shape class can share one launch (P0 for blocks below
 // `split`, P1 above): node_pre's scalar-row and vector-row GEMMs fill the chip together.
-template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, bool DUAL = false>
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, bool DUAL = false,
+          class SK = DynSK>
 __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
     const bool second = DUAL && (int)blockIdx.x >= split;
     const TpProb& P = second ? P1 : P0;
@@ -69,9 +70,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
         __builtin_amdgcn_make_buffer_rsrc((void*)(NV ? P.Av : P.As), (short)0, 0x7FFFFFF0, 0x00020000);
     auto load_a = [&](int rt, int i, float4 (&a)[2]) {
         // branch-free: both the scalar- and the vector-chunk offsets are computed and selected,
-        // so one pair of loads is issued from one code path
+        // so one pair of loads is issued from one code path; chunks outside [c_lo, c_hi) (ring
+        // padding) and rows past the end read zeros
         const int row = rt * 16 + c16;
-        const bool rok = row < P.rows;
+        const bool rok = row < P.rows && i < c_hi;
         const bool sc = !NV || i < ks_chunks;                      // wave-uniform
         const int v = sc ? 0 : i - ks_chunks;
         const int plane = NV ? tp_udiv_small(v, kv_inv) : 0;
@@ -85,18 +87,66 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
         a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
     };
 
-    // A is double-buffered with fixed roles (bA <- even chunks of a tile's K range, bB <- odd
-    // ones, the next tile's first chunk always into bA): no register move ever reads a load in
-    // flight.  The first load is issued before the weight staging so both latencies overlap.
+    // A streams through a ring of PF chunk buffers with fixed roles: chunk c_lo + u of a tile
+    // lives in ring[u % PF] (the chunk stream is padded to a multiple of PF), and the load of
+    // chunk u + PF - 1 (wrapping into the next tile) is issued before the MFMAs of chunk u, so
+    // PF - 1 chunks are in flight behind the current one.  The first PF - 1 loads are issued
+    // before the weight staging so both latencies overlap.
     const unsigned long long c_start = P.dbg ? clock64() : 0ull;
     unsigned long long c_loop = 0ull, c_epi = 0ull, c_mark = 0ull;   // per-phase sums over tiles
     int rt = wid;
-    float4 bA[2], bB[2];
-    if (rt < row_tiles && c_hi > c_lo) load_a(rt, c_lo, bA);
+    const int nck = c_hi - c_lo;
+    const int nc_pad = (nck + PF - 1) / PF * PF;
+    float4 ring[PF][2];
+
+    // ---- static schedule (SK::on): items of a tile = K0 scalar chunks (the first NA(i) sub-tiles
+    // live) then KV chunks of each vector plane; split-K slice s owns items [s N / KS, (s+1) N / KS)
+    constexpr int SNIT = SK::K0 + 3 * SK::KV;
+    auto load_item = [&](auto ic, int rt_, float4 (&a)[2]) {
+        constexpr int item = decltype(ic)::value;
+        constexpr bool sc = item < SK::K0;
+        constexpr int v = sc ? 0 : item - SK::K0;
+        constexpr int plane = sc ? 0 : v / (SK::KV > 0 ? SK::KV : 1);
+        constexpr int kc = sc ? item : v - plane * SK::KV;
+        const int row = rt_ * 16 + c16;
+        const int k = kc * 32 + 8 * qd;
+        const bool ok = row < P.rows && k < (sc ? P.K[0] : P.Kv);
+        const size_t eo = sc ? (size_t)row * P.lda_s + k : (size_t)plane * P.plane_stride + (size_t)row * P.lda_v + k;
+        const uint32_t off = ok ? (uint32_t)(eo * 4) : 0x7FFFFFF0u;
+        const __amdgpu_buffer_rsrc_t rs = sc ? rsS : rsV;
+        a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
+    };
+    auto slice_call = [&](auto&& fn) {
+        static_for<0, KS>([&](auto sc_) {
+            if (slice == decltype(sc_)::value) fn(sc_);
+        });
+    };
+    if constexpr (SK::on) {
+        slice_call([&](auto sc_) {
+            constexpr int lo = decltype(sc_)::value * SNIT / KS, hi = (decltype(sc_)::value + 1) * SNIT / KS;
+            static_for<0, PF - 1>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                if constexpr (lo + u < hi) load_item(std::integral_constant<int, lo + u>{}, rt, ring[u % PF]);
+            });
+        });
+    } else {
+#pragma unroll
+        for (int u = 0; u < PF - 1; ++u) load_a(rt, c_lo + u, ring[u]);
+    }
 
     // ---- stage the CG chunk images of this group in LDS (LDS-DMA, verbatim copy; the image
     // array holds a multiple of 4 chunks, so a group never runs past it)
-    tp_dma_image<WAVES>(P.B + (size_t)cgroup * CG * P.img_floats, lds, CG * P.img_floats);
+    {
+        const int stride = P.img_stride > 0 ? P.img_stride : P.img_floats;
+        if (stride == P.img_floats) {
+            tp_dma_image<WAVES>(P.B + (size_t)cgroup * CG * P.img_floats, lds, CG * P.img_floats);
+        } else {
+#pragma unroll
+            for (int g = 0; g < CG; ++g)
+                tp_dma_image<WAVES>(P.B + (size_t)(cgroup * CG + g) * stride, lds + g * P.img_floats, P.img_floats);
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const unsigned long long c_staged = P.dbg ? clock64() : 0ull;
@@ -171,21 +221,97 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                     }
                 }
             };
-            if (rt < row_tiles) {
-                int i = c_lo;
-                // sched_barrier keeps each prefetch issued ahead of the MFMAs that follow it
-                for (; i + 1 < c_hi; i += 2) {
-                    load_a(rt, i + 1, bB);
-                    __builtin_amdgcn_sched_barrier(0);
-                    chunk(bA, i);
-                    if (i + 2 < c_hi) load_a(rt, i + 2, bA);
-                    else if (next_rt < row_tiles) load_a(next_rt, c_lo, bA);
-                    __builtin_amdgcn_sched_barrier(0);
-                    chunk(bB, i + 1);
+            // CG == 1: the vector chunks' 8 steps alternate between two accumulators per plane so
+            // consecutive MFMAs are independent (16x16x4 f32: 32-cycle issue, 40-cycle latency)
+            floatx4 accv2[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) accv2[pl] = floatx4{0.f, 0.f, 0.f, 0.f};
+            auto compute_item = [&](auto ic, const float4 (&cb)[2]) {
+                constexpr int item = decltype(ic)::value;
+                constexpr bool sc = item < SK::K0;
+                const float av[8] = {cb[0].x, cb[0].y, cb[0].z, cb[0].w, cb[1].x, cb[1].y, cb[1].z, cb[1].w};
+                if constexpr (sc) {
+                    constexpr int NA = (item < SK::K0 ? 1 : 0) + (NS > 1 && item < SK::K1 ? 1 : 0) +
+                                       (NS > 2 && item < SK::K2 ? 1 : 0);
+                    float4 b[CG][NA][2];
+#pragma unroll
+                    for (int g = 0; g < CG; ++g)
+#pragma unroll
+                        for (int j = 0; j < NA; ++j) {
+                            const float* bp = &lds[g * stride_g + sub_off[j] + item * 512 + 4 * lane];
+                            b[g][j][0] = *reinterpret_cast<const float4*>(bp);
+                            b[g][j][1] = *reinterpret_cast<const float4*>(bp + 256);
+                        }
+#pragma unroll
+                    for (int s = 0; s < 8; ++s)
+#pragma unroll
+                        for (int g = 0; g < CG; ++g)
+#pragma unroll
+                            for (int j = 0; j < NA; ++j)
+                                acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], f4get(b[g][j][s >> 2], s & 3),
+                                                                                 acc[g][j], 0, 0, 0);
+                } else {
+                    constexpr int v = item - SK::K0, plane = v / SK::KV, kc = v - plane * SK::KV;
+                    float4 b[CG][2];
+#pragma unroll
+                    for (int g = 0; g < CG; ++g) {
+                        const float* bp = &lds[g * stride_g + sub_off[NS] + kc * 512 + 4 * lane];
+                        b[g][0] = *reinterpret_cast<const float4*>(bp);
+                        b[g][1] = *reinterpret_cast<const float4*>(bp + 256);
+                    }
+#pragma unroll
+                    for (int s = 0; s < 8; ++s) {
+                        if constexpr (CG == 1) {
+                            if (s & 1)
+                                accv2[plane] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], f4get(b[0][s >> 2], s & 3),
+                                                                                    accv2[plane], 0, 0, 0);
+                            else
+                                acc[0][NS + plane] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                    av[s], f4get(b[0][s >> 2], s & 3), acc[0][NS + plane], 0, 0, 0);
+                        } else {
+#pragma unroll
+                            for (int g = 0; g < CG; ++g)
+                                acc[g][NS + plane] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                    av[s], f4get(b[g][s >> 2], s & 3), acc[g][NS + plane], 0, 0, 0);
+                        }
+                    }
                 }
-                if (i < c_hi) {   // odd chunk count: the last chunk sits in bA
-                    chunk(bA, i);
-                    if (next_rt < row_tiles) load_a(next_rt, c_lo, bA);
+            };
+            if (SK::on && rt < row_tiles) {
+                if constexpr (SK::on) {
+                    slice_call([&](auto sc_) {
+                        constexpr int lo = decltype(sc_)::value * SNIT / KS;
+                        constexpr int n = (decltype(sc_)::value + 1) * SNIT / KS - lo;
+                        static_for<0, n>([&](auto uc) {
+                            constexpr int u = decltype(uc)::value;
+                            if constexpr (u + PF - 1 < n)
+                                load_item(std::integral_constant<int, lo + u + PF - 1>{}, rt, ring[(u + PF - 1) % PF]);
+                            __builtin_amdgcn_sched_barrier(0);
+                            compute_item(std::integral_constant<int, lo + u>{}, ring[u % PF]);
+                            __builtin_amdgcn_sched_barrier(0);
+                        });
+                        // the next tile's first chunks, behind this tile's epilogue
+                        static_for<0, PF - 1>([&](auto uc) {
+                            constexpr int u = decltype(uc)::value;
+                            if constexpr (u < n) load_item(std::integral_constant<int, lo + u>{}, next_rt, ring[u % PF]);
+                        });
+                    });
+                    if constexpr (CG == 1 && NV)
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) acc[0][NS + pl] += accv2[pl];
+                }
+            } else if (!SK::on && rt < row_tiles) {
+                // sched_barrier keeps each prefetch issued ahead of the MFMAs that follow it
+                for (int u0 = 0; u0 < nc_pad; u0 += PF) {
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) {
+                        int pu = u0 + u + PF - 1, prt = rt;
+                        if (pu >= nc_pad) { pu -= nc_pad; prt = next_rt; }
+                        load_a(prt, c_lo + pu, ring[(u + PF - 1) % PF]);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (u0 + u < nck) chunk(ring[u], c_lo + u0 + u);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
             }
 
@@ -225,8 +351,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                 if constexpr (EPI == TP_PLAIN) {
 #pragma unroll
                     for (int j = 0; j < NS; ++j) {
-                        const int col = ((cgroup * CG + g) * NS + j) * 16 + c16;
-                        if (col < P.ncols)
+                        const bool pm = P.col_part_stride > 0;
+                        const int col = pm ? (P.col_part0 + j) * P.col_part_stride + ch
+                                           : ((cgroup * CG + g) * NS + j) * 16 + c16;
+                        if (pm ? ch < M : col < P.ncols)
 #pragma unroll
                             for (int jj = 0; jj < 4; ++jj)
                                 if (row0 + jj < P.rows) P.C[(size_t)(row0 + jj) * P.ldc + col] = acc[g][j][jj];
@@ -410,28 +538,45 @@ int tp16_geom(TpProb& p, int num_cus, int* blocks) {
     return NBX_OK;
 }
 
-template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, bool DUAL>
+template <class SK>
+int tp16_check_static(const TpProb& p) {
+    if constexpr (SK::on) {
+        auto kc = [](int K) { return (K + 31) / 32; };
+        const bool ok = kc(p.K[0]) == SK::K0 && (p.NS < 2 || kc(p.K[1]) == SK::K1) &&
+                        (p.NS < 3 || kc(p.K[2]) == SK::K2) && (p.NV ? kc(p.Kv) : 0) == SK::KV;
+        if (!ok) {
+            set_error("tp16: static chunk schedule does not match the problem's K");
+            return NBX_E_INVAL;
+        }
+    }
+    return NBX_OK;
+}
+
+template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, bool DUAL, class SK = DynSK>
 int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
     if (b0 + b1 == 0) return NBX_OK;
+    if (int rc = tp16_check_static<SK>(p0)) return rc;
+    if (DUAL)
+        if (int rc = tp16_check_static<SK>(p1)) return rc;
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL>,
+        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
     const size_t lds = (size_t)std::max(b0 ? p0.lds_floats : 0, b1 ? p1.lds_floats : 0) * 4;
-    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL>), dim3(b0 + b1), dim3(64 * WAVES), lds, st,
-                       p0, p1, b0);
+    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>), dim3(b0 + b1), dim3(64 * WAVES), lds,
+                       st, p0, p1, b0);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }
 
 // p.chunks = number of 16-channel chunks; grid = ceil(chunks / CG) groups x blocks_per_chunk
-template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1>
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, class SK = DynSK>
 int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     int b = 0;
     if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p, num_cus, &b)) return rc;
-    return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, false>(p, p, b, 0, st);
+    return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, false, SK>(p, p, b, 0, st);
 }
 
 // two independent problems in one launch (same template shape)

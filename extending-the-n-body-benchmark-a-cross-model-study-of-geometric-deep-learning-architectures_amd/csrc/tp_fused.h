@@ -18,6 +18,8 @@
 // consecutive k (lane half h supplies k = 16h + s at MFMA step s for both
 // operands: the sum is unchanged).
 #pragma once
+#include <type_traits>
+
 #include "nbx_internal.h"
 
 namespace nbx {
@@ -39,6 +41,10 @@ struct TpProb {
     // "TP operand images"); a block copies its chunk's image into LDS verbatim
     const float* B;
     int img_floats;
+    int img_stride;      // tp16: floats between consecutive chunk images (0: img_floats)
+    // tp16 PLAIN: 0 -> column ((chunk * NS + j) * 16 + c); > 0 -> part-major output
+    // columns (col_part0 + j) * col_part_stride + chunk * 16 + c, valid below M
+    int col_part_stride, col_part0;
     int rows, chunks, M;  // M = real channels (epilogue mask)
     int epi;
     // PLAIN: C[row][chunk*NS*32 + 32 j + col]
@@ -61,6 +67,29 @@ struct TpProb {
 };
 
 constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
+
+// Chunk schedule of a TP's K loop.  DynSK: chunk counts read from TpProb at run time (any
+// shape).  StatSK<K0, K1, K2, KV>: the counts of 32-deep chunks of the scalar sub-tiles and of
+// the vector sub-tile are compile-time, so the whole per-tile stream of A chunks is unrolled with
+// static ring slots and static accumulator selection -- no branches around the MFMAs and no
+// accumulator copies at control-flow merges (the dynamic loop pays ~50 v_mov per chunk for them).
+struct DynSK {
+    static constexpr bool on = false;
+    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0;
+};
+template <int A, int B, int C, int V>
+struct StatSK {
+    static constexpr bool on = true;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V;
+};
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
 
 // v_exp_f32 + v_rcp_f32 (1 ulp) instead of the IEEE division sequence
 __device__ inline float tp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -95,7 +124,7 @@ __device__ inline void tp_img_offsets(const TpProb& P, int cw, int (&off)[NS + 1
     off[NS] = o;
 }
 
-template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2>
+template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2, class SK = DynSK>
 __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(const TpProb P) {
     constexpr int THREADS = 64 * WAVES;
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -147,8 +176,33 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     const unsigned long long c_start = P.dbg ? clock64() : 0ull;
     int rt = wid;
     float4 buf[D][4];
+    // static schedule (SK::on): items = K0 scalar chunks, then KV chunks per vector plane
+    constexpr int SNIT = SK::K0 + 3 * SK::KV;
+    auto load_item = [&](auto ic, int rt_, float4 (&a)[4]) {
+        constexpr int item = decltype(ic)::value;
+        constexpr bool sc = item < SK::K0;
+        constexpr int v = sc ? 0 : item - SK::K0;
+        constexpr int plane = sc ? 0 : v / (SK::KV > 0 ? SK::KV : 1);
+        constexpr int kc = sc ? item : v - plane * SK::KV;
+        const int row = rt_ * 32 + r;
+        const int k = kc * 32 + 16 * h;
+        const bool ok = row < P.rows && k < (sc ? P.K[0] : P.Kv);
+        const size_t eo = sc ? (size_t)row * P.lda_s + k : (size_t)plane * P.plane_stride + (size_t)row * P.lda_v + k;
+        const uint32_t off = ok ? (uint32_t)(eo * 4) : 0x7FFFFFF0u;
+        const __amdgpu_buffer_rsrc_t rs = sc ? rsS : rsV;
 #pragma unroll
-    for (int u = 0; u < D - 1; ++u) load_a(rt, u, buf[u]);
+        for (int q = 0; q < 4; ++q)
+            a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 * q : off, 0, 0));
+    };
+    if constexpr (SK::on) {
+        static_for<0, D - 1>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            if constexpr (u < SNIT) load_item(std::integral_constant<int, u>{}, rt, buf[u % D]);
+        });
+    } else {
+#pragma unroll
+        for (int u = 0; u < D - 1; ++u) load_a(rt, u, buf[u]);
+    }
 
     // ---- stage this chunk's weight image in LDS (LDS-DMA, verbatim copy)
     tp_dma_image<WAVES>(P.B + (size_t)chunk * P.img_floats, lds, P.img_floats);
@@ -207,7 +261,53 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     }
                 }
             };
-            for (int i0 = 0; i0 < nc_pad; i0 += D) {
+            auto compute_item = [&](auto ic, const float4 (&cur)[4]) {
+                constexpr int item = decltype(ic)::value;
+                if constexpr (item < SK::K0) {
+                    static_for<0, NS>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        constexpr int KCj = j == 0 ? SK::K0 : j == 1 ? SK::K1 : SK::K2;
+                        if constexpr (item < KCj) {
+                            const float* bp = &lds[off[j] + item * 1024 + 4 * lane];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const float4 b4 = *reinterpret_cast<const float4*>(bp + 256 * q);
+                                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4.x, acc[j], 0, 0, 0);
+                                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4.y, acc[j], 0, 0, 0);
+                                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4.z, acc[j], 0, 0, 0);
+                                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4.w, acc[j], 0, 0, 0);
+                            }
+                        }
+                    });
+                } else {
+                    constexpr int v = item - SK::K0, plane = v / SK::KV, kc = v - plane * SK::KV;
+                    const float* bp = &lds[off[NS] + kc * 1024 + 4 * lane];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 b4 = *reinterpret_cast<const float4*>(bp + 256 * q);
+                        acc[NS + plane] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].x, b4.x, acc[NS + plane], 0, 0, 0);
+                        acc[NS + plane] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].y, b4.y, acc[NS + plane], 0, 0, 0);
+                        acc[NS + plane] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].z, b4.z, acc[NS + plane], 0, 0, 0);
+                        acc[NS + plane] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4.w, acc[NS + plane], 0, 0, 0);
+                    }
+                }
+            };
+            if constexpr (SK::on) {
+                static_for<0, SNIT>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    if constexpr (u + D - 1 < SNIT)
+                        load_item(std::integral_constant<int, u + D - 1>{}, rt, buf[(u + D - 1) % D]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute_item(std::integral_constant<int, u>{}, buf[u % D]);
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+                // the next tile's first chunks, behind this tile's epilogue
+                static_for<0, D - 1>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    if constexpr (u < SNIT) load_item(std::integral_constant<int, u>{}, next_rt, buf[u % D]);
+                });
+            }
+            for (int i0 = 0; !SK::on && i0 < nc_pad; i0 += D) {
 #pragma unroll
                 for (int u = 0; u < D; ++u) {
                     // prefetch chunk i0 + u + D - 1 (wrapping into the next tile) into the buffer
@@ -428,7 +528,7 @@ inline void tp_geometry(TpProb& p, int waves = TP_WAVES, int num_cus = 256) {
     p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
 }
 
-template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2>
+template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2, class SK = DynSK>
 int tp_launch(const TpProb& p, hipStream_t st) {
     if (p.rows <= 0 || p.chunks <= 0) return NBX_OK;
     if ((double)p.rows * p.lda_s * 4.0 >= 2147483632.0 ||
@@ -443,11 +543,19 @@ int tp_launch(const TpProb& p, hipStream_t st) {
     }
     static bool attr_set = false;  // per instantiation
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp_fused_kernel<NS, NV, EPI, WAVES, D>,
+        NBX_HIP(hipFuncSetAttribute((const void*)tp_fused_kernel<NS, NV, EPI, WAVES, D, SK>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((tp_fused_kernel<NS, NV, EPI, WAVES, D>), dim3(p.chunks * p.blocks_per_chunk), dim3(64 * WAVES),
+    if constexpr (SK::on) {
+        auto kc = [](int K) { return (K + 31) / 32; };
+        if (!(kc(p.K[0]) == SK::K0 && (NS < 2 || kc(p.K[1]) == SK::K1) && (NS < 3 || kc(p.K[2]) == SK::K2) &&
+              (NV ? kc(p.Kv) : 0) == SK::KV)) {
+            set_error("tp_fused: static chunk schedule does not match the problem's K");
+            return NBX_E_INVAL;
+        }
+    }
+    hipLaunchKernelGGL((tp_fused_kernel<NS, NV, EPI, WAVES, D, SK>), dim3(p.chunks * p.blocks_per_chunk), dim3(64 * WAVES),
                        lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;

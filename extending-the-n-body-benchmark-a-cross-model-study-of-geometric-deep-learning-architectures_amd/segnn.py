@@ -238,8 +238,9 @@ class SEGNN(nn.Module):
     @staticmethod
     def tp_images(P: dict, mul: int) -> dict:
         """packed_matrices -> the device images the kernels stage (msg2: 32-channel
-        chunks for the 32x32 message kernel; every node TP: 16-channel chunks, the
-        chunk count padded to a multiple of 4 so any channel-group size <= 4 divides it)."""
+        chunks for the 32x32 message kernel; every other TP: 16-channel chunks, the
+        chunk count padded to a multiple of 4 so any channel-group size <= 4 divides it;
+        node_pre: 6 parts [P_dst s|gate|t, P_src s|gate|t] per 16-channel chunk)."""
         M = mul
         c16 = -(-M // 16)
         c16 = -(-c16 // 4) * 4
@@ -250,12 +251,9 @@ class SEGNN(nn.Module):
             pre, base = (key.rsplit(".", 1) + [""])[:2] if "." in key else ("", key)
             pre = pre + "." if pre else ""
             if base in ("node_pre_s_t", "node_pre_v_t"):
-                B = P[key]                                    # [6M][M]: 48-column chunks of 3 x 16
-                n48 = -(-6 * M // 48)
-                n48p = -(-n48 // 4) * 4
-                B = torch.nn.functional.pad(B, (0, 0, 0, n48p * 48 - 6 * M)).reshape(n48p, 3, 16, M)
-                subs = [(B[:, j].reshape(n48p * 16, M), M) for j in range(3)]
-                out[pre + base[:-2] + "_img"] = img(subs, None, 16, n48p)
+                B = P[key]                                    # [6M][M]: 6 parts of M output columns
+                subs = [(B[j * M:(j + 1) * M], M) for j in range(6)]
+                out[pre + base[:-2] + "_img"] = img(subs, None, 16, c16)
             elif base in ("msg2_s_t", "upd1_s_t", "upd2_s_t", "pp1_s_t"):
                 stem = base[:-4]
                 S, V = P[key], P[pre + stem + "_v_t"]

@@ -98,8 +98,8 @@ int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size,
  *     CW = 32 (v_mfma_f32_32x32x2_f32): [q 4][h 2][c 32][e 4]     = W[c][32 kc + 16 h + 4 q + e]
  *   so lane l of a wave reads 16 contiguous bytes per ds_read_b128 (bank-conflict free).
  * msg2_img uses CW = 32 with ceil(mul/32) chunks; every other image CW = 16 with
- * ceil(.../16) chunks rounded up to a multiple of 4.  node_pre: NS = 3 parts of 16
- * columns per chunk = output columns [48 c + 16 j, 48 c + 16 j + 16) of the *_t matrix.
+ * ceil(mul/16) chunks rounded up to a multiple of 4.  node_pre: 6 parts of mul
+ * columns (P_dst s, gate, t, P_src s, gate, t), chunk c = channels [16 c, 16 c + 16) of each.
  */
 #define NBX_SEGNN_MAX_LAYERS 64
 

@@ -56,8 +56,8 @@ def test_tp_images_shapes(hidden):
     P = SEGNN.tp_images(m.packed_matrices(), M)
     kc = lambda K: -(-K // 32)  # noqa: E731
     c16 = -(-(-(-M // 16)) // 4) * 4
-    n48 = -(-(-(-6 * M // 48)) // 4) * 4
-    assert P["layers.0.node_pre_s_img"].shape == (n48, 3 * kc(M) * 512)
+    assert P["layers.0.node_pre_s_img"].shape == (c16, 6 * kc(M) * 512)
+    assert P["layers.0.node_pre_v_img"].shape == (c16, 6 * kc(M) * 512)
     assert P["layers.0.msg2_img"].shape == (-(-M // 32), (2 * kc(2 * M) + 2 * kc(M)) * 1024)
     assert P["layers.1.upd1_img"].shape == (c16, (2 * kc(4 * M) + 2 * kc(2 * M)) * 512)
     assert P["layers.1.upd2_img"].shape == (c16, (kc(2 * M) + 2 * kc(M)) * 512)
