@@ -32,6 +32,7 @@ struct MsgPreProb {
     const float* EG;     // [V*G][8] per edge slot: rhat xyz, |rel|, m_src m_dst
     const float* amf;    // [2][3M] (dist, m_i m_j) -> (s, gate, t)
     const float* bias;   // [2M]   (s, gate)
+    const float* xcoef;  // pending feature BatchNorm of X (previous layer): [sc_s(M) | sc_v(M) | sh(M)], or null
     float* M1S;          // [V*G][2M]
     float* M1V;          // [3][V*G][M]
     long V;
@@ -42,15 +43,21 @@ struct MsgPreProb {
     int per_chunk;       // persistent blocks per chunk
     int img_floats;      // F = 6 * ceil(M/32) * 512
     unsigned long long* dbg;  // optional per-wave phase clocks (tuning only)
+    int diag;                 // tuning only: 1 = edge waves idle (timing of the GEMM side alone)
 };
 
 constexpr int MP_THREADS = 512;
-constexpr int MP_EX = 4 * 6 * 256;   // one exchange buffer: [4 planes][6 parts][16 rows][16 channels]
+// one exchange buffer: [4 planes][6 parts][16 rows][MP_RS], 16 channels per row padded to 20
+// floats so the GEMM waves' stores (lane quarters qd = 0/1 hold rows 4 apart) hit different
+// bank halves, while rows stay 16-byte aligned for the edge waves' ds_read_b128
+constexpr int MP_RS = 20, MP_PART = 16 * MP_RS;
+constexpr int MP_EX = 4 * 6 * MP_PART;
 
 __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
     float* EX = lds + 2 * F;   // [2 buffers][MP_EX]
+    float* XC = EX + 2 * MP_EX;  // pending BN of X per k: [sc_s | sc_v | sh] x (KC * 32), zero past M
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
     const bool gemm_wave = wave < 4;
     const int plane = wave & 3;
@@ -85,6 +92,15 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
     // both weight images of this chunk -> LDS (DMA, verbatim)
     tp_dma_image<8>(P.Simg + (size_t)chunk * F, lds, F);
     tp_dma_image<8>(P.Vimg + (size_t)chunk * F, lds + F, F);
+
+    // the previous layer's feature BatchNorm is applied to X here, as it is loaded (lazy BN:
+    // X in HBM holds the pre-normalisation values); identity when xcoef is null
+    for (int i = t; i < 3 * KC * 32; i += MP_THREADS) {
+        const int part = i / (KC * 32), k = i - part * KC * 32;
+        float v = 0.f;
+        if (k < M) v = P.xcoef ? P.xcoef[part * M + k] : (part < 2 ? 1.f : 0.f);
+        XC[i] = v;
+    }
 
     // edge waves: thread = (edge slot of the group, channel quad cq); per-quad constants
     const int et = t - 256, cq = et & 3, ch0 = chunk * 16 + 4 * cq;
@@ -140,8 +156,19 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
                 for (int kc = 0; kc < KCMAX; ++kc) {
                     if (kc >= KC) break;
                     if (kc + 1 < KC) load_b(kc + 1, b[(kc + 1) & 1]);
-                    const float av[8] = {abuf[kc][0].x, abuf[kc][0].y, abuf[kc][0].z, abuf[kc][0].w,
-                                         abuf[kc][1].x, abuf[kc][1].y, abuf[kc][1].z, abuf[kc][1].w};
+                    // x = sc * x~ + sh (shift on the 0e plane only)
+                    const float* xc = XC + (plane ? KC * 32 : 0) + kc * 32 + 8 * qd;
+                    const float4 sc0 = *reinterpret_cast<const float4*>(xc);
+                    const float4 sc1 = *reinterpret_cast<const float4*>(xc + 4);
+                    float4 sh0{0.f, 0.f, 0.f, 0.f}, sh1{0.f, 0.f, 0.f, 0.f};
+                    if (plane == 0) {
+                        sh0 = *reinterpret_cast<const float4*>(XC + 2 * KC * 32 + kc * 32 + 8 * qd);
+                        sh1 = *reinterpret_cast<const float4*>(XC + 2 * KC * 32 + kc * 32 + 8 * qd + 4);
+                    }
+                    const float av[8] = {fmaf(sc0.x, abuf[kc][0].x, sh0.x), fmaf(sc0.y, abuf[kc][0].y, sh0.y),
+                                         fmaf(sc0.z, abuf[kc][0].z, sh0.z), fmaf(sc0.w, abuf[kc][0].w, sh0.w),
+                                         fmaf(sc1.x, abuf[kc][1].x, sh1.x), fmaf(sc1.y, abuf[kc][1].y, sh1.y),
+                                         fmaf(sc1.z, abuf[kc][1].z, sh1.z), fmaf(sc1.w, abuf[kc][1].w, sh1.w)};
                     const float4 (&bc)[6][2] = b[kc & 1];
 #pragma unroll
                     for (int s = 0; s < 8; ++s)
@@ -154,21 +181,21 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
 #pragma unroll
                 for (int kc = 0; kc < KCMAX; ++kc)
                     if (kc < KC) load_a(i + 1, kc, abuf[kc]);
-                float* ex = EX + (i & 1) * MP_EX + plane * 6 * 256;
+                float* ex = EX + (i & 1) * MP_EX + plane * 6 * MP_PART;
 #pragma unroll
                 for (int j = 0; j < 6; ++j)
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) ex[j * 256 + (4 * qd + jj) * 16 + c16] = acc[j][jj];
+                    for (int jj = 0; jj < 4; ++jj) ex[j * MP_PART + (4 * qd + jj) * MP_RS + c16] = acc[j][jj];
                 tick(c_gemm);
             }
-        } else if (i > 0 && live) {
+        } else if (i > 0 && live && !P.diag) {
             // ---- edges of group i-1
             const float4 geo_cur = geo_next;
             const float pm_cur = pm_next;
             load_geo(i, geo_next, pm_next);
             const float* exb = EX + ((i - 1) & 1) * MP_EX + 4 * cq;
             auto xv = [&](int pl, int part, int row) {
-                return *reinterpret_cast<const float4*>(exb + (pl * 6 + part) * 256 + row * 16);
+                return *reinterpret_cast<const float4*>(exb + (pl * 6 + part) * MP_PART + row * MP_RS);
             };
             const int64_t node0 = (int64_t)(pblk + (i - 1) * P.per_chunk) * NG;
             for (int it = et >> 2; it < group_items; it += 64) {
@@ -225,7 +252,9 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
     }
 }
 
-inline size_t msg_pre_lds_bytes(const MsgPreProb& p) { return ((size_t)2 * p.img_floats + 2 * MP_EX) * 4; }
+inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
+    return ((size_t)2 * p.img_floats + 2 * MP_EX + 3 * 32 * ((p.M + 31) / 32)) * 4;
+}
 
 // nodes per group for systems of N nodes (0 if the fused path does not apply)
 inline int msg_pre_group(int N) { return (N >= 2 && N <= 16) ? (16 / N) * N : 0; }

@@ -220,19 +220,23 @@ __global__ void bn_finalize_kernel(const double* __restrict__ partial, int wpc, 
 // sum_j BN(m_ij) = scale * sum_j m_ij + deg * shift), then the update_layer_1
 // GEMM inputs: U1S [V][4M] = [x_s | a_s | x_v.na | a_v.na], U1V [3][V][2M] = [x_v[:,k] | a_v[:,k]]
 __global__ void upd_pre_kernel(const float* __restrict__ X, const float* __restrict__ AGG,
-                               const float* __restrict__ NA, const float* __restrict__ coef, float deg, int64_t V,
-                               int M, float* __restrict__ U1S, float* __restrict__ U1V) {
+                               const float* __restrict__ NA, const float* __restrict__ coef,
+                               const float* __restrict__ xcoef, float deg, int64_t V, int M,
+                               float* __restrict__ U1S, float* __restrict__ U1V) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
     const float sc_s = coef[w], sc_v = coef[M + w], sh = coef[2 * M + w] * deg;
+    // pending feature BatchNorm of X (previous layer; identity for layer 0)
+    const float xs_sc = xcoef ? xcoef[w] : 1.f, xv_sc = xcoef ? xcoef[M + w] : 1.f;
+    const float xs_sh = xcoef ? xcoef[2 * M + w] : 0.f;
     for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
         const float* na = NA + 4 * n;
-        const float xs = X[n * M + w];
+        const float xs = fmaf(xs_sc, X[n * M + w], xs_sh);
         const float as = sc_s * AGG[n * M + w] + sh;
         float xdot = 0.f, adot = 0.f;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const float xv = X[((1 + k) * V + n) * M + w];
+            const float xv = xv_sc * X[((1 + k) * V + n) * M + w];
             const float av = sc_v * AGG[((1 + k) * V + n) * M + w];
             xdot += xv * na[1 + k];
             adot += av * na[1 + k];
@@ -580,6 +584,7 @@ int run_msg_pre(nbx::MsgPreProb& p, hipStream_t st, KernelTiming* tm) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
     if (debug) {
         p.dbg = tp_dbg_buf(st);
+        p.diag = getenv("NBX_MP_NOEDGE") != nullptr;
         if (int rc = nbx::msg_pre_launch(p, st)) return rc;
         const int n = p.chunks * p.per_chunk * 8;
         std::vector<unsigned long long> h((size_t)n * 4);
@@ -667,14 +672,25 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     hipLaunchKernelGGL(embed_kernel, ew_grid(V, M), ewb, 0, st, ws.X0, ws.NA, w->emb, w->emb_bias, V, M, ws.X);
     NBX_LAUNCH_CHECK("embed");
 
+    // Lazy feature BatchNorm: X in HBM holds each layer's pre-normalisation output and its
+    // consumers in the next layer (message_layer_1, the update inputs, the residual) apply
+    // the pending per-channel scale/shift (ws.coef_feat) as they read it; null = identity.
+    const bool fused_msg = N > 1 && nbx::msg_pre_group((int)N) > 0 && M <= 128;
     for (int l = 0; l < w->num_layers; ++l) {
         const nbx_segnn_layer& L = w->layers[l];
-        if (N > 1 && nbx::msg_pre_group((int)N) > 0 && M <= 128) {
+        const float* xprev = l > 0 ? ws.coef_feat : nullptr;
+        if (xprev && !fused_msg && N > 1) {
+            // the unfused message path reads X directly: normalise it in place first
+            hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M);
+            NBX_LAUNCH_CHECK("bn_apply");
+            xprev = nullptr;
+        }
+        if (fused_msg) {
             // message_layer_1: node precomputation + edge combination + gate in one kernel
             nbx::MsgPreProb mp;
             memset(&mp, 0, sizeof(mp));
             mp.X = ws.X; mp.Simg = L.node_pre_s_img; mp.Vimg = L.node_pre_v_img; mp.EG = ws.EG;
-            mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V;
+            mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V; mp.xcoef = xprev;
             mp.V = V; mp.N = (int)N; mp.G = (int)d.G; mp.M = M; mp.NG = nbx::msg_pre_group((int)N);
             if (int rc = run_msg_pre(mp, st, tm)) return rc;
         } else if (N > 1) {
@@ -728,7 +744,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                            w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
                            L.msg_bn_running_var, ws.coef_msg);
         NBX_LAUNCH_CHECK("bn_finalize(msg)");
-        hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg,
+        hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg, xprev,
                            (float)(N - 1), V, M, ws.U1S, ws.U1V);
         NBX_LAUNCH_CHECK("upd_pre");
         {
@@ -751,6 +767,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
+            p.xcoef = xprev;
             p.chunks = (M + 15) / 16;
             if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             wpc_feat = p.waves_per_chunk;
@@ -758,6 +775,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
                            wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
                            L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat);
+    }
+    // the last layer's feature BatchNorm, before the pre-pooling TPs
+    if (w->num_layers > 0) {
         hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M);
         NBX_LAUNCH_CHECK("bn_apply");
     }

@@ -436,6 +436,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                 } else if constexpr (EPI == TP_RESID) {
                     const bool live = ch < M;
                     const float b = live ? P.bias[ch] : 0.f;
+                    // the residual X still carries the previous layer's pending BatchNorm
+                    const float xs_sc = live && P.xcoef ? P.xcoef[ch] : 1.f;
+                    const float xv_sc = live && P.xcoef ? P.xcoef[M + ch] : 1.f;
+                    const float xs_sh = live && P.xcoef ? P.xcoef[2 * M + ch] : 0.f;
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) {
                         const int row = row0 + jj;
@@ -443,14 +447,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                         const float* na = P.geom + (size_t)row * 4;
                         const float tt = acc[g][1][jj];
                         float* xs = P.out_s + (size_t)row * M + ch;
-                        const float s = *xs + (acc[g][0][jj] + b);
+                        const float s = fmaf(xs_sc, *xs, xs_sh) + (acc[g][0][jj] + b);
                         *xs = s;
                         float* x0 = P.out_v + (size_t)row * M + ch;
                         float* x1 = x0 + P.out_plane;
                         float* x2 = x1 + P.out_plane;
-                        const float v0 = *x0 + (na[1] * tt + acc[g][NS + 0][jj]);
-                        const float v1 = *x1 + (na[2] * tt + acc[g][NS + 1][jj]);
-                        const float v2 = *x2 + (na[3] * tt + acc[g][NS + 2][jj]);
+                        const float v0 = xv_sc * *x0 + (na[1] * tt + acc[g][NS + 0][jj]);
+                        const float v1 = xv_sc * *x1 + (na[2] * tt + acc[g][NS + 1][jj]);
+                        const float v2 = xv_sc * *x2 + (na[3] * tt + acc[g][NS + 2][jj]);
                         *x0 = v0; *x1 = v1; *x2 = v2;
                         st0[g] += (double)s;
                         st1[g] += (double)s * s;

@@ -53,6 +53,7 @@ struct TpProb {
     // epilogue operands
     const float* bias;   // gate: [2M] (s, gate); resid: [M]
     const float* geom;   // MSG: per-edge [rows][8] (rhat xyz ...); GATE_NODE/RESID: node attrs [rows][4]
+    const float* xcoef;  // RESID: pending feature BN of the residual X [sc_s | sc_v | sh] (M each), or null
     int group;           // MSG: edges per destination (power of two <= 32)
     int valid_per_group; // MSG: real edges per destination (<= group)
     float* out_s;        // MSG: AGG plane 0 [nodes][M]; GATE_NODE: U2S [rows][2M]; RESID: X plane 0
