@@ -132,11 +132,13 @@ def bench_segnn(a, rank, world, device, P):
             n_k[k] += kn[k]
             fl_k[k] += kfl[k]
         fwd_ms += tot.value
-    # rocprofv3 names of the four fused TP launch kinds (csrc/segnn.hip::forward_impl)
-    names = ["void nbx::tp16_kernel<3, 0, 0, 2, 8, 3, 1, true>(nbx::TpProb, nbx::TpProb, int)", "void nbx::tp_fused_kernel<3, 1, 1>(nbx::TpProb)",
-             "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false>(nbx::TpProb, nbx::TpProb, int)",
-             "void nbx::tp16_kernel<2, 1, 3, 2, 8, 3, 2, false>(nbx::TpProb, nbx::TpProb, int)"]
-    roles = ["message_layer_1 node halves", "message_layer_2 + gate + aggregation + BN sums",
+    # rocprofv3 names of the four timed launch kinds at C2 (csrc/segnn.hip::forward_impl)
+    names = ["nbx::msg_pre_kernel(nbx::MsgPreProb)",
+             "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3> >(nbx::TpProb)",
+             "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSK<12, 12, 6, 6> >(nbx::TpProb, nbx::TpProb, int)",
+             "void nbx::tp16_kernel<2, 1, 3, 2, 8, 3, 2, false, nbx::StatSK<6, 3, 0, 3> >(nbx::TpProb, nbx::TpProb, int)"]
+    roles = ["message_layer_1: node GEMM + edge combination + gate (flops: the node GEMM)",
+             "message_layer_2 + gate + aggregation + BN sums",
              "update_layer_1 + gate (pre_pool1 uses CG=2)", "update_layer_2 + residual + BN sums"]
     per_kind = {}
     for k in range(4):
