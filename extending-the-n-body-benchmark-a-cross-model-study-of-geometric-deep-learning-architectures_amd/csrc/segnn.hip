@@ -84,7 +84,7 @@ __global__ void featurize_kernel(const float* __restrict__ pos, const float* __r
 // embedding_layer: O3TensorProduct(2x1o+1x0e -> hidden, node attrs) (segnn.py:69-71,170)
 __global__ void embed_kernel(const float* __restrict__ X0, const float* __restrict__ NA,
                              const float* __restrict__ emb, const float* __restrict__ emb_b, int64_t V, int M,
-                             float* __restrict__ X) {
+                             float* __restrict__ X, float* __restrict__ XD) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
     const float a0 = emb[w], a1 = emb[M + w], b0 = emb[2 * M + w], b1 = emb[3 * M + w];
@@ -95,8 +95,14 @@ __global__ void embed_kernel(const float* __restrict__ X0, const float* __restri
         const float u0n = x0[0] * na[1] + x0[1] * na[2] + x0[2] * na[3];
         const float u1n = x0[3] * na[1] + x0[4] * na[2] + x0[5] * na[3];
         X[n * M + w] = b0 * u0n + b1 * u1n + c * x0[6] + bias;
+        float xd = 0.f;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) X[((1 + k) * V + n) * M + w] = a0 * x0[k] + a1 * x0[3 + k] + dd * x0[6] * na[1 + k];
+        for (int k = 0; k < 3; ++k) {
+            const float xv = a0 * x0[k] + a1 * x0[3 + k] + dd * x0[6] * na[1 + k];
+            X[((1 + k) * V + n) * M + w] = xv;
+            xd += xv * na[1 + k];
+        }
+        if (XD) XD[n * M + w] = xd;   // x_v . na, an input of update_layer_1
     }
 }
 
@@ -249,7 +255,8 @@ __global__ void upd_pre_kernel(const float* __restrict__ X, const float* __restr
 }
 
 // feature BatchNorm apply (in place on X)
-__global__ void bn_apply_kernel(float* __restrict__ X, const float* __restrict__ coef, int64_t V, int M) {
+__global__ void bn_apply_kernel(float* __restrict__ X, const float* __restrict__ coef, int64_t V, int M,
+                                float* __restrict__ XD) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
     const float sc_s = coef[w], sc_v = coef[M + w], sh = coef[2 * M + w];
@@ -257,6 +264,7 @@ __global__ void bn_apply_kernel(float* __restrict__ X, const float* __restrict__
         X[n * M + w] = sc_s * X[n * M + w] + sh;
 #pragma unroll
         for (int k = 0; k < 3; ++k) X[((1 + k) * V + n) * M + w] *= sc_v;
+        if (XD) XD[n * M + w] *= sc_v;   // x_v . na is linear in x_v
     }
 }
 
@@ -363,6 +371,7 @@ int64_t partial_doubles(const Dims& d) {
 
 struct Workspace {
     float *X, *NA, *X0, *EG, *NP, *M1S, *M1V, *AGG, *U1S, *U1V, *U2S, *U2V, *coef_msg, *coef_feat, *out;
+    float *XD, *AD;   // x_v . na and aggregated a_v . na per node and channel (segmented update_layer_1)
     double* partial;
     size_t bytes;
 };
@@ -394,6 +403,8 @@ size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
     w.coef_msg = (float*)take(3 * M, 4);
     w.coef_feat = (float*)take(3 * M, 4);
     w.out = (float*)take(6 * V, 4);
+    w.XD = (float*)take(V * M, 4);
+    w.AD = (float*)take(V * M, 4);
     w.bytes = (off + 255) & ~size_t(255);
     if (ws) *ws = w;
     return w.bytes;
@@ -467,6 +478,8 @@ bool sk_matches(const nbx::TpProb& p, int NS, int NV) {
 // K chunk schedules per TP at mul = 96 and mul = 32
 using SK_UPD1 = nbx::StatSK<12, 12, 6, 6>;
 using SK_UPD1_32 = nbx::StatSK<4, 4, 2, 2>;
+using SK_UPD1_SEG = nbx::StatSK<12, 12, 6, 6, 4>;
+using SK_UPD1_32_SEG = nbx::StatSK<4, 4, 2, 2, 4>;
 using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
 using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
 using SK_GATE = nbx::StatSK<6, 6, 3, 3>;     // pre_pool1 (and message_layer_2's shape)
@@ -669,7 +682,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
 
     hipLaunchKernelGGL(featurize_kernel, dim3((unsigned)nbx::ceil_div(V, 256)), dim3(256), 0, st, pos, vel, mass, V,
                        (int)N, (int)d.G, ws.NA, ws.X0, ws.EG);
-    hipLaunchKernelGGL(embed_kernel, ew_grid(V, M), ewb, 0, st, ws.X0, ws.NA, w->emb, w->emb_bias, V, M, ws.X);
+    // update_layer_1 reads its [x | BN(agg)] input straight from X / AGG and the two dot buffers
+    // (no materialised U1) when the static segmented schedule applies (mul = 96 or 32)
+    const bool seg_upd = static_enabled() && (M == 96 || M == 32);
+    hipLaunchKernelGGL(embed_kernel, ew_grid(V, M), ewb, 0, st, ws.X0, ws.NA, w->emb, w->emb_bias, V, M, ws.X,
+                       seg_upd ? ws.XD : nullptr);
     NBX_LAUNCH_CHECK("embed");
 
     // Lazy feature BatchNorm: X in HBM holds each layer's pre-normalisation output and its
@@ -681,7 +698,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         const float* xprev = l > 0 ? ws.coef_feat : nullptr;
         if (xprev && !fused_msg && N > 1) {
             // the unfused message path reads X directly: normalise it in place first
-            hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M);
+            hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M,
+                               seg_upd ? ws.XD : nullptr);
             NBX_LAUNCH_CHECK("bn_apply");
             xprev = nullptr;
         }
@@ -730,12 +748,14 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.Av = ws.M1V; p.lda_v = M; p.plane_stride = Ep * M; p.Kv = M;
             p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G; p.valid_per_group = (int)(N - 1);
             p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
+            if (seg_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
             if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
                 if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm)) return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
             } else {
                 NBX_HIP(hipMemsetAsync(ws.AGG, 0, sizeof(float) * 4 * V * M, st));
+                NBX_HIP(hipMemsetAsync(ws.AD, 0, sizeof(float) * V * M, st));
                 NBX_HIP(hipMemsetAsync(ws.partial, 0, sizeof(double) * 48 * ((M + 15) / 16), st));
             }
         }
@@ -744,19 +764,39 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                            w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
                            L.msg_bn_running_var, ws.coef_msg);
         NBX_LAUNCH_CHECK("bn_finalize(msg)");
-        hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg, xprev,
-                           (float)(N - 1), V, M, ws.U1S, ws.U1V);
-        NBX_LAUNCH_CHECK("upd_pre");
-        {
-            // update_layer_1 + gate -> inputs of update_layer_2
+        if (seg_upd) {
+            // update_layer_1 + gate, input segments [x_s | a_s | x_v.na | a_v.na] and [x_v | a_v]
+            // read from X / AGG / XD / AD with the pending feature BN and the message BN applied
+            // per (segment, channel) as the A chunks are consumed
             nbx::TpProb p = tp_base((int)V, d);
-            p.As = ws.U1S; p.lda_s = 4 * M; p.B = L.upd1_img;
-            p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M;
-            p.Av = ws.U1V; p.lda_v = 2 * M; p.plane_stride = V * 2 * M;
-            p.Kv = 2 * M;
+            p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M; p.Kv = 2 * M;
+            p.lda_s = 4 * M; p.lda_v = 2 * M;
+            p.seg_s[0] = ws.X; p.seg_s[1] = ws.AGG; p.seg_s[2] = ws.XD; p.seg_s[3] = ws.AD;
+            p.seg_v[0] = ws.X + V * M; p.seg_v[1] = ws.AGG + V * M; p.seg_vplane = V * M;
+            p.xcoef = xprev; p.mcoef = ws.coef_msg; p.deg = (float)(N - 1);
+            p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
-            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 1, SK_UPD1, SK_UPD1_32>(p, st, tm)) return rc;
+            if (M == 96) {
+                if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG>(p, st, tm)) return rc;
+            } else {
+                if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG>(p, st, tm)) return rc;
+            }
+        } else {
+            hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg, xprev,
+                               (float)(N - 1), V, M, ws.U1S, ws.U1V);
+            NBX_LAUNCH_CHECK("upd_pre");
+            {
+                // update_layer_1 + gate -> inputs of update_layer_2
+                nbx::TpProb p = tp_base((int)V, d);
+                p.As = ws.U1S; p.lda_s = 4 * M; p.B = L.upd1_img;
+                p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M;
+                p.Av = ws.U1V; p.lda_v = 2 * M; p.plane_stride = V * 2 * M;
+                p.Kv = 2 * M;
+                p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
+                p.chunks = (M + 15) / 16;
+                if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 1, SK_UPD1, SK_UPD1_32>(p, st, tm)) return rc;
+            }
         }
         int wpc_feat;
         {
@@ -768,6 +808,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
             p.xcoef = xprev;
+            if (seg_upd) { p.out_dot = ws.XD; }
             p.chunks = (M + 15) / 16;
             if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             wpc_feat = p.waves_per_chunk;
@@ -778,7 +819,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     }
     // the last layer's feature BatchNorm, before the pre-pooling TPs
     if (w->num_layers > 0) {
-        hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M);
+        hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M, (float*)nullptr);
         NBX_LAUNCH_CHECK("bn_apply");
     }
     // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)

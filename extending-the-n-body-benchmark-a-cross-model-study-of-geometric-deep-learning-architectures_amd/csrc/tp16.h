@@ -109,13 +109,27 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
         constexpr int plane = sc ? 0 : v / (SK::KV > 0 ? SK::KV : 1);
         constexpr int kc = sc ? item : v - plane * SK::KV;
         const int row = rt_ * 16 + c16;
-        const int k = kc * 32 + 8 * qd;
-        const bool ok = row < P.rows && k < (sc ? P.K[0] : P.Kv);
-        const size_t eo = sc ? (size_t)row * P.lda_s + k : (size_t)plane * P.plane_stride + (size_t)row * P.lda_v + k;
-        const uint32_t off = ok ? (uint32_t)(eo * 4) : 0x7FFFFFF0u;
-        const __amdgpu_buffer_rsrc_t rs = sc ? rsS : rsV;
-        a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
+        if constexpr (SK::SEG == 4) {
+            // segment q of width M = (K0 / 4) chunks (scalar) or (KV / 2) chunks (vector)
+            constexpr int cps = sc ? SK::K0 / 4 : SK::KV / 2;
+            constexpr int q = kc / cps, kk = (kc - q * cps) * 32;
+            const int k = kk + 8 * qd;
+            const bool ok = row < P.rows;
+            const float* base = sc ? P.seg_s[q] : P.seg_v[q] + (size_t)plane * P.seg_vplane;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFF0, 0x00020000);
+            const uint32_t off = ok ? (uint32_t)(((size_t)row * P.M + k) * 4) : 0x7FFFFFF0u;
+            a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+            a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
+        } else {
+            const int k = kc * 32 + 8 * qd;
+            const bool ok = row < P.rows && k < (sc ? P.K[0] : P.Kv);
+            const size_t eo =
+                sc ? (size_t)row * P.lda_s + k : (size_t)plane * P.plane_stride + (size_t)row * P.lda_v + k;
+            const uint32_t off = ok ? (uint32_t)(eo * 4) : 0x7FFFFFF0u;
+            const __amdgpu_buffer_rsrc_t rs = sc ? rsS : rsV;
+            a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+            a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
+        }
     };
     auto slice_call = [&](auto&& fn) {
         static_for<0, KS>([&](auto sc_) {
@@ -145,6 +159,27 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
 #pragma unroll
             for (int g = 0; g < CG; ++g)
                 tp_dma_image<WAVES>(P.B + (size_t)(cgroup * CG + g) * stride, lds + g * P.img_floats, P.img_floats);
+        }
+    }
+    // segmented update input: per-(segment, k) scale / shift table, after the images
+    float* segtab = lds + CG * P.img_floats;
+    if constexpr (SK::SEG == 4) {
+        const int M = P.M;
+        for (int i = t; i < 10 * M; i += THREADS) {
+            const int part = i / M, k = i - part * M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
+            float v;
+            switch (part) {
+                case 0: v = P.xcoef ? P.xcoef[k] : 1.f; break;
+                case 1: v = P.mcoef[k]; break;
+                case 2: v = P.xcoef ? P.xcoef[M + k] : 1.f; break;
+                case 3: v = P.mcoef[M + k]; break;
+                case 4: v = P.xcoef ? P.xcoef[2 * M + k] : 0.f; break;
+                case 5: v = P.deg * P.mcoef[2 * M + k]; break;
+                case 8: v = P.xcoef ? P.xcoef[M + k] : 1.f; break;
+                case 9: v = P.mcoef[M + k]; break;
+                default: v = 0.f;
+            }
+            segtab[i] = v;
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -229,7 +264,28 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
             auto compute_item = [&](auto ic, const float4 (&cb)[2]) {
                 constexpr int item = decltype(ic)::value;
                 constexpr bool sc = item < SK::K0;
-                const float av[8] = {cb[0].x, cb[0].y, cb[0].z, cb[0].w, cb[1].x, cb[1].y, cb[1].z, cb[1].w};
+                float av[8] = {cb[0].x, cb[0].y, cb[0].z, cb[0].w, cb[1].x, cb[1].y, cb[1].z, cb[1].w};
+                if constexpr (SK::SEG == 4) {
+                    constexpr int kc = sc ? item : (item - SK::K0) % SK::KV;
+                    constexpr int cps = sc ? SK::K0 / 4 : SK::KV / 2;
+                    constexpr int q = kc / cps, kk = (kc - q * cps) * 32;
+                    const int M = P.M;
+                    const float* tsc = segtab + (sc ? q * M : 8 * M + q * M) + kk + 8 * qd;
+                    const float4 s0 = *reinterpret_cast<const float4*>(tsc);
+                    const float4 s1 = *reinterpret_cast<const float4*>(tsc + 4);
+                    const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                    if constexpr (sc && q < 2) {
+                        const float* tsh = segtab + 4 * M + q * M + kk + 8 * qd;
+                        const float4 h0 = *reinterpret_cast<const float4*>(tsh);
+                        const float4 h1 = *reinterpret_cast<const float4*>(tsh + 4);
+                        const float shv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) av[e] = fmaf(scv[e], av[e], shv[e]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) av[e] *= scv[e];
+                    }
+                }
                 if constexpr (sc) {
                     constexpr int NA = (item < SK::K0 ? 1 : 0) + (NS > 1 && item < SK::K1 ? 1 : 0) +
                                        (NS > 2 && item < SK::K2 ? 1 : 0);
@@ -455,6 +511,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                         const float v0 = xv_sc * *x0 + (na[1] * tt + acc[g][NS + 0][jj]);
                         const float v1 = xv_sc * *x1 + (na[2] * tt + acc[g][NS + 1][jj]);
                         const float v2 = xv_sc * *x2 + (na[3] * tt + acc[g][NS + 2][jj]);
+                        if (P.out_dot) P.out_dot[(size_t)row * M + ch] = v0 * na[1] + v1 * na[2] + v2 * na[3];
                         *x0 = v0; *x1 = v1; *x2 = v2;
                         st0[g] += (double)s;
                         st1[g] += (double)s * s;
@@ -520,7 +577,7 @@ int tp16_geom(TpProb& p, int num_cus, int* blocks) {
             return NBX_E_INVAL;
         }
     p.img_floats = tp_img_floats(p, 16);
-    p.lds_floats = tp16_lds_floats<CG>(p);
+    p.lds_floats = tp16_lds_floats<CG>(p) + (p.seg_s[0] ? ((10 * p.M + 3) & ~3) : 0);
     if (KS > 1) p.lds_floats += (WAVES / KS) * (KS - 1) * CG * (NS + 3 * NV) * 4 * 64;
     const size_t lds = (size_t)p.lds_floats * 4;
     if (lds > 160 * 1024) {
@@ -550,6 +607,11 @@ int tp16_check_static(const TpProb& p) {
                         (p.NS < 3 || kc(p.K[2]) == SK::K2) && (p.NV ? kc(p.Kv) : 0) == SK::KV;
         if (!ok) {
             set_error("tp16: static chunk schedule does not match the problem's K");
+            return NBX_E_INVAL;
+        }
+        if (SK::SEG == 4 && (p.M * 4 != SK::K0 * 32 || p.M * 2 != SK::KV * 32 || !p.seg_s[0] || !p.seg_s[1] ||
+                             !p.seg_s[2] || !p.seg_s[3] || !p.seg_v[0] || !p.seg_v[1] || !p.mcoef)) {
+            set_error("tp16: segmented update input needs mul %% 32 == 0 and all segment pointers");
             return NBX_E_INVAL;
         }
     }

@@ -65,6 +65,20 @@ struct TpProb {
     int blocks_per_chunk;
     int lds_floats;
     unsigned long long* dbg;  // optional per-wave phase clocks [waves][4] (tuning only)
+    // tp16 static path with StatSK<..., SEG = 4> (update_layer_1 without a materialised input):
+    // scalar A = 4 segments of M columns read from seg_s[q] ([rows][M]: x_s, a_s, x_v.na, a_v.na),
+    // vector A = 2 segments from seg_v[q] (planes seg_vplane apart: x_v, a_v); each element is
+    // scaled / shifted per (segment, k): x segments by the pending feature BN (xcoef, or identity),
+    // a segments by the message BN (mcoef, shift x deg)
+    const float* seg_s[4];
+    const float* seg_v[2];
+    long seg_vplane;
+    const float* mcoef;
+    float deg;
+    // dot outputs (null: none): MSG: out_dot[dst][ch] = sum_k a_v,k na_k[dst] (na: node attrs
+    // [V][4]); RESID: out_dot[row][ch] = sum_k x_v,k na_k[row] of the new x
+    const float* na;
+    float* out_dot;
 };
 
 constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
@@ -76,12 +90,12 @@ constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
 // accumulator copies at control-flow merges (the dynamic loop pays ~50 v_mov per chunk for them).
 struct DynSK {
     static constexpr bool on = false;
-    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0;
+    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0, SEG = 0;
 };
-template <int A, int B, int C, int V>
+template <int A, int B, int C, int V, int S = 0>
 struct StatSK {
     static constexpr bool on = true;
-    static constexpr int K0 = A, K1 = B, K2 = C, KV = V;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S;
 };
 
 template <int I, int N, class F>
@@ -379,6 +393,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                         P.out_v[o] = a1;
                         P.out_v[P.out_plane + o] = a2;
                         P.out_v[2 * P.out_plane + o] = a3;
+                        if (P.out_dot) {
+                            const float4 na4 = *reinterpret_cast<const float4*>(P.na + (size_t)(row >> lg) * 4);
+                            P.out_dot[o] = a1 * na4.y + a2 * na4.z + a3 * na4.w;
+                        }
                     }
                 };
                 if (G <= 4) {
