@@ -20,6 +20,11 @@ LIB = os.path.join(OUT_DIR, "libnbx.so")
 ARCH = os.environ.get("NBX_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
          "-munsafe-fp-atomics"]
+# per-file extra flags (measured: disabling packed fp32 in msg_pre.hip, whose VALU work runs beside
+# the other wave's MFMAs, did not help: +1 %)
+FILE_FLAGS = {}
+if os.environ.get("NBX_PACKED_MSG_PRE") == "1":
+    FILE_FLAGS = {}
 
 
 def _hipcc() -> str:
@@ -46,7 +51,7 @@ def build(jobs: int = 8, verbose: bool = False, force: bool = False) -> str:
         o = os.path.join(OBJ_DIR, os.path.basename(s)[:-4] + ".o")
         objs.append(o)
         if force or _needs(o, [s] + headers):
-            cmds.append([hipcc, *FLAGS, "-c", s, "-o", o])
+            cmds.append([hipcc, *FLAGS, *FILE_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:

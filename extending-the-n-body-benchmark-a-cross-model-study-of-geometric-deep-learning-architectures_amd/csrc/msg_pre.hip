@@ -1,0 +1,252 @@
+// Fused message_layer_1 kernel (see msg_pre.h for the algorithm and data layout).
+#include "msg_pre.h"
+#include "tp16.h"
+
+namespace nbx {
+
+constexpr int MP_THREADS = 512;
+// one exchange buffer: [4 planes][6 parts][16 rows][MP_RS], 16 channels per row padded to 20
+// floats so the GEMM waves' stores (lane quarters qd = 0/1 hold rows 4 apart) hit different
+// bank halves, while rows stay 16-byte aligned for the edge waves' ds_read_b128
+constexpr int MP_RS = 20, MP_PART = 16 * MP_RS;
+constexpr int MP_EX = 4 * 6 * MP_PART;
+
+__global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
+    float* EX = lds + 2 * F;   // [2 buffers][MP_EX]
+    float* XC = EX + 2 * MP_EX;  // pending BN of X per k: [sc_s | sc_v | sh] x (KC * 32), zero past M
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
+    const bool gemm_wave = wave < 4;
+    const int plane = wave & 3;
+    const unsigned long long c_start = P.dbg ? clock64() : 0ull;
+    const int chunk = blockIdx.x % P.chunks, pblk = blockIdx.x / P.chunks;
+    const int my_groups = pblk < P.n_slabs ? (P.n_slabs - 1 - pblk) / P.per_chunk + 1 : 0;
+    const int KC = (M + 31) >> 5;
+    const int lg = __builtin_ctz((unsigned)G);
+    const float invN = 1.0f / (float)N;
+    const int64_t Ep = P.V * G;
+
+    // GEMM waves: A = X[plane][node][k], two float4 per lane per 32-deep chunk (lane quarter qd
+    // supplies k = 8 qd + s at MFMA step s), bounds-checked buffer loads (zeros past M / V)
+    const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)P.X, (short)0, 0x7FFFFFF0, 0x00020000);
+    auto load_a = [&](int i, int kc, float4 (&a)[2]) {
+        const int grp = pblk + i * P.per_chunk;
+        const int64_t node = (int64_t)grp * NG + c16;
+        const int k = kc * 32 + 8 * qd;
+        const bool ok = i < my_groups && c16 < NG && node < P.V && k < M;
+        const uint32_t off = ok ? (uint32_t)((((int64_t)plane * P.V + node) * M + k) * 4) : 0x7FFFFFF0u;
+        a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsX, off, 0, 0));
+        a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsX, ok ? off + 16 : off, 0, 0));
+    };
+    constexpr int KCMAX = 4;   // M <= 128 (launch check)
+    float4 abuf[KCMAX][2];
+    if (gemm_wave) {
+#pragma unroll
+        for (int kc = 0; kc < KCMAX; ++kc)
+            if (kc < KC) load_a(0, kc, abuf[kc]);
+    }
+
+    // both weight images of this chunk -> LDS (DMA, verbatim)
+    tp_dma_image<8>(P.Simg + (size_t)chunk * F, lds, F);
+    tp_dma_image<8>(P.Vimg + (size_t)chunk * F, lds + F, F);
+
+    // the previous layer's feature BatchNorm is applied to X here, as it is loaded (lazy BN:
+    // X in HBM holds the pre-normalisation values); identity when xcoef is null
+    for (int i = t; i < 3 * KC * 32; i += MP_THREADS) {
+        const int part = i / (KC * 32), k = i - part * KC * 32;
+        float v = 0.f;
+        if (k < M) v = P.xcoef ? P.xcoef[part * M + k] : (part < 2 ? 1.f : 0.f);
+        XC[i] = v;
+    }
+
+    // edge waves: thread = (edge slot of the group, channel quad cq); per-quad constants
+    const int et = t - 256, cq = et & 3, ch0 = chunk * 16 + 4 * cq;
+    const bool live = !gemm_wave && ch0 < M;   // M % 4 == 0: a live quad is live in all 4 lanes
+    float4 ea0{}, eg0{}, et0{}, ea1{}, eg1{}, et1{}, ba{}, bg{};
+    if (live) {
+        auto ld4 = [&](int o) { return *reinterpret_cast<const float4*>(P.amf + o + ch0); };
+        ea0 = ld4(0); eg0 = ld4(M); et0 = ld4(2 * M); ea1 = ld4(3 * M); eg1 = ld4(4 * M); et1 = ld4(5 * M);
+        ba = *reinterpret_cast<const float4*>(P.bias + ch0);
+        bg = *reinterpret_cast<const float4*>(P.bias + M + ch0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const float* img = lds + (plane ? F : 0);
+    const int group_items = NG * G;
+    unsigned long long c_mark = P.dbg ? clock64() : 0ull, c_gemm = 0ull, c_ex = 0ull, c_edge = 0ull;
+    const unsigned long long c_stage = c_mark;
+    auto tick = [&](unsigned long long& acc) {
+        if (P.dbg) { const unsigned long long c = clock64(); acc += c - c_mark; c_mark = c; }
+    };
+    // edge waves: the geometry of the thread's first edge slot of the next group, prefetched
+    // one stage ahead
+    auto load_geo = [&](int gi, float4& g4, float& pm) {
+        const int64_t e = ((int64_t)(pblk + gi * P.per_chunk) * NG) * G + (et >> 2);
+        const bool ok = live && gi < my_groups && (et >> 2) < group_items && e < Ep;
+        g4 = ok ? *reinterpret_cast<const float4*>(P.EG + e * 8) : float4{0.f, 0.f, 0.f, 0.f};
+        pm = ok ? P.EG[e * 8 + 4] : 0.f;
+    };
+    float4 geo_next{};
+    float pm_next = 0.f;
+    load_geo(0, geo_next, pm_next);
+    for (int i = 0; i <= my_groups; ++i) {
+        if (gemm_wave) {
+            if (i < my_groups) {
+                // ---- node GEMM of group i: 16 rows x 96 columns (6 parts x 16 channels)
+                floatx4 acc[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                // B fragments double-buffered across the 32-deep K chunks: the reads of chunk
+                // kc + 1 are in flight while chunk kc's 48 MFMAs issue
+                float4 b[2][6][2];
+                auto load_b = [&](int kc, float4 (&bb)[6][2]) {
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) {
+                        const float* bp = img + (j * KC + kc) * 512 + 4 * lane;
+                        bb[j][0] = *reinterpret_cast<const float4*>(bp);
+                        bb[j][1] = *reinterpret_cast<const float4*>(bp + 256);
+                    }
+                };
+                load_b(0, b[0]);
+#pragma unroll
+                for (int kc = 0; kc < KCMAX; ++kc) {
+                    if (kc >= KC) break;
+                    if (kc + 1 < KC) load_b(kc + 1, b[(kc + 1) & 1]);
+                    // x = sc * x~ + sh (shift on the 0e plane only)
+                    const float* xc = XC + (plane ? KC * 32 : 0) + kc * 32 + 8 * qd;
+                    const float4 sc0 = *reinterpret_cast<const float4*>(xc);
+                    const float4 sc1 = *reinterpret_cast<const float4*>(xc + 4);
+                    float4 sh0{0.f, 0.f, 0.f, 0.f}, sh1{0.f, 0.f, 0.f, 0.f};
+                    if (plane == 0) {
+                        sh0 = *reinterpret_cast<const float4*>(XC + 2 * KC * 32 + kc * 32 + 8 * qd);
+                        sh1 = *reinterpret_cast<const float4*>(XC + 2 * KC * 32 + kc * 32 + 8 * qd + 4);
+                    }
+                    const float av[8] = {fmaf(sc0.x, abuf[kc][0].x, sh0.x), fmaf(sc0.y, abuf[kc][0].y, sh0.y),
+                                         fmaf(sc0.z, abuf[kc][0].z, sh0.z), fmaf(sc0.w, abuf[kc][0].w, sh0.w),
+                                         fmaf(sc1.x, abuf[kc][1].x, sh1.x), fmaf(sc1.y, abuf[kc][1].y, sh1.y),
+                                         fmaf(sc1.z, abuf[kc][1].z, sh1.z), fmaf(sc1.w, abuf[kc][1].w, sh1.w)};
+                    const float4 (&bc)[6][2] = b[kc & 1];
+#pragma unroll
+                    for (int s = 0; s < 8; ++s)
+#pragma unroll
+                        for (int j = 0; j < 6; ++j)
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], f4get(bc[j][s >> 2], s & 3), acc[j], 0,
+                                                                          0, 0);
+                }
+                // prefetch the next group's rows
+#pragma unroll
+                for (int kc = 0; kc < KCMAX; ++kc)
+                    if (kc < KC) load_a(i + 1, kc, abuf[kc]);
+                float* ex = EX + (i & 1) * MP_EX + plane * 6 * MP_PART;
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) ex[j * MP_PART + (4 * qd + jj) * MP_RS + c16] = acc[j][jj];
+                tick(c_gemm);
+            }
+        } else if (i > 0 && live && !P.diag) {
+            // ---- edges of group i-1
+            const float4 geo_cur = geo_next;
+            const float pm_cur = pm_next;
+            load_geo(i, geo_next, pm_next);
+            const float* exb = EX + ((i - 1) & 1) * MP_EX + 4 * cq;
+            auto xv = [&](int pl, int part, int row) {
+                return *reinterpret_cast<const float4*>(exb + (pl * 6 + part) * MP_PART + row * MP_RS);
+            };
+            const int64_t node0 = (int64_t)(pblk + (i - 1) * P.per_chunk) * NG;
+            for (int it = et >> 2; it < group_items; it += 64) {
+                const int ld = it >> lg, q = it & (G - 1);
+                const int64_t dn = node0 + ld;
+                if (dn >= P.V) break;
+                const int64_t e = dn * G + q;
+                float4* m1s = reinterpret_cast<float4*>(P.M1S + e * 2 * M + ch0);
+                float4* m1v0 = reinterpret_cast<float4*>(P.M1V + e * M + ch0);
+                float4* m1v1 = reinterpret_cast<float4*>(P.M1V + (Ep + e) * M + ch0);
+                float4* m1v2 = reinterpret_cast<float4*>(P.M1V + (2 * Ep + e) * M + ch0);
+                if (q >= N - 1) {   // padding slot
+                    const float4 z{0.f, 0.f, 0.f, 0.f};
+                    m1s[0] = z; m1s[M / 4] = z; *m1v0 = z; *m1v1 = z; *m1v2 = z;
+                    continue;
+                }
+                const int d = ld - N * tp_udiv_small(ld, invN);        // position in the system
+                const int sl = ld - d + (q < d ? q : q + 1);            // source node, same group
+                const bool first = it == (et >> 2);
+                const float4 g4 = first ? geo_cur : *reinterpret_cast<const float4*>(P.EG + e * 8);
+                const float pm = first ? pm_cur : P.EG[e * 8 + 4];
+                const float hk[3] = {g4.x, g4.y, g4.z};
+                const float dist = g4.w;
+                float4 sa = xv(0, 0, ld) + xv(0, 3, sl) + ea0 * dist + ea1 * pm + ba;
+                float4 sg = xv(0, 1, ld) + xv(0, 4, sl) + eg0 * dist + eg1 * pm + bg;
+                const float4 tt = xv(0, 2, ld) + xv(0, 5, sl) + et0 * dist + et1 * pm;
+                float4 v[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    sa += hk[k] * (xv(1 + k, 0, ld) + xv(1 + k, 3, sl));
+                    sg += hk[k] * (xv(1 + k, 1, ld) + xv(1 + k, 4, sl));
+                    v[k] = hk[k] * tt + xv(1 + k, 2, ld) + xv(1 + k, 5, sl);
+                }
+                float4 gg, ms;
+                gg.x = kC_SIGMOID * tp_sigmoid(sg.x); gg.y = kC_SIGMOID * tp_sigmoid(sg.y);
+                gg.z = kC_SIGMOID * tp_sigmoid(sg.z); gg.w = kC_SIGMOID * tp_sigmoid(sg.w);
+                ms.x = kC_SILU * tp_silu(sa.x); ms.y = kC_SILU * tp_silu(sa.y);
+                ms.z = kC_SILU * tp_silu(sa.z); ms.w = kC_SILU * tp_silu(sa.w);
+                const float4 mv0 = gg * v[0], mv1 = gg * v[1], mv2 = gg * v[2];
+                *m1v0 = mv0; *m1v1 = mv1; *m1v2 = mv2;
+                m1s[0] = ms;
+                m1s[M / 4] = mv0 * hk[0] + mv1 * hk[1] + mv2 * hk[2];
+            }
+            tick(c_edge);
+        }
+        // LDS hand-off only: wait for this wave's LDS traffic, not for its global stores
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        tick(c_ex);
+    }
+    if (P.dbg && lane == 0) {
+        unsigned long long* d = P.dbg + ((size_t)blockIdx.x * 8 + wave) * 4;
+        d[0] = c_stage - c_start; d[1] = c_gemm; d[2] = c_ex; d[3] = c_edge;
+    }
+}
+
+inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
+    return ((size_t)2 * p.img_floats + 2 * MP_EX + 3 * 32 * ((p.M + 31) / 32)) * 4;
+}
+
+int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
+    if (p.V <= 0) return NBX_OK;
+    if (p.M > 128 || p.NG <= 0) {
+        set_error("msg_pre: needs mul <= 128 and 2 <= N <= 16 (got mul %d, N %d)", p.M, p.N);
+        return NBX_E_UNSUPPORTED;
+    }
+    if ((double)4 * p.V * p.M * 4.0 >= 2147483632.0) {
+        set_error("msg_pre: X spans >= 2 GiB (32-bit buffer offsets)");
+        return NBX_E_UNSUPPORTED;
+    }
+    p.chunks = (p.M + 15) / 16;
+    p.img_floats = 6 * ((p.M + 31) / 32) * 512;
+    p.n_slabs = (int)((p.V + p.NG - 1) / p.NG);
+    // one block per CU (LDS-bound); balance the group rounds over the chunk's blocks
+    int per = num_cus / p.chunks;
+    if (per < 1) per = 1;
+    const int rounds = (p.n_slabs + per - 1) / per;
+    per = (p.n_slabs + rounds - 1) / rounds;
+    p.per_chunk = per;
+    const size_t lds = msg_pre_lds_bytes(p);
+    if (lds > 160 * 1024) {
+        set_error("msg_pre: %zu bytes of LDS (> 160 KiB)", lds);
+        return NBX_E_UNSUPPORTED;
+    }
+    static bool attr_set = false;
+    if (!attr_set) {
+        NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(msg_pre_kernel, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
+}  // namespace nbx
