@@ -41,57 +41,64 @@ __device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 // threadIdx.y = row lane; a block covers ROWS_PER_BLOCK rows x 32 channels.
 constexpr int EW_X = 32, EW_Y = 8, ROWS_PER_BLOCK = 16;
 
-// ---------------------------------------------------------------- featurise
-// O3Transform (o3_building_blocks.py:231-278) + catch_isolated_nodes (segnn.py:136-148)
-__global__ void featurize_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
-                                 const float* __restrict__ mass, int64_t V, int N, int G, float* __restrict__ NA,
-                                 float* __restrict__ X0, float* __restrict__ EG) {
-    const int64_t node = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (node >= V) return;
-    const int64_t b = node / N;
-    const int d = (int)(node - b * N);
-    const float px = pos[3 * node], py = pos[3 * node + 1], pz = pos[3 * node + 2];
-    const float vx = vel[3 * node], vy = vel[3 * node + 1], vz = vel[3 * node + 2];
-    const float m = mass[node];
-    float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (int q = 0; q < N - 1; ++q) {
-        const int64_t s = b * N + (q < d ? q : q + 1);
-        const float rx = pos[3 * s] - px, ry = pos[3 * s + 1] - py, rz = pos[3 * s + 2] - pz;
-        const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
-        const float den = fmaxf(dist, 1e-12f);
-        const float hx = rx / den, hy = ry / den, hz = rz / den;
-        float* eg = EG + (node * G + q) * 8;
-        eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s] * m;
-        sx += kSH_C1 * hx; sy += kSH_C1 * hy; sz += kSH_C1 * hz;
+// ---------------------------------------------------------------- featurise + embedding
+// O3Transform (o3_building_blocks.py:231-278) + catch_isolated_nodes (segnn.py:136-148), then
+// embedding_layer: O3TensorProduct(2x1o+1x0e -> hidden, node attrs) (segnn.py:69-71,170).
+// featurise + embedding in one launch: a block of FE_NODES nodes first runs O3Transform /
+// catch_isolated_nodes per node (thread = node; NA and EG to HBM, X0 kept in LDS), then the
+// embedding TP per (node, channel).
+constexpr int FE_NODES = 32;
+__global__ void featurize_embed_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
+                                       const float* __restrict__ mass, int64_t V, int N, int G,
+                                       const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
+                                       float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
+                                       float* __restrict__ XD) {
+    __shared__ float sx0[FE_NODES][8];
+    __shared__ float sna[FE_NODES][4];
+    const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
+    const int t = threadIdx.x;
+    if (t < FE_NODES && n0 + t < V) {
+        const int64_t node = n0 + t;
+        const int64_t b = node / N;
+        const int d = (int)(node - b * N);
+        const float px = pos[3 * node], py = pos[3 * node + 1], pz = pos[3 * node + 2];
+        const float vx = vel[3 * node], vy = vel[3 * node + 1], vz = vel[3 * node + 2];
+        const float m = mass[node];
+        float sxh = 0.f, syh = 0.f, szh = 0.f;
+        for (int q = 0; q < N - 1; ++q) {
+            const int64_t s2 = b * N + (q < d ? q : q + 1);
+            const float rx = pos[3 * s2] - px, ry = pos[3 * s2 + 1] - py, rz = pos[3 * s2 + 2] - pz;
+            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+            const float den = fmaxf(dist, 1e-12f);
+            const float hx = rx / den, hy = ry / den, hz = rz / den;
+            float* eg = EG + (node * G + q) * 8;
+            eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s2] * m;
+            sxh += kSH_C1 * hx; syh += kSH_C1 * hy; szh += kSH_C1 * hz;
+        }
+        for (int q = N - 1; q < G; ++q) {
+            float* eg = EG + (node * G + q) * 8;
+            eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
+        }
+        const float cnt = (float)(N - 1 > 0 ? N - 1 : 1);
+        const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
+        const float vden = fmaxf(vn, 1e-12f);
+        const float na1 = sxh / cnt + kSH_C1 * (vx / vden), na2 = syh / cnt + kSH_C1 * (vy / vden);
+        const float na3 = szh / cnt + kSH_C1 * (vz / vden);
+        NA[4 * node + 0] = 1.0f; NA[4 * node + 1] = na1; NA[4 * node + 2] = na2; NA[4 * node + 3] = na3;
+        sna[t][0] = 1.0f; sna[t][1] = na1; sna[t][2] = na2; sna[t][3] = na3;
+        const float mp = (px + py + pz) / 3.0f;  // pos.mean(1): mean over xyz (reference quirk)
+        sx0[t][0] = px - mp; sx0[t][1] = py - mp; sx0[t][2] = pz - mp;
+        sx0[t][3] = vx; sx0[t][4] = vy; sx0[t][5] = vz; sx0[t][6] = vn; sx0[t][7] = 0.f;
     }
-    for (int q = N - 1; q < G; ++q) {
-        float* eg = EG + (node * G + q) * 8;
-        eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
-    }
-    const float cnt = (float)(N - 1 > 0 ? N - 1 : 1);
-    const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
-    const float vden = fmaxf(vn, 1e-12f);
-    NA[4 * node + 0] = 1.0f;
-    NA[4 * node + 1] = sx / cnt + kSH_C1 * (vx / vden);
-    NA[4 * node + 2] = sy / cnt + kSH_C1 * (vy / vden);
-    NA[4 * node + 3] = sz / cnt + kSH_C1 * (vz / vden);
-    const float mp = (px + py + pz) / 3.0f;  // pos.mean(1): mean over xyz (reference quirk)
-    float* x0 = X0 + 8 * node;
-    x0[0] = px - mp; x0[1] = py - mp; x0[2] = pz - mp;
-    x0[3] = vx; x0[4] = vy; x0[5] = vz; x0[6] = vn; x0[7] = 0.f;
-}
-
-// embedding_layer: O3TensorProduct(2x1o+1x0e -> hidden, node attrs) (segnn.py:69-71,170)
-__global__ void embed_kernel(const float* __restrict__ X0, const float* __restrict__ NA,
-                             const float* __restrict__ emb, const float* __restrict__ emb_b, int64_t V, int M,
-                             float* __restrict__ X, float* __restrict__ XD) {
-    const int w = blockIdx.y * EW_X + threadIdx.x;
-    if (w >= M) return;
-    const float a0 = emb[w], a1 = emb[M + w], b0 = emb[2 * M + w], b1 = emb[3 * M + w];
-    const float c = emb[4 * M + w], dd = emb[5 * M + w], bias = emb_b[w];
-    for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
-        const float* x0 = X0 + 8 * n;
-        const float* na = NA + 4 * n;
+    __syncthreads();
+    const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
+    for (int idx = t; idx < nn * M; idx += blockDim.x) {
+        const int ln = idx / M, w = idx - ln * M;
+        const int64_t n = n0 + ln;
+        const float a0 = emb[w], a1 = emb[M + w], b0 = emb[2 * M + w], b1 = emb[3 * M + w];
+        const float c = emb[4 * M + w], dd = emb[5 * M + w], bias = emb_b[w];
+        const float* x0 = sx0[ln];
+        const float* na = sna[ln];
         const float u0n = x0[0] * na[1] + x0[1] * na[2] + x0[2] * na[3];
         const float u1n = x0[3] * na[1] + x0[4] * na[2] + x0[5] * na[3];
         X[n * M + w] = b0 * u0n + b1 * u1n + c * x0[6] + bias;
@@ -102,7 +109,7 @@ __global__ void embed_kernel(const float* __restrict__ X0, const float* __restri
             X[((1 + k) * V + n) * M + w] = xv;
             xd += xv * na[1 + k];
         }
-        if (XD) XD[n * M + w] = xd;   // x_v . na, an input of update_layer_1
+        if (XD) XD[n * M + w] = xd;
     }
 }
 
@@ -268,26 +275,42 @@ __global__ void bn_apply_kernel(float* __restrict__ X, const float* __restrict__
     }
 }
 
-// pre_pool1 inputs from X: U2S [V][2M] = [x_s | x_v.na], U2V = x_v (a view of X planes 1..3)
-__global__ void pp_pre_kernel(const float* __restrict__ X, const float* __restrict__ NA, int64_t V, int M,
-                              float* __restrict__ U2S) {
+// pre_pool1 inputs from X with the last layer's pending feature BatchNorm applied (coef, or
+// identity when null): U1S [V][2M] = [x_s | x_v.na], U1V [3][V][M] = x_v
+__global__ void pp_pre_kernel(const float* __restrict__ X, const float* __restrict__ NA,
+                              const float* __restrict__ coef, int64_t V, int M, float* __restrict__ U1S,
+                              float* __restrict__ U1V) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
+    const float sc_s = coef ? coef[w] : 1.f, sc_v = coef ? coef[M + w] : 1.f, sh = coef ? coef[2 * M + w] : 0.f;
     for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
         const float* na = NA + 4 * n;
         float dot = 0.f;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) dot += X[((1 + k) * V + n) * M + w] * na[1 + k];
-        U2S[n * 2 * M + w] = X[n * M + w];
-        U2S[n * 2 * M + M + w] = dot;
+        for (int k = 0; k < 3; ++k) {
+            const float xv = sc_v * X[((1 + k) * V + n) * M + w];
+            U1V[((int64_t)k * V + n) * M + w] = xv;
+            dot += xv * na[1 + k];
+        }
+        U1S[n * 2 * M + w] = fmaf(sc_s, X[n * M + w], sh);
+        U1S[n * 2 * M + M + w] = dot;
     }
 }
 
-// pre_pool2: O3TensorProduct(hidden -> 2x1o, node attrs); one wave per node,
-// lanes stride over channels, shuffle reduction.  out [V][6] = (c0 xyz, c1 xyz).
+// Optional fused self-feed state update (infer_self_feed.py:182-211, target pos_dt+vel):
+// pos += out[:3], vel = out[3:], and the new state is written as trajectory frame `frame`.
+struct RolloutUpdate {
+    float* pos;
+    float* vel;
+    float* traj_pos;
+    float* traj_vel;
+    int64_t frame, num_frames;
+    int N;
+};
+
 __global__ void pp2_kernel(const float* __restrict__ H2S, const float* __restrict__ H2V,
                            const float* __restrict__ NA, const float* __restrict__ W, int64_t V, int M,
-                           float* __restrict__ out) {
+                           float* __restrict__ out, RolloutUpdate U) {
     const int64_t n = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (n >= V) return;
@@ -306,12 +329,21 @@ __global__ void pp2_kernel(const float* __restrict__ H2S, const float* __restric
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off);
-    if (lane == 0) {
+    if (lane < 3) {
+        const int k = lane;
         const float* na = NA + 4 * n;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            out[6 * n + k] = na[1 + k] * acc[0] + acc[2 + k];
-            out[6 * n + 3 + k] = na[1 + k] * acc[1] + acc[5 + k];
+        const float dp = na[1 + k] * acc[0] + acc[2 + k];
+        const float nv = na[1 + k] * acc[1] + acc[5 + k];
+        out[6 * n + k] = dp;
+        out[6 * n + 3 + k] = nv;
+        if (U.pos) {
+            const float p = U.pos[3 * n + k] + dp;
+            U.pos[3 * n + k] = p;
+            U.vel[3 * n + k] = nv;
+            const int64_t b = n / U.N, d = n - b * U.N;
+            const int64_t o = ((b * U.num_frames + U.frame) * U.N + d) * 3 + k;
+            U.traj_pos[o] = p;
+            U.traj_vel[o] = nv;
         }
     }
 }
@@ -370,7 +402,7 @@ int64_t partial_doubles(const Dims& d) {
 }
 
 struct Workspace {
-    float *X, *NA, *X0, *EG, *NP, *M1S, *M1V, *AGG, *U1S, *U1V, *U2S, *U2V, *coef_msg, *coef_feat, *out;
+    float *X, *NA, *EG, *NP, *M1S, *M1V, *AGG, *U1S, *U1V, *U2S, *U2V, *coef_msg, *coef_feat, *out;
     float *XD, *AD;   // x_v . na and aggregated a_v . na per node and channel (segmented update_layer_1)
     double* partial;
     size_t bytes;
@@ -390,7 +422,6 @@ size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
     w.partial = (double*)take((size_t)partial_doubles(d), 8);
     w.X = (float*)take(4 * V * M, 4);
     w.NA = (float*)take(4 * V, 4);
-    w.X0 = (float*)take(8 * V, 4);
     w.EG = (float*)take(8 * Ep, 4);
     w.NP = (float*)take(4 * V * 6 * M, 4);
     w.M1S = (float*)take(Ep * 2 * M, 4);
@@ -674,18 +705,19 @@ nbx::TpProb tp_base(int rows, const Dims& d) {
 }
 
 int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass, int64_t B,
-                 int64_t N, float* out, const Workspace& ws, hipStream_t st, KernelTiming* tm = nullptr) {
+                 int64_t N, float* out, const Workspace& ws, hipStream_t st, KernelTiming* tm = nullptr,
+                 const RolloutUpdate* upd = nullptr) {
     const int M = w->mul;
     const Dims d = dims_of(B, N, M);
     const int64_t V = d.V, Ep = d.Ep;
     const dim3 ewb(EW_X, EW_Y);
 
-    hipLaunchKernelGGL(featurize_kernel, dim3((unsigned)nbx::ceil_div(V, 256)), dim3(256), 0, st, pos, vel, mass, V,
-                       (int)N, (int)d.G, ws.NA, ws.X0, ws.EG);
+
     // update_layer_1 reads its [x | BN(agg)] input straight from X / AGG and the two dot buffers
     // (no materialised U1) when the static segmented schedule applies (mul = 96 or 32)
     const bool seg_upd = static_enabled() && (M == 96 || M == 32);
-    hipLaunchKernelGGL(embed_kernel, ew_grid(V, M), ewb, 0, st, ws.X0, ws.NA, w->emb, w->emb_bias, V, M, ws.X,
+    hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(256), 0, st, pos, vel,
+                       mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
                        seg_upd ? ws.XD : nullptr);
     NBX_LAUNCH_CHECK("embed");
 
@@ -817,24 +849,23 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                            wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
                            L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat);
     }
-    // the last layer's feature BatchNorm, before the pre-pooling TPs
-    if (w->num_layers > 0) {
-        hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M, (float*)nullptr);
-        NBX_LAUNCH_CHECK("bn_apply");
-    }
+
     // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)
-    hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA, V, M, ws.U1S);
+    // pre_pool1 inputs with the last layer's pending feature BatchNorm applied
+    hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA,
+                       w->num_layers > 0 ? ws.coef_feat : nullptr, V, M, ws.U1S, ws.U1V);
     {
         nbx::TpProb p = tp_base((int)V, d);
         p.As = ws.U1S; p.lda_s = 2 * M; p.B = w->pp1_img;
         p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
-        p.Av = ws.X + V * M; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
+        p.Av = ws.U1V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
         if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 2, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
     }
+    RolloutUpdate none{};
     hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,
-                       w->pp2, V, M, out);
+                       w->pp2, V, M, out, upd ? *upd : none);
     NBX_LAUNCH_CHECK("pre_pool2");
     return NBX_OK;
 }
@@ -881,10 +912,9 @@ extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* 
                        num_frames, traj_pos, traj_vel);
     NBX_LAUNCH_CHECK("rollout_update");
     for (int64_t f = 1; f < num_frames; ++f) {
-        if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st)) return rc;
-        hipLaunchKernelGGL(rollout_update_kernel, dim3(ub), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, f,
-                           num_frames, traj_pos, traj_vel);
-        NBX_LAUNCH_CHECK("rollout_update");
+        // the state update + trajectory write of frame f is fused into pre_pool2's epilogue
+        const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N};
+        if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd)) return rc;
     }
     return NBX_OK;
 }
