@@ -15,16 +15,19 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "lib")
-OBJ_DIR = os.path.join(HERE, "lib", "obj")
-LIB = os.path.join(OUT_DIR, "libnbx.so")
+# NBX_BUILD_TAG: a side build (lib/libnbx_<tag>.so, loaded with NBX_LIB=...) for A/B timing only
+_TAG = os.environ.get("NBX_BUILD_TAG", "")
+OBJ_DIR = os.path.join(HERE, "lib", "obj" + (f"_{_TAG}" if _TAG else ""))
+LIB = os.path.join(OUT_DIR, f"libnbx_{_TAG}.so" if _TAG else "libnbx.so")
 ARCH = os.environ.get("NBX_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
          "-munsafe-fp-atomics"]
 # per-file extra flags (measured: disabling packed fp32 in msg_pre.hip, whose VALU work runs beside
-# the other wave's MFMAs, did not help: +1 %)
+# the other wave's MFMAs, did not help: +1 %); NBX_FILE_FLAGS="file.hip:-flag,-flag;..." adds more
 FILE_FLAGS = {}
-if os.environ.get("NBX_PACKED_MSG_PRE") == "1":
-    FILE_FLAGS = {}
+for _item in filter(None, os.environ.get("NBX_FILE_FLAGS", "").split(";")):
+    _f, _fl = _item.split(":", 1)
+    FILE_FLAGS.setdefault(_f, []).extend(_fl.split(","))
 
 
 def _hipcc() -> str:

@@ -468,7 +468,7 @@ int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     p.NS = NS;
     p.NV = NV;
     p.epi = EPI;
-    nbx::tp_geometry(p, WAVES);
+    nbx::tp_geometry(p, WAVES, 256, SK::PREC);
     if (!tm) return nbx::tp_launch<NS, NV, EPI, WAVES, D, SK>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
@@ -515,6 +515,19 @@ using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
 using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
 using SK_GATE = nbx::StatSK<6, 6, 3, 3>;     // pre_pool1 (and message_layer_2's shape)
 using SK_GATE_32 = nbx::StatSK<2, 2, 1, 1>;
+using SK_MSG2_X3 = nbx::StatSKX3<6, 6, 3, 3>;
+using SK_MSG2_32_X3 = nbx::StatSKX3<2, 2, 1, 1>;
+
+// message_layer_2 on the split-precision MFMA path when the weights carry a bf16x3 image
+// (NBX_X3=0: fp32 MFMA path, A/B only)
+bool x3_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NBX_X3");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
 
 // Tuning switch for A/B runs on the GPU box (NBX_MSG_VARIANT=<waves>x<depth>, e.g. 8x3);
 // the default is the measured best.
@@ -558,16 +571,19 @@ int tp_debug_dump(const nbx::TpProb& p, hipStream_t st, int waves) {
 }
 
 template <int NS, int NV, int EPI>
-int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
-    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
-    if (debug) {
-        p.dbg = tp_dbg_buf(st);
-        int rc = run_tp<NS, NV, EPI, 8, 3>(p, st, tm);
-        if (rc) return rc;
-        return tp_debug_dump(p, st, 8);
-    }
+int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3) {
     // message_layer_2 at mul = 96 / 32: fully unrolled static chunk schedule
     if (static_enabled()) {
+        if (img_x3 && x3_enabled()) {
+            const float* fp32_img = p.B;
+            p.B = static_cast<const float*>(img_x3);
+            if (sk_matches<SK_MSG2_X3>(p, NS, NV)) {
+                if (getenv("NBX_X3_D4")) return run_tp<NS, NV, EPI, 8, 4, SK_MSG2_X3>(p, st, tm);
+                return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_X3>(p, st, tm);
+            }
+            if (sk_matches<SK_MSG2_32_X3>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_32_X3>(p, st, tm);
+            p.B = fp32_img;
+        }
         if (sk_matches<SK_GATE>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_GATE>(p, st, tm);
         if (sk_matches<SK_GATE_32>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_GATE_32>(p, st, tm);
     }
@@ -576,6 +592,15 @@ int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
         case 84: return run_tp<NS, NV, EPI, 8, 4>(p, st, tm);
         default: return run_tp<NS, NV, EPI, 8, 3>(p, st, tm);
     }
+}
+
+template <int NS, int NV, int EPI>
+int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3 = nullptr) {
+    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
+    if (debug) p.dbg = tp_dbg_buf(st);
+    const int rc = run_tp_msg_sel<NS, NV, EPI>(p, st, tm, img_x3);
+    if (rc || !debug) return rc;
+    return tp_debug_dump(p, st, 8);
 }
 
 
@@ -782,7 +807,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
             if (seg_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
             if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
-                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm)) return rc;
+                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3)) return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
             } else {

@@ -25,6 +25,8 @@
 namespace nbx {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3 };
 
@@ -90,13 +92,57 @@ constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
 // accumulator copies at control-flow merges (the dynamic loop pays ~50 v_mov per chunk for them).
 struct DynSK {
     static constexpr bool on = false;
-    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0, SEG = 0;
+    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0, SEG = 0, PREC = 0;
 };
 template <int A, int B, int C, int V, int S = 0>
 struct StatSK {
     static constexpr bool on = true;
-    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 0;
 };
+
+// StatSK with the split-precision MFMA path (include/nbx.h "bf16x3 images"): A and B are split
+// into three bf16 parts each and every product is the fp32 sum of the six leading cross terms on
+// v_mfma_f32_32x32x16_bf16 -- fp32-level accuracy at 2.7x the fp32 MFMA rate (12 x 32 cycles per
+// 32 x 32 x 32 block instead of 16 x 64).  The weight image is the bf16x3 one (1.5x the fp32 bytes).
+template <int A, int B, int C, int V>
+struct StatSKX3 {
+    static constexpr bool on = true;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = 0, PREC = 1;
+};
+
+// x = hi + mid + lo (+ <= 2^-27 |x|), each part bf16: RNE conversions (v_cvt_pk_bf16_f32, two
+// elements per instruction), the residuals are exact (v_pk_add_f32); 4.5 VALU per element
+typedef __bf16 tp_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float tp_f2 __attribute__((ext_vector_type(2)));
+typedef unsigned tp_u4 __attribute__((ext_vector_type(4)));
+__device__ inline unsigned tp_pk_bf16(tp_f2 v) { return __builtin_bit_cast(unsigned, __builtin_convertvector(v, tp_bf16x2)); }
+__device__ inline tp_f2 tp_unpk_bf16(unsigned u) {
+    return tp_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+// plain v_sub_f32 (kept from being SLP-packed into v_pk_add_f32, which costs extra cycles beside
+// MFMAs -- MI355X_MICROARCH "price of one filler beside MFMAs")
+__device__ inline float tp_sub(float a, float b) {
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline tp_f2 tp_sub2(tp_f2 a, tp_f2 b) { return tp_f2{tp_sub(a.x, b.x), tp_sub(a.y, b.y)}; }
+__device__ inline void tp_split3(const float4& a, const float4& b, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+    const tp_f2 f[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+    tp_u4 H, Mi, L;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const unsigned h = tp_pk_bf16(f[i]);
+        const tp_f2 r = tp_sub2(f[i], tp_unpk_bf16(h));
+        const unsigned m = tp_pk_bf16(r);
+        H[i] = h;
+        Mi[i] = m;
+        L[i] = tp_pk_bf16(tp_sub2(r, tp_unpk_bf16(m)));
+    }
+    hi = __builtin_bit_cast(bf16x8, H);
+    mid = __builtin_bit_cast(bf16x8, Mi);
+    lo = __builtin_bit_cast(bf16x8, L);
+}
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -149,6 +195,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
 
     int off[NS + 1];
     tp_img_offsets<NS>(P, 32, off);
+    static_assert(SK::PREC == 0 || SK::on, "split-precision path needs a static schedule");
+    const bf16x8* ldsx = reinterpret_cast<const bf16x8*>(lds);   // PREC 1: 384 bf16x8 per 32-deep block
 
     const int ks_chunks = (P.K[0] + 31) >> 5;            // K_S = K[0] (sub-tile 0 uses all of it)
     const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
@@ -160,6 +208,13 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     const int wid = blk * WAVES + wave;                  // wave index within this chunk
 
     double st0 = 0.0, st1 = 0.0, st2 = 0.0;              // BN partial sums for column r
+    // MSG epilogue operands that do not depend on the tile, loaded before the first K loop
+    float ba = 0.f, bg = 0.f;
+    const int lg = EPI == TP_MSG ? __builtin_ctz((unsigned)P.group) : 0;
+    if constexpr (EPI == TP_MSG) {
+        const int ch = chunk * 32 + r;
+        if (ch < P.M) { ba = P.bias[ch]; bg = P.bias[P.M + ch]; }
+    }
 
     // A-chunk loader: chunk i of a row tile -> 16 floats per lane (4 x dwordx4).  Bounds-checked
     // buffer loads, branch-free (invalid lanes, padding chunks and tiles past the end read zeros
@@ -237,10 +292,14 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
             const int next_rt = rt + wstride;
             // MSG: this tile's edge geometry (rhat) is fetched now and parked in LDS before the
             // epilogue, so the epilogue reads it without global-memory latency
+            // (and, for the dot output, the node attributes of its 32 / group destinations)
             float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
             if constexpr (EPI == TP_MSG) {
                 const int grow = rt * 32 + r;
                 if (h == 0 && grow < P.rows) gq = *reinterpret_cast<const float4*>(P.geom + (size_t)grow * 8);
+                const int dst = ((rt * 32) >> lg) + r;
+                if (h == 1 && P.out_dot && r < (32 >> lg) && dst < (P.rows >> lg))
+                    gq = *reinterpret_cast<const float4*>(P.na + (size_t)dst * 4);
             }
             auto chunk_mma = [&](const float4 (&cur)[4], int i) {
                 if (i < ks_chunks) {
@@ -276,6 +335,43 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     }
                 }
             };
+            // PREC 1: item u's A chunk, split into [part][m] bf16x8 (lane (r, h) holds k = 16 h + 4 q + e
+            // of the chunk; MFMA m takes k = 16 h + 8 m + j)
+            auto split_item = [&](const float4 (&cur)[4], bf16x8 (&a)[3][2]) {
+                tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
+                tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+            };
+            auto mma_item_x3 = [&](auto ic, const bf16x8 (&a)[3][2]) {
+                constexpr int item = decltype(ic)::value;
+                {
+                    // block [p][m][lane][j]: smallest terms first
+                    auto mma6 = [&](floatx16& c, int blk) {
+                        const bf16x8* bp = ldsx + blk * 384 + lane;
+#pragma unroll
+                        for (int m = 0; m < 2; ++m) {
+                            const bf16x8 b0 = bp[m * 64], b1 = bp[(2 + m) * 64], b2 = bp[(4 + m) * 64];
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b0, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b1, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b2, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b0, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b1, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b0, c, 0, 0, 0);
+                        }
+                    };
+                    // first block of each sub-tile (compile-time image offsets)
+                    constexpr int OB[4] = {0, SK::K0, SK::K0 + SK::K1, SK::K0 + SK::K1 + SK::K2};
+                    if constexpr (item < SK::K0) {
+                        static_for<0, NS>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            constexpr int KCj = j == 0 ? SK::K0 : j == 1 ? SK::K1 : SK::K2;
+                            if constexpr (item < KCj) mma6(acc[j], OB[j] + item);
+                        });
+                    } else {
+                        constexpr int v = item - SK::K0, plane = v / SK::KV, kc = v - plane * SK::KV;
+                        mma6(acc[NS + plane], OB[NS] + kc);
+                    }
+                }
+            };
             auto compute_item = [&](auto ic, const float4 (&cur)[4]) {
                 constexpr int item = decltype(ic)::value;
                 if constexpr (item < SK::K0) {
@@ -307,7 +403,46 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     }
                 }
             };
-            if constexpr (SK::on) {
+            if constexpr (SK::PREC == 1) {
+                // the split of item u + 1 runs in the shadow of item u's MFMAs (no barrier between them)
+                bf16x8 ax[2][3][2];
+                split_item(buf[0], ax[0]);
+                static_for<0, SNIT>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    if constexpr (u + D - 1 < SNIT)
+                        load_item(std::integral_constant<int, u + D - 1>{}, rt, buf[(u + D - 1) % D]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mma_item_x3(std::integral_constant<int, u>{}, ax[u % 2]);
+                    if constexpr (u + 1 < SNIT) {
+                        // pin the split below the barrier (its pure arithmetic would otherwise be
+                        // hoisted into the previous region by instruction selection)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            floatx4 v = __builtin_bit_cast(floatx4, buf[(u + 1) % D][q]);
+                            asm volatile("" : "+v"(v));
+                            buf[(u + 1) % D][q] = __builtin_bit_cast(float4, v);
+                        }
+                        split_item(buf[(u + 1) % D], ax[(u + 1) % 2]);
+                        // ... and its results above the next barrier (else they sink into the next block)
+#pragma unroll
+                        for (int p3 = 0; p3 < 3; ++p3)
+#pragma unroll
+                            for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(ax[(u + 1) % 2][p3][m]));
+                        // spread the split's VALU over the MFMA gaps (<= ~5 per gap hide, MI355X_MICROARCH)
+                        constexpr int nm = u < SK::K0 ? 12 * ((u < SK::K2) + (u < SK::K1) + 1) : 12;
+                        constexpr int per = (120 + nm - 1) / nm;
+                        static_for<0, nm>([&](auto) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
+                        });
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+                static_for<0, D - 1>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    if constexpr (u < SNIT) load_item(std::integral_constant<int, u>{}, next_rt, buf[u % D]);
+                });
+            } else if constexpr (SK::on) {
                 static_for<0, SNIT>([&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     if constexpr (u + D - 1 < SNIT)
@@ -356,9 +491,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                 // rows are edges, dst-major, `group` (power of two) slots per destination
                 const int M = P.M;
                 const bool live = ch < M;
-                const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
-                float4* gl = reinterpret_cast<float4*>(lds + P.lds_floats) + wave * 32;   // [32 rows] rhat
-                if (h == 0) gl[r] = gq;
+                float4* gl = reinterpret_cast<float4*>(lds + P.lds_floats) + wave * 64;   // [32 rows] rhat
+                float4* gn = gl + 32;                                                     // [32 / group] na
+                if (h == 0) gl[r] = gq; else gn[r] = gq;
                 __builtin_amdgcn_wave_barrier();
                 float ms[16], mv0[16], mv1[16], mv2[16];
                 float f0 = 0.f, f1 = 0.f, f2 = 0.f;   // per-tile BN partials (16 rows), fp64 across tiles
@@ -385,7 +520,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                 // aggregate the `group` consecutive rows of each destination (all indices
                 // compile-time so the per-row arrays stay in registers)
                 const int G = P.group;
-                const int lg = __builtin_ctz((unsigned)G);
                 auto put = [&](int row, float a0, float a1, float a2, float a3) {
                     if (live && row < P.rows) {
                         const size_t o = (size_t)(row >> lg) * M + ch;
@@ -394,7 +528,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                         P.out_v[P.out_plane + o] = a2;
                         P.out_v[2 * P.out_plane + o] = a3;
                         if (P.out_dot) {
-                            const float4 na4 = *reinterpret_cast<const float4*>(P.na + (size_t)(row >> lg) * 4);
+                            const float4 na4 = gn[(row - row0) >> lg];
                             P.out_dot[o] = a1 * na4.y + a2 * na4.z + a3 * na4.w;
                         }
                     }
@@ -531,9 +665,10 @@ inline int tp_lds_floats(const TpProb& p) { return tp_img_floats(p, 32); }
 
 // Grid: `blocks_per_chunk` blocks per 32-channel chunk, chosen to fill the CUs
 // (as many blocks per CU as the LDS footprint allows) without idle waves.
-inline void tp_geometry(TpProb& p, int waves = TP_WAVES, int num_cus = 256) {
-    p.img_floats = tp_img_floats(p, 32);
-    p.lds_floats = tp_lds_floats(p);
+// prec 1: bf16x3 image, 1.5x the floats of the fp32 one.
+inline void tp_geometry(TpProb& p, int waves = TP_WAVES, int num_cus = 256, int prec = 0) {
+    p.img_floats = tp_img_floats(p, 32) * (prec ? 3 : 2) / 2;
+    p.lds_floats = p.img_floats;
     const int lds_bytes = p.lds_floats * 4;
     int per_cu = (160 * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
     if (per_cu < 1) per_cu = 1;
@@ -555,7 +690,7 @@ int tp_launch(const TpProb& p, hipStream_t st) {
         set_error("tp: A operand spans >= 2 GiB (32-bit buffer offsets)");
         return NBX_E_UNSUPPORTED;
     }
-    const size_t lds = (size_t)p.lds_floats * 4 + (EPI == TP_MSG ? (size_t)WAVES * 32 * 16 : 0);
+    const size_t lds = (size_t)p.lds_floats * 4 + (EPI == TP_MSG ? (size_t)WAVES * 64 * 16 : 0);
     if (lds > 160 * 1024) {
         set_error("tp_fused: weight chunk needs %zu bytes of LDS (> 160 KiB)", lds);
         return NBX_E_UNSUPPORTED;

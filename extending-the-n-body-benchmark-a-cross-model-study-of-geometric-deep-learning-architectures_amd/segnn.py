@@ -236,6 +236,36 @@ class SEGNN(nn.Module):
         return torch.cat(blocks, 1).contiguous()
 
     @staticmethod
+    def split_bf16x3(W: torch.Tensor):
+        """W = hi + mid + lo with each part rounded to bf16 (residual <= 2^-27 |W|): the
+        operands of the split-precision MFMA path (include/nbx.h "bf16x3 images")."""
+        W = W.float()
+        hi = W.to(torch.bfloat16)
+        r = W - hi.float()
+        mid = r.to(torch.bfloat16)
+        lo = (r - mid.float()).to(torch.bfloat16)
+        return hi, mid, lo
+
+    @staticmethod
+    def frag_image_x3(subs, vec, chunks: int) -> torch.Tensor:
+        """bf16x3 image for the 32x32x16 bf16 MFMA (32-channel chunks): per sub-tile and 32-deep
+        K chunk kc the block [part p 3][m 2][lane 64][j 8] holds part p of
+        W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j], zero past K / rows.
+        Returned as int16 bit patterns [chunks][F16]."""
+        blocks = []
+        for W, K in list(subs) + ([vec] if vec is not None else []):
+            kc = (K + 31) // 32
+            X = torch.zeros(chunks * 32, kc * 32, dtype=torch.float32, device=W.device)
+            n = min(W.shape[0], chunks * 32)
+            X[:n, :K] = W[:n, :K].float()
+            parts = torch.stack([t.float() for t in SEGNN.split_bf16x3(X)])      # [3][rows][kc*32]
+            # [p][c][r 32][kc][h 2][m 2][j 8] -> [c][kc][p][m][h][r][j]
+            Y = parts.reshape(3, chunks, 32, kc, 2, 2, 8).permute(1, 3, 0, 5, 4, 2, 6)
+            blocks.append(Y.reshape(chunks, -1))
+        img = torch.cat(blocks, 1).contiguous().to(torch.bfloat16)
+        return img.view(torch.int16)
+
+    @staticmethod
     def tp_images(P: dict, mul: int) -> dict:
         """packed_matrices -> the device images the kernels stage (msg2: 32-channel
         chunks for the 32x32 message kernel; every other TP: 16-channel chunks, the
@@ -264,6 +294,7 @@ class SEGNN(nn.Module):
                 subs = [(S[j * M:(j + 1) * M], Ks[j]) for j in range(parts)]
                 if stem == "msg2":
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 32, c32)
+                    out[pre + stem + "_img_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c32)
                 else:
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 16, c16)
             elif base.endswith("_v_t"):

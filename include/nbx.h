@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 2
+#define NBX_ABI_VERSION 3
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -100,6 +100,15 @@ int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size,
  * msg2_img uses CW = 32 with ceil(mul/32) chunks; every other image CW = 16 with
  * ceil(mul/16) chunks rounded up to a multiple of 4.  node_pre: 6 parts of mul
  * columns (P_dst s, gate, t, P_src s, gate, t), chunk c = channels [16 c, 16 c + 16) of each.
+ *
+ * bf16x3 images (*_img_x3, optional, NULL = fp32 MFMA path): the split-precision
+ * path writes every weight as W = hi + mid + lo, each part rounded to bf16
+ * (|W - hi - mid - lo| <= 2^-27 |W|), and every activation the same way as it is
+ * loaded; a product accumulates in fp32 the six terms hi.hi + hi.mid + mid.hi +
+ * hi.lo + mid.mid + lo.hi (dropped terms <= 2^-24 relative), fp32-level accuracy
+ * on v_mfma_f32_32x32x16_bf16.  Layout (CW = 32): per sub-tile block and 32-deep
+ * K chunk kc, [part p 3][m 2][lane 64][j 8] bf16 = part p of
+ * W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j].
  */
 #define NBX_SEGNN_MAX_LAYERS 64
 
@@ -109,6 +118,7 @@ typedef struct nbx_segnn_layer {
     const float* msg1_amf;     /* [2][3*mul]    amf (dist, m_i m_j) -> [s(2mul) t(mul)] */
     const float* msg1_bias;    /* [2*mul] */
     const float* msg2_img;     /* parts of [3*mul][2*mul] [m_s | m_v.rhat] -> [s | gate | t] + [mul][mul] m_v[:,k] -> v */
+    const void* msg2_img_x3;   /* the same operand as a bf16x3 split image ("bf16x3 images"), or NULL */
     const float* msg2_bias;    /* [2*mul] */
     const float* upd1_img;     /* [3*mul][4*mul] [x_s a_s x_v.na a_v.na] -> [s | gate | t] + [mul][2*mul] -> v */
     const float* upd1_bias;    /* [2*mul] */

@@ -1,3 +1,9 @@
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -m pytest tests/test_gpu_segnn.py tests/test_gpu_native.py tests/test_boundary.py -q -p no:cacheprovider > gpurun_out/t.log 2>&1; rc=$?; grep -E "passed|failed|FAILED|max err" gpurun_out/t.log | head -30; [ $rc -ne 0 ] && exit $rc
-bash scripts/ab_msg.sh 8x3
+timeout -k 10 300 python -m pytest tests/test_gpu_segnn.py -q -x -p no:cacheprovider > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -ne 0 ] && exit $rc
+for cfg in "NBX_X3=1" "NBX_X3=0"; do
+env $cfg NBX_TP_DEBUG=1 timeout -k 10 120 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/dbg.json 2> gpurun_out/dbg.err || exit 1
+echo "$cfg"; grep "tp_debug" gpurun_out/dbg.err | sed 's/span=[0-9]* //' | sort | uniq -c | sort -rn | head -2
+env $cfg timeout -k 10 120 python bench.py --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/b.json 2>gpurun_out/b.err || exit 1
+python -c "
+import json;d=json.loads(open('gpurun_out/b.json').read().strip().splitlines()[-1]);print(d['value'],{k[-30:]:v['avg_launch_us'] for k,v in d['roofline']['per_kind'].items()})"
+done

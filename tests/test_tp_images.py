@@ -59,7 +59,41 @@ def test_tp_images_shapes(hidden):
     assert P["layers.0.node_pre_s_img"].shape == (c16, 6 * kc(M) * 512)
     assert P["layers.0.node_pre_v_img"].shape == (c16, 6 * kc(M) * 512)
     assert P["layers.0.msg2_img"].shape == (-(-M // 32), (2 * kc(2 * M) + 2 * kc(M)) * 1024)
+    assert P["layers.0.msg2_img_x3"].shape == (-(-M // 32), (2 * kc(2 * M) + 2 * kc(M)) * 3072)
+    assert P["layers.0.msg2_img_x3"].dtype == torch.int16
     assert P["layers.1.upd1_img"].shape == (c16, (2 * kc(4 * M) + 2 * kc(2 * M)) * 512)
     assert P["layers.1.upd2_img"].shape == (c16, (kc(2 * M) + 2 * kc(M)) * 512)
     assert P["pp1_img"].shape == (c16, (2 * kc(2 * M) + 2 * kc(M)) * 512)
     assert not any(k.endswith("_s_t") or k.endswith("_v_t") for k in P)
+
+
+def test_frag_image_x3_addressing_and_split():
+    """bf16x3 image (tp_fused.h StatSKX3 path): lane l, MFMA m, element j of part p holds part p of
+    W[32 c + (l & 31)][32 kc + 16 (l >> 5) + 8 m + j]; hi + mid + lo reconstructs W to 2^-27."""
+    g = torch.Generator().manual_seed(1)
+    rows, Ks = 40, (64, 40)
+    subs = [(torch.randn(rows, max(Ks), generator=g) * 10.0 ** torch.randint(-3, 3, (rows, 1), generator=g), K)
+            for K in Ks]
+    vec = (torch.randn(rows, 32, generator=g), 32)
+    chunks = -(-rows // 32)
+    img = SEGNN.frag_image_x3(subs, vec, chunks).view(torch.bfloat16).float().numpy()
+    kcs = [-(-K // 32) for K in Ks] + [1]
+    assert img.shape == (chunks, sum(kcs) * 3072)
+    offs = np.concatenate([[0], np.cumsum(kcs)[:-1]]) * 3072
+    mats = [(W.double().numpy(), K) for W, K in subs] + [(vec[0].double().numpy(), vec[1])]
+    lane = np.arange(64)
+    for (W, K), off, kc_n in zip(mats, offs, kcs):
+        for c in range(chunks):
+            for kc in range(kc_n):
+                for m in range(2):
+                    blk = img[c, off + kc * 3072:off + (kc + 1) * 3072].reshape(3, 2, 64, 8)[:, m]
+                    ch = c * 32 + lane % 32
+                    k = 32 * kc + 16 * (lane // 32)[:, None] + 8 * m + np.arange(8)[None, :]
+                    want = np.zeros((64, 8))
+                    ok = (ch[:, None] < W.shape[0]) & (k < K)
+                    want[ok] = W[np.broadcast_to(ch[:, None], k.shape)[ok], k[ok]]
+                    got = blk.astype(np.float64).sum(0)
+                    np.testing.assert_allclose(got, want, rtol=2.0 ** -26, atol=0)
+                    # the parts are ordered and non-overlapping: |mid| <= ulp_bf16(hi)/2, |lo| <= ulp(mid)/2
+                    assert np.all(np.abs(blk[1]) <= np.abs(blk[0]) * 2.0 ** -8 + 1e-38)
+                    assert np.all(np.abs(blk[2]) <= np.abs(blk[1]) * 2.0 ** -8 + 1e-38)
