@@ -133,10 +133,10 @@ def bench_segnn(a, rank, world, device, P):
             fl_k[k] += kfl[k]
         fwd_ms += tot.value
     # rocprofv3 names of the four timed launch kinds at C2 (csrc/segnn.hip::forward_impl)
-    names = ["nbx::msg_pre_kernel(nbx::MsgPreProb)",
-             ("void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3> >(nbx::TpProb)"
-              if os.environ.get("NBX_X3") == "0" else
-              "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSKX3<6, 6, 3, 3> >(nbx::TpProb)"),
+    x3 = os.environ.get("NBX_X3") != "0"
+    names = [f"void nbx::msg_pre_kernel<{'true' if x3 else 'false'}>(nbx::MsgPreProb)",
+             ("void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSKX3<6, 6, 3, 3> >(nbx::TpProb)" if x3 else
+              "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3> >(nbx::TpProb)"),
              "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSK<12, 12, 6, 6, 4> >(nbx::TpProb, nbx::TpProb, int)",
              "void nbx::tp16_kernel<2, 1, 3, 2, 8, 3, 2, false, nbx::StatSK<6, 3, 0, 3> >(nbx::TpProb, nbx::TpProb, int)"]
     roles = ["message_layer_1: node GEMM + edge combination + gate (flops: the node GEMM)",

@@ -29,6 +29,7 @@ struct MsgPreProb {
     const float* X;      // [4][V][M]
     const float* Simg;   // [c16][F] image of node_pre_s: 6 parts x 16 channels per chunk (CW = 16)
     const float* Vimg;   // [c16][F] image of node_pre_v
+                         // (x3: the bf16x3 images, include/nbx.h "bf16x3 images")
     const float* EG;     // [V*G][8] per edge slot: rhat xyz, |rel|, m_src m_dst
     const float* amf;    // [2][3M] (dist, m_i m_j) -> (s, gate, t)
     const float* bias;   // [2M]   (s, gate)
@@ -41,7 +42,8 @@ struct MsgPreProb {
     int n_slabs;         // node groups: ceil(V / NG)
     int chunks;          // ceil(M / 16)
     int per_chunk;       // persistent blocks per chunk
-    int img_floats;      // F = 6 * ceil(M/32) * 512
+    int img_floats;      // F = 6 * ceil(M/32) * 512 (x3: * 768)
+    int x3;              // node GEMM on the split-precision bf16x3 MFMA path
     unsigned long long* dbg;  // optional per-wave phase clocks (tuning only)
     int diag;                 // tuning only: 1 = edge waves idle (timing of the GEMM side alone)
 };

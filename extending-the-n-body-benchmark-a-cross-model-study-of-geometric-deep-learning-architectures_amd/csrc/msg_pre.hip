@@ -8,12 +8,19 @@ constexpr int MP_THREADS = 512;
 // one exchange buffer: [4 planes][6 parts][16 rows][MP_RS], 16 channels per row padded to 20
 // floats so the GEMM waves' stores (lane quarters qd = 0/1 hold rows 4 apart) hit different
 // bank halves, while rows stay 16-byte aligned for the edge waves' ds_read_b128
-constexpr int MP_RS = 20, MP_PART = 16 * MP_RS;
-constexpr int MP_EX = 4 * 6 * MP_PART;
+// (X3: rows unpadded, 16 floats, so that two buffers fit beside the larger bf16x3 images)
+template <bool X3> struct MpEx {
+    static constexpr int RS = X3 ? 16 : 20, PART = 16 * RS, EX = 4 * 6 * PART;
+};
 
-__global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb P) {
+// X3: the node GEMM on the split-precision path (tp_fused.h StatSKX3; bf16x3 CW = 16 images,
+// v_mfma_f32_16x16x32_bf16 whose A fragment -- lane quarter qd holds k = 8 qd + j -- is exactly
+// the X chunk a lane loads)
+template <bool X3>
+__global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const MsgPreProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
+    constexpr int MP_RS = MpEx<X3>::RS, MP_PART = MpEx<X3>::PART, MP_EX = MpEx<X3>::EX;
     float* EX = lds + 2 * F;   // [2 buffers][MP_EX]
     float* XC = EX + 2 * MP_EX;  // pending BN of X per k: [sc_s | sc_v | sh] x (KC * 32), zero past M
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
@@ -92,10 +99,17 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
     float pm_next = 0.f;
     load_geo(0, geo_next, pm_next);
     for (int i = 0; i <= my_groups; ++i) {
+        floatx4 acc[6];
+        auto write_ex = [&](int buf) {
+            float* ex = EX + buf * MP_EX + plane * 6 * MP_PART;
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) ex[j * MP_PART + (4 * qd + jj) * MP_RS + c16] = acc[j][jj];
+        };
         if (gemm_wave) {
             if (i < my_groups) {
                 // ---- node GEMM of group i: 16 rows x 96 columns (6 parts x 16 channels)
-                floatx4 acc[6];
 #pragma unroll
                 for (int j = 0; j < 6; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
                 // B fragments double-buffered across the 32-deep K chunks: the reads of chunk
@@ -109,11 +123,11 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
                         bb[j][1] = *reinterpret_cast<const float4*>(bp + 256);
                     }
                 };
-                load_b(0, b[0]);
+                if constexpr (!X3) load_b(0, b[0]);
 #pragma unroll
                 for (int kc = 0; kc < KCMAX; ++kc) {
                     if (kc >= KC) break;
-                    if (kc + 1 < KC) load_b(kc + 1, b[(kc + 1) & 1]);
+                    if (!X3 && kc + 1 < KC) load_b(kc + 1, b[(kc + 1) & 1]);
                     // x = sc * x~ + sh (shift on the 0e plane only)
                     const float* xc = XC + (plane ? KC * 32 : 0) + kc * 32 + 8 * qd;
                     const float4 sc0 = *reinterpret_cast<const float4*>(xc);
@@ -127,23 +141,47 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
                                          fmaf(sc0.z, abuf[kc][0].z, sh0.z), fmaf(sc0.w, abuf[kc][0].w, sh0.w),
                                          fmaf(sc1.x, abuf[kc][1].x, sh1.x), fmaf(sc1.y, abuf[kc][1].y, sh1.y),
                                          fmaf(sc1.z, abuf[kc][1].z, sh1.z), fmaf(sc1.w, abuf[kc][1].w, sh1.w)};
-                    const float4 (&bc)[6][2] = b[kc & 1];
-#pragma unroll
-                    for (int s = 0; s < 8; ++s)
+                    if constexpr (X3) {
+                        bf16x8 a[3];
+                        tp_split3(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]}, a[0], a[1],
+                                  a[2]);
+                        const bf16x8* bp = reinterpret_cast<const bf16x8*>(img) + kc * 192 + lane;
+                        bf16x8 bx[6][3];
 #pragma unroll
                         for (int j = 0; j < 6; ++j)
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], f4get(bc[j][s >> 2], s & 3), acc[j], 0,
-                                                                          0, 0);
+#pragma unroll
+                            for (int p3 = 0; p3 < 3; ++p3) bx[j][p3] = bp[j * KC * 192 + p3 * 64];
+                        // six cross terms, smallest first, round-robin over the 6 accumulators
+                        constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+                        // The MFMAs run as one fenced block in this round-robin order, and the next
+                        // chunk's operand loads start a pad after it.  Measured: when the scheduler
+                        // interleaved the next chunk's ds_reads with back-to-back dependent MFMAs, LDS
+                        // returns overwrote the A/B registers of an MFMA still waiting on its
+                        // accumulator, corrupting a few node groups per launch.
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int tt = 0; tt < 6; ++tt)
+#pragma unroll
+                            for (int j = 0; j < 6; ++j)
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], bx[j][TB[tt]], acc[j], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        asm volatile("s_nop 7\n\ts_nop 7");
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else {
+                        const float4 (&bc)[6][2] = b[kc & 1];
+#pragma unroll
+                        for (int s = 0; s < 8; ++s)
+#pragma unroll
+                            for (int j = 0; j < 6; ++j)
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], f4get(bc[j][s >> 2], s & 3),
+                                                                              acc[j], 0, 0, 0);
+                    }
                 }
                 // prefetch the next group's rows
 #pragma unroll
                 for (int kc = 0; kc < KCMAX; ++kc)
                     if (kc < KC) load_a(i + 1, kc, abuf[kc]);
-                float* ex = EX + (i & 1) * MP_EX + plane * 6 * MP_PART;
-#pragma unroll
-                for (int j = 0; j < 6; ++j)
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) ex[j * MP_PART + (4 * qd + jj) * MP_RS + c16] = acc[j][jj];
+                write_ex(i & 1);
                 tick(c_gemm);
             }
         } else if (i > 0 && live && !P.diag) {
@@ -200,8 +238,10 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
             tick(c_edge);
         }
         // LDS hand-off only: wait for this wave's LDS traffic, not for its global stores
+        // (the empty asm after each barrier keeps the compiler from hoisting LDS accesses above it)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         tick(c_ex);
     }
     if (P.dbg && lane == 0) {
@@ -211,7 +251,7 @@ __global__ __launch_bounds__(MP_THREADS, 2) void msg_pre_kernel(const MsgPreProb
 }
 
 inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
-    return ((size_t)2 * p.img_floats + 2 * MP_EX + 3 * 32 * ((p.M + 31) / 32)) * 4;
+    return ((size_t)2 * p.img_floats + 2 * (p.x3 ? MpEx<true>::EX : MpEx<false>::EX) + 3 * 32 * ((p.M + 31) / 32)) * 4;
 }
 
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
@@ -225,7 +265,7 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         return NBX_E_UNSUPPORTED;
     }
     p.chunks = (p.M + 15) / 16;
-    p.img_floats = 6 * ((p.M + 31) / 32) * 512;
+    p.img_floats = 6 * ((p.M + 31) / 32) * (p.x3 ? 768 : 512);
     p.n_slabs = (int)((p.V + p.NG - 1) / p.NG);
     // one block per CU (LDS-bound); balance the group rounds over the chunk's blocks
     int per = num_cus / p.chunks;
@@ -240,11 +280,16 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
     }
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL(msg_pre_kernel, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    if (p.x3)
+        hipLaunchKernelGGL(msg_pre_kernel<true>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    else
+        hipLaunchKernelGGL(msg_pre_kernel<false>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

@@ -552,21 +552,25 @@ unsigned long long* tp_dbg_buf(hipStream_t st) {
 // NBX_TP_DEBUG=1: per-wave phase clocks of the message kernel printed to stderr (tuning only)
 int tp_debug_dump(const nbx::TpProb& p, hipStream_t st, int waves) {
     const int n = p.chunks * p.blocks_per_chunk * waves;
-    std::vector<unsigned long long> h((size_t)n * 4);
+    std::vector<unsigned long long> h((size_t)n * 6);
     NBX_HIP(hipStreamSynchronize(st));
     NBX_HIP(hipMemcpy(h.data(), p.dbg, h.size() * 8, hipMemcpyDeviceToHost));
-    unsigned long long t0 = ~0ull, t3 = 0;
-    double s01 = 0, s12 = 0, s23 = 0;
+    unsigned long long w0 = ~0ull, w1 = 0;
+    double s01 = 0, s12 = 0, s23 = 0, sw = 0, sc = 0;
     int cnt = 0;
     for (int i = 0; i < n; ++i) {
-        const unsigned long long* d = &h[(size_t)i * 4];
+        const unsigned long long* d = &h[(size_t)i * 6];
         if (!d[3]) continue;
-        t0 = std::min(t0, d[0]);
-        t3 = std::max(t3, d[3]);
+        w0 = std::min(w0, d[4]);
+        w1 = std::max(w1, d[5]);
+        sw += (double)(d[5] - d[4]);
+        sc += (double)(d[3] - d[0]);
         if (d[2]) { s01 += d[1] - d[0]; s12 += d[2] - d[1]; s23 += d[3] - d[2]; ++cnt; }
     }
-    fprintf(stderr, "tp_debug waves=%d span=%llu stage=%.0f loop=%.0f epi=%.0f (avg clocks)\n", cnt, t3 - t0,
-            s01 / std::max(cnt, 1), s12 / std::max(cnt, 1), s23 / std::max(cnt, 1));
+    // wall_clock64 ticks at 100 MHz on every XCD: the waves' span and the shader clock rate
+    fprintf(stderr, "tp_debug waves=%d stage=%.0f loop=%.0f epi=%.0f (avg clocks) waves_span=%.2fus wave_avg=%.2fus clk=%.2fGHz\n",
+            cnt, s01 / std::max(cnt, 1), s12 / std::max(cnt, 1), s23 / std::max(cnt, 1), (w1 - w0) / 100.0,
+            sw / std::max(cnt, 1) / 100.0, sw > 0 ? sc / sw * 0.1 : 0.0);
     return NBX_OK;
 }
 
@@ -767,6 +771,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             mp.X = ws.X; mp.Simg = L.node_pre_s_img; mp.Vimg = L.node_pre_v_img; mp.EG = ws.EG;
             mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V; mp.xcoef = xprev;
             mp.V = V; mp.N = (int)N; mp.G = (int)d.G; mp.M = M; mp.NG = nbx::msg_pre_group((int)N);
+            if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && x3_enabled() && !getenv("NBX_X3_NOMP")) {
+                mp.Simg = static_cast<const float*>(L.node_pre_s_img_x3);
+                mp.Vimg = static_cast<const float*>(L.node_pre_v_img_x3);
+                mp.x3 = 1;
+            }
             if (int rc = run_msg_pre(mp, st, tm)) return rc;
         } else if (N > 1) {
             // systems larger than a 16-row tile: node precomputation (plain GEMM, part-major

@@ -244,6 +244,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     // (the stream is padded to a multiple of D), and the load for chunk i + D - 1 is issued
     // before the MFMAs of chunk i.  The first D - 1 loads go out before the weight staging.
     const unsigned long long c_start = P.dbg ? clock64() : 0ull;
+    const unsigned long long w_start = P.dbg ? wall_clock64() : 0ull;   // 100 MHz, chip-wide
     int rt = wid;
     float4 buf[D][4];
     // static schedule (SK::on): items = K0 scalar chunks, then KV chunks per vector plane
@@ -628,8 +629,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     }
 done:
     if (P.dbg && lane == 0) {
-        unsigned long long* d = P.dbg + ((size_t)blockIdx.x * WAVES + wave) * 4;
+        unsigned long long* d = P.dbg + ((size_t)blockIdx.x * WAVES + wave) * 6;
         d[0] = c_start; d[1] = c_staged; d[2] = c_loop; d[3] = clock64();
+        d[4] = w_start; d[5] = wall_clock64();
     }
     if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
         // reduce the block's waves in LDS: one partial row per block, layout [chunk][block][3][32]

@@ -247,20 +247,26 @@ class SEGNN(nn.Module):
         return hi, mid, lo
 
     @staticmethod
-    def frag_image_x3(subs, vec, chunks: int) -> torch.Tensor:
-        """bf16x3 image for the 32x32x16 bf16 MFMA (32-channel chunks): per sub-tile and 32-deep
-        K chunk kc the block [part p 3][m 2][lane 64][j 8] holds part p of
-        W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j], zero past K / rows.
-        Returned as int16 bit patterns [chunks][F16]."""
+    def frag_image_x3(subs, vec, chunks: int, cw: int = 32) -> torch.Tensor:
+        """bf16x3 image (include/nbx.h "bf16x3 images"), per sub-tile and 32-deep K chunk kc:
+          cw = 32 (v_mfma_f32_32x32x16_bf16): block [part p 3][m 2][lane 64][j 8] = part p of
+                  W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j];
+          cw = 16 (v_mfma_f32_16x16x32_bf16): block [part p 3][lane 64][j 8] = part p of
+                  W[c = 16 chunk + (lane & 15)][k = 32 kc + 8 (lane >> 4) + j];
+        zero past K / rows.  Returned as int16 bit patterns [chunks][F16]."""
         blocks = []
         for W, K in list(subs) + ([vec] if vec is not None else []):
             kc = (K + 31) // 32
-            X = torch.zeros(chunks * 32, kc * 32, dtype=torch.float32, device=W.device)
-            n = min(W.shape[0], chunks * 32)
+            X = torch.zeros(chunks * cw, kc * 32, dtype=torch.float32, device=W.device)
+            n = min(W.shape[0], chunks * cw)
             X[:n, :K] = W[:n, :K].float()
             parts = torch.stack([t.float() for t in SEGNN.split_bf16x3(X)])      # [3][rows][kc*32]
-            # [p][c][r 32][kc][h 2][m 2][j 8] -> [c][kc][p][m][h][r][j]
-            Y = parts.reshape(3, chunks, 32, kc, 2, 2, 8).permute(1, 3, 0, 5, 4, 2, 6)
+            if cw == 32:
+                # [p][c][r 32][kc][h 2][m 2][j 8] -> [c][kc][p][m][h][r][j]
+                Y = parts.reshape(3, chunks, 32, kc, 2, 2, 8).permute(1, 3, 0, 5, 4, 2, 6)
+            else:
+                # [p][c][r 16][kc][qd 4][j 8] -> [c][kc][p][qd][r][j]
+                Y = parts.reshape(3, chunks, 16, kc, 4, 8).permute(1, 3, 0, 4, 2, 5)
             blocks.append(Y.reshape(chunks, -1))
         img = torch.cat(blocks, 1).contiguous().to(torch.bfloat16)
         return img.view(torch.int16)
@@ -284,6 +290,7 @@ class SEGNN(nn.Module):
                 B = P[key]                                    # [6M][M]: 6 parts of M output columns
                 subs = [(B[j * M:(j + 1) * M], M) for j in range(6)]
                 out[pre + base[:-2] + "_img"] = img(subs, None, 16, c16)
+                out[pre + base[:-2] + "_img_x3"] = SEGNN.frag_image_x3(subs, None, c16, 16)
             elif base in ("msg2_s_t", "upd1_s_t", "upd2_s_t", "pp1_s_t"):
                 stem = base[:-4]
                 S, V = P[key], P[pre + stem + "_v_t"]

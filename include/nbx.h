@@ -106,15 +106,20 @@ int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size,
  * (|W - hi - mid - lo| <= 2^-27 |W|), and every activation the same way as it is
  * loaded; a product accumulates in fp32 the six terms hi.hi + hi.mid + mid.hi +
  * hi.lo + mid.mid + lo.hi (dropped terms <= 2^-24 relative), fp32-level accuracy
- * on v_mfma_f32_32x32x16_bf16.  Layout (CW = 32): per sub-tile block and 32-deep
- * K chunk kc, [part p 3][m 2][lane 64][j 8] bf16 = part p of
- * W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j].
+ * on v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16.  Layout per sub-tile block and
+ * 32-deep K chunk kc:
+ *   CW = 32: [part p 3][m 2][lane 64][j 8] bf16 = part p of
+ *            W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j];
+ *   CW = 16: [part p 3][lane 64][j 8] bf16 = part p of
+ *            W[c = 16 chunk + (lane & 15)][k = 32 kc + 8 (lane >> 4) + j].
  */
 #define NBX_SEGNN_MAX_LAYERS 64
 
 typedef struct nbx_segnn_layer {
     const float* node_pre_s_img; /* image of [6*mul][mul] x_s -> [P_dst(2mul) R_dst(mul) P_src(2mul) R_src(mul)] */
     const float* node_pre_v_img; /* image of [6*mul][mul] x_v[:,k] -> [Q_dst(2mul) S_dst(mul) Q_src(2mul) S_src(mul)] */
+    const void* node_pre_s_img_x3; /* bf16x3 images of the same (CW = 16), or NULL */
+    const void* node_pre_v_img_x3;
     const float* msg1_amf;     /* [2][3*mul]    amf (dist, m_i m_j) -> [s(2mul) t(mul)] */
     const float* msg1_bias;    /* [2*mul] */
     const float* msg2_img;     /* parts of [3*mul][2*mul] [m_s | m_v.rhat] -> [s | gate | t] + [mul][mul] m_v[:,k] -> v */

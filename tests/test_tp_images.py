@@ -97,3 +97,25 @@ def test_frag_image_x3_addressing_and_split():
                     # the parts are ordered and non-overlapping: |mid| <= ulp_bf16(hi)/2, |lo| <= ulp(mid)/2
                     assert np.all(np.abs(blk[1]) <= np.abs(blk[0]) * 2.0 ** -8 + 1e-38)
                     assert np.all(np.abs(blk[2]) <= np.abs(blk[1]) * 2.0 ** -8 + 1e-38)
+
+
+def test_frag_image_x3_cw16_addressing():
+    """CW = 16 bf16x3 image (msg_pre.hip X3 node GEMM, v_mfma_f32_16x16x32_bf16): lane l, element j
+    of part p holds part p of W[16 c + (l & 15)][32 kc + 8 (l >> 4) + j]."""
+    g = torch.Generator().manual_seed(2)
+    rows, Ks = 40, (96, 96)
+    subs = [(torch.randn(rows, 96, generator=g), K) for K in Ks]
+    chunks = -(-rows // 16)
+    img = SEGNN.frag_image_x3(subs, None, chunks, 16).view(torch.bfloat16).float().numpy()
+    assert img.shape == (chunks, 2 * 3 * 3 * 64 * 8)
+    lane = np.arange(64)
+    for j, (W, K) in enumerate(subs):
+        W = W.double().numpy()
+        for c in range(chunks):
+            for kc in range(3):
+                off = (j * 3 + kc) * 1536
+                blk = img[c, off:off + 1536].reshape(3, 64, 8)
+                ch = c * 16 + lane % 16
+                k = 32 * kc + 8 * (lane // 16)[:, None] + np.arange(8)[None, :]
+                want = np.where(ch[:, None] < rows, W[np.minimum(ch, rows - 1)[:, None], k], 0.0)
+                np.testing.assert_allclose(blk.astype(np.float64).sum(0), want, rtol=2.0 ** -26, atol=0)
