@@ -663,11 +663,17 @@ int run_msg_pre(nbx::MsgPreProb& p, hipStream_t st, KernelTiming* tm) {
         std::vector<unsigned long long> h((size_t)n * 4);
         NBX_HIP(hipStreamSynchronize(st));
         NBX_HIP(hipMemcpy(h.data(), p.dbg, h.size() * 8, hipMemcpyDeviceToHost));
-        double s[4] = {0, 0, 0, 0};
-        for (int i = 0; i < n; ++i)
+        // waves 0-3 of a block run the GEMM, 4-7 the edges: average each counter over its role
+        double s[4] = {0, 0, 0, 0}, exg = 0, exe = 0;
+        for (int i = 0; i < n; ++i) {
             for (int k = 0; k < 4; ++k) s[k] += (double)h[(size_t)i * 4 + k];
-        fprintf(stderr, "tp_debug msg_pre waves=%d slabs=%d per_chunk=%d stage=%.0f gemm=%.0f ex=%.0f edge=%.0f\n", n,
-                p.n_slabs, p.per_chunk, s[0] / n, s[1] / n, s[2] / n, s[3] / n);
+            ((i & 7) < 4 ? exg : exe) += (double)h[(size_t)i * 4 + 2];
+        }
+        const double half = n / 2.0;
+        fprintf(stderr,
+                "tp_debug msg_pre waves=%d slabs=%d per_chunk=%d stage=%.0f gemm=%.0f ex(gemm waves)=%.0f edge=%.0f "
+                "ex(edge waves)=%.0f (avg clocks per wave of the role)\n",
+                n, p.n_slabs, p.per_chunk, s[0] / n, s[1] / half, exg / half, s[3] / half, exe / half);
         return NBX_OK;
     }
     if (!tm) return nbx::msg_pre_launch(p, st);

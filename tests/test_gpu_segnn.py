@@ -162,3 +162,14 @@ def test_non_fc_graph_rejected(hip_device):
     g.edge_index = G.fc_edge_index(2, 5, hip_device).flip(0)
     with pytest.raises(NotImplementedError):
         model(g)
+
+
+def test_forward_deterministic_c2(hip_device):
+    """Repeated C2 forwards are bit-identical (no run-to-run variation from the kernels' LDS
+    hand-offs or MFMA operand staging)."""
+    model = make_model(192, 6, hip_device, perturb_bn=False).eval()
+    B, N = 1024, 5
+    pos, vel, mass = states(B, N, seed=5)
+    outs = [gpu_forward(model, pos, vel, mass, B, N, hip_device) for _ in range(3)]
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
