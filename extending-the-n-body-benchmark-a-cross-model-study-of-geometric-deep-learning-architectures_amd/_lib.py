@@ -22,7 +22,7 @@ c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_fl
 class SegnnLayer(ctypes.Structure):
     _fields_ = [(n, c_p) for n in (
         "node_pre_s_img", "node_pre_v_img", "node_pre_s_img_x3", "node_pre_v_img_x3", "msg1_amf", "msg1_bias", "msg2_img", "msg2_img_x3", "msg2_bias",
-        "upd1_img", "upd1_bias", "upd2_img", "upd2_bias",
+        "upd1_img", "upd1_img_x3", "upd1_bias", "upd2_img", "upd2_bias",
         "msg_bn_weight", "msg_bn_bias", "msg_bn_running_mean", "msg_bn_running_var",
         "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var")]
 

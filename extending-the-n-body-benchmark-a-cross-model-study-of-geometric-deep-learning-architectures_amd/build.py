@@ -22,9 +22,11 @@ LIB = os.path.join(OUT_DIR, f"libnbx_{_TAG}.so" if _TAG else "libnbx.so")
 ARCH = os.environ.get("NBX_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
          "-munsafe-fp-atomics"]
-# per-file extra flags (measured: disabling packed fp32 in msg_pre.hip, whose VALU work runs beside
-# the other wave's MFMAs, did not help: +1 %); NBX_FILE_FLAGS="file.hip:-flag,-flag;..." adds more
-FILE_FLAGS = {}
+# per-file extra flags: the split-precision MFMA kernels' VALU work (operand splits, the message
+# kernel's edge combination) runs beside MFMAs, where packed fp32 VALU costs extra cycles; with
+# SLP vectorisation off these files run 1.8 % more steps/s (measured, C2).
+# NBX_FILE_FLAGS="file.hip:-flag,-flag;..." adds more (A/B builds).
+FILE_FLAGS = {"segnn.hip": ["-fno-slp-vectorize"], "msg_pre.hip": ["-fno-slp-vectorize"]}
 for _item in filter(None, os.environ.get("NBX_FILE_FLAGS", "").split(";")):
     _f, _fl = _item.split(":", 1)
     FILE_FLAGS.setdefault(_f, []).extend(_fl.split(","))

@@ -510,6 +510,7 @@ bool sk_matches(const nbx::TpProb& p, int NS, int NV) {
 using SK_UPD1 = nbx::StatSK<12, 12, 6, 6>;
 using SK_UPD1_32 = nbx::StatSK<4, 4, 2, 2>;
 using SK_UPD1_SEG = nbx::StatSK<12, 12, 6, 6, 4>;
+using SK_UPD1_SEG_X3 = nbx::StatSKX3<12, 12, 6, 6, 4>;
 using SK_UPD1_32_SEG = nbx::StatSK<4, 4, 2, 2, 4>;
 using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
 using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
@@ -849,7 +850,10 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
-            if (M == 96) {
+            if (M == 96 && L.upd1_img_x3 && x3_enabled()) {
+                p.B = static_cast<const float*>(L.upd1_img_x3);
+                if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_X3>(p, st, tm)) return rc;
+            } else if (M == 96) {
                 if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG>(p, st, tm)) return rc;
             } else {
                 if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG>(p, st, tm)) return rc;

@@ -28,7 +28,7 @@ constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
 // `split`, P1 above): node_pre's scalar-row and vector-row GEMMs fill the chip together.
 template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, bool DUAL = false,
           class SK = DynSK>
-__global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
+__global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
     const bool second = DUAL && (int)blockIdx.x >= split;
     const TpProb& P = second ? P1 : P0;
     const int bidx = second ? (int)blockIdx.x - split : (int)blockIdx.x;
@@ -261,10 +261,13 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
             floatx4 accv2[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) accv2[pl] = floatx4{0.f, 0.f, 0.f, 0.f};
-            auto compute_item = [&](auto ic, const float4 (&cb)[2]) {
+            // item's A chunk (lane quarter qd: k = 8 qd + e), with the segmented input's per-(segment, k)
+            // BatchNorm scale / shift applied
+            auto item_a = [&](auto ic, const float4 (&cb)[2], float (&av)[8]) {
                 constexpr int item = decltype(ic)::value;
                 constexpr bool sc = item < SK::K0;
-                float av[8] = {cb[0].x, cb[0].y, cb[0].z, cb[0].w, cb[1].x, cb[1].y, cb[1].z, cb[1].w};
+                av[0] = cb[0].x; av[1] = cb[0].y; av[2] = cb[0].z; av[3] = cb[0].w;
+                av[4] = cb[1].x; av[5] = cb[1].y; av[6] = cb[1].z; av[7] = cb[1].w;
                 if constexpr (SK::SEG == 4) {
                     constexpr int kc = sc ? item : (item - SK::K0) % SK::KV;
                     constexpr int cps = sc ? SK::K0 / 4 : SK::KV / 2;
@@ -286,6 +289,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                         for (int e = 0; e < 8; ++e) av[e] *= scv[e];
                     }
                 }
+            };
+            auto compute_item = [&](auto ic, const float4 (&cb)[2]) {
+                constexpr int item = decltype(ic)::value;
+                constexpr bool sc = item < SK::K0;
+                float av[8];
+                item_a(ic, cb, av);
                 if constexpr (sc) {
                     constexpr int NA = (item < SK::K0 ? 1 : 0) + (NS > 1 && item < SK::K1 ? 1 : 0) +
                                        (NS > 2 && item < SK::K2 ? 1 : 0);
@@ -333,7 +342,117 @@ __global__ __launch_bounds__(64 * WAVES, 2) void tp16_kernel(const TpProb P0, co
                     }
                 }
             };
-            if (SK::on && rt < row_tiles) {
+            if (SK::PREC == 1 && rt < row_tiles) {
+                if constexpr (SK::PREC == 1) {
+                    // Split-precision path (tp_fused.h StatSKX3): v_mfma_f32_16x16x32_bf16, whose A
+                    // fragment (lane quarter qd: k = 8 qd + j) is exactly the chunk a lane loads.
+                    // Item u's B fragments are read from LDS while item u-1's MFMAs run, into a
+                    // register set that stays allocated (empty asm uses) until item u+1's MFMAs have
+                    // issued: a register is never refilled while an MFMA reading it may be pending
+                    // (msg_pre.hip: LDS returns overwriting a pending MFMA's operands corrupted data).
+                    constexpr int OB[4] = {0, SK::K0, SK::K0 + SK::K1, SK::K0 + SK::K1 + SK::K2};
+                    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+                    auto read_b = [&](auto ic, bf16x8 (&bx)[CG][NS > 1 ? NS : 1][3]) {
+                        constexpr int item = decltype(ic)::value;
+                        if constexpr (item < SK::K0) {
+                            static_for<0, NS>([&](auto jc) {
+                                constexpr int j = decltype(jc)::value;
+                                constexpr int KCj = j == 0 ? SK::K0 : j == 1 ? SK::K1 : SK::K2;
+                                if constexpr (item < KCj)
+#pragma unroll
+                                    for (int g = 0; g < CG; ++g)
+#pragma unroll
+                                        for (int p3 = 0; p3 < 3; ++p3)
+                                            bx[g][j][p3] = reinterpret_cast<const bf16x8*>(lds + g * stride_g)
+                                                [(OB[j] + item) * 192 + p3 * 64 + lane];
+                            });
+                        } else {
+                            constexpr int kc = (item - SK::K0) % SK::KV;
+#pragma unroll
+                            for (int g = 0; g < CG; ++g)
+#pragma unroll
+                                for (int p3 = 0; p3 < 3; ++p3)
+                                    bx[g][0][p3] = reinterpret_cast<const bf16x8*>(lds + g * stride_g)
+                                        [(OB[NS] + kc) * 192 + p3 * 64 + lane];
+                        }
+                    };
+                    auto keep = [&](const bf16x8& v) { asm volatile("" ::"v"(v)); };
+                    slice_call([&](auto sc_) {
+                        constexpr int lo = decltype(sc_)::value * SNIT / KS;
+                        constexpr int n = (decltype(sc_)::value + 1) * SNIT / KS - lo;
+                        bf16x8 bx[3][CG][NS > 1 ? NS : 1][3];   // item u in set u % 3
+                        bf16x8 ax[3][3];
+                        read_b(std::integral_constant<int, lo>{}, bx[0]);
+                        static_for<0, n>([&](auto uc) {
+                            constexpr int u = decltype(uc)::value, item = lo + u;
+                            if constexpr (u + PF - 1 < n)
+                                load_item(std::integral_constant<int, item + PF - 1>{}, rt, ring[(u + PF - 1) % PF]);
+                            __builtin_amdgcn_sched_barrier(0);
+                            if constexpr (u + 1 < n) read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % 3]);
+                            float av[8];
+                            item_a(std::integral_constant<int, item>{}, ring[u % PF], av);
+                            tp_split3(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]},
+                                      ax[u % 3][0], ax[u % 3][1], ax[u % 3][2]);
+                            const bf16x8 (&b)[CG][NS > 1 ? NS : 1][3] = bx[u % 3];
+                            const bf16x8 (&a)[3] = ax[u % 3];
+                            if constexpr (item < SK::K0) {
+                                constexpr int NA = 1 + (NS > 1 && item < SK::K1 ? 1 : 0) + (NS > 2 && item < SK::K2 ? 1 : 0);
+#pragma unroll
+                                for (int tt = 0; tt < 6; ++tt)
+#pragma unroll
+                                    for (int g = 0; g < CG; ++g)
+#pragma unroll
+                                        for (int j = 0; j < NA; ++j)
+                                            acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], b[g][j][TB[tt]],
+                                                                                                acc[g][j], 0, 0, 0);
+                            } else {
+                                constexpr int plane = (item - SK::K0) / SK::KV;
+#pragma unroll
+                                for (int tt = 0; tt < 6; ++tt) {
+                                    if constexpr (CG == 1) {
+                                        if (tt & 1)
+                                            accv2[plane] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                                a[TA[tt]], b[0][0][TB[tt]], accv2[plane], 0, 0, 0);
+                                        else
+                                            acc[0][NS + plane] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                                a[TA[tt]], b[0][0][TB[tt]], acc[0][NS + plane], 0, 0, 0);
+                                    } else {
+#pragma unroll
+                                        for (int g = 0; g < CG; ++g)
+                                            acc[g][NS + plane] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                                a[TA[tt]], b[g][0][TB[tt]], acc[g][NS + plane], 0, 0, 0);
+                                    }
+                                }
+                            }
+                            // item u-1's operands may be reused from here on
+                            if constexpr (u > 0) {
+                                constexpr int pu = (u + 2) % 3, pitem = item - 1;   // item u-1's set
+                                constexpr int PNA = pitem < SK::K0 ? 1 + (NS > 1 && pitem < SK::K1 ? 1 : 0) +
+                                                                         (NS > 2 && pitem < SK::K2 ? 1 : 0)
+                                                                   : 1;
+#pragma unroll
+                                for (int p3 = 0; p3 < 3; ++p3) keep(ax[pu][p3]);
+#pragma unroll
+                                for (int g = 0; g < CG; ++g)
+#pragma unroll
+                                    for (int j = 0; j < PNA; ++j)
+#pragma unroll
+                                        for (int p3 = 0; p3 < 3; ++p3) keep(bx[pu][g][j][p3]);
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                        });
+                        // the last item's operands: a pad for its MFMAs, then free
+                        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+                        static_for<0, PF - 1>([&](auto uc) {
+                            constexpr int u = decltype(uc)::value;
+                            if constexpr (u < n) load_item(std::integral_constant<int, lo + u>{}, next_rt, ring[u % PF]);
+                        });
+                    });
+                    if constexpr (CG == 1 && NV)
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) acc[0][NS + pl] += accv2[pl];
+                }
+            } else if (SK::on && rt < row_tiles) {
                 if constexpr (SK::on) {
                     slice_call([&](auto sc_) {
                         constexpr int lo = decltype(sc_)::value * SNIT / KS;
@@ -559,8 +678,9 @@ template <int CG>
 inline int tp16_lds_floats(const TpProb& p) { return tp_img_floats(p, 16) * CG; }
 
 // geometry of one problem: fills p.lds_floats / blocks_per_chunk, returns the block count
+// prec 1: bf16x3 images (1.5x the floats of the fp32 ones)
 template <int NS, int NV, int EPI, int CG, int WAVES, int KS>
-int tp16_geom(TpProb& p, int num_cus, int* blocks) {
+int tp16_geom(TpProb& p, int num_cus, int* blocks, int prec = 0) {
     p.NS = NS;
     p.NV = NV;
     p.epi = EPI;
@@ -576,8 +696,8 @@ int tp16_geom(TpProb& p, int num_cus, int* blocks) {
             set_error("tp16: scalar sub-tile K must be non-increasing");
             return NBX_E_INVAL;
         }
-    p.img_floats = tp_img_floats(p, 16);
-    p.lds_floats = tp16_lds_floats<CG>(p) + (p.seg_s[0] ? ((10 * p.M + 3) & ~3) : 0);
+    p.img_floats = tp_img_floats(p, 16) * (prec ? 3 : 2) / 2;
+    p.lds_floats = p.img_floats * CG + (p.seg_s[0] ? ((10 * p.M + 3) & ~3) : 0);
     if (KS > 1) p.lds_floats += (WAVES / KS) * (KS - 1) * CG * (NS + 3 * NV) * 4 * 64;
     const size_t lds = (size_t)p.lds_floats * 4;
     if (lds > 160 * 1024) {
@@ -641,7 +761,7 @@ int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
 template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, class SK = DynSK>
 int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     int b = 0;
-    if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p, num_cus, &b)) return rc;
+    if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p, num_cus, &b, SK::PREC)) return rc;
     return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, false, SK>(p, p, b, 0, st);
 }
 

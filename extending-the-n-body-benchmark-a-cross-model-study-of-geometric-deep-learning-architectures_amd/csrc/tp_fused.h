@@ -104,10 +104,10 @@ struct StatSK {
 // into three bf16 parts each and every product is the fp32 sum of the six leading cross terms on
 // v_mfma_f32_32x32x16_bf16 -- fp32-level accuracy at 2.7x the fp32 MFMA rate (12 x 32 cycles per
 // 32 x 32 x 32 block instead of 16 x 64).  The weight image is the bf16x3 one (1.5x the fp32 bytes).
-template <int A, int B, int C, int V>
+template <int A, int B, int C, int V, int S = 0>
 struct StatSKX3 {
     static constexpr bool on = true;
-    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = 0, PREC = 1;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 1;
 };
 
 // x = hi + mid + lo (+ <= 2^-27 |x|), each part bf16: RNE conversions (v_cvt_pk_bf16_f32, two
@@ -119,13 +119,10 @@ __device__ inline unsigned tp_pk_bf16(tp_f2 v) { return __builtin_bit_cast(unsig
 __device__ inline tp_f2 tp_unpk_bf16(unsigned u) {
     return tp_f2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
 }
-// plain v_sub_f32 (kept from being SLP-packed into v_pk_add_f32, which costs extra cycles beside
-// MFMAs -- MI355X_MICROARCH "price of one filler beside MFMAs")
-__device__ inline float tp_sub(float a, float b) {
-    float r;
-    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
+// plain v_sub_f32: the files holding split-precision kernels are built with -fno-slp-vectorize
+// (build.py), so these are not packed into v_pk_add_f32, which costs extra cycles beside MFMAs
+// (MI355X_MICROARCH "price of one filler beside MFMAs"; measured +1.8 % steps/s)
+__device__ inline float tp_sub(float a, float b) { return a - b; }
 __device__ inline tp_f2 tp_sub2(tp_f2 a, tp_f2 b) { return tp_f2{tp_sub(a.x, b.x), tp_sub(a.y, b.y)}; }
 __device__ inline void tp_split3(const float4& a, const float4& b, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
     const tp_f2 f[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};

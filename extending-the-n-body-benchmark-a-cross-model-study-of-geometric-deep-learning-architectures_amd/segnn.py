@@ -304,6 +304,8 @@ class SEGNN(nn.Module):
                     out[pre + stem + "_img_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c32)
                 else:
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 16, c16)
+                    if stem == "upd1":
+                        out[pre + stem + "_img_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c16, 16)
             elif base.endswith("_v_t"):
                 continue
             else:

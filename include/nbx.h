@@ -126,6 +126,7 @@ typedef struct nbx_segnn_layer {
     const void* msg2_img_x3;   /* the same operand as a bf16x3 split image ("bf16x3 images"), or NULL */
     const float* msg2_bias;    /* [2*mul] */
     const float* upd1_img;     /* [3*mul][4*mul] [x_s a_s x_v.na a_v.na] -> [s | gate | t] + [mul][2*mul] -> v */
+    const void* upd1_img_x3;   /* bf16x3 image of the same (CW = 16), or NULL */
     const float* upd1_bias;    /* [2*mul] */
     const float* upd2_img;     /* [2*mul][2*mul] [h_s | h_v.na] -> [s | t] + [mul][mul] -> v */
     const float* upd2_bias;    /* [mul] */

@@ -62,6 +62,7 @@ def test_tp_images_shapes(hidden):
     assert P["layers.0.msg2_img_x3"].shape == (-(-M // 32), (2 * kc(2 * M) + 2 * kc(M)) * 3072)
     assert P["layers.0.msg2_img_x3"].dtype == torch.int16
     assert P["layers.1.upd1_img"].shape == (c16, (2 * kc(4 * M) + 2 * kc(2 * M)) * 512)
+    assert P["layers.1.upd1_img_x3"].shape == (c16, (2 * kc(4 * M) + 2 * kc(2 * M)) * 1536)
     assert P["layers.1.upd2_img"].shape == (c16, (kc(2 * M) + 2 * kc(M)) * 512)
     assert P["pp1_img"].shape == (c16, (2 * kc(2 * M) + 2 * kc(M)) * 512)
     assert not any(k.endswith("_s_t") or k.endswith("_v_t") for k in P)
