@@ -40,6 +40,8 @@ sys.path.insert(0, ROOT)
 HIDDEN, LAYERS, NBODY, BATCH = 192, 6, 5, 1024
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0         # MI355X_MICROARCH.md: BF16 MFMA, dense (~2.5 PF)
+X3_TERMS = 6                           # bf16x3 split: bf16 MFMA products per fp32 product
 FP64_VALU_PEAK_TFLOPS = 78.6           # MI355X spec; no f64 MFMA used by the integrator
 SURVEY_GFLOP_PER_STEP = 67.73          # algorithmic work of the reference formulation
 
@@ -171,6 +173,14 @@ def bench_segnn(a, rank, world, device, P):
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                      "avg_launch_us": round(dom_avg_s * 1e6, 3), "gflop_per_launch": round(dom_flops / 1e9, 4),
+                     # achieved / frac: fp32-accurate GEMM flops against the fp32 MFMA peak; the
+                     # split-precision path executes them as X3_TERMS bf16 MFMA products each
+                     "mfma_path": ("bf16x3 split (fp32-accurate), v_mfma_f32_*_bf16" if x3 else
+                                   "fp32, v_mfma_f32_*_f32"),
+                     "executed_bf16_tflops": round(achieved_tflops * X3_TERMS, 2) if x3 else None,
+                     "executed_bf16_frac": (round(achieved_tflops * X3_TERMS / BF16_MFMA_PEAK_TFLOPS, 4)
+                                            if x3 else None),
+                     "timing": "hipExtLaunchKernel start/stop events (kernel execution interval)",
                      "fused_tp_share_of_forward": round(sum(ms_k) / fwd_ms, 3), "per_kind": per_kind},
         "finite": finite,
     }

@@ -287,9 +287,9 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         attr_set = true;
     }
     if (p.x3)
-        hipLaunchKernelGGL(msg_pre_kernel<true>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+        NBX_TIMED_LAUNCH(msg_pre_kernel<true>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     else
-        hipLaunchKernelGGL(msg_pre_kernel<false>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+        NBX_TIMED_LAUNCH(msg_pre_kernel<false>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

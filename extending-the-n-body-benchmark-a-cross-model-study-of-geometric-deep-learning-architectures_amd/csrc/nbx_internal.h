@@ -1,5 +1,6 @@
 // Internal helpers shared by the libnbx translation units (not part of the ABI).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -32,6 +33,39 @@ int hip_error(hipError_t e, const char* where);
 #define NBX_LAUNCH_CHECK(name) NBX_HIP(hipGetLastError())
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Kernel-execution timing for the *_forward_timed entry points: when a start / stop event pair is
+// armed, the next NBX_TIMED_LAUNCH records the kernel's own begin / end on them
+// (hipExtLaunchKernel: the same interval a profiler's kernel trace reports, without the
+// dispatch overhead a hipEventRecord pair around the launch adds); the pair is consumed.
+struct ArmedEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+inline ArmedEvents& armed_events() {
+    static thread_local ArmedEvents e;
+    return e;
+}
+// after a launcher that may have returned without launching: record a zero interval instead
+inline hipError_t disarm_events(hipStream_t st) {
+    ArmedEvents& e = armed_events();
+    hipError_t r = hipSuccess;
+    if (e.start) {
+        r = hipEventRecord(e.start, st);
+        if (r == hipSuccess) r = hipEventRecord(e.stop, st);
+    }
+    e.start = e.stop = nullptr;
+    return r;
+}
+#define NBX_TIMED_LAUNCH(kernel, grid, block, shmem, stream, ...)                                           \
+    do {                                                                                                  \
+        ::nbx::ArmedEvents& _ae = ::nbx::armed_events();                                                  \
+        if (_ae.start) {                                                                                  \
+            hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, _ae.start, _ae.stop, 0, __VA_ARGS__); \
+            _ae.start = _ae.stop = nullptr;                                                               \
+        } else {                                                                                          \
+            hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                          \
+        }                                                                                                 \
+    } while (0)
 
 // e3nn / SEGNN constants (oracle/e3nn_lite.py documents their derivation)
 constexpr float kSH_C0 = 0.28209479177387814f;   // 1/sqrt(4 pi)

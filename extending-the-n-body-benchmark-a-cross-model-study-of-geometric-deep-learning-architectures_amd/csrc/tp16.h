@@ -751,8 +751,8 @@ int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
         attr_set = true;
     }
     const size_t lds = (size_t)std::max(b0 ? p0.lds_floats : 0, b1 ? p1.lds_floats : 0) * 4;
-    hipLaunchKernelGGL((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>), dim3(b0 + b1), dim3(64 * WAVES), lds,
-                       st, p0, p1, b0);
+    NBX_TIMED_LAUNCH((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>), dim3(b0 + b1), dim3(64 * WAVES), lds,
+                     st, p0, p1, b0);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

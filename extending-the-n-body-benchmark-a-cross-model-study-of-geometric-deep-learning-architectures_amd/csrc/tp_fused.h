@@ -708,8 +708,8 @@ int tp_launch(const TpProb& p, hipStream_t st) {
             return NBX_E_INVAL;
         }
     }
-    hipLaunchKernelGGL((tp_fused_kernel<NS, NV, EPI, WAVES, D, SK>), dim3(p.chunks * p.blocks_per_chunk), dim3(64 * WAVES),
-                       lds, st, p);
+    NBX_TIMED_LAUNCH((tp_fused_kernel<NS, NV, EPI, WAVES, D, SK>), dim3(p.chunks * p.blocks_per_chunk), dim3(64 * WAVES),
+                     lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }
