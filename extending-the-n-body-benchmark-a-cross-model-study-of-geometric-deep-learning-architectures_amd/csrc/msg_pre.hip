@@ -8,7 +8,10 @@ constexpr int MP_THREADS = 512;
 // one exchange buffer: [4 planes][6 parts][16 rows][MP_RS], 16 channels per row padded to 20
 // floats so the GEMM waves' stores (lane quarters qd = 0/1 hold rows 4 apart) hit different
 // bank halves, while rows stay 16-byte aligned for the edge waves' ds_read_b128
-// (X3: rows unpadded, 16 floats, so that two buffers fit beside the larger bf16x3 images)
+// (X3: rows unpadded, 16 floats, so that two buffers fit beside the larger bf16x3 images; the
+// channel quads of row r are stored XOR-swizzled by (r >> 2) & 3 instead, which keeps the GEMM
+// waves' stores -- lane quarters hold rows 4 apart -- on distinct banks and the edge waves'
+// float4 reads whole)
 template <bool X3> struct MpEx {
     static constexpr int RS = X3 ? 16 : 20, PART = 16 * RS, EX = 4 * 6 * PART;
 };
@@ -105,7 +108,10 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
 #pragma unroll
             for (int j = 0; j < 6; ++j)
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) ex[j * MP_PART + (4 * qd + jj) * MP_RS + c16] = acc[j][jj];
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int col = X3 ? (c16 & 3) | (((c16 >> 2) ^ qd) << 2) : c16;   // row (4 qd + jj) >> 2 = qd
+                    ex[j * MP_PART + (4 * qd + jj) * MP_RS + col] = acc[j][jj];
+                }
         };
         if (gemm_wave) {
             if (i < my_groups) {
@@ -189,9 +195,10 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
             const float4 geo_cur = geo_next;
             const float pm_cur = pm_next;
             load_geo(i, geo_next, pm_next);
-            const float* exb = EX + ((i - 1) & 1) * MP_EX + 4 * cq;
+            const float* exb = EX + ((i - 1) & 1) * MP_EX;
             auto xv = [&](int pl, int part, int row) {
-                return *reinterpret_cast<const float4*>(exb + (pl * 6 + part) * MP_PART + row * MP_RS);
+                const int q = X3 ? cq ^ ((row >> 2) & 3) : cq;
+                return *reinterpret_cast<const float4*>(exb + (pl * 6 + part) * MP_PART + row * MP_RS + 4 * q);
             };
             const int64_t node0 = (int64_t)(pblk + (i - 1) * P.per_chunk) * NG;
             for (int it = et >> 2; it < group_items; it += 64) {
