@@ -136,7 +136,7 @@ def bench_segnn(a, rank, world, device, P):
         fwd_ms += tot.value
     # rocprofv3 names of the four timed launch kinds at C2 (csrc/segnn.hip::forward_impl)
     x3 = os.environ.get("NBX_X3") != "0"
-    names = [f"void nbx::msg_pre_kernel<{'true' if x3 else 'false'}>(nbx::MsgPreProb)",
+    names = [("void nbx::msg_pre_kernel<true, 3>(nbx::MsgPreProb)" if x3 else "void nbx::msg_pre_kernel<false, 0>(nbx::MsgPreProb)"),
              ("void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSKX3<6, 6, 3, 3> >(nbx::TpProb)" if x3 else
               "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3> >(nbx::TpProb)"),
              "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSK<12, 12, 6, 6, 4> >(nbx::TpProb, nbx::TpProb, int)",

@@ -19,7 +19,8 @@ template <bool X3> struct MpEx {
 // X3: the node GEMM on the split-precision path (tp_fused.h StatSKX3; bf16x3 CW = 16 images,
 // v_mfma_f32_16x16x32_bf16 whose A fragment -- lane quarter qd holds k = 8 qd + j -- is exactly
 // the X chunk a lane loads)
-template <bool X3>
+// (X3 runs a static schedule over KCT = ceil(M / 32) K chunks)
+template <bool X3, int KCT = 0>
 __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const MsgPreProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
@@ -118,6 +119,58 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                 // ---- node GEMM of group i: 16 rows x 96 columns (6 parts x 16 channels)
 #pragma unroll
                 for (int j = 0; j < 6; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (X3) {
+                    // Split-precision node GEMM, static over the KCT chunks.  Chunk kc+1's B
+                    // fragments are read while the second half of chunk kc's MFMAs issues, into
+                    // registers last read by chunk kc-1's MFMAs -- at least 18 MFMAs (288 cycles)
+                    // earlier, so no pending MFMA's operands are refilled (msg_pre.hip history:
+                    // LDS returns overwriting the operands of a pending MFMA corrupted groups).
+                    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+                    const bf16x8* bimg = reinterpret_cast<const bf16x8*>(img) + lane;
+                    bf16x8 bx[2][6][3], ax[2][3];
+                    auto read_b = [&](int kc, bf16x8 (&bb)[6][3]) {
+#pragma unroll
+                        for (int j = 0; j < 6; ++j)
+#pragma unroll
+                            for (int p3 = 0; p3 < 3; ++p3) bb[j][p3] = bimg[(j * KCT + kc) * 192 + p3 * 64];
+                    };
+                    read_b(0, bx[0]);
+                    static_for<0, KCT>([&](auto kcc) {
+                        constexpr int kc = decltype(kcc)::value;
+                        // x = sc * x~ + sh (shift on the 0e plane only), split into bf16 x3
+                        const float* xc = XC + (plane ? KCT * 32 : 0) + kc * 32 + 8 * qd;
+                        const float4 sc0 = *reinterpret_cast<const float4*>(xc);
+                        const float4 sc1 = *reinterpret_cast<const float4*>(xc + 4);
+                        float4 sh0{0.f, 0.f, 0.f, 0.f}, sh1{0.f, 0.f, 0.f, 0.f};
+                        if (plane == 0) {
+                            sh0 = *reinterpret_cast<const float4*>(XC + 2 * KCT * 32 + kc * 32 + 8 * qd);
+                            sh1 = *reinterpret_cast<const float4*>(XC + 2 * KCT * 32 + kc * 32 + 8 * qd + 4);
+                        }
+                        const float4 v0{fmaf(sc0.x, abuf[kc][0].x, sh0.x), fmaf(sc0.y, abuf[kc][0].y, sh0.y),
+                                        fmaf(sc0.z, abuf[kc][0].z, sh0.z), fmaf(sc0.w, abuf[kc][0].w, sh0.w)};
+                        const float4 v1{fmaf(sc1.x, abuf[kc][1].x, sh1.x), fmaf(sc1.y, abuf[kc][1].y, sh1.y),
+                                        fmaf(sc1.z, abuf[kc][1].z, sh1.z), fmaf(sc1.w, abuf[kc][1].w, sh1.w)};
+                        tp_split3(v0, v1, ax[kc & 1][0], ax[kc & 1][1], ax[kc & 1][2]);
+                        const bf16x8 (&a)[3] = ax[kc & 1];
+                        const bf16x8 (&b)[6][3] = bx[kc & 1];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+                            for (int j = 0; j < 6; ++j)
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], b[j][TB[tt]], acc[j], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if constexpr (kc + 1 < KCT) read_b(kc + 1, bx[(kc + 1) & 1]);
+#pragma unroll
+                        for (int tt = 3; tt < 6; ++tt)
+#pragma unroll
+                            for (int j = 0; j < 6; ++j)
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], b[j][TB[tt]], acc[j], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                    // the next group's B reads are 18+ MFMAs away; the A prefetch below only
+                    // refills abuf (read by VALU, not by the MFMAs)
+                }
                 // B fragments double-buffered across the 32-deep K chunks: the reads of chunk
                 // kc + 1 are in flight while chunk kc's 48 MFMAs issue
                 float4 b[2][6][2];
@@ -132,7 +185,7 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                 if constexpr (!X3) load_b(0, b[0]);
 #pragma unroll
                 for (int kc = 0; kc < KCMAX; ++kc) {
-                    if (kc >= KC) break;
+                    if (X3 || kc >= KC) break;
                     if (!X3 && kc + 1 < KC) load_b(kc + 1, b[(kc + 1) & 1]);
                     // x = sc * x~ + sh (shift on the 0e plane only)
                     const float* xc = XC + (plane ? KC * 32 : 0) + kc * 32 + 8 * qd;
@@ -147,33 +200,7 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                                          fmaf(sc0.z, abuf[kc][0].z, sh0.z), fmaf(sc0.w, abuf[kc][0].w, sh0.w),
                                          fmaf(sc1.x, abuf[kc][1].x, sh1.x), fmaf(sc1.y, abuf[kc][1].y, sh1.y),
                                          fmaf(sc1.z, abuf[kc][1].z, sh1.z), fmaf(sc1.w, abuf[kc][1].w, sh1.w)};
-                    if constexpr (X3) {
-                        bf16x8 a[3];
-                        tp_split3(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]}, a[0], a[1],
-                                  a[2]);
-                        const bf16x8* bp = reinterpret_cast<const bf16x8*>(img) + kc * 192 + lane;
-                        bf16x8 bx[6][3];
-#pragma unroll
-                        for (int j = 0; j < 6; ++j)
-#pragma unroll
-                            for (int p3 = 0; p3 < 3; ++p3) bx[j][p3] = bp[j * KC * 192 + p3 * 64];
-                        // six cross terms, smallest first, round-robin over the 6 accumulators
-                        constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
-                        // The MFMAs run as one fenced block in this round-robin order, and the next
-                        // chunk's operand loads start a pad after it.  Measured: when the scheduler
-                        // interleaved the next chunk's ds_reads with back-to-back dependent MFMAs, LDS
-                        // returns overwrote the A/B registers of an MFMA still waiting on its
-                        // accumulator, corrupting a few node groups per launch.
-                        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                        for (int tt = 0; tt < 6; ++tt)
-#pragma unroll
-                            for (int j = 0; j < 6; ++j)
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], bx[j][TB[tt]], acc[j], 0, 0, 0);
-                        __builtin_amdgcn_sched_barrier(0);
-                        asm volatile("s_nop 7\n\ts_nop 7");
-                        __builtin_amdgcn_sched_barrier(0);
-                    } else {
+                    {
                         const float4 (&bc)[6][2] = b[kc & 1];
 #pragma unroll
                         for (int s = 0; s < 8; ++s)
@@ -289,12 +316,20 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
     if (!attr_set) {
         NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024));
-        NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
+        for (const void* k : {(const void*)msg_pre_kernel<true, 1>, (const void*)msg_pre_kernel<true, 2>,
+                              (const void*)msg_pre_kernel<true, 3>, (const void*)msg_pre_kernel<true, 4>})
+            NBX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    if (p.x3)
-        NBX_TIMED_LAUNCH(msg_pre_kernel<true>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    const int kct = (p.M + 31) / 32;
+    if (p.x3 && kct == 3)
+        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 3>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    else if (p.x3 && kct == 1)
+        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 1>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    else if (p.x3 && kct == 2)
+        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 2>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    else if (p.x3)
+        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 4>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     else
         NBX_TIMED_LAUNCH(msg_pre_kernel<false>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
