@@ -47,7 +47,7 @@ constexpr int EW_X = 32, EW_Y = 8, ROWS_PER_BLOCK = 16;
 // featurise + embedding in one launch: a block of FE_NODES nodes first runs O3Transform /
 // catch_isolated_nodes per node (thread = node; NA and EG to HBM, X0 kept in LDS), then the
 // embedding TP per (node, channel).
-constexpr int FE_NODES = 32;
+constexpr int FE_NODES = 8;   // nodes per block: V / 8 blocks fill the chip at the C2 size
 __global__ void featurize_embed_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
                                        const float* __restrict__ mass, int64_t V, int N, int G,
                                        const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
@@ -69,8 +69,8 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
             const int64_t s2 = b * N + (q < d ? q : q + 1);
             const float rx = pos[3 * s2] - px, ry = pos[3 * s2 + 1] - py, rz = pos[3 * s2 + 2] - pz;
             const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
-            const float den = fmaxf(dist, 1e-12f);
-            const float hx = rx / den, hy = ry / den, hz = rz / den;
+            const float inv = 1.0f / fmaxf(dist, 1e-12f);
+            const float hx = rx * inv, hy = ry * inv, hz = rz * inv;
             float* eg = EG + (node * G + q) * 8;
             eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s2] * m;
             sxh += kSH_C1 * hx; syh += kSH_C1 * hy; szh += kSH_C1 * hz;
@@ -92,11 +92,15 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
     }
     __syncthreads();
     const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
-    for (int idx = t; idx < nn * M; idx += blockDim.x) {
-        const int ln = idx / M, w = idx - ln * M;
+    // thread = (channel w, node lane): the embedding coefficients of w are loaded once
+    const int lanes = (int)blockDim.x >= M ? (int)blockDim.x / M : 1;
+    const int l0 = lanes > 1 ? t / M : 0;
+    if (l0 >= lanes) return;
+    for (int w = lanes > 1 ? t % M : t; w < M; w += lanes > 1 ? M : (int)blockDim.x) {
+    const float a0 = emb[w], a1 = emb[M + w], b0 = emb[2 * M + w], b1 = emb[3 * M + w];
+    const float c = emb[4 * M + w], dd = emb[5 * M + w], bias = emb_b[w];
+    for (int ln = l0; ln < nn; ln += lanes) {
         const int64_t n = n0 + ln;
-        const float a0 = emb[w], a1 = emb[M + w], b0 = emb[2 * M + w], b1 = emb[3 * M + w];
-        const float c = emb[4 * M + w], dd = emb[5 * M + w], bias = emb_b[w];
         const float* x0 = sx0[ln];
         const float* na = sna[ln];
         const float u0n = x0[0] * na[1] + x0[1] * na[2] + x0[2] * na[3];
@@ -110,6 +114,7 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
             xd += xv * na[1 + k];
         }
         if (XD) XD[n * M + w] = xd;
+    }
     }
 }
 
@@ -610,18 +615,25 @@ int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img
 
 
 int tp16_debug_dump(const unsigned long long* dbg, int n, hipStream_t st, const char* label) {
-    std::vector<unsigned long long> h((size_t)n * 4);
+    std::vector<unsigned long long> h((size_t)n * 6);
     NBX_HIP(hipStreamSynchronize(st));
     NBX_HIP(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
-    double s01 = 0, s12 = 0, s23 = 0;
+    double s01 = 0, s12 = 0, s23 = 0, sw = 0;
+    unsigned long long w0 = ~0ull, w1 = 0;
     int cnt = 0;
     for (int i = 0; i < n; ++i) {
-        const unsigned long long* d = &h[(size_t)i * 4];
+        const unsigned long long* d = &h[(size_t)i * 6];
         if (!d[1]) continue;
         s01 += d[1] - d[0]; s12 += d[2]; s23 += d[3]; ++cnt;
+        w0 = std::min(w0, d[4]);
+        w1 = std::max(w1, d[5]);
+        sw += (double)(d[5] - d[4]);
     }
-    fprintf(stderr, "tp_debug %s waves=%d/%d stage=%.0f loop=%.0f epi=%.0f (avg clocks per wave, loop/epi summed over its tiles)\n", label, cnt, n,
-            s01 / std::max(cnt, 1), s12 / std::max(cnt, 1), s23 / std::max(cnt, 1));
+    fprintf(stderr,
+            "tp_debug %s waves=%d/%d stage=%.0f loop=%.0f epi=%.0f (avg clocks per wave, loop/epi summed over its "
+            "tiles) waves_span=%.2fus wave_avg=%.2fus\n",
+            label, cnt, n, s01 / std::max(cnt, 1), s12 / std::max(cnt, 1), s23 / std::max(cnt, 1), (w1 - w0) / 100.0,
+            sw / std::max(cnt, 1) / 100.0);
     return NBX_OK;
 }
 
@@ -752,7 +764,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // update_layer_1 reads its [x | BN(agg)] input straight from X / AGG and the two dot buffers
     // (no materialised U1) when the static segmented schedule applies (mul = 96 or 32)
     const bool seg_upd = static_enabled() && (M == 96 || M == 32);
-    hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(256), 0, st, pos, vel,
+    // block: whole multiples of the channel count (192 threads at mul = 96), >= FE_NODES
+    const unsigned fe_threads = (unsigned)std::max(64, std::min(1024, M * std::max(1, 256 / M)));
+    hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st, pos, vel,
                        mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
                        seg_upd ? ws.XD : nullptr);
     NBX_LAUNCH_CHECK("embed");

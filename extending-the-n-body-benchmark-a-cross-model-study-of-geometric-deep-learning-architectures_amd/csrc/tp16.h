@@ -93,6 +93,7 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
     // PF - 1 chunks are in flight behind the current one.  The first PF - 1 loads are issued
     // before the weight staging so both latencies overlap.
     const unsigned long long c_start = P.dbg ? clock64() : 0ull;
+    const unsigned long long w_start = P.dbg ? wall_clock64() : 0ull;   // 100 MHz, chip-wide
     unsigned long long c_loop = 0ull, c_epi = 0ull, c_mark = 0ull;   // per-phase sums over tiles
     int rt = wid;
     const int nck = c_hi - c_lo;
@@ -643,9 +644,9 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
         }
     }
     if (P.dbg && lane == 0) {
-        unsigned long long* d = P.dbg + ((size_t)bidx * WAVES + wave) * 4;
-        // [start, staged, sum over tiles of the K loop, sum over tiles of the epilogue]
-        d[0] = c_start; d[1] = c_staged; d[2] = c_loop; d[3] = c_epi;
+        unsigned long long* d = P.dbg + ((size_t)bidx * WAVES + wave) * 6;
+        // [start, staged, sum over tiles of the K loop, sum over tiles of the epilogue, wall start]
+        d[0] = c_start; d[1] = c_staged; d[2] = c_loop; d[3] = c_epi; d[4] = w_start;
     }
     if constexpr (EPI == TP_MSG || EPI == TP_RESID) {
         // reduce the 8 waves of the block in LDS (the weights are no longer needed), one
@@ -672,6 +673,7 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
             if (ch16 < nchunks16) P.partial[((size_t)ch16 * P.blocks_per_chunk + blk) * 48 + st * 16 + c] = acc;
         }
     }
+    if (P.dbg && lane == 0) P.dbg[((size_t)bidx * WAVES + wave) * 6 + 5] = wall_clock64();   // wall end
 }
 
 template <int CG>
