@@ -249,25 +249,42 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                 const float pm = first ? pm_cur : P.EG[e * 8 + 4];
                 const float hk[3] = {g4.x, g4.y, g4.z};
                 const float dist = g4.w;
-                float4 sa = xv(0, 0, ld) + xv(0, 3, sl) + ea0 * dist + ea1 * pm + ba;
-                float4 sg = xv(0, 1, ld) + xv(0, 4, sl) + eg0 * dist + eg1 * pm + bg;
-                const float4 tt = xv(0, 2, ld) + xv(0, 5, sl) + et0 * dist + et1 * pm;
-                float4 v[3];
+                // scalar per channel (no packed fp32: it runs beside the GEMM wave's MFMAs, where
+                // v_pk_* ops cost extra issue cycles)
+                float4 xd[4][6], xs[4][6];   // [plane][part] of the destination / source rows
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    sa += hk[k] * (xv(1 + k, 0, ld) + xv(1 + k, 3, sl));
-                    sg += hk[k] * (xv(1 + k, 1, ld) + xv(1 + k, 4, sl));
-                    v[k] = hk[k] * tt + xv(1 + k, 2, ld) + xv(1 + k, 5, sl);
+                for (int pl = 0; pl < 4; ++pl)
+#pragma unroll
+                    for (int pt = 0; pt < 3; ++pt) {
+                        xd[pl][pt] = xv(pl, pt, ld);
+                        xs[pl][pt] = xv(pl, 3 + pt, sl);
+                    }
+                float o_ms[4], o_v0[4], o_v1[4], o_v2[4], o_dot[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    auto X = [&](const float4& f) { return f4get(f, c); };
+                    float sa = fmaf(X(ea1), pm, fmaf(X(ea0), dist, X(xd[0][0]) + X(xs[0][0]))) + X(ba);
+                    float sg = fmaf(X(eg1), pm, fmaf(X(eg0), dist, X(xd[0][1]) + X(xs[0][1]))) + X(bg);
+                    const float tt = fmaf(X(et1), pm, fmaf(X(et0), dist, X(xd[0][2]) + X(xs[0][2])));
+                    float v[3];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        sa = fmaf(hk[k], X(xd[1 + k][0]) + X(xs[1 + k][0]), sa);
+                        sg = fmaf(hk[k], X(xd[1 + k][1]) + X(xs[1 + k][1]), sg);
+                        v[k] = fmaf(hk[k], tt, X(xd[1 + k][2])) + X(xs[1 + k][2]);
+                    }
+                    const float gg = kC_SIGMOID * tp_sigmoid(sg);
+                    o_ms[c] = kC_SILU * tp_silu(sa);
+                    o_v0[c] = gg * v[0];
+                    o_v1[c] = gg * v[1];
+                    o_v2[c] = gg * v[2];
+                    o_dot[c] = fmaf(o_v2[c], hk[2], fmaf(o_v1[c], hk[1], o_v0[c] * hk[0]));
                 }
-                float4 gg, ms;
-                gg.x = kC_SIGMOID * tp_sigmoid(sg.x); gg.y = kC_SIGMOID * tp_sigmoid(sg.y);
-                gg.z = kC_SIGMOID * tp_sigmoid(sg.z); gg.w = kC_SIGMOID * tp_sigmoid(sg.w);
-                ms.x = kC_SILU * tp_silu(sa.x); ms.y = kC_SILU * tp_silu(sa.y);
-                ms.z = kC_SILU * tp_silu(sa.z); ms.w = kC_SILU * tp_silu(sa.w);
-                const float4 mv0 = gg * v[0], mv1 = gg * v[1], mv2 = gg * v[2];
-                *m1v0 = mv0; *m1v1 = mv1; *m1v2 = mv2;
-                m1s[0] = ms;
-                m1s[M / 4] = mv0 * hk[0] + mv1 * hk[1] + mv2 * hk[2];
+                *m1v0 = float4{o_v0[0], o_v0[1], o_v0[2], o_v0[3]};
+                *m1v1 = float4{o_v1[0], o_v1[1], o_v1[2], o_v1[3]};
+                *m1v2 = float4{o_v2[0], o_v2[1], o_v2[2], o_v2[3]};
+                m1s[0] = float4{o_ms[0], o_ms[1], o_ms[2], o_ms[3]};
+                m1s[M / 4] = float4{o_dot[0], o_dot[1], o_dot[2], o_dot[3]};
             }
             tick(c_edge);
         }
