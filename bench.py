@@ -136,14 +136,19 @@ def bench_segnn(a, rank, world, device, P):
         fwd_ms += tot.value
     # rocprofv3 names of the four timed launch kinds at C2 (csrc/segnn.hip::forward_impl)
     x3 = os.environ.get("NBX_X3") != "0"
-    names = [("void nbx::msg_pre_kernel<true, 3>(nbx::MsgPreProb)" if x3 else "void nbx::msg_pre_kernel<false, 0>(nbx::MsgPreProb)"),
-             ("void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSKX3<6, 6, 3, 3> >(nbx::TpProb)" if x3 else
-              "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3> >(nbx::TpProb)"),
-             "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSK<12, 12, 6, 6, 4> >(nbx::TpProb, nbx::TpProb, int)",
-             "void nbx::tp16_kernel<2, 1, 3, 2, 8, 3, 2, false, nbx::StatSK<6, 3, 0, 3> >(nbx::TpProb, nbx::TpProb, int)"]
+    names = [("void nbx::msg_pre_kernel<true, 3>(nbx::MsgPreProb)" if x3 else
+              "void nbx::msg_pre_kernel<false, 0>(nbx::MsgPreProb)"),
+             ("void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSKX3<6, 6, 3, 3, 0> >(nbx::TpProb)" if x3 else
+              "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3, 0> >(nbx::TpProb)"),
+             ("void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSKX3<12, 12, 6, 6, 4> >(nbx::TpProb, "
+              "nbx::TpProb, int)" if x3 else
+              "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSK<12, 12, 6, 6, 4> >(nbx::TpProb, "
+              "nbx::TpProb, int)"),
+             "void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, nbx::StatSK<6, 3, 0, 3, 0> >(nbx::TpProb, nbx::TpProb, int)"]
     roles = ["message_layer_1: node GEMM + edge combination + gate (flops: the node GEMM)",
              "message_layer_2 + gate + aggregation + BN sums",
-             "update_layer_1 + gate (pre_pool1 uses CG=2)", "update_layer_2 + residual + BN sums"]
+             "update_layer_1 + gate (the kind's average includes pre_pool1, once per forward)",
+             "update_layer_2 + residual + BN sums"]
     per_kind = {}
     for k in range(4):
         if n_k[k]:

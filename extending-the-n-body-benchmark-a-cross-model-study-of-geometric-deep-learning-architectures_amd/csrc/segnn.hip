@@ -900,7 +900,20 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.xcoef = xprev;
             if (seg_upd) { p.out_dot = ws.XD; }
             p.chunks = (M + 15) / 16;
-            if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+            // update_layer_2: one 16-channel chunk per wave, full K (CG 1, KS 1; measured against CG 2 / KS 2,
+            // CG 1 / KS 2, CG 2 / KS 1, CG 1 / KS 4: 15.1 vs 17.8 / 16.3 / 19.5 / 20.9 us). NBX_UPD2_VARIANT=CG*10+KS
+            static const int upd2_var = getenv("NBX_UPD2_VARIANT") ? atoi(getenv("NBX_UPD2_VARIANT")) : 11;
+            if (upd2_var == 11) {
+                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+            } else if (upd2_var == 12) {
+                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+            } else if (upd2_var == 21) {
+                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+            } else if (upd2_var == 14) {
+                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 4, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+            } else {
+                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+            }
             wpc_feat = p.waves_per_chunk;
         }
         hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
@@ -919,7 +932,15 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.Av = ws.U1V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
-        if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 2, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
+        // pre_pool1: CG 1 / KS 1 (measured against CG 2: -0.8 % step time). NBX_PP1_VARIANT=CG*10+KS (tuning)
+        static const int pp1_var = getenv("NBX_PP1_VARIANT") ? atoi(getenv("NBX_PP1_VARIANT")) : 11;
+        if (pp1_var == 11) {
+            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
+        } else if (pp1_var == 12) {
+            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 2, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
+        } else {
+            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 2, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
+        }
     }
     RolloutUpdate none{};
     hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,
