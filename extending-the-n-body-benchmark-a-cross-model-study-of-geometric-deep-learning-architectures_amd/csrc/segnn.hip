@@ -55,29 +55,60 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
                                        float* __restrict__ XD) {
     __shared__ float sx0[FE_NODES][8];
     __shared__ float sna[FE_NODES][4];
+    __shared__ float shs[FE_NODES][32][3];   // per (node, edge slot) kSH_C1 * rhat
     const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
     const int t = threadIdx.x;
-    if (t < FE_NODES && n0 + t < V) {
-        const int64_t node = n0 + t;
+    // edge geometry: one thread per (node, slot) pair (G <= 32; larger systems: one thread per node)
+    const bool par = G <= 32;
+    for (int pq = t; par && pq < FE_NODES * G; pq += blockDim.x) {
+        const int ln = pq / G, q = pq - ln * G;
+        const int64_t node = n0 + ln;
+        if (node >= V) continue;
+        float* eg = EG + (node * G + q) * 8;
+        if (q >= N - 1) {
+            eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
+            shs[ln][q][0] = shs[ln][q][1] = shs[ln][q][2] = 0.f;
+            continue;
+        }
         const int64_t b = node / N;
         const int d = (int)(node - b * N);
+        const int64_t s2 = b * N + (q < d ? q : q + 1);
+        const float rx = pos[3 * s2] - pos[3 * node], ry = pos[3 * s2 + 1] - pos[3 * node + 1];
+        const float rz = pos[3 * s2 + 2] - pos[3 * node + 2];
+        const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+        const float inv = 1.0f / fmaxf(dist, 1e-12f);
+        const float hx = rx * inv, hy = ry * inv, hz = rz * inv;
+        eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s2] * mass[node];
+        shs[ln][q][0] = kSH_C1 * hx; shs[ln][q][1] = kSH_C1 * hy; shs[ln][q][2] = kSH_C1 * hz;
+    }
+    __syncthreads();
+    if (t < FE_NODES && n0 + t < V) {
+        const int64_t node = n0 + t;
         const float px = pos[3 * node], py = pos[3 * node + 1], pz = pos[3 * node + 2];
         const float vx = vel[3 * node], vy = vel[3 * node + 1], vz = vel[3 * node + 2];
-        const float m = mass[node];
         float sxh = 0.f, syh = 0.f, szh = 0.f;
-        for (int q = 0; q < N - 1; ++q) {
-            const int64_t s2 = b * N + (q < d ? q : q + 1);
-            const float rx = pos[3 * s2] - px, ry = pos[3 * s2 + 1] - py, rz = pos[3 * s2 + 2] - pz;
-            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
-            const float inv = 1.0f / fmaxf(dist, 1e-12f);
-            const float hx = rx * inv, hy = ry * inv, hz = rz * inv;
-            float* eg = EG + (node * G + q) * 8;
-            eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s2] * m;
-            sxh += kSH_C1 * hx; syh += kSH_C1 * hy; szh += kSH_C1 * hz;
-        }
-        for (int q = N - 1; q < G; ++q) {
-            float* eg = EG + (node * G + q) * 8;
-            eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
+        if (par) {
+            for (int q = 0; q < N - 1; ++q) {
+                sxh += shs[t][q][0]; syh += shs[t][q][1]; szh += shs[t][q][2];
+            }
+        } else {
+            const int64_t b = node / N;
+            const int d = (int)(node - b * N);
+            const float m = mass[node];
+            for (int q = 0; q < N - 1; ++q) {
+                const int64_t s2 = b * N + (q < d ? q : q + 1);
+                const float rx = pos[3 * s2] - px, ry = pos[3 * s2 + 1] - py, rz = pos[3 * s2 + 2] - pz;
+                const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+                const float inv = 1.0f / fmaxf(dist, 1e-12f);
+                const float hx = rx * inv, hy = ry * inv, hz = rz * inv;
+                float* eg = EG + (node * G + q) * 8;
+                eg[0] = hx; eg[1] = hy; eg[2] = hz; eg[3] = dist; eg[4] = mass[s2] * m;
+                sxh += kSH_C1 * hx; syh += kSH_C1 * hy; szh += kSH_C1 * hz;
+            }
+            for (int q = N - 1; q < G; ++q) {
+                float* eg = EG + (node * G + q) * 8;
+                eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
+            }
         }
         const float cnt = (float)(N - 1 > 0 ? N - 1 : 1);
         const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
