@@ -552,6 +552,8 @@ using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
 using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
 using SK_GATE = nbx::StatSK<6, 6, 3, 3>;     // pre_pool1 (and message_layer_2's shape)
 using SK_GATE_32 = nbx::StatSK<2, 2, 1, 1>;
+using SK_PP1_SEG = nbx::StatSK<6, 6, 3, 3, 2>;   // pre_pool1 reading [x_s | x_v.na] + x_v from X / XD
+using SK_PP1_32_SEG = nbx::StatSK<2, 2, 1, 1, 2>;
 using SK_MSG2_X3 = nbx::StatSKX3<6, 6, 3, 3>;
 using SK_MSG2_32_X3 = nbx::StatSKX3<2, 2, 1, 1>;
 
@@ -953,7 +955,24 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     }
 
     // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)
-    // pre_pool1 inputs with the last layer's pending feature BatchNorm applied
+    // pre_pool1 inputs with the last layer's pending feature BatchNorm applied: read segment by
+    // segment from X and XD (x_v . na) with the scale / shift applied as the A chunks are consumed
+    // (static schedules at mul 96 / 32), else materialised by pp_pre_kernel
+    if (seg_upd) {
+        nbx::TpProb p = tp_base((int)V, d);
+        p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M; p.Kv = M;
+        p.lda_s = 2 * M; p.lda_v = M;
+        p.seg_s[0] = ws.X; p.seg_s[1] = ws.XD; p.seg_v[0] = ws.X + V * M; p.seg_vplane = V * M;
+        p.xcoef = w->num_layers > 0 ? ws.coef_feat : nullptr;
+        p.B = w->pp1_img;
+        p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
+        p.chunks = (M + 15) / 16;
+        if (M == 96) {
+            if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG>(p, st, tm)) return rc;
+        } else {
+            if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG>(p, st, tm)) return rc;
+        }
+    } else {
     hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA,
                        w->num_layers > 0 ? ws.coef_feat : nullptr, V, M, ws.U1S, ws.U1V);
     {
@@ -972,6 +991,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         } else {
             if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 2, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
         }
+    }
     }
     RolloutUpdate none{};
     hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,

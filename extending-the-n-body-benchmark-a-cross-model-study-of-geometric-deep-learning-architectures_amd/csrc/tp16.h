@@ -110,9 +110,9 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
         constexpr int plane = sc ? 0 : v / (SK::KV > 0 ? SK::KV : 1);
         constexpr int kc = sc ? item : v - plane * SK::KV;
         const int row = rt_ * 16 + c16;
-        if constexpr (SK::SEG == 4) {
-            // segment q of width M = (K0 / 4) chunks (scalar) or (KV / 2) chunks (vector)
-            constexpr int cps = sc ? SK::K0 / 4 : SK::KV / 2;
+        if constexpr (SK::SEG > 0) {
+            // segment q of width M = (K0 / SEG) chunks (scalar) or (KV / (SEG / 2)) chunks (vector)
+            constexpr int cps = sc ? SK::K0 / SK::SEG : SK::KV / (SK::SEG / 2);
             constexpr int q = kc / cps, kk = (kc - q * cps) * 32;
             const int k = kk + 8 * qd;
             const bool ok = row < P.rows;
@@ -164,20 +164,20 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
     }
     // segmented update input: per-(segment, k) scale / shift table, after the images
     float* segtab = lds + CG * P.img_floats;
-    if constexpr (SK::SEG == 4) {
+    if constexpr (SK::SEG > 0) {
         const int M = P.M;
         for (int i = t; i < 10 * M; i += THREADS) {
             const int part = i / M, k = i - part * M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
             float v;
             switch (part) {
                 case 0: v = P.xcoef ? P.xcoef[k] : 1.f; break;
-                case 1: v = P.mcoef[k]; break;
+                case 1: v = SK::SEG == 4 ? P.mcoef[k] : 0.f; break;
                 case 2: v = P.xcoef ? P.xcoef[M + k] : 1.f; break;
-                case 3: v = P.mcoef[M + k]; break;
+                case 3: v = SK::SEG == 4 ? P.mcoef[M + k] : 0.f; break;
                 case 4: v = P.xcoef ? P.xcoef[2 * M + k] : 0.f; break;
-                case 5: v = P.deg * P.mcoef[2 * M + k]; break;
+                case 5: v = SK::SEG == 4 ? P.deg * P.mcoef[2 * M + k] : 0.f; break;
                 case 8: v = P.xcoef ? P.xcoef[M + k] : 1.f; break;
-                case 9: v = P.mcoef[M + k]; break;
+                case 9: v = SK::SEG == 4 ? P.mcoef[M + k] : 0.f; break;
                 default: v = 0.f;
             }
             segtab[i] = v;
@@ -269,16 +269,20 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                 constexpr bool sc = item < SK::K0;
                 av[0] = cb[0].x; av[1] = cb[0].y; av[2] = cb[0].z; av[3] = cb[0].w;
                 av[4] = cb[1].x; av[5] = cb[1].y; av[6] = cb[1].z; av[7] = cb[1].w;
-                if constexpr (SK::SEG == 4) {
+                if constexpr (SK::SEG > 0) {
+                    // table parts (segtab): scalar segment q -> part q (SEG 4) / 2 q (SEG 2: x_s, x_v.na),
+                    // shifts for the 0e segments x_s (and a_s), vector segment q -> part 8 + q
                     constexpr int kc = sc ? item : (item - SK::K0) % SK::KV;
-                    constexpr int cps = sc ? SK::K0 / 4 : SK::KV / 2;
+                    constexpr int cps = sc ? SK::K0 / SK::SEG : SK::KV / (SK::SEG / 2);
                     constexpr int q = kc / cps, kk = (kc - q * cps) * 32;
+                    constexpr int part = sc ? (SK::SEG == 4 ? q : 2 * q) : 8 + q;
+                    constexpr bool shifted = sc && (SK::SEG == 4 ? q < 2 : q == 0);
                     const int M = P.M;
-                    const float* tsc = segtab + (sc ? q * M : 8 * M + q * M) + kk + 8 * qd;
+                    const float* tsc = segtab + part * M + kk + 8 * qd;
                     const float4 s0 = *reinterpret_cast<const float4*>(tsc);
                     const float4 s1 = *reinterpret_cast<const float4*>(tsc + 4);
                     const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-                    if constexpr (sc && q < 2) {
+                    if constexpr (shifted) {
                         const float* tsh = segtab + 4 * M + q * M + kk + 8 * qd;
                         const float4 h0 = *reinterpret_cast<const float4*>(tsh);
                         const float4 h1 = *reinterpret_cast<const float4*>(tsh + 4);
@@ -729,6 +733,11 @@ int tp16_check_static(const TpProb& p) {
                         (p.NS < 3 || kc(p.K[2]) == SK::K2) && (p.NV ? kc(p.Kv) : 0) == SK::KV;
         if (!ok) {
             set_error("tp16: static chunk schedule does not match the problem's K");
+            return NBX_E_INVAL;
+        }
+        if (SK::SEG == 2 && (p.M * 2 != SK::K0 * 32 || p.M != SK::KV * 32 || !p.seg_s[0] || !p.seg_s[1] ||
+                             !p.seg_v[0])) {
+            set_error("tp16: segmented pre_pool input needs mul %% 32 == 0 and the segment pointers");
             return NBX_E_INVAL;
         }
         if (SK::SEG == 4 && (p.M * 4 != SK::K0 * 32 || p.M * 2 != SK::KV * 32 || !p.seg_s[0] || !p.seg_s[1] ||
