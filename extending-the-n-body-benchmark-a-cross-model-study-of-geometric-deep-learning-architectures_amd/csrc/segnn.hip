@@ -48,22 +48,24 @@ constexpr int EW_X = 32, EW_Y = 8, ROWS_PER_BLOCK = 16;
 // catch_isolated_nodes per node (thread = node; NA and EG to HBM, X0 kept in LDS), then the
 // embedding TP per (node, channel).
 constexpr int FE_NODES = 8;   // nodes per block: V / 8 blocks fill the chip at the C2 size
-__global__ void featurize_embed_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
-                                       const float* __restrict__ mass, int64_t V, int N, int G,
-                                       const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
-                                       float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
-                                       float* __restrict__ XD) {
-    __shared__ float sx0[FE_NODES][8];
-    __shared__ float sna[FE_NODES][4];
-    __shared__ float shs[FE_NODES][32][3];   // per (node, edge slot) kSH_C1 * rhat
-    const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
+// Featurise + embed the nodes [n0, n0 + nn) of whole systems.  lpos / lvel hold the positions
+// and velocities from node pbase on: the global arrays (pbase 0) in featurize_embed_kernel, the
+// block's LDS copy of the updated state in the rollout's fused pre_pool2 (rollout_pp2_kernel).
+template <int NB>
+__device__ __forceinline__ void featurize_nodes(const float* lpos, const float* lvel, int64_t pbase,
+                                                const float* __restrict__ mass, int64_t V, int N, int G,
+                                                const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
+                                                float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
+                                                float* __restrict__ XD, int64_t n0, int nn) {
+    __shared__ float sx0[NB][8];
+    __shared__ float sna[NB][4];
+    __shared__ float shs[NB][32][3];   // per (node, edge slot) kSH_C1 * rhat
     const int t = threadIdx.x;
     // edge geometry: one thread per (node, slot) pair (G <= 32; larger systems: one thread per node)
     const bool par = G <= 32;
-    for (int pq = t; par && pq < FE_NODES * G; pq += blockDim.x) {
+    for (int pq = t; par && pq < nn * G; pq += blockDim.x) {
         const int ln = pq / G, q = pq - ln * G;
         const int64_t node = n0 + ln;
-        if (node >= V) continue;
         float* eg = EG + (node * G + q) * 8;
         if (q >= N - 1) {
             eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
@@ -73,8 +75,10 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
         const int64_t b = node / N;
         const int d = (int)(node - b * N);
         const int64_t s2 = b * N + (q < d ? q : q + 1);
-        const float rx = pos[3 * s2] - pos[3 * node], ry = pos[3 * s2 + 1] - pos[3 * node + 1];
-        const float rz = pos[3 * s2 + 2] - pos[3 * node + 2];
+        const float* ps = lpos + 3 * (s2 - pbase);
+        const float* pd = lpos + 3 * (node - pbase);
+        const float rx = ps[0] - pd[0], ry = ps[1] - pd[1];
+        const float rz = ps[2] - pd[2];
         const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
         const float inv = 1.0f / fmaxf(dist, 1e-12f);
         const float hx = rx * inv, hy = ry * inv, hz = rz * inv;
@@ -82,10 +86,12 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
         shs[ln][q][0] = kSH_C1 * hx; shs[ln][q][1] = kSH_C1 * hy; shs[ln][q][2] = kSH_C1 * hz;
     }
     __syncthreads();
-    if (t < FE_NODES && n0 + t < V) {
+    if (t < nn) {
         const int64_t node = n0 + t;
-        const float px = pos[3 * node], py = pos[3 * node + 1], pz = pos[3 * node + 2];
-        const float vx = vel[3 * node], vy = vel[3 * node + 1], vz = vel[3 * node + 2];
+        const float* pp = lpos + 3 * (node - pbase);
+        const float* pv = lvel + 3 * (node - pbase);
+        const float px = pp[0], py = pp[1], pz = pp[2];
+        const float vx = pv[0], vy = pv[1], vz = pv[2];
         float sxh = 0.f, syh = 0.f, szh = 0.f;
         if (par) {
             for (int q = 0; q < N - 1; ++q) {
@@ -97,7 +103,8 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
             const float m = mass[node];
             for (int q = 0; q < N - 1; ++q) {
                 const int64_t s2 = b * N + (q < d ? q : q + 1);
-                const float rx = pos[3 * s2] - px, ry = pos[3 * s2 + 1] - py, rz = pos[3 * s2 + 2] - pz;
+                const float* ps = lpos + 3 * (s2 - pbase);
+                const float rx = ps[0] - px, ry = ps[1] - py, rz = ps[2] - pz;
                 const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
                 const float inv = 1.0f / fmaxf(dist, 1e-12f);
                 const float hx = rx * inv, hy = ry * inv, hz = rz * inv;
@@ -122,7 +129,6 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
         sx0[t][3] = vx; sx0[t][4] = vy; sx0[t][5] = vz; sx0[t][6] = vn; sx0[t][7] = 0.f;
     }
     __syncthreads();
-    const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
     // thread = (channel w, node lane): the embedding coefficients of w are loaded once
     const int lanes = (int)blockDim.x >= M ? (int)blockDim.x / M : 1;
     const int l0 = lanes > 1 ? t / M : 0;
@@ -147,6 +153,16 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
         if (XD) XD[n * M + w] = xd;
     }
     }
+}
+
+__global__ void featurize_embed_kernel(const float* __restrict__ pos, const float* __restrict__ vel,
+                                       const float* __restrict__ mass, int64_t V, int N, int G,
+                                       const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
+                                       float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
+                                       float* __restrict__ XD) {
+    const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
+    const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
+    featurize_nodes<FE_NODES>(pos, vel, 0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn);
 }
 
 // ---------------------------------------------------------------- message
@@ -342,14 +358,15 @@ struct RolloutUpdate {
     float* traj_vel;
     int64_t frame, num_frames;
     int N;
+    int featurize_next;   // rollout_pp2_kernel: also featurise + embed the next frame's input
 };
 
-__global__ void pp2_kernel(const float* __restrict__ H2S, const float* __restrict__ H2V,
-                           const float* __restrict__ NA, const float* __restrict__ W, int64_t V, int M,
-                           float* __restrict__ out, RolloutUpdate U) {
-    const int64_t n = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (n >= V) return;
+// pre_pool2 of node n by one wave (lanes over M); lanes 0-2 write out[n] and, in a rollout, the
+// updated state (also to sp / sv when non-null)
+__device__ __forceinline__ void pp2_node(const float* __restrict__ H2S, const float* __restrict__ H2V,
+                                         const float* __restrict__ NA, const float* __restrict__ W, int64_t V, int M,
+                                         float* __restrict__ out, const RolloutUpdate& U, int64_t n, int lane,
+                                         float* sp, float* sv) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // t0, t1, v0xyz, v1xyz
     for (int u = lane; u < M; u += 64) {
         const float hs = H2S[n * 2 * M + u];
@@ -380,8 +397,36 @@ __global__ void pp2_kernel(const float* __restrict__ H2S, const float* __restric
             const int64_t o = ((b * U.num_frames + U.frame) * U.N + d) * 3 + k;
             U.traj_pos[o] = p;
             U.traj_vel[o] = nv;
+            if (sp) { sp[k] = p; sv[k] = nv; }
         }
     }
+}
+
+__global__ void pp2_kernel(const float* __restrict__ H2S, const float* __restrict__ H2V,
+                           const float* __restrict__ NA, const float* __restrict__ W, int64_t V, int M,
+                           float* __restrict__ out, RolloutUpdate U) {
+    const int64_t n = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (n >= V) return;
+    pp2_node(H2S, H2V, NA, W, V, M, out, U, n, threadIdx.x & 63, nullptr, nullptr);
+}
+
+// Rollout frames before the last: pre_pool2 + the state update of this frame, then the next
+// frame's featurisation + embedding (featurize_embed_kernel's work) from the updated state, in
+// one launch.  A block owns nb nodes = whole systems (one wave per node), so every position a
+// system's edges need is in the block's LDS after the barrier.
+constexpr int RPP2_MAX = 16;   // nodes (waves) per block
+__global__ __launch_bounds__(64 * RPP2_MAX) void rollout_pp2_kernel(
+    const float* __restrict__ H2S, const float* __restrict__ H2V, float* __restrict__ NA, const float* __restrict__ W,
+    int64_t V, int M, float* __restrict__ out, RolloutUpdate U, int nb, const float* __restrict__ mass, int N, int G,
+    const float* __restrict__ emb, const float* __restrict__ emb_b, float* __restrict__ EG, float* __restrict__ X,
+    float* __restrict__ XD) {
+    __shared__ float spos[RPP2_MAX][3], svel[RPP2_MAX][3];
+    const int64_t n0 = blockIdx.x * (int64_t)nb;
+    const int wv = threadIdx.x >> 6;
+    const int nn = (int)(V - n0 < nb ? V - n0 : nb);
+    if (wv < nn) pp2_node(H2S, H2V, NA, W, V, M, out, U, n0 + wv, threadIdx.x & 63, spos[wv], svel[wv]);
+    __syncthreads();   // all of this block's NA reads are done before featurize_nodes rewrites it
+    featurize_nodes<RPP2_MAX>(&spos[0][0], &svel[0][0], n0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn);
 }
 
 // self-feed state update (infer_self_feed.py:182-194, target pos_dt+vel) and trajectory write
@@ -787,7 +832,7 @@ nbx::TpProb tp_base(int rows, const Dims& d) {
 
 int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass, int64_t B,
                  int64_t N, float* out, const Workspace& ws, hipStream_t st, KernelTiming* tm = nullptr,
-                 const RolloutUpdate* upd = nullptr) {
+                 const RolloutUpdate* upd = nullptr, bool featurized = false) {
     const int M = w->mul;
     const Dims d = dims_of(B, N, M);
     const int64_t V = d.V, Ep = d.Ep;
@@ -799,10 +844,13 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     const bool seg_upd = static_enabled() && (M == 96 || M == 32);
     // block: whole multiples of the channel count (192 threads at mul = 96), >= FE_NODES
     const unsigned fe_threads = (unsigned)std::max(64, std::min(1024, M * std::max(1, 256 / M)));
-    hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st, pos, vel,
-                       mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
-                       seg_upd ? ws.XD : nullptr);
-    NBX_LAUNCH_CHECK("embed");
+    // (featurized: a rollout's previous rollout_pp2_kernel already wrote NA / EG / X / XD)
+    if (!featurized) {
+        hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st,
+                           pos, vel, mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
+                           seg_upd ? ws.XD : nullptr);
+        NBX_LAUNCH_CHECK("embed");
+    }
 
     // Lazy feature BatchNorm: X in HBM holds each layer's pre-normalisation output and its
     // consumers in the next layer (message_layer_1, the update inputs, the residual) apply
@@ -993,6 +1041,14 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         }
     }
     }
+    if (upd && upd->featurize_next) {
+        const int nb = (int)N * std::max(1, 8 / (int)N);   // whole systems, N <= RPP2_MAX
+        hipLaunchKernelGGL(rollout_pp2_kernel, dim3((unsigned)nbx::ceil_div(V, nb)), dim3(64 * nb), 0, st, ws.U2S,
+                           ws.U2V, ws.NA, w->pp2, V, M, out, *upd, nb, mass, (int)N, (int)d.G, w->emb, w->emb_bias,
+                           ws.EG, ws.X, seg_upd ? ws.XD : nullptr);
+        NBX_LAUNCH_CHECK("pre_pool2 + next featurise");
+        return NBX_OK;
+    }
     RolloutUpdate none{};
     hipLaunchKernelGGL(pp2_kernel, dim3((unsigned)nbx::ceil_div(V, 4)), dim3(256), 0, st, ws.U2S, ws.U2V, ws.NA,
                        w->pp2, V, M, out, upd ? *upd : none);
@@ -1041,10 +1097,14 @@ extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* 
     hipLaunchKernelGGL(rollout_update_kernel, dim3(ub), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
                        num_frames, traj_pos, traj_vel);
     NBX_LAUNCH_CHECK("rollout_update");
+    // whole systems per rollout_pp2_kernel block (NBX_NO_FE_FUSE: tuning / A-B only)
+    static const bool no_fuse = getenv("NBX_NO_FE_FUSE") != nullptr;
+    const bool fuse = !no_fuse && N <= RPP2_MAX;
     for (int64_t f = 1; f < num_frames; ++f) {
-        // the state update + trajectory write of frame f is fused into pre_pool2's epilogue
-        const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N};
-        if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd)) return rc;
+        // the state update + trajectory write of frame f is fused into pre_pool2's epilogue, and
+        // (fuse) so is the featurisation of frame f + 1's input
+        const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N, fuse && f + 1 < num_frames};
+        if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd, fuse && f >= 2)) return rc;
     }
     return NBX_OK;
 }

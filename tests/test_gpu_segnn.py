@@ -131,10 +131,12 @@ def test_rollout_matches_oracle(hip_device):
     assert mse <= 1e-5, mse
 
 
-def test_rollout_equals_repeated_forward(hip_device):
-    """rollout() is exactly the self-feed loop over forward(): same kernels, same order."""
-    model = make_model(64, 2, hip_device).train()
-    B, N, T = 8, 5, 4
+@pytest.mark.parametrize("hidden,B,N", [(64, 8, 5), (192, 16, 5), (64, 8, 3), (64, 4, 16), (64, 2, 20)])
+def test_rollout_equals_repeated_forward(hip_device, hidden, B, N):
+    """rollout() is exactly the self-feed loop over forward(): same arithmetic, same order (also
+    with the next frame's featurisation fused into pre_pool2, N <= 16, and without it, N = 20)."""
+    model = make_model(hidden, 2, hip_device).train()
+    T = 4
     pos, vel, mass = states(B, N, seed=8)
     sd0 = {k: v.clone() for k, v in model.state_dict().items()}
     loc = torch.tensor(pos.reshape(B, N, 3), dtype=torch.float32, device=hip_device)
