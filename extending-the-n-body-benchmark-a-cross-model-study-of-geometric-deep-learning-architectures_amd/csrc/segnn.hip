@@ -223,60 +223,74 @@ __global__ void msg1_kernel(const float* __restrict__ NP, const float* __restric
     }
 }
 
-// e3nn BatchNorm (train mode) finalisation: one 64-lane group per channel
-// reduces the per-wave partials of the fused TP kernel in a fixed order, then computes
-// scale/shift and the running-stat update r <- (1-m) r + m * batch_stat.
+// e3nn BatchNorm (train mode) finalisation: one block per channel chunk of the producing
+// TP kernel. The chunk's partial rows [wpc][3][cw] are read coalesced (thread = (row phase,
+// column), all loads of a thread issued back to back), the row phases are combined in LDS in a
+// fixed order (deterministic), then one thread per channel computes scale/shift and the
+// running-stat update r <- (1-m) r + m * batch_stat.  The per-channel parameters are loaded
+// before the reduction so their latency overlaps it.
 // coef layout: [0..2M) scale (0e then 1o channels), [2M..3M) shift (0e).
-__global__ void bn_finalize_kernel(const double* __restrict__ partial, int wpc, int cw, double count, int M, int training,
-                                   float eps, float momentum, const float* __restrict__ weight,
-                                   const float* __restrict__ bias, float* __restrict__ rmean,
-                                   float* __restrict__ rvar, float* __restrict__ coef) {
-    const int group = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (group >= 2 * M) return;
-    const bool scalar = group < M;
-    const int c = scalar ? group : group - M;
+constexpr int BNF_THREADS = 1024;
+__global__ __launch_bounds__(BNF_THREADS) void bn_finalize_kernel(
+        const double* __restrict__ partial, int wpc, int cw, double count, int M, int training, float eps,
+        float momentum, const float* __restrict__ weight, const float* __restrict__ bias,
+        float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ coef) {
+    __shared__ double red[BNF_THREADS];
+    const int chunk = blockIdx.x, t = threadIdx.x;
+    const int ncol = 3 * cw, phases = BNF_THREADS / ncol;
+    // finalising threads: t < cw -> 0e channel, cw <= t < 2cw -> 1o channel
+    const bool scalar = t < cw;
+    const int c = chunk * cw + (scalar ? t : t - cw);
+    const bool fin = t < 2 * cw && c < M;
+    float wgt = 0.f, bs = 0.f, rm = 0.f, rv = 0.f;
+    if (fin) {
+        wgt = weight[scalar ? c : M + c];
+        rv = rvar[scalar ? c : M + c];
+        if (scalar) { bs = bias[c]; rm = rmean[c]; }
+    }
     double a = 0.0, b = 0.0;
     if (training) {
-        // partial layout of the fused TP kernels: [chunk][wave][3][cw], cw = chunk width (16 or 32)
-        const double* p = partial + (size_t)(c / cw) * wpc * 3 * cw + (c % cw);
-        for (int i = lane; i < wpc; i += 64) {
-            if (scalar) {
-                a += p[(size_t)i * 3 * cw];
-                b += p[(size_t)i * 3 * cw + cw];
-            } else {
-                a += p[(size_t)i * 3 * cw + 2 * cw];
-            }
+        const int col = t % ncol, ph = t / ncol;
+        double acc = 0.0;
+        if (ph < phases) {
+            const double* p = partial + (size_t)chunk * wpc * ncol + col;
+#pragma unroll 8
+            for (int i = ph; i < wpc; i += phases) acc += p[(size_t)i * ncol];
         }
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_xor(a, off);
-            b += __shfl_xor(b, off);
+        red[t] = acc;
+        __syncthreads();
+        if (fin) {
+            const int ca = scalar ? t : 2 * cw + (t - cw);
+            for (int q = 0; q < phases; ++q) a += red[q * ncol + ca];
+            if (scalar)
+                for (int q = 0; q < phases; ++q) b += red[q * ncol + cw + t];
         }
     }
-    if (lane != 0) return;
+    if (!fin) return;
     if (scalar) {
         double mu, var;
         if (training) {
             mu = a / count;
             var = b / count - mu * mu;
             if (var < 0.0) var = 0.0;
-            rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mu;
-            rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)var;
+            rmean[c] = (1.0f - momentum) * rm + momentum * (float)mu;
+            rvar[c] = (1.0f - momentum) * rv + momentum * (float)var;
         } else {
-            mu = rmean[c];
-            var = rvar[c];
+            mu = rm;
+            var = rv;
         }
-        const float sc = (float)(1.0 / sqrt(var + (double)eps)) * weight[c];
+        const float sc = (float)(1.0 / sqrt(var + (double)eps)) * wgt;
         coef[c] = sc;
-        coef[2 * M + c] = bias[c] - sc * (float)mu;
+        coef[2 * M + c] = bs - sc * (float)mu;
     } else {
         double n;
         if (training) {
             n = a / (3.0 * count);
-            rvar[M + c] = (1.0f - momentum) * rvar[M + c] + momentum * (float)n;
+            rvar[M + c] = (1.0f - momentum) * rv + momentum * (float)n;
         } else {
-            n = rvar[M + c];
+            n = rv;
         }
-        coef[M + c] = (float)(1.0 / sqrt(n + (double)eps)) * weight[M + c];
+        coef[M + c] = (float)(1.0 / sqrt(n + (double)eps)) * wgt;
     }
 }
 
@@ -927,8 +941,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 NBX_HIP(hipMemsetAsync(ws.partial, 0, sizeof(double) * 48 * ((M + 15) / 16), st));
             }
         }
-        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
-                           wpc_msg, cw_msg, (double)(V * (N - 1) > 0 ? V * (N - 1) : 1), M, w->training, w->bn_eps,
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, cw_msg)), dim3(BNF_THREADS), 0, st,
+                           ws.partial, wpc_msg, cw_msg, (double)(V * (N - 1) > 0 ? V * (N - 1) : 1), M, w->training, w->bn_eps,
                            w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
                            L.msg_bn_running_var, ws.coef_msg);
         NBX_LAUNCH_CHECK("bn_finalize(msg)");
@@ -997,8 +1011,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             }
             wpc_feat = p.waves_per_chunk;
         }
-        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(2 * M, 4)), dim3(256), 0, st, ws.partial,
-                           wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, 16)), dim3(BNF_THREADS), 0, st,
+                           ws.partial, wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
                            L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat);
     }
 
