@@ -34,6 +34,8 @@ struct MsgPreProb {
     const float* amf;    // [2][3M] (dist, m_i m_j) -> (s, gate, t)
     const float* bias;   // [2M]   (s, gate)
     const float* xcoef;  // pending feature BatchNorm of X (previous layer): [sc_s(M) | sc_v(M) | sh(M)], or null
+    BnSrc xbn;           // xbn.sums non-null: that BatchNorm finalised here from atomic sums (xcoef unused);
+                         // block 0 stores the coefficients to xbn.coef_out for the layer's later consumers
     float* M1S;          // [V*G][2M]
     float* M1V;          // [3][V*G][M]
     long V;

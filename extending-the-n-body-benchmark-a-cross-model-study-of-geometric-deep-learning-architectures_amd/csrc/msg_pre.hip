@@ -67,7 +67,9 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
     for (int i = t; i < 3 * KC * 32; i += MP_THREADS) {
         const int part = i / (KC * 32), k = i - part * KC * 32;
         float v = 0.f;
-        if (k < M) v = P.xcoef ? P.xcoef[part * M + k] : (part < 2 ? 1.f : 0.f);
+        if (k < M)
+            v = P.xbn.sums ? bn_coef(P.xbn, M, part, k, blockIdx.x == 0)
+                           : (P.xcoef ? P.xcoef[part * M + k] : (part < 2 ? 1.f : 0.f));
         XC[i] = v;
     }
 

@@ -500,6 +500,7 @@ struct Workspace {
     float *X, *NA, *EG, *NP, *M1S, *M1V, *AGG, *U1S, *U1V, *U2S, *U2V, *coef_msg, *coef_feat, *out;
     float *XD, *AD;   // x_v . na and aggregated a_v . na per node and channel (segmented update_layer_1)
     double* partial;
+    double* bn_sums;  // atomic-mode BatchNorm sums: [2 x NBX_SEGNN_MAX_LAYERS][3][M] (message, feature per layer)
     size_t bytes;
 };
 
@@ -515,6 +516,7 @@ size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
     };
     Workspace w;
     w.partial = (double*)take((size_t)partial_doubles(d), 8);
+    w.bn_sums = (double*)take((size_t)2 * NBX_SEGNN_MAX_LAYERS * 3 * M, 8);
     w.X = (float*)take(4 * V * M, 4);
     w.NA = (float*)take(4 * V, 4);
     w.EG = (float*)take(8 * Ep, 4);
@@ -585,6 +587,17 @@ int run_tp(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
 // The node TPs run a fully unrolled K loop when their chunk counts match one of the static
 // schedules compiled here (the C2 width mul = 96 and mul = 32), else the run-time-shaped loop.
 // NBX_STATIC=0 forces the run-time loop (A/B only).
+// BatchNorm statistics by fp64 atomics, finalised inside the consuming kernel (no finalize
+// launch; NBX_BN_ATOMIC=0 restores the partial rows + bn_finalize_kernel path)
+bool bn_atomic_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NBX_BN_ATOMIC");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 bool static_enabled() {
     static int v = -1;
     if (v < 0) {
@@ -870,6 +883,13 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // consumers in the next layer (message_layer_1, the update inputs, the residual) apply
     // the pending per-channel scale/shift (ws.coef_feat) as they read it; null = identity.
     const bool fused_msg = N > 1 && nbx::msg_pre_group((int)N) > 0 && M <= 128;
+    // atomic BatchNorm statistics: the message BN is finalised by update_layer_1 (segmented input),
+    // the feature BN of layers 0..L-2 by the next layer's message_layer_1 (the last layer's feeds
+    // pre_pool1 through the finalize launch)
+    const bool bn_atomic = bn_atomic_enabled() && fused_msg && seg_upd;
+    auto sums_of = [&](int l, int kind) { return ws.bn_sums + ((size_t)2 * l + kind) * 3 * M; };
+    if (bn_atomic && w->num_layers > 0)
+        NBX_HIP(hipMemsetAsync(ws.bn_sums, 0, sizeof(double) * 2 * w->num_layers * 3 * M, st));
     for (int l = 0; l < w->num_layers; ++l) {
         const nbx_segnn_layer& L = w->layers[l];
         const float* xprev = l > 0 ? ws.coef_feat : nullptr;
@@ -887,6 +907,12 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             mp.X = ws.X; mp.Simg = L.node_pre_s_img; mp.Vimg = L.node_pre_v_img; mp.EG = ws.EG;
             mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V; mp.xcoef = xprev;
             mp.V = V; mp.N = (int)N; mp.G = (int)d.G; mp.M = M; mp.NG = nbx::msg_pre_group((int)N);
+            if (bn_atomic && l > 0) {
+                const nbx_segnn_layer& Lp = w->layers[l - 1];
+                mp.xbn = nbx::BnSrc{sums_of(l - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias, Lp.feat_bn_running_mean,
+                                    Lp.feat_bn_running_var, ws.coef_feat, (double)V, w->bn_eps, w->bn_momentum,
+                                    w->training, 1};
+            }
             if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && x3_enabled() && !getenv("NBX_X3_NOMP")) {
                 mp.Simg = static_cast<const float*>(L.node_pre_s_img_x3);
                 mp.Vimg = static_cast<const float*>(L.node_pre_v_img_x3);
@@ -931,6 +957,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G; p.valid_per_group = (int)(N - 1);
             p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
             if (seg_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
+            if (bn_atomic) p.bn_sums = sums_of(l, 0);
             if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
                 if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3)) return rc;
                 wpc_msg = p.waves_per_chunk;
@@ -941,11 +968,13 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 NBX_HIP(hipMemsetAsync(ws.partial, 0, sizeof(double) * 48 * ((M + 15) / 16), st));
             }
         }
-        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, cw_msg)), dim3(BNF_THREADS), 0, st,
-                           ws.partial, wpc_msg, cw_msg, (double)(V * (N - 1) > 0 ? V * (N - 1) : 1), M, w->training, w->bn_eps,
-                           w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
-                           L.msg_bn_running_var, ws.coef_msg);
-        NBX_LAUNCH_CHECK("bn_finalize(msg)");
+        if (!bn_atomic) {
+            hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, cw_msg)), dim3(BNF_THREADS), 0, st,
+                               ws.partial, wpc_msg, cw_msg, (double)(V * (N - 1) > 0 ? V * (N - 1) : 1), M, w->training,
+                               w->bn_eps, w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
+                               L.msg_bn_running_var, ws.coef_msg);
+            NBX_LAUNCH_CHECK("bn_finalize(msg)");
+        }
         if (seg_upd) {
             // update_layer_1 + gate, input segments [x_s | a_s | x_v.na | a_v.na] and [x_v | a_v]
             // read from X / AGG / XD / AD with the pending feature BN and the message BN applied
@@ -956,6 +985,10 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.seg_s[0] = ws.X; p.seg_s[1] = ws.AGG; p.seg_s[2] = ws.XD; p.seg_s[3] = ws.AD;
             p.seg_v[0] = ws.X + V * M; p.seg_v[1] = ws.AGG + V * M; p.seg_vplane = V * M;
             p.xcoef = xprev; p.mcoef = ws.coef_msg; p.deg = (float)(N - 1);
+            if (bn_atomic)
+                p.mbn = nbx::BnSrc{sums_of(l, 0), L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
+                                   L.msg_bn_running_var, ws.coef_msg, (double)(V * (N - 1)), w->bn_eps,
+                                   w->bn_momentum, w->training, 1};
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
@@ -992,6 +1025,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
+            const bool feat_atomic = bn_atomic && l + 1 < w->num_layers;
+            if (feat_atomic) p.bn_sums = sums_of(l, 1);
             p.xcoef = xprev;
             if (seg_upd) { p.out_dot = ws.XD; }
             p.chunks = (M + 15) / 16;
@@ -1011,9 +1046,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             }
             wpc_feat = p.waves_per_chunk;
         }
-        hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, 16)), dim3(BNF_THREADS), 0, st,
-                           ws.partial, wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum, L.feat_bn_weight,
-                           L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat);
+        if (!(bn_atomic && l + 1 < w->num_layers))
+            hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, 16)), dim3(BNF_THREADS), 0, st,
+                               ws.partial, wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum,
+                               L.feat_bn_weight, L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var,
+                               ws.coef_feat);
     }
 
     // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)

@@ -166,9 +166,17 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
     float* segtab = lds + CG * P.img_floats;
     if constexpr (SK::SEG > 0) {
         const int M = P.M;
+        const bool mfin = SK::SEG == 4 && P.mbn.sums != nullptr;   // message BN finalised here
+        const bool own = blockIdx.x == 0;
         for (int i = t; i < 10 * M; i += THREADS) {
             const int part = i / M, k = i - part * M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
             float v;
+            if (mfin && (part == 1 || part == 3 || part == 5 || part == 9)) {
+                const int bp = part == 1 ? 0 : part == 5 ? 2 : 1;
+                v = bn_coef(P.mbn, M, bp, k, own && part != 9);
+                segtab[i] = part == 5 ? P.deg * v : v;
+                continue;
+            }
             switch (part) {
                 case 0: v = P.xcoef ? P.xcoef[k] : 1.f; break;
                 case 1: v = SK::SEG == 4 ? P.mcoef[k] : 0.f; break;
@@ -674,7 +682,12 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
             double acc = 0.0;
             for (int w = 0; w < WAVES; ++w) acc += red[((g * 3 + st) * WAVES + w) * 16 + c];
             const int ch16 = cgroup * CG + g;
-            if (ch16 < nchunks16) P.partial[((size_t)ch16 * P.blocks_per_chunk + blk) * 48 + st * 16 + c] = acc;
+            if (P.bn_sums) {
+                const int ch = ch16 * 16 + c;
+                if (ch16 < nchunks16 && ch < P.M) bn_atomic_add(P.bn_sums + st * P.M + ch, acc);
+            } else if (ch16 < nchunks16) {
+                P.partial[((size_t)ch16 * P.blocks_per_chunk + blk) * 48 + st * 16 + c] = acc;
+            }
         }
     }
     if (P.dbg && lane == 0) P.dbg[((size_t)bidx * WAVES + wave) * 6 + 5] = wall_clock64();   // wall end

@@ -30,6 +30,66 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3 };
 
+// BatchNorm statistics accumulated by the producing kernel with device-scope fp64 atomics
+// ([3][M]: sum s and sum s^2 over the 0e channels, sum |v|^2 over the 1o channels) and
+// finalised by the consuming kernel in its prologue (bn_coef), in place of a separate
+// finalize launch.  Sums arrive in any order: results can differ run to run in the last bits.
+struct BnSrc {
+    const double* sums;   // null: not in use
+    const float* weight;
+    const float* bias;
+    float* rmean;
+    float* rvar;
+    float* coef_out;      // block 0 stores [sc_s | sc_v | sh] here for later consumers, or null
+    double count;
+    float eps, momentum;
+    int training;
+    int update;           // block 0 applies the running-stat update
+};
+
+// Coefficient `part` (0: 0e scale, 1: 1o scale, 2: 0e shift) of channel k, the same arithmetic
+// as segnn.hip bn_finalize_kernel; the owner (one thread of block 0 per (part, k)) also writes
+// the running statistics (parts 0 and 1) and coef_out.
+__device__ inline float bn_coef(const BnSrc& b, int M, int part, int k, bool owner) {
+    if (part == 1) {
+        const double n = b.training ? b.sums[2 * M + k] / (3.0 * b.count) : (double)b.rvar[M + k];
+        const float sc = (float)(1.0 / sqrt(n + (double)b.eps)) * b.weight[M + k];
+        if (owner) {
+            if (b.training && b.update) b.rvar[M + k] = (1.0f - b.momentum) * b.rvar[M + k] + b.momentum * (float)n;
+            if (b.coef_out) b.coef_out[M + k] = sc;
+        }
+        return sc;
+    }
+    double mu, var;
+    if (b.training) {
+        mu = b.sums[k] / b.count;
+        var = b.sums[M + k] / b.count - mu * mu;
+        if (var < 0.0) var = 0.0;
+    } else {
+        mu = b.rmean[k];
+        var = b.rvar[k];
+    }
+    const float sc = (float)(1.0 / sqrt(var + (double)b.eps)) * b.weight[k];
+    const float sh = b.bias[k] - sc * (float)mu;
+    if (owner) {
+        if (part == 0) {
+            if (b.training && b.update) {
+                b.rmean[k] = (1.0f - b.momentum) * b.rmean[k] + b.momentum * (float)mu;
+                b.rvar[k] = (1.0f - b.momentum) * b.rvar[k] + b.momentum * (float)var;
+            }
+            if (b.coef_out) b.coef_out[k] = sc;
+        } else if (b.coef_out) {
+            b.coef_out[2 * M + k] = sh;
+        }
+    }
+    return part == 0 ? sc : sh;
+}
+
+// no-return device-scope fp64 add (executes at the memory side, so adders on every XCD agree)
+__device__ inline void bn_atomic_add(double* p, double v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct TpProb {
     // scalar part: NS sub-tiles, sub-tile j contracts the first K_j columns of A
     const float* As;   // [rows][lda_s]
@@ -62,6 +122,7 @@ struct TpProb {
     float* out_v;        // MSG: AGG planes 1..3; GATE_NODE: U2V planes; RESID: X planes 1..3
     long out_plane;      // stride between output planes (elements)
     double* partial;     // MSG / RESID: [chunks][waves_per_chunk][3][32] fp64 BN partial sums
+    double* bn_sums;     // MSG / RESID atomic mode (non-null): [3][M] fp64 sums instead of partial rows
     int waves_per_chunk;
     // grid geometry (set by the launcher)
     int blocks_per_chunk;
@@ -76,6 +137,7 @@ struct TpProb {
     const float* seg_v[2];
     long seg_vplane;
     const float* mcoef;
+    BnSrc mbn;           // SEG = 4 with mbn.sums: message BN finalised here from atomic sums (mcoef unused)
     float deg;
     // dot outputs (null: none): MSG: out_dot[dst][ch] = sum_k a_v,k na_k[dst] (na: node attrs
     // [V][4]); RESID: out_dot[row][ch] = sum_k x_v,k na_k[row] of the new x
@@ -647,7 +709,12 @@ done:
             const int st = t / 32, c = t % 32;
             double acc = 0.0;
             for (int w = 0; w < WAVES; ++w) acc += red[(st * WAVES + w) * 32 + c];
-            P.partial[((size_t)chunk * P.blocks_per_chunk + blk) * 96 + st * 32 + c] = acc;
+            if (P.bn_sums) {
+                const int ch = chunk * 32 + c;
+                if (ch < P.M) bn_atomic_add(P.bn_sums + st * P.M + ch, acc);
+            } else {
+                P.partial[((size_t)chunk * P.blocks_per_chunk + blk) * 96 + st * 32 + c] = acc;
+            }
         }
     }
 }
