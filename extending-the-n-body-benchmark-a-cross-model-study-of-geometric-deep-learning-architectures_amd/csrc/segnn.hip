@@ -159,7 +159,9 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
                                        const float* __restrict__ mass, int64_t V, int N, int G,
                                        const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
                                        float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
-                                       float* __restrict__ XD) {
+                                       float* __restrict__ XD, double* __restrict__ zsum, int nzero) {
+    // zero the forward's atomic BatchNorm sums (nzero = 0: not in use)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += gridDim.x * blockDim.x) zsum[i] = 0.0;
     const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
     const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
     featurize_nodes<FE_NODES>(pos, vel, 0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn);
@@ -433,8 +435,10 @@ __global__ __launch_bounds__(64 * RPP2_MAX) void rollout_pp2_kernel(
     const float* __restrict__ H2S, const float* __restrict__ H2V, float* __restrict__ NA, const float* __restrict__ W,
     int64_t V, int M, float* __restrict__ out, RolloutUpdate U, int nb, const float* __restrict__ mass, int N, int G,
     const float* __restrict__ emb, const float* __restrict__ emb_b, float* __restrict__ EG, float* __restrict__ X,
-    float* __restrict__ XD) {
+    float* __restrict__ XD, double* __restrict__ zsum, int nzero) {
     __shared__ float spos[RPP2_MAX][3], svel[RPP2_MAX][3];
+    // zero the next forward's atomic BatchNorm sums (this forward's last consumer, pre_pool1, is done)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += gridDim.x * blockDim.x) zsum[i] = 0.0;
     const int64_t n0 = blockIdx.x * (int64_t)nb;
     const int wv = threadIdx.x >> 6;
     const int nn = (int)(V - n0 < nb ? V - n0 : nb);
@@ -871,25 +875,25 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     const bool seg_upd = static_enabled() && (M == 96 || M == 32);
     // block: whole multiples of the channel count (192 threads at mul = 96), >= FE_NODES
     const unsigned fe_threads = (unsigned)std::max(64, std::min(1024, M * std::max(1, 256 / M)));
-    // (featurized: a rollout's previous rollout_pp2_kernel already wrote NA / EG / X / XD)
-    if (!featurized) {
-        hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st,
-                           pos, vel, mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
-                           seg_upd ? ws.XD : nullptr);
-        NBX_LAUNCH_CHECK("embed");
-    }
-
     // Lazy feature BatchNorm: X in HBM holds each layer's pre-normalisation output and its
     // consumers in the next layer (message_layer_1, the update inputs, the residual) apply
     // the pending per-channel scale/shift (ws.coef_feat) as they read it; null = identity.
     const bool fused_msg = N > 1 && nbx::msg_pre_group((int)N) > 0 && M <= 128;
     // atomic BatchNorm statistics: the message BN is finalised by update_layer_1 (segmented input),
-    // the feature BN of layers 0..L-2 by the next layer's message_layer_1 (the last layer's feeds
-    // pre_pool1 through the finalize launch)
+    // the feature BN of layers 0..L-2 by the next layer's message_layer_1, the last layer's by
+    // pre_pool1 (segmented input); the sums are zeroed by the featurising kernel of the forward
     const bool bn_atomic = bn_atomic_enabled() && fused_msg && seg_upd;
     auto sums_of = [&](int l, int kind) { return ws.bn_sums + ((size_t)2 * l + kind) * 3 * M; };
-    if (bn_atomic && w->num_layers > 0)
-        NBX_HIP(hipMemsetAsync(ws.bn_sums, 0, sizeof(double) * 2 * w->num_layers * 3 * M, st));
+    // (featurized: the previous rollout_pp2_kernel zeroed them)
+    const int nzero = bn_atomic ? 2 * w->num_layers * 3 * M : 0;
+    // (featurized: a rollout's previous rollout_pp2_kernel already wrote NA / EG / X / XD)
+    if (!featurized) {
+        hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st,
+                           pos, vel, mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
+                           seg_upd ? ws.XD : nullptr, ws.bn_sums, nzero);
+        NBX_LAUNCH_CHECK("embed");
+    }
+
     for (int l = 0; l < w->num_layers; ++l) {
         const nbx_segnn_layer& L = w->layers[l];
         const float* xprev = l > 0 ? ws.coef_feat : nullptr;
@@ -1025,7 +1029,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
             p.bias = L.upd2_bias; p.geom = ws.NA; p.out_s = ws.X; p.out_v = ws.X + V * M; p.out_plane = V * M;
             p.partial = ws.partial;
-            const bool feat_atomic = bn_atomic && l + 1 < w->num_layers;
+            const bool feat_atomic = bn_atomic;
             if (feat_atomic) p.bn_sums = sums_of(l, 1);
             p.xcoef = xprev;
             if (seg_upd) { p.out_dot = ws.XD; }
@@ -1046,7 +1050,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             }
             wpc_feat = p.waves_per_chunk;
         }
-        if (!(bn_atomic && l + 1 < w->num_layers))
+        if (!bn_atomic)
             hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, 16)), dim3(BNF_THREADS), 0, st,
                                ws.partial, wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum,
                                L.feat_bn_weight, L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var,
@@ -1063,6 +1067,12 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.lda_s = 2 * M; p.lda_v = M;
         p.seg_s[0] = ws.X; p.seg_s[1] = ws.XD; p.seg_v[0] = ws.X + V * M; p.seg_vplane = V * M;
         p.xcoef = w->num_layers > 0 ? ws.coef_feat : nullptr;
+        if (bn_atomic && w->num_layers > 0) {
+            const nbx_segnn_layer& Lp = w->layers[w->num_layers - 1];
+            p.xbn = nbx::BnSrc{sums_of(w->num_layers - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias,
+                               Lp.feat_bn_running_mean, Lp.feat_bn_running_var, ws.coef_feat, (double)V, w->bn_eps,
+                               w->bn_momentum, w->training, 1};
+        }
         p.B = w->pp1_img;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
@@ -1096,7 +1106,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         const int nb = (int)N * std::max(1, 8 / (int)N);   // whole systems, N <= RPP2_MAX
         hipLaunchKernelGGL(rollout_pp2_kernel, dim3((unsigned)nbx::ceil_div(V, nb)), dim3(64 * nb), 0, st, ws.U2S,
                            ws.U2V, ws.NA, w->pp2, V, M, out, *upd, nb, mass, (int)N, (int)d.G, w->emb, w->emb_bias,
-                           ws.EG, ws.X, seg_upd ? ws.XD : nullptr);
+                           ws.EG, ws.X, seg_upd ? ws.XD : nullptr, ws.bn_sums, nzero);
         NBX_LAUNCH_CHECK("pre_pool2 + next featurise");
         return NBX_OK;
     }

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
         const int M = P.M;
         const bool mfin = SK::SEG == 4 && P.mbn.sums != nullptr;   // message BN finalised here
         const bool own = blockIdx.x == 0;
+        const bool xfin = P.xbn.sums != nullptr;                    // pending feature BN finalised here
         for (int i = t; i < 10 * M; i += THREADS) {
             const int part = i / M, k = i - part * M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
             float v;
@@ -175,6 +176,11 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                 const int bp = part == 1 ? 0 : part == 5 ? 2 : 1;
                 v = bn_coef(P.mbn, M, bp, k, own && part != 9);
                 segtab[i] = part == 5 ? P.deg * v : v;
+                continue;
+            }
+            if (xfin && (part == 0 || part == 2 || part == 4 || part == 8)) {
+                const int bp = part == 0 ? 0 : part == 4 ? 2 : 1;
+                segtab[i] = bn_coef(P.xbn, M, bp, k, own && part != 8);
                 continue;
             }
             switch (part) {

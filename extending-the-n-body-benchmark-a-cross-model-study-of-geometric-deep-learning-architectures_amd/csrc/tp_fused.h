@@ -138,6 +138,8 @@ struct TpProb {
     long seg_vplane;
     const float* mcoef;
     BnSrc mbn;           // SEG = 4 with mbn.sums: message BN finalised here from atomic sums (mcoef unused)
+    BnSrc xbn;           // SEG > 0 with xbn.sums: pending feature BN finalised here (the segment table's
+                         // x parts; xcoef unused there)
     float deg;
     // dot outputs (null: none): MSG: out_dot[dst][ch] = sum_k a_v,k na_k[dst] (na: node attrs
     // [V][4]); RESID: out_dot[row][ch] = sum_k x_v,k na_k[row] of the new x
