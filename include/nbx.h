@@ -161,7 +161,10 @@ int nbx_segnn_workspace_bytes(int64_t batch_size, int64_t num_nodes, int32_t mul
 
 /* O3Transform + catch_isolated_nodes + SEGNN.forward in one call
  * (infer_self_feed.py:115-130 graph build and model(graph)).
- * pos/vel [B*N,3], mass [B*N] fp32 -> out [B*N, 6] = (2x1o: delta-pos, vel). */
+ * pos/vel [B*N,3], mass [B*N] fp32 -> out [B*N, 6] = (2x1o: delta-pos, vel).
+ * Train mode (w->training = 1): the BatchNorm batch statistics are fp64 sums accumulated
+ * with device-scope atomics, so repeated calls can differ in the last float bits (eval mode
+ * is bit-reproducible); the running statistics are updated in place as in the reference. */
 int nbx_segnn_forward(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
                       int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
                       void* stream);
