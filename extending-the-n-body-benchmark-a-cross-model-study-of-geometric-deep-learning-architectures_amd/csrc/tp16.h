@@ -205,6 +205,30 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
     float* kred = lds + P.lds_floats - (KS > 1 ? TW * (KS - 1) * NACC * 4 * 64 : 0);  // split-K partials
     for (int it = 0; it < iters; ++it) {
         {
+            // RESID: the epilogue's residual X rows and node attributes, loaded before the K loop so
+            // their latency hides under the MFMAs (not after the last chunk)
+            float rres[EPI == TP_RESID ? CG : 1][4][4];
+            float rna[4][3];
+            if constexpr (EPI == TP_RESID) {
+                const int row0p = rt * 16 + 4 * qd;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int row = row0p + jj;
+                    const bool rok = rt < row_tiles && row < P.rows;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) rna[jj][k] = rok ? P.geom[(size_t)row * 4 + 1 + k] : 0.f;
+#pragma unroll
+                    for (int g = 0; g < CG; ++g) {
+                        const int ch = (cgroup * CG + g) * 16 + c16;
+                        const bool ok = rok && ch < P.M;
+                        const size_t o = (size_t)row * P.M + ch;
+                        rres[g][jj][0] = ok ? P.out_s[o] : 0.f;
+                        rres[g][jj][1] = ok ? P.out_v[o] : 0.f;
+                        rres[g][jj][2] = ok ? P.out_v[P.out_plane + o] : 0.f;
+                        rres[g][jj][3] = ok ? P.out_v[2 * P.out_plane + o] : 0.f;
+                    }
+                }
+            }
             floatx4 acc[CG][NS + 3 * NV];
 #pragma unroll
             for (int g = 0; g < CG; ++g)
@@ -638,17 +662,17 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                     for (int jj = 0; jj < 4; ++jj) {
                         const int row = row0 + jj;
                         if (!live || row >= P.rows) continue;
-                        const float* na = P.geom + (size_t)row * 4;
+                        const float* na = rna[jj] - 1;   // na[1..3]
                         const float tt = acc[g][1][jj];
                         float* xs = P.out_s + (size_t)row * M + ch;
-                        const float s = fmaf(xs_sc, *xs, xs_sh) + (acc[g][0][jj] + b);
+                        const float s = fmaf(xs_sc, rres[g][jj][0], xs_sh) + (acc[g][0][jj] + b);
                         *xs = s;
                         float* x0 = P.out_v + (size_t)row * M + ch;
                         float* x1 = x0 + P.out_plane;
                         float* x2 = x1 + P.out_plane;
-                        const float v0 = xv_sc * *x0 + (na[1] * tt + acc[g][NS + 0][jj]);
-                        const float v1 = xv_sc * *x1 + (na[2] * tt + acc[g][NS + 1][jj]);
-                        const float v2 = xv_sc * *x2 + (na[3] * tt + acc[g][NS + 2][jj]);
+                        const float v0 = xv_sc * rres[g][jj][1] + (na[1] * tt + acc[g][NS + 0][jj]);
+                        const float v1 = xv_sc * rres[g][jj][2] + (na[2] * tt + acc[g][NS + 1][jj]);
+                        const float v2 = xv_sc * rres[g][jj][3] + (na[3] * tt + acc[g][NS + 2][jj]);
                         if (P.out_dot) P.out_dot[(size_t)row * M + ch] = v0 * na[1] + v1 * na[2] + v2 * na[3];
                         *x0 = v0; *x1 = v1; *x2 = v2;
                         st0[g] += (double)s;
