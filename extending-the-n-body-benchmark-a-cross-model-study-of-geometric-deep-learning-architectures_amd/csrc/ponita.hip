@@ -365,12 +365,22 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
         if (mom)
             hipLaunchKernelGGL(po_moments_kernel, dim3(512), dim3(256), 0, st, ws.X1, VO * C, mom + 6 * l + 2);
         {
-            const int PR = std::max(1, std::min(O, (int)((64 * 1024) / ((size_t)O * C * 4))));
+            // orientation range per block: X1 is re-read once per range, so the range is as wide as
+            // a 72 KiB FK slice allows while two blocks still fit a CU (C3: 7 of 20 orientations,
+            // 3 ranges; measured 308 -> 280 us against 64 KiB / 4 ranges, and 358 us at 100 KiB /
+            // 2 ranges with one block per CU).  NBX_PO_FK_LDS: the budget in bytes (tuning)
+            static const size_t fk_lds = getenv("NBX_PO_FK_LDS") ? (size_t)atol(getenv("NBX_PO_FK_LDS")) : 72 * 1024;
+            const int PR = std::max(1, std::min(O, (int)(fk_lds / ((size_t)O * C * 4))));
             const int R = (O + PR - 1) / PR;
             const int npi = PO_FIB_THREADS / (C / 4);
             const int gx = (int)std::min<int64_t>((d.V + npi - 1) / npi, std::max(1, 1024 / R));
             const size_t lds = (size_t)O * PR * C * 4;
             auto kern = O <= 20 ? po_fiber_ln_kernel<20, 4> : po_fiber_ln_kernel<PO_OMAX, 2>;
+            if (lds > 64 * 1024) {
+                NBX_CHECK_ARG(lds <= 160 * 1024, "ponita: fibre kernel slice needs %zu bytes of LDS", lds);
+                NBX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds));
+            }
             if (int rc = nbx::timed(tm, st, PK_FIBER, 2.0 * VO * O * C, (double)VO * C * f4 * 2, [&] {
                     hipLaunchKernelGGL(kern, dim3(gx, R), dim3(PO_FIB_THREADS), lds, st, ws.X1,
                                        ws.FK + (size_t)l * C, L * C, Ly.conv_bias, Ly.norm_w, Ly.norm_b, d.V, O, C,
