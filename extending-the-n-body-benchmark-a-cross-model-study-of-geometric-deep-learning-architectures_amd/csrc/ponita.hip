@@ -146,11 +146,13 @@ __global__ __launch_bounds__(PO_FIB_THREADS, MINW) void po_fiber_ln_kernel(
     const int CG = C >> 2, npi = PO_FIB_THREADS / CG;
     const int t = threadIdx.x, ns = t / CG, cg = t - ns * CG, c = 4 * cg;
     const int p0 = blockIdx.y * PR, pn = min(PR, O - p0);
-    // FK slice -> LDS [o][pl][C]
+    // FK slice -> LDS [o][pl][C], addressed as float4 so every access is one 16-byte LDS op
+    // (float indices with a run-time C let the compiler split them into ds_read2_b32 pairs,
+    // which bank-conflict 4-way: 70 % of the kernel's LDS cycles were conflicts)
+    float4* fk4 = reinterpret_cast<float4*>(fks);
     for (int i = t; i < O * pn * CG; i += PO_FIB_THREADS) {
         const int o = i / (pn * CG), r = i - o * pn * CG, pl = r / CG, q = r - pl * CG;
-        *reinterpret_cast<float4*>(&fks[(o * PR + pl) * C + 4 * q]) =
-            *reinterpret_cast<const float4*>(FK + (size_t)(o * O + p0 + pl) * ldfk + 4 * q);
+        fk4[(o * PR + pl) * CG + q] = *reinterpret_cast<const float4*>(FK + (size_t)(o * O + p0 + pl) * ldfk + 4 * q);
     }
     __syncthreads();
     const float4 cb = *reinterpret_cast<const float4*>(cbias + c);
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(PO_FIB_THREADS, MINW) void po_fiber_ln_kernel(
 #pragma unroll
             for (int o = 0; o < OMAX; ++o) {
                 if (o < O) {
-                    const float4 f = *reinterpret_cast<const float4*>(&fks[(o * PR + pl) * C + c]);
+                    const float4 f = fk4[(o * PR + pl) * CG + cg];
                     a.x += x[o].x * f.x;
                     a.y += x[o].y * f.y;
                     a.z += x[o].z * f.z;
@@ -365,11 +367,10 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
         if (mom)
             hipLaunchKernelGGL(po_moments_kernel, dim3(512), dim3(256), 0, st, ws.X1, VO * C, mom + 6 * l + 2);
         {
-            // orientation range per block: X1 is re-read once per range, so the range is as wide as
-            // a 72 KiB FK slice allows while two blocks still fit a CU (C3: 7 of 20 orientations,
-            // 3 ranges; measured 308 -> 280 us against 64 KiB / 4 ranges, and 358 us at 100 KiB /
-            // 2 ranges with one block per CU).  NBX_PO_FK_LDS: the budget in bytes (tuning)
-            static const size_t fk_lds = getenv("NBX_PO_FK_LDS") ? (size_t)atol(getenv("NBX_PO_FK_LDS")) : 72 * 1024;
+            // orientation range per block (X1 is re-read once per range): a 64 KiB FK slice, C3: 6 of
+            // 20 orientations, 4 ranges -- with conflict-free LDS reads 176 us against 196 us for
+            // 72 KiB / 3 ranges (occupancy beats the re-read).  NBX_PO_FK_LDS: the budget in bytes (tuning)
+            static const size_t fk_lds = getenv("NBX_PO_FK_LDS") ? (size_t)atol(getenv("NBX_PO_FK_LDS")) : 64 * 1024;
             const int PR = std::max(1, std::min(O, (int)(fk_lds / ((size_t)O * C * 4))));
             const int R = (O + PR - 1) / PR;
             const int npi = PO_FIB_THREADS / (C / 4);
