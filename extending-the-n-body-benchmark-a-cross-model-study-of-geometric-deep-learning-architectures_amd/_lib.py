@@ -12,7 +12,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 3
+ABI_VERSION = 4
+ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
 c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double,
@@ -27,10 +28,15 @@ class SegnnLayer(ctypes.Structure):
         "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var")]
 
 
+# nbx_allreduce_fn: int (*)(double* buf, int64_t count, void* stream, void* ctx)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_p, c_i64, c_p, c_p)
+
+
 class SegnnWeights(ctypes.Structure):
     _fields_ = [("mul", c_i32), ("num_layers", c_i32), ("training", c_i32), ("bn_eps", c_f),
                 ("bn_momentum", c_f)] + [(n, c_p) for n in (
                     "emb", "emb_bias", "pp1_img", "pp1_bias", "pp2")] + [
+                ("bn_allreduce", ALLREDUCE_FN), ("bn_allreduce_ctx", c_p), ("bn_global_batch", c_i64),
                 ("layers", SegnnLayer * MAX_LAYERS)]
 
 
@@ -85,9 +91,9 @@ _SIGNATURES = {
     "nbx_egnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_egnn_forward": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_sz,
                                         c_p]),
-    "nbx_egnn_rollout": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p,
+    "nbx_egnn_rollout": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p,
                                         c_p, c_sz, c_p]),
-    "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
+    "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
                                          c_p, c_p, c_p, c_sz, c_p]),
     "nbx_ponita_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_i64, c_i64,
                                                   ctypes.POINTER(c_sz)]),
@@ -96,7 +102,7 @@ _SIGNATURES = {
     "nbx_ponita_forward_timed": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                                 c_p, c_sz, c_p, c_f * 8, c_i32 * 8, c_d * 8, c_d * 8,
                                                 ctypes.POINTER(c_f)]),
-    "nbx_ponita_rollout": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
+    "nbx_ponita_rollout": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
                                           c_p, c_p, c_p, c_sz, c_p]),
 }
 

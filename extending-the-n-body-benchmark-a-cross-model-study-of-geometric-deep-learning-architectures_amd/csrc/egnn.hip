@@ -279,7 +279,7 @@ extern "C" int nbx_egnn_forward(const nbx_egnn_weights* w, const float* pos, con
 }
 
 extern "C" int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t B,
-                                int64_t N, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                                int64_t N, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                                 size_t workspace_bytes, void* stream) {
     EgnnWs ws;
     if (int rc = egnn_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
@@ -287,11 +287,11 @@ extern "C" int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* ve
     hipStream_t st = (hipStream_t)stream;
     const int64_t V = B * N;
     hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
-                       num_frames, traj_pos, traj_vel);
+                       num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     for (int64_t f = 1; f < num_frames; ++f) {
         if (int rc = egnn_forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st)) return rc;
         hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, f,
-                           num_frames, traj_pos, traj_vel);
+                           num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     }
     NBX_LAUNCH_CHECK("egnn rollout");
     return NBX_OK;

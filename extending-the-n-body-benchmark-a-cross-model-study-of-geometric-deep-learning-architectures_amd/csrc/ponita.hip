@@ -487,7 +487,7 @@ extern "C" int nbx_ponita_forward_timed(const nbx_ponita_weights* w, const float
 }
 
 extern "C" int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass, int64_t B,
-                                  int64_t N, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                                  int64_t N, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                                   size_t workspace_bytes, void* stream) {
     PoDims d;
     PoWs ws;
@@ -496,11 +496,11 @@ extern "C" int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float
     hipStream_t st = (hipStream_t)stream;
     const int64_t V = d.V;
     hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
-                       (int64_t)0, num_frames, traj_pos, traj_vel);
+                       (int64_t)0, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     for (int64_t f = 1; f < num_frames; ++f) {
         if (int rc = po_forward_impl(w, pos, vel, mass, d, ws.out, nullptr, ws, st)) return rc;
         hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
-                           f, num_frames, traj_pos, traj_vel);
+                           f, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     }
     NBX_LAUNCH_CHECK("ponita rollout");
     return NBX_OK;

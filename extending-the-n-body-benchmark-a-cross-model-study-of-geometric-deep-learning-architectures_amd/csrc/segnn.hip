@@ -375,6 +375,7 @@ struct RolloutUpdate {
     int64_t frame, num_frames;
     int N;
     int featurize_next;   // rollout_pp2_kernel: also featurise + embed the next frame's input
+    int absolute;         // target "pos+vel" (NBX_ROLLOUT_ABSOLUTE): pos = out[:3] instead of pos += out[:3]
 };
 
 // pre_pool2 of node n by one wave (lanes over M); lanes 0-2 write out[n] and, in a rollout, the
@@ -406,7 +407,7 @@ __device__ __forceinline__ void pp2_node(const float* __restrict__ H2S, const fl
         out[6 * n + k] = dp;
         out[6 * n + 3 + k] = nv;
         if (U.pos) {
-            const float p = U.pos[3 * n + k] + dp;
+            const float p = U.absolute ? dp : U.pos[3 * n + k] + dp;
             U.pos[3 * n + k] = p;
             U.vel[3 * n + k] = nv;
             const int64_t b = n / U.N, d = n - b * U.N;
@@ -884,6 +885,23 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // pre_pool1 (segmented input); the sums are zeroed by the featurising kernel of the forward
     const bool bn_atomic = bn_atomic_enabled() && fused_msg && seg_upd;
     auto sums_of = [&](int l, int kind) { return ws.bn_sums + ((size_t)2 * l + kind) * 3 * M; };
+    // SyncBN (w->bn_allreduce): the batch statistics are reduced over every rank between the
+    // producing kernel and the finalising consumer, and normalised by the global counts
+    const bool sync = w->bn_allreduce != nullptr && w->training;
+    if (sync && !bn_atomic) {
+        nbx::set_error("segnn: SyncBN (bn_allreduce) needs the atomic BatchNorm path (mul 96 or 32, 2 <= N <= 16)");
+        return NBX_E_UNSUPPORTED;
+    }
+    const int64_t Bg = sync && w->bn_global_batch > 0 ? w->bn_global_batch : B;
+    const double cnt_nodes = (double)(Bg * N), cnt_edges = (double)(Bg * N * (N - 1));
+    auto sync_bn = [&](double* sums) -> int {
+        if (!sync) return NBX_OK;
+        if (w->bn_allreduce(sums, (int64_t)3 * M, (void*)st, w->bn_allreduce_ctx) != 0) {
+            nbx::set_error("segnn: bn_allreduce hook failed");
+            return NBX_E_HIP;
+        }
+        return NBX_OK;
+    };
     // (featurized: the previous rollout_pp2_kernel zeroed them)
     const int nzero = bn_atomic ? 2 * w->num_layers * 3 * M : 0;
     // (featurized: a rollout's previous rollout_pp2_kernel already wrote NA / EG / X / XD)
@@ -914,7 +932,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if (bn_atomic && l > 0) {
                 const nbx_segnn_layer& Lp = w->layers[l - 1];
                 mp.xbn = nbx::BnSrc{sums_of(l - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias, Lp.feat_bn_running_mean,
-                                    Lp.feat_bn_running_var, ws.coef_feat, (double)V, w->bn_eps, w->bn_momentum,
+                                    Lp.feat_bn_running_var, ws.coef_feat, cnt_nodes, w->bn_eps, w->bn_momentum,
                                     w->training, 1};
             }
             if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && x3_enabled() && !getenv("NBX_X3_NOMP")) {
@@ -966,6 +984,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3)) return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
+                if (int rc = sync_bn(sums_of(l, 0))) return rc;
             } else {
                 NBX_HIP(hipMemsetAsync(ws.AGG, 0, sizeof(float) * 4 * V * M, st));
                 NBX_HIP(hipMemsetAsync(ws.AD, 0, sizeof(float) * V * M, st));
@@ -991,7 +1010,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.xcoef = xprev; p.mcoef = ws.coef_msg; p.deg = (float)(N - 1);
             if (bn_atomic)
                 p.mbn = nbx::BnSrc{sums_of(l, 0), L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
-                                   L.msg_bn_running_var, ws.coef_msg, (double)(V * (N - 1)), w->bn_eps,
+                                   L.msg_bn_running_var, ws.coef_msg, cnt_edges, w->bn_eps,
                                    w->bn_momentum, w->training, 1};
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
@@ -1049,6 +1068,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             }
             wpc_feat = p.waves_per_chunk;
+            if (int rc = sync_bn(sums_of(l, 1))) return rc;
         }
         if (!bn_atomic)
             hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, 16)), dim3(BNF_THREADS), 0, st,
@@ -1070,7 +1090,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         if (bn_atomic && w->num_layers > 0) {
             const nbx_segnn_layer& Lp = w->layers[w->num_layers - 1];
             p.xbn = nbx::BnSrc{sums_of(w->num_layers - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias,
-                               Lp.feat_bn_running_mean, Lp.feat_bn_running_var, ws.coef_feat, (double)V, w->bn_eps,
+                               Lp.feat_bn_running_mean, Lp.feat_bn_running_var, ws.coef_feat, cnt_nodes, w->bn_eps,
                                w->bn_momentum, w->training, 1};
         }
         p.B = w->pp1_img;
@@ -1147,8 +1167,8 @@ extern "C" int nbx_segnn_forward(const nbx_segnn_weights* w, const float* pos, c
 }
 
 extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass, int64_t B,
-                                 int64_t N, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
-                                 size_t workspace_bytes, void* stream) {
+                                 int64_t N, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
     Workspace ws;
     if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     NBX_CHECK_ARG(num_frames >= 1, "nbx_segnn_rollout: num_frames must be >= 1");
@@ -1164,7 +1184,8 @@ extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* 
     for (int64_t f = 1; f < num_frames; ++f) {
         // the state update + trajectory write of frame f is fused into pre_pool2's epilogue, and
         // (fuse) so is the featurisation of frame f + 1's input
-        const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N, fuse && f + 1 < num_frames};
+        const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N, fuse && f + 1 < num_frames,
+                                (flags & NBX_ROLLOUT_ABSOLUTE) ? 1 : 0};
         if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd, fuse && f >= 2)) return rc;
     }
     return NBX_OK;

@@ -65,8 +65,11 @@ class GravityDatasetOtf:
     def __init__(self, dataset_name="nbody_small", target="pos_dt+vel", path=DEFAULT_DATA_PATH, batch_size=8,
                  sim_length=10000, sample_freq=10, noise_var=0, num_nodes=5, vel_norm=1e-16,
                  interaction_strength=2, dt=0.01, softening=0.2, double_precision=False, center_of_mass=False,
-                 lmax_attr=1, use_cached=False, cache_data=True, device=None, data_path="saved_simulations"):
-        # the hash covers exactly the reference's constructor arguments (device / data_path are ours)
+                 lmax_attr=1, use_cached=False, cache_data=True, device=None, data_path="saved_simulations",
+                 shard_generation=False):
+        # the hash covers exactly the reference's constructor arguments (device / data_path /
+        # shard_generation are ours)
+        self.shard_generation = shard_generation
         self.locals = {"dataset_name": dataset_name, "target": target, "batch_size": batch_size,
                        "sim_length": sim_length, "sample_freq": sample_freq, "noise_var": noise_var,
                        "num_nodes": num_nodes, "vel_norm": vel_norm, "interaction_strength": interaction_strength,
@@ -99,13 +102,17 @@ class GravityDatasetOtf:
                           interaction_strength=self.interaction_strength, dt=self.dt, softening=self.softening,
                           device=self.device)
 
-    def get_ground_truth_trajectories(self, batch_size=None, seeds=None):
+    def get_ground_truth_trajectories(self, batch_size=None, seeds=None, shard=None):
         """lines 91-107: ``batch_size`` trajectories ``(pos, vel, force, mass)`` of
-        ``sim_length / sample_freq`` frames, integrated in one device launch."""
+        ``sim_length / sample_freq`` frames, integrated in one device launch.  ``shard``
+        (default: the constructor's ``shard_generation``): under torch.distributed each rank
+        integrates its block of the trajectories and one all-gather assembles the batch on
+        every rank (the reference's ProcessPool, lines 96-104, spread over GPUs)."""
         if batch_size is None:
             batch_size = self.batch_size
+        shard = self.shard_generation if shard is None else shard
         batch_data = self.simulation.sample_trajectory_batch(batch_size, self.sim_length, self.sample_freq,
-                                                             seeds=seeds)
+                                                             seeds=seeds, shard=shard)
         return batch_data, self.get_serializable_attributes()
 
     def _load_more_batches(self):

@@ -199,7 +199,7 @@ class EGNNMultiChannel(nn.Module):
         if N is None:
             from .segnn import SEGNN
             B, N = SEGNN.infer_system_size(V, graph.edge_index.shape[1])
-            from .graph import fc_edge_index
+            from .graph import _fc_edge_index_shared as fc_edge_index
             if not torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device)):
                 raise NotImplementedError("native EGNN-MC needs the fully-connected edge_index")
         else:
@@ -218,7 +218,9 @@ class EGNNMultiChannel(nn.Module):
         return out.to(pos.dtype)
 
     @torch.no_grad()
-    def rollout(self, loc, vel, mass, num_frames: int):
+    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False):
+        """Device-resident self-feed (infer_self_feed.py:161-194); ``absolute``: pos = pred[:, :3]
+        (targets other than "pos_dt+vel") instead of pos += pred[:, :3]."""
         device = loc.device
         B, N, _ = loc.shape
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
@@ -228,6 +230,7 @@ class EGNNMultiChannel(nn.Module):
         W = self._weights(device)
         ws = self._workspace(B, N, device)
         _lib.check(_lib.lib().nbx_egnn_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                               num_frames, _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
+                                               num_frames, _lib.ROLLOUT_ABSOLUTE if absolute else 0,
+                                               _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
                                                ws.numel(), _lib.stream_ptr(device)), "nbx_egnn_rollout")
         return tp, tv

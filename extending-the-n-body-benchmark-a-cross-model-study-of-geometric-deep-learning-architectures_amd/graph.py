@@ -2,16 +2,20 @@
 by libnbx (bit-exact with the reference)."""
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import torch
 
 from . import _lib
 
-_cache = {}
+_CACHE_MAX = 8
+_cache: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
 
 
-def fc_edge_index(batch_size: int, num_nodes: int, device) -> torch.Tensor:
-    """_build_fully_connected_edge_index (build_fully_connected_graph.py:4-20).
-    Cached per (B, N, device): the pattern is a pure function of the sizes."""
+def _fc_edge_index_shared(batch_size: int, num_nodes: int, device) -> torch.Tensor:
+    """Internal read-only copy of the fully-connected pattern, cached per (B, N, device)
+    (LRU, at most _CACHE_MAX entries).  Used by the models to validate a graph's
+    edge_index; never handed to callers."""
     device = torch.device(device)
     key = (int(batch_size), int(num_nodes), device)
     ei = _cache.get(key)
@@ -21,7 +25,18 @@ def fc_edge_index(batch_size: int, num_nodes: int, device) -> torch.Tensor:
         _lib.check(_lib.lib().nbx_fc_edge_index(batch_size, num_nodes, _lib.dev_ptr(ei), _lib.stream_ptr(device)),
                    "nbx_fc_edge_index")
         _cache[key] = ei
+        while len(_cache) > _CACHE_MAX:
+            _cache.popitem(last=False)
+    else:
+        _cache.move_to_end(key)
     return ei
+
+
+def fc_edge_index(batch_size: int, num_nodes: int, device) -> torch.Tensor:
+    """_build_fully_connected_edge_index (build_fully_connected_graph.py:4-20).
+    Returns a fresh tensor on every call, like the reference (callers may modify it
+    in place, e.g. to offset indices while collating)."""
+    return _fc_edge_index_shared(batch_size, num_nodes, device).clone()
 
 
 def build_graph_with_knn(loc, batch_size, num_nodes, device, num_neighbors):

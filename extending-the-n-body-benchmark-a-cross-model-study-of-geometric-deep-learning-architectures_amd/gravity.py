@@ -98,33 +98,46 @@ class GravitySim:
             o += np.random.randn(Ts, self.n_balls, self.dim) * self.noise_var
         return out[0], out[1], out[2], mass
 
-    def sample_trajectory_batch(self, batch_size, T=10000, sample_freq=10, seeds=None):
+    def sample_trajectory_batch(self, batch_size, T=10000, sample_freq=10, seeds=None, shard=False):
         """``batch_size`` independent ``sample_trajectory`` calls integrated in one launch.
         Each trajectory consumes the legacy RNG exactly as the reference's does
         (seed -> initial conditions -> observation noise; the integration itself draws
         nothing), so trajectory i equals ``sample_trajectory(random_seed=seeds[i])``.
-        ``seeds=None`` means OS entropy per trajectory, like the reference dataset."""
+        ``seeds=None`` means OS entropy per trajectory, like the reference dataset.
+
+        ``shard=True`` under torch.distributed (one process per GPU; the reference's
+        ProcessPool, dataset_gravity_otf.py:96-104, spread over GPUs): each rank integrates
+        its contiguous block of the trajectories (parallel.shard_range) and one all-gather
+        (RCCL over xGMI) gives every rank the whole batch in trajectory order."""
+        from . import parallel as P
         if seeds is None:
             seeds = [None] * batch_size
         if len(seeds) != batch_size:
             raise ValueError("need one seed per trajectory")
+        world = P.world() if shard else 1
+        start, count = P.shard_range(batch_size, P.rank(), world) if world > 1 else (0, batch_size)
         Ts = T // sample_freq
-        ics, noise = [], []
-        for s in seeds:
+        ics = []
+        for s in seeds[start:start + count]:
             pos, vel, mass = self.initial_conditions(s)
-            ics.append((pos, vel, mass))
-            noise.append([np.random.randn(Ts, self.n_balls, self.dim) * self.noise_var for _ in range(3)])
-        pos = np.stack([p for p, _, _ in ics])
-        vel = np.stack([v for _, v, _ in ics])
-        mass = np.stack([m for _, _, m in ics])
-        ps, vs, fs = (t.cpu().numpy() for t in self.sample_trajectories(pos, vel, mass, T, sample_freq))
-        out = []
-        for i in range(batch_size):
-            traj = [ps[i], vs[i], fs[i]]
-            for o, n in zip(traj, noise[i]):
-                o += n
-            out.append((traj[0], traj[1], traj[2], ics[i][2]))
-        return out
+            nz = [np.random.randn(Ts, self.n_balls, self.dim) * self.noise_var for _ in range(3)]
+            ics.append((pos, vel, mass, nz))
+        N = self.n_balls
+        pos = np.stack([c[0] for c in ics]) if ics else np.zeros((0, N, 3))
+        vel = np.stack([c[1] for c in ics]) if ics else np.zeros((0, N, 3))
+        mass = np.stack([c[2] for c in ics]) if ics else np.zeros((0, N, 1))
+        if count:
+            ps, vs, fs = self.sample_trajectories(pos, vel, mass, T, sample_freq)
+        else:
+            ps = vs = fs = torch.zeros(0, Ts, N, 3, dtype=torch.float64, device=self.device)
+        if ics and self.noise_var:
+            noise = torch.as_tensor(np.stack([np.stack(c[3]) for c in ics]), device=self.device)   # [S, 3, Ts, N, 3]
+            ps, vs, fs = ps + noise[:, 0], vs + noise[:, 1], fs + noise[:, 2]
+        m = torch.as_tensor(mass, dtype=torch.float64, device=self.device)
+        if world > 1:
+            ps, vs, fs, m = (P.all_gather_shards(t.contiguous(), batch_size) for t in (ps, vs, fs, m))
+        ps, vs, fs, m = (t.cpu().numpy() for t in (ps, vs, fs, m))
+        return [(ps[i], vs[i], fs[i], m[i]) for i in range(batch_size)]
 
     def _energy(self, pos, vel, mass, G):
         """synthetic_sim.py:450-473 (host numpy, evaluation only)."""

@@ -28,7 +28,7 @@ from . import _lib
 from .dataloaders import get_device
 from .dataset import GravityDatasetOtf
 
-__all__ = ["run_inference", "SelfFeedError", "MACROS_DIR_NAME", "STEPS_TO_RETURN_MULTIPLIER", "nbody_energies",
+__all__ = ["run_inference", "load_model_for_inference", "SelfFeedError", "MACROS_DIR_NAME", "STEPS_TO_RETURN_MULTIPLIER", "nbody_energies",
            "get_dataset_metadata_path", "load_dataset_from_metadata_file", "SelfFeedTrainer"]
 
 MACROS_DIR_NAME = "visualize_macros"
@@ -97,14 +97,50 @@ def nbody_energies(loc, vel, G, softening, device=None):
     return {"potential": mp, "kinetic": mk, "total": mp + mk}
 
 
+def load_model_for_inference(model_path, model_type, device):
+    """utils/nbody_utils.py:1316-1373 + load_checkpoint (:1376-1407): the family's default
+    constructor, the checkpoint's ``model_state_dict`` (or a bare state_dict), then
+    ``eval()`` on ``device``.  Checkpoints are read with ``torch.load(weights_only=True)``
+    (tensors and plain containers only).  Like the reference, only segnn / ponita load here."""
+    from .ponita import PONITA_NBODY
+    from .segnn import SEGNN
+    print(f"Initializing model of type '{model_type}' on device {device}")
+    if model_type == "segnn":
+        model = SEGNN()
+    elif model_type == "ponita":
+        model = PONITA_NBODY()
+    else:
+        raise ValueError(f"Unsupported model_type: {model_type}")
+    print(f"Loading checkpoint from {model_path} on device {device}")
+    ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
+    if isinstance(ckpt, dict) and "model_state_dict" in ckpt:
+        model.load_state_dict(ckpt["model_state_dict"])
+    elif isinstance(ckpt, dict) and all(isinstance(v, torch.Tensor) for v in ckpt.values()):
+        model.load_state_dict(ckpt)
+    else:
+        raise ValueError("Checkpoint does not contain a model state dict.")
+    model.eval().to(device)
+    return model
+
+
 @torch.no_grad()
 def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=None, print_step=True, n_bodies=None,
-                  plot_macros=False, num_neighbors=None, device=None, max_rollout_steps=None, dataset=None):
+                  plot_macros=False, num_neighbors=None, device=None, max_rollout_steps=None, dataset=None,
+                  shard=None):
     """infer_self_feed.py:20-254.  Returns ``(trajectories_save_dir,
     combined_locations [2,B,T,N,3], combined_velocities [2,B,T,N,3])``.
 
     The dataset comes from ``dataset`` if given, else from the run's metadata file
-    (``model_path``), else from the dataloader's dataset attributes."""
+    (``model_path``), else from the dataloader's dataset attributes.  ``model=None``
+    loads ``model_path`` like the reference (load_model_for_inference).
+
+    ``shard`` (default: on when torch.distributed has more than one rank): one process
+    per GPU, each rank integrates the ground truth of its contiguous block of the B
+    systems and rolls it out; a SEGNN in train mode keeps the reference's full-batch
+    BatchNorm statistics through SyncBN (12 all-reduces of 288 doubles per step); one
+    all-gather at the end assembles the [2, B, T, N, 3] arrays on every rank and rank 0
+    writes the files."""
+    from . import parallel as P
     torch.manual_seed(42)
     if device is None:
         device = get_device()
@@ -130,11 +166,20 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
                 n_bodies = meta["num_nodes"]
         dataset = load_dataset_from_metadata_file(None, n_bodies=n_bodies, device=device, metadata=meta)
     if model is None:
-        raise NotImplementedError("pass the model instance (checkpoint loading: model.load_state_dict)")
+        if model_path is None:
+            raise ValueError("run_inference needs a model or a model_path")
+        model = load_model_for_inference(model_path, model_type, device)
     model = model.double() if dataset.double_precision else model.float()
 
+    world = P.world()
+    shard = (world > 1) if shard is None else (bool(shard) and world > 1)
     batch_size = dataset.batch_size
-    batch_data, _ = dataset.get_ground_truth_trajectories(batch_size=batch_size)
+    if shard:
+        start, count = P.shard_range(batch_size, P.rank(), world)
+        batch_data, _ = dataset.get_ground_truth_trajectories(batch_size=count, shard=False)
+    else:
+        count = batch_size
+        batch_data, _ = dataset.get_ground_truth_trajectories(batch_size=batch_size)
     loc_actual, vel_actual, force_actual, mass_actual = [torch.from_numpy(np.array(d)) for d in zip(*batch_data)]
     output_dims = loc_actual.shape[-1]
     n_nodes = loc_actual.shape[-2]
@@ -156,33 +201,52 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
     dtype = torch.float64 if dataset.double_precision else torch.float32
     loc0 = loc_actual[:, 0].to(device=device, dtype=dtype)
     vel0 = vel_actual[:, 0].to(device=device, dtype=dtype)
-    mass0 = mass_actual.reshape(batch_size, n_nodes, 1).to(device=device, dtype=dtype)
+    mass0 = mass_actual.reshape(count, n_nodes, 1).to(device=device, dtype=dtype)
     if print_step:
-        print(f"Predicting {num_steps - 1} steps for {batch_size} simulations (device-resident rollout)")
-    tp, tv = model.rollout(loc0, vel0, mass0, num_steps)
+        print(f"Predicting {num_steps - 1} steps for {batch_size} simulations (device-resident rollout"
+              + (f", {count} on rank {P.rank()} of {world})" if shard else ")"))
+    # infer_self_feed.py:185-186: only "pos_dt+vel" adds the prediction to the previous position
+    kw = {"absolute": True} if dataset.target != "pos_dt+vel" else {}
+    sync = shard and hasattr(model, "enable_sync_batchnorm") and model.training
+    if sync:
+        model.enable_sync_batchnorm()
+    try:
+        tp, tv = model.rollout(loc0, vel0, mass0, num_steps, **kw)
+    finally:
+        if sync:
+            model.disable_sync_batchnorm()
     print("Finished prediction for all simulations")
+    steps_in_actual = loc_actual.shape[1]
+    loc_actual = loc_actual.reshape(count, steps_in_actual, n_nodes, output_dims)
+    vel_actual = vel_actual.reshape(count, steps_in_actual, n_nodes, output_dims)
+    if shard:   # the one collective of the sharded rollout: [count, T, N, 3] x 4 -> [B, T, N, 3] x 4
+        gt = [t.to(device=device, dtype=loc_actual.dtype).contiguous() for t in (loc_actual, vel_actual)]
+        loc_actual, vel_actual = (P.all_gather_shards(t, batch_size) for t in gt)
+        tp, tv = (P.all_gather_shards(t.contiguous(), batch_size) for t in (tp, tv))
     loc_pred = tp.to(dtype).cpu().numpy()
     vel_pred = tv.to(dtype).cpu().numpy()
-    steps_in_actual = loc_actual.shape[1]
-    loc_actual = loc_actual.view(batch_size, steps_in_actual, n_nodes, output_dims).numpy()
-    vel_actual = vel_actual.view(batch_size, steps_in_actual, n_nodes, output_dims).numpy()
+    loc_actual = loc_actual.cpu().numpy() if torch.is_tensor(loc_actual) else loc_actual
+    vel_actual = vel_actual.cpu().numpy() if torch.is_tensor(vel_actual) else vel_actual
     combined_locations = np.stack([loc_actual, loc_pred], axis=0)
     combined_velocities = np.stack([vel_actual, vel_pred], axis=0)
 
     if not save_dir:
         base = os.path.dirname(model_path) if model_path else "."
         save_dir = f"{base}/generated_trajectories/{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}"
-    os.makedirs(save_dir, exist_ok=True)
-    if plot_macros:
-        warnings.warn("plot_macros is outside the native rollout scope; skipped")
     out_dir = os.path.join(save_dir, "trajectories_data")
-    os.makedirs(out_dir, exist_ok=True)
-    for i in range(batch_size):
-        np.save(os.path.join(out_dir, f"loc_actual_sim_{i}.npy"), loc_actual[i])
-        np.save(os.path.join(out_dir, f"loc_pred_sim_{i}.npy"), loc_pred[i])
-        np.save(os.path.join(out_dir, f"vel_actual_sim_{i}.npy"), vel_actual[i])
-        np.save(os.path.join(out_dir, f"vel_pred_sim_{i}.npy"), vel_pred[i])
-    print(f"Saved actual and predicted trajectories for all simulations to {out_dir}")
+    if P.rank() == 0 or not shard:
+        os.makedirs(save_dir, exist_ok=True)
+        if plot_macros:
+            warnings.warn("plot_macros is outside the native rollout scope; skipped")
+        os.makedirs(out_dir, exist_ok=True)
+        for i in range(batch_size):
+            np.save(os.path.join(out_dir, f"loc_actual_sim_{i}.npy"), loc_actual[i])
+            np.save(os.path.join(out_dir, f"loc_pred_sim_{i}.npy"), loc_pred[i])
+            np.save(os.path.join(out_dir, f"vel_actual_sim_{i}.npy"), vel_actual[i])
+            np.save(os.path.join(out_dir, f"vel_pred_sim_{i}.npy"), vel_pred[i])
+        print(f"Saved actual and predicted trajectories for all simulations to {out_dir}")
+    if shard:
+        P.barrier()
     return out_dir, combined_locations, combined_velocities
 
 

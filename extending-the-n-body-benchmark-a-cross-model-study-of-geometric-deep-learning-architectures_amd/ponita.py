@@ -299,7 +299,7 @@ class PONITA_NBODY(nn.Module):
         if N is None:
             from .segnn import SEGNN
             B, N = SEGNN.infer_system_size(V, graph.edge_index.shape[1])
-            from .graph import fc_edge_index
+            from .graph import _fc_edge_index_shared as fc_edge_index
             if not torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device)):
                 raise NotImplementedError("native PONITA needs the fully-connected edge_index")
         else:
@@ -326,12 +326,14 @@ class PONITA_NBODY(nn.Module):
         return out.to(pos.dtype)
 
     @torch.no_grad()
-    def rollout(self, loc, vel, mass, num_frames: int):
+    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False):
         """Self-feed loop (infer_self_feed.py:131-147,182-194) device-resident:
         loc/vel [B,N,3], mass [B,N,1] -> trajectories [B, T, N, 3] each, frame 0 =
         the initial state.  A model still owing its one-time calibration runs one
         calibrating forward on the initial state first, as the reference's first
-        step would."""
+        step would.  ``absolute``: pos = pred[:, :3] (targets other than "pos_dt+vel",
+        infer_self_feed.py:185-186) instead of pos += pred[:, :3]."""
+        flags = _lib.ROLLOUT_ABSOLUTE if absolute else 0
         device = loc.device
         B, N, _ = loc.shape
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
@@ -349,7 +351,7 @@ class PONITA_NBODY(nn.Module):
         ws = self._workspace(W, B, N, device)
         if first is None:
             _lib.check(_lib.lib().nbx_ponita_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                                     num_frames, _lib.dev_ptr(tp), _lib.dev_ptr(tv),
+                                                     num_frames, flags, _lib.dev_ptr(tp), _lib.dev_ptr(tv),
                                                      _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
                        "nbx_ponita_rollout")
             return tp, tv
@@ -357,12 +359,12 @@ class PONITA_NBODY(nn.Module):
         tp[:, 0], tv[:, 0] = p, v
         if num_frames == 1:
             return tp, tv
-        p = p + first[:, :3].reshape(B, N, 3)
+        p = first[:, :3].reshape(B, N, 3).contiguous() if absolute else p + first[:, :3].reshape(B, N, 3)
         v = first[:, 3:].reshape(B, N, 3).contiguous()
         rp = torch.empty(B, num_frames - 1, N, 3, device=device, dtype=torch.float32)
         rv = torch.empty_like(rp)
         _lib.check(_lib.lib().nbx_ponita_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                                 num_frames - 1, _lib.dev_ptr(rp), _lib.dev_ptr(rv),
+                                                 num_frames - 1, flags, _lib.dev_ptr(rp), _lib.dev_ptr(rv),
                                                  _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
                    "nbx_ponita_rollout")
         tp[:, 1:], tv[:, 1:] = rp, rv

@@ -139,6 +139,8 @@ class SEGNN(nn.Module):
         self._packed = None
         self._ws = None
         self._warned_dtype = False
+        self._bn_group = None        # SyncBN process group (enable_sync_batchnorm)
+        self._bn_hook = None
 
     # ------------------------------------------------------------ reference API
     def get_model_size(self):
@@ -312,13 +314,26 @@ class SEGNN(nn.Module):
                 out[key] = P[key]
         return out
 
+    def _bn_buffers(self):
+        for layer in self.layers:
+            for bn in (layer.message_norm, layer.feature_norm):
+                yield bn.running_mean
+                yield bn.running_var
+
     def pack_weights(self, device):
-        """Build the nbx_segnn_weights struct (device pointers) from packed_matrices."""
+        """Build the nbx_segnn_weights struct (device pointers) from packed_matrices.
+
+        The kernels update the BatchNorm running statistics in place in fp32.  When the
+        module's buffers are fp32 device tensors the struct points straight at them; after
+        ``model.double()`` (the reference's default precision_mode, infer_self_feed.py:45-48)
+        it points at fp32 device shadows that ``_bn_sync_in`` / ``_bn_sync_out`` copy from /
+        back into the fp64 buffers around every native call."""
         P = self.tp_images(self.packed_matrices(device), self.mul)
         W = _lib.SegnnWeights()
         W.mul, W.num_layers, W.bn_eps, W.bn_momentum = self.mul, self.num_layers, 1e-5, 0.1
         for k in ("emb", "emb_bias", "pp1_img", "pp1_bias", "pp2"):
             setattr(W, k, P[k].data_ptr())
+        shadows = []
         for li, layer in enumerate(self.layers):
             L = W.layers[li]
             for name, _ in L._fields_:
@@ -326,13 +341,17 @@ class SEGNN(nn.Module):
                 if key in P:
                     setattr(L, name, P[key].data_ptr())
             for name, bn in (("msg", layer.message_norm), ("feat", layer.feature_norm)):
-                # running stats are updated IN PLACE by the kernels: point at the module's buffers
                 for stat in ("running_mean", "running_var"):
                     buf = getattr(bn, stat)
-                    if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
-                        raise _lib.NbxError("BatchNorm running stats must be contiguous fp32 on the device")
-                    setattr(L, f"{name}_bn_{stat}", buf.data_ptr())
-        self._packed = (self._param_version(), W, P)
+                    if not buf.is_cuda:
+                        raise _lib.NbxError("BatchNorm running stats must live on the HIP device")
+                    if buf.dtype == torch.float32 and buf.is_contiguous():
+                        setattr(L, f"{name}_bn_{stat}", buf.data_ptr())   # updated in place
+                    else:
+                        sh = torch.empty(buf.shape, dtype=torch.float32, device=buf.device)
+                        shadows.append((buf, sh))
+                        setattr(L, f"{name}_bn_{stat}", sh.data_ptr())
+        self._packed = (self._param_version(), W, P, shadows)
         return W
 
     def _weights(self, device):
@@ -341,6 +360,58 @@ class SEGNN(nn.Module):
         W = self._packed[1]
         W.training = 1 if self.training else 0
         return W
+
+    # ------------------------------------------------------------ SyncBN (multi-GPU)
+    def enable_sync_batchnorm(self, group=None):
+        """Train-mode BatchNorm over the union of every rank's batch (the reference's
+        single-process statistics, segnn.py:233-235,257-261,282-283, when the batch is sharded
+        over ranks): after each producing kernel the [3][mul] fp64 sums of that BatchNorm are
+        all-reduced over ``group`` (torch.distributed; RCCL under the ``nccl`` backend) on the
+        launch stream and normalised by the global counts.  12 all-reduces per forward."""
+        import torch.distributed as dist
+        self._bn_group = group if group is not None else dist.group.WORLD
+        return self
+
+    def disable_sync_batchnorm(self):
+        self._bn_group = None
+        return self
+
+    def _allreduce_cb(self, buf, count, stream, ctx):
+        try:
+            import torch.distributed as dist
+            ws = self._ws
+            off = int(buf) - ws.data_ptr()
+            if off < 0 or off + 8 * count > ws.numel() or off % 8:
+                raise _lib.NbxError("bn_allreduce: buffer outside the workspace")
+            dist.all_reduce(ws[off:off + 8 * count].view(torch.float64), group=self._bn_group)
+            return 0
+        except Exception:  # reported to the library as a failed hook -> NbxError in the caller
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    def _arm_sync(self, W, B, device):
+        """Point the weight struct's hook at the SyncBN callback (or clear it) for one call."""
+        if self._bn_group is None or not self.training:
+            W.bn_allreduce = _lib.ALLREDUCE_FN()
+            W.bn_global_batch = 0
+            return
+        import torch.distributed as dist
+        if self._bn_hook is None:
+            self._bn_hook = _lib.ALLREDUCE_FN(self._allreduce_cb)
+        nb = torch.tensor([B], dtype=torch.int64, device=device)
+        dist.all_reduce(nb, group=self._bn_group)
+        W.bn_allreduce = self._bn_hook
+        W.bn_global_batch = int(nb.item())
+
+    def _bn_sync_in(self):
+        for buf, sh in self._packed[3]:
+            sh.copy_(buf)
+
+    def _bn_sync_out(self):
+        if self.training:
+            for buf, sh in self._packed[3]:
+                buf.copy_(sh)
 
     def _workspace(self, B, N, device):
         nbytes = _lib.c_sz()
@@ -377,7 +448,7 @@ class SEGNN(nn.Module):
             B = V // N
         else:
             B, N = self.infer_system_size(V, edge_index.shape[1])
-            from .graph import fc_edge_index
+            from .graph import _fc_edge_index_shared as fc_edge_index
             if not torch.equal(edge_index.to(device), fc_edge_index(B, N, device)):
                 raise NotImplementedError("native SEGNN needs the fully-connected edge_index of "
                                           "build_graph_with_knn (num_neighbors = N-1)")
@@ -391,15 +462,19 @@ class SEGNN(nn.Module):
         out = torch.empty(V, 6, device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(B, N, device)
+        self._arm_sync(W, B, device)
+        self._bn_sync_in()
         _lib.check(_lib.lib().nbx_segnn_forward(
             W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(out),
             _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_forward")
+        self._bn_sync_out()
         return out.to(out_dtype)
 
     @torch.no_grad()
-    def rollout(self, loc, vel, mass, num_frames: int):
-        """Device-resident self-feed (infer_self_feed.py:99-194, target pos_dt+vel).
-        loc/vel [B,N,3], mass [B,N,1] -> (traj_loc, traj_vel) [B, num_frames, N, 3] fp32."""
+    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False):
+        """Device-resident self-feed (infer_self_feed.py:99-194): loc/vel [B,N,3], mass [B,N,1]
+        -> (traj_loc, traj_vel) [B, num_frames, N, 3] fp32.  ``absolute``: the model predicts
+        positions (dataset targets other than "pos_dt+vel", infer_self_feed.py:185-186)."""
         device = loc.device
         self._check_params(device)
         B, N, _ = loc.shape
@@ -409,7 +484,11 @@ class SEGNN(nn.Module):
         tv = torch.empty_like(tp)
         W = self._weights(device)
         ws = self._workspace(B, N, device)
+        self._arm_sync(W, B, device)
+        self._bn_sync_in()
         _lib.check(_lib.lib().nbx_segnn_rollout(
-            W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames, _lib.dev_ptr(tp),
-            _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_rollout")
+            W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames,
+            _lib.ROLLOUT_ABSOLUTE if absolute else 0, _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
+            ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_rollout")
+        self._bn_sync_out()
         return tp, tv

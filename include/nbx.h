@@ -22,13 +22,17 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 3
+#define NBX_ABI_VERSION 4
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
 #define NBX_E_UNSUPPORTED 2 /* configuration outside the native path */
 #define NBX_E_HIP 3        /* HIP runtime error (message has details) */
 #define NBX_E_WORKSPACE 4  /* workspace too small */
+
+/* rollout flags */
+#define NBX_ROLLOUT_ABSOLUTE 1 /* the model predicts absolute positions: pos = pred[:, :3] (every dataset target
+                                  other than "pos_dt+vel", infer_self_feed.py:185-186); default pos += pred[:, :3] */
 
 int nbx_abi_version(void);
 const char* nbx_last_error(void);
@@ -115,6 +119,11 @@ int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size,
  */
 #define NBX_SEGNN_MAX_LAYERS 64
 
+/* Cross-rank sum hook: sums `count` doubles at device address `buf` over all ranks in place;
+ * the reduction must be ordered after the work already enqueued on `stream` and before the work
+ * enqueued after the call returns.  Returns 0 on success. */
+typedef int (*nbx_allreduce_fn)(double* buf, int64_t count, void* stream, void* ctx);
+
 typedef struct nbx_segnn_layer {
     const float* node_pre_s_img; /* image of [6*mul][mul] x_s -> [P_dst(2mul) R_dst(mul) P_src(2mul) R_src(mul)] */
     const float* node_pre_v_img; /* image of [6*mul][mul] x_v[:,k] -> [Q_dst(2mul) S_dst(mul) Q_src(2mul) S_src(mul)] */
@@ -153,6 +162,16 @@ typedef struct nbx_segnn_weights {
     const float* pp1_img;  /* pre_pool1 (gate TP, node attrs): [3*mul][2*mul] + [mul][mul] */
     const float* pp1_bias; /* [2*mul] */
     const float* pp2;      /* [2][2][mul]: (s->1o, v->1o) x (out channel 0, 1) */
+    /* SyncBN (the multi-GPU form of the reference's train-mode BatchNorm, models/segnn/segnn.py:233-235,
+     * 257-261, 282-283): when non-NULL and training, the library calls bn_allreduce after each
+     * producing kernel to sum a layer's [3][mul] fp64 BatchNorm sums (sum s, sum s^2 over the 0e
+     * channels, sum |v|^2 over the 1o channels) over every rank, in place, ordered on `stream`
+     * (e.g. an RCCL all-reduce enqueued on it), and normalises by the global counts of
+     * bn_global_batch systems (0: this call's batch).  12 calls per forward at 6 layers.  Requires
+     * the atomic BatchNorm path (mul 96 or 32, 2 <= N <= 16); NBX_E_UNSUPPORTED otherwise. */
+    nbx_allreduce_fn bn_allreduce;
+    void* bn_allreduce_ctx;
+    int64_t bn_global_batch;
     nbx_segnn_layer layers[NBX_SEGNN_MAX_LAYERS];
 } nbx_segnn_weights;
 
@@ -180,12 +199,14 @@ int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* pos, const 
                             void* stream, float* kind_ms, int32_t* kind_launches, double* kind_flops, float* total_ms);
 
 /* Device-resident self-feed rollout (helper_scripts/infer_self_feed.py:99-194,
- * target "pos_dt+vel", force zeroed, mass constant): starting from pos/vel
- * [B,N,3] it runs num_frames-1 model steps; traj_pos/traj_vel [B, num_frames, N, 3]
- * receive frame 0 = the initial state and frame t = the state after t steps.
- * pos/vel are updated to the final state.  No host synchronisation inside. */
+ * force zeroed, mass constant): starting from pos/vel [B,N,3] it runs num_frames-1
+ * model steps; traj_pos/traj_vel [B, num_frames, N, 3] receive frame 0 = the initial
+ * state and frame t = the state after t steps.  flags: 0 (target "pos_dt+vel":
+ * pos += pred[:, :3]) or NBX_ROLLOUT_ABSOLUTE (pos = pred[:, :3]); vel = pred[:, 3:].
+ * pos/vel are updated to the final state.  No host synchronisation inside (except
+ * what a SyncBN hook does). */
 int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass,
-                      int64_t batch_size, int64_t num_nodes, int64_t num_frames,
+                      int64_t batch_size, int64_t num_nodes, int64_t num_frames, int32_t flags,
                       float* traj_pos, float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
 
 
@@ -243,7 +264,7 @@ int nbx_egnn_forward(const nbx_egnn_weights* w, const float* pos, const float* v
  * infer_self_feed.py:161-194 (two heads: pos_dt, vel); same contract as
  * nbx_segnn_rollout. */
 int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
-                     int64_t num_nodes, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                     int64_t num_nodes, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                      size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
@@ -311,7 +332,7 @@ int nbx_ponita_forward_timed(const nbx_ponita_weights* w, const float* pos, cons
 /* Device-resident self-feed rollout with the PONITA branch of
  * infer_self_feed.py:131-147,182-194; same contract as nbx_segnn_rollout. */
 int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
-                       int64_t num_nodes, int64_t num_frames, float* traj_pos, float* traj_vel, void* workspace,
+                       int64_t num_nodes, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                        size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus

@@ -19,7 +19,7 @@ run() {
 for s in $STEPS; do
   case $s in
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run gpu_tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests) run gpu_tests 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py --steps 100 --warmup 10 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o segnn \
                -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;

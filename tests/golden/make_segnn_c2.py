@@ -1,0 +1,73 @@
+"""Generate the C2-size SEGNN rollout fixture from the CPU oracle (build container).
+
+    python tests/golden/make_segnn_c2.py [--frames 11]
+
+C2 = SEGNN lmax_h=1, hidden 192, 6 layers, N=5, B=1024 (BASELINE.json configs[1]).
+Weights: ``torch.manual_seed(0); SEGNN(hidden_features=192, num_layers=6)`` (CPU
+RNG, deterministic for the pinned torch of this image; the fixture stores a
+checksum the test re-verifies).  Initial states: frame 0 of
+``GravitySim(n_balls=5, interaction_strength=2, dt=0.01, softening=0.2)`` with
+seeds 0..1023, the reference's sample_trajectory RNG recipe
+(synthetic_sim.py:357-381).  Rollout: oracle/rollout.py (infer_self_feed.py:99-194)
+in fp64 with train-mode BatchNorm (the reference rollout never calls eval()),
+``--frames`` frames.  The oracle's SEGNN is the e3nn restatement of
+oracle/segnn.py: parity vs e3nn itself is UNPINNED (e3nn is absent).
+
+Output: tests/golden/segnn_c2_rollout.npz (trajectories stored as fp32).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+B, N, HIDDEN, LAYERS = 1024, 5, 192, 6
+
+
+def c2_model():
+    import nbody_amd.segnn as S
+    torch.manual_seed(0)
+    return S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS)
+
+
+def weight_checksum(model):
+    return float(sum(t.double().abs().sum().item() for k, t in model.state_dict().items()))
+
+
+def initial_states():
+    from oracle.gravity import initial_conditions
+    loc = np.empty((B, N, 3))
+    vel = np.empty((B, N, 3))
+    for b in range(B):
+        loc[b], vel[b], _ = initial_conditions(N, b)
+    return loc, vel, np.ones((B, N, 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=11)
+    a = ap.parse_args()
+    from oracle.rollout import rollout, segnn_step
+    from oracle.segnn import SEGNNOracle
+    model = c2_model()
+    params = {k: t.double().numpy().copy() for k, t in model.state_dict().items()}
+    loc, vel, mass = initial_states()
+    om = SEGNNOracle(hidden_features=HIDDEN, num_layers=LAYERS)
+    t0 = time.time()
+    tl, tv = rollout(segnn_step(om, params, training=True), loc, vel, np.zeros_like(loc), mass, a.frames)
+    print(f"oracle rollout of {a.frames - 1} steps: {time.time() - t0:.1f} s")
+    np.savez_compressed(os.path.join(HERE, "segnn_c2_rollout.npz"), loc0=loc, vel0=vel,
+                        traj_loc=tl.astype(np.float32), traj_vel=tv.astype(np.float32),
+                        weight_checksum=np.float64(weight_checksum(model)))
+
+
+if __name__ == "__main__":
+    main()

@@ -70,7 +70,38 @@ def test_struct_layout_matches_header():
     assert [f for f, _ in lib.SegnnWeights._fields_] == wf
     head = 3 * 4 + 2 * 4   # mul, num_layers, training, bn_eps, bn_momentum
     head = (head + 7) // 8 * 8
-    assert ctypes.sizeof(lib.SegnnWeights) == head + w_ptrs * 8 + lib.MAX_LAYERS * layer_ptrs * 8
+    extra = 8 + 8          # bn_allreduce (function pointer), bn_global_batch (int64)
+    assert ctypes.sizeof(lib.SegnnWeights) == head + w_ptrs * 8 + extra + lib.MAX_LAYERS * layer_ptrs * 8
+
+
+def test_struct_offsets_match_the_c_compiler(tmp_path):
+    """Every field offset and struct size of the ctypes mirrors equals what gcc computes
+    from include/nbx.h (the header is plain C)."""
+    import shutil
+    import subprocess
+
+    import nbody_amd._lib as lib
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {"nbx_segnn_layer": lib.SegnnLayer, "nbx_segnn_weights": lib.SegnnWeights,
+               "nbx_egnn_layer": lib.EgnnLayer, "nbx_egnn_head": lib.EgnnHead, "nbx_egnn_weights": lib.EgnnWeights,
+               "nbx_ponita_layer": lib.PonitaLayer, "nbx_ponita_weights": lib.PonitaWeights}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "nbx.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, cls in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
 
 
 def test_product_fails_loudly_without_device():

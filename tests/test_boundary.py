@@ -73,7 +73,7 @@ def fake_trajectories(B, T, N, seed=0):
 def fake_sim(monkeypatch):
     calls = []
 
-    def sample(self, batch_size, T=10000, sample_freq=10, seeds=None):
+    def sample(self, batch_size, T=10000, sample_freq=10, seeds=None, shard=False):
         calls.append((batch_size, T, sample_freq))
         return fake_trajectories(batch_size, T // sample_freq, self.n_balls, seed=len(calls))
     monkeypatch.setattr(D.GravitySim, "sample_trajectory_batch", sample)

@@ -1,9 +1,13 @@
 """GPU parity of the fused SEGNN path (fp32 HIP) against the fp64 CPU oracle.
 
-Tolerance (north_star: "a stated fp32 tolerance"): max |gpu - oracle| <=
-2e-4 * max|oracle| + 1e-5 for one forward; rollouts compare per-frame with a
-budget that grows with the horizon (fp32 rounding is amplified by the
-autoregressive feedback); running BatchNorm statistics to 1e-4 relative."""
+Tolerances (north_star: "a stated fp32 tolerance"):
+* one forward: per output column c, max |gpu - oracle| <= 1e-5 * max|oracle[:, c]| + 1e-7
+  (the kernels measure ~1.2e-6 relative; the bound is ~10x that);
+* rollouts: per-frame relative error budget growing with the horizon (fp32 rounding is
+  amplified by the autoregressive feedback) and north_star's rollout MSE <= 1e-5, checked
+  at the C2 configuration (hidden 192, 6 layers, B=1024) over 10 steps against the fixture
+  tests/golden/segnn_c2_rollout.npz (tests/golden/make_segnn_c2.py);
+* running BatchNorm statistics to 1e-4 relative."""
 import numpy as np
 import pytest
 import torch
@@ -70,6 +74,15 @@ def assert_close(got, ref, rel=2e-4, abs_=1e-5):
     assert err <= rel * scale + abs_, f"max err {err:.3e} vs scale {scale:.3e}"
 
 
+def assert_close_cols(got, ref, rel=1e-5, abs_=1e-7):
+    """Per output column: max |got - ref| <= rel * max |ref[:, c]| + abs_."""
+    got, ref = got.reshape(-1, got.shape[-1]), ref.reshape(-1, ref.shape[-1])
+    err = np.abs(got - ref).max(0)
+    scale = np.abs(ref).max(0)
+    bad = err > rel * scale + abs_
+    assert not bad.any(), f"column errors {err} vs scales {scale} (rel {rel})"
+
+
 @pytest.mark.parametrize("hidden,layers,B,N,training", [
     (16, 1, 2, 5, True), (32, 2, 4, 5, True), (64, 3, 8, 5, False), (192, 6, 16, 5, True),
     (192, 6, 3, 2, True), (24, 2, 3, 7, True), (192, 2, 2, 20, True)])
@@ -80,7 +93,7 @@ def test_forward_matches_oracle(hip_device, hidden, layers, B, N, training):
     pos, vel, mass = states(B, N)
     ref, stats = oracle_forward(model, params, pos, vel, mass, B, N, training)
     got = gpu_forward(model, pos, vel, mass, B, N, hip_device)
-    assert_close(got, ref)
+    assert_close_cols(got, ref)
     if training:   # running statistics updated in place like the train-mode reference module
         sd = model.state_dict()
         for k, v in stats.items():
@@ -94,7 +107,7 @@ def test_forward_c2_full_batch(hip_device):
     B, N = 1024, 5
     pos, vel, mass = states(B, N, seed=3)
     ref, _ = oracle_forward(model, params, pos, vel, mass, B, N, True)
-    assert_close(gpu_forward(model, pos, vel, mass, B, N, hip_device), ref)
+    assert_close_cols(gpu_forward(model, pos, vel, mass, B, N, hip_device), ref)
 
 
 def test_batch_permutation_property(hip_device):
@@ -169,14 +182,63 @@ def test_non_fc_graph_rejected(hip_device):
 
 
 def test_forward_deterministic_c2(hip_device):
-    """Repeated C2 forwards agree (no run-to-run variation from the kernels' LDS hand-offs or
-    MFMA operand staging: that hazard corrupted whole node groups, errors of O(1)).  The BatchNorm
-    statistics are fp64 atomic sums whose arrival order varies, so repeats may differ in the last
-    float bits: the bound is 1e-5 relative to the output scale, far below any corruption."""
+    """Repeated eval-mode C2 forwards are bit-identical (no run-to-run variation from the
+    kernels' LDS hand-offs or MFMA operand staging: that hazard corrupted whole node groups,
+    errors of O(1); eval mode reads no atomic sums, so nothing may vary)."""
     model = make_model(192, 6, hip_device, perturb_bn=False).eval()
     B, N = 1024, 5
     pos, vel, mass = states(B, N, seed=5)
     outs = [gpu_forward(model, pos, vel, mass, B, N, hip_device) for _ in range(3)]
-    scale = np.abs(outs[0]).max()
     for o in outs[1:]:
-        assert np.abs(o - outs[0]).max() <= 1e-5 * scale
+        np.testing.assert_array_equal(o, outs[0])
+
+
+def test_forward_repeat_train_mode_c2(hip_device):
+    """Train-mode C2 forwards agree to the last float bits: the BatchNorm batch statistics are
+    fp64 atomic sums whose arrival order varies (<= 1e-6 relative), far below the O(1)
+    errors of an operand-corruption hazard."""
+    model = make_model(192, 6, hip_device, perturb_bn=False).train()
+    B, N = 1024, 5
+    pos, vel, mass = states(B, N, seed=6)
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    outs = []
+    for _ in range(3):
+        model.load_state_dict(sd0)
+        outs.append(gpu_forward(model, pos, vel, mass, B, N, hip_device))
+    scale = np.abs(outs[0]).max(0)
+    for o in outs[1:]:
+        assert (np.abs(o - outs[0]).max(0) <= 1e-6 * scale).all()
+
+
+def c2_fixture():
+    import os
+    p = os.path.join(os.path.dirname(__file__), "golden", "segnn_c2_rollout.npz")
+    return np.load(p)
+
+
+def test_rollout_c2_matches_oracle_fixture(hip_device):
+    """north_star: rollout MSE <= 1e-5 vs the reference at C2 (hidden 192, 6 layers, N=5,
+    B=1024, train-mode BatchNorm, GravitySim initial states), over a 10-step horizon, against
+    the fp64 oracle rollout of tests/golden/make_segnn_c2.py.  Per-step errors are printed."""
+    import nbody_amd.segnn as S2
+    fx = c2_fixture()
+    torch.manual_seed(0)
+    model = S2.SEGNN(hidden_features=192, num_layers=6)
+    cs = float(sum(t.double().abs().sum().item() for t in model.state_dict().values()))
+    assert abs(cs - float(fx["weight_checksum"])) <= 1e-9 * abs(cs), "C2 weights differ from the fixture's"
+    model = model.to(hip_device).train()
+    rl, rv = fx["traj_loc"].astype(np.float64), fx["traj_vel"].astype(np.float64)
+    T = rl.shape[1]
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = model.rollout(t(fx["loc0"]), t(fx["vel0"]), t(np.ones(fx["loc0"].shape[:2] + (1,))), T)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    mse_steps = []
+    for k in range(1, T):
+        mse = float(((tp[:, k] - rl[:, k]) ** 2).mean())
+        rel = float(np.abs(tp[:, k] - rl[:, k]).max() / np.abs(rl[:, k]).max())
+        mse_steps.append(mse)
+        print(f"C2 rollout step {k}: pos MSE {mse:.3e}, max rel err pos {rel:.3e}, "
+              f"vel {np.abs(tv[:, k] - rv[:, k]).max() / np.abs(rv[:, k]).max():.3e}")
+        assert rel <= 1e-4 * k, (k, rel)
+    assert max(mse_steps) <= 1e-5, mse_steps
+    assert float(((tp - rl) ** 2).mean()) <= 1e-5

@@ -255,3 +255,38 @@ def test_gpu_rollout_equals_repeated_forward(hip_device):
         p, v = p + out[:, :3], out[:, 3:]
         assert torch.equal(tp[:, k].reshape(-1, 3), p)
         assert torch.equal(tv[:, k].reshape(-1, 3), v)
+
+
+@pytest.mark.gpu
+def test_gpu_c3_full_batch_slices_match_oracle(hip_device):
+    """C3 at its full size (hidden 128, 6 layers, 20 orientations, basis 128, B = 4096:
+    838 MB kernel-basis buffer, > 2^31-byte row offsets in the edge-slot arrays): forward and
+    a 3-frame rollout of the whole batch on the device; PONITA has no cross-system coupling,
+    so a 64-system slice from the start, middle and end of the batch is checked against the
+    oracle run on those systems alone."""
+    B, N, T = 4096, 5, 3
+    m = make(128, 6, num_ori=20).to(hip_device)
+    m.eval()
+    rng = np.random.default_rng(5)
+    loc, vel = rng.standard_normal((B, N, 3)), rng.standard_normal((B, N, 3)) * 0.5
+    mass = np.ones((B, N, 1))
+    with torch.no_grad():
+        out = m(gpu_graph(loc, vel, mass, B, N, hip_device)).double().cpu().numpy().reshape(B, N, 6)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = m.rollout(t(loc), t(vel), t(mass), T)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    params = oracle_params(m)
+    grid = m.model.ori_grid.double().cpu().numpy()
+    S = 64
+    ei = fc_edge_index(S, N)
+    for s0 in (0, B // 2 - S // 2, B - S):
+        sl = slice(s0, s0 + S)
+        p, v = loc[sl].reshape(-1, 3), vel[sl].reshape(-1, 3)
+        ref = op.forward(params, mass[sl].reshape(-1, 1), v[:, None, :], ei, p[ei[0]] - p[ei[1]], grid, 6)
+        got = out[sl].reshape(-1, 6)
+        assert np.abs(got - ref).max() <= 2e-4 * np.abs(ref).max() + 1e-6, s0
+        rl, rv = oracle_rollout(ponita_step(params, grid, 6), loc[sl], vel[sl], np.zeros_like(loc[sl]), mass[sl], T)
+        for k in range(T):
+            tol = 2e-4 * (k + 1)
+            assert np.abs(tp[sl, k] - rl[:, k]).max() <= tol * np.abs(rl[:, k]).max() + 1e-6, (s0, k)
+            assert np.abs(tv[sl, k] - rv[:, k]).max() <= tol * np.abs(rv[:, k]).max() + 1e-6, (s0, k)
