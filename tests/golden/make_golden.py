@@ -176,6 +176,31 @@ def make_gravity(ref_mods):
     np.savez_compressed(os.path.join(HERE, "gravity.npz"), **out)
 
 
+def make_cache(ref_mods):
+    """A ground-truth cache file in the reference's format: the list of B
+    ``sample_trajectory`` tuples that GravityDatasetOtf.get_ground_truth_trajectories returns
+    (dataset_gravity_otf.py:91-107), written with the reference's own call
+    ``pickle.dump(data, file)`` (_save_simulations, :118-135) into
+    ``<data_path>/<sha256 of the constructor arguments>/0.pkl`` (:52-56,176-183).  The
+    reference module itself cannot be imported here (matplotlib is absent and importing it
+    creates a directory inside the read-only reference tree), so the folder name is computed
+    by the same json/sha256 rule and the trajectories come from the reference's GravitySim."""
+    import hashlib
+    import json
+    import pickle
+    GravitySim = ref_mods["sim"].GravitySim
+    kw = {"dataset_name": "nbody_small", "target": "pos_dt+vel", "batch_size": 3, "sim_length": 200,
+          "sample_freq": 10, "noise_var": 0, "num_nodes": 5, "vel_norm": 1e-16, "interaction_strength": 2,
+          "dt": 0.01, "softening": 0.2, "double_precision": False, "center_of_mass": False, "lmax_attr": 1}
+    folder = hashlib.sha256(json.dumps(kw, sort_keys=True).encode()).hexdigest()
+    sim = GravitySim(noise_var=0, n_balls=5, vel_norm=1e-16, interaction_strength=2, dt=0.01, softening=0.2)
+    data = [sim.sample_trajectory(200, 10, random_seed=s) for s in (11, 12, 13)]
+    d = os.path.join(HERE, "ref_cache", folder)
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "0.pkl"), "wb") as f:
+        pickle.dump(data, f)
+
+
 def _initial_states(sim_cls, B, N, T=100):
     sim = sim_cls(n_balls=N, interaction_strength=2, dt=0.01, softening=0.2, noise_var=0)
     trajs = [sim.sample_trajectory(T=T, sample_freq=10, random_seed=s) for s in range(B)]
@@ -270,6 +295,7 @@ def make_egnn_mc(ref_mods, Data):
 
 
 def main():
+    sys.dont_write_bytecode = True   # never write __pycache__ into the read-only reference tree
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default=os.environ.get("NBODY_REFERENCE", "/root/reference"))
     ap.add_argument("--only", default=None)
@@ -280,7 +306,7 @@ def main():
         "graph": importlib.import_module("utils.build_fully_connected_graph"),
         "sim": importlib.import_module("datasets.nbody.dataset.synthetic_sim"),
     }
-    jobs = {"graph": make_graph, "gravity": make_gravity}
+    jobs = {"graph": make_graph, "gravity": make_gravity, "cache": make_cache}
     if a.only in (None, "ponita"):
         mods["ponita"] = importlib.import_module("models.ponita.ponita_nbody")
     if a.only in (None, "egnn_mc"):

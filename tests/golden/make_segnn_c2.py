@@ -10,7 +10,10 @@ checksum the test re-verifies).  Initial states: frame 0 of
 seeds 0..1023, the reference's sample_trajectory RNG recipe
 (synthetic_sim.py:357-381).  Rollout: oracle/rollout.py (infer_self_feed.py:99-194)
 in fp64 with train-mode BatchNorm (the reference rollout never calls eval()),
-``--frames`` frames.  The oracle's SEGNN is the e3nn restatement of
+``--frames`` frames, from the fp32-rounded initial states the device path sees; plus
+the same rollout from states moved by one fp32 ulp (the reference's own sensitivity:
+with random-init weights and batch-coupled train-mode BatchNorm the rollout turns
+chaotic within ~5 steps).  The oracle's SEGNN is the e3nn restatement of
 oracle/segnn.py: parity vs e3nn itself is UNPINNED (e3nn is absent).
 
 Output: tests/golden/segnn_c2_rollout.npz (trajectories stored as fp32).
@@ -60,12 +63,21 @@ def main():
     model = c2_model()
     params = {k: t.double().numpy().copy() for k, t in model.state_dict().items()}
     loc, vel, mass = initial_states()
+    # the device path consumes fp32 states: the oracle starts from the same fp32-rounded values
+    loc, vel = loc.astype(np.float32).astype(np.float64), vel.astype(np.float32).astype(np.float64)
     om = SEGNNOracle(hidden_features=HIDDEN, num_layers=LAYERS)
     t0 = time.time()
-    tl, tv = rollout(segnn_step(om, params, training=True), loc, vel, np.zeros_like(loc), mass, a.frames)
+    tl, tv = rollout(segnn_step(om, dict(params), training=True), loc, vel, np.zeros_like(loc), mass, a.frames)
     print(f"oracle rollout of {a.frames - 1} steps: {time.time() - t0:.1f} s")
+    # the reference's own sensitivity: the same fp64 rollout from initial states moved by one
+    # fp32 ulp (another equally valid fp32 rounding of the same physical state)
+    up = lambda x: np.nextafter(x.astype(np.float32), np.float32(np.inf)).astype(np.float64)
+    pl, pv = rollout(segnn_step(om, dict(params), training=True), up(loc), up(vel), np.zeros_like(loc), mass,
+                     a.frames)
+    print(f"perturbed oracle rollout done: {time.time() - t0:.1f} s")
     np.savez_compressed(os.path.join(HERE, "segnn_c2_rollout.npz"), loc0=loc, vel0=vel,
                         traj_loc=tl.astype(np.float32), traj_vel=tv.astype(np.float32),
+                        pert_loc=pl.astype(np.float32), pert_vel=pv.astype(np.float32),
                         weight_checksum=np.float64(weight_checksum(model)))
 
 

@@ -111,6 +111,37 @@ def test_cache_roundtrip_and_getitem_targets(tmp_path, fake_sim):
     assert f0 not in ds2.unused_indices_queue[0]
 
 
+def test_cache_interchange_with_reference_written_file(tmp_path):
+    """A cache written in the reference's format (tests/golden/make_golden.py make_cache: the
+    reference GravitySim's trajectories, pickled with the reference's own pickle.dump call into
+    the sha256-named folder) is found and loaded by our GravityDatasetOtf(use_cached=True); and a
+    cache we write reads back through the stdlib pickle the reference uses
+    (dataset_gravity_otf.py:118-167)."""
+    import shutil
+    src = os.path.join(os.path.dirname(__file__), "golden", "ref_cache")
+    shutil.copytree(src, tmp_path / "saved_simulations")
+    ds = D.GravityDatasetOtf(batch_size=3, sim_length=200, num_nodes=5, device="cpu", use_cached=True,
+                             data_path=str(tmp_path / "saved_simulations"))
+    assert ds.cache_index == 1                      # loaded 0.pkl, did not regenerate
+    batch = ds.data_queue[0]
+    assert len(batch) == 3
+    for pos, vel, force, mass in batch:
+        assert pos.shape == vel.shape == force.shape == (20, 5, 3) and mass.shape == (5, 1)
+        np.testing.assert_allclose(force, np.asarray(
+            __import__("oracle.gravity", fromlist=["x"]).compute_acceleration(pos, mass, 2.0, 0.2)) * mass,
+            rtol=1e-12, atol=1e-12)
+    loc, vel, force, mass, y = ds[0]
+    assert loc.shape == (3, 5, 3) and y.shape == (3, 5, 6)
+    out = tmp_path / "ours.pkl"
+    D.save_cached_simulations(str(out), batch)
+    with open(out, "rb") as f:
+        back = pickle.load(f)
+    assert isinstance(back, list) and all(isinstance(t, tuple) and len(t) == 4 for t in back)
+    for ta, tb in zip(back, batch):
+        for xa, xb in zip(ta, tb):
+            np.testing.assert_array_equal(xa, xb)
+
+
 def test_cache_loader_refuses_code(tmp_path):
     class Evil:
         def __reduce__(self):

@@ -79,6 +79,7 @@ def test_rollout_absolute_target(hip_device, kind):
     model = small_model(kind, hip_device)
     if kind == "ponita":
         model.eval()   # no calibration: the rollout and the forwards see the same weights
+        model.model.materialize()
     rng = np.random.default_rng(1)
     loc = torch.tensor(rng.standard_normal((B, N, 3)), dtype=torch.float32, device=hip_device)
     vel = torch.tensor(rng.standard_normal((B, N, 3)), dtype=torch.float32, device=hip_device)
