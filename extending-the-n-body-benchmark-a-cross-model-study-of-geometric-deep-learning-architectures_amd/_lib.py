@@ -83,6 +83,7 @@ _SIGNATURES = {
     "nbx_gravity_sample": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_d, c_d, c_d,
                                           c_p, c_p, c_p, c_p]),
     "nbx_nbody_energies": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_i64, c_d, c_d, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_ks_2samp_stat": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),

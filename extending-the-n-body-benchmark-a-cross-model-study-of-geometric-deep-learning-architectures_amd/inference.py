@@ -277,4 +277,32 @@ class SelfFeedTrainer:
         G, soft = float(sim.interaction_strength), float(sim.softening)
         self.last_energies = {"simulation": self._compute_nbody_energies(locs[0], vels[0], G, soft),
                               "self_feed": self._compute_nbody_energies(locs[1], vels[1], G, soft)}
+        self.self_feed_postprocess_common(energies=self.last_energies, steps_survived=steps,
+                                          save_dir=f"{self.save_dir_path}/checkpoints/{self.step_count}",
+                                          metrics_filename="nbody_macro_metrics.json")
         return steps
+
+    def self_feed_postprocess_common(self, *, energies, steps_survived, save_dir,
+                                     metrics_filename="nbody_macro_metrics.json"):
+        """trainer.py:668-779 for the N-body energies: steps within the energy-ratio
+        thresholds, KS p-values of the energy series (device statistics, ks.py) and their
+        Fisher combination, persisted as ``metrics_filename`` in the reference's JSON layout.
+        W&B logging and plotting are outside the native scope; the results are kept in
+        ``self.last_macros``."""
+        from .ks import energy_steps_within, macro_pvalues
+        os.makedirs(save_dir, exist_ok=True)
+        steps_metric = energy_steps_within(energies["simulation"]["total"], energies["self_feed"]["total"])
+        print("Self feed energy within " + "| ".join(f"{t * 100:.0f}%: {n} steps" for t, n in steps_metric.items()))
+        pvals, p_combined = macro_pvalues(energies)
+        f = lambda v: float(v) if v == v else float("nan")
+        to_json = {
+            "energies": {f"{src}_{k}": np.asarray(energies[side][k]).tolist()
+                         for src, side in (("simulation", "simulation"), ("self_feed", "self_feed"))
+                         for k in ("total", "potential", "kinetic")},
+            "ks_pvalues": {**{k: f(v) for k, v in pvals.items()}, "combined": f(p_combined)},
+        }
+        with open(os.path.join(save_dir, metrics_filename), "w") as fh:
+            json.dump(to_json, fh)
+        self.last_macros = {"steps_within": steps_metric, "ks_pvalues": pvals, "ks_combined": p_combined,
+                            "steps_survived": int(steps_survived)}
+        return steps_metric

@@ -79,6 +79,16 @@ int nbx_nbody_energies(const double* loc, const double* vel, int64_t batch_size,
                        int64_t num_nodes, double G, double softening, double* kinetic, double* potential,
                        double* mean_kinetic, double* mean_potential, void* stream);
 
+/* Self-feed macro statistics (utils/ks_utils.py:7-17 `_ks_p`, driven by
+ * trainer.py:668-722): for each of num_pairs pairs (a[p, :na], b[p, :nb]) (rows lda / ldb
+ * doubles apart, device memory) the two-sample Kolmogorov-Smirnov statistic of the non-NaN
+ * values, D = max_x |F_a(x) - F_b(x)| with F(x) = #{<= x} / n over every sample (scipy
+ * ks_2samp's statistic, bit-exact) -> d_out[p] (NaN if either side has no numbers) and, if
+ * n_out is non-NULL, the non-NaN counts n_out[2p], n_out[2p+1].  One workgroup per pair;
+ * na, nb <= 8192.  The p-value is a host-side function of (D, n_a, n_b). */
+int nbx_ks_2samp_stat(const double* a, int64_t na, int64_t lda, const double* b, int64_t nb, int64_t ldb,
+                      int64_t num_pairs, double* d_out, int64_t* n_out, void* stream);
+
 /* ------------------------------------------------------------------------
  * SEGNN (models/segnn/segnn.py:17-304, o3_building_blocks.py:10-278) — fp32.
  *

@@ -203,6 +203,7 @@ class FullyConnectedTP:
         for (i1, i2, io, (m1, m2, mo)), W, c in zip(self.instructions, self.weight_views(w), self.coeffs):
             d1, d2, do = self.irreps_in1[i1][1].dim, self.irreps_in2[i2][1].dim, self.irreps_out[io][1].dim
             C = wigner_3j(self.irreps_in1[i1][1].l, self.irreps_in2[i2][1].l, self.irreps_out[io][1].l)
+            C = C.astype(out.dtype)      # fp32 runs stay in fp32 (the C2 fixture's fp32 reference)
             a = x1[:, s1[i1]].reshape(Z, m1, d1)
             b = x2[:, s2[i2]].reshape(Z, m2, d2)
             # t[z,u,v,k] = sum_ij a[z,u,i] b[z,v,j] C[i,j,k]

@@ -57,7 +57,7 @@ class O3TP:
         if x2 is None:
             x2 = np.ones((x1.shape[0], 1), dtype=x1.dtype)
         out = self.tp(x1, x2, p[prefix + "tp.weight"])
-        out = out / self.sqrt_k_correction
+        out = out / self.sqrt_k_correction.astype(out.dtype)
         if len(self.bias_idx):
             out[:, self.bias_idx] += p[prefix + "biases"]
         return out

@@ -13,7 +13,8 @@ in fp64 with train-mode BatchNorm (the reference rollout never calls eval()),
 ``--frames`` frames, from the fp32-rounded initial states the device path sees; plus
 the same rollout from states moved by one fp32 ulp (the reference's own sensitivity:
 with random-init weights and batch-coupled train-mode BatchNorm the rollout turns
-chaotic within ~5 steps).  The oracle's SEGNN is the e3nn restatement of
+chaotic within ~5 steps), and the oracle rollout computed entirely in fp32 arithmetic (the
+scale of error fp32 rounding alone produces).  The oracle's SEGNN is the e3nn restatement of
 oracle/segnn.py: parity vs e3nn itself is UNPINNED (e3nn is absent).
 
 Output: tests/golden/segnn_c2_rollout.npz (trajectories stored as fp32).
@@ -75,9 +76,17 @@ def main():
     pl, pv = rollout(segnn_step(om, dict(params), training=True), up(loc), up(vel), np.zeros_like(loc), mass,
                      a.frames)
     print(f"perturbed oracle rollout done: {time.time() - t0:.1f} s")
+    # and the same oracle computed entirely in fp32 arithmetic: how far fp32 rounding alone
+    # takes this rollout from the fp64 one (the scale of any fp32 implementation's error)
+    p32 = {k: v.astype(np.float32) for k, v in params.items()}
+    f32 = lambda x: x.astype(np.float32)
+    fl, fv = rollout(segnn_step(om, p32, training=True), f32(loc), f32(vel), f32(np.zeros_like(loc)), f32(mass),
+                     a.frames)
+    print(f"fp32 oracle rollout done: {time.time() - t0:.1f} s, dtype {fl.dtype}")
     np.savez_compressed(os.path.join(HERE, "segnn_c2_rollout.npz"), loc0=loc, vel0=vel,
                         traj_loc=tl.astype(np.float32), traj_vel=tv.astype(np.float32),
                         pert_loc=pl.astype(np.float32), pert_vel=pv.astype(np.float32),
+                        f32_loc=fl.astype(np.float32), f32_vel=fv.astype(np.float32),
                         weight_checksum=np.float64(weight_checksum(model)))
 
 
