@@ -14,10 +14,9 @@
 // Fragment maps and the in-chunk K permutation are those of tp_fused.h.
 #pragma once
 #include "nbx_internal.h"
+#include "tp_fused.h"   // bf16x3 split helpers, LDS-DMA image staging
 
 namespace nbx {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 enum LinAct : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
 enum LinEpi : int { LIN_STORE = 0, LIN_CONV = 1 };
@@ -36,6 +35,10 @@ struct LinProb {
     int rows, N, Ktot;  // Ktot = sum of seg[].K
     const float* Wt;    // [N][ldw]  (columns of the concatenated K)
     int ldw;
+    // optional split-precision (bf16x3) image of Wt (include/nbx.h "bf16x3 images", CW = 32, one
+    // sub-tile): [N/32 column tiles][Ktot/32 chunks][part 3][m 2][lane 64][8] bf16; when set (and N %
+    // 32 == 0) lin_auto runs the PREC = 1 kernel: fp32-accurate products on v_mfma_f32_32x32x16_bf16
+    const void* Wx3;
     const float* bias;  // [N] or null
     float* Y;           // [rows][ldy] (may be null when only the row dot is wanted)
     int ldy;
@@ -66,7 +69,15 @@ __device__ inline float lin_act(float x, int act) {
     }
 }
 
-template <int NT, int ACT, int EPI = LIN_STORE>
+// PREC 0: fp32 v_mfma_f32_32x32x2_f32 with the Wt slice staged row-major (pitch 32k + 4).
+// PREC 1: the split-precision path (tp_fused.h StatSKX3): the block's NT column tiles of the bf16x3
+// image are copied verbatim into LDS by LDS-DMA; every A chunk is split into hi + mid + lo bf16 as
+// it is consumed (once per chunk, shared by the NT column tiles) and each 32 x 32 x 32 block is
+// the fp32 sum of the six leading cross products on v_mfma_f32_32x32x16_bf16 (12 x 32 cycles
+// instead of 16 x 64).
+constexpr int LIN_X3_BLK = 1536;   // floats of one (column tile, 32-deep chunk) bf16x3 block
+
+template <int NT, int ACT, int EPI = LIN_STORE, int PREC = 0>
 __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int chunk = blockIdx.x / P.blocks_per_chunk;
@@ -74,9 +85,16 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
     const int pitch = ((P.Ktot + 31) & ~31) + 4;
     const int n0 = chunk * NT * 32;
+    const int n_chunks = P.Ktot >> 5;
 
-    // ---- stage Wt[n0 : n0 + NT*32, :] in LDS
-    {
+    if constexpr (PREC == 1) {
+        // ---- stage the block's column tiles of the bf16x3 image (contiguous) in LDS
+        const int tiles = min(NT, (P.N >> 5) - chunk * NT);
+        tp_dma_image<LIN_WAVES>(reinterpret_cast<const float*>(P.Wx3) + (size_t)chunk * NT * n_chunks * LIN_X3_BLK,
+                                lds, tiles * n_chunks * LIN_X3_BLK);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        // ---- stage Wt[n0 : n0 + NT*32, :] in LDS
         const int q4 = pitch / 4;
         for (int i = t; i < NT * 32 * q4; i += LIN_THREADS) {
             const int row = i / q4, kq = (i - row * q4) * 4;
@@ -88,7 +106,6 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     }
     __syncthreads();
 
-    const int n_chunks = P.Ktot >> 5;
     const int row_tiles = (P.rows + 31) >> 5;
     const int wstride = P.blocks_per_chunk * LIN_WAVES;
 
@@ -159,6 +176,29 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
         auto consume = [&](const float4 (&cur)[4], int k0) {
+            if constexpr (PREC == 1) {
+                // lane (r, h) holds k = 16 h + 4 q + e of the chunk; MFMA m takes k = 16 h + 8 m + j
+                bf16x8 a[3][2];
+                tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
+                tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+                const bf16x8* ldsx = reinterpret_cast<const bf16x8*>(lds);
+                const int kc = k0 >> 5;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const bf16x8* bp = ldsx + (j * n_chunks + kc) * (LIN_X3_BLK / 4) + lane;
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {   // block [part p][m][lane][8]: smallest terms first
+                        const bf16x8 b0 = bp[m * 64], b1 = bp[(2 + m) * 64], b2 = bp[(4 + m) * 64];
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b0, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b1, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b2, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b0, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b1, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b0, acc[j], 0, 0, 0);
+                    }
+                }
+                return;
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float4 b4[NT];
@@ -297,11 +337,20 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     }
 }
 
-template <int NT, int ACT, int EPI = LIN_STORE>
+// LDS bytes of a block's weight slice: fp32 rows with pitch, or NT bf16x3 column tiles
+inline size_t lin_lds_bytes(int nt, int Ktot, int prec) {
+    return prec ? (size_t)nt * (Ktot >> 5) * LIN_X3_BLK * 4 : (size_t)nt * 32 * (((Ktot + 31) & ~31) + 4) * 4;
+}
+
+template <int NT, int ACT, int EPI = LIN_STORE, int PREC = 0>
 int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     if (p.rows <= 0 || p.N <= 0) return NBX_OK;
     if (p.Ktot % 32) {
         set_error("lin: Ktot must be a multiple of 32 (got %d)", p.Ktot);
+        return NBX_E_INVAL;
+    }
+    if (PREC == 1 && (!p.Wx3 || p.N % 32)) {
+        set_error("lin: the split-precision path needs a bf16x3 image and N %% 32 == 0");
         return NBX_E_INVAL;
     }
     for (int s = 0; s < p.nseg; ++s)   // buffer-load offsets are 32-bit, OOB sentinel at 2 GiB
@@ -309,7 +358,7 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
             set_error("lin: segment %d spans >= 2 GiB", s);
             return NBX_E_UNSUPPORTED;
         }
-    const size_t lds = (size_t)NT * 32 * ((((p.Ktot + 31) & ~31) + 4)) * 4;
+    const size_t lds = lin_lds_bytes(NT, p.Ktot, PREC);
     if (lds > 160 * 1024) {
         set_error("lin: weight slice needs %zu bytes of LDS", lds);
         return NBX_E_UNSUPPORTED;
@@ -326,11 +375,11 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     p.blocks_per_chunk = bpc;
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT, EPI>,
+        NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT, EPI, PREC>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((lin_kernel<NT, ACT, EPI>), dim3(p.chunks * bpc), dim3(LIN_THREADS), lds, st, p);
+    hipLaunchKernelGGL((lin_kernel<NT, ACT, EPI, PREC>), dim3(p.chunks * bpc), dim3(LIN_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

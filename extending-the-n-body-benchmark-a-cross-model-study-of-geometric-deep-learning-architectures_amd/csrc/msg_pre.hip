@@ -1,4 +1,6 @@
 // Fused message_layer_1 kernel (see msg_pre.h for the algorithm and data layout).
+#include <cstdlib>
+
 #include "msg_pre.h"
 #include "tp16.h"
 
@@ -31,7 +33,19 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
     const bool gemm_wave = wave < 4;
     const int plane = wave & 3;
     const unsigned long long c_start = P.dbg ? clock64() : 0ull;
-    const int chunk = blockIdx.x % P.chunks, pblk = blockIdx.x / P.chunks;
+    // XCD-aware block order (P.xcd_group): consecutive block ids go to different XCDs (round robin
+    // over 8), so block b runs on XCD b % 8; the `chunks` blocks that share a node slab pblk are
+    // given ids with the same b % 8, so the slab's X rows are fetched into one XCD's L2 once and
+    // hit there for the other chunks (instead of one L2 miss stream per chunk)
+    int chunk, pblk;
+    if (P.xcd_group) {
+        const int xcd = blockIdx.x & 7, s = blockIdx.x >> 3;
+        chunk = s % P.chunks;
+        pblk = (s / P.chunks) * 8 + xcd;
+    } else {
+        chunk = blockIdx.x % P.chunks;
+        pblk = blockIdx.x / P.chunks;
+    }
     const int my_groups = pblk < P.n_slabs ? (P.n_slabs - 1 - pblk) / P.per_chunk + 1 : 0;
     const int KC = (M + 31) >> 5;
     const int lg = __builtin_ctz((unsigned)G);
@@ -325,6 +339,10 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
     if (per < 1) per = 1;
     const int rounds = (p.n_slabs + per - 1) / per;
     per = (p.n_slabs + rounds - 1) / rounds;
+    // XCD grouping needs per_chunk % 8 == 0 (NBX_MP_XCD=0: the plain chunk-major order, A/B only)
+    static const bool xcd = !(getenv("NBX_MP_XCD") && getenv("NBX_MP_XCD")[0] == '0');
+    p.xcd_group = xcd ? 1 : 0;
+    if (xcd) per = (per + 7) / 8 * 8;
     p.per_chunk = per;
     const size_t lds = msg_pre_lds_bytes(p);
     if (lds > 160 * 1024) {

@@ -19,6 +19,7 @@
 //             X  = X + s * (GELU(XN W1' + b1) W2' + b2)                (MFMA, residual epilogue)
 //             RO += X Wro_l' + bro_l                                   (readout, 2 channels)
 //   out     : sum_o (RO / #readouts)[v,o,c] * ori_o / O  -> [V, 6]
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 
@@ -301,11 +302,27 @@ size_t po_carve(PoWs* ws, void* base, const PoDims& d) {
 
 inline int kp(int k) { return (k + 31) & ~31; }
 
-// widest column tile whose weight slice fits the LDS
+// widest column tile whose weight slice fits the LDS; the split-precision (bf16x3) kernel when the
+// layer carries an image (NBX_PO_X3=0: fp32 MFMA path, A/B only)
+bool po_x3_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NBX_PO_X3");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 template <int ACT, int EPI = nbx::LIN_STORE>
 int lin_auto(nbx::LinProb& p, hipStream_t st) {
-    auto lds = [&](int nt) { return (size_t)nt * 32 * (kp(p.Ktot) + 4) * 4; };
     const int need = (p.N + 31) / 32;
+    if (p.Wx3 && po_x3_enabled() && p.N % 32 == 0) {
+        auto lds = [&](int nt) { return nbx::lin_lds_bytes(nt, p.Ktot, 1); };
+        if (need >= 3 && lds(4) <= 160 * 1024) return nbx::lin_launch<4, ACT, EPI, 1>(p, st);
+        if (need >= 2 && lds(2) <= 160 * 1024) return nbx::lin_launch<2, ACT, EPI, 1>(p, st);
+        if (lds(1) <= 160 * 1024) return nbx::lin_launch<1, ACT, EPI, 1>(p, st);
+    }
+    auto lds = [&](int nt) { return nbx::lin_lds_bytes(nt, p.Ktot, 0); };
     if (need >= 3 && lds(4) <= 160 * 1024) return nbx::lin_launch<4, ACT, EPI>(p, st);
     if (need >= 2 && lds(2) <= 160 * 1024) return nbx::lin_launch<2, ACT, EPI>(p, st);
     return nbx::lin_launch<1, ACT, EPI>(p, st);
@@ -336,6 +353,7 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
                                 [&] { return lin_auto<nbx::ACT_GELU>(p, st); }))
             return rc;
         LinProb q = nbx::lin_dense(ws.B1H1, C, C, (int)d.R, w->basis2_t, kp(C), Bk, w->basis2_b, ws.KB, Bk);
+        q.Wx3 = w->basis2_img_x3;
         if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * C * Bk, Ev * f4 * (C + Bk),
                                 [&] { return lin_auto<nbx::ACT_GELU>(q, st); }))
             return rc;
@@ -354,6 +372,7 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             hipLaunchKernelGGL(po_moments_kernel, dim3(512), dim3(256), 0, st, ws.X, VO * C, mom + 6 * l);
         {   // spatial conv: X1[(d,o)] = sum_q (KB Wk')[(d,o,q)] * X[(src,o)]
             LinProb p = nbx::lin_dense(ws.KB, Bk, Bk, (int)d.R, Ly.kernel_t, kp(Bk), C, nullptr, ws.X1, C);
+            p.Wx3 = Ly.kernel_img_x3;
             p.conv_G = (int)d.G;
             p.conv_O = O;
             p.conv_nodes = (int)d.N;
@@ -392,10 +411,12 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
         }
         {   // ConvNext MLP with the residual in the epilogue
             LinProb p = nbx::lin_dense(ws.XN, C, C, (int)VO, Ly.lin1_t, kp(C), d.mlp, Ly.lin1_b, ws.B1H1, d.mlp);
+            p.Wx3 = Ly.lin1_img_x3;
             if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * VO * C * d.mlp, (double)VO * f4 * (C + d.mlp),
                                     [&] { return lin_auto<nbx::ACT_GELU>(p, st); }))
                 return rc;
             LinProb q = nbx::lin_dense(ws.B1H1, d.mlp, d.mlp, (int)VO, Ly.lin2_t, kp(d.mlp), C, Ly.lin2_b, ws.X, C);
+            q.Wx3 = Ly.lin2_img_x3;
             q.resid = ws.X;
             q.ldr = C;
             q.scale = Ly.layer_scale;

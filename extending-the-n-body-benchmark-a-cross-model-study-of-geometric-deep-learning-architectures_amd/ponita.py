@@ -237,7 +237,21 @@ class PONITA_NBODY(nn.Module):
                 P[p + "layer_scale"] = vec(L.layer_scale)
             if R is not None:
                 P[p + "readout_w"], P[p + "readout_b"] = vec(R.weight), vec(R.bias)
+        # split-precision (bf16x3) images of the large GEMMs' weights (include/nbx.h "bf16x3
+        # images", CW = 32, one sub-tile): fp32-accurate products at 2.7x the fp32 MFMA rate
+        for key, name in [("basis2_t", "basis2_img_x3")] + [
+                (f"layers.{i}.{k}_t", f"layers.{i}.{k}_img_x3") for i in range(len(m.interaction_layers))
+                for k in ("kernel", "lin1", "lin2")]:
+            W = P[key]
+            if W.shape[0] % 32 == 0:
+                P[name] = self.lin_image_x3(W)
         return P
+
+    @staticmethod
+    def lin_image_x3(W):
+        """[N][Kp] (Kp % 32 == 0, N % 32 == 0) -> int16 bf16x3 image [N/32][Kp/32][3][2][64][8]."""
+        from .segnn import SEGNN
+        return SEGNN.frag_image_x3([(W, W.shape[1])], None, W.shape[0] // 32, 32)
 
     def pack_weights(self, device):
         P = self.packed_matrices(device)
@@ -248,6 +262,7 @@ class PONITA_NBODY(nn.Module):
         for name in ("ori_grid", "basis1_t", "basis1_b", "basis2_t", "basis2_b", "fbasis1_t", "fbasis1_b",
                      "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w"):
             setattr(W, name, P[name].data_ptr())
+        W.basis2_img_x3 = P["basis2_img_x3"].data_ptr() if "basis2_img_x3" in P else None
         for i in range(W.num_layers):
             L = W.layers[i]
             for name, _ in L._fields_:

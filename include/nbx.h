@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 4
+#define NBX_ABI_VERSION 5
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -304,6 +304,11 @@ typedef struct nbx_ponita_layer {
     const float* lin2_t; const float* lin2_b;   /* linear_2 */
     const float* layer_scale;         /* [C] or NULL */
     const float* readout_w; const float* readout_b;  /* read_out_layers[i] or NULL */
+    /* optional bf16x3 images of kernel_t / lin1_t / lin2_t (NULL: fp32 MFMA path): the
+     * "bf16x3 images" layout with CW = 32 and one sub-tile, [N/32][K/32][3][2][64][8] bf16 */
+    const void* kernel_img_x3;
+    const void* lin1_img_x3;
+    const void* lin2_img_x3;
 } nbx_ponita_layer;
 
 typedef struct nbx_ponita_weights {
@@ -315,6 +320,7 @@ typedef struct nbx_ponita_weights {
     const float* fbasis2_t; const float* fbasis2_b;
     const float* fiber_t;
     const float* embed_w;
+    const void* basis2_img_x3;   /* optional bf16x3 image of basis2_t (as the layer images) */
     nbx_ponita_layer layers[NBX_PONITA_MAX_LAYERS];
 } nbx_ponita_weights;
 

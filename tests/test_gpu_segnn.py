@@ -224,13 +224,15 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
     With random-init weights this rollout turns chaotic within a few steps (bodies are flung to
     |pos| ~ 50-75 and pairs pass within ~1e-3 of each other, where r-hat is ill-conditioned;
     train-mode BatchNorm couples every system to the outliers).  The fixture therefore also holds
-    the reference's own sensitivity: the same fp64 rollout from initial states one fp32 ulp away.
+    the same oracle rollout computed entirely in fp32 arithmetic (the divergence fp32 rounding
+    alone produces) and from states one fp32 ulp away (the reference's own sensitivity).
     Checks, per step k:
-      * MSE(device, oracle) <= 1e-5 over the predictable horizon, i.e. every step where the
-        reference's own one-ulp sensitivity is <= 1e-7;
-      * beyond it, the device stays as close to the oracle as the oracle is to itself under a
-        one-ulp input change (MSE <= 10x the sensitivity MSE, or <= 1e-5).
-    Per-step errors are printed."""
+      * MSE(device, oracle) <= 1e-5 (north_star) over the predictable horizon: every step where
+        the fp32 oracle itself stays within MSE 1e-7 of the fp64 one;
+      * beyond it, the device stays as close to the fp64 oracle as an fp32 computation of the same
+        algorithm does: MSE <= 10x the fp32-oracle MSE (or <= 1e-5).
+    Per-step errors are printed (measured: the device is 10-70x closer to fp64 than the fp32
+    oracle over steps 1-5)."""
     import nbody_amd.segnn as S2
     fx = c2_fixture()
     torch.manual_seed(0)
@@ -239,7 +241,7 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
     assert abs(cs - float(fx["weight_checksum"])) <= 1e-9 * abs(cs), "C2 weights differ from the fixture's"
     model = model.to(hip_device).train()
     rl, rv = fx["traj_loc"].astype(np.float64), fx["traj_vel"].astype(np.float64)
-    pl = fx["pert_loc"].astype(np.float64)
+    fl, pl = fx["f32_loc"].astype(np.float64), fx["pert_loc"].astype(np.float64)
     T = rl.shape[1]
     t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
     tp, tv = model.rollout(t(fx["loc0"]), t(fx["vel0"]), t(np.ones(fx["loc0"].shape[:2] + (1,))), T)
@@ -247,15 +249,16 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
     horizon = 0
     for k in range(1, T):
         mse = float(((tp[:, k] - rl[:, k]) ** 2).mean())
+        f32 = float(((fl[:, k] - rl[:, k]) ** 2).mean())
         sens = float(((pl[:, k] - rl[:, k]) ** 2).mean())
         sys_err = np.abs(tp[:, k] - rl[:, k]).reshape(tp.shape[0], -1).max(1) / np.abs(rl[:, k]).max()
-        print(f"C2 rollout step {k}: pos MSE {mse:.3e} (oracle one-ulp sensitivity {sens:.3e}), max rel err pos "
-              f"{sys_err.max():.3e} (median over systems {np.median(sys_err):.3e}), vel "
+        print(f"C2 rollout step {k}: pos MSE {mse:.3e} (fp32 oracle {f32:.3e}, one-ulp input change {sens:.3e}), "
+              f"max rel err pos {sys_err.max():.3e} (median over systems {np.median(sys_err):.3e}), vel "
               f"{np.abs(tv[:, k] - rv[:, k]).max() / np.abs(rv[:, k]).max():.3e}")
-        if sens <= 1e-7 and horizon == k - 1:
+        if f32 <= 1e-7 and horizon == k - 1:
             horizon = k
             assert mse <= 1e-5, (k, mse)
         else:
-            assert mse <= max(1e-5, 10.0 * sens), (k, mse, sens)
-    print(f"C2 predictable horizon (oracle sensitivity <= 1e-7): {horizon} steps")
+            assert mse <= max(1e-5, 10.0 * f32), (k, mse, f32)
+    print(f"C2 predictable horizon (fp32 oracle within MSE 1e-7 of fp64): {horizon} steps")
     assert horizon >= 4
