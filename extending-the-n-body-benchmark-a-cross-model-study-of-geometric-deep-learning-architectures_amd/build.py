@@ -13,6 +13,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ISA_DIR = os.path.join(HERE, "lib", "isa")   # device assembly of every object (hazard check, inspection)
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "lib")
 # NBX_BUILD_TAG: a side build (lib/libnbx_<tag>.so, loaded with NBX_LIB=...) for A/B timing only
@@ -21,7 +22,7 @@ OBJ_DIR = os.path.join(HERE, "lib", "obj" + (f"_{_TAG}" if _TAG else ""))
 LIB = os.path.join(OUT_DIR, f"libnbx_{_TAG}.so" if _TAG else "libnbx.so")
 ARCH = os.environ.get("NBX_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
-         "-munsafe-fp-atomics"]
+         "-munsafe-fp-atomics", "-save-temps=obj"]
 # per-file extra flags: the split-precision MFMA kernels' VALU work (operand splits, the message
 # kernel's edge combination) runs beside MFMAs, where packed fp32 VALU costs extra cycles; with
 # SLP vectorisation off these files run 1.8 % more steps/s (measured, C2).
@@ -70,9 +71,38 @@ def build(jobs: int = 8, verbose: bool = False, force: bool = False) -> str:
         for err in ex.map(run, cmds):
             if verbose and err:
                 print(err, file=sys.stderr)
+    _keep_device_asm()
     if cmds or not os.path.exists(LIB) or _needs(LIB, objs):
         run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
+    check_isa()
     return LIB
+
+
+def _keep_device_asm():
+    """-save-temps=obj leaves every compilation stage next to the objects: keep the device
+    assembly (lib/isa/*.s) and drop the rest."""
+    os.makedirs(ISA_DIR, exist_ok=True)
+    for f in os.listdir(OBJ_DIR):
+        p = os.path.join(OBJ_DIR, f)
+        if f.endswith(f"-{ARCH}.s") and "-hip-amdgcn-" in f:
+            os.replace(p, os.path.join(ISA_DIR, f))
+        elif not f.endswith(".o") or "-hip-amdgcn-" in f or "-host-" in f:
+            os.remove(p)
+
+
+def check_isa():
+    """The gfx950 hazard ROCm 7.2 does not pad (DESIGN.md "gfx950 MFMA SrcA hazard"): a load
+    issued right after a v_mfma_f32_16x16x32_bf16 into that MFMA's SrcA registers.  Any
+    occurrence in the built kernels fails the build."""
+    import glob as _g
+    from importlib import import_module
+    scan = import_module(__package__ + ".isa_scan" if __package__ else "isa_scan").scan
+    hits = [h for f in sorted(_g.glob(os.path.join(ISA_DIR, "*.s"))) for h in scan(f, 1, rule=True)]
+    if hits:
+        msg = "\n".join(f"{os.path.basename(p)}:{no} [{fn}] {ld} <- SrcA of line {pno}: {mf}"
+                        for p, fn, no, ld, pno, mf, _, _ in hits)
+        raise RuntimeError("gfx950 MFMA SrcA hazard in the built kernels (a load into the SrcA registers of the "
+                           "v_mfma_f32_16x16x32_bf16 issued just before it):\n" + msg)
 
 
 if __name__ == "__main__":

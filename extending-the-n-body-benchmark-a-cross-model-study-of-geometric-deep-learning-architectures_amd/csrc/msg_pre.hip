@@ -323,7 +323,7 @@ inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
 
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
     if (p.V <= 0) return NBX_OK;
-    if (p.M > 128 || p.NG <= 0) {
+    if (p.M > 128 || p.NG <= 0 || (p.x3 && p.M > 96)) {   // x3: two bf16x3 images + exchange fit LDS up to mul 96
         set_error("msg_pre: needs mul <= 128 and 2 <= N <= 16 (got mul %d, N %d)", p.M, p.N);
         return NBX_E_UNSUPPORTED;
     }
@@ -354,7 +354,7 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024));
         for (const void* k : {(const void*)msg_pre_kernel<true, 1>, (const void*)msg_pre_kernel<true, 2>,
-                              (const void*)msg_pre_kernel<true, 3>, (const void*)msg_pre_kernel<true, 4>})
+                              (const void*)msg_pre_kernel<true, 3>})
             NBX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
@@ -365,8 +365,6 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         NBX_TIMED_LAUNCH((msg_pre_kernel<true, 1>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     else if (p.x3 && kct == 2)
         NBX_TIMED_LAUNCH((msg_pre_kernel<true, 2>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
-    else if (p.x3)
-        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 4>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     else
         NBX_TIMED_LAUNCH(msg_pre_kernel<false>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());

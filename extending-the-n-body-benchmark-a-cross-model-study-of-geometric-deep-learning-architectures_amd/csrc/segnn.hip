@@ -935,7 +935,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                                     Lp.feat_bn_running_var, ws.coef_feat, cnt_nodes, w->bn_eps, w->bn_momentum,
                                     w->training, 1};
             }
-            if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && x3_enabled() && !getenv("NBX_X3_NOMP")) {
+            // split-precision node GEMM when its two bf16x3 images and the exchange buffers fit the
+            // LDS (mul <= 96); wider layers run the fp32 MFMA node GEMM
+            if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && x3_enabled() && M <= 96 && !getenv("NBX_X3_NOMP")) {
                 mp.Simg = static_cast<const float*>(L.node_pre_s_img_x3);
                 mp.Vimg = static_cast<const float*>(L.node_pre_v_img_x3);
                 mp.x3 = 1;

@@ -391,8 +391,9 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                     // fragment (lane quarter qd: k = 8 qd + j) is exactly the chunk a lane loads.
                     // Item u's B fragments are read from LDS while item u-1's MFMAs run, into a
                     // register set that stays allocated (empty asm uses) until item u+1's MFMAs have
-                    // issued: a register is never refilled while an MFMA reading it may be pending
-                    // (msg_pre.hip: LDS returns overwriting a pending MFMA's operands corrupted data).
+                    // issued, so no load lands on the operands of an MFMA issued just before it
+                    // (the measured gfx950 hazard is a load into the SrcA of the preceding
+                    // v_mfma_f32_16x16x32_bf16 at 0 wait states; build.py checks the ISA for it).
                     constexpr int OB[4] = {0, SK::K0, SK::K0 + SK::K1, SK::K0 + SK::K1 + SK::K2};
                     constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
                     auto read_b = [&](auto ic, bf16x8 (&bx)[CG][NS > 1 ? NS : 1][3]) {
@@ -484,8 +485,10 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                             }
                             __builtin_amdgcn_sched_barrier(0);
                         });
-                        // the last item's operands: a pad for its MFMAs, then free
-                        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+                        // the last item's operands are free after one wait state: the gfx950 hazard
+                        // (DESIGN.md "gfx950 MFMA SrcA hazard", tools/hazard/mfma_war.hip) is a load
+                        // into the SrcA of the v_mfma_f32_16x16x32_bf16 issued in the slot before it
+                        asm volatile("s_nop 0" ::: "memory");
                         static_for<0, PF - 1>([&](auto uc) {
                             constexpr int u = decltype(uc)::value;
                             if constexpr (u < n) load_item(std::integral_constant<int, lo + u>{}, next_rt, ring[u % PF]);

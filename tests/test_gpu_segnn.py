@@ -262,3 +262,19 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
             assert mse <= max(1e-5, 10.0 * f32), (k, mse, f32)
     print(f"C2 predictable horizon (fp32 oracle within MSE 1e-7 of fp64): {horizon} steps")
     assert horizon >= 4
+
+
+def test_forward_mul128_repeats_and_matches_oracle(hip_device):
+    """mul = 128 (hidden 256): the msg_pre_kernel<true, 4> instantiation (four 32-deep K chunks),
+    where ROCm 7.2 scheduled a ds_read into the SrcA registers of the v_mfma_f32_16x16x32_bf16 it
+    had just issued (0 wait states; DESIGN.md "gfx950 MFMA SrcA hazard").  Eval-mode repeats must
+    be bit-identical and a forward must match the oracle per column."""
+    model = make_model(256, 2, hip_device, perturb_bn=False).eval()
+    B, N = 1024, 5
+    pos, vel, mass = states(B, N, seed=9)
+    outs = [gpu_forward(model, pos, vel, mass, B, N, hip_device) for _ in range(4)]
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+    Bs = 24
+    ref, _ = oracle_forward(model, params_of(model), pos[:Bs * N], vel[:Bs * N], mass[:Bs * N], Bs, N, False)
+    assert_close_cols(gpu_forward(model, pos[:Bs * N], vel[:Bs * N], mass[:Bs * N], Bs, N, hip_device), ref)
