@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 5
+ABI_VERSION = 6
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
@@ -75,6 +75,34 @@ class PonitaWeights(ctypes.Structure):
         ("layers", PonitaLayer * PONITA_MAX_LAYERS)]
 
 
+EQV2_MAX_LAYERS = 32
+
+
+class Eqv2Radial(ctypes.Structure):
+    _fields_ = [(n, c_p) for n in ("a", "c", "us", "ut", "ln1_w", "ln1_b", "w1", "b1", "ln2_w", "ln2_b", "w2_x3", "w2",
+                                   "b2")]
+
+
+class Eqv2Attn(ctypes.Structure):
+    _fields_ = [("rad", Eqv2Radial)] + [(n, c_p) for n in (
+        "fc0_x3", "fc0_b", "fc1_x3", "c20_x3", "c20_b", "c21_x3", "alpha_norm_w", "alpha_norm_b", "alpha_dot",
+        "proj_t", "proj_b")]
+
+
+class Eqv2Block(ctypes.Structure):
+    _fields_ = [("norm1_w", c_p), ("norm1_b", c_p), ("ga", Eqv2Attn)] + [(n, c_p) for n in (
+        "norm2_w", "norm2_b", "gate_t", "gate_b", "lin1_t", "lin1_b", "lin2_t", "lin2_b")]
+
+
+class Eqv2Weights(ctypes.Structure):
+    _fields_ = [(n, c_i32) for n in ("sphere_channels", "attn_hidden", "num_heads", "alpha_channels", "value_channels",
+                                     "ffn_hidden", "edge_channels", "num_layers", "num_elements")] + [
+        (n, c_p) for n in ("grid_attn_to", "grid_attn_from", "grid_ffn_to", "grid_ffn_from", "sphere_emb", "vel_t",
+                           "vel_b")] + [
+        ("edge_degree", Eqv2Radial), ("norm_w", c_p), ("norm_b", c_p), ("force", Eqv2Attn),
+        ("blocks", Eqv2Block * EQV2_MAX_LAYERS)]
+
+
 _SIGNATURES = {
     "nbx_abi_version": (ctypes.c_int, []),
     "nbx_last_error": (ctypes.c_char_p, []),
@@ -106,6 +134,11 @@ _SIGNATURES = {
                                                 ctypes.POINTER(c_f)]),
     "nbx_ponita_rollout": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
                                           c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_eqv2_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "nbx_eqv2_forward": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_p, c_p, c_p, c_i64, c_i64, c_p, ctypes.c_uint64,
+                                        c_p, c_p, c_sz, c_p]),
+    "nbx_eqv2_rollout": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
+                                        ctypes.c_uint64, c_p, c_p, c_p, c_sz, c_p]),
 }
 
 _lib = None

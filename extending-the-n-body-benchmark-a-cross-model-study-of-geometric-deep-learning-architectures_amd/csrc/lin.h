@@ -19,7 +19,7 @@
 namespace nbx {
 
 enum LinAct : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
-enum LinEpi : int { LIN_STORE = 0, LIN_CONV = 1 };
+enum LinEpi : int { LIN_STORE = 0, LIN_CONV = 1, LIN_EQMSG = 2 };
 
 struct LinSeg {
     const float* ptr;   // segment base
@@ -56,6 +56,16 @@ struct LinProb {
     int conv_ldx;
     int blocks_per_chunk;
     int chunks;         // ceil(N / (NT*32))
+    // LIN_EQMSG (EquiformerV2 SO(2)-conv input, eqv2.hip): rows are edges of fully-connected systems of
+    // eq_nodes nodes; the block's 5 column tiles are the radial-function outputs of one 32-channel block
+    // of the message [x_src | x_dst] for the 5 groups (m=0: l=0,1,2; m=1: l=1,2).  The epilogue rotates
+    // the gathered node irreps into the edge frame (eq_rot: R rows, D^2 rows m=-1,0,1) and writes
+    // rad * message to eq_a0 [rows][3 * 2C] (m = 0) and eq_a1 [2 rows][2 * 2C] (m = +1 row, m = -1 row).
+    const float* eq_x;  // [V][9][C]
+    const float* eq_rot;
+    float* eq_a0;
+    float* eq_a1;
+    int eq_C, eq_nodes;
 };
 
 constexpr int LIN_WAVES = 8, LIN_THREADS = 64 * LIN_WAVES;
@@ -241,7 +251,49 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
             }
         }
         // ---- epilogue: col = n0 + 32 j + r; row = rt*32 + (e&3) + 8(e>>2) + 4h
-        if constexpr (EPI == LIN_CONV) {
+        if constexpr (EPI == LIN_EQMSG) {
+            static_assert(NT == 5, "LIN_EQMSG: one block = the 5 groups of one 32-channel block");
+            const int C = P.eq_C, C2 = 2 * C, NN = P.eq_nodes, deg = NN - 1, per = NN * deg;
+            const int ch = chunk * 32 + r;                  // message channel (< C: source node, else target)
+            const bool tgt = ch >= C;
+            const int cc = tgt ? ch - C : ch;
+            float bb[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bb[j] = P.bias[n0 + 32 * j + r];
+#pragma unroll 2
+            for (int e = 0; e < 16; ++e) {
+                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (row >= P.rows) continue;
+                const int b = row / per, rr = row - b * per, i = rr / deg, jj = rr - i * deg;
+                const int node = b * NN + (tgt ? (jj < i ? jj : jj + 1) : i);
+                const float* xp = P.eq_x + (size_t)node * 9 * C + cc;
+                float x[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) x[k] = xp[k * C];
+                const float* D = P.eq_rot + (size_t)row * 32;
+                const float m0 = x[0];
+                const float m1 = D[3] * x[1] + D[4] * x[2] + D[5] * x[3];
+                const float re1 = D[6] * x[1] + D[7] * x[2] + D[8] * x[3];
+                const float im1 = D[0] * x[1] + D[1] * x[2] + D[2] * x[3];
+                float im2 = 0.f, m2 = 0.f, re2 = 0.f;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    im2 += D[9 + k] * x[4 + k];
+                    m2 += D[14 + k] * x[4 + k];
+                    re2 += D[19 + k] * x[4 + k];
+                }
+                float* a0 = P.eq_a0 + (size_t)row * 3 * C2 + ch;
+                a0[0] = (acc[0][e] + bb[0]) * m0;
+                a0[C2] = (acc[1][e] + bb[1]) * m1;
+                a0[2 * C2] = (acc[2][e] + bb[2]) * m2;
+                const float r3 = acc[3][e] + bb[3], r4 = acc[4][e] + bb[4];
+                float* a1 = P.eq_a1 + (size_t)row * 4 * C2 + ch;
+                a1[0] = r3 * re1;
+                a1[C2] = r4 * re2;
+                a1[2 * C2] = r3 * im1;
+                a1[3 * C2] = r4 * im2;
+            }
+        } else if constexpr (EPI == LIN_CONV) {
             const int G = P.conv_G, O = P.conv_O, NN = P.conv_nodes;
             // gathered source row offset of each accumulator row (-1: padded slot / past the end),
             // shared by all NT column sub-tiles

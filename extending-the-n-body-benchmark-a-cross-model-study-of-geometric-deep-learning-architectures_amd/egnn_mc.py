@@ -106,7 +106,7 @@ class EGNNMultiChannel(nn.Module):
         return self.hidden_node_dim
 
     # ------------------------------------------------------------ packing
-    def _version(self):
+    def _param_version(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def packed_matrices(self, device, dtype=torch.float32):
@@ -173,13 +173,13 @@ class EGNNMultiChannel(nn.Module):
         for t in range(len(self.heads)):
             for name, _ in W.heads[t]._fields_:
                 setattr(W.heads[t], name, P[f"heads.{t}.{name}"].data_ptr())
-        self._packed = (self._version(), W, P)
+        self._packed = (self._param_version(), W, P)
         return W
 
     def _weights(self, device):
         if self._native_reason:
             raise NotImplementedError(self._native_reason)
-        if self._packed is None or self._packed[0] != self._version():
+        if self._packed is None or self._packed[0] != self._param_version():
             self.pack_weights(device)
         return self._packed[1]
 

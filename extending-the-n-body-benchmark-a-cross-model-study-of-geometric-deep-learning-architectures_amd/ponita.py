@@ -203,7 +203,7 @@ class PONITA_NBODY(nn.Module):
         return self.hidden_dim
 
     # ------------------------------------------------------------ packing
-    def _version(self):
+    def _param_version(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters()) + (
             self.model.ori_grid.data_ptr(), self.model.ori_grid._version)
 
@@ -268,14 +268,14 @@ class PONITA_NBODY(nn.Module):
             for name, _ in L._fields_:
                 t = P.get(f"layers.{i}.{name}")
                 setattr(L, name, t.data_ptr() if t is not None else None)
-        self._packed = (self._version(), W, P)
+        self._packed = (self._param_version(), W, P)
         return W
 
     def _weights(self, device):
         if self._native_reason:
             raise NotImplementedError(self._native_reason)
         self.model.materialize()
-        if self._packed is None or self._packed[0] != self._version():
+        if self._packed is None or self._packed[0] != self._param_version():
             self.pack_weights(device)
         return self._packed[1]
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 5
+#define NBX_ABI_VERSION 6
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -350,6 +350,94 @@ int nbx_ponita_forward_timed(const nbx_ponita_weights* w, const float* pos, cons
 int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
                        int64_t num_nodes, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                        size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * EquiformerV2 (models/equiformer_v2/architecture/equiformer_v2_nbody.py:57-575 on the tuple
+ * branch of helper_scripts/infer_self_feed.py:178-181, eval mode) — fp32.
+ *
+ * Scope: lmax_list = [2], mmax_list = [1] (one resolution), norm_type "rms_norm_sh",
+ * distance_function "projection", use_atom_edge_embedding (not shared), use_m_share_rad False,
+ * separable S2 activations, sphere_channels C in {32, 64}, attn_hidden H and ffn_hidden F in {32, 64},
+ * edge_channels He in {32, 64}, num_heads * attn_alpha_channels <= 64 (alpha <= 16),
+ * num_heads * attn_value_channels in {8, 16, 32}, fully-connected systems of N <= 64 nodes.
+ * Atomic numbers are (int) mass, clamped to [0, num_elements).
+ *
+ * Radial functions (RadialFunction [1024 + 2 He, He, He, R]) are passed with their first Linear
+ * folded over the input it sees: x_edge = [distance_expansion(d) | source_emb[z_s] | target_emb[z_t]]
+ * (an affine function of d plus two table lookups), so h1 = d * a + c + us[z_s] + ut[z_t]:
+ *   a = W0[:, :1024] w_de, c = W0[:, :1024] b_de + b0, us = (W0[:, 1024:1024+He] E_s^T)^T [Z][He],
+ *   ut likewise.  The last Linear (He -> R) is a bf16x3 image (CW = 32, "bf16x3 images" above) of
+ * its weight with rows permuted: attention radials R = 10 C, output column
+ * n = 160 cb + 32 g + i <- original row g * 2C + 32 cb + i (g = 0..4 = m0 l0, m0 l1, m0 l2, m1 l1,
+ * m1 l2; cb = 32-channel block of the message [x_src | x_dst]); bias permuted alike.  The edge-degree
+ * radial (R = 3 C) keeps its row order and is a plain fp32 matrix [3C][He].
+ * GEMM images (*_x3) are bf16x3 images of nn.Linear weights [out][in] with out zero-padded to a
+ * multiple of 32 (biases padded alike).  Node-side matrices are stored input-major ("_t": [in][out]):
+ *   proj_t [3][nh nv][Cout], gate_t [C][F], lin1_t [3][C][F], lin2_t [3][F][C], vel_t [3][3C].
+ * Grids: SO3_Grid(2, 1) (attention) and SO3_Grid(2, 2) (FFN) to/from matrices [points][coeffs]
+ * (so3.py:543-618; 18 x 7 and 42 x 9).
+ */
+#define NBX_EQV2_MAX_LAYERS 32
+
+typedef struct nbx_eqv2_radial {
+    const float* a; const float* c;        /* [He] */
+    const float* us; const float* ut;      /* [num_elements][He] */
+    const float* ln1_w; const float* ln1_b;
+    const float* w1; const float* b1;      /* net.3 [He][He] (nn.Linear layout), [He] */
+    const float* ln2_w; const float* ln2_b;
+    const void* w2_x3;                     /* net.6 image (attention radials, permuted), or NULL */
+    const float* w2;                       /* net.6 [R][He] fp32 (edge-degree radial) */
+    const float* b2;                       /* [R] */
+} nbx_eqv2_radial;
+
+typedef struct nbx_eqv2_attn {             /* SO2EquivariantGraphAttention */
+    nbx_eqv2_radial rad;                   /* so2_conv_1.rad_func (with this module's atom embeddings) */
+    const void* fc0_x3; const float* fc0_b;  /* so2_conv_1.fc_m0 [nh na + H + 3 H][3 * 2C] */
+    const void* fc1_x3;                      /* so2_conv_1.so2_m_conv.0.fc [4H][2 * 2C] */
+    const void* c20_x3; const float* c20_b;  /* so2_conv_2.fc_m0 [3 nh nv][3H] */
+    const void* c21_x3;                      /* so2_conv_2.so2_m_conv.0.fc [4 nh nv][2H] */
+    const float* alpha_norm_w; const float* alpha_norm_b;   /* [na] */
+    const float* alpha_dot;                  /* [nh][na] */
+    const float* proj_t; const float* proj_b;  /* proj (SO3_LinearV2) [3][nh nv][Cout], [Cout] */
+} nbx_eqv2_attn;
+
+typedef struct nbx_eqv2_block {            /* TransBlockV2 */
+    const float* norm1_w; const float* norm1_b;   /* [3][C], [C] */
+    nbx_eqv2_attn ga;
+    const float* norm2_w; const float* norm2_b;
+    const float* gate_t; const float* gate_b;     /* ffn.gating_linear */
+    const float* lin1_t; const float* lin1_b;     /* ffn.so3_linear_1 */
+    const float* lin2_t; const float* lin2_b;     /* ffn.so3_linear_2 */
+} nbx_eqv2_block;
+
+typedef struct nbx_eqv2_weights {
+    int32_t sphere_channels, attn_hidden, num_heads, alpha_channels, value_channels, ffn_hidden,
+        edge_channels, num_layers, num_elements;
+    const float* grid_attn_to; const float* grid_attn_from;   /* [18][7] */
+    const float* grid_ffn_to; const float* grid_ffn_from;     /* [42][9] */
+    const float* sphere_emb;                  /* [num_elements][C] */
+    const float* vel_t; const float* vel_b;   /* velocity_embedding [3][3C], [3C] */
+    nbx_eqv2_radial edge_degree;              /* R = 3C (m = 0 coefficients of l = 0, 1, 2) */
+    const float* norm_w; const float* norm_b; /* final norm */
+    nbx_eqv2_attn force;                      /* force_block (Cout = 2) */
+    nbx_eqv2_block blocks[NBX_EQV2_MAX_LAYERS];
+} nbx_eqv2_weights;
+
+int nbx_eqv2_workspace_bytes(const nbx_eqv2_weights* w, int64_t batch_size, int64_t num_nodes, size_t* bytes);
+
+/* EquiformerV2_nbody.forward((pos, vel, force, mass, pos), batch): pos/vel [B*N,3], mass [B*N] ->
+ * out [B*N, 6] (delta pos | vel).  init_edge_rot_mat (edge_rot_mat.py:21) draws one random vector per
+ * edge; `gauge` supplies them (fp32 [E][3], uniform [0,1), E = B*N*(N-1) in the fully-connected
+ * order) or, when NULL, they are drawn on the device from a counter-based hash of (seed, edge). */
+int nbx_eqv2_forward(const nbx_eqv2_weights* w, const float* pos, const float* vel, const float* mass,
+                     int64_t batch_size, int64_t num_nodes, const float* gauge, uint64_t seed, float* out,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* Device-resident self-feed rollout through the tuple branch (infer_self_feed.py:99-194), same
+ * contract as nbx_segnn_rollout; step t draws its gauges from the hash of (seed, t, edge). */
+int nbx_eqv2_rollout(const nbx_eqv2_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
+                     int64_t num_nodes, int64_t num_frames, int32_t flags, uint64_t seed, float* traj_pos,
+                     float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

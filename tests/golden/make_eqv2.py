@@ -207,6 +207,16 @@ def main():
     out["roll/gauge"] = torch.stack(gauge.record).numpy()
     out["roll/loc"], out["roll/vel"] = torch.stack(L, 1).numpy(), torch.stack(V, 1).numpy()
 
+    # ---- the reference's seeded initialisation (torch.manual_seed(0), C4 widths): per parameter the
+    # first values and the float64 sum, to pin the RNG consumption order of the module tree
+    torch.manual_seed(0)
+    ref = mod.EquiformerV2_nbody(device="cpu", **C4)
+    names = [k for k, _ in ref.named_parameters()]
+    out["seed0/names"] = np.array(names)
+    out["seed0/head"] = np.stack([np.pad(p.detach().reshape(-1)[:4].double().numpy(), (0, 4 - min(4, p.numel())))
+                                  for _, p in ref.named_parameters()])
+    out["seed0/sum"] = np.array([p.detach().double().sum().item() for _, p in ref.named_parameters()])
+
     np.savez_compressed(os.path.join(HERE, "eqv2.npz"), **out)
     with open(os.path.join(HERE, "eqv2_state.json"), "w") as f:
         json.dump(state, f, indent=1, sort_keys=True)

@@ -85,7 +85,9 @@ def test_struct_offsets_match_the_c_compiler(tmp_path):
         pytest.skip("gcc not available")
     structs = {"nbx_segnn_layer": lib.SegnnLayer, "nbx_segnn_weights": lib.SegnnWeights,
                "nbx_egnn_layer": lib.EgnnLayer, "nbx_egnn_head": lib.EgnnHead, "nbx_egnn_weights": lib.EgnnWeights,
-               "nbx_ponita_layer": lib.PonitaLayer, "nbx_ponita_weights": lib.PonitaWeights}
+               "nbx_ponita_layer": lib.PonitaLayer, "nbx_ponita_weights": lib.PonitaWeights,
+               "nbx_eqv2_radial": lib.Eqv2Radial, "nbx_eqv2_attn": lib.Eqv2Attn, "nbx_eqv2_block": lib.Eqv2Block,
+               "nbx_eqv2_weights": lib.Eqv2Weights}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "nbx.h"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
