@@ -31,10 +31,10 @@ namespace {
 constexpr int ROT = 32;                              // floats per edge record
 constexpr float kAvgDegree = 23.395238876342773f;    // equiformer_v2_nbody.py:36
 constexpr float kRescale2 = 1.2909944487358056f;     // sqrt(5 / 3): get_rotate_inv_rescale, l = 2 > mmax = 1
-constexpr int NODE_WAVES = 4;
 constexpr int GA = 18, GF = 42;                      // SO3_Grid(2,1): 6 x 3 points; SO3_Grid(2,2): 6 x 7
 
-__device__ inline float silu(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (1 ulp) instead of an IEEE division sequence
+__device__ inline float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 __device__ inline float wave_sum(float v) {
 #pragma unroll
@@ -127,39 +127,27 @@ __global__ void eqv2_edge_kernel(const float* __restrict__ pos, const float* __r
     out[24] = dist;
 }
 
-// ---- RadialFunction up to the second hidden layer (radial_function.py:5-32), first Linear folded:
-// h1 = SiLU(LN(d a + c + us[z_src] + ut[z_dst])), H2 = SiLU(LN(W1 h1 + b1)).  One wave per edge,
-// lane = channel; W1's row of the lane stays in registers across the wave's edges.
+// ---- RadialFunction first hidden layer (radial_function.py:5-32), first Linear folded:
+// H1 = SiLU(LN(d a + c + us[z_src] + ut[z_dst])).  One wave per edge, lane = channel.  The second
+// hidden layer (Linear + LN + SiLU) is a GEMM with the LIN_LNSILU epilogue (lin.h).
 template <int HE>
 __global__ __launch_bounds__(256) void eqv2_radial_kernel(const float* __restrict__ rot, const int* __restrict__ zn,
                                                          const nbx_eqv2_radial W, int64_t E, int N,
-                                                         float* __restrict__ H2) {
+                                                         float* __restrict__ H1) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool on = lane < HE;
     const int c = on ? lane : 0;
-    float w1[HE];
-#pragma unroll
-    for (int k = 0; k < HE; ++k) w1[k] = W.w1[c * HE + k];
-    const float a = W.a[c], cc = W.c[c], g1 = W.ln1_w[c], bb1 = W.ln1_b[c], b1 = W.b1[c], g2 = W.ln2_w[c],
-                bb2 = W.ln2_b[c];
+    const float a = W.a[c], cc = W.c[c], g1 = W.ln1_w[c], bb1 = W.ln1_b[c];
     const float inv = 1.0f / HE;
     for (int64_t e = blockIdx.x * 4 + wave; e < E; e += (int64_t)gridDim.x * 4) {
         int64_t s, t;
         edge_nodes(e, N, s, t);
         const float d = rot[e * ROT + 24];
-        float v = on ? d * a + cc + W.us[zn[s] * HE + c] + W.ut[zn[t] * HE + c] : 0.f;
-        float mu = wave_sum(v) * inv;
-        float dv = on ? v - mu : 0.f;
-        float var = wave_sum(dv * dv) * inv;
-        const float h = on ? silu(dv / sqrtf(var + 1e-5f) * g1 + bb1) : 0.f;
-        float y = b1;
-#pragma unroll
-        for (int k = 0; k < HE; ++k) y += w1[k] * __shfl(h, k);
-        y = on ? y : 0.f;
-        mu = wave_sum(y) * inv;
-        dv = on ? y - mu : 0.f;
-        var = wave_sum(dv * dv) * inv;
-        if (on) H2[e * HE + c] = silu(dv / sqrtf(var + 1e-5f) * g2 + bb2);
+        const float v = on ? d * a + cc + W.us[zn[s] * HE + c] + W.ut[zn[t] * HE + c] : 0.f;
+        const float mu = wave_sum(v) * inv;
+        const float dv = on ? v - mu : 0.f;
+        const float var = wave_sum(dv * dv) * inv;
+        if (on) H1[e * HE + c] = silu(dv / sqrtf(var + 1e-5f) * g1 + bb1);
     }
 }
 
@@ -177,65 +165,66 @@ struct S2Args {
 };
 
 __global__ __launch_bounds__(256) void eqv2_s2act_kernel(const S2Args A) {
-    __shared__ float gt[GA * 7], gf[GA * 7];
-    for (int i = threadIdx.x; i < GA * 7; i += blockDim.x) {
-        gt[i] = A.gto[i];
-        gf[i] = A.gfrom[i];
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // one thread per (edge, hidden channel); the grid matrices are read with uniform addresses
+    // (scalar loads, SGPR operands): no LDS traffic in the 18-point loop
+    const float* __restrict__ gt = A.gto;
+    const float* __restrict__ gf = A.gfrom;
     const int H = A.H, ex = A.nh * A.na;
-    for (int64_t e = blockIdx.x * 4 + wave; e < A.E; e += (int64_t)gridDim.x * 4) {
-        const float* y0 = A.Y0 + e * A.ld0;
-        const float* yr = A.Y1 + 2 * e * 4 * H;
-        const float* yi = yr + 4 * H;
-        if (lane < H) {
-            const int h = lane;
-            float v[7];
-            v[0] = y0[ex + H + h];
-            v[2] = y0[ex + 2 * H + h];
-            v[5] = y0[ex + 3 * H + h];
-            v[3] = yr[h] - yi[2 * H + h];            // m = +1, l = 1
-            v[6] = yr[H + h] - yi[3 * H + h];        // m = +1, l = 2
-            v[1] = yi[h] + yr[2 * H + h];            // m = -1, l = 1
-            v[4] = yi[H + h] + yr[3 * H + h];        // m = -1, l = 2
-            float o[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t e = gid / H;
+    const int h = (int)(gid - e * H);
+    if (e >= A.E) return;
+    const float* y0 = A.Y0 + e * A.ld0;
+    const float* yr = A.Y1 + 2 * e * 4 * H;
+    const float* yi = yr + 4 * H;
+    float v[7];
+    v[0] = y0[ex + H + h];
+    v[2] = y0[ex + 2 * H + h];
+    v[5] = y0[ex + 3 * H + h];
+    v[3] = yr[h] - yi[2 * H + h];            // m = +1, l = 1
+    v[6] = yr[H + h] - yi[3 * H + h];        // m = +1, l = 2
+    v[1] = yi[h] + yr[2 * H + h];            // m = -1, l = 1
+    v[4] = yi[H + h] + yr[3 * H + h];        // m = -1, l = 2
+    const float gate = y0[ex + h];
+    float o[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int p = 0; p < GA; ++p) {
-                float gv = 0.f;
+    for (int p = 0; p < GA; ++p) {
+        float gv = 0.f;
 #pragma unroll
-                for (int i = 0; i < 7; ++i) gv += gt[p * 7 + i] * v[i];
-                const float sg = silu(gv);
+        for (int i = 0; i < 7; ++i) gv += gt[p * 7 + i] * v[i];
+        const float sg = silu(gv);
 #pragma unroll
-                for (int i = 0; i < 7; ++i) o[i] += gf[p * 7 + i] * sg;
-            }
-            o[0] = silu(y0[ex + h]);
-            float* z0 = A.Z0 + e * 3 * H + h;
-            z0[0] = o[0];
-            z0[H] = o[2];
-            z0[2 * H] = o[5];
-            float* z1 = A.Z1 + 2 * e * 2 * H + h;
-            z1[0] = o[3];
-            z1[H] = o[6];
-            z1[2 * H] = o[1];
-            z1[3 * H] = o[4];
+        for (int i = 0; i < 7; ++i) o[i] += gf[p * 7 + i] * sg;
+    }
+    o[0] = silu(gate);
+    float* z0 = A.Z0 + e * 3 * H + h;
+    z0[0] = o[0];
+    z0[H] = o[2];
+    z0[2 * H] = o[5];
+    float* z1 = A.Z1 + 2 * e * 2 * H + h;
+    z1[0] = o[3];
+    z1[H] = o[6];
+    z1[2 * H] = o[1];
+    z1[3 * H] = o[4];
+    if (h < A.nh) {   // alpha_norm (LayerNorm), SmoothLeakyReLU(0.2), alpha_dot for head h
+        const float* xa = y0 + h * A.na;
+        float xs[16];
+        float mu = 0.f;
+        for (int k = 0; k < A.na; ++k) {
+            xs[k] = xa[k];
+            mu += xs[k];
         }
-        if (lane < A.nh) {   // alpha_norm (LayerNorm), SmoothLeakyReLU(0.2), alpha_dot
-            const float* xa = y0 + lane * A.na;
-            float mu = 0.f;
-            for (int k = 0; k < A.na; ++k) mu += xa[k];
-            mu /= A.na;
-            float var = 0.f;
-            for (int k = 0; k < A.na; ++k) var += (xa[k] - mu) * (xa[k] - mu);
-            const float rs = 1.0f / sqrtf(var / A.na + 1e-5f);
-            float lg = 0.f;
-            for (int k = 0; k < A.na; ++k) {
-                const float y = (xa[k] - mu) * rs * A.an_w[k] + A.an_b[k];
-                const float sg = 1.0f / (1.0f + __expf(-y));
-                lg += (0.6f * y + 0.4f * y * (2.0f * sg - 1.0f)) * A.adot[lane * A.na + k];
-            }
-            A.L[e * A.nh + lane] = lg;
+        mu /= A.na;
+        float var = 0.f;
+        for (int k = 0; k < A.na; ++k) var += (xs[k] - mu) * (xs[k] - mu);
+        const float rs = 1.0f / sqrtf(var / A.na + 1e-5f);
+        float lg = 0.f;
+        for (int k = 0; k < A.na; ++k) {
+            const float y = (xs[k] - mu) * rs * A.an_w[k] + A.an_b[k];
+            const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+            lg += (0.6f * y + 0.4f * y * (2.0f * sg - 1.0f)) * A.adot[h * A.na + k];
         }
+        A.L[e * A.nh + h] = lg;
     }
 }
 
@@ -282,16 +271,20 @@ __device__ inline void rms_norm(const float (&x)[9], float (&y)[9], const float*
 }
 
 template <int MODE>
-__global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeArgs A) {
-    __shared__ float s_alpha[NODE_WAVES][64 * 8];
-    __shared__ float s_vec[NODE_WAVES][9 * 64];
-    __shared__ float s_vec2[NODE_WAVES][9 * 64];
+__global__ __launch_bounds__(64) void eqv2_node_kernel(const NodeArgs A) {
+    // one single-wave workgroup per node (lane = channel): enough waves in flight to hide the
+    // gathers; the per-node weight reads come from L2
+    __shared__ float s_alpha[64 * 8];
+    __shared__ float s_vec[9 * 64];
+    __shared__ float s_vec2[9 * 64];
     __shared__ float s_gt[GF * 9], s_gf[GF * 9];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x;
     const int C = A.C, F = A.F, N = A.N, deg = N - 1;
-    const int64_t sys = blockIdx.x;
+    const int64_t node = blockIdx.x;
+    const int64_t sys = node / N;
+    const int t = (int)(node - sys * N);
     if (MODE == NODE_BLOCK) {
-        for (int i = threadIdx.x; i < GF * 9; i += blockDim.x) {
+        for (int i = lane; i < GF * 9; i += 64) {
             s_gt[i] = A.gto[i];
             s_gf[i] = A.gfrom[i];
         }
@@ -299,10 +292,8 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeAr
     __syncthreads();
     const int c = lane < C ? lane : 0;
     const bool on = lane < C;
-    for (int t0 = 0; t0 < N; t0 += NODE_WAVES) {
-        const int t = t0 + wave;
-        const bool active = t < N;
-        const int64_t node = sys * N + (active ? t : 0);
+    const bool active = true;
+    {
         auto edge_of = [&](int q) -> int64_t {   // q-th incoming edge of node t (source q' != t)
             const int s = q < t ? q : q + 1;
             return sys * N * deg + (int64_t)s * deg + (t < s ? t : t - 1);
@@ -336,7 +327,7 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeAr
         } else {
             // ---- attention: softmax over the N-1 incoming edges per head
             const int KV = A.nh * A.nv;
-            float* sal = s_alpha[wave];
+            float* sal = s_alpha;
             if (active && lane < A.nh) {
                 float mx = -INFINITY;
                 for (int q = 0; q < deg; ++q) mx = fmaxf(mx, A.L[edge_of(q) * A.nh + lane]);
@@ -375,7 +366,7 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeAr
 #pragma unroll
             for (int i = 0; i < 9; ++i)
                 for (int o = KV; o < 64; o <<= 1) agg[i] += __shfl_xor(agg[i], o);
-            float* sag = s_vec[wave];
+            float* sag = s_vec;
             if (lane < KV)
 #pragma unroll
                 for (int i = 0; i < 9; ++i) sag[i * KV + lane] = agg[i];
@@ -397,9 +388,9 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeAr
             y[0] += A.proj_b[co];
             if (MODE == NODE_FORCE) {
                 // pred = proj output: channel 0 l = 1 -> delta pos, channel 1 l = 1 -> vel
-                if (active && lane < 2)
+                if (lane < 2)
                     for (int j = 0; j < 3; ++j) A.out[node * 6 + 3 * lane + j] = y[1 + j];
-                continue;
+                return;
             }
             const float* xo = A.X + node * 9 * C + c;
 #pragma unroll
@@ -407,7 +398,7 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeAr
             // ---- norm_2 + FFN
             float xn[9];
             rms_norm(x, xn, A.norm2_w, A.norm2_b, c, on, C);
-            float* sx = s_vec[wave];
+            float* sx = s_vec;
             __syncthreads();
             if (on)
 #pragma unroll
@@ -440,7 +431,7 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void eqv2_node_kernel(const NodeAr
                 for (int i = 0; i < 9; ++i) o[i] += s_gf[p * 9 + i] * sg;
             }
             o[0] = silu(gate);
-            float* sa = s_vec2[wave];
+            float* sa = s_vec2;
             if (fon)
 #pragma unroll
                 for (int i = 0; i < 9; ++i) sa[i * F + f] = o[i];
@@ -519,13 +510,21 @@ size_t eqv2_carve(EqWs* ws, void* base, const nbx_eqv2_weights* w, int64_t B, in
 unsigned g1(int64_t n) { return (unsigned)nbx::ceil_div(n > 0 ? n : 1, 256); }
 unsigned gwave(int64_t n) { return (unsigned)std::min<int64_t>(nbx::ceil_div(n > 0 ? n : 1, 4), 8192); }
 
+// H2 = SiLU(LN(W1 SiLU(LN(h1_pre)) + b1)): the per-edge first layer, then an MFMA GEMM with the
+// LayerNorm + SiLU epilogue (He = 32 or 64 columns: one column chunk).  H1 lives in the A0 buffer.
 int radial(const nbx_eqv2_weights* w, const nbx_eqv2_radial& R, const EqWs& ws, int64_t E, int N, hipStream_t st) {
-    if (w->edge_channels == 64)
-        hipLaunchKernelGGL(eqv2_radial_kernel<64>, dim3(gwave(E)), dim3(256), 0, st, ws.rot, ws.zn, R, E, N, ws.H2);
+    const int He = w->edge_channels;
+    float* H1 = ws.A0;
+    if (He == 64)
+        hipLaunchKernelGGL(eqv2_radial_kernel<64>, dim3(gwave(E)), dim3(256), 0, st, ws.rot, ws.zn, R, E, N, H1);
     else
-        hipLaunchKernelGGL(eqv2_radial_kernel<32>, dim3(gwave(E)), dim3(256), 0, st, ws.rot, ws.zn, R, E, N, ws.H2);
+        hipLaunchKernelGGL(eqv2_radial_kernel<32>, dim3(gwave(E)), dim3(256), 0, st, ws.rot, ws.zn, R, E, N, H1);
     NBX_LAUNCH_CHECK("eqv2 radial");
-    return NBX_OK;
+    nbx::LinProb p = nbx::lin_dense(H1, He, He, (int)E, R.w1, He, He, R.b1, ws.H2, He);
+    p.ln_w = R.ln2_w;
+    p.ln_b = R.ln2_b;
+    if (He == 64) return nbx::lin_launch<2, nbx::ACT_NONE, nbx::LIN_LNSILU>(p, st);
+    return nbx::lin_launch<1, nbx::ACT_NONE, nbx::LIN_LNSILU>(p, st);
 }
 
 // x3 GEMM: Y[rows][ldy] = A[rows][K] W^T (+ bias), N padded to 32
@@ -560,7 +559,7 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
     if (int rc = gemm_x3(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, 4 * H, nullptr, ws.Y1, 4 * H, st)) return rc;
     S2Args s{ws.Y0, ws.ld0, ws.Y1, w->grid_attn_to, w->grid_attn_from, Aw.alpha_norm_w, Aw.alpha_norm_b,
              Aw.alpha_dot, nh, w->alpha_channels, H, E, ws.Z0, ws.Z1, ws.L};
-    hipLaunchKernelGGL(eqv2_s2act_kernel, dim3(gwave(E)), dim3(256), 0, st, s);
+    hipLaunchKernelGGL(eqv2_s2act_kernel, dim3(g1(E * H)), dim3(256), 0, st, s);
     NBX_LAUNCH_CHECK("eqv2 s2act");
     if (int rc = gemm_x3(ws.Z0, 3 * H, iE, Aw.c20_x3, ws.ldv0, Aw.c20_b, ws.V0, ws.ldv0, st)) return rc;
     if (int rc = gemm_x3(ws.Z1, 2 * H, 2 * iE, Aw.c21_x3, ws.ldv1, nullptr, ws.V1, ws.ldv1, st)) return rc;
@@ -599,7 +598,7 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         a.Red = ws.Y0; a.semb = w->sphere_emb; a.vel = vel; a.vel_t = w->vel_t; a.vel_b = w->vel_b; a.zn = ws.zn;
         a.nnorm_w = w->num_layers ? w->blocks[0].norm1_w : w->norm_w;
         a.nnorm_b = w->num_layers ? w->blocks[0].norm1_b : w->norm_b;
-        hipLaunchKernelGGL(eqv2_node_kernel<NODE_INIT>, dim3((unsigned)B), dim3(64 * NODE_WAVES), 0, st, a);
+        hipLaunchKernelGGL(eqv2_node_kernel<NODE_INIT>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
         NBX_LAUNCH_CHECK("eqv2 node init");
     }
     for (int l = 0; l < w->num_layers; ++l) {
@@ -614,13 +613,13 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         const bool last = l + 1 == w->num_layers;
         a.nnorm_w = last ? w->norm_w : w->blocks[l + 1].norm1_w;
         a.nnorm_b = last ? w->norm_b : w->blocks[l + 1].norm1_b;
-        hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)B), dim3(64 * NODE_WAVES), 0, st, a);
+        hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
         NBX_LAUNCH_CHECK("eqv2 node block");
     }
     if (int rc = attention_edges(w, w->force, ws, B, N, st)) return rc;
     NodeArgs a = node_args(w, ws, N);
     a.proj_t = w->force.proj_t; a.proj_b = w->force.proj_b; a.cout = 2; a.out = out;
-    hipLaunchKernelGGL(eqv2_node_kernel<NODE_FORCE>, dim3((unsigned)B), dim3(64 * NODE_WAVES), 0, st, a);
+    hipLaunchKernelGGL(eqv2_node_kernel<NODE_FORCE>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
     NBX_LAUNCH_CHECK("eqv2 node force");
     return NBX_OK;
 }

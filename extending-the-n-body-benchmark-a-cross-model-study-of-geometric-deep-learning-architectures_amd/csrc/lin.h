@@ -19,7 +19,7 @@
 namespace nbx {
 
 enum LinAct : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
-enum LinEpi : int { LIN_STORE = 0, LIN_CONV = 1, LIN_EQMSG = 2 };
+enum LinEpi : int { LIN_STORE = 0, LIN_CONV = 1, LIN_EQMSG = 2, LIN_LNSILU = 3 };
 
 struct LinSeg {
     const float* ptr;   // segment base
@@ -66,6 +66,10 @@ struct LinProb {
     float* eq_a0;
     float* eq_a1;
     int eq_C, eq_nodes;
+    // LIN_LNSILU: Y = SiLU(LayerNorm(acc + bias) * ln_w + ln_b) over the row's N = NT * 32 columns
+    // (one column chunk), eps 1e-5 (EquiformerV2 RadialFunction hidden layers)
+    const float* ln_w;
+    const float* ln_b;
 };
 
 constexpr int LIN_WAVES = 8, LIN_THREADS = 64 * LIN_WAVES;
@@ -292,6 +296,38 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
                 a1[C2] = r4 * re2;
                 a1[2 * C2] = r3 * im1;
                 a1[3 * C2] = r4 * im2;
+            }
+        } else if constexpr (EPI == LIN_LNSILU) {
+            float bb[NT], gw[NT], gb[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                bb[j] = P.bias[32 * j + r];
+                gw[j] = P.ln_w[32 * j + r];
+                gb[j] = P.ln_b[32 * j + r];
+            }
+            const float invn = 1.0f / (NT * 32);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                float y[NT], s = 0.f;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    y[j] = acc[j][e] + bb[j];
+                    s += y[j];
+                }
+                for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);   // the 32 lanes of this row
+                const float mu = s * invn;
+                float q = 0.f;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) q += (y[j] - mu) * (y[j] - mu);
+                for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o);
+                const float rs = 1.0f / sqrtf(q * invn + 1e-5f);
+                if (row < P.rows)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        const float z = (y[j] - mu) * rs * gw[j] + gb[j];
+                        P.Y[(size_t)row * P.ldy + 32 * j + r] = z * __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+                    }
             }
         } else if constexpr (EPI == LIN_CONV) {
             const int G = P.conv_G, O = P.conv_O, NN = P.conv_nodes;
