@@ -18,6 +18,7 @@ Secondary configurations (not the headline; same JSON shape):
   --model ponita   C3: PONITA hidden 128, 6 layers, 20 orientations, basis 128, N=5,
                    global batch 4096 sharded over the ranks ("strong" scaling).
   --model egnn_mc  C1: EGNN-MC 6 x 128, N=5, batch 64 per rank ("weak").
+  --model eqv2     C4: EquiformerV2 (config.yaml widths), N=20, batch 256 per rank ("weak").
   --model gravity  C5: ground-truth integrator, 10 000 systems x N=100, --steps
                    KDK steps (sample_freq 10), systems sharded over the ranks ("strong").
 
@@ -161,7 +162,7 @@ def bench_segnn(a, rank, world, device, P):
     dom_avg_s = ms_k[dom] / n_k[dom] / 1e3
     dom_flops = fl_k[dom] / n_k[dom]
     achieved_tflops = dom_flops / dom_avg_s / 1e12
-    traffic = pmc_traffic(names[dom])
+    traffic = pmc_traffic(names[dom], "segnn")
     value = a.steps / elapsed * world
     result = {
         "metric": "self-feed rollout steps/sec, SEGNN N=5 batch=1024",
@@ -194,18 +195,28 @@ def bench_segnn(a, rank, world, device, P):
     return result
 
 
-def pmc_traffic(kernel_name):
-    pmc = os.path.join(ROOT, "profiles", "pmc_tp_kernels.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            return json.load(f)["kernels"].get(kernel_name, {}).get("hbm_bytes_per_launch")
+def pmc_traffic(kernel_name, model=None):
+    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary
+    (profiles/r*/pmc_<model>.json, written by scripts/profile_models.sh: 2 x FETCH_SIZE +
+    WRITE_SIZE per dispatch, MI355X_MICROARCH.md's gfx950 correction), else None."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{model}.json")), reverse=True) if model else []
+    cands.append(os.path.join(ROOT, "profiles", "pmc_tp_kernels.json"))
+    for pmc in cands:
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                v = json.load(f)["kernels"].get(kernel_name, {}).get("hbm_bytes_per_launch")
+            if v is not None:
+                return v
     return None
 
 
 # ---------------------------------------------------------------- C3 PONITA
-PONITA_KIND_NAMES = ["void nbx::lin_kernel<4, 0, 1>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0>(nbx::LinProb)",
-                     "void nbx::lin_kernel<2, 0, 0>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0>(nbx::LinProb)",
-                     "void (anonymous namespace)::po_fiber_ln_kernel<20, 4>(...)"]
+# rocprofv3 names at C3 with the bf16x3 images (ponita.hip lin_auto: PREC = 1, NT by the image's LDS size)
+PONITA_KIND_NAMES = ["void nbx::lin_kernel<4, 0, 1, 1>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0, 1>(nbx::LinProb)",
+                     "void nbx::lin_kernel<1, 0, 0, 1>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0, 1>(nbx::LinProb)",
+                     "void (anonymous namespace)::po_fiber_ln_kernel<20, 4>(float const*, float const*, int, "
+                     "float const*, float const*, float const*, long, int, int, int, float*, double*)"]
 PONITA_KIND_ROLES = ["FiberBundleConv spatial kernel GEMM + gather/aggregate epilogue", "ConvNext linear_1 + GELU",
                      "ConvNext linear_2 + layer_scale + residual", "kernel basis MLP (2 GEMMs)",
                      "fibre conv + bias + LayerNorm"]
@@ -263,7 +274,7 @@ def bench_ponita(a, rank, world, device, P):
         ach = acc[2, dom] / acc[1, dom] / dom_s / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
-    roof.update({"traffic": pmc_traffic(PONITA_KIND_NAMES[dom]), "kernel": PONITA_KIND_NAMES[dom],
+    roof.update({"traffic": pmc_traffic(PONITA_KIND_NAMES[dom], "ponita"), "kernel": PONITA_KIND_NAMES[dom],
                  "role": PONITA_KIND_ROLES[dom], "avg_launch_us": round(dom_s * 1e6, 2), "per_kind": per_kind})
     value = a.steps / elapsed
     result = {
@@ -346,6 +357,105 @@ def bench_egnn(a, rank, world, device, P):
     return result
 
 
+# ---------------------------------------------------------------- C4 EquiformerV2
+EQV2_C4 = dict(num_layers=4, attn_hidden_channels=64, sphere_channels=64, num_heads=4, attn_alpha_channels=8,
+               attn_value_channels=4, ffn_hidden_channels=64, lmax_list=[2], mmax_list=[1], grid_resolution=None,
+               edge_channels=64, use_atom_edge_embedding=True, share_atom_edge_embedding=False,
+               distance_function="projection", num_distance_basis=64, attn_activation="scaled_silu",
+               use_s2_act_attn=False, ffn_activation="scaled_silu", max_neighbors=5, max_radius=4096.0)
+EQV2_KINDS = ["radial hidden layers (per-edge layer + GEMM with LayerNorm/SiLU epilogue)",
+              "radial output GEMM + rotated-message epilogue (A0/A1)", "SO(2) conv 1, m=0 GEMM",
+              "SO(2) conv 1, m=1 GEMM", "separable S2 activation + attention logits", "SO(2) conv 2 GEMMs",
+              "node kernels (softmax, inverse rotation, proj, FFN, norms)", "edge frame + edge-degree embedding"]
+EQV2_GEMM = "void nbx::lin_kernel<2, 0, 0, 1>(nbx::LinProb)"   # kinds 2, 3, 5 (4 launches per attention)
+
+
+def bench_eqv2(a, rank, world, device, P):
+    from nbody_amd import _lib
+    from nbody_amd.equiformer_v2 import EquiformerV2_nbody
+    B, N = a.batch or 256, 20
+    torch.manual_seed(0)
+    model = EquiformerV2_nbody(**EQV2_C4).to(device).eval()
+    loc, vel, mass = initial_states(B, N, rank * B)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    loc_d, vel_d, mass_d = t(loc), t(vel), t(mass)
+    model.rollout(loc_d, vel_d, mass_d, max(a.warmup, 1) + 1, seed=1)
+
+    def work():
+        tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1, seed=2)
+        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
+        return tp
+    tp, elapsed = timed_region(work, device, P)
+    finite = bool(torch.isfinite(tp).all().item())
+
+    W = model._weights(device)
+    ws = model._workspace(W, B, N, device)
+    p32, v32, m32 = loc_d.reshape(-1, 3), vel_d.reshape(-1, 3), mass_d.reshape(-1)
+    out = torch.empty(B * N, 6, device=device)
+    kms, kn, kfl, kby, tot = (_lib.c_f * 8)(), (_lib.c_i32 * 8)(), (_lib.c_d * 8)(), (_lib.c_d * 8)(), _lib.c_f()
+    acc = np.zeros((4, 8))
+    fwd, reps = 0.0, 3
+    for _ in range(reps):
+        _lib.check(_lib.lib().nbx_eqv2_forward_timed(W, _lib.dev_ptr(p32), _lib.dev_ptr(v32), _lib.dev_ptr(m32), B, N,
+                                                     None, 7, _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
+                                                     _lib.stream_ptr(device), kms, kn, kfl, kby, tot),
+                   "nbx_eqv2_forward_timed")
+        acc += np.array([list(kms), list(kn), list(kfl), list(kby)])
+        fwd += tot.value
+    per_kind = {}
+    for k in range(8):
+        if acc[1, k]:
+            sec = acc[0, k] / 1e3
+            per_kind[EQV2_KINDS[k]] = {"avg_group_us": round(sec / acc[1, k] * 1e6, 2),
+                                       "tflops": round(acc[2, k] / sec / 1e12, 3),
+                                       "gbs": round(acc[3, k] / sec / 1e9, 1), "share_of_forward": round(acc[0, k] / fwd, 3)}
+    # dominant kernel: the bf16x3 SO(2) GEMM kernel (kinds 2, 3, 5: 4 launches per attention block)
+    g_ms = acc[0, 2] + acc[0, 3] + acc[0, 5]
+    g_n = acc[1, 2] + acc[1, 3] + 2 * acc[1, 5]
+    g_fl = acc[2, 2] + acc[2, 3] + acc[2, 5]
+    g_avg_s = g_ms / g_n / 1e3
+    ach = g_fl / (g_ms / 1e3) / 1e12
+    roof = {"bound": "mfma", "kernel": EQV2_GEMM, "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": pmc_traffic(EQV2_GEMM, "eqv2"), "avg_launch_us": round(g_avg_s * 1e6, 2),
+            "gflop_per_launch": round(g_fl / g_n / 1e9, 4),
+            "mfma_path": "bf16x3 split (fp32-accurate), v_mfma_f32_32x32x16_bf16",
+            "executed_bf16_tflops": round(ach * X3_TERMS, 2),
+            "executed_bf16_frac": round(ach * X3_TERMS / BF16_MFMA_PEAK_TFLOPS, 4),
+            "timing": "HIP event pairs around each launch group on the launch stream",
+            "gemm_share_of_forward": round(g_ms / fwd, 3), "per_kind": per_kind}
+    value = a.steps / elapsed * world
+    result = {
+        "metric": "self-feed rollout steps/sec, EquiformerV2 N=20 batch=256", "value": round(value, 3),
+        "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states N=20, seeded random-init weights, device-hash edge gauges)",
+        "config": {"workload": "C4: EquiformerV2 4 layers, sphere 64, attn hidden 64, 4 heads (alpha 8, value 4), "
+                               "ffn 64, lmax [2], mmax [1], edge channels 64, N=20, batch 256 per GPU",
+                   "model": "EquiformerV2", "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}"},
+        "trajectory_steps_per_s": round(value * B, 1),
+        "algorithmic_tflops": round(value / world * acc[2].sum() / reps / 1e12, 3),
+        "roofline": roof, "finite": finite}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_eqv2(model, B)
+    return result
+
+
+def cpu_baseline_eqv2(model, B_glob, B_s=128):
+    from oracle import equiformer_v2 as EQ
+    p = {k: v.detach().double().cpu() for k, v in model.named_parameters()}
+    loc, vel, mass = initial_states(B_s, 20, 0)
+    g = np.random.default_rng(0).uniform(0, 1, (B_s * 20 * 19, 3))
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    EQ.forward(EQV2_C4, p, loc, vel, mass, B_s, 20, g)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / (dt * B_glob / B_s), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"1 forward of B={B_s} systems with the torch fp64 CPU oracle (oracle/equiformer_v2.py), "
+                      f"{dt:.2f} s, scaled x{B_glob // B_s} to the B={B_glob} batch; torch threads={threads}"}
+
+
 # ---------------------------------------------------------------- C5 integrator
 def bench_gravity(a, rank, world, device, P):
     from nbody_amd.gravity import GravitySim
@@ -414,17 +524,18 @@ def main():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
-    ap.add_argument("--model", default="segnn", choices=["segnn", "ponita", "egnn_mc", "gravity"])
+    ap.add_argument("--model", default="segnn", choices=["segnn", "ponita", "egnn_mc", "eqv2", "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     a = ap.parse_args()
-    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "gravity": (1000, 100)}
+    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "eqv2": (20, 2), "gravity": (1000, 100)}
     a.steps = a.steps if a.steps is not None else defaults[a.model][0]
     a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
 
     from nbody_amd import parallel as P
     rank, world, device = P.init_from_env()
-    fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "gravity": bench_gravity}[a.model]
+    fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "eqv2": bench_eqv2,
+          "gravity": bench_gravity}[a.model]
     result = fn(a, rank, world, device, P)
     if rank == 0:
         print(json.dumps(result), flush=True)

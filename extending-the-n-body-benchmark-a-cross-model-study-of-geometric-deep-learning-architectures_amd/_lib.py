@@ -137,6 +137,9 @@ _SIGNATURES = {
     "nbx_eqv2_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "nbx_eqv2_forward": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_p, c_p, c_p, c_i64, c_i64, c_p, ctypes.c_uint64,
                                         c_p, c_p, c_sz, c_p]),
+    "nbx_eqv2_forward_timed": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_p, c_p, c_p, c_i64, c_i64, c_p,
+                                              ctypes.c_uint64, c_p, c_p, c_sz, c_p, c_f * 8, c_i32 * 8, c_d * 8,
+                                              c_d * 8, ctypes.POINTER(c_f)]),
     "nbx_eqv2_rollout": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
                                         ctypes.c_uint64, c_p, c_p, c_p, c_sz, c_p]),
 }

@@ -474,6 +474,40 @@ struct EqWs {
 
 inline int ceil32(int x) { return (x + 31) & ~31; }
 
+// ---- per-kind timing for nbx_eqv2_forward_timed: HIP event pairs around each launch group on the
+// launch stream, with the group's algorithmic flops (2 x MACs of the fp32-accurate products) and
+// HBM bytes (its tensor inputs + outputs once).  Kinds: 0 radial hidden layers, 1 radial output GEMM
+// + message epilogue, 2 SO(2) conv 1 m = 0 GEMM, 3 SO(2) conv 1 m = 1 GEMM, 4 S2 activation +
+// logits, 5 SO(2) conv 2 GEMMs, 6 node kernels, 7 edge frame + edge-degree embedding.
+constexpr int EQ_KINDS = 8;
+struct EqTimer {
+    static constexpr int MAXR = 512;
+    hipEvent_t ev[2 * MAXR];
+    int kind[MAXR];
+    int n = 0;
+    double flops[EQ_KINDS] = {}, bytes[EQ_KINDS] = {};
+};
+thread_local EqTimer* g_timer = nullptr;
+struct TScope {
+    hipStream_t st;
+    bool on = false;
+    TScope(int k, hipStream_t s, double fl, double by) : st(s) {
+        EqTimer* T = g_timer;
+        if (T && T->n < EqTimer::MAXR - 1) {
+            on = hipEventRecord(T->ev[2 * T->n], st) == hipSuccess;
+            T->kind[T->n] = k;
+            T->flops[k] += fl;
+            T->bytes[k] += by;
+        }
+    }
+    ~TScope() {
+        if (on) {
+            (void)hipEventRecord(g_timer->ev[2 * g_timer->n + 1], st);
+            g_timer->n++;
+        }
+    }
+};
+
 size_t eqv2_carve(EqWs* ws, void* base, const nbx_eqv2_weights* w, int64_t B, int64_t N) {
     const int C = w->sphere_channels, H = w->attn_hidden, He = w->edge_channels, KV = w->num_heads * w->value_channels;
     const int64_t V = B * N, E = V * (N - 1);
@@ -542,8 +576,14 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
     const int nh = w->num_heads, KV = nh * w->value_channels;
     const int64_t V = B * N, E = V * (N - 1);
     const int iE = (int)E;
-    if (int rc = radial(w, Aw.rad, ws, E, N, st)) return rc;
+    const double e = (double)E, f4 = 4.0;
+    const int na = w->alpha_channels, n0r = nh * na + 4 * H;
+    {
+        TScope ts(0, st, 2.0 * e * He * He, f4 * e * (2 * He + 2 * He + 1));
+        if (int rc = radial(w, Aw.rad, ws, E, N, st)) return rc;
+    }
     {   // rad = H2 W2^T + b2 (columns permuted), epilogue: A0/A1 = rad * rotated [x_src | x_dst]
+        TScope ts(1, st, 2.0 * e * He * 10 * C, f4 * e * (He + 14 * C + 25));
         nbx::LinProb p = nbx::lin_dense(ws.H2, He, He, iE, nullptr, He, 10 * C, Aw.rad.b2, nullptr, 0);
         p.Wx3 = Aw.rad.w2_x3;
         p.eq_x = ws.XN;
@@ -555,14 +595,26 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
         if (int rc = nbx::lin_launch<5, nbx::ACT_NONE, nbx::LIN_EQMSG, 1>(p, st)) return rc;
     }
     const int n0 = ceil32(nh * w->alpha_channels + 4 * H);
-    if (int rc = gemm_x3(ws.A0, 6 * C, iE, Aw.fc0_x3, n0, Aw.fc0_b, ws.Y0, ws.ld0, st)) return rc;
-    if (int rc = gemm_x3(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, 4 * H, nullptr, ws.Y1, 4 * H, st)) return rc;
+    {
+        TScope ts(2, st, 2.0 * e * 6 * C * n0r, f4 * e * (6 * C + n0r));
+        if (int rc = gemm_x3(ws.A0, 6 * C, iE, Aw.fc0_x3, n0, Aw.fc0_b, ws.Y0, ws.ld0, st)) return rc;
+    }
+    {
+        TScope ts(3, st, 2.0 * 2 * e * 4 * C * 4 * H, f4 * 2 * e * (4 * C + 4 * H));
+        if (int rc = gemm_x3(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, 4 * H, nullptr, ws.Y1, 4 * H, st)) return rc;
+    }
     S2Args s{ws.Y0, ws.ld0, ws.Y1, w->grid_attn_to, w->grid_attn_from, Aw.alpha_norm_w, Aw.alpha_norm_b,
              Aw.alpha_dot, nh, w->alpha_channels, H, E, ws.Z0, ws.Z1, ws.L};
-    hipLaunchKernelGGL(eqv2_s2act_kernel, dim3(g1(E * H)), dim3(256), 0, st, s);
-    NBX_LAUNCH_CHECK("eqv2 s2act");
-    if (int rc = gemm_x3(ws.Z0, 3 * H, iE, Aw.c20_x3, ws.ldv0, Aw.c20_b, ws.V0, ws.ldv0, st)) return rc;
-    if (int rc = gemm_x3(ws.Z1, 2 * H, 2 * iE, Aw.c21_x3, ws.ldv1, nullptr, ws.V1, ws.ldv1, st)) return rc;
+    {
+        TScope ts(4, st, 2.0 * e * H * GA * 14, f4 * e * (n0r + 8 * H + 7 * H + nh));
+        hipLaunchKernelGGL(eqv2_s2act_kernel, dim3(g1(E * H)), dim3(256), 0, st, s);
+        NBX_LAUNCH_CHECK("eqv2 s2act");
+    }
+    {
+        TScope ts(5, st, 2.0 * e * (3 * H * 3 * KV + 2 * 2 * H * 4 * KV), f4 * e * (7 * H + 11 * KV));
+        if (int rc = gemm_x3(ws.Z0, 3 * H, iE, Aw.c20_x3, ws.ldv0, Aw.c20_b, ws.V0, ws.ldv0, st)) return rc;
+        if (int rc = gemm_x3(ws.Z1, 2 * H, 2 * iE, Aw.c21_x3, ws.ldv1, nullptr, ws.V1, ws.ldv1, st)) return rc;
+    }
     (void)KV;
     return NBX_OK;
 }
@@ -583,6 +635,14 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
                       hipStream_t st) {
     const int N = (int)N64, C = w->sphere_channels, He = w->edge_channels;
     const int64_t V = B * N, E = V * (N - 1);
+    const int F = w->ffn_hidden, KV = w->num_heads * w->value_channels;
+    const double e = (double)E, v = (double)V, f4 = 4.0;
+    // node kernel per block: proj + FFN flops, reads V0/V1/L/rot + X, writes X, XN
+    const double node_fl = 2.0 * v * (9.0 * KV * C + C * F + 9.0 * C * F * 2 + GF * 18.0 * F) +
+                           2.0 * e * (25.0 + 7.0) * KV;
+    const double node_by = f4 * (e * (11.0 * KV + w->num_heads + 25) + v * 27.0 * C);
+    {
+    TScope ts_all(7, st, 2.0 * e * He * (He + 3 * C), f4 * (e * (32 + 2 * He + 3 * C) + v * 19.0 * C));
     hipLaunchKernelGGL(eqv2_edge_kernel, dim3(g1(std::max(V, E))), dim3(256), 0, st, pos, mass, gauge, seed, frame, V,
                        N, w->num_elements, ws.rot, ws.zn);
     NBX_LAUNCH_CHECK("eqv2 edge");
@@ -601,6 +661,7 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         hipLaunchKernelGGL(eqv2_node_kernel<NODE_INIT>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
         NBX_LAUNCH_CHECK("eqv2 node init");
     }
+    }
     for (int l = 0; l < w->num_layers; ++l) {
         const nbx_eqv2_block& Bk = w->blocks[l];
         if (int rc = attention_edges(w, Bk.ga, ws, B, N, st)) return rc;
@@ -613,12 +674,14 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         const bool last = l + 1 == w->num_layers;
         a.nnorm_w = last ? w->norm_w : w->blocks[l + 1].norm1_w;
         a.nnorm_b = last ? w->norm_b : w->blocks[l + 1].norm1_b;
+        TScope ts(6, st, node_fl, node_by);
         hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
         NBX_LAUNCH_CHECK("eqv2 node block");
     }
     if (int rc = attention_edges(w, w->force, ws, B, N, st)) return rc;
     NodeArgs a = node_args(w, ws, N);
     a.proj_t = w->force.proj_t; a.proj_b = w->force.proj_b; a.cout = 2; a.out = out;
+    TScope ts(6, st, 2.0 * e * 32.0 * KV + 2.0 * v * 9.0 * KV * 2, f4 * (e * (11.0 * KV + w->num_heads + 25) + v * 6));
     hipLaunchKernelGGL(eqv2_node_kernel<NODE_FORCE>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
     NBX_LAUNCH_CHECK("eqv2 node force");
     return NBX_OK;
@@ -661,6 +724,46 @@ extern "C" int nbx_eqv2_forward(const nbx_eqv2_weights* w, const float* pos, con
     EqWs ws;
     if (int rc = eqv2_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     return eqv2_forward_impl(w, pos, vel, mass, B, N, gauge, seed, 0, out, ws, (hipStream_t)stream);
+}
+
+extern "C" int nbx_eqv2_forward_timed(const nbx_eqv2_weights* w, const float* pos, const float* vel,
+                                      const float* mass, int64_t B, int64_t N, const float* gauge, uint64_t seed,
+                                      float* out, void* workspace, size_t workspace_bytes, void* stream,
+                                      float kind_ms[8], int32_t kind_launches[8], double kind_flops[8],
+                                      double kind_bytes[8], float* total_ms) {
+    EqWs ws;
+    if (int rc = eqv2_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    static EqTimer T;
+    static bool made = false;
+    if (!made) {
+        for (auto& ev : T.ev) NBX_HIP(hipEventCreate(&ev));
+        made = true;
+    }
+    T.n = 0;
+    for (int k = 0; k < EQ_KINDS; ++k) T.flops[k] = T.bytes[k] = 0.0;
+    hipEvent_t t0 = T.ev[2 * EqTimer::MAXR - 2], t1 = T.ev[2 * EqTimer::MAXR - 1];
+    NBX_HIP(hipEventRecord(t0, st));
+    g_timer = &T;
+    const int rc = eqv2_forward_impl(w, pos, vel, mass, B, N, gauge, seed, 0, out, ws, st);
+    g_timer = nullptr;
+    if (rc) return rc;
+    NBX_HIP(hipEventRecord(t1, st));
+    NBX_HIP(hipEventSynchronize(t1));
+    for (int k = 0; k < EQ_KINDS; ++k) {
+        kind_ms[k] = 0.f;
+        kind_launches[k] = 0;
+        kind_flops[k] = T.flops[k];
+        kind_bytes[k] = T.bytes[k];
+    }
+    for (int i = 0; i < T.n && i < EqTimer::MAXR - 1; ++i) {
+        float ms = 0.f;
+        NBX_HIP(hipEventElapsedTime(&ms, T.ev[2 * i], T.ev[2 * i + 1]));
+        kind_ms[T.kind[i]] += ms;
+        kind_launches[T.kind[i]] += 1;
+    }
+    NBX_HIP(hipEventElapsedTime(total_ms, t0, t1));
+    return NBX_OK;
 }
 
 extern "C" int nbx_eqv2_rollout(const nbx_eqv2_weights* w, float* pos, float* vel, const float* mass, int64_t B,

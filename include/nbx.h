@@ -433,6 +433,17 @@ int nbx_eqv2_forward(const nbx_eqv2_weights* w, const float* pos, const float* v
                      int64_t batch_size, int64_t num_nodes, const float* gauge, uint64_t seed, float* out,
                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* nbx_eqv2_forward with HIP event pairs around each launch group on `stream` (synchronises; not
+ * graph-capturable): per kind k (0 radial hidden layers, 1 radial output GEMM + message epilogue,
+ * 2 SO(2) conv 1 m=0 GEMM, 3 SO(2) conv 1 m=1 GEMM, 4 S2 activation + logits, 5 SO(2) conv 2 GEMMs,
+ * 6 node kernels, 7 edge frame + edge-degree embedding) the summed time, launch-group count, and the
+ * algorithmic flops (2 x MACs of fp32-accurate products) and HBM bytes (inputs + outputs once);
+ * total_ms = the whole forward. */
+int nbx_eqv2_forward_timed(const nbx_eqv2_weights* w, const float* pos, const float* vel, const float* mass,
+                           int64_t batch_size, int64_t num_nodes, const float* gauge, uint64_t seed, float* out,
+                           void* workspace, size_t workspace_bytes, void* stream, float kind_ms[8],
+                           int32_t kind_launches[8], double kind_flops[8], double kind_bytes[8], float* total_ms);
+
 /* Device-resident self-feed rollout through the tuple branch (infer_self_feed.py:99-194), same
  * contract as nbx_segnn_rollout; step t draws its gauges from the hash of (seed, t, edge). */
 int nbx_eqv2_rollout(const nbx_eqv2_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,

@@ -7,11 +7,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 export TMPDIR=/tmp
-MODELS="${*:-segnn ponita egnn_mc gravity}"
+MODELS="${*:-segnn ponita egnn_mc eqv2 gravity}"
 declare -A ARGS=(
   [segnn]="--model segnn --steps 20 --warmup 2 --no-cpu-baseline"
   [ponita]="--model ponita --steps 4 --warmup 1 --no-cpu-baseline"
   [egnn_mc]="--model egnn_mc --steps 50 --warmup 5 --no-cpu-baseline"
+  [eqv2]="--model eqv2 --steps 5 --warmup 1 --no-cpu-baseline"
   [gravity]="--model gravity --steps 200 --warmup 10 --no-cpu-baseline"
 )
 mkdir -p gpurun_out/prof
