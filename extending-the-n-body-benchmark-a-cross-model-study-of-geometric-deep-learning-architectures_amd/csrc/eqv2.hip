@@ -569,6 +569,21 @@ int gemm_x3(const float* A, int K, int rows, const void* Wx3, int N, const float
     return nbx::lin_launch<2, nbx::ACT_NONE, nbx::LIN_STORE, 1>(p, st);
 }
 
+// row-panel x3 GEMM over all N = 32 ntiles columns (chunk-major image; lin.h lin_rp_kernel)
+int gemm_rp(const float* A, int K, int rows, const void* Wx3, int ntiles, const float* bias, float* Y, int ldy,
+            hipStream_t st) {
+    nbx::LinRpProb p{A, K, rows, K, Wx3, bias, Y, ldy, 32 * ntiles};
+    switch (ntiles) {
+        case 4: return nbx::lin_rp_launch<4, nbx::ACT_NONE>(p, st);
+        case 5: return nbx::lin_rp_launch<5, nbx::ACT_NONE>(p, st);
+        case 8: return nbx::lin_rp_launch<8, nbx::ACT_NONE>(p, st);
+        case 9: return nbx::lin_rp_launch<9, nbx::ACT_NONE>(p, st);
+        default:
+            nbx::set_error("eqv2: no row-panel GEMM for %d column tiles", ntiles);
+            return NBX_E_UNSUPPORTED;
+    }
+}
+
 // SO2EquivariantGraphAttention (transformer_block.py:226-370) up to the per-edge values and logits
 int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const EqWs& ws, int64_t B, int N,
                     hipStream_t st) {
@@ -597,11 +612,11 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
     const int n0 = ceil32(nh * w->alpha_channels + 4 * H);
     {
         TScope ts(2, st, 2.0 * e * 6 * C * n0r, f4 * e * (6 * C + n0r));
-        if (int rc = gemm_x3(ws.A0, 6 * C, iE, Aw.fc0_x3, n0, Aw.fc0_b, ws.Y0, ws.ld0, st)) return rc;
+        if (int rc = gemm_rp(ws.A0, 6 * C, iE, Aw.fc0_x3, n0 / 32, Aw.fc0_b, ws.Y0, ws.ld0, st)) return rc;
     }
     {
         TScope ts(3, st, 2.0 * 2 * e * 4 * C * 4 * H, f4 * 2 * e * (4 * C + 4 * H));
-        if (int rc = gemm_x3(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, 4 * H, nullptr, ws.Y1, 4 * H, st)) return rc;
+        if (int rc = gemm_rp(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, 4 * H / 32, nullptr, ws.Y1, 4 * H, st)) return rc;
     }
     S2Args s{ws.Y0, ws.ld0, ws.Y1, w->grid_attn_to, w->grid_attn_from, Aw.alpha_norm_w, Aw.alpha_norm_b,
              Aw.alpha_dot, nh, w->alpha_channels, H, E, ws.Z0, ws.Z1, ws.L};

@@ -472,6 +472,121 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     return NBX_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Row-panel split-precision GEMM: Y[row, n] = act(sum_k A[row, k] W[n, k] + bias[n]) for ALL
+// NTILES * 32 output columns in one workgroup, so A is read from HBM exactly once (the weight-
+// stationary lin_kernel re-reads A once per column chunk).  The weights stream through LDS by 32-deep
+// K chunk: a chunk-major bf16x3 image [K/32][NTILES][3][2][64][8] bf16 (the "bf16x3 images" blocks
+// reordered so one chunk of every column tile is contiguous), double-buffered by LDS-DMA while the
+// MFMAs consume the other buffer.  8 waves, one 32-row tile each (a 256-row panel per workgroup).
+struct LinRpProb {
+    const float* A;
+    int lda, rows, K;   // K % 32 == 0
+    const void* Wx3;    // chunk-major image
+    const float* bias;  // [NTILES * 32] or null
+    float* Y;
+    int ldy, N;         // N: columns stored (<= NTILES * 32)
+};
+
+constexpr int RP_WAVES = 8;
+
+template <int NTILES, int ACT>
+__global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpProb P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int SLAB = NTILES * LIN_X3_BLK;          // floats of one K chunk of every column tile
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+    const int nk = P.K >> 5;
+    const int rt = blockIdx.x * RP_WAVES + wave;
+    const int row = rt * 32 + r;
+    const bool ok = row < P.rows;
+    const float* W = reinterpret_cast<const float*>(P.Wx3);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.A, (short)0, 0x7FFFFFF0, 0x00020000);
+    const uint32_t base = (uint32_t)(((size_t)(ok ? row : 0) * P.lda + 16 * h) * 4);
+    auto load_a = [&](int kc, float4 (&a)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rs, ok ? base + (uint32_t)(kc * 128 + 16 * q) : 0x7FFFFFF0u, 0, 0));
+    };
+    floatx16 acc[NTILES];
+#pragma unroll
+    for (int j = 0; j < NTILES; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    // one A register buffer: a chunk is split into hi / mid / lo bf16 first, then the next chunk's A
+    // load is issued into the same registers and lands while this chunk's MFMAs run
+    auto mfmas = [&](const bf16x8 (&a)[3][2], const float* buf) {
+        const bf16x8* ldsx = reinterpret_cast<const bf16x8*>(buf);
+#pragma unroll
+        for (int j = 0; j < NTILES; ++j) {
+            const bf16x8* bp = ldsx + j * (LIN_X3_BLK / 4) + lane;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {   // smallest terms first (as lin_kernel PREC 1)
+                const bf16x8 b0 = bp[m * 64], b1 = bp[(2 + m) * 64], b2 = bp[(4 + m) * 64];
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b1, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b2, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b1, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b0, acc[j], 0, 0, 0);
+            }
+        }
+    };
+    float4 cur[4];
+    tp_dma_image<RP_WAVES>(W, lds, SLAB);
+    load_a(0, cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+        bf16x8 a[3][2];
+        tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
+        tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+        if (kc + 1 < nk) {
+            load_a(kc + 1, cur);
+            tp_dma_image<RP_WAVES>(W + (size_t)(kc + 1) * SLAB, lds + ((kc + 1) & 1) * SLAB, SLAB);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(a, lds + (kc & 1) * SLAB);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < NTILES; ++j) {
+        const int col = 32 * j + r;
+        const bool live = col < P.N;
+        const float b = (live && P.bias) ? P.bias[col] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int rr = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (live && rr < P.rows) P.Y[(size_t)rr * P.ldy + col] = lin_act(acc[j][e] + b, ACT);
+        }
+    }
+}
+
+template <int NTILES, int ACT>
+int lin_rp_launch(const LinRpProb& p, hipStream_t st) {
+    if (p.rows <= 0) return NBX_OK;
+    if (p.K % 32 || !p.Wx3 || p.N > NTILES * 32) {
+        set_error("lin_rp: K %% 32 == 0, an image and N <= %d required", NTILES * 32);
+        return NBX_E_INVAL;
+    }
+    if ((double)p.rows * p.lda * 4.0 >= 2147483632.0) {
+        set_error("lin_rp: A spans >= 2 GiB");
+        return NBX_E_UNSUPPORTED;
+    }
+    const size_t lds = 2 * (size_t)NTILES * LIN_X3_BLK * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NBX_HIP(hipFuncSetAttribute((const void*)lin_rp_kernel<NTILES, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr_set = true;
+    }
+    const unsigned blocks = (unsigned)((p.rows + 32 * RP_WAVES - 1) / (32 * RP_WAVES));
+    hipLaunchKernelGGL((lin_rp_kernel<NTILES, ACT>), dim3(blocks), dim3(64 * RP_WAVES), lds, st, p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
 inline LinProb lin_dense(const float* A, int lda, int K, int rows, const float* Wt, int ldw, int N, const float* bias,
                          float* Y, int ldy) {
     LinProb p;

@@ -351,6 +351,13 @@ class EquiformerV2_nbody(nn.Module):
         rows = W.shape[0]
         return SEGNN.frag_image_x3([(W.float(), W.shape[1])], None, -(-rows // 32), 32)
 
+    @classmethod
+    def _image_chunk_major(cls, W):
+        """[N/32][K/32] blocks -> [K/32][N/32] (include/nbx.h: so2_conv_1 images)."""
+        img = cls._image(W)
+        nt, kc = img.shape[0], W.shape[1] // 32
+        return img.reshape(nt, kc, -1).transpose(0, 1).contiguous()
+
     def packed_tensors(self, device):
         """Every device tensor the C-ABI weight struct points at, keyed by struct path."""
         C, He = self.sphere_channels, self.edge_channels
@@ -387,9 +394,9 @@ class EquiformerV2_nbody(nn.Module):
             radial(prefix + "rad.", A.so2_conv_1.rad_func, A.source_embedding, A.target_embedding, True)
             fc0 = A.so2_conv_1.fc_m0
             n0 = c32(fc0.out_features)
-            P[prefix + "fc0_x3"] = self._image(fc0.weight.detach().to(device))
+            P[prefix + "fc0_x3"] = self._image_chunk_major(fc0.weight.detach().to(device))
             P[prefix + "fc0_b"] = v(pad(fc0.bias.detach(), n0))
-            P[prefix + "fc1_x3"] = self._image(A.so2_conv_1.so2_m_conv[0].fc.weight.detach().to(device))
+            P[prefix + "fc1_x3"] = self._image_chunk_major(A.so2_conv_1.so2_m_conv[0].fc.weight.detach().to(device))
             c20 = A.so2_conv_2.fc_m0
             P[prefix + "c20_x3"] = self._image(c20.weight.detach().to(device))
             P[prefix + "c20_b"] = v(pad(c20.bias.detach(), c32(c20.out_features)))

@@ -392,6 +392,9 @@ typedef struct nbx_eqv2_radial {
 
 typedef struct nbx_eqv2_attn {             /* SO2EquivariantGraphAttention */
     nbx_eqv2_radial rad;                   /* so2_conv_1.rad_func (with this module's atom embeddings) */
+    /* so2_conv_1 weights as CHUNK-MAJOR bf16x3 images [K/32][N/32][3][2][64][8] (the blocks of the
+     * "bf16x3 images" layout with the K-chunk index outermost): the row-panel GEMM streams one K
+     * chunk of every column tile per step */
     const void* fc0_x3; const float* fc0_b;  /* so2_conv_1.fc_m0 [nh na + H + 3 H][3 * 2C] */
     const void* fc1_x3;                      /* so2_conv_1.so2_m_conv.0.fc [4H][2 * 2C] */
     const void* c20_x3; const float* c20_b;  /* so2_conv_2.fc_m0 [3 nh nv][3H] */
