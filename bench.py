@@ -341,8 +341,11 @@ def bench_egnn(a, rank, world, device, P):
         "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights)",
         "config": {"workload": "C1: EGNN-MC 6 x 128, norm_diff, tanh, N=5, batch 64 per GPU", "model": "EGNN-MC",
                    "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "launch", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-                     "note": "C1 is launch/latency bound (SURVEY §8d): ~60 launches per step on 1280 edges"},
+        "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                     "kernel": "egnn_persist_kernel<128>: one workgroup per system runs the whole rollout",
+                     "note": "C1 is latency bound (SURVEY §8d): 64 systems = 64 workgroups, each a serial chain of "
+                             "~30 dependent block GEMM / reduction phases per layer on 20 edges; one launch per "
+                             "rollout (was ~60 launches per step)"},
         "finite": bool(torch.isfinite(tp).all().item())}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle.rollout import egnn_mc_step, rollout

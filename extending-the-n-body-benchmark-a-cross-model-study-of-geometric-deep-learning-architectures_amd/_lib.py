@@ -55,7 +55,7 @@ class EgnnHead(ctypes.Structure):
 
 class EgnnWeights(ctypes.Structure):
     _fields_ = [(n, c_i32) for n in ("hidden", "num_layers", "num_heads", "recurrent", "norm_diff", "use_tanh")] + [
-        ("coords_weight", c_f), ("emb_t", c_p), ("emb_b", c_p), ("heads", EgnnHead * 2),
+        ("coords_weight", c_f), ("emb_t", c_p), ("emb_b", c_p), ("persist_blob", c_p), ("heads", EgnnHead * 2),
         ("layers", EgnnLayer * EGNN_MAX_LAYERS)]
 
 

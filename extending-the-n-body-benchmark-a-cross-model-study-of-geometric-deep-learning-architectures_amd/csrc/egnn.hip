@@ -10,6 +10,7 @@
 // edge MLP's input [h_row | h_col | radial, edge_attr] is gathered inside the
 // kernel's A loader (no concatenated edge tensor is materialised), and the two
 // 128 -> 1 heads (coord_mlp, coord_mlp_vel) are row dot products in the epilogue.
+#include <cstdlib>
 #include <cstring>
 
 #include "lin.h"
@@ -117,6 +118,322 @@ __global__ void egnn_headin_kernel(const float* __restrict__ coord, const float*
         HX[8 * v + 3 + k] = vel[3 * v + k];
     }
     HX[8 * v + 6] = HX[8 * v + 7] = 0.f;
+}
+
+// ===================================================================================================
+// Persistent per-system path: one workgroup per system runs preprocessing, every layer, both heads
+// and (for a rollout) every frame with the system's state in LDS — one launch per rollout instead of
+// ~60 per step.  GEMMs are block-wide fp32 FMA GEMMs over LDS activations (rows = the system's
+// N(N-1) <= 56 edges or N <= 8 nodes): thread (n, s) owns output column n and K-slice s, partial sums
+// are reduced through LDS in a fixed order (deterministic).  Weights come input-major from the
+// persist blob (include/nbx.h), each weight read once per workgroup per layer (coalesced over n).
+constexpr int EP_THREADS = 512, EP_NMAX = 8, EP_EMAX = EP_NMAX * (EP_NMAX - 1), EP_RC = 12;
+
+struct EgnnPersist {
+    const float* blob;
+    int L, N, heads, recurrent, norm_diff, use_tanh;
+    float coords_weight;
+    float* pos; float* vel; const float* mass;   // [B N 3], [B N 3], [B N]; pos / vel updated in place
+    int64_t frames;                              // 0: one forward into out; >= 1: rollout frames
+    int absolute;
+    float* traj_pos; float* traj_vel;            // [B][frames][N][3]
+    float* out;                                  // [B N][3 heads]
+};
+
+__device__ inline float ep_silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Y[r][n] = act(bias[n] + sum_k X[r][k] Wi[k][n]), r < rows, n < H; X, Y in LDS (row strides ldx, ldy,
+// ldx % 4 == 0), K % 4 == 0.  Register-blocked: a thread owns 4 adjacent columns and a K-slice, so each
+// broadcast LDS read of 4 k-values of a row feeds 16 FMAs; the K-slices held by one wave are summed
+// with lane shuffles, the 8 waves' partials through LDS in a fixed order.  All threads call it.
+template <int H>
+__device__ void ep_gemm(const float* X, int rows, int ldx, int K, const float* __restrict__ Wi,
+                        const float* __restrict__ bias, float* Y, int ldy, bool silu_act, float* part) {
+    constexpr int CG = H / 4;                  // column groups per wave (32, 16, 8)
+    constexpr int SPW = 64 / CG;               // K-slices per wave (2, 4, 8)
+    constexpr int S = SPW * (EP_THREADS / 64); // K-slices in the workgroup
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int cg = lane % CG, s = wave * SPW + lane / CG, n0 = 4 * cg;
+    const int Kc = (((K + S - 1) / S) + 3) & ~3;
+    const int k0 = min(K, s * Kc), k1 = min(K, k0 + Kc);
+    for (int r0 = 0; r0 < rows; r0 += EP_RC) {
+        const int rc = min(EP_RC, rows - r0);
+        float4 acc[EP_RC];
+#pragma unroll
+        for (int r = 0; r < EP_RC; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = k0; k < k1; k += 4) {
+            const float4 w0 = *reinterpret_cast<const float4*>(&Wi[(size_t)k * H + n0]);
+            const float4 w1 = *reinterpret_cast<const float4*>(&Wi[(size_t)(k + 1) * H + n0]);
+            const float4 w2 = *reinterpret_cast<const float4*>(&Wi[(size_t)(k + 2) * H + n0]);
+            const float4 w3 = *reinterpret_cast<const float4*>(&Wi[(size_t)(k + 3) * H + n0]);
+#pragma unroll
+            for (int r = 0; r < EP_RC; ++r) {
+                if (r < rc) {
+                    const float4 x = *reinterpret_cast<const float4*>(&X[(r0 + r) * ldx + k]);
+                    acc[r].x += x.x * w0.x + x.y * w1.x + x.z * w2.x + x.w * w3.x;
+                    acc[r].y += x.x * w0.y + x.y * w1.y + x.z * w2.y + x.w * w3.y;
+                    acc[r].z += x.x * w0.z + x.y * w1.z + x.z * w2.z + x.w * w3.z;
+                    acc[r].w += x.x * w0.w + x.y * w1.w + x.z * w2.w + x.w * w3.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < EP_RC; ++r) {
+            if (r < rc) {
+#pragma unroll
+                for (int o = CG; o < 64; o <<= 1) {       // the wave's K-slices (fixed order)
+                    acc[r].x += __shfl_xor(acc[r].x, o);
+                    acc[r].y += __shfl_xor(acc[r].y, o);
+                    acc[r].z += __shfl_xor(acc[r].z, o);
+                    acc[r].w += __shfl_xor(acc[r].w, o);
+                }
+                if (lane < CG) *reinterpret_cast<float4*>(&part[(wave * EP_RC + r) * H + n0]) = acc[r];
+            }
+        }
+        __syncthreads();
+        for (int o = tid; o < rc * H; o += EP_THREADS) {
+            const int r = o / H, nn = o - r * H;
+            float v = bias ? bias[nn] : 0.f;
+            for (int w = 0; w < EP_THREADS / 64; ++w) v += part[(w * EP_RC + r) * H + nn];
+            Y[(r0 + r) * ldy + nn] = silu_act ? ep_silu(v) : v;
+        }
+        __syncthreads();
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(EP_THREADS, 1) void egnn_persist_kernel(const EgnnPersist P) {
+    constexpr int LD_E = 2 * H + 8, LD_H8 = H + 8;
+    constexpr int LAYER = 8 * H * H + 16 * H + 4, HEAD = 2 * H * H + 14 * H + 4;
+    constexpr int S = EP_THREADS / 64;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* sA = lds;                                 // [EMAX][2H + 8]: edge input, later EF [E][H]
+    float* sB = sA + EP_EMAX * LD_E;                 // [EMAX][H]: EF1 / c0 out / v0 out / n0 out / head hidden
+    float* sH = sB + EP_EMAX * H;                    // [NMAX][H]
+    float* sHn = sH + EP_NMAX * H;                   // [NMAX][H]
+    float* sX = sHn + EP_NMAX * H;                   // [NMAX][2H]: node input [h | agg], heads [h | hx]
+    float* sP = sX + EP_NMAX * 2 * H;                // [S][RC][H] partial sums
+    float* sm = sP + S * EP_RC * H;                  // small state
+    float* pos0 = sm;             // [N][3]
+    float* coord = pos0 + 3 * EP_NMAX;
+    float* velv = coord + 3 * EP_NMAX;
+    float* mass = velv + 3 * EP_NMAX;            // [N]
+    float* ea = mass + EP_NMAX;                  // [E][4]
+    float* diff = ea + 4 * EP_EMAX;              // [E][3]
+    float* cdot = diff + 3 * EP_EMAX;            // [E]
+    float* vdot = cdot + EP_EMAX;                // [N]
+    float* pred = vdot + EP_NMAX;                // [N][6]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = P.N, deg = N - 1, E = N * deg;
+    const int64_t sys = blockIdx.x;
+    const float* emb_i = P.blob;
+    const float* emb_b = emb_i + 2 * H;
+    const float* layer0 = emb_b + H;
+    const float* head0 = layer0 + (size_t)P.L * LAYER;
+    auto erow = [&](int e) { return e / deg; };
+    auto ecol = [&](int e) { const int i = e / deg, j = e - i * deg; return j < i ? j : j + 1; };
+
+    for (int i = tid; i < 3 * N; i += EP_THREADS) {
+        pos0[i] = P.pos[sys * N * 3 + i];
+        velv[i] = P.vel[sys * N * 3 + i];
+    }
+    for (int i = tid; i < N; i += EP_THREADS) mass[i] = P.mass[sys * N + i];
+    __syncthreads();
+    auto write_frame = [&](int64_t f) {
+        for (int i = tid; i < 3 * N; i += EP_THREADS) {
+            P.traj_pos[((sys * P.frames) + f) * N * 3 + i] = pos0[i];
+            P.traj_vel[((sys * P.frames) + f) * N * 3 + i] = velv[i];
+        }
+    };
+    if (P.frames >= 1) write_frame(0);
+    const int64_t steps = P.frames >= 1 ? P.frames - 1 : 1;
+    for (int64_t f = 1; f <= steps; ++f) {
+        // ---- preprocess_batch (egnn_mc_n_body_dataloader.py:8-56): x = [|vel|, mass], edge_attr
+        for (int o = tid; o < N * H; o += EP_THREADS) {
+            const int i = o / H, n = o - i * H;
+            const float vx = velv[3 * i], vy = velv[3 * i + 1], vz = velv[3 * i + 2];
+            sH[i * H + n] = emb_b[n] + sqrtf(vx * vx + vy * vy + vz * vz) * emb_i[n] + mass[i] * emb_i[H + n];
+        }
+        for (int e = tid; e < E; e += EP_THREADS) {
+            const int r = erow(e), c = ecol(e);
+            const float dx = pos0[3 * r] - pos0[3 * c], dy = pos0[3 * r + 1] - pos0[3 * c + 1],
+                        dz = pos0[3 * r + 2] - pos0[3 * c + 2];
+            const float d2 = dx * dx + dy * dy + dz * dz, d = fmaxf(sqrtf(d2), 1e-12f);
+            const float hx = dx / d, hy = dy / d, hz = dz / d;
+            ea[4 * e] = mass[r] * mass[c];
+            ea[4 * e + 1] = velv[3 * r] * hx + velv[3 * r + 1] * hy + velv[3 * r + 2] * hz;
+            ea[4 * e + 2] = velv[3 * c] * hx + velv[3 * c + 1] * hy + velv[3 * c + 2] * hz;
+            ea[4 * e + 3] = d2;
+        }
+        for (int i = tid; i < 3 * N; i += EP_THREADS) coord[i] = pos0[i];
+        __syncthreads();
+        float* h = sH;
+        float* hn = sHn;
+        for (int l = 0; l < P.L; ++l) {
+            const float* Wl = layer0 + (size_t)l * LAYER;
+            const float *e0_i = Wl, *e0_b = e0_i + LD_E * H, *e1_i = e0_b + H, *e1_b = e1_i + H * H,
+                        *c0_i = e1_b + H, *c0_b = c0_i + H * H, *c1_w = c0_b + H, *v0_i = c1_w + H,
+                        *v0_b = v0_i + H * H, *v1_w = v0_b + H, *v1_b = v1_w + H, *n0_i = v1_b + 4,
+                        *n0_b = n0_i + 2 * H * H, *n1_i = n0_b + H, *n1_b = n1_i + H * H;
+            // coord2radial (egnn_mc.py:155-164) + edge input [h_row | h_col | radial, edge_attr]
+            for (int e = tid; e < E; e += EP_THREADS) {
+                const int r = erow(e), c = ecol(e);
+                float dx = coord[3 * r] - coord[3 * c], dy = coord[3 * r + 1] - coord[3 * c + 1],
+                      dz = coord[3 * r + 2] - coord[3 * c + 2];
+                const float radial = dx * dx + dy * dy + dz * dz;
+                if (P.norm_diff) {
+                    const float nrm = fmaxf(sqrtf(radial), 1.0f);
+                    dx /= nrm; dy /= nrm; dz /= nrm;
+                }
+                diff[3 * e] = dx; diff[3 * e + 1] = dy; diff[3 * e + 2] = dz;
+                float* x = sA + e * LD_E + 2 * H;
+                x[0] = radial; x[1] = ea[4 * e]; x[2] = ea[4 * e + 1]; x[3] = ea[4 * e + 2]; x[4] = ea[4 * e + 3];
+                x[5] = x[6] = x[7] = 0.f;
+            }
+            for (int o = tid; o < E * H; o += EP_THREADS) {
+                const int e = o / H, n = o - e * H;
+                sA[e * LD_E + n] = h[erow(e) * H + n];
+                sA[e * LD_E + H + n] = h[ecol(e) * H + n];
+            }
+            __syncthreads();
+            ep_gemm<H>(sA, E, LD_E, LD_E, e0_i, e0_b, sB, H, true, sP);       // edge_mlp[0] + SiLU
+            ep_gemm<H>(sB, E, H, H, e1_i, e1_b, sA, H, true, sP);             // edge_mlp[2] + SiLU -> EF
+            ep_gemm<H>(sA, E, H, H, c0_i, c0_b, sB, H, true, sP);             // coord_mlp[0] + SiLU
+            for (int e = wave; e < E; e += EP_THREADS / 64) {                   // coord_mlp[2] (no bias)
+                float v = 0.f;
+                for (int n = lane; n < H; n += 64) v += sB[e * H + n] * c1_w[n];
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+                if (lane == 0) cdot[e] = P.use_tanh ? tanhf(v) : v;
+            }
+            __syncthreads();
+            ep_gemm<H>(h, N, H, H, v0_i, v0_b, sB, H, true, sP);              // coord_mlp_vel[0] + SiLU
+            for (int i = wave; i < N; i += EP_THREADS / 64) {
+                float v = 0.f;
+                for (int n = lane; n < H; n += 64) v += sB[i * H + n] * v1_w[n];
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+                if (lane == 0) vdot[i] = v + v1_b[0];
+            }
+            for (int o = tid; o < N * H; o += EP_THREADS) {                   // node input [h | mean_j EF]
+                const int i = o / H, n = o - i * H;
+                float a = 0.f;
+                for (int q = 0; q < deg; ++q) a += sA[(i * deg + q) * H + n];
+                sX[i * 2 * H + n] = h[i * H + n];
+                sX[i * 2 * H + H + n] = deg > 0 ? a / (float)deg : 0.f;
+            }
+            __syncthreads();
+            ep_gemm<H>(sX, N, 2 * H, 2 * H, n0_i, n0_b, sB, H, true, sP);     // node_mlp[0] + SiLU
+            ep_gemm<H>(sB, N, H, H, n1_i, n1_b, hn, H, false, sP);            // node_mlp[2]
+            if (P.recurrent)
+                for (int o = tid; o < N * H; o += EP_THREADS) hn[o] += h[o];
+            // coord_model + velocity term (egnn_mc.py:135-153, 178-183)
+            for (int o = tid; o < 3 * N; o += EP_THREADS) {
+                const int i = o / 3, k = o - 3 * i;
+                float a = 0.f;
+                for (int q = 0; q < deg; ++q) {
+                    const int e = i * deg + q;
+                    a += fminf(fmaxf(diff[3 * e + k] * cdot[e], -100.f), 100.f);
+                }
+                coord[o] += (deg > 0 ? a / (float)deg : 0.f) * P.coords_weight + vdot[i] * velv[o];
+            }
+            __syncthreads();
+            float* t = h; h = hn; hn = t;
+        }
+        // ---- vector heads: [h | coord - pos, vel, 0, 0] -> SiLU -> SiLU -> 3
+        for (int o = tid; o < N * LD_H8; o += EP_THREADS) {
+            const int i = o / LD_H8, k = o - i * LD_H8;
+            float v = 0.f;
+            if (k < H) v = h[i * H + k];
+            else if (k < H + 3) v = coord[3 * i + k - H] - pos0[3 * i + k - H];
+            else if (k < H + 6) v = velv[3 * i + k - H - 3];
+            sX[i * LD_H8 + k] = v;
+        }
+        __syncthreads();
+        for (int t = 0; t < P.heads; ++t) {
+            const float* Wh = head0 + (size_t)t * HEAD;
+            const float *w0_i = Wh, *b0 = w0_i + LD_H8 * H, *w1_i = b0 + H, *b1 = w1_i + H * H, *w2_i = b1 + H,
+                        *b2 = w2_i + 4 * H;
+            ep_gemm<H>(sX, N, LD_H8, LD_H8, w0_i, b0, sB, H, true, sP);
+            ep_gemm<H>(sB, N, H, H, w1_i, b1, sA, H, true, sP);
+            for (int i = wave; i < N; i += EP_THREADS / 64) {
+                float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+                for (int n = lane; n < H; n += 64) {
+                    const float x = sA[i * H + n];
+                    v0 += x * w2_i[4 * n];
+                    v1 += x * w2_i[4 * n + 1];
+                    v2 += x * w2_i[4 * n + 2];
+                }
+                for (int o = 32; o > 0; o >>= 1) {
+                    v0 += __shfl_xor(v0, o);
+                    v1 += __shfl_xor(v1, o);
+                    v2 += __shfl_xor(v2, o);
+                }
+                if (lane == 0) {
+                    pred[6 * i + 3 * t] = v0 + b2[0];
+                    pred[6 * i + 3 * t + 1] = v1 + b2[1];
+                    pred[6 * i + 3 * t + 2] = v2 + b2[2];
+                }
+            }
+            __syncthreads();
+        }
+        if (P.frames == 0) {
+            for (int o = tid; o < N * 3 * P.heads; o += EP_THREADS) {
+                const int i = o / (3 * P.heads), k = o - i * 3 * P.heads;
+                P.out[(sys * N + i) * 3 * P.heads + k] = pred[6 * i + k];
+            }
+            return;
+        }
+        // ---- self-feed state update (infer_self_feed.py:182-194)
+        for (int o = tid; o < 3 * N; o += EP_THREADS) {
+            const int i = o / 3, k = o - 3 * i;
+            pos0[o] = P.absolute ? pred[6 * i + k] : pos0[o] + pred[6 * i + k];
+            velv[o] = pred[6 * i + 3 + k];
+        }
+        __syncthreads();
+        write_frame(f);
+    }
+    for (int i = tid; i < 3 * N; i += EP_THREADS) {
+        P.pos[sys * N * 3 + i] = pos0[i];
+        P.vel[sys * N * 3 + i] = velv[i];
+    }
+}
+
+size_t ep_lds_bytes(int H) {
+    const int S = EP_THREADS / 64;
+    const size_t fl = (size_t)EP_EMAX * (2 * H + 8) + EP_EMAX * H + 2 * EP_NMAX * H + EP_NMAX * 2 * H +
+                      (size_t)S * EP_RC * H + 3 * 3 * EP_NMAX + EP_NMAX + 4 * EP_EMAX + 3 * EP_EMAX + EP_EMAX +
+                      EP_NMAX + 6 * EP_NMAX;
+    return fl * 4;
+}
+
+bool ep_usable(const nbx_egnn_weights* w, int64_t N) {
+    static const bool off = getenv("NBX_EGNN_PERSIST") && getenv("NBX_EGNN_PERSIST")[0] == '0';
+    return !off && w->persist_blob && (w->hidden == 32 || w->hidden == 64 || w->hidden == 128) && N >= 2 &&
+           N <= EP_NMAX && w->num_heads >= 1 && w->num_heads <= 2;
+}
+
+template <int H>
+int ep_launch_h(const EgnnPersist& p, int64_t B, hipStream_t st) {
+    const size_t lds = ep_lds_bytes(H);
+    static bool attr = false;
+    if (!attr) {
+        NBX_HIP(hipFuncSetAttribute((const void*)egnn_persist_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(egnn_persist_kernel<H>, dim3((unsigned)B), dim3(EP_THREADS), lds, st, p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
+int ep_launch(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t B, int64_t N,
+              int64_t frames, int absolute, float* traj_pos, float* traj_vel, float* out, hipStream_t st) {
+    EgnnPersist p{w->persist_blob, w->num_layers, (int)N, w->num_heads, w->recurrent, w->norm_diff, w->use_tanh,
+                  w->coords_weight, pos, vel, mass, frames, absolute, traj_pos, traj_vel, out};
+    switch (w->hidden) {
+        case 32: return ep_launch_h<32>(p, B, st);
+        case 64: return ep_launch_h<64>(p, B, st);
+        default: return ep_launch_h<128>(p, B, st);
+    }
 }
 
 struct EgnnWs {
@@ -275,6 +592,9 @@ extern "C" int nbx_egnn_forward(const nbx_egnn_weights* w, const float* pos, con
                                 void* stream) {
     EgnnWs ws;
     if (int rc = egnn_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    if (ep_usable(w, N))   // frames = 0: one forward, pos / vel read only
+        return ep_launch(w, const_cast<float*>(pos), const_cast<float*>(vel), mass, B, N, 0, 0, nullptr, nullptr, out,
+                         (hipStream_t)stream);
     return egnn_forward_impl(w, pos, vel, mass, B, N, out, ws, (hipStream_t)stream);
 }
 
@@ -285,6 +605,9 @@ extern "C" int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* ve
     if (int rc = egnn_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     NBX_CHECK_ARG(num_frames >= 1 && w->num_heads == 2, "nbx_egnn_rollout: needs 2 heads (pos_dt, vel), frames >= 1");
     hipStream_t st = (hipStream_t)stream;
+    if (ep_usable(w, N))   // the whole rollout in one launch
+        return ep_launch(w, pos, vel, mass, B, N, num_frames, flags & NBX_ROLLOUT_ABSOLUTE, traj_pos, traj_vel, nullptr,
+                         st);
     const int64_t V = B * N;
     hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
                        num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);

@@ -154,7 +154,37 @@ class EGNNMultiChannel(nn.Module):
             P[p + "b1"] = vec(head.net[2].bias)
             P[p + "w2_t"] = pad_cols(head.net[4].weight.detach(), [(H, kp)])
             P[p + "b2"] = vec(head.net[4].bias)
+        P["persist_blob"] = self.persist_blob(device)
         return P
+
+    def persist_blob(self, device):
+        """The input-major weight blob of the persistent per-system kernel (include/nbx.h)."""
+        H = self.hidden_node_dim
+        f = dict(device=device, dtype=torch.float32)
+
+        def t(w, rows=None, cols=None):          # nn.Linear [out][in] -> [in][out], zero-padded
+            x = w.detach().to(**f).T
+            r, c = rows or x.shape[0], cols or x.shape[1]
+            return torch.nn.functional.pad(x, (0, c - x.shape[1], 0, r - x.shape[0])).reshape(-1)
+
+        def v(b, n=None):
+            x = b.detach().to(**f).reshape(-1)
+            return torch.nn.functional.pad(x, (0, (n or x.numel()) - x.numel()))
+
+        parts = [t(self.embedding.weight), v(self.embedding.bias)]
+        for L in self.layers:
+            parts += [t(L.edge_mlp[0].weight, rows=2 * H + 8), v(L.edge_mlp[0].bias), t(L.edge_mlp[2].weight),
+                      v(L.edge_mlp[2].bias), t(L.coord_mlp[0].weight), v(L.coord_mlp[0].bias),
+                      v(L.coord_mlp[2].weight), t(L.coord_mlp_vel[0].weight), v(L.coord_mlp_vel[0].bias),
+                      v(L.coord_mlp_vel[2].weight), v(L.coord_mlp_vel[2].bias, 4), t(L.node_mlp[0].weight),
+                      v(L.node_mlp[0].bias), t(L.node_mlp[2].weight), v(L.node_mlp[2].bias)]
+        for head in self.heads:
+            parts += [t(head.net[0].weight, rows=H + 8), v(head.net[0].bias), t(head.net[2].weight),
+                      v(head.net[2].bias), t(head.net[4].weight, cols=4), v(head.net[4].bias, 4)]
+        blob = torch.cat(parts).contiguous()
+        L_, nh = len(self.layers), len(self.heads)
+        assert blob.numel() == 3 * H + L_ * (8 * H * H + 16 * H + 4) + nh * (2 * H * H + 14 * H + 4)
+        return blob
 
     def pack_weights(self, device):
         P = self.packed_matrices(device)
@@ -163,6 +193,7 @@ class EGNNMultiChannel(nn.Module):
         W.recurrent, W.norm_diff, W.use_tanh = int(self.recurrent), int(self.norm_diff), int(self.use_tanh)
         W.coords_weight = float(self.coords_weight)
         W.emb_t, W.emb_b = P["emb_t"].data_ptr(), P["emb_b"].data_ptr()
+        W.persist_blob = P["persist_blob"].data_ptr()
         for i in range(self.num_layers):
             L = W.layers[i]
             for name, _ in L._fields_:

@@ -254,10 +254,20 @@ typedef struct nbx_egnn_head {
     const float* w2_t; const float* b2;   /* net.4 (-> 3) */
 } nbx_egnn_head;
 
+/* persist_blob (optional; NULL = the per-layer GEMM path): every weight once more, input-major
+ * ([K][out], "_i"), contiguous, for the persistent per-system kernel (one workgroup per system runs
+ * every layer, the heads and the whole rollout on chip; hidden in {32, 64, 128}, N <= 8):
+ *   emb_i [2][H] | emb_b [H]
+ *   per layer: e0_i [2H + 8][H] (h_row | h_col | radial, edge_attr[4], 0, 0, 0) | e0_b [H] | e1_i [H][H] |
+ *              e1_b | c0_i [H][H] | c0_b | c1_w [H] | v0_i [H][H] | v0_b | v1_w [H] | v1_b [4] (1 used) |
+ *              n0_i [2H][H] (h | agg) | n0_b | n1_i [H][H] | n1_b            (8 H^2 + 16 H + 4 floats)
+ *   per head:  w0_i [H + 8][H] (h | coord - pos, vel, 0, 0) | b0 [H] | w1_i [H][H] | b1 [H] |
+ *              w2_i [H][4] (3 used) | b2 [4]                                  (2 H^2 + 14 H + 4 floats) */
 typedef struct nbx_egnn_weights {
     int32_t hidden, num_layers, num_heads, recurrent, norm_diff, use_tanh;
     float coords_weight;
     const float* emb_t; const float* emb_b;
+    const float* persist_blob;
     nbx_egnn_head heads[2];
     nbx_egnn_layer layers[NBX_EGNN_MAX_LAYERS];
 } nbx_egnn_weights;
