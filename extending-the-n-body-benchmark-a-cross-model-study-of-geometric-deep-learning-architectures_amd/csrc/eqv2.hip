@@ -572,7 +572,7 @@ int gemm_x3(const float* A, int K, int rows, const void* Wx3, int N, const float
 // row-panel x3 GEMM over all N = 32 ntiles columns (chunk-major image; lin.h lin_rp_kernel)
 int gemm_rp(const float* A, int K, int rows, const void* Wx3, int ntiles, const float* bias, float* Y, int ldy,
             hipStream_t st) {
-    nbx::LinRpProb p{A, K, rows, K, Wx3, bias, Y, ldy, 32 * ntiles};
+    nbx::LinRpProb p{A, K, rows, K, Wx3, bias, Y, ldy, 32 * ntiles, nullptr, 0, nullptr};
     switch (ntiles) {
         case 4: return nbx::lin_rp_launch<4, nbx::ACT_NONE>(p, st);
         case 5: return nbx::lin_rp_launch<5, nbx::ACT_NONE>(p, st);

@@ -398,13 +398,19 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
                 const float b = (live && P.bias) ? P.bias[col] : 0.f;
                 const float sc = (live && P.scale) ? P.scale[col] : 1.f;
                 const float dw = (live && P.dotw) ? P.dotw[col] : 0.f;
+                float res[16];   // residual loads batched ahead of their uses
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    res[e] = (P.resid && live && row < P.rows) ? P.resid[(size_t)row * P.ldr + col] : 0.f;
+                }
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                     const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                     float y = lin_act(acc[j][e] + b, ACT);
                     dot[e] += y * dw;
                     if (live && row < P.rows && P.Y) {
-                        if (P.resid) y = P.resid[(size_t)row * P.ldr + col] + sc * y;
+                        if (P.resid) y = res[e] + sc * y;
                         P.Y[(size_t)row * P.ldy + col] = y;
                     }
                 }
@@ -486,6 +492,9 @@ struct LinRpProb {
     const float* bias;  // [NTILES * 32] or null
     float* Y;
     int ldy, N;         // N: columns stored (<= NTILES * 32)
+    const float* resid; // optional: Y = R + scale (.) act(...)  (R may alias Y)
+    int ldr;
+    const float* scale; // optional per-column scale (layer_scale)
 };
 
 constexpr int RP_WAVES = 8;
@@ -532,33 +541,94 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
             }
         }
     };
-    float4 cur[4];
-    tp_dma_image<RP_WAVES>(W, lds, SLAB);
-    load_a(0, cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kc = 0; kc < nk; ++kc) {
-        bf16x8 a[3][2];
-        tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
-        tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
-        if (kc + 1 < nk) {
-            load_a(kc + 1, cur);
-            tp_dma_image<RP_WAVES>(W + (size_t)(kc + 1) * SLAB, lds + ((kc + 1) & 1) * SLAB, SLAB);
+    if constexpr (NTILES <= 5) {
+        // small panels (N <= 160): three LDS slabs and two A register buffers, both streams issued two
+        // chunks ahead.  At the end of chunk kc only chunk kc + 2's slab pieces and A loads may still be
+        // in flight: vmcnt(this wave's slab pieces + 4) (the slab pieces per wave are counted so the
+        // immediate is exact).
+        const int ndma = (6 * NTILES - wave + RP_WAVES - 1) / RP_WAVES;
+        auto wait_all_but_one_chunk = [&]() {
+            switch (ndma) {
+                case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+                case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+                case 3: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+                case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+                default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+            }
+        };
+        float4 bA[4], bB[4];
+        tp_dma_image<RP_WAVES>(W, lds, SLAB);
+        load_a(0, bA);
+        if (nk > 1) {
+            tp_dma_image<RP_WAVES>(W + SLAB, lds + SLAB, SLAB);
+            load_a(1, bB);
+            wait_all_but_one_chunk();
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas(a, lds + (kc & 1) * SLAB);
+        __builtin_amdgcn_s_barrier();
+        auto step = [&](int kc, float4 (&cur)[4]) {
+            bf16x8 a[3][2];
+            tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
+            tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+            const bool ahead = kc + 2 < nk;
+            if (ahead) {
+                tp_dma_image<RP_WAVES>(W + (size_t)(kc + 2) * SLAB, lds + ((kc + 2) % 3) * SLAB, SLAB);
+                load_a(kc + 2, cur);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(a, lds + (kc % 3) * SLAB);
+            if (ahead)
+                wait_all_but_one_chunk();
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        };
+        for (int kc = 0; kc < nk; kc += 2) {
+            step(kc, bA);
+            if (kc + 1 < nk) step(kc + 1, bB);
+        }
+    } else {
+        float4 cur[4];
+        tp_dma_image<RP_WAVES>(W, lds, SLAB);
+        load_a(0, cur);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        __builtin_amdgcn_s_barrier();
+        for (int kc = 0; kc < nk; ++kc) {
+            bf16x8 a[3][2];
+            tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
+            tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+            if (kc + 1 < nk) {
+                load_a(kc + 1, cur);
+                tp_dma_image<RP_WAVES>(W + (size_t)(kc + 1) * SLAB, lds + ((kc + 1) & 1) * SLAB, SLAB);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(a, lds + (kc & 1) * SLAB);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
     }
 #pragma unroll
     for (int j = 0; j < NTILES; ++j) {
         const int col = 32 * j + r;
         const bool live = col < P.N;
         const float b = (live && P.bias) ? P.bias[col] : 0.f;
+        const float sc = (live && P.scale) ? P.scale[col] : 1.f;
+        // residual: all 16 loads of the tile issued before any use (one latency, not 16)
+        float res[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int rr = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            if (live && rr < P.rows) P.Y[(size_t)rr * P.ldy + col] = lin_act(acc[j][e] + b, ACT);
+            res[e] = (P.resid && live && rr < P.rows) ? P.resid[(size_t)rr * P.ldr + col] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int rr = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (live && rr < P.rows) {
+                float y = lin_act(acc[j][e] + b, ACT);
+                if (P.resid) y = res[e] + sc * y;
+                P.Y[(size_t)rr * P.ldy + col] = y;
+            }
         }
     }
 }
@@ -574,7 +644,7 @@ int lin_rp_launch(const LinRpProb& p, hipStream_t st) {
         set_error("lin_rp: A spans >= 2 GiB");
         return NBX_E_UNSUPPORTED;
     }
-    const size_t lds = 2 * (size_t)NTILES * LIN_X3_BLK * 4;
+    const size_t lds = (NTILES <= 5 ? 3 : 2) * (size_t)NTILES * LIN_X3_BLK * 4;
     static bool attr_set = false;
     if (!attr_set) {
         NBX_HIP(hipFuncSetAttribute((const void*)lin_rp_kernel<NTILES, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,

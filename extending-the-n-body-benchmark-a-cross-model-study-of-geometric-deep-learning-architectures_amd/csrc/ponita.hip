@@ -415,13 +415,26 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * VO * C * d.mlp, (double)VO * f4 * (C + d.mlp),
                                     [&] { return lin_auto<nbx::ACT_GELU>(p, st); }))
                 return rc;
-            LinProb q = nbx::lin_dense(ws.B1H1, d.mlp, d.mlp, (int)VO, Ly.lin2_t, kp(d.mlp), C, Ly.lin2_b, ws.X, C);
-            q.Wx3 = Ly.lin2_img_x3;
-            q.resid = ws.X;
-            q.ldr = C;
-            q.scale = Ly.layer_scale;
-            if (int rc = nbx::timed(tm, st, PK_LIN2, 2.0 * VO * C * d.mlp, (double)VO * f4 * (d.mlp + 2 * C),
-                                    [&] { return lin_auto<nbx::ACT_NONE>(q, st); }))
+            // linear_2 (K = 4C -> C): the row-panel kernel reads the [V O][4C] hidden activations once
+            // (the column-chunked kernel re-read them C / 32 times); the image is chunk-major
+            auto lin2 = [&]() -> int {
+                if (Ly.lin2_img_x3 && po_x3_enabled() && d.mlp % 32 == 0) {
+                    nbx::LinRpProb r{ws.B1H1, d.mlp, (int)VO, d.mlp, Ly.lin2_img_x3, Ly.lin2_b, ws.X, C, C,
+                                     ws.X, C, Ly.layer_scale};
+                    switch (C) {
+                        case 32: return nbx::lin_rp_launch<1, nbx::ACT_NONE>(r, st);
+                        case 64: return nbx::lin_rp_launch<2, nbx::ACT_NONE>(r, st);
+                        case 128: return nbx::lin_rp_launch<4, nbx::ACT_NONE>(r, st);
+                        default: break;
+                    }
+                }
+                LinProb q = nbx::lin_dense(ws.B1H1, d.mlp, d.mlp, (int)VO, Ly.lin2_t, kp(d.mlp), C, Ly.lin2_b, ws.X, C);
+                q.resid = ws.X;
+                q.ldr = C;
+                q.scale = Ly.layer_scale;
+                return lin_auto<nbx::ACT_NONE>(q, st);
+            };
+            if (int rc = nbx::timed(tm, st, PK_LIN2, 2.0 * VO * C * d.mlp, (double)VO * f4 * (d.mlp + 2 * C), lin2))
                 return rc;
         }
         if (Ly.readout_w) {

@@ -245,6 +245,9 @@ class PONITA_NBODY(nn.Module):
             W = P[key]
             if W.shape[0] % 32 == 0:
                 P[name] = self.lin_image_x3(W)
+                if name.endswith("lin2_img_x3"):   # the row-panel kernel streams K chunks: chunk-major
+                    img = P[name]
+                    P[name] = img.reshape(img.shape[0], W.shape[1] // 32, -1).transpose(0, 1).contiguous()
         return P
 
     @staticmethod

@@ -315,7 +315,8 @@ typedef struct nbx_ponita_layer {
     const float* layer_scale;         /* [C] or NULL */
     const float* readout_w; const float* readout_b;  /* read_out_layers[i] or NULL */
     /* optional bf16x3 images of kernel_t / lin1_t / lin2_t (NULL: fp32 MFMA path): the
-     * "bf16x3 images" layout with CW = 32 and one sub-tile, [N/32][K/32][3][2][64][8] bf16 */
+     * "bf16x3 images" layout with CW = 32 and one sub-tile, [N/32][K/32][3][2][64][8] bf16;
+     * lin2's image is chunk-major, [K/32][N/32][3][2][64][8] (the row-panel GEMM streams K chunks) */
     const void* kernel_img_x3;
     const void* lin1_img_x3;
     const void* lin2_img_x3;
