@@ -1,6 +1,6 @@
 """N-body dataloaders of the plugin registry — drop-ins for
 dataloaders/{base_dataloader,n_body_dataloader,segnn_n_body_dataloader,
-ponita_n_body_dataloader,egnn_mc_n_body_dataloader}.py.
+ponita_n_body_dataloader,egnn_mc_n_body_dataloader,equiformer_v2_n_body_dataloader}.py.
 
 ``preprocess_batch`` builds the graph the native models consume: positions,
 velocities, masses and the (device-built, bit-exact) fully-connected
@@ -22,7 +22,7 @@ from .dataset import GravityDatasetOtf
 from .graph import build_graph_with_knn
 
 __all__ = ["get_device", "BaseDataLoader", "NBodyDataLoader", "SegnnNBodyDataLoader", "PonitaNBodyDataLoader",
-           "EgnnMcNBodyDataLoader"]
+           "EgnnMcNBodyDataLoader", "EquiformerV2NBodyDataLoader"]
 
 
 def get_device(gpu_id=None):
@@ -146,4 +146,21 @@ class EgnnMcNBodyDataLoader(NBodyDataLoader):
             batch.batch = torch.arange(self.args.batch_size, device=device).repeat_interleave(n).long()
         if getattr(batch, "mass", None) is None:
             batch.mass = torch.ones(batch.vel.size(0), 1, device=device, dtype=batch.vel.dtype)
+        return batch
+
+
+class EquiformerV2NBodyDataLoader(NBodyDataLoader):
+    """dataloaders/equiformer_v2_n_body_dataloader.py:7-58: kNN (here: min(max_neighbors, N-1))
+    edge index, node_type zeros, edge_attr = |pos_row - pos_col|, node_attr = vel, x = mass."""
+
+    def preprocess_batch(self, data, device, training=True):
+        batch = data.to(device)
+        n_nodes = self.dataset.num_nodes
+        k = min(getattr(self.args, "max_neighbors", min(n_nodes - 1, 32)), n_nodes - 1)
+        self._edges(batch, device, k)
+        row, col = batch.edge_index
+        batch.node_type = torch.zeros(self.args.batch_size * n_nodes, dtype=torch.long, device=device)
+        batch.edge_attr = torch.norm(batch.pos[row] - batch.pos[col], dim=-1, keepdim=True)
+        batch.node_attr = batch.vel
+        batch.x = batch.mass
         return batch

@@ -33,7 +33,7 @@ __all__ = ["run_inference", "load_model_for_inference", "SelfFeedError", "MACROS
 
 MACROS_DIR_NAME = "visualize_macros"
 STEPS_TO_RETURN_MULTIPLIER = 100
-NATIVE_MODEL_TYPES = ("segnn", "ponita", "egnn_mc")
+NATIVE_MODEL_TYPES = ("segnn", "ponita", "egnn_mc", "equiformer_v2")
 
 
 class SelfFeedError(RuntimeError):
@@ -101,11 +101,25 @@ def load_model_for_inference(model_path, model_type, device):
     """utils/nbody_utils.py:1316-1373 + load_checkpoint (:1376-1407): the family's default
     constructor, the checkpoint's ``model_state_dict`` (or a bare state_dict), then
     ``eval()`` on ``device``.  Checkpoints are read with ``torch.load(weights_only=True)``
-    (tensors and plain containers only).  Like the reference, only segnn / ponita load here."""
+    (tensors and plain containers only).  Like the reference: equiformer(_v2), segnn, ponita."""
+    from .equiformer_v2 import EquiformerV2_nbody
     from .ponita import PONITA_NBODY
     from .segnn import SEGNN
     print(f"Initializing model of type '{model_type}' on device {device}")
-    if model_type == "segnn":
+    if model_type == "equiformer":
+        model = EquiformerV2_nbody(device)
+    elif model_type == "equiformer_v2":   # nbody_utils.py:1324-1361
+        model = EquiformerV2_nbody(
+            device=device, use_pbc=False, regress_forces=True, otf_graph=True, max_neighbors=5, max_radius=4096.0,
+            max_num_elements=90, num_layers=3, attn_hidden_channels=32, sphere_channels=32, num_heads=2,
+            attn_alpha_channels=8, attn_value_channels=4, ffn_hidden_channels=64, norm_type="rms_norm_sh",
+            lmax_list=[2], mmax_list=[1], grid_resolution=None, num_sphere_samples=32, edge_channels=32,
+            use_atom_edge_embedding=True, share_atom_edge_embedding=False, use_m_share_rad=False,
+            distance_function="projection", num_distance_basis=64, attn_activation="scaled_silu",
+            use_s2_act_attn=False, use_attn_renorm=True, ffn_activation="scaled_silu", use_gate_act=False,
+            use_grid_mlp=False, use_sep_s2_act=True, alpha_drop=0.01, drop_path_rate=0.0, proj_drop=0.0,
+            weight_init="normal")
+    elif model_type == "segnn":
         model = SEGNN()
     elif model_type == "ponita":
         model = PONITA_NBODY()

@@ -31,7 +31,7 @@ def test_parse_args_defaults_and_overrides():
 
 def test_parse_args_rejects_unknown_plugins_and_bad_class_paths(tmp_path):
     with pytest.raises(ValueError):
-        parse_args(["--model_type", "equiformer_v2"])
+        parse_args(["--model_type", "painn"])
     with pytest.raises(Exception):
         parse_args(["--model.class_path", "nbody_amd.nope.Missing"])
 
@@ -40,6 +40,8 @@ def test_parse_args_rejects_unknown_plugins_and_bad_class_paths(tmp_path):
     ("segnn", "segnn_nbody", "SEGNN", lambda m: sum(p.numel() for p in m.parameters()) == 1947552),
     ("ponita", "ponita_nbody", "PONITA_NBODY", lambda m: m.hidden_dim == 128 and m.layers == 6),
     ("egnn_mc", "egnn_mc_nbody", "EGNNMultiChannel", lambda m: m.target_names == ("pos_dt", "vel")),
+    ("equiformer_v2", "equiformer_v2_nbody", "EquiformerV2_nbody",
+     lambda m: (m.num_layers, m.sphere_channels, m.lmax_list, m.mmax_list) == (3, 32, [2], [1])),
 ])
 def test_create_model(model_type, dl, cls, check):
     args, _ = parse_args(["--model_type", model_type, "--dataloader_type", dl])
@@ -47,6 +49,44 @@ def test_create_model(model_type, dl, cls, check):
     m = create_model(args)
     assert type(m).__name__ == cls and check(m)
     assert load_class_from_args(args, "dataloader").__name__.lower().startswith(model_type.replace("_", ""))
+
+
+def test_inference_builds_equiformer_v2_config(tmp_path):
+    """nbody_utils.py:1322-1361: run_inference's equiformer_v2 branch (3 layers, 32 channels),
+    loading a checkpoint written in the reference's {"model_state_dict": ...} layout."""
+    from nbody_amd.equiformer_v2 import EquiformerV2_nbody
+    torch.manual_seed(1)
+    src = EquiformerV2_nbody(num_layers=3, attn_hidden_channels=32, sphere_channels=32, num_heads=2,
+                             attn_alpha_channels=8, attn_value_channels=4, ffn_hidden_channels=64, lmax_list=[2],
+                             mmax_list=[1], edge_channels=32, num_distance_basis=64)
+    torch.save({"model_state_dict": src.state_dict()}, tmp_path / "ckpt.pth")
+    m = I.load_model_for_inference(str(tmp_path / "ckpt.pth"), "equiformer_v2", "cpu")
+    for (k, a), b in zip(src.state_dict().items(), m.state_dict().values()):
+        assert torch.equal(a, b), k
+    assert (m.num_layers, m.sphere_channels, m.num_heads, m.ffn_hidden_channels, m.alpha_drop) == (3, 32, 2, 64, 0.01)
+    assert "equiformer_v2" in I.NATIVE_MODEL_TYPES
+
+
+def test_equiformer_v2_dataloader_attributes(monkeypatch):
+    """equiformer_v2_n_body_dataloader.py:8-50 host logic; the device kNN builder is swapped for the
+    oracle's (its own parity is in tests/test_gpu_native.py)."""
+    import nbody_amd.dataloaders as DL
+    from oracle import graph as og
+    monkeypatch.setattr(DL, "build_graph_with_knn", lambda pos, B, n, dev, k: torch.as_tensor(
+        og.build_graph_with_knn(pos.numpy(), B, n, k)))
+    EquiformerV2NBodyDataLoader = DL.EquiformerV2NBodyDataLoader
+    args, _ = parse_args(["--model_type", "equiformer_v2", "--dataloader_type", "equiformer_v2_nbody",
+                          "--dataloader.batch_size", "2", "--dataloader.gravity_dataset.num_atoms", "4"])
+    dl = EquiformerV2NBodyDataLoader.__new__(EquiformerV2NBodyDataLoader)
+    dl.args = args
+    dl.dataset = type("DS", (), {"num_nodes": 4})()
+    pos = torch.randn(8, 3, dtype=torch.float64)
+    b = dl.preprocess_batch(Batch.from_data_list([Data(pos=pos[i * 4:(i + 1) * 4], vel=torch.randn(4, 3),
+                                                       mass=torch.ones(4, 1)) for i in range(2)]), "cpu")
+    assert b.edge_index.shape == (2, 2 * 4 * 3)          # min(max_neighbors=5, N-1) = 3 neighbours
+    row, col = b.edge_index
+    torch.testing.assert_close(b.edge_attr[:, 0], (pos[row] - pos[col]).norm(dim=-1))
+    assert b.node_type.shape == (8,) and torch.equal(b.x, b.mass) and torch.equal(b.node_attr, b.vel)
 
 
 def test_segnn_needs_segnn_dataloader():
