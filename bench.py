@@ -212,9 +212,10 @@ def pmc_traffic(kernel_name, model=None):
 
 
 # ---------------------------------------------------------------- C3 PONITA
-# rocprofv3 names at C3 with the bf16x3 images (ponita.hip lin_auto: PREC = 1, NT by the image's LDS size)
+# rocprofv3 names at C3 with the bf16x3 images (ponita.hip lin_auto: PREC = 1, NT by the image's LDS size;
+# linear_2 on the row-panel kernel: 128 output columns = 4 tiles)
 PONITA_KIND_NAMES = ["void nbx::lin_kernel<4, 0, 1, 1>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0, 1>(nbx::LinProb)",
-                     "void nbx::lin_kernel<1, 0, 0, 1>(nbx::LinProb)", "void nbx::lin_kernel<4, 2, 0, 1>(nbx::LinProb)",
+                     "void nbx::lin_rp_kernel<4, 0>(nbx::LinRpProb)", "void nbx::lin_kernel<4, 2, 0, 1>(nbx::LinProb)",
                      "void (anonymous namespace)::po_fiber_ln_kernel<20, 4>(float const*, float const*, int, "
                      "float const*, float const*, float const*, long, int, int, int, float*, double*)"]
 PONITA_KIND_ROLES = ["FiberBundleConv spatial kernel GEMM + gather/aggregate epilogue", "ConvNext linear_1 + GELU",
@@ -370,7 +371,9 @@ EQV2_KINDS = ["radial hidden layers (per-edge layer + GEMM with LayerNorm/SiLU e
               "radial output GEMM + rotated-message epilogue (A0/A1)", "SO(2) conv 1, m=0 GEMM",
               "SO(2) conv 1, m=1 GEMM", "separable S2 activation + attention logits", "SO(2) conv 2 GEMMs",
               "node kernels (softmax, inverse rotation, proj, FFN, norms)", "edge frame + edge-degree embedding"]
-EQV2_GEMM = "void nbx::lin_kernel<2, 0, 0, 1>(nbx::LinProb)"   # kinds 2, 3, 5 (4 launches per attention)
+# rocprofv3 names of the one-launch GEMM kinds at C4 (eqv2.hip gemm_rp: row-panel bf16x3, all output
+# columns per workgroup; 288 = 32 alpha + 4 x 64 hidden m=0 outputs -> 9 tiles, 4 x 64 m=1 outputs -> 8)
+EQV2_GEMM_NAMES = {2: "void nbx::lin_rp_kernel<9, 0>(nbx::LinRpProb)", 3: "void nbx::lin_rp_kernel<8, 0>(nbx::LinRpProb)"}
 
 
 def bench_eqv2(a, rank, world, device, P):
@@ -412,21 +415,21 @@ def bench_eqv2(a, rank, world, device, P):
             per_kind[EQV2_KINDS[k]] = {"avg_group_us": round(sec / acc[1, k] * 1e6, 2),
                                        "tflops": round(acc[2, k] / sec / 1e12, 3),
                                        "gbs": round(acc[3, k] / sec / 1e9, 1), "share_of_forward": round(acc[0, k] / fwd, 3)}
-    # dominant kernel: the bf16x3 SO(2) GEMM kernel (kinds 2, 3, 5: 4 launches per attention block)
-    g_ms = acc[0, 2] + acc[0, 3] + acc[0, 5]
-    g_n = acc[1, 2] + acc[1, 3] + 2 * acc[1, 5]
-    g_fl = acc[2, 2] + acc[2, 3] + acc[2, 5]
-    g_avg_s = g_ms / g_n / 1e3
-    ach = g_fl / (g_ms / 1e3) / 1e12
-    roof = {"bound": "mfma", "kernel": EQV2_GEMM, "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": pmc_traffic(EQV2_GEMM, "eqv2"), "avg_launch_us": round(g_avg_s * 1e6, 2),
-            "gflop_per_launch": round(g_fl / g_n / 1e9, 4),
+    # dominant kernel: the larger of the two SO(2) conv 1 row-panel GEMMs (one launch per attention block each)
+    dom = max(EQV2_GEMM_NAMES, key=lambda k: acc[0, k])
+    g_avg_s = acc[0, dom] / acc[1, dom] / 1e3
+    ach = acc[2, dom] / (acc[0, dom] / 1e3) / 1e12
+    gemm_ms = acc[0, 2] + acc[0, 3] + acc[0, 5]
+    roof = {"bound": "mfma", "kernel": EQV2_GEMM_NAMES[dom], "role": EQV2_KINDS[dom], "achieved": round(ach, 3),
+            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": pmc_traffic(EQV2_GEMM_NAMES[dom], "eqv2"), "avg_launch_us": round(g_avg_s * 1e6, 2),
+            "gflop_per_launch": round(acc[2, dom] / acc[1, dom] / 1e9, 4),
+            "algorithmic_mb_per_launch": round(acc[3, dom] / acc[1, dom] / 1e6, 3),
             "mfma_path": "bf16x3 split (fp32-accurate), v_mfma_f32_32x32x16_bf16",
             "executed_bf16_tflops": round(ach * X3_TERMS, 2),
             "executed_bf16_frac": round(ach * X3_TERMS / BF16_MFMA_PEAK_TFLOPS, 4),
             "timing": "HIP event pairs around each launch group on the launch stream",
-            "gemm_share_of_forward": round(g_ms / fwd, 3), "per_kind": per_kind}
+            "gemm_share_of_forward": round(gemm_ms / fwd, 3), "per_kind": per_kind}
     value = a.steps / elapsed * world
     result = {
         "metric": "self-feed rollout steps/sec, EquiformerV2 N=20 batch=256", "value": round(value, 3),
