@@ -1,5 +1,10 @@
-timeout -k 5 60 ./tools/hazard/mfma_war > gpurun_out/mfma_war.txt 2>&1
-cat gpurun_out/mfma_war.txt
-timeout -k 10 400 python -u -m pytest tests/test_ponita.py tests/test_gpu_segnn.py::test_rollout_c2_matches_oracle_fixture -m gpu -v -s -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/t4.log 2>&1
-grep -E "C2 |passed|failed|Error|PASS|FAIL" gpurun_out/t4.log | tail -30
-for v in "" "NBX_PO_X3=0"; do timeout -k 10 200 env $v python bench.py --model ponita --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/po_$v.json 2>gpurun_out/po_err.txt || { tail -5 gpurun_out/po_err.txt; exit 1; }; python -c "import json;d=json.load(open('gpurun_out/po_$v.json'));print('$v', d['value'], {k[:20]:v['avg_launch_us'] for k,v in d['roofline']['per_kind'].items()})"; done
+#!/bin/bash
+# scratch GPU step: staging probe + SEGNN bench + SEGNN GPU tests
+set -u
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+mkdir -p gpurun_out
+NBX_STAGE_PROBE=1 NBX_TP_DEBUG=1 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/dbg1.json 2> gpurun_out/dbg1.err || exit 1
+grep "tp_debug" gpurun_out/dbg1.err | sed -n '60,63p'
+timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline > gpurun_out/b1.json 2>/dev/null || exit 1
+python -c "import json;d=json.load(open('gpurun_out/b1.json'));print('segnn', d['value'], d['ms_per_step'], {k[:30]:v['avg_launch_us'] for k,v in d['roofline']['per_kind'].items()})"
+timeout -k 10 300 python -m pytest tests/test_gpu_segnn.py tests/test_gpu_rollout.py -m gpu -q -x -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1; tail -3 gpurun_out/t.log
