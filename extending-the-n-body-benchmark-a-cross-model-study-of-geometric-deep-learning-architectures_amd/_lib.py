@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 6
+ABI_VERSION = 7
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
@@ -65,7 +65,7 @@ PONITA_MAX_LAYERS = 64
 class PonitaLayer(ctypes.Structure):
     _fields_ = [(n, c_p) for n in ("kernel_t", "conv_bias", "norm_w", "norm_b", "lin1_t", "lin1_b", "lin2_t",
                                    "lin2_b", "layer_scale", "readout_w", "readout_b", "kernel_img_x3",
-                                   "lin1_img_x3", "lin2_img_x3")]
+                                   "lin1_img_x3", "lin2_img_x3", "ffn_img_x3")]
 
 
 class PonitaWeights(ctypes.Structure):

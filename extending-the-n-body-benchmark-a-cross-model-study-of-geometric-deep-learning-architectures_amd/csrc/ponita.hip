@@ -22,6 +22,8 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <cstdio>
+#include <vector>
 
 #include "launch_timer.h"
 #include "lin.h"
@@ -302,6 +304,350 @@ size_t po_carve(PoWs* ws, void* base, const PoDims& d) {
 
 inline int kp(int k) { return (k + 31) & ~31; }
 
+// ---- fused ConvNext MLP (nn/convnext.py:19-27): X = X + s * (GELU(XN W1' + b1) W2' + b2), with the
+// [rows][4C] hidden activation kept in registers.  A workgroup owns FFN_WAVES x 32 fibre-point rows;
+// each wave holds its 32 x C input rows pre-split into bf16x3 MFMA operands and walks the hidden
+// dimension in 32-wide chunks j:
+//   GEMM 1  D1 = W1[32j..32j+31, :] x XN^T (32 hidden x 32 rows, v_mfma_f32_32x32x16_bf16 with the
+//           weights as the A operand), so lane (row = lane & 31, h = lane >> 5) ends up holding
+//           hidden units (e & 3) + 8 (e >> 2) + 4 h of its own row in register e;
+//   GELU    + b1 (branch-free erfc form), split into bf16x3 in place: registers 8m..8m+7 are the A
+//           operand of MFMA step m;
+//   GEMM 2  acc[t] += H_j x W2'[.., 32t..32t+31] for the C/32 output tiles; the weight image's K
+//           order is permuted on the host to match the registers (ponita.py _ffn_image), so the
+//           hidden activations never leave the lane that computed them.
+// Software pipeline: iteration j issues GEMM 1 of chunk j + 1 beside chunk j's GELU and GEMM 2.
+// The weights stream through two LDS rings of three buffers (W1 chunks, W2 chunks; C/32 blocks of
+// 6 KiB each) by LDS-DMA, W1 three chunks and W2 two chunks ahead of use, with an exact vmcnt (the
+// DMA pieces per wave are counted; nothing else is in flight inside the loop).  HBM traffic: XN and
+// X read once, X written once; the 4C-wide hidden activation (839 MB per layer at C3) is never stored.
+constexpr int FFN_WAVES = 4;
+
+// exact-GELU 0.5 x (1 + erf(x / sqrt2)) = 0.5 x erfc(-x / sqrt2) without branches (OCML's erff
+// branches on |x|, which splits the MFMA loop into basic blocks the scheduler cannot interleave):
+// erfc(z) = t exp(-z^2 + P(t)), t = 1 / (1 + z / 2), z >= 0, with the Chebyshev-fitted P of
+// Numerical Recipes (erfcc, fractional error < 1.2e-7 everywhere), and erfc(-z) = 2 - erfc(z).
+// Max |error| over [-12, 12] in fp32: 3.8e-7 (the erff form: 4.5e-7).
+__device__ inline float gelu_nb(float x) {
+    const float u = x * 0.70710678118654752f, z = fabsf(u);
+    const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);
+    float p = 0.17087277f;
+    p = fmaf(p, t, -0.82215223f);
+    p = fmaf(p, t, 1.48851587f);
+    p = fmaf(p, t, -1.13520398f);
+    p = fmaf(p, t, 0.27886807f);
+    p = fmaf(p, t, -0.18628806f);
+    p = fmaf(p, t, 0.09678418f);
+    p = fmaf(p, t, 0.37409196f);
+    p = fmaf(p, t, 1.00002368f);
+    p = fmaf(p, t, -1.26551223f);
+    const float ec = t * __expf(fmaf(-z, z, p));
+    return 0.5f * x * (u >= 0.f ? 2.0f - ec : ec);
+}
+
+struct FfnProb {
+    const float* XN;      // [rows][C] LayerNorm output (GEMM 1 input)
+    float* X;             // [rows][C] residual in, layer output (in place)
+    const void* img;      // [F/32] slabs [W1 chunk | W2 chunk] (include/nbx.h ffn_img_x3)
+    const float* b1;      // [F]
+    const float* b2;      // [C]
+    const float* scale;   // [C] layer_scale or null
+    int64_t rows;
+    int F;                // hidden width (multiple of 32, <= FFN_FMAX)
+    unsigned long long* dbg;   // tuning only (NBX_PO_FFN_DEBUG): per-wave phase clocks [4]
+};
+constexpr int FFN_FMAX = 1024;
+
+template <int NT>   // NT = C / 32
+__global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb P) {
+    using nbx::bf16x8;
+    using nbx::floatx16;
+    constexpr int C = NT * 32;
+    constexpr int PART = NT * nbx::LIN_X3_BLK;   // floats of one chunk's W1 (or W2) blocks
+    constexpr int PW = PART / 256 / FFN_WAVES;    // DMA pieces per wave per part
+    static_assert(PART % (256 * FFN_WAVES) == 0, "po_ffn: a part must split evenly over the waves");
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* ring1 = lds;                 // 3 x PART: W1 chunks (chunk c in slot c % 3)
+    float* ring2 = lds + 3 * PART;      // 3 x PART: W2 chunks
+    float* b1s = lds + 6 * PART;        // [F]
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+    const int nj = P.F >> 5;
+    const int64_t row0 = ((int64_t)blockIdx.x * FFN_WAVES + wave) * 32;
+    const int64_t row = row0 + r;
+    const bool ok = row < P.rows;
+    const float* img = reinterpret_cast<const float*>(P.img);
+    const unsigned long long c0t = P.dbg ? clock64() : 0ull;
+    auto w1src = [&](int j) { return img + (size_t)j * 2 * PART; };
+    auto w2src = [&](int j) { return img + (size_t)j * 2 * PART + PART; };
+
+    // prologue: input rows (lane (row, h) holds k = 32 kc + 16 h + 8 m + i, the image K order), b1,
+    // W1 chunks 0-2 and W2 chunk 0; W2 chunk 1 then goes in flight
+    bf16x8 ax[NT][3][2];
+    {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.XN, (short)0, 0x7FFFFFF0, 0x00020000);
+        const uint32_t base = (uint32_t)(((ok ? row : 0) * C + 16 * h) * 4);
+        float4 a[NT][4];
+#pragma unroll
+        for (int kc = 0; kc < NT; ++kc)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                a[kc][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, ok ? base + (uint32_t)(kc * 128 + 16 * q) : 0x7FFFFFF0u, 0, 0));
+        float bv[FFN_FMAX / (64 * FFN_WAVES)];
+#pragma unroll
+        for (int u = 0; u < FFN_FMAX / (64 * FFN_WAVES); ++u) {
+            const int i = t + u * 64 * FFN_WAVES;
+            bv[u] = i < P.F ? P.b1[i] : 0.f;
+        }
+        for (int c = 0; c < 3 && c < nj; ++c) nbx::tp_dma_image<FFN_WAVES>(w1src(c), ring1 + c * PART, PART);
+        nbx::tp_dma_image<FFN_WAVES>(w2src(0), ring2, PART);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < FFN_FMAX / (64 * FFN_WAVES); ++u) {
+            const int i = t + u * 64 * FFN_WAVES;
+            if (i < P.F) b1s[i] = bv[u];
+        }
+#pragma unroll
+        for (int kc = 0; kc < NT; ++kc) {
+            nbx::tp_split3(a[kc][0], a[kc][1], ax[kc][0][0], ax[kc][1][0], ax[kc][2][0]);
+            nbx::tp_split3(a[kc][2], a[kc][3], ax[kc][0][1], ax[kc][1][1], ax[kc][2][1]);
+        }
+        // the input operands live in AGPRs for the whole loop (MFMA reads A/B from either file), which
+        // leaves the architectural VGPRs to the weight fragments and the GELU arithmetic
+#pragma unroll
+        for (int kc = 0; kc < NT; ++kc)
+#pragma unroll
+            for (int p3 = 0; p3 < 3; ++p3)
+#pragma unroll
+                for (int m = 0; m < 2; ++m) asm volatile("" : "+a"(ax[kc][p3][m]));
+    }
+    __syncthreads();
+    if (nj > 1) nbx::tp_dma_image<FFN_WAVES>(w2src(1), ring2 + PART, PART);
+
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    // GEMM 1 of one hidden chunk into one accumulator (a dependent chain of v_mfma_f32_32x32x16_bf16
+    // issues at full rate; the first MFMA takes an inline 0 accumulator)
+    auto gemm1 = [&](const float* buf) {
+        // all of the chunk's fragments are read first (one LDS latency per chunk, not per 6 MFMAs)
+        const bf16x8* w1 = reinterpret_cast<const bf16x8*>(buf) + lane;
+        bf16x8 b[NT][2][3];
+#pragma unroll
+        for (int kc = 0; kc < NT; ++kc)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int p3 = 0; p3 < 3; ++p3) b[kc][m][p3] = w1[kc * (nbx::LIN_X3_BLK / 4) + m * 64 + p3 * 128];
+        floatx16 g;
+#pragma unroll
+        for (int kc = 0; kc < NT; ++kc)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const bf16x8(&a)[3][2] = ax[kc];
+                const bf16x8(&w)[3] = b[kc][m];
+                if (kc == 0 && m == 0)
+                    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[2][m], floatx16{}, 0, 0, 0);
+                else
+                    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[2][m], g, 0, 0, 0);
+                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a[1][m], g, 0, 0, 0);
+                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], a[0][m], g, 0, 0, 0);
+                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[1][m], g, 0, 0, 0);
+                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a[0][m], g, 0, 0, 0);
+                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[0][m], g, 0, 0, 0);
+            }
+        return g;
+    };
+    // b1 + GELU of chunk j's GEMM 1 result, split into the GEMM 2 A operand (registers 8m..8m+7 ->
+    // MFMA step m)
+    auto gelu_split = [&](int j, const floatx16& g, bf16x8 (&hx)[3][2]) {
+        float hv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) hv[e] = gelu_nb(g[e] + b1s[32 * j + (e & 3) + 8 * (e >> 2) + 4 * h]);
+        nbx::tp_split3(float4{hv[0], hv[1], hv[2], hv[3]}, float4{hv[4], hv[5], hv[6], hv[7]}, hx[0][0], hx[1][0], hx[2][0]);
+        nbx::tp_split3(float4{hv[8], hv[9], hv[10], hv[11]}, float4{hv[12], hv[13], hv[14], hv[15]}, hx[0][1], hx[1][1],
+                       hx[2][1]);
+    };
+    auto gemm2 = [&](const float* buf, const bf16x8 (&hx)[3][2]) {
+        const bf16x8* w2 = reinterpret_cast<const bf16x8*>(buf) + lane;
+        bf16x8 b[NT][2][3];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int p3 = 0; p3 < 3; ++p3) b[tt][m][p3] = w2[tt * (nbx::LIN_X3_BLK / 4) + m * 64 + p3 * 128];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const bf16x8(&w)[3] = b[tt][m];
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[2][m], w[0], acc[tt], 0, 0, 0);
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[1][m], w[1], acc[tt], 0, 0, 0);
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[0][m], w[2], acc[tt], 0, 0, 0);
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[1][m], w[0], acc[tt], 0, 0, 0);
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[0][m], w[1], acc[tt], 0, 0, 0);
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[0][m], w[0], acc[tt], 0, 0, 0);
+            }
+    };
+    // Two-deep software pipeline: iteration j issues GEMM 1 of chunk j + 2 and GEMM 2 of chunk j
+    // (96 MFMAs, none waiting on VALU work) and, between them, GELU + split of chunk j + 1 (whose
+    // GEMM 1 ran in iteration j - 1); scheduling groups interleave ~4 vector instructions per MFMA.
+    // Rings: iteration j reads W1 chunk j + 2 and W2 chunk j; it refills W1 slot j % 3 with chunk
+    // j + 3 (needed next iteration) and W2 slot (j + 2) % 3 with chunk j + 2.
+    floatx16 gq[2];
+    bf16x8 hq[2][3][2];
+    gq[0] = gemm1(ring1);                               // chunk 0
+    if (nj > 1) gq[1] = gemm1(ring1 + PART);           // chunk 1
+    gelu_split(0, gq[0], hq[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                      // ring1 slot 0 is refilled in iteration 0
+    const unsigned long long c1t = P.dbg ? clock64() : 0ull;
+    // DMA of one part with a compile-time piece count per wave (no loop in the scheduling region)
+    auto dma_part = [&](const float* src, float* dst) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            const int p = wave + i * FFN_WAVES;
+            __builtin_amdgcn_global_load_lds((const void*)(src + p * 256 + lane * 4),
+                                             (__attribute__((address_space(3))) void*)(dst + p * 256), 16, 0, 0);
+        }
+    };
+    // iteration j; FULL: every step of the steady state (W1 chunk j + 3 and W2 chunk j + 2 exist), so
+    // the body is one basic block the scheduling groups can interleave
+    // SLOT: j % 3 when known at compile time (the steady state is unrolled by 6), else -1
+    auto iteration = [&](int j, auto par, auto full, auto slotc) {
+        constexpr int cur = decltype(par)::value, nxt = 1 - cur;
+        constexpr bool FULL = decltype(full)::value;
+        constexpr int SLOT = decltype(slotc)::value;
+        const int s0 = SLOT >= 0 ? SLOT : j % 3, s2 = SLOT >= 0 ? (SLOT + 2) % 3 : (j + 2) % 3;
+        const bool d1 = FULL || j + 3 < nj, d2 = FULL || j + 2 < nj;
+        if (d1) dma_part(w1src(j + 3), ring1 + s0 * PART);
+        if (d2) dma_part(w2src(j + 2), ring2 + s2 * PART);
+        // gq[nxt] holds chunk j + 1's GEMM 1 result; gq[cur] receives chunk j + 2's
+        if (FULL || j + 1 < nj) gelu_split(j + 1, gq[nxt], hq[nxt]);
+        if (FULL || j + 2 < nj) gq[cur] = gemm1(ring1 + s2 * PART);
+        gemm2(ring2 + s0 * PART, hq[cur]);
+        if constexpr (FULL) {
+            // GEMM 1's fragment reads first; its 12 NT MFMAs each followed by ~5 vector instructions
+            // (the GELU of chunk j + 1) with GEMM 2's fragment reads spread among them, so every
+            // read lands long before its MFMA; then GEMM 2's MFMAs with the remaining vector work
+            __builtin_amdgcn_sched_group_barrier(0x100, 6 * NT, 0);
+#pragma unroll
+            for (int i = 0; i < 12 * NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                if (i & 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 12 * NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            }
+        }
+        // the next iteration reads W1 chunk j + 3 (issued above) and W2 chunk j + 1 (issued in j - 1):
+        // only W2 chunk j + 2's pieces may stay in flight
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using IN = std::integral_constant<int, -1>;
+    int j = 0;
+    for (; j + 8 < nj; j += 6) {   // j % 6 == 0: parities and ring slots are compile-time
+        iteration(j, I0{}, std::true_type{}, I0{});
+        iteration(j + 1, I1{}, std::true_type{}, I1{});
+        iteration(j + 2, I0{}, std::true_type{}, I2{});
+        iteration(j + 3, I1{}, std::true_type{}, I0{});
+        iteration(j + 4, I0{}, std::true_type{}, I1{});
+        iteration(j + 5, I1{}, std::true_type{}, I2{});
+    }
+    for (; j < nj; j += 2) {
+        iteration(j, I0{}, std::false_type{}, IN{});
+        if (j + 1 < nj) iteration(j + 1, I1{}, std::false_type{}, IN{});
+    }
+    const unsigned long long c2t = P.dbg ? clock64() : 0ull;
+
+    // epilogue: X = X + s * (acc + b2).  The accumulators (lane -> column, register e -> row
+    // (e & 3) + 8 (e >> 2) + 4 h) are transposed through this wave's slice of the now idle rings,
+    // so the residual loads and the stores are row-contiguous float4 (16 each per lane, not 64)
+    {
+        constexpr int LDR = C + 8;                        // padded row stride (floats)
+        float* tile = lds + wave * 32 * LDR;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const int col = 32 * tt + r;
+            const float b = P.b2[col];
+            const float sc = P.scale ? P.scale[col] : 1.f;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) tile[((e & 3) + 8 * (e >> 2) + 4 * h) * LDR + col] = sc * (acc[tt][e] + b);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's own tile: no cross-wave hand-off
+        constexpr int F4 = 32 * C / 4 / 64;   // float4 per lane
+        float4 res[F4];
+#pragma unroll
+        for (int i = 0; i < F4; ++i) {
+            const int f = lane + 64 * i, rr = f / (C / 4), c4 = f % (C / 4);
+            res[i] = row0 + rr < P.rows ? *reinterpret_cast<const float4*>(P.X + (row0 + rr) * C + 4 * c4)
+                                        : float4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < F4; ++i) {
+            const int f = lane + 64 * i, rr = f / (C / 4), c4 = f % (C / 4);
+            const float4 v = *reinterpret_cast<const float4*>(tile + rr * LDR + 4 * c4);
+            if (row0 + rr < P.rows)
+                *reinterpret_cast<float4*>(P.X + (row0 + rr) * C + 4 * c4) =
+                    float4{res[i].x + v.x, res[i].y + v.y, res[i].z + v.z, res[i].w + v.w};
+        }
+    }
+    if (P.dbg && lane == 0) {
+        unsigned long long* d = P.dbg + ((size_t)blockIdx.x * FFN_WAVES + wave) * 4;
+        d[0] = c1t - c0t; d[1] = c2t - c1t; d[2] = 0; d[3] = clock64() - c2t;
+    }
+}
+
+template <int NT>
+int po_ffn_launch(const FfnProb& p, hipStream_t st) {
+    if (p.rows <= 0) return NBX_OK;
+    NBX_CHECK_ARG(p.F % 32 == 0 && p.F >= 32 && p.F <= FFN_FMAX && p.img && p.b1 && p.b2,
+                  "po_ffn: 32 <= F <= %d, F %% 32 == 0, an image, b1 and b2 required", FFN_FMAX);
+    NBX_CHECK_ARG((double)p.rows * NT * 32 * 4.0 < 2147483632.0, "po_ffn: XN spans >= 2 GiB");
+    const size_t lds = (6 * (size_t)NT * nbx::LIN_X3_BLK + p.F) * 4;
+    NBX_CHECK_ARG(lds <= 160 * 1024, "po_ffn: %zu bytes of LDS", lds);
+    static bool attr_set = false;
+    if (!attr_set) {
+        NBX_HIP(hipFuncSetAttribute((const void*)po_ffn_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr_set = true;
+    }
+    const unsigned blocks = (unsigned)((p.rows + 32 * FFN_WAVES - 1) / (32 * FFN_WAVES));
+    static const bool debug = getenv("NBX_PO_FFN_DEBUG") != nullptr;
+    static unsigned long long* dbg = nullptr;
+    FfnProb q = p;
+    const size_t nw = (size_t)blocks * FFN_WAVES;
+    if (debug && !dbg) NBX_HIP(hipMalloc(&dbg, nw * 4 * sizeof(unsigned long long)));
+    q.dbg = debug ? dbg : nullptr;
+    hipLaunchKernelGGL(po_ffn_kernel<NT>, dim3(blocks), dim3(64 * FFN_WAVES), lds, st, q);
+    NBX_HIP(hipGetLastError());
+    if (debug) {   // tuning only: average clocks per wave of prologue / loop / loop-end waits / epilogue
+        std::vector<unsigned long long> hb(nw * 4);
+        NBX_HIP(hipStreamSynchronize(st));
+        NBX_HIP(hipMemcpy(hb.data(), dbg, hb.size() * 8, hipMemcpyDeviceToHost));
+        double a[4] = {0, 0, 0, 0};
+        for (size_t i = 0; i < nw; ++i)
+            for (int k = 0; k < 4; ++k) a[k] += (double)hb[i * 4 + k];
+        fprintf(stderr, "po_ffn_debug waves=%zu prologue=%.0f loop=%.0f epilogue=%.0f clocks/wave\n", nw, a[0] / nw,
+                a[1] / nw, a[3] / nw);
+    }
+    return NBX_OK;
+}
+
 // widest column tile whose weight slice fits the LDS; the split-precision (bf16x3) kernel when the
 // layer carries an image (NBX_PO_X3=0: fp32 MFMA path, A/B only)
 bool po_x3_enabled() {
@@ -409,7 +755,15 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
                 }))
                 return rc;
         }
-        {   // ConvNext MLP with the residual in the epilogue
+        if (Ly.ffn_img_x3 && po_x3_enabled() && (C == 64 || C == 128) && d.mlp % 32 == 0 && d.mlp <= FFN_FMAX) {
+            // ConvNext MLP fused (linear_1 + GELU + linear_2 + layer_scale + residual): the hidden
+            // activation stays in registers (po_ffn_kernel)
+            const FfnProb fp{ws.XN, ws.X, Ly.ffn_img_x3, Ly.lin1_b, Ly.lin2_b, Ly.layer_scale, VO, d.mlp, nullptr};
+            if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * 2.0 * VO * C * d.mlp, (double)VO * f4 * 3 * C, [&] {
+                    return C == 128 ? po_ffn_launch<4>(fp, st) : po_ffn_launch<2>(fp, st);
+                }))
+                return rc;
+        } else {   // ConvNext MLP with the residual in the epilogue
             LinProb p = nbx::lin_dense(ws.XN, C, C, (int)VO, Ly.lin1_t, kp(C), d.mlp, Ly.lin1_b, ws.B1H1, d.mlp);
             p.Wx3 = Ly.lin1_img_x3;
             if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * VO * C * d.mlp, (double)VO * f4 * (C + d.mlp),

@@ -248,7 +248,29 @@ class PONITA_NBODY(nn.Module):
                 if name.endswith("lin2_img_x3"):   # the row-panel kernel streams K chunks: chunk-major
                     img = P[name]
                     P[name] = img.reshape(img.shape[0], W.shape[1] // 32, -1).transpose(0, 1).contiguous()
+        C = m.hidden_dim
+        for i in range(len(m.interaction_layers)):
+            p = f"layers.{i}."
+            if C in (64, 128) and P[p + "lin1_t"].shape[0] % 32 == 0:
+                P[p + "ffn_img_x3"] = self._ffn_image(P[p + "lin1_t"], P[p + "lin2_t"])
         return P
+
+    # hidden index held by image K slot q = 16 h + 8 m + i of a 32-wide chunk in the fused ConvNext MLP:
+    # the register order of the 32x32 MFMA result that becomes GEMM 2's A operand (csrc/ponita.hip
+    # po_ffn_kernel)
+    FFN_PERM = [(q % 8 & 3) + 16 * ((q // 8) % 2) + 8 * ((q % 8) >> 2) + 4 * (q // 16) for q in range(32)]
+
+    @classmethod
+    def _ffn_image(cls, W1, W2):
+        """include/nbx.h nbx_ponita_layer.ffn_img_x3: per 32-wide hidden chunk one slab
+        [linear_1 rows of the chunk][linear_2 columns of the chunk, K order permuted]."""
+        F, C = W1.shape[0], W2.shape[0]
+        nj = F // 32
+        img1 = cls.lin_image_x3(W1).reshape(nj, -1)                       # [F/32][C/32 blocks]
+        perm = torch.tensor([32 * j + q for j in range(nj) for q in cls.FFN_PERM], device=W2.device)
+        W2p = W2[:, :F][:, perm].contiguous()
+        img2 = cls.lin_image_x3(W2p).reshape(C // 32, nj, -1).transpose(0, 1).reshape(nj, -1)
+        return torch.cat([img1, img2], 1).contiguous()
 
     @staticmethod
     def lin_image_x3(W):

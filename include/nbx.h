@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 6
+#define NBX_ABI_VERSION 7
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -320,6 +320,13 @@ typedef struct nbx_ponita_layer {
     const void* kernel_img_x3;
     const void* lin1_img_x3;
     const void* lin2_img_x3;
+    /* optional (ABI 7): the fused ConvNext MLP's slabs, one per 32-wide hidden chunk j (NULL: the
+     * two-GEMM path): [linear_1 rows 32j..32j+31 as (C/32) K-chunk blocks [3][2][64][8] bf16 (the
+     * "bf16x3 images" block with the hidden units as rows)] [linear_2 columns of chunk j for the C/32
+     * output tiles, same block layout, with the hidden index inside the chunk permuted: image slot
+     * 16 h + 8 m + i holds hidden unit (i & 3) + 16 m + 8 (i >> 2) + 4 h]; used when hidden C is 64
+     * or 128 and 4C <= 1024 (ponita.py _ffn_image); lin1_b / lin2_b / layer_scale as above */
+    const void* ffn_img_x3;
 } nbx_ponita_layer;
 
 typedef struct nbx_ponita_weights {

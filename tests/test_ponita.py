@@ -290,3 +290,52 @@ def test_gpu_c3_full_batch_slices_match_oracle(hip_device):
             tol = 2e-4 * (k + 1)
             assert np.abs(tp[sl, k] - rl[:, k]).max() <= tol * np.abs(rl[:, k]).max() + 1e-6, (s0, k)
             assert np.abs(tv[sl, k] - rv[:, k]).max() <= tol * np.abs(rv[:, k]).max() + 1e-6, (s0, k)
+
+
+def test_ffn_image_layout():
+    """The fused ConvNext MLP slabs (include/nbx.h nbx_ponita_layer.ffn_img_x3) decode to linear_1's
+    rows, linear_2's columns under the register-order permutation the kernel relies on
+    (po_ffn_kernel: image K slot 16 h + 8 m + i <-> hidden unit (i & 3) + 16 m + 8 (i >> 2) + 4 h);
+    the three bf16 parts sum back to the fp32 weight within 2^-24 relative."""
+    torch.manual_seed(3)
+    C, F = 64, 256
+    W1, W2 = torch.randn(F, C), torch.randn(C, F)
+    img = P.PONITA_NBODY._ffn_image(W1, W2)
+    nj, NT, BLK = F // 32, C // 32, 3 * 2 * 64 * 8
+    assert img.shape == (nj, 2 * 2 * NT * 1536) and img.dtype == torch.int16
+    bf = img.contiguous().view(torch.bfloat16).float().reshape(nj, 2, NT, 3, 2, 64, 8)
+    lane = torch.arange(64)
+    for j in range(nj):
+        for t in range(NT):
+            for m in range(2):
+                for i in range(8):
+                    w1 = bf[j, 0, t, :, m, :, i].sum(0)           # lane (hidden, h), K chunk t
+                    k = 32 * t + 16 * (lane >> 5) + 8 * m + i
+                    ref1 = W1[32 * j + (lane & 31), k]
+                    assert torch.allclose(w1, ref1, rtol=2 ** -22, atol=0)
+                    w2 = bf[j, 1, t, :, m, :, i].sum(0)           # lane (out column, h), output tile t
+                    hid = 32 * j + (i & 3) + 16 * m + 8 * (i >> 2) + 4 * (lane >> 5)
+                    ref2 = W2[32 * t + (lane & 31), hid]
+                    assert torch.allclose(w2, ref2, rtol=2 ** -22, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hidden", [64, 128])
+def test_gpu_fused_convnext_matches_two_gemm_path(hip_device, hidden):
+    """po_ffn_kernel (ConvNext MLP fused, hidden activation in registers) against the two-GEMM path
+    (linear_1 -> HBM -> linear_2) on the same weights: both are fp32-accurate bf16x3 products, so
+    they agree to fp32 rounding."""
+    B, N = 96, 5
+    m = make(hidden, 2, num_ori=12).to(hip_device)
+    m.eval()
+    rng = np.random.default_rng(21)
+    loc, vel = rng.standard_normal((B, N, 3)), rng.standard_normal((B, N, 3)) * 0.5
+    mass = np.ones((B, N, 1))
+    with torch.no_grad():
+        fused = m(gpu_graph(loc, vel, mass, B, N, hip_device)).double().cpu().numpy()
+        W = m._weights(hip_device)
+        for i in range(W.num_layers):
+            assert W.layers[i].ffn_img_x3
+            W.layers[i].ffn_img_x3 = None
+        plain = m(gpu_graph(loc, vel, mass, B, N, hip_device)).double().cpu().numpy()
+    assert np.abs(fused - plain).max() <= 2e-5 * np.abs(plain).max() + 1e-7
