@@ -123,6 +123,11 @@ _SIGNATURES = {
                                         c_p]),
     "nbx_egnn_rollout": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p,
                                         c_p, c_sz, c_p]),
+    "nbx_egnn_train_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "nbx_egnn_train_forward": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_sz,
+                                              c_p]),
+    "nbx_egnn_train_backward": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p,
+                                               c_sz, c_p]),
     "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
                                          c_p, c_p, c_p, c_sz, c_p]),
     "nbx_ponita_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_i64, c_i64,

@@ -1,0 +1,685 @@
+// EGNN-MC training step on the device: a forward that keeps the activations the backward needs, and
+// the backward of the whole network (embedding, every _EGNNMessageBlock, both vector heads) to the
+// gradient of the persistent kernel's weight blob (include/nbx.h "EGNN-MC persist blob").
+//
+// Reference: models/egnn_mc/egnn_mc.py:45-295 (the module trained by trainer.py:233-358 through
+// loss.backward()), dataloaders/egnn_mc_n_body_dataloader.py:8-56 (node / edge inputs: data, no
+// gradient).  The host wraps the pair in a torch.autograd.Function whose input is the blob built
+// from the parameters by differentiable ops, so torch routes the blob gradient to every parameter
+// and the reference trainer's optimizer / clipping / scheduler run unchanged.
+//
+// One 512-thread workgroup per system (N <= 8 bodies, E = N (N - 1) edges), fp32 FMA arithmetic
+// over LDS-resident activations (the per-system products are 20-56 rows; these are latency-bound
+// reductions, not MFMA work).  Saved per system and layer (global scratch):
+//   hin [N][H], coord_in [N][4], ZE1 ZEF ZC1 [E][H] (pre-activations), U [E] (coord head before
+//   tanh), ZV1 ZN1 AGG [N][H]; after the layers: h [N][H], coord [N][4], per head ZG1 ZG2 [N][H].
+// Weight gradients of one workgroup accumulate into its own slice of a partial buffer
+// [G][blob] (systems g, g + G, ...); a second kernel sums the G slices (deterministic order).
+#include <cstring>
+
+#include "nbx_internal.h"
+
+namespace {
+
+constexpr int ET_THREADS = 512;
+
+__device__ inline float et_sig(float z) { return 1.0f / (1.0f + __expf(-z)); }
+__device__ inline float et_silu(float z) { return z * et_sig(z); }
+__device__ inline float et_dsilu(float z) {
+    const float s = et_sig(z);
+    return s * (1.0f + z * (1.0f - s));
+}
+
+// Y[r][n] = b[n] + sum_k X[r][k] W[k][n] (W input-major [K][ldw]); Zs (global, optional) gets the
+// pre-activation; Y gets act(.) with act 1 = SiLU.  X / Y in LDS.  All threads call.
+__device__ void et_gemm(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
+                        const float* __restrict__ b, int Nc, float* Y, int ldy, int act, float* Zs) {
+    for (int o = threadIdx.x; o < rows * Nc; o += ET_THREADS) {
+        const int r = o / Nc, n = o - r * Nc;
+        float v = b ? b[n] : 0.f;
+        const float* x = X + r * ldx;
+        for (int k = 0; k < K; ++k) v = fmaf(x[k], W[(size_t)k * ldw + n], v);
+        if (Zs) Zs[r * Nc + n] = v;
+        Y[r * ldy + n] = act == 1 ? et_silu(v) : v;
+    }
+    __syncthreads();
+}
+
+// dX[r][k] (+)= sum_n dZ[r][n] W[k][n]
+__device__ void et_gemm_t(const float* dZ, int rows, int ldz, int Nc, const float* __restrict__ W, int ldw, int K,
+                          float* dX, int ldx, bool accumulate) {
+    for (int o = threadIdx.x; o < rows * K; o += ET_THREADS) {
+        const int r = o / K, k = o - r * K;
+        const float* w = W + (size_t)k * ldw;
+        const float* z = dZ + r * ldz;
+        float v = 0.f;
+        for (int n = 0; n < Nc; ++n) v = fmaf(z[n], w[n], v);
+        dX[r * ldx + k] = accumulate ? dX[r * ldx + k] + v : v;
+    }
+    __syncthreads();
+}
+
+// G[k][n] += sum_r X[r][k] dZ[r][n] (k < K), gb[n] += sum_r dZ[r][n]; G / gb global (this
+// workgroup's partial slice), X / dZ in LDS
+__device__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* dZ, int ldz, int Nc, float* G, int ldg,
+                         float* gb) {
+    for (int o = threadIdx.x; o < K * Nc; o += ET_THREADS) {
+        const int k = o / Nc, n = o - k * Nc;
+        float v = 0.f;
+        for (int r = 0; r < rows; ++r) v = fmaf(X[r * ldx + k], dZ[r * ldz + n], v);
+        G[(size_t)k * ldg + n] += v;
+    }
+    if (gb)
+        for (int n = threadIdx.x; n < Nc; n += ET_THREADS) {
+            float v = 0.f;
+            for (int r = 0; r < rows; ++r) v += dZ[r * ldz + n];
+            gb[n] += v;
+        }
+    __syncthreads();
+}
+
+struct EgnnTrain {
+    const float* blob;      // weights (persist blob layout)
+    int L, N, heads, recurrent, norm_diff, use_tanh, H;
+    float coords_weight;
+    const float* pos; const float* vel; const float* mass;   // [B N 3], [B N 3], [B N]
+    int64_t B;
+    float* save;            // [B][save_floats]
+    int64_t save_floats;
+    float* out;             // forward: [B N][3 heads]
+    const float* dout;      // backward: dL/dout [B N][3 heads]
+    float* gpart;           // backward: [G][blob_floats] partial weight gradients (zeroed by the host)
+    int64_t blob_floats;
+};
+
+// blob offsets (include/nbx.h): embedding [2][H] + b[H]; per layer e0 [2H+8][H] e0b e1 [H][H] e1b
+// c0 [H][H] c0b c1w [H] v0 [H][H] v0b v1w [H] v1b [4] n0 [2H][H] n0b n1 [H][H] n1b; per head
+// w0 [H+8][H] b0 w1 [H][H] b1 w2 [H][4] b2 [4]
+struct LayerOff {
+    int64_t e0, e0b, e1, e1b, c0, c0b, c1w, v0, v0b, v1w, v1b, n0, n0b, n1, n1b;
+};
+__device__ inline LayerOff layer_off(int H, int l) {
+    LayerOff o;
+    const int64_t LAYER = 8LL * H * H + 16LL * H + 4;
+    o.e0 = 3LL * H + l * LAYER;
+    o.e0b = o.e0 + (2LL * H + 8) * H;
+    o.e1 = o.e0b + H; o.e1b = o.e1 + (int64_t)H * H;
+    o.c0 = o.e1b + H; o.c0b = o.c0 + (int64_t)H * H;
+    o.c1w = o.c0b + H;
+    o.v0 = o.c1w + H; o.v0b = o.v0 + (int64_t)H * H;
+    o.v1w = o.v0b + H; o.v1b = o.v1w + H;
+    o.n0 = o.v1b + 4; o.n0b = o.n0 + 2LL * H * H;
+    o.n1 = o.n0b + H; o.n1b = o.n1 + (int64_t)H * H;
+    return o;
+}
+struct HeadOff {
+    int64_t w0, b0, w1, b1, w2, b2;
+};
+__device__ inline HeadOff head_off(int H, int L, int t) {
+    HeadOff o;
+    const int64_t LAYER = 8LL * H * H + 16LL * H + 4, HEAD = 2LL * H * H + 14LL * H + 4;
+    o.w0 = 3LL * H + L * LAYER + t * HEAD;
+    o.b0 = o.w0 + (H + 8LL) * H;
+    o.w1 = o.b0 + H; o.b1 = o.w1 + (int64_t)H * H;
+    o.w2 = o.b1 + H; o.b2 = o.w2 + 4LL * H;
+    return o;
+}
+
+// per-system saved layout (floats)
+struct SaveOff {
+    int64_t layer, hin, cin, ze1, zef, zc1, u, zv1, zn1, agg;   // within a layer
+    int64_t hfin, cfin, head, zg1, zg2;                          // after the layers
+};
+__host__ __device__ inline SaveOff save_off(int N, int H, int L) {
+    const int E = N * (N - 1);
+    SaveOff s;
+    s.hin = 0; s.cin = s.hin + (int64_t)N * H; s.ze1 = s.cin + 4LL * N; s.zef = s.ze1 + (int64_t)E * H;
+    s.zc1 = s.zef + (int64_t)E * H; s.u = s.zc1 + (int64_t)E * H; s.zv1 = s.u + E; s.zn1 = s.zv1 + (int64_t)N * H;
+    s.agg = s.zn1 + (int64_t)N * H;
+    s.layer = s.agg + (int64_t)N * H;
+    s.hfin = L * s.layer; s.cfin = s.hfin + (int64_t)N * H;
+    s.zg1 = 0; s.zg2 = (int64_t)N * H; s.head = 2LL * N * H;
+    return s;
+}
+__host__ __device__ inline int64_t save_floats(int N, int H, int L, int heads) {
+    const SaveOff s = save_off(N, H, L);
+    return s.cfin + 4LL * N + heads * s.head;
+}
+
+// LDS (floats), E = N (N - 1): X [E][2H+8] | dX [E][2H+8] | A B C [E][H] | n0..n4 [N][2H] | small
+__host__ __device__ inline size_t train_lds_floats(int N, int H) {
+    const int E = N * (N - 1);
+    return 2 * (size_t)E * (2 * H + 8) + 3 * (size_t)E * H + 5 * (size_t)N * 2 * H + 64 * 8 + 16 * (size_t)E + 32 * (size_t)N;
+}
+
+struct Lds {
+    float *X, *dX, *A, *Bq, *Cq, *n0, *n1, *n2, *n3, *n4;
+    float *pos0, *coord, *velv, *mass, *ea, *diff, *diffn, *radial, *cd, *vd, *dvd, *dcd, *dcoord, *dpred, *tmp;
+};
+__device__ inline Lds carve_lds(float* lds, int N, int H) {
+    const int E = N * (N - 1);
+    Lds s;
+    float* p = lds;
+    s.X = p; p += (size_t)E * (2 * H + 8);
+    s.dX = p; p += (size_t)E * (2 * H + 8);
+    s.A = p; p += (size_t)E * H;
+    s.Bq = p; p += (size_t)E * H;
+    s.Cq = p; p += (size_t)E * H;
+    s.n0 = p; p += 2 * N * H;
+    s.n1 = p; p += 2 * N * H;
+    s.n2 = p; p += 2 * N * H;
+    s.n3 = p; p += 2 * N * H;
+    s.n4 = p; p += 2 * N * H;
+    s.pos0 = p; p += 32;
+    s.coord = p; p += 32;
+    s.velv = p; p += 32;
+    s.mass = p; p += 32;
+    s.dcoord = p; p += 32;
+    s.dpred = p; p += 64;
+    s.vd = p; p += 8;
+    s.dvd = p; p += 8;
+    s.tmp = p; p += 64;
+    s.ea = p; p += 4 * E;
+    s.diff = p; p += 3 * E;
+    s.diffn = p; p += 3 * E;
+    s.radial = p; p += E;
+    s.cd = p; p += E;
+    s.dcd = p; p += E;
+    return s;
+}
+
+__device__ inline int e_row(int e, int deg) { return e / deg; }
+__device__ inline int e_col(int e, int deg) {
+    const int i = e / deg, j = e - i * deg;
+    return j < i ? j : j + 1;
+}
+
+// node / edge inputs of one system into LDS (egnn_mc_n_body_dataloader.py:8-56)
+__device__ void load_system(const EgnnTrain& P, const Lds& s, int64_t sys) {
+    const int N = P.N, deg = N - 1, E = N * deg;
+    for (int i = threadIdx.x; i < 3 * N; i += ET_THREADS) {
+        s.pos0[i] = P.pos[sys * N * 3 + i];
+        s.velv[i] = P.vel[sys * N * 3 + i];
+    }
+    for (int i = threadIdx.x; i < N; i += ET_THREADS) s.mass[i] = P.mass[sys * N + i];
+    __syncthreads();
+    for (int e = threadIdx.x; e < E; e += ET_THREADS) {
+        const int r = e_row(e, deg), c = e_col(e, deg);
+        const float dx = s.pos0[3 * r] - s.pos0[3 * c], dy = s.pos0[3 * r + 1] - s.pos0[3 * c + 1],
+                    dz = s.pos0[3 * r + 2] - s.pos0[3 * c + 2];
+        const float d2 = dx * dx + dy * dy + dz * dz, d = fmaxf(sqrtf(d2), 1e-12f);
+        const float hx = dx / d, hy = dy / d, hz = dz / d;
+        s.ea[4 * e] = s.mass[r] * s.mass[c];
+        s.ea[4 * e + 1] = s.velv[3 * r] * hx + s.velv[3 * r + 1] * hy + s.velv[3 * r + 2] * hz;
+        s.ea[4 * e + 2] = s.velv[3 * c] * hx + s.velv[3 * c + 1] * hy + s.velv[3 * c + 2] * hz;
+        s.ea[4 * e + 3] = d2;
+    }
+    __syncthreads();
+}
+
+// coord2radial (egnn_mc.py:155-164) of the coordinates in s.coord
+__device__ void geometry(const EgnnTrain& P, const Lds& s) {
+    const int N = P.N, deg = N - 1, E = N * deg;
+    for (int e = threadIdx.x; e < E; e += ET_THREADS) {
+        const int r = e_row(e, deg), c = e_col(e, deg);
+        float d[3];
+        for (int k = 0; k < 3; ++k) d[k] = s.coord[4 * r + k] - s.coord[4 * c + k];
+        const float radial = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        const float nrm = P.norm_diff ? fmaxf(sqrtf(radial), 1.0f) : 1.0f;
+        for (int k = 0; k < 3; ++k) {
+            s.diff[3 * e + k] = d[k];
+            s.diffn[3 * e + k] = d[k] / nrm;
+        }
+        s.radial[e] = radial;
+    }
+    __syncthreads();
+}
+
+// edge input [h_row | h_col | radial, edge_attr, 0 0 0] from h in LDS [N][H]
+__device__ void edge_input(const EgnnTrain& P, const Lds& s, const float* h) {
+    const int N = P.N, deg = N - 1, E = N * deg, H = P.H, LX = 2 * H + 8;
+    for (int o = threadIdx.x; o < E * LX; o += ET_THREADS) {
+        const int e = o / LX, k = o - e * LX;
+        float v;
+        if (k < H) v = h[e_row(e, deg) * H + k];
+        else if (k < 2 * H) v = h[e_col(e, deg) * H + k - H];
+        else if (k == 2 * H) v = s.radial[e];
+        else if (k < 2 * H + 5) v = s.ea[4 * e + k - 2 * H - 1];
+        else v = 0.f;
+        s.X[o] = v;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTrain P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int N = P.N, deg = N - 1, E = N * deg, H = P.H, LX = 2 * H + 8;
+    const Lds s = carve_lds(lds, N, H);
+    const int64_t sys = blockIdx.x;
+    const SaveOff so = save_off(N, H, P.L);
+    float* sv = P.save + sys * P.save_floats;
+    load_system(P, s, sys);
+    // embedding: x = [|vel|, mass] (Linear 2 -> H)
+    float* h = s.n0;
+    for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
+        const int i = o / H, n = o - i * H;
+        const float vx = s.velv[3 * i], vy = s.velv[3 * i + 1], vz = s.velv[3 * i + 2];
+        h[o] = P.blob[2 * H + n] + sqrtf(vx * vx + vy * vy + vz * vz) * P.blob[n] + s.mass[i] * P.blob[H + n];
+    }
+    for (int i = threadIdx.x; i < N; i += ET_THREADS)
+        for (int k = 0; k < 4; ++k) s.coord[4 * i + k] = k < 3 ? s.pos0[3 * i + k] : 0.f;
+    __syncthreads();
+    for (int l = 0; l < P.L; ++l) {
+        const LayerOff w = layer_off(H, l);
+        float* sl = sv + l * so.layer;
+        for (int o = threadIdx.x; o < N * H; o += ET_THREADS) sl[so.hin + o] = h[o];
+        for (int o = threadIdx.x; o < 4 * N; o += ET_THREADS) sl[so.cin + o] = s.coord[o];
+        geometry(P, s);
+        edge_input(P, s, h);
+        et_gemm(s.X, E, LX, LX, P.blob + w.e0, H, P.blob + w.e0b, H, s.A, H, 1, sl + so.ze1);    // E1
+        et_gemm(s.A, E, H, H, P.blob + w.e1, H, P.blob + w.e1b, H, s.Bq, H, 1, sl + so.zef);      // EF
+        et_gemm(s.Bq, E, H, H, P.blob + w.c0, H, P.blob + w.c0b, H, s.A, H, 1, sl + so.zc1);      // C1
+        for (int e = threadIdx.x; e < E; e += ET_THREADS) {                                        // coord head
+            float u = 0.f;
+            for (int n = 0; n < H; ++n) u = fmaf(s.A[e * H + n], P.blob[w.c1w + n], u);
+            sl[so.u + e] = u;
+            s.cd[e] = P.use_tanh ? tanhf(u) : u;
+        }
+        et_gemm(h, N, H, H, P.blob + w.v0, H, P.blob + w.v0b, H, s.n1, H, 1, sl + so.zv1);        // V1
+        for (int i = threadIdx.x; i < N; i += ET_THREADS) {
+            float v = P.blob[w.v1b];
+            for (int n = 0; n < H; ++n) v = fmaf(s.n1[i * H + n], P.blob[w.v1w + n], v);
+            s.vd[i] = v;
+        }
+        for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {                                   // [h | mean EF]
+            const int i = o / H, n = o - i * H;
+            float a = 0.f;
+            for (int q = 0; q < deg; ++q) a += s.Bq[(i * deg + q) * H + n];
+            a = deg > 0 ? a / (float)deg : 0.f;
+            sl[so.agg + o] = a;
+            s.n2[i * 2 * H + n] = h[o];
+            s.n2[i * 2 * H + H + n] = a;
+        }
+        __syncthreads();
+        et_gemm(s.n2, N, 2 * H, 2 * H, P.blob + w.n0, H, P.blob + w.n0b, H, s.n3, H, 1, sl + so.zn1);   // N1
+        float* hn = h == s.n0 ? s.n4 : s.n0;
+        et_gemm(s.n3, N, H, H, P.blob + w.n1, H, P.blob + w.n1b, H, hn, H, 0, nullptr);
+        for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {   // coord_model + velocity term
+            const int i = o / 3, k = o - 3 * i;
+            float a = 0.f;
+            for (int q = 0; q < deg; ++q) {
+                const int e = i * deg + q;
+                a += fminf(fmaxf(s.diffn[3 * e + k] * s.cd[e], -100.f), 100.f);
+            }
+            s.tmp[o] = (deg > 0 ? a / (float)deg : 0.f) * P.coords_weight + s.vd[i] * s.velv[o];
+        }
+        if (P.recurrent)
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) hn[o] += h[o];
+        __syncthreads();
+        for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) s.coord[4 * (o / 3) + o % 3] += s.tmp[o];
+        __syncthreads();
+        h = hn;
+    }
+    for (int o = threadIdx.x; o < N * H; o += ET_THREADS) sv[so.hfin + o] = h[o];
+    for (int o = threadIdx.x; o < 4 * N; o += ET_THREADS) sv[so.cfin + o] = s.coord[o];
+    // heads: [h | coord - pos, vel, 0 0] -> SiLU -> SiLU -> 3
+    const int LH = H + 8;
+    for (int o = threadIdx.x; o < N * LH; o += ET_THREADS) {
+        const int i = o / LH, k = o - i * LH;
+        float v = 0.f;
+        if (k < H) v = h[i * H + k];
+        else if (k < H + 3) v = s.coord[4 * i + k - H] - s.pos0[3 * i + k - H];
+        else if (k < H + 6) v = s.velv[3 * i + k - H - 3];
+        s.X[o] = v;
+    }
+    __syncthreads();
+    for (int t = 0; t < P.heads; ++t) {
+        const HeadOff w = head_off(H, P.L, t);
+        float* sh = sv + so.cfin + 4 * N + t * so.head;
+        et_gemm(s.X, N, LH, LH, P.blob + w.w0, H, P.blob + w.b0, H, s.n1, H, 1, sh + so.zg1);
+        et_gemm(s.n1, N, H, H, P.blob + w.w1, H, P.blob + w.b1, H, s.n2, H, 1, sh + so.zg2);
+        for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {
+            const int i = o / 3, k = o - 3 * i;
+            float v = P.blob[w.b2 + k];
+            for (int n = 0; n < H; ++n) v = fmaf(s.n2[i * H + n], P.blob[w.w2 + 4 * n + k], v);
+            P.out[(sys * N + i) * 3 * P.heads + 3 * t + k] = v;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTrain P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int N = P.N, deg = N - 1, E = N * deg, H = P.H, LX = 2 * H + 8, LH = H + 8;
+    const Lds s = carve_lds(lds, N, H);
+    const SaveOff so = save_off(N, H, P.L);
+    float* G = P.gpart + (int64_t)blockIdx.x * P.blob_floats;
+    for (int64_t sys = blockIdx.x; sys < P.B; sys += gridDim.x) {
+        const float* sv = P.save + sys * P.save_floats;
+        load_system(P, s, sys);
+        for (int o = threadIdx.x; o < 3 * N * P.heads; o += ET_THREADS) s.dpred[o] = P.dout[sys * N * 3 * P.heads + o];
+        // dh (s.n0) and dcoord start at zero
+        float* dh = s.n0;
+        for (int o = threadIdx.x; o < N * H; o += ET_THREADS) dh[o] = 0.f;
+        for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) s.dcoord[o] = 0.f;
+        // ---- heads
+        for (int o = threadIdx.x; o < N * LH; o += ET_THREADS) {   // head input from the saved final state
+            const int i = o / LH, k = o - i * LH;
+            float v = 0.f;
+            if (k < H) v = sv[so.hfin + i * H + k];
+            else if (k < H + 3) v = sv[so.cfin + 4 * i + k - H] - s.pos0[3 * i + k - H];
+            else if (k < H + 6) v = s.velv[3 * i + k - H - 3];
+            s.X[o] = v;
+        }
+        __syncthreads();
+        for (int t = 0; t < P.heads; ++t) {
+            const HeadOff w = head_off(H, P.L, t);
+            const float* sh = sv + so.cfin + 4 * N + t * so.head;
+            // G1 = silu(ZG1) -> n1, G2 = silu(ZG2) -> n2
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
+                s.n1[o] = et_silu(sh[so.zg1 + o]);
+                s.n2[o] = et_silu(sh[so.zg2 + o]);
+            }
+            for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {   // dpred of this head -> tmp [N][3]
+                const int i = o / 3, k = o - 3 * i;
+                s.tmp[o] = s.dpred[i * 3 * P.heads + 3 * t + k];
+            }
+            __syncthreads();
+            // pred = G2 W2 + b2: dG2 = dpred W2^T; gW2 += G2^T dpred (3 of 4 columns); gb2
+            for (int o = threadIdx.x; o < H * 3; o += ET_THREADS) {
+                const int n = o / 3, k = o - 3 * n;
+                float v = 0.f;
+                for (int i = 0; i < N; ++i) v = fmaf(s.n2[i * H + n], s.tmp[3 * i + k], v);
+                G[w.w2 + 4 * n + k] += v;
+            }
+            for (int k = threadIdx.x; k < 3; k += ET_THREADS) {
+                float v = 0.f;
+                for (int i = 0; i < N; ++i) v += s.tmp[3 * i + k];
+                G[w.b2 + k] += v;
+            }
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {   // dZG2 -> n3
+                const int i = o / H, n = o - i * H;
+                float v = 0.f;
+                for (int k = 0; k < 3; ++k) v = fmaf(s.tmp[3 * i + k], P.blob[w.w2 + 4 * n + k], v);
+                s.n3[o] = v * et_dsilu(sh[so.zg2 + o]);
+            }
+            __syncthreads();
+            et_wgrad(s.n1, N, H, H, s.n3, H, H, G + w.w1, H, G + w.b1);
+            et_gemm_t(s.n3, N, H, H, P.blob + w.w1, H, H, s.n4, H, false);   // dG1 -> n4
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) s.n4[o] *= et_dsilu(sh[so.zg1 + o]);   // dZG1
+            __syncthreads();
+            et_wgrad(s.X, N, LH, LH, s.n4, H, H, G + w.w0, H, G + w.b0);
+            et_gemm_t(s.n4, N, H, H, P.blob + w.w0, H, LH, s.dX, LH, false);   // dXh [N][H+8]
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) dh[o] += s.dX[(o / H) * LH + o % H];
+            for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) s.dcoord[o] += s.dX[(o / 3) * LH + H + o % 3];
+            __syncthreads();
+        }
+        // ---- layers, last to first
+        for (int l = P.L - 1; l >= 0; --l) {
+            const LayerOff w = layer_off(H, l);
+            const float* sl = sv + l * so.layer;
+            const float* hin = sl + so.hin;
+            for (int o = threadIdx.x; o < 4 * N; o += ET_THREADS) s.coord[o] = sl[so.cin + o];
+            __syncthreads();
+            geometry(P, s);
+            for (int e = threadIdx.x; e < E; e += ET_THREADS) {
+                const float u = sl[so.u + e];
+                s.cd[e] = P.use_tanh ? tanhf(u) : u;
+            }
+            // V1 = silu(ZV1) -> n1, vd
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) s.n1[o] = et_silu(sl[so.zv1 + o]);
+            __syncthreads();
+            for (int i = threadIdx.x; i < N; i += ET_THREADS) {
+                float v = 0.f;
+                for (int k = 0; k < 3; ++k) v = fmaf(s.dcoord[3 * i + k], s.velv[3 * i + k], v);
+                s.dvd[i] = v;
+            }
+            // (a) coord_model: dtrans -> ddiffn (s.dX rows as [E][3] scratch), dcd
+            float* ddn = s.dX;
+            const float inv_deg = deg > 0 ? 1.0f / (float)deg : 0.f;
+            for (int e = threadIdx.x; e < E; e += ET_THREADS) {
+                const int r = e_row(e, deg);
+                float dc = 0.f;
+                for (int k = 0; k < 3; ++k) {
+                    const float tr = s.diffn[3 * e + k] * s.cd[e];
+                    const float dt = (tr >= -100.f && tr <= 100.f) ? s.dcoord[3 * r + k] * P.coords_weight * inv_deg : 0.f;
+                    ddn[3 * e + k] = dt * s.cd[e];
+                    dc = fmaf(dt, s.diffn[3 * e + k], dc);
+                }
+                s.dcd[e] = dc;
+            }
+            __syncthreads();
+            // (b) node_mlp: dhn = dh; N1 = silu(ZN1) -> n2; Xn = [hin, AGG] -> n3 (2H wide)
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
+                const int i = o / H, n = o - i * H;
+                s.n2[o] = et_silu(sl[so.zn1 + o]);
+                s.n3[i * 2 * H + n] = hin[o];
+                s.n3[i * 2 * H + H + n] = sl[so.agg + o];
+            }
+            __syncthreads();
+            et_wgrad(s.n2, N, H, H, dh, H, H, G + w.n1, H, G + w.n1b);
+            et_gemm_t(dh, N, H, H, P.blob + w.n1, H, H, s.n4, H, false);   // dN1 -> n4
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) s.n4[o] *= et_dsilu(sl[so.zn1 + o]);   // dZN1
+            __syncthreads();
+            et_wgrad(s.n3, N, 2 * H, 2 * H, s.n4, H, H, G + w.n0, H, G + w.n0b);
+            // dXn = dZN1 Wn0^T -> n2 ([N][2H]); dh_in = (recurrent ? dh : 0) + dXn[:, :H]; dAGG = dXn[:, H:]
+            et_gemm_t(s.n4, N, H, H, P.blob + w.n0, H, 2 * H, s.n2, 2 * H, false);
+            float* dhin = s.n3;   // [N][H] (n3 is free again)
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
+                const int i = o / H, n = o - i * H;
+                dhin[o] = (P.recurrent ? dh[o] : 0.f) + s.n2[i * 2 * H + n];
+            }
+            __syncthreads();
+            // (c) coord_mlp_vel: dV1 = dvd w_v1; gw_v1, gb_v1; dZV1 -> n4; dh_in += dZV1 Wv0^T
+            for (int n = threadIdx.x; n < H; n += ET_THREADS) {
+                float v = 0.f;
+                for (int i = 0; i < N; ++i) v = fmaf(s.dvd[i], s.n1[i * H + n], v);
+                G[w.v1w + n] += v;
+            }
+            if (threadIdx.x == 0) {
+                float v = 0.f;
+                for (int i = 0; i < N; ++i) v += s.dvd[i];
+                G[w.v1b] += v;
+            }
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
+                const int i = o / H, n = o - i * H;
+                s.n4[o] = s.dvd[i] * P.blob[w.v1w + n] * et_dsilu(sl[so.zv1 + o]);
+            }
+            __syncthreads();
+            et_wgrad(hin, N, H, H, s.n4, H, H, G + w.v0, H, G + w.v0b);
+            et_gemm_t(s.n4, N, H, H, P.blob + w.v0, H, H, dhin, H, true);
+            // (d) coord_mlp: dU = dcd (1 - cd^2); C1 = silu(ZC1) -> A; EF = silu(ZEF) -> Bq
+            for (int o = threadIdx.x; o < E * H; o += ET_THREADS) {
+                s.A[o] = et_silu(sl[so.zc1 + o]);
+                s.Bq[o] = et_silu(sl[so.zef + o]);
+            }
+            for (int e = threadIdx.x; e < E; e += ET_THREADS)
+                s.dcd[e] = P.use_tanh ? s.dcd[e] * (1.0f - s.cd[e] * s.cd[e]) : s.dcd[e];   // -> dU
+            __syncthreads();
+            for (int n = threadIdx.x; n < H; n += ET_THREADS) {   // gw_c1 += sum_e dU_e C1_e
+                float v = 0.f;
+                for (int e = 0; e < E; ++e) v = fmaf(s.dcd[e], s.A[e * H + n], v);
+                G[w.c1w + n] += v;
+            }
+            for (int o = threadIdx.x; o < E * H; o += ET_THREADS) {   // dZC1 -> Cq
+                const int e = o / H, n = o - e * H;
+                s.Cq[o] = s.dcd[e] * P.blob[w.c1w + n] * et_dsilu(sl[so.zc1 + o]);
+            }
+            __syncthreads();
+            et_wgrad(s.Bq, E, H, H, s.Cq, H, H, G + w.c0, H, G + w.c0b);
+            et_gemm_t(s.Cq, E, H, H, P.blob + w.c0, H, H, s.A, H, false);   // dEF -> A
+            // (e) dEF += dAGG[row] / deg
+            for (int o = threadIdx.x; o < E * H; o += ET_THREADS) {
+                const int e = o / H, n = o - e * H;
+                s.A[o] += s.n2[e_row(e, deg) * 2 * H + H + n] * inv_deg;
+            }
+            __syncthreads();
+            // (f) edge_mlp: dZEF = dEF silu'(ZEF) -> Cq; E1 = silu(ZE1) -> Bq
+            for (int o = threadIdx.x; o < E * H; o += ET_THREADS) {
+                s.Cq[o] = s.A[o] * et_dsilu(sl[so.zef + o]);
+                s.Bq[o] = et_silu(sl[so.ze1 + o]);
+            }
+            __syncthreads();
+            et_wgrad(s.Bq, E, H, H, s.Cq, H, H, G + w.e1, H, G + w.e1b);
+            et_gemm_t(s.Cq, E, H, H, P.blob + w.e1, H, H, s.A, H, false);   // dE1 -> A
+            for (int o = threadIdx.x; o < E * H; o += ET_THREADS) s.A[o] *= et_dsilu(sl[so.ze1 + o]);   // dZE1
+            __syncthreads();
+            edge_input(P, s, hin);                                         // X (for gWe0)
+            et_wgrad(s.X, E, LX, LX, s.A, H, H, G + w.e0, H, G + w.e0b);
+            // dX = dZE1 We0^T, only the columns that carry gradient: [0, 2H] (h_row, h_col, radial);
+            // ddn still lives in the first 3E floats of s.dX, so the product goes to s.X (X is done)
+            et_gemm_t(s.A, E, H, H, P.blob + w.e0, H, 2 * H + 1, s.X, LX, false);
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {   // dh_in[row] / dh_in[col] sums
+                const int i = o / H, n = o - i * H;
+                float v = 0.f;
+                for (int e = 0; e < E; ++e) {
+                    if (e_row(e, deg) == i) v += s.X[e * LX + n];
+                    if (e_col(e, deg) == i) v += s.X[e * LX + H + n];
+                }
+                dhin[o] += v;
+            }
+            // (g) geometry: ddiff = 2 dradial diff + J(diffn)^T ddiffn; dcoord[row] += ddiff, [col] -= ddiff
+            float* dd = s.dX + 3 * E;   // [E][3] after ddn
+            for (int e = threadIdx.x; e < E; e += ET_THREADS) {
+                const float dr = s.X[e * LX + 2 * H];
+                float d[3], dn[3], n[3];
+                for (int k = 0; k < 3; ++k) {
+                    d[k] = s.diff[3 * e + k];
+                    dn[k] = ddn[3 * e + k];
+                    n[k] = s.diffn[3 * e + k];
+                }
+                const float len = sqrtf(s.radial[e]);
+                float g[3];
+                if (P.norm_diff && len > 1.0f) {
+                    const float nd = n[0] * dn[0] + n[1] * dn[1] + n[2] * dn[2];
+                    for (int k = 0; k < 3; ++k) g[k] = (dn[k] - n[k] * nd) / len;
+                } else {
+                    for (int k = 0; k < 3; ++k) g[k] = dn[k];
+                }
+                for (int k = 0; k < 3; ++k) dd[3 * e + k] = g[k] + 2.0f * dr * d[k];
+            }
+            __syncthreads();
+            for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {
+                const int i = o / 3, k = o - 3 * i;
+                float v = 0.f;
+                for (int e = 0; e < E; ++e) {
+                    if (e_row(e, deg) == i) v += dd[3 * e + k];
+                    if (e_col(e, deg) == i) v -= dd[3 * e + k];
+                }
+                s.dcoord[o] += v;
+            }
+            for (int o = threadIdx.x; o < N * H; o += ET_THREADS) dh[o] = dhin[o];
+            __syncthreads();
+        }
+        // ---- embedding: h0 = b + |vel| w[0] + mass w[1]
+        for (int n = threadIdx.x; n < H; n += ET_THREADS) {
+            float g0 = 0.f, g1 = 0.f, gb = 0.f;
+            for (int i = 0; i < N; ++i) {
+                const float vx = s.velv[3 * i], vy = s.velv[3 * i + 1], vz = s.velv[3 * i + 2];
+                g0 = fmaf(sqrtf(vx * vx + vy * vy + vz * vz), dh[i * H + n], g0);
+                g1 = fmaf(s.mass[i], dh[i * H + n], g1);
+                gb += dh[i * H + n];
+            }
+            G[n] += g0;
+            G[H + n] += g1;
+            G[2 * H + n] += gb;
+        }
+        __syncthreads();
+    }
+}
+
+// grad[i] = sum_g part[g][i]
+__global__ void egnn_grad_reduce_kernel(const float* __restrict__ part, int G, int64_t n, float* __restrict__ grad) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = 0.f;
+    for (int g = 0; g < G; ++g) v += part[(int64_t)g * n + i];
+    grad[i] = v;
+}
+
+int64_t blob_floats(const nbx_egnn_weights* w) {
+    const int64_t H = w->hidden;
+    return 3 * H + w->num_layers * (8 * H * H + 16 * H + 4) + w->num_heads * (2 * H * H + 14 * H + 4);
+}
+
+int check_train(const nbx_egnn_weights* w, int64_t B, int64_t N) {
+    NBX_CHECK_ARG(w && w->persist_blob, "egnn train: needs the persist blob");
+    NBX_CHECK_ARG(w->hidden % 4 == 0 && w->hidden >= 4 && w->num_heads >= 1 && w->num_heads <= 2,
+                  "egnn train: hidden %% 4 == 0, 1-2 heads");
+    NBX_CHECK_ARG(B >= 1 && N >= 2 && N <= 8, "egnn train: 2 <= N <= 8");
+    const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
+    if (lds > 160 * 1024) {
+        nbx::set_error("egnn train: N = %lld at hidden %d needs %zu bytes of LDS", (long long)N, w->hidden, lds);
+        return NBX_E_UNSUPPORTED;
+    }
+    return NBX_OK;
+}
+
+constexpr int TRAIN_GROUPS = 64;   // backward workgroups (partial gradient slices)
+
+}  // namespace
+
+extern "C" int nbx_egnn_train_workspace_bytes(const nbx_egnn_weights* w, int64_t B, int64_t N, size_t* bytes) {
+    NBX_CHECK_ARG(w && bytes && B >= 1 && N >= 2, "nbx_egnn_train_workspace_bytes: bad arguments");
+    const int64_t sf = save_floats((int)N, w->hidden, w->num_layers, w->num_heads);
+    const int64_t G = B < TRAIN_GROUPS ? B : TRAIN_GROUPS;
+    *bytes = (size_t)(B * sf + G * blob_floats(w)) * 4;
+    return NBX_OK;
+}
+
+extern "C" int nbx_egnn_train_forward(const nbx_egnn_weights* w, const float* pos, const float* vel, const float* mass,
+                                      int64_t B, int64_t N, float* out, void* workspace, size_t workspace_bytes,
+                                      void* stream) {
+    if (int rc = check_train(w, B, N)) return rc;
+    size_t need = 0;
+    nbx_egnn_train_workspace_bytes(w, B, N, &need);
+    NBX_CHECK_ARG(workspace && workspace_bytes >= need, "egnn train: workspace too small (%zu < %zu)", workspace_bytes, need);
+    EgnnTrain p{};
+    p.blob = w->persist_blob; p.L = w->num_layers; p.N = (int)N; p.heads = w->num_heads; p.recurrent = w->recurrent;
+    p.norm_diff = w->norm_diff; p.use_tanh = w->use_tanh; p.H = w->hidden; p.coords_weight = w->coords_weight;
+    p.pos = pos; p.vel = vel; p.mass = mass; p.B = B;
+    p.save = static_cast<float*>(workspace);
+    p.save_floats = save_floats((int)N, w->hidden, w->num_layers, w->num_heads);
+    p.out = out;
+    const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
+    static bool attr = false;
+    if (!attr) {
+        NBX_HIP(hipFuncSetAttribute((const void*)egnn_train_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        NBX_HIP(hipFuncSetAttribute((const void*)egnn_train_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(egnn_train_fwd_kernel, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}
+
+extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* pos, const float* vel,
+                                       const float* mass, int64_t B, int64_t N, const float* grad_out, float* grad_blob,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
+    if (int rc = check_train(w, B, N)) return rc;
+    size_t need = 0;
+    nbx_egnn_train_workspace_bytes(w, B, N, &need);
+    NBX_CHECK_ARG(workspace && workspace_bytes >= need && grad_out && grad_blob,
+                  "egnn train backward: workspace too small or null gradient buffers");
+    hipStream_t st = (hipStream_t)stream;
+    EgnnTrain p{};
+    p.blob = w->persist_blob; p.L = w->num_layers; p.N = (int)N; p.heads = w->num_heads; p.recurrent = w->recurrent;
+    p.norm_diff = w->norm_diff; p.use_tanh = w->use_tanh; p.H = w->hidden; p.coords_weight = w->coords_weight;
+    p.pos = pos; p.vel = vel; p.mass = mass; p.B = B;
+    p.save = static_cast<float*>(workspace);
+    p.save_floats = save_floats((int)N, w->hidden, w->num_layers, w->num_heads);
+    p.dout = grad_out;
+    p.blob_floats = blob_floats(w);
+    p.gpart = p.save + B * p.save_floats;
+    const int G = (int)(B < TRAIN_GROUPS ? B : TRAIN_GROUPS);
+    NBX_HIP(hipMemsetAsync(p.gpart, 0, sizeof(float) * (size_t)G * p.blob_floats, st));
+    const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
+    hipLaunchKernelGGL(egnn_train_bwd_kernel, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p);
+    NBX_HIP(hipGetLastError());
+    hipLaunchKernelGGL(egnn_grad_reduce_kernel, dim3((unsigned)((p.blob_floats + 255) / 256)), dim3(256), 0, st, p.gpart,
+                       G, p.blob_floats, grad_blob);
+    NBX_HIP(hipGetLastError());
+    return NBX_OK;
+}

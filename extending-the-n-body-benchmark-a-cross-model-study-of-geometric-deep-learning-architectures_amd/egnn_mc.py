@@ -157,18 +157,21 @@ class EGNNMultiChannel(nn.Module):
         P["persist_blob"] = self.persist_blob(device)
         return P
 
-    def persist_blob(self, device):
-        """The input-major weight blob of the persistent per-system kernel (include/nbx.h)."""
+    def persist_blob(self, device, differentiable: bool = False):
+        """The input-major weight blob of the persistent per-system kernel (include/nbx.h).
+        ``differentiable``: built from the parameters with autograd-tracked ops, so a gradient
+        of the blob (nbx_egnn_train_backward) flows back to every parameter."""
         H = self.hidden_node_dim
         f = dict(device=device, dtype=torch.float32)
+        src = (lambda w: w) if differentiable else (lambda w: w.detach())
 
         def t(w, rows=None, cols=None):          # nn.Linear [out][in] -> [in][out], zero-padded
-            x = w.detach().to(**f).T
+            x = src(w).to(**f).T
             r, c = rows or x.shape[0], cols or x.shape[1]
             return torch.nn.functional.pad(x, (0, c - x.shape[1], 0, r - x.shape[0])).reshape(-1)
 
         def v(b, n=None):
-            x = b.detach().to(**f).reshape(-1)
+            x = src(b).to(**f).reshape(-1)
             return torch.nn.functional.pad(x, (0, (n or x.numel()) - x.numel()))
 
         parts = [t(self.embedding.weight), v(self.embedding.bias)]
@@ -222,6 +225,14 @@ class EGNNMultiChannel(nn.Module):
         return self._ws
 
     # ------------------------------------------------------------ forward
+    def _trainable(self, N: int) -> bool:
+        """Shapes the native training step covers (csrc/egnn_train.hip check_train): 2 <= N <= 8
+        within 160 KiB of LDS; elsewhere a grad-mode forward returns the inference result, which
+        carries no autograd graph (loss.backward() then fails loudly)."""
+        H, E = self.hidden_node_dim, N * (N - 1)
+        lds = 2 * E * (2 * H + 8) + 3 * E * H + 10 * N * H + 512 + 16 * E + 32 * N
+        return 2 <= N <= 8 and H % 4 == 0 and lds * 4 <= 160 * 1024 and 1 <= len(self.heads) <= 2
+
     def forward(self, graph):
         pos = graph.pos
         device = pos.device
@@ -240,6 +251,12 @@ class EGNNMultiChannel(nn.Module):
         mass = getattr(graph, "mass", None)
         m = f(mass.reshape(-1)) if mass is not None else torch.ones(V, device=device)
         p, v = f(pos), f(graph.vel)
+        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()) and self._trainable(N):
+            # training step (trainer.py:233-358): the native forward keeps its activations and
+            # loss.backward() runs the native backward (csrc/egnn_train.hip)
+            W = self._weights(device)
+            blob = self.persist_blob(device, differentiable=True)
+            return _EgnnTrainFn.apply(blob, W, p, v, m, B, N).to(pos.dtype)
         out = torch.empty(V, 3 * len(self.heads), device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(B, N, device)
@@ -265,3 +282,38 @@ class EGNNMultiChannel(nn.Module):
                                                _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
                                                ws.numel(), _lib.stream_ptr(device)), "nbx_egnn_rollout")
         return tp, tv
+
+
+class _EgnnTrainFn(torch.autograd.Function):
+    """Native training forward / backward of EGNNMultiChannel (include/nbx.h
+    nbx_egnn_train_forward / nbx_egnn_train_backward): input = the differentiable weight blob,
+    output = pred [V, 3 heads]; backward returns dL/dblob, which autograd maps onto the parameters
+    through EGNNMultiChannel.persist_blob(differentiable=True)."""
+
+    @staticmethod
+    def forward(ctx, blob, W, pos, vel, mass, B, N):
+        device = pos.device
+        n = _lib.c_sz()
+        _lib.check(_lib.lib().nbx_egnn_train_workspace_bytes(W, B, N, n), "nbx_egnn_train_workspace_bytes")
+        ws = torch.empty(n.value, dtype=torch.uint8, device=device)
+        out = torch.empty(B * N, 3 * W.num_heads, device=device, dtype=torch.float32)
+        _lib.check(_lib.lib().nbx_egnn_train_forward(W, _lib.dev_ptr(pos), _lib.dev_ptr(vel), _lib.dev_ptr(mass), B, N,
+                                                     _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
+                                                     _lib.stream_ptr(device)), "nbx_egnn_train_forward")
+        ctx.W, ctx.B, ctx.N, ctx.ws = W, B, N, ws
+        ctx.save_for_backward(pos, vel, mass)
+        ctx.blob_shape = blob.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        pos, vel, mass = ctx.saved_tensors
+        device = pos.device
+        g = grad_out.detach().to(device=device, dtype=torch.float32).contiguous()
+        grad_blob = torch.empty(ctx.blob_shape, device=device, dtype=torch.float32)
+        _lib.check(_lib.lib().nbx_egnn_train_backward(ctx.W, _lib.dev_ptr(pos), _lib.dev_ptr(vel), _lib.dev_ptr(mass),
+                                                      ctx.B, ctx.N, _lib.dev_ptr(g), _lib.dev_ptr(grad_blob),
+                                                      _lib.dev_ptr(ctx.ws), ctx.ws.numel(),
+                                                      _lib.stream_ptr(device)), "nbx_egnn_train_backward")
+        ctx.ws = None
+        return grad_blob, None, None, None, None, None, None

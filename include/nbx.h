@@ -287,6 +287,24 @@ int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* vel, const fl
                      int64_t num_nodes, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* EGNN-MC training step (trainer.py:233-358: pred = model(graph); loss.backward()), ABI 7.
+ * nbx_egnn_train_forward runs the forward of `batch_size` fully-connected systems of 2..8 bodies
+ * (hidden % 4 == 0; the LDS bound allows N <= 6 at hidden 128) from the persist blob and keeps the
+ * activations the backward needs in `workspace` (nbx_egnn_train_workspace_bytes: B x the per-system
+ * save area + the backward's partial gradient slices); out [B N][3 heads] as nbx_egnn_forward.
+ * nbx_egnn_train_backward, given dL/dout [B N][3 heads] and the same workspace, writes dL/dblob
+ * (grad_blob: the persist blob's length and layout; every entry written, padding included) —
+ * the gradient of every weight of models/egnn_mc/egnn_mc.py:211-295 through the embedding, all
+ * _EGNNMessageBlock layers (edge / coord / velocity / node MLPs, the clamped coordinate update and
+ * the coordinate geometry) and the vector heads.  Inputs (pos, vel, mass) are data: no gradient. */
+int nbx_egnn_train_workspace_bytes(const nbx_egnn_weights* w, int64_t batch_size, int64_t num_nodes, size_t* bytes);
+int nbx_egnn_train_forward(const nbx_egnn_weights* w, const float* pos, const float* vel, const float* mass,
+                           int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
+                           void* stream);
+int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* pos, const float* vel, const float* mass,
+                            int64_t batch_size, int64_t num_nodes, const float* grad_out, float* grad_blob,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * PONITA fibre bundle (models/ponita/ponita_nbody.py:9-95,
  * models/ponita/models/ponita_pg.py:56-192, nn/conv.py:65-140,

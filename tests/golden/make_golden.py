@@ -294,6 +294,36 @@ def make_egnn_mc(ref_mods, Data):
     np.savez_compressed(os.path.join(HERE, "egnn_mc.npz"), **out)
 
 
+def make_egnn_grad(ref_mods, Data):
+    """Parameter gradients of the reference EGNNMultiChannel (float64 autograd) for
+    loss = sum(pred * G) with a seeded G, i.e. dL/dpred = G: the fixture of the native
+    training backward (csrc/egnn_train.hip).  Two widths; N = 5 and 6."""
+    EGNN = ref_mods["egnn"].EGNNMultiChannel
+    DL = ref_mods["egnn_dl"].EgnnMcNBodyDataLoader
+    out = {}
+    for tag, (H, L, B, N) in {"h32": (32, 2, 4, 5), "h64": (64, 3, 3, 6)}.items():
+        loc, vel, force, mass = _initial_states(ref_mods["sim"].GravitySim, B, N)
+        torch.manual_seed(1)
+        model = EGNN(node_input_dim=2, edge_attr_dim=4, hidden_node_dim=H, hidden_edge_dim=H, hidden_coord_dim=H,
+                     num_layers=L, target_names=("pos_dt", "vel"), activation="silu", coords_weight=1.0,
+                     recurrent=True, norm_diff=True, tanh=True, device="cpu").double()
+        fake = types.SimpleNamespace(args=types.SimpleNamespace(batch_size=B, num_neighbors=None),
+                                     dataset=types.SimpleNamespace(num_nodes=N))
+        graph = Data(pos=torch.from_numpy(loc).reshape(-1, 3), vel=torch.from_numpy(vel).reshape(-1, 3),
+                     force=torch.from_numpy(force).reshape(-1, 3), mass=torch.from_numpy(mass).reshape(-1, 1))
+        graph.batch = torch.arange(B).repeat_interleave(N).long()
+        graph = DL.preprocess_batch(fake, graph, device="cpu", training=True)
+        pred = model(graph)
+        G = torch.from_numpy(np.random.default_rng(5).standard_normal(pred.shape))
+        (pred * G).sum().backward()
+        out[f"{tag}/loc"], out[f"{tag}/vel"], out[f"{tag}/mass"] = loc, vel, mass
+        out[f"{tag}/G"], out[f"{tag}/pred"] = G.numpy(), pred.detach().numpy()
+        for k, prm in model.named_parameters():
+            out[f"{tag}/param/{k}"] = prm.detach().numpy()
+            out[f"{tag}/grad/{k}"] = prm.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "egnn_mc_grad.npz"), **out)
+
+
 def main():
     sys.dont_write_bytecode = True   # never write __pycache__ into the read-only reference tree
     ap = argparse.ArgumentParser()
@@ -319,6 +349,10 @@ def main():
         make_ponita(mods, Data)
     if a.only in (None, "egnn_mc"):
         make_egnn_mc(mods, Data)
+    if a.only in ("egnn_grad",):
+        mods["egnn"] = importlib.import_module("models.egnn_mc.egnn_mc")
+        mods["egnn_dl"] = importlib.import_module("dataloaders.egnn_mc_n_body_dataloader")
+        make_egnn_grad(mods, Data)
 
 
 if __name__ == "__main__":

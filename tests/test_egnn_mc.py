@@ -90,7 +90,8 @@ def test_gpu_forward_matches_reference(hip_device, golden):
     gr.vel = torch.tensor(g["vel"].reshape(-1, 3), dtype=torch.float32, device=hip_device)
     gr.mass = torch.tensor(g["mass"].reshape(-1, 1), dtype=torch.float32, device=hip_device)
     gr.edge_index = G.fc_edge_index(4, 5, hip_device)
-    out = model(gr).double().cpu().numpy()
+    with torch.no_grad():   # the inference kernel (grad mode runs the training forward, tested below)
+        out = model(gr).double().cpu().numpy()
     ref = g["f64/pred"]
     assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
 
@@ -126,5 +127,86 @@ def test_gpu_forward_matches_oracle(hip_device, B, N, hidden, layers):
     gr.vel = torch.tensor(vel, dtype=torch.float32, device=hip_device)
     gr.mass = torch.tensor(mass, dtype=torch.float32, device=hip_device)
     gr.edge_index = G.fc_edge_index(B, N, hip_device)
-    out = model(gr).double().cpu().numpy()
+    with torch.no_grad():
+        out = model(gr).double().cpu().numpy()
     assert np.abs(out - ref).max() <= 2e-4 * np.abs(ref).max() + 1e-6
+
+
+# ------------------------------------------------------------------ training step (csrc/egnn_train.hip)
+def _grad_model(Z, tag, device):
+    H = Z[f"{tag}/param/embedding.weight"].shape[0]
+    L = len({k.split(".")[1] for k in Z.files if k.startswith(f"{tag}/param/layers.")})
+    model = make(H, L, torch.float32).to(device)
+    with torch.no_grad():
+        for k, p in model.named_parameters():
+            p.copy_(torch.from_numpy(Z[f"{tag}/param/{k}"]).float())
+    return model
+
+
+def _grad_graph(Z, tag, device):
+    gr = Graph()
+    B, N = Z[f"{tag}/loc"].shape[:2]
+    t = lambda a, w: torch.tensor(a.reshape(-1, w), dtype=torch.float32, device=device)
+    gr.pos, gr.vel, gr.mass = t(Z[f"{tag}/loc"], 3), t(Z[f"{tag}/vel"], 3), t(Z[f"{tag}/mass"], 1)
+    gr.edge_index = G.fc_edge_index(B, N, device)
+    return gr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["h32", "h64"])
+def test_gpu_training_gradients_match_reference(hip_device, golden, tag):
+    """loss = sum(pred * G): every parameter gradient of the native backward against the reference
+    module's float64 autograd (tests/golden/egnn_mc_grad.npz, make_golden.py --only egnn_grad).
+    Tolerance per tensor: |g - ref| <= 2e-4 max|ref| + 1e-7 (fp32 forward + backward)."""
+    Z = golden("egnn_mc_grad")
+    model = _grad_model(Z, tag, hip_device)
+    pred = model(_grad_graph(Z, tag, hip_device))
+    assert pred.grad_fn is not None
+    ref = Z[f"{tag}/pred"]
+    got = pred.detach().double().cpu().numpy()
+    assert np.abs(got - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+    (pred * torch.tensor(Z[f"{tag}/G"], dtype=torch.float32, device=hip_device)).sum().backward()
+    for k, p in model.named_parameters():
+        r = Z[f"{tag}/grad/{k}"]
+        g = p.grad.double().cpu().numpy()
+        assert np.abs(g - r).max() <= 2e-4 * np.abs(r).max() + 1e-7, (k, np.abs(g - r).max(), np.abs(r).max())
+
+
+@pytest.mark.gpu
+def test_gpu_training_step_c1_shape(hip_device):
+    """C1 widths (6 x 128, B = 64, N = 5): an optimizer step through the reference trainer's calls
+    (zero_grad, forward, MSE loss, backward, clip, step) runs on the native path, the gradient is
+    finite and equals the sum of two half-batch gradients (systems are independent)."""
+    torch.manual_seed(0)
+    model = make(128, 6, torch.float32).to(hip_device)
+    rng = np.random.default_rng(3)
+    B, N = 64, 5
+    pos, vel = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3)) * 0.5
+    tgt = torch.tensor(rng.standard_normal((B * N, 6)) * 0.1, dtype=torch.float32, device=hip_device)
+
+    def graph(lo, hi):
+        gr = Graph()
+        gr.pos = torch.tensor(pos[lo * N:hi * N], dtype=torch.float32, device=hip_device)
+        gr.vel = torch.tensor(vel[lo * N:hi * N], dtype=torch.float32, device=hip_device)
+        gr.mass = torch.ones(gr.pos.shape[0], 1, device=hip_device)
+        gr.edge_index = G.fc_edge_index(hi - lo, N, hip_device)
+        return gr
+
+    def grads(lo, hi):
+        model.zero_grad()
+        loss = ((model(graph(lo, hi)) - tgt[lo * N:hi * N]) ** 2).sum()
+        loss.backward()
+        return [p.grad.clone() for p in model.parameters()]
+
+    full, a, b = grads(0, B), grads(0, B // 2), grads(B // 2, B)
+    for f, x, y in zip(full, a, b):
+        assert torch.isfinite(f).all()
+        assert torch.allclose(f, x + y, rtol=1e-4, atol=1e-6 * f.abs().max().item())
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    before = [p.detach().clone() for p in model.parameters()]
+    opt.zero_grad()
+    loss = torch.nn.functional.mse_loss(model(graph(0, B)), tgt)
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    opt.step()
+    assert any(not torch.equal(p0, p1) for p0, p1 in zip(before, model.parameters()))

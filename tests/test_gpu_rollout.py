@@ -41,7 +41,8 @@ def step_forward(model, kind, l, v, m, B, N, device):
     g.pos, g.vel, g.mass, g.edge_index = l, v, m, G.fc_edge_index(B, N, device)
     if kind == "ponita":
         g.x, g.vec = m, v.reshape(-1, 1, 3)
-    return model(g)
+    with torch.no_grad():   # the rollout's inference forward (grad mode would run EGNN-MC's training forward)
+        return model(g)
 
 
 @pytest.mark.parametrize("kind", ["segnn", "ponita", "egnn_mc"])
