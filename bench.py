@@ -19,6 +19,8 @@ Secondary configurations (not the headline; same JSON shape):
                    global batch 4096 sharded over the ranks ("strong" scaling).
   --model egnn_mc  C1: EGNN-MC 6 x 128, N=5, batch 64 per rank ("weak").
   --model eqv2     C4: EquiformerV2 (config.yaml widths), N=20, batch 256 per rank ("weak").
+  --model egnn_mc_train  SURVEY 8(f)4: EGNN-MC training step (C1 widths, forward + backward + Adam,
+                   gradients all-reduced over ranks), batch 64 per rank ("weak").
   --model gravity  C5: ground-truth integrator, 10 000 systems x N=100, --steps
                    KDK steps (sample_freq 10), systems sharded over the ranks ("strong").
 
@@ -28,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -363,6 +366,92 @@ def bench_egnn(a, rank, world, device, P):
     return result
 
 
+# ---------------------------------------------------------------- C1-shaped EGNN-MC training step
+def bench_egnn_train(a, rank, world, device, P):
+    """one training step of the reference trainer (trainer.py:233-358, standard
+    precision): zero_grad, native forward (activations kept), MSE loss, loss.backward() -> native
+    backward (csrc/egnn_train.hip), gradient all-reduce over ranks (data parallel, RCCL), clip to
+    norm 1, Adam step.  C1 widths (6 x 128), N=5, batch 64 per rank ("weak")."""
+    from nbody_amd.egnn_mc import EGNNMultiChannel
+    B, N = a.batch or 64, 5
+    torch.manual_seed(0)
+    model = EGNNMultiChannel(node_input_dim=2, edge_attr_dim=4, hidden_node_dim=128, hidden_edge_dim=128,
+                             hidden_coord_dim=128, num_layers=6, target_names=("pos_dt", "vel"), norm_diff=True,
+                             tanh=True, device=device)
+    loc, vel, mass = initial_states(B, N, rank * B)
+    rng = np.random.default_rng(100 + rank)
+
+    class _G:
+        pass
+    from nbody_amd.graph import fc_edge_index
+    g = _G()
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    g.pos, g.vel, g.mass = t(loc.reshape(-1, 3)), t(vel.reshape(-1, 3)), t(mass.reshape(-1, 1))
+    g.edge_index = fc_edge_index(B, N, device)
+    g.nbx_system_size = N
+    target = t(rng.standard_normal((B * N, 6)) * 0.1)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    params = list(model.parameters())
+
+    def train_step():
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(g), target)
+        loss.backward()
+        if world > 1:   # data parallel: one bucketed all-reduce of every gradient
+            flat = torch.cat([q.grad.reshape(-1) for q in params])
+            torch.distributed.all_reduce(flat)
+            flat /= world
+            o = 0
+            for q in params:
+                q.grad.copy_(flat[o:o + q.numel()].view_as(q))
+                o += q.numel()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        return loss
+
+    for _ in range(max(a.warmup, 1)):
+        train_step()
+
+    def work():
+        for _ in range(a.steps):
+            loss = train_step()
+        return loss
+    loss, elapsed = timed_region(work, device, P)
+    value = a.steps / elapsed * world
+    result = {
+        "metric": "EGNN-MC training steps/sec (C1 widths, forward + backward + Adam)", "value": round(value, 3),
+        "unit": "train steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states, random targets, seeded random-init weights)",
+        "config": {"workload": "SURVEY 8(f)4: EGNN-MC 6 x 128 training step, N=5, batch 64 per GPU, MSE loss, "
+                               "grad-norm clip 1, Adam", "model": "EGNN-MC", "global_batch": B * world,
+                   "seq_len": a.steps, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                     "kernel": "egnn_train_fwd_kernel / egnn_train_bwd_kernel: one workgroup per system",
+                     "note": "64 systems = 64 workgroups of 20-edge fp32 reductions: latency bound like C1"},
+        "loss": float(loss.item()), "finite": bool(math.isfinite(float(loss.item())))}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import egnn_mc_torch as OT
+        Pc = {k: v.detach().double().cpu().clone().requires_grad_(True) for k, v in model.named_parameters()}
+        optc = torch.optim.Adam(list(Pc.values()), lr=1e-4)
+        pc, vc, mc = (torch.from_numpy(x.reshape(-1, w)).double() for x, w in ((loc, 3), (vel, 3), (mass, 1)))
+        tc = target.double().cpu()
+        steps = 10
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            optc.zero_grad()
+            lc = torch.nn.functional.mse_loss(OT.forward(Pc, pc, vc, mc, B, N, 6), tc)
+            lc.backward()
+            torch.nn.utils.clip_grad_norm_(list(Pc.values()), 1.0)
+            optc.step()
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": steps / dt, "unit": "train steps/s", "cores": torch.get_num_threads(),
+                                  "kind": "port", "sample": f"{steps} training steps of the B={B} batch, torch fp64 "
+                                                            f"autograd restatement (oracle/egnn_mc_torch.py), {dt:.2f} s"}
+    return result
+
+
 # ---------------------------------------------------------------- C4 EquiformerV2
 EQV2_C4 = dict(num_layers=4, attn_hidden_channels=64, sphere_channels=64, num_heads=4, attn_alpha_channels=8,
                attn_value_channels=4, ffn_hidden_channels=64, lmax_list=[2], mmax_list=[1], grid_resolution=None,
@@ -532,18 +621,20 @@ def main():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
-    ap.add_argument("--model", default="segnn", choices=["segnn", "ponita", "egnn_mc", "eqv2", "gravity"])
+    ap.add_argument("--model", default="segnn",
+                    choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "eqv2", "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     a = ap.parse_args()
-    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "eqv2": (20, 2), "gravity": (1000, 100)}
+    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5), "eqv2": (20, 2),
+                "gravity": (1000, 100)}
     a.steps = a.steps if a.steps is not None else defaults[a.model][0]
     a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
 
     from nbody_amd import parallel as P
     rank, world, device = P.init_from_env()
-    fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "eqv2": bench_eqv2,
-          "gravity": bench_gravity}[a.model]
+    fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "egnn_mc_train": bench_egnn_train,
+          "eqv2": bench_eqv2, "gravity": bench_gravity}[a.model]
     result = fn(a, rank, world, device, P)
     if rank == 0:
         print(json.dumps(result), flush=True)

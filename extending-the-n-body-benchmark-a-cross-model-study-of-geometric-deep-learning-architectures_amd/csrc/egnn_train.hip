@@ -30,17 +30,37 @@ __device__ inline float et_dsilu(float z) {
     return s * (1.0f + z * (1.0f - s));
 }
 
+// The block-wide products below give every thread RB = 4 independent rows (accumulation chains)
+// of one output column, so each weight load feeds 4 FMAs and the chains overlap their latency.
+constexpr int RB = 4;
+
 // Y[r][n] = b[n] + sum_k X[r][k] W[k][n] (W input-major [K][ldw]); Zs (global, optional) gets the
 // pre-activation; Y gets act(.) with act 1 = SiLU.  X / Y in LDS.  All threads call.
 __device__ void et_gemm(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
                         const float* __restrict__ b, int Nc, float* Y, int ldy, int act, float* Zs) {
-    for (int o = threadIdx.x; o < rows * Nc; o += ET_THREADS) {
-        const int r = o / Nc, n = o - r * Nc;
-        float v = b ? b[n] : 0.f;
-        const float* x = X + r * ldx;
-        for (int k = 0; k < K; ++k) v = fmaf(x[k], W[(size_t)k * ldw + n], v);
-        if (Zs) Zs[r * Nc + n] = v;
-        Y[r * ldy + n] = act == 1 ? et_silu(v) : v;
+    const int rg = (rows + RB - 1) / RB;
+    for (int o = threadIdx.x; o < rg * Nc; o += ET_THREADS) {
+        const int g = o / Nc, n = o - g * Nc, r0 = g * RB;
+        float v[RB];
+        const float* x[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            v[j] = b ? b[n] : 0.f;
+            x[j] = X + (r0 + j < rows ? r0 + j : r0) * ldx;
+        }
+#pragma unroll 16
+        for (int k = 0; k < K; ++k) {
+            const float w = W[(size_t)k * ldw + n];
+#pragma unroll
+            for (int j = 0; j < RB; ++j) v[j] = fmaf(x[j][k], w, v[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            const int r = r0 + j;
+            if (r >= rows) break;
+            if (Zs) Zs[r * Nc + n] = v[j];
+            Y[r * ldy + n] = act == 1 ? et_silu(v[j]) : v[j];
+        }
     }
     __syncthreads();
 }
@@ -48,26 +68,56 @@ __device__ void et_gemm(const float* X, int rows, int ldx, int K, const float* _
 // dX[r][k] (+)= sum_n dZ[r][n] W[k][n]
 __device__ void et_gemm_t(const float* dZ, int rows, int ldz, int Nc, const float* __restrict__ W, int ldw, int K,
                           float* dX, int ldx, bool accumulate) {
-    for (int o = threadIdx.x; o < rows * K; o += ET_THREADS) {
-        const int r = o / K, k = o - r * K;
+    const int rg = (rows + RB - 1) / RB;
+    for (int o = threadIdx.x; o < rg * K; o += ET_THREADS) {
+        const int g = o / K, k = o - g * K, r0 = g * RB;
         const float* w = W + (size_t)k * ldw;
-        const float* z = dZ + r * ldz;
-        float v = 0.f;
-        for (int n = 0; n < Nc; ++n) v = fmaf(z[n], w[n], v);
-        dX[r * ldx + k] = accumulate ? dX[r * ldx + k] + v : v;
+        float v[RB];
+        const float* z[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            v[j] = 0.f;
+            z[j] = dZ + (r0 + j < rows ? r0 + j : r0) * ldz;
+        }
+        // Nc, ldz and ldw are multiples of 4 and the rows 16-byte aligned: float4 along n
+#pragma unroll 4
+        for (int n = 0; n < Nc; n += 4) {
+            const float4 ww = *reinterpret_cast<const float4*>(w + n);
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+                const float4 zz = *reinterpret_cast<const float4*>(z[j] + n);
+                v[j] = fmaf(zz.x, ww.x, fmaf(zz.y, ww.y, fmaf(zz.z, ww.z, fmaf(zz.w, ww.w, v[j]))));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            const int r = r0 + j;
+            if (r >= rows) break;
+            dX[r * ldx + k] = accumulate ? dX[r * ldx + k] + v[j] : v[j];
+        }
     }
     __syncthreads();
 }
 
 // G[k][n] += sum_r X[r][k] dZ[r][n] (k < K), gb[n] += sum_r dZ[r][n]; G / gb global (this
-// workgroup's partial slice), X / dZ in LDS
+// workgroup's partial slice), X / dZ in LDS or global; a thread owns RB consecutive k of one n
 __device__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* dZ, int ldz, int Nc, float* G, int ldg,
                          float* gb) {
-    for (int o = threadIdx.x; o < K * Nc; o += ET_THREADS) {
-        const int k = o / Nc, n = o - k * Nc;
-        float v = 0.f;
-        for (int r = 0; r < rows; ++r) v = fmaf(X[r * ldx + k], dZ[r * ldz + n], v);
-        G[(size_t)k * ldg + n] += v;
+    const int kg = (K + RB - 1) / RB;
+    for (int o = threadIdx.x; o < kg * Nc; o += ET_THREADS) {
+        const int g = o / Nc, n = o - g * Nc, k0 = g * RB;
+        float v[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) v[j] = 0.f;
+        for (int r = 0; r < rows; ++r) {
+            const float z = dZ[r * ldz + n];
+            const float* x = X + r * ldx + k0;
+#pragma unroll
+            for (int j = 0; j < RB; ++j) v[j] = fmaf(k0 + j < K ? x[j] : 0.f, z, v[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+            if (k0 + j < K) G[(size_t)(k0 + j) * ldg + n] += v[j];
     }
     if (gb)
         for (int n = threadIdx.x; n < Nc; n += ET_THREADS) {

@@ -210,3 +210,21 @@ def test_gpu_training_step_c1_shape(hip_device):
     torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
     opt.step()
     assert any(not torch.equal(p0, p1) for p0, p1 in zip(before, model.parameters()))
+
+
+@pytest.mark.parametrize("tag", ["h32", "h64"])
+def test_torch_restatement_matches_reference_gradients(golden, tag):
+    """oracle/egnn_mc_torch.py (the CPU baseline of bench.py --model egnn_mc_train) reproduces the
+    reference's float64 prediction and parameter gradients."""
+    from oracle import egnn_mc_torch as OT
+    Z = golden("egnn_mc_grad")
+    P = {k[len(f"{tag}/param/"):]: torch.from_numpy(Z[k]).clone().requires_grad_(True)
+         for k in Z.files if k.startswith(f"{tag}/param/")}
+    B, N = Z[f"{tag}/loc"].shape[:2]
+    L = len({k.split(".")[1] for k in P if k.startswith("layers.")})
+    t = lambda a, w: torch.from_numpy(a.reshape(-1, w))
+    pred = OT.forward(P, t(Z[f"{tag}/loc"], 3), t(Z[f"{tag}/vel"], 3), t(Z[f"{tag}/mass"], 1), B, N, L)
+    np.testing.assert_allclose(pred.detach().numpy(), Z[f"{tag}/pred"], rtol=1e-10, atol=1e-12)
+    (pred * torch.from_numpy(Z[f"{tag}/G"])).sum().backward()
+    for k, p in P.items():
+        np.testing.assert_allclose(p.grad.numpy(), Z[f"{tag}/grad/{k}"], rtol=1e-9, atol=1e-12, err_msg=k)
