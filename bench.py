@@ -397,14 +397,7 @@ def bench_egnn_train(a, rank, world, device, P):
         opt.zero_grad()
         loss = torch.nn.functional.mse_loss(model(g), target)
         loss.backward()
-        if world > 1:   # data parallel: one bucketed all-reduce of every gradient
-            flat = torch.cat([q.grad.reshape(-1) for q in params])
-            torch.distributed.all_reduce(flat)
-            flat /= world
-            o = 0
-            for q in params:
-                q.grad.copy_(flat[o:o + q.numel()].view_as(q))
-                o += q.numel()
+        P.allreduce_gradients(params)   # data parallel over RCCL (one bucket at C1); no-op on one rank
         torch.nn.utils.clip_grad_norm_(params, 1.0)
         opt.step()
         return loss

@@ -191,3 +191,47 @@ def test_sharded_run_inference_reassembles_in_order(tmp_path):
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
     assert len(res[0][2]) == 4 * 7
+
+
+# ------------------------------------------------------------------ data-parallel gradients
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from nbody_amd import parallel as P
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        lin = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.Tanh(), torch.nn.Linear(7, 3)).double()
+        x = torch.randn(8 * world, 5, dtype=torch.float64)
+        y = torch.randn(8 * world, 3, dtype=torch.float64)
+        sl = slice(8 * rank, 8 * rank + 8)
+        torch.nn.functional.mse_loss(lin(x[sl]), y[sl]).backward()
+        P.allreduce_gradients(lin.parameters(), bucket_bytes=100)   # several buckets
+        q.put((rank, [p.grad.clone() for p in lin.parameters()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_gradients_equals_full_batch_mean_over_gloo():
+    """Each rank's mean-loss gradient on its shard, averaged over ranks, equals the full-batch
+    gradient (equal shards) -- the data-parallel step bench.py --model egnn_mc_train takes."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    lin = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.Tanh(), torch.nn.Linear(7, 3)).double()
+    x = torch.randn(8 * world, 5, dtype=torch.float64)
+    y = torch.randn(8 * world, 3, dtype=torch.float64)
+    torch.nn.functional.mse_loss(lin(x), y).backward()
+    for r in range(world):
+        for g, p in zip(res[r], lin.parameters()):
+            torch.testing.assert_close(g, p.grad, rtol=1e-12, atol=1e-14)
