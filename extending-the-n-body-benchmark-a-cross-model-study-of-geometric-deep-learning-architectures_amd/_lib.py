@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 7
+ABI_VERSION = 8
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
@@ -130,6 +130,10 @@ _SIGNATURES = {
                                                c_sz, c_p]),
     "nbx_segnn_rollout": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
                                          c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_segnn_forward_graph": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
+                                               c_i64, c_p, c_p, c_sz, c_p]),
+    "nbx_segnn_rollout_knn": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
+                                             c_i32, c_i64, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_ponita_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_i64, c_i64,
                                                   ctypes.POINTER(c_sz)]),
     "nbx_ponita_forward": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,

@@ -38,6 +38,7 @@ struct MsgPreProb {
                          // block 0 stores the coefficients to xbn.coef_out for the layer's later consumers
     float* M1S;          // [V*G][2M]
     float* M1V;          // [3][V*G][M]
+    const int* slot;     // general graphs: [V*G] source (local index) per slot, -1 padding; null = fully connected
     long V;
     int N, G, M;
     int NG;              // nodes per group (whole systems, <= 16)

@@ -253,13 +253,14 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                 float4* m1v0 = reinterpret_cast<float4*>(P.M1V + e * M + ch0);
                 float4* m1v1 = reinterpret_cast<float4*>(P.M1V + (Ep + e) * M + ch0);
                 float4* m1v2 = reinterpret_cast<float4*>(P.M1V + (2 * Ep + e) * M + ch0);
-                if (q >= N - 1) {   // padding slot
+                const int d = ld - N * tp_udiv_small(ld, invN);        // position in the system
+                const int sq = P.slot ? P.slot[e] : (q < N - 1 ? (q < d ? q : q + 1) : -1);
+                if (sq < 0) {   // padding slot
                     const float4 z{0.f, 0.f, 0.f, 0.f};
                     m1s[0] = z; m1s[M / 4] = z; *m1v0 = z; *m1v1 = z; *m1v2 = z;
                     continue;
                 }
-                const int d = ld - N * tp_udiv_small(ld, invN);        // position in the system
-                const int sl = ld - d + (q < d ? q : q + 1);            // source node, same group
+                const int sl = ld - d + sq;                              // source node, same group
                 const bool first = it == (et >> 2);
                 const float4 g4 = first ? geo_cur : *reinterpret_cast<const float4*>(P.EG + e * 8);
                 const float pm = first ? pm_cur : P.EG[e * 8 + 4];

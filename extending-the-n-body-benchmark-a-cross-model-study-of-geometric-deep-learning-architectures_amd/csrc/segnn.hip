@@ -9,7 +9,10 @@
 //   EG   [Ep][8]     per edge slot (dst-major): rhat xyz, |rel|, m_src*m_dst
 //   edges are enumerated dst-major in G = next_pow2(N-1) slots per destination:
 //   slot e = dst*G + q, q < N-1 is the edge from the q-th other node of the system,
-//   q >= N-1 is padding (zero rows, masked).  A node's messages are then G
+//   q >= N-1 is padding (zero rows, masked).  General graphs (a kNN graph of
+//   build_graph_with_knn, any simple within-system graph): SLOT [V][G] int32 names the source
+//   (local index) of slot q of each destination, sources ascending, -1 past the node's in-degree
+//   DEG[dst]; padding slots carry |rel| = -1 in EG.  A node's messages are then G
 //   consecutive rows, i.e. registers of one lane in the MFMA accumulator tile,
 //   and aggregate without atomics (Ep = V*G; G = 4 at N = 5: no padding).
 // Every O(3) tensor product with l <= 1 is split into a "scalar-row" GEMM
@@ -56,7 +59,8 @@ __device__ __forceinline__ void featurize_nodes(const float* lpos, const float* 
                                                 const float* __restrict__ mass, int64_t V, int N, int G,
                                                 const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
                                                 float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
-                                                float* __restrict__ XD, int64_t n0, int nn) {
+                                                float* __restrict__ XD, int64_t n0, int nn,
+                                                const int* __restrict__ slot, const float* __restrict__ degv) {
     __shared__ float sx0[NB][8];
     __shared__ float sna[NB][4];
     __shared__ float shs[NB][32][3];   // per (node, edge slot) kSH_C1 * rhat
@@ -67,14 +71,16 @@ __device__ __forceinline__ void featurize_nodes(const float* lpos, const float* 
         const int ln = pq / G, q = pq - ln * G;
         const int64_t node = n0 + ln;
         float* eg = EG + (node * G + q) * 8;
-        if (q >= N - 1) {
-            eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
+        const int64_t b = node / N;
+        const int d = (int)(node - b * N);
+        const int sq = slot ? slot[node * G + q] : (q < N - 1 ? (q < d ? q : q + 1) : -1);
+        if (sq < 0) {   // padding slot (general graphs mark it with |rel| = -1)
+            eg[0] = eg[1] = eg[2] = eg[4] = 0.f;
+            eg[3] = slot ? -1.f : 0.f;
             shs[ln][q][0] = shs[ln][q][1] = shs[ln][q][2] = 0.f;
             continue;
         }
-        const int64_t b = node / N;
-        const int d = (int)(node - b * N);
-        const int64_t s2 = b * N + (q < d ? q : q + 1);
+        const int64_t s2 = b * N + sq;
         const float* ps = lpos + 3 * (s2 - pbase);
         const float* pd = lpos + 3 * (node - pbase);
         const float rx = ps[0] - pd[0], ry = ps[1] - pd[1];
@@ -94,7 +100,7 @@ __device__ __forceinline__ void featurize_nodes(const float* lpos, const float* 
         const float vx = pv[0], vy = pv[1], vz = pv[2];
         float sxh = 0.f, syh = 0.f, szh = 0.f;
         if (par) {
-            for (int q = 0; q < N - 1; ++q) {
+            for (int q = 0; q < (slot ? G : N - 1); ++q) {
                 sxh += shs[t][q][0]; syh += shs[t][q][1]; szh += shs[t][q][2];
             }
         } else {
@@ -117,11 +123,13 @@ __device__ __forceinline__ void featurize_nodes(const float* lpos, const float* 
                 eg[0] = eg[1] = eg[2] = eg[3] = eg[4] = 0.f;
             }
         }
-        const float cnt = (float)(N - 1 > 0 ? N - 1 : 1);
+        // scatter(reduce="mean") at edge_index[1]: a node without incoming edges gets 0
+        const float cnt = slot ? degv[node] : (float)(N - 1);
+        const float inv_cnt = cnt > 0.f ? 1.0f / cnt : 0.f;
         const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
         const float vden = fmaxf(vn, 1e-12f);
-        const float na1 = sxh / cnt + kSH_C1 * (vx / vden), na2 = syh / cnt + kSH_C1 * (vy / vden);
-        const float na3 = szh / cnt + kSH_C1 * (vz / vden);
+        const float na1 = sxh * inv_cnt + kSH_C1 * (vx / vden), na2 = syh * inv_cnt + kSH_C1 * (vy / vden);
+        const float na3 = szh * inv_cnt + kSH_C1 * (vz / vden);
         NA[4 * node + 0] = 1.0f; NA[4 * node + 1] = na1; NA[4 * node + 2] = na2; NA[4 * node + 3] = na3;
         sna[t][0] = 1.0f; sna[t][1] = na1; sna[t][2] = na2; sna[t][3] = na3;
         const float mp = (px + py + pz) / 3.0f;  // pos.mean(1): mean over xyz (reference quirk)
@@ -159,12 +167,13 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
                                        const float* __restrict__ mass, int64_t V, int N, int G,
                                        const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
                                        float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
-                                       float* __restrict__ XD, double* __restrict__ zsum, int nzero) {
+                                       float* __restrict__ XD, double* __restrict__ zsum, int nzero,
+                                       const int* __restrict__ slot, const float* __restrict__ degv) {
     // zero the forward's atomic BatchNorm sums (nzero = 0: not in use)
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += gridDim.x * blockDim.x) zsum[i] = 0.0;
     const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
     const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
-    featurize_nodes<FE_NODES>(pos, vel, 0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn);
+    featurize_nodes<FE_NODES>(pos, vel, 0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn, slot, degv);
 }
 
 // ---------------------------------------------------------------- message
@@ -175,7 +184,7 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
 // then Gate -> M1S [E][2M] = [m_s | m_v . rhat], M1V [3][E][M] = m_v
 __global__ void msg1_kernel(const float* __restrict__ NP, const float* __restrict__ EG,
                             const float* __restrict__ amfw, const float* __restrict__ bias, int64_t V, int N, int G,
-                            int M, float* __restrict__ M1S, float* __restrict__ M1V) {
+                            int M, float* __restrict__ M1S, float* __restrict__ M1V, const int* __restrict__ slot) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
     const int64_t E = V * G;
@@ -186,15 +195,16 @@ __global__ void msg1_kernel(const float* __restrict__ NP, const float* __restric
     for (int64_t e = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; e < E && e < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; e += EW_Y) {
         const int64_t dn = e / G;
         const int q = (int)(e - dn * G);
-        if (q >= N - 1) {  // padding slot
+        const int64_t b = dn / N;
+        const int d = (int)(dn - b * N);
+        const int sq = slot ? slot[e] : (q < N - 1 ? (q < d ? q : q + 1) : -1);
+        if (sq < 0) {  // padding slot
             M1S[e * 2 * M + w] = 0.f;
             M1S[e * 2 * M + M + w] = 0.f;
             for (int k = 0; k < 3; ++k) M1V[((int64_t)k * E + e) * M + w] = 0.f;
             continue;
         }
-        const int64_t b = dn / N;
-        const int d = (int)(dn - b * N);
-        const int64_t sn = b * N + (q < d ? q : q + 1);
+        const int64_t sn = b * N + sq;
         const float* eg = EG + e * 8;
         const float hx = eg[0], hy = eg[1], hz = eg[2], dist = eg[3], pm = eg[4];
         const float* sd = NP + dn * ld;
@@ -303,17 +313,17 @@ __global__ __launch_bounds__(BNF_THREADS) void bn_finalize_kernel(
 __global__ void upd_pre_kernel(const float* __restrict__ X, const float* __restrict__ AGG,
                                const float* __restrict__ NA, const float* __restrict__ coef,
                                const float* __restrict__ xcoef, float deg, int64_t V, int M,
-                               float* __restrict__ U1S, float* __restrict__ U1V) {
+                               float* __restrict__ U1S, float* __restrict__ U1V, const float* __restrict__ degv) {
     const int w = blockIdx.y * EW_X + threadIdx.x;
     if (w >= M) return;
-    const float sc_s = coef[w], sc_v = coef[M + w], sh = coef[2 * M + w] * deg;
+    const float sc_s = coef[w], sc_v = coef[M + w], sh1 = coef[2 * M + w];
     // pending feature BatchNorm of X (previous layer; identity for layer 0)
     const float xs_sc = xcoef ? xcoef[w] : 1.f, xv_sc = xcoef ? xcoef[M + w] : 1.f;
     const float xs_sh = xcoef ? xcoef[2 * M + w] : 0.f;
     for (int64_t n = blockIdx.x * (int64_t)ROWS_PER_BLOCK + threadIdx.y; n < V && n < (blockIdx.x + 1) * (int64_t)ROWS_PER_BLOCK; n += EW_Y) {
         const float* na = NA + 4 * n;
         const float xs = fmaf(xs_sc, X[n * M + w], xs_sh);
-        const float as = sc_s * AGG[n * M + w] + sh;
+        const float as = sc_s * AGG[n * M + w] + sh1 * (degv ? degv[n] : deg);   // deg: in-degree
         float xdot = 0.f, adot = 0.f;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -445,7 +455,8 @@ __global__ __launch_bounds__(64 * RPP2_MAX) void rollout_pp2_kernel(
     const int nn = (int)(V - n0 < nb ? V - n0 : nb);
     if (wv < nn) pp2_node(H2S, H2V, NA, W, V, M, out, U, n0 + wv, threadIdx.x & 63, spos[wv], svel[wv]);
     __syncthreads();   // all of this block's NA reads are done before featurize_nodes rewrites it
-    featurize_nodes<RPP2_MAX>(&spos[0][0], &svel[0][0], n0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn);
+    featurize_nodes<RPP2_MAX>(&spos[0][0], &svel[0][0], n0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn,
+                              nullptr, nullptr);
 }
 
 // self-feed state update (infer_self_feed.py:182-194, target pos_dt+vel) and trajectory write
@@ -467,6 +478,71 @@ __global__ void rollout_update_kernel(float* __restrict__ pos, float* __restrict
     const int64_t o = ((b * num_frames + frame) * N + d) * 3 + k;
     traj_pos[o] = p;
     traj_vel[o] = v;
+}
+
+// ---------------------------------------------------------------- general graphs
+// A graph's adjacency per destination: ADJ[dst] bit s = an edge from local node s of dst's system.
+// From an edge_index (utils/build_fully_connected_graph.py layout, [2][E] int64, row = source,
+// col = target): err bits 1 out of range, 2 across systems, 4 self-loop, 8 duplicate edge.
+__global__ void graph_adj_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t V, int N,
+                                 unsigned long long* __restrict__ adj, int* __restrict__ err) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = ei[e], t = ei[E + e];
+        int bad = 0;
+        if (s < 0 || t < 0 || s >= V || t >= V) bad = 1;
+        else if (s / N != t / N) bad = 2;
+        else if (s == t) bad = 4;
+        if (bad) { atomicOr(err + (e & 63), bad); continue; }
+        const unsigned long long bit = 1ull << (int)(s - (s / N) * N);
+        if (atomicOr(adj + t, bit) & bit) atomicOr(err + (e & 63), 8);
+    }
+}
+
+// kNN branch of build_graph_with_knn (build_fully_connected_graph.py:42-80) straight into the
+// adjacency: node i's k nearest others by (fp64 distance, index), the first pick (self) dropped,
+// exactly as nbx_knn_edge_index (csrc/graph.hip) selects them; edges i -> neighbour.
+__global__ void knn_adj_kernel(const float* __restrict__ pos, int64_t V, int N, int k,
+                               unsigned long long* __restrict__ adj) {
+    const int64_t node = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (node >= V) return;
+    const int64_t b = node / N;
+    const int i = (int)(node - b * N);
+    const float* sys = pos + b * N * 3;
+    double d[33];
+    const double xi = sys[3 * i], yi = sys[3 * i + 1], zi = sys[3 * i + 2];
+    for (int j = 0; j < N; ++j) {
+        const double dx = xi - (double)sys[3 * j], dy = yi - (double)sys[3 * j + 1], dz = zi - (double)sys[3 * j + 2];
+        d[j] = sqrt(dx * dx + dy * dy + dz * dz);
+    }
+    unsigned long long taken = 0;
+    for (int s = 0; s <= k; ++s) {
+        int best = -1;
+        for (int j = 0; j < N; ++j) {
+            if ((taken >> j) & 1ull) continue;
+            if (best < 0 || d[j] < d[best]) best = j;
+        }
+        taken |= 1ull << best;
+        if (s > 0) atomicOr(adj + b * N + best, 1ull << i);
+    }
+}
+
+// adjacency -> slot table (sources ascending) and in-degree; err bit 16: in-degree above G
+// (only possible with self-loops, which the kNN selection yields for coincident nodes)
+__global__ void graph_slots_kernel(const unsigned long long* __restrict__ adj, int64_t V, int G,
+                                   int* __restrict__ slot, float* __restrict__ degv, int* __restrict__ err) {
+    const int64_t node = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (node >= V) return;
+    unsigned long long m = adj[node];
+    int q = 0;
+    while (m) {
+        const int s = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        if (q < G) slot[node * G + q] = s;
+        ++q;
+    }
+    if (q > G) atomicOr(err + (node & 63), 16);
+    degv[node] = (float)(q < G ? q : G);
+    for (int r = q; r < G; ++r) slot[node * G + r] = -1;
 }
 
 // ---------------------------------------------------------------- host side
@@ -504,6 +580,10 @@ int64_t partial_doubles(const Dims& d) {
 struct Workspace {
     float *X, *NA, *EG, *NP, *M1S, *M1V, *AGG, *U1S, *U1V, *U2S, *U2V, *coef_msg, *coef_feat, *out;
     float *XD, *AD;   // x_v . na and aggregated a_v . na per node and channel (segmented update_layer_1)
+    int* SLOT;        // general graphs: [Ep] source of each slot (-1 padding)
+    float* DEG;       // general graphs: [V] in-degree
+    unsigned long long* ADJ;   // general graphs: [V] source bit masks
+    int* ERR;         // general graphs: [64] validation flags
     double* partial;
     double* bn_sums;  // atomic-mode BatchNorm sums: [2 x NBX_SEGNN_MAX_LAYERS][3][M] (message, feature per layer)
     size_t bytes;
@@ -538,6 +618,10 @@ size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
     w.out = (float*)take(6 * V, 4);
     w.XD = (float*)take(V * M, 4);
     w.AD = (float*)take(V * M, 4);
+    w.SLOT = (int*)take(Ep, 4);
+    w.DEG = (float*)take(V, 4);
+    w.ADJ = (unsigned long long*)take(V, 8);
+    w.ERR = (int*)take(64, 4);
     w.bytes = (off + 255) & ~size_t(255);
     if (ws) *ws = w;
     return w.bytes;
@@ -862,9 +946,15 @@ nbx::TpProb tp_base(int rows, const Dims& d) {
     return p;
 }
 
+// A general (non fully-connected) graph as slot tables in the workspace (ws.SLOT / ws.DEG),
+// `edges` real edges in total.
+struct GraphSlots {
+    double edges;
+};
+
 int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass, int64_t B,
                  int64_t N, float* out, const Workspace& ws, hipStream_t st, KernelTiming* tm = nullptr,
-                 const RolloutUpdate* upd = nullptr, bool featurized = false) {
+                 const RolloutUpdate* upd = nullptr, bool featurized = false, const GraphSlots* gr = nullptr) {
     const int M = w->mul;
     const Dims d = dims_of(B, N, M);
     const int64_t V = d.V, Ep = d.Ep;
@@ -873,7 +963,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
 
     // update_layer_1 reads its [x | BN(agg)] input straight from X / AGG and the two dot buffers
     // (no materialised U1) when the static segmented schedule applies (mul = 96 or 32)
-    const bool seg_upd = static_enabled() && (M == 96 || M == 32);
+    // (general graphs: the segmented input folds the message BN shift x a constant degree, so
+    // they take the materialised path with per-node in-degrees)
+    const bool seg_upd = static_enabled() && (M == 96 || M == 32) && !gr;
+    const int* slot = gr ? ws.SLOT : nullptr;
+    const float* degv = gr ? ws.DEG : nullptr;
     // block: whole multiples of the channel count (192 threads at mul = 96), >= FE_NODES
     const unsigned fe_threads = (unsigned)std::max(64, std::min(1024, M * std::max(1, 256 / M)));
     // Lazy feature BatchNorm: X in HBM holds each layer's pre-normalisation output and its
@@ -889,11 +983,12 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // producing kernel and the finalising consumer, and normalised by the global counts
     const bool sync = w->bn_allreduce != nullptr && w->training;
     if (sync && !bn_atomic) {
-        nbx::set_error("segnn: SyncBN (bn_allreduce) needs the atomic BatchNorm path (mul 96 or 32, 2 <= N <= 16)");
+        nbx::set_error("segnn: SyncBN (bn_allreduce) needs the atomic BatchNorm path (mul 96 or 32, 2 <= N <= 16, "
+                       "fully-connected graphs)");
         return NBX_E_UNSUPPORTED;
     }
     const int64_t Bg = sync && w->bn_global_batch > 0 ? w->bn_global_batch : B;
-    const double cnt_nodes = (double)(Bg * N), cnt_edges = (double)(Bg * N * (N - 1));
+    const double cnt_nodes = (double)(Bg * N), cnt_edges = gr ? gr->edges : (double)(Bg * N * (N - 1));
     auto sync_bn = [&](double* sums) -> int {
         if (!sync) return NBX_OK;
         if (w->bn_allreduce(sums, (int64_t)3 * M, (void*)st, w->bn_allreduce_ctx) != 0) {
@@ -908,7 +1003,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     if (!featurized) {
         hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st,
                            pos, vel, mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
-                           seg_upd ? ws.XD : nullptr, ws.bn_sums, nzero);
+                           seg_upd ? ws.XD : nullptr, ws.bn_sums, nzero, slot, degv);
         NBX_LAUNCH_CHECK("embed");
     }
 
@@ -929,6 +1024,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             mp.X = ws.X; mp.Simg = L.node_pre_s_img; mp.Vimg = L.node_pre_v_img; mp.EG = ws.EG;
             mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V; mp.xcoef = xprev;
             mp.V = V; mp.N = (int)N; mp.G = (int)d.G; mp.M = M; mp.NG = nbx::msg_pre_group((int)N);
+            mp.slot = slot;
             if (bn_atomic && l > 0) {
                 const nbx_segnn_layer& Lp = w->layers[l - 1];
                 mp.xbn = nbx::BnSrc{sums_of(l - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias, Lp.feat_bn_running_mean,
@@ -968,7 +1064,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 if (int rc = run_tp16_pair<3, 0, nbx::TP_PLAIN, 2>(pp[0], pp[1], st, tm)) return rc;
             }
             hipLaunchKernelGGL(msg1_kernel, ew_grid(Ep, M), ewb, 0, st, ws.NP, ws.EG, L.msg1_amf, L.msg1_bias, V,
-                               (int)N, (int)d.G, M, ws.M1S, ws.M1V);
+                               (int)N, (int)d.G, M, ws.M1S, ws.M1V, slot);
             NBX_LAUNCH_CHECK("msg1");
         }
         int wpc_msg = 1, cw_msg = 16;
@@ -978,7 +1074,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.As = ws.M1S; p.lda_s = 2 * M; p.B = L.msg2_img;
             p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
             p.Av = ws.M1V; p.lda_v = M; p.plane_stride = Ep * M; p.Kv = M;
-            p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G; p.valid_per_group = (int)(N - 1);
+            p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G;
+            p.valid_per_group = gr ? (int)d.G : (int)(N - 1);   // general graphs: padding rows have |rel| < 0
             p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
             if (seg_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
             if (bn_atomic) p.bn_sums = sums_of(l, 0);
@@ -995,7 +1092,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         }
         if (!bn_atomic) {
             hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, cw_msg)), dim3(BNF_THREADS), 0, st,
-                               ws.partial, wpc_msg, cw_msg, (double)(V * (N - 1) > 0 ? V * (N - 1) : 1), M, w->training,
+                               ws.partial, wpc_msg, cw_msg, std::max(1.0, cnt_edges), M, w->training,
                                w->bn_eps, w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
                                L.msg_bn_running_var, ws.coef_msg);
             NBX_LAUNCH_CHECK("bn_finalize(msg)");
@@ -1027,7 +1124,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             }
         } else {
             hipLaunchKernelGGL(upd_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.AGG, ws.NA, ws.coef_msg, xprev,
-                               (float)(N - 1), V, M, ws.U1S, ws.U1V);
+                               (float)(N - 1), V, M, ws.U1S, ws.U1V, degv);
             NBX_LAUNCH_CHECK("upd_pre");
             {
                 // update_layer_1 + gate -> inputs of update_layer_2
@@ -1124,7 +1221,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         }
     }
     }
-    if (upd && upd->featurize_next) {
+    if (upd && upd->featurize_next && !gr) {
         const int nb = (int)N * std::max(1, 8 / (int)N);   // whole systems, N <= RPP2_MAX
         hipLaunchKernelGGL(rollout_pp2_kernel, dim3((unsigned)nbx::ceil_div(V, nb)), dim3(64 * nb), 0, st, ws.U2S,
                            ws.U2V, ws.NA, w->pp2, V, M, out, *upd, nb, mass, (int)N, (int)d.G, w->emb, w->emb_bias,
@@ -1189,6 +1286,92 @@ extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* 
         const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N, fuse && f + 1 < num_frames,
                                 (flags & NBX_ROLLOUT_ABSOLUTE) ? 1 : 0};
         if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd, fuse && f >= 2)) return rc;
+    }
+    return NBX_OK;
+}
+
+namespace {
+
+// Slot tables of a graph given as an edge_index, validated (one host synchronisation).
+int slots_from_edges(const int64_t* ei, int64_t E, int64_t B, int64_t N, const Workspace& ws, hipStream_t st) {
+    const Dims d = dims_of(B, N, 4);
+    NBX_HIP(hipMemsetAsync(ws.ADJ, 0, sizeof(unsigned long long) * d.V, st));
+    NBX_HIP(hipMemsetAsync(ws.ERR, 0, sizeof(int) * 64, st));
+    if (E > 0) {
+        const unsigned blocks = (unsigned)std::min<int64_t>(nbx::ceil_div(E, 256), 65536);
+        hipLaunchKernelGGL(graph_adj_kernel, dim3(blocks), dim3(256), 0, st, ei, E, d.V, (int)N, ws.ADJ, ws.ERR);
+        NBX_LAUNCH_CHECK("graph_adj");
+    }
+    hipLaunchKernelGGL(graph_slots_kernel, dim3((unsigned)nbx::ceil_div(d.V, 256)), dim3(256), 0, st, ws.ADJ, d.V,
+                       (int)d.G, ws.SLOT, ws.DEG, ws.ERR);
+    NBX_LAUNCH_CHECK("graph_slots");
+    int herr[64];
+    NBX_HIP(hipMemcpyAsync(herr, ws.ERR, sizeof(herr), hipMemcpyDeviceToHost, st));
+    NBX_HIP(hipStreamSynchronize(st));
+    int e = 0;
+    for (int i = 0; i < 64; ++i) e |= herr[i];
+    if (e) {
+        nbx::set_error("segnn: unsupported edge_index (%s%s%s%s%s)", (e & 1) ? "node index out of range " : "",
+                       (e & 2) ? "edge between systems " : "", (e & 4) ? "self-loop " : "",
+                       (e & 8) ? "duplicate edge " : "", (e & 16) ? "in-degree above the slot count" : "");
+        return NBX_E_INVAL;
+    }
+    return NBX_OK;
+}
+
+// kNN slot tables from the current positions (no synchronisation)
+int slots_from_knn(const float* pos, int64_t B, int64_t N, int k, const Workspace& ws, hipStream_t st) {
+    const Dims d = dims_of(B, N, 4);
+    NBX_HIP(hipMemsetAsync(ws.ADJ, 0, sizeof(unsigned long long) * d.V, st));
+    const unsigned blocks = (unsigned)nbx::ceil_div(d.V, 128);
+    hipLaunchKernelGGL(knn_adj_kernel, dim3(blocks), dim3(128), 0, st, pos, d.V, (int)N, k, ws.ADJ);
+    NBX_LAUNCH_CHECK("knn_adj");
+    hipLaunchKernelGGL(graph_slots_kernel, dim3((unsigned)nbx::ceil_div(d.V, 256)), dim3(256), 0, st, ws.ADJ, d.V,
+                       (int)d.G, ws.SLOT, ws.DEG, ws.ERR);
+    NBX_LAUNCH_CHECK("graph_slots");
+    return NBX_OK;
+}
+
+}  // namespace
+
+extern "C" int nbx_segnn_forward_graph(const nbx_segnn_weights* w, const float* pos, const float* vel,
+                                       const float* mass, int64_t B, int64_t N, const int64_t* edge_index,
+                                       int64_t num_edges, float* out, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
+    Workspace ws;
+    if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    NBX_CHECK_ARG(num_edges >= 1 && edge_index != nullptr, "nbx_segnn_forward_graph: need at least one edge");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = slots_from_edges(edge_index, num_edges, B, N, ws, st)) return rc;
+    const GraphSlots gr{(double)num_edges};
+    return forward_impl(w, pos, vel, mass, B, N, out, ws, st, nullptr, nullptr, false, &gr);
+}
+
+extern "C" int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass, int64_t B,
+                                     int64_t N, int64_t num_frames, int32_t flags, int64_t num_neighbors,
+                                     float* traj_pos, float* traj_vel, void* workspace, size_t workspace_bytes,
+                                     void* stream) {
+    if (num_neighbors < 0) num_neighbors = N - 1;   // the reference's None
+    NBX_CHECK_ARG(num_neighbors < N, "Graph cannot have more neighbors than there are nodes in simulation - 1");
+    if (num_neighbors == N - 1)   // build_graph_with_knn returns the fully-connected pattern
+        return nbx_segnn_rollout(w, pos, vel, mass, B, N, num_frames, flags, traj_pos, traj_vel, workspace,
+                                 workspace_bytes, stream);
+    NBX_CHECK_ARG(num_neighbors >= 1, "nbx_segnn_rollout_knn: num_neighbors must be >= 1");
+    Workspace ws;
+    if (int rc = prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    NBX_CHECK_ARG(num_frames >= 1, "nbx_segnn_rollout_knn: num_frames must be >= 1");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t V = B * N;
+    hipLaunchKernelGGL(rollout_update_kernel, dim3((unsigned)nbx::ceil_div(V * 3, 256)), dim3(256), 0, st, pos, vel,
+                       ws.out, V, (int)N, (int64_t)0, num_frames, traj_pos, traj_vel);
+    NBX_LAUNCH_CHECK("rollout_update");
+    const GraphSlots gr{(double)(V * num_neighbors)};
+    for (int64_t f = 1; f < num_frames; ++f) {
+        // the graph is rebuilt from each frame's positions (infer_self_feed.py:121-123)
+        if (int rc = slots_from_knn(pos, B, N, (int)num_neighbors, ws, st)) return rc;
+        const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N, 0,
+                                (flags & NBX_ROLLOUT_ABSOLUTE) ? 1 : 0};
+        if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd, false, &gr)) return rc;
     }
     return NBX_OK;
 }

@@ -587,8 +587,9 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) {
                         const int row = row0 + jj;
-                        const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group;
                         const float* gm = P.geom + (size_t)(row < P.rows ? row : 0) * 8;
+                        const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group &&
+                                        gm[3] >= 0.f;   // |rel| < 0: a general graph's padding slot
                         const float s = kC_SILU * tp_silu(acc[g][0][jj] + ba);
                         const float gg = kC_SIGMOID * tp_sigmoid(acc[g][1][jj] + bg);
                         const float tt = acc[g][2][jj];

@@ -563,8 +563,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                 for (int e = 0; e < 16; ++e) {
                     const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
                     const int row = row0 + rr;
-                    const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group;
-                    const float4 g = gl[rr];
+                    const float4 g = gl[rr];   // .w = |rel|, < 0 on a general graph's padding slots
+                    const bool ok = live && row < P.rows && (row & (P.group - 1)) < P.valid_per_group && g.w >= 0.f;
                     const float s = kC_SILU * tp_silu(acc[0][e] + ba);
                     const float gg = kC_SIGMOID * tp_sigmoid(acc[1][e] + bg);
                     const float tt = acc[2][e];

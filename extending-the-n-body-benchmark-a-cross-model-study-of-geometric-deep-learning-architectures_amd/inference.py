@@ -16,6 +16,7 @@ a warning.
 from __future__ import annotations
 
 import json
+import inspect
 import os
 import re
 import warnings
@@ -198,8 +199,15 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
     output_dims = loc_actual.shape[-1]
     n_nodes = loc_actual.shape[-2]
     num_neighbors = num_neighbors if num_neighbors is not None else n_nodes - 1
-    if num_neighbors != n_nodes - 1:
-        raise NotImplementedError("the native rollout runs fully-connected systems (num_neighbors = N - 1)")
+    knn = {}
+    if model_type in ("segnn", "ponita"):   # the branches that build_graph_with_knn (lines 121-123, 137-139)
+        if num_neighbors >= n_nodes:
+            raise ValueError("Graph cannot have more neighbors than there are nodes in simulation - 1")
+        if num_neighbors != n_nodes - 1:
+            if "num_neighbors" not in inspect.signature(model.rollout).parameters:
+                raise NotImplementedError(f"native {model_type} rollout: kNN graphs (num_neighbors < N-1) "
+                                          "are not supported")
+            knn = {"num_neighbors": int(num_neighbors)}
     num_steps = loc_actual.shape[1]
     if max_rollout_steps is not None:
         try:
@@ -221,6 +229,7 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
               + (f", {count} on rank {P.rank()} of {world})" if shard else ")"))
     # infer_self_feed.py:185-186: only "pos_dt+vel" adds the prediction to the previous position
     kw = {"absolute": True} if dataset.target != "pos_dt+vel" else {}
+    kw.update(knn)
     sync = shard and hasattr(model, "enable_sync_batchnorm") and model.training
     if sync:
         model.enable_sync_batchnorm()

@@ -435,23 +435,40 @@ class SEGNN(nn.Module):
             raise NotImplementedError("native SEGNN needs fully-connected systems of equal size")
         return num_nodes // n, n
 
+    def _graph_layout(self, graph, V, E, device):
+        """(B, N, fully_connected) of a batched graph of equal-size systems.  N comes from
+        ``graph.nbx_system_size`` (this package's dataloaders), else from ``graph.batch`` (the
+        reference's graphs: arange(B).repeat_interleave(N)), else from a fully-connected edge count."""
+        N = getattr(graph, "nbx_system_size", None)
+        batch = getattr(graph, "batch", None)
+        if N is not None:
+            N = int(N)
+        elif batch is not None and batch.numel() == V:
+            b = batch.to(device)
+            B = int(b.max().item()) + 1
+            if V % B or not torch.equal(b, torch.arange(B, device=device).repeat_interleave(V // B)):
+                raise NotImplementedError("native SEGNN needs contiguous systems of equal size")
+            N = V // B
+        else:
+            B, N = self.infer_system_size(V, E)
+        if V % N:
+            raise NotImplementedError("native SEGNN needs systems of equal size")
+        B = V // N
+        fc = E == V * (N - 1)
+        if fc and getattr(graph, "nbx_system_size", None) is None:
+            from .graph import _fc_edge_index_shared as fc_edge_index
+            fc = torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device))
+        return B, N, fc
+
     def forward(self, graph):
-        """graph: pos [V,3], vel [V,3], mass [V,1], edge_index (fully connected,
-        utils/build_fully_connected_graph.py order).  Returns [V, 6] in the
-        graph's dtype; computes in fp32."""
+        """graph: pos [V,3], vel [V,3], mass [V,1], edge_index (build_graph_with_knn: the
+        fully-connected pattern, its kNN graphs, or any simple graph inside equal-size systems),
+        batch.  Returns [V, 6] in the graph's dtype; computes in fp32."""
         pos = graph.pos
         device = pos.device
         V = pos.shape[0]
         edge_index = graph.edge_index
-        if getattr(graph, "nbx_system_size", None) is not None:
-            N = int(graph.nbx_system_size)
-            B = V // N
-        else:
-            B, N = self.infer_system_size(V, edge_index.shape[1])
-            from .graph import _fc_edge_index_shared as fc_edge_index
-            if not torch.equal(edge_index.to(device), fc_edge_index(B, N, device)):
-                raise NotImplementedError("native SEGNN needs the fully-connected edge_index of "
-                                          "build_graph_with_knn (num_neighbors = N-1)")
+        B, N, fc = self._graph_layout(graph, V, edge_index.shape[1], device)
         out_dtype = pos.dtype
         if out_dtype != torch.float32 and not self._warned_dtype:
             warnings.warn("SEGNN HIP path computes in fp32; inputs are cast", stacklevel=2)
@@ -464,17 +481,26 @@ class SEGNN(nn.Module):
         ws = self._workspace(B, N, device)
         self._arm_sync(W, B, device)
         self._bn_sync_in()
-        _lib.check(_lib.lib().nbx_segnn_forward(
-            W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(out),
-            _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_forward")
+        if fc:
+            _lib.check(_lib.lib().nbx_segnn_forward(
+                W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(out),
+                _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_forward")
+        else:
+            ei = edge_index.to(device=device, dtype=torch.int64).contiguous()
+            _lib.check(_lib.lib().nbx_segnn_forward_graph(
+                W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(ei), ei.shape[1],
+                _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                "nbx_segnn_forward_graph")
         self._bn_sync_out()
         return out.to(out_dtype)
 
     @torch.no_grad()
-    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False):
+    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False, num_neighbors=None):
         """Device-resident self-feed (infer_self_feed.py:99-194): loc/vel [B,N,3], mass [B,N,1]
         -> (traj_loc, traj_vel) [B, num_frames, N, 3] fp32.  ``absolute``: the model predicts
-        positions (dataset targets other than "pos_dt+vel", infer_self_feed.py:185-186)."""
+        positions (dataset targets other than "pos_dt+vel", infer_self_feed.py:185-186).
+        ``num_neighbors``: each frame's graph is build_graph_with_knn's kNN graph of that frame's
+        positions (None / N-1: fully connected)."""
         device = loc.device
         self._check_params(device)
         B, N, _ = loc.shape
@@ -486,9 +512,18 @@ class SEGNN(nn.Module):
         ws = self._workspace(B, N, device)
         self._arm_sync(W, B, device)
         self._bn_sync_in()
-        _lib.check(_lib.lib().nbx_segnn_rollout(
-            W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames,
-            _lib.ROLLOUT_ABSOLUTE if absolute else 0, _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
-            ws.numel(), _lib.stream_ptr(device)), "nbx_segnn_rollout")
+        flags = _lib.ROLLOUT_ABSOLUTE if absolute else 0
+        if num_neighbors is None or int(num_neighbors) == N - 1:
+            _lib.check(_lib.lib().nbx_segnn_rollout(
+                W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames, flags,
+                _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                "nbx_segnn_rollout")
+        else:
+            if self._bn_group is not None and self.training:
+                raise NotImplementedError("SyncBN rollouts need fully-connected graphs")
+            _lib.check(_lib.lib().nbx_segnn_rollout_knn(
+                W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames, flags,
+                int(num_neighbors), _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(),
+                _lib.stream_ptr(device)), "nbx_segnn_rollout_knn")
         self._bn_sync_out()
         return tp, tv

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 7
+#define NBX_ABI_VERSION 8
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -218,6 +218,27 @@ int nbx_segnn_forward_timed(const nbx_segnn_weights* w, const float* pos, const 
 int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass,
                       int64_t batch_size, int64_t num_nodes, int64_t num_frames, int32_t flags,
                       float* traj_pos, float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
+
+/* General graphs (ABI 8).  nbx_segnn_forward on the graph `edge_index` (int64 [2][num_edges],
+ * device memory, row = source, col = target: the layout of build_graph_with_knn,
+ * utils/build_fully_connected_graph.py:23-80, e.g. its kNN branch with num_neighbors < N-1) instead
+ * of the fully-connected pattern: messages flow source -> target and aggregate at the target
+ * (MessagePassing aggr="add"), node attributes average the edge attributes over a node's incoming
+ * edges (0 for a node without any, O3Transform's scatter mean), the message BatchNorm counts the real
+ * edges.  Every edge must join two different nodes of one system, without duplicates; returns
+ * NBX_E_INVAL otherwise.  Synchronises `stream` once (the validation).  Not with SyncBN. */
+int nbx_segnn_forward_graph(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
+                            int64_t batch_size, int64_t num_nodes, const int64_t* edge_index, int64_t num_edges,
+                            float* out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* nbx_segnn_rollout with the reference's num_neighbors (infer_self_feed.py:58,121-123): every frame's
+ * graph is the kNN graph of that frame's positions (build_graph_with_knn's kNN branch, selected on
+ * the device as nbx_knn_edge_index does).  num_neighbors = N-1 or < 0 (None): the fully-connected
+ * nbx_segnn_rollout; >= N: NBX_E_INVAL (the reference's ValueError). */
+int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, const float* mass,
+                          int64_t batch_size, int64_t num_nodes, int64_t num_frames, int32_t flags,
+                          int64_t num_neighbors, float* traj_pos, float* traj_vel, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 
 /* ------------------------------------------------------------------------

@@ -14,11 +14,12 @@ from .graph import build_graph_with_knn
 from .segnn import o3_transform
 
 
-def segnn_step(model, params, training=True, lmax_attr=1):
+def segnn_step(model, params, training=True, lmax_attr=1, num_neighbors=None):
     """SEGNN branch (lines 115-130).  BatchNorm running stats are updated in
-    ``params`` after every step, as the train-mode reference module does."""
+    ``params`` after every step, as the train-mode reference module does.
+    ``num_neighbors``: the kNN graph of each frame (None: N - 1, fully connected)."""
     def f(loc, vel, force, mass, B, N):
-        ei = build_graph_with_knn(loc, B, N, N - 1)
+        ei = build_graph_with_knn(loc, B, N, N - 1 if num_neighbors is None else num_neighbors)
         x, ea, na, amf = o3_transform(loc, vel, mass, ei, lmax_attr)
         out, stats = model.forward(params, x, ei, ea, na, amf, training=training)
         params.update(stats)
@@ -26,10 +27,10 @@ def segnn_step(model, params, training=True, lmax_attr=1):
     return f
 
 
-def ponita_step(params, ori_grid, num_layers):
+def ponita_step(params, ori_grid, num_layers, num_neighbors=None):
     """PONITA branch (lines 131-147): x = mass, vec = vel[:, None], rel_pos."""
     def f(loc, vel, force, mass, B, N):
-        ei = build_graph_with_knn(loc, B, N, N - 1)
+        ei = build_graph_with_knn(loc, B, N, N - 1 if num_neighbors is None else num_neighbors)
         rel = loc[ei[0]] - loc[ei[1]]
         return ponita_oracle.forward(params, mass, vel[:, None, :], ei, rel, ori_grid, num_layers)
     return f

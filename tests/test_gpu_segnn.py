@@ -14,7 +14,7 @@ import torch
 
 import nbody_amd.graph as G
 import nbody_amd.segnn as S
-from oracle.graph import fc_edge_index
+from oracle.graph import fc_edge_index, knn_edge_index
 from oracle.rollout import rollout as oracle_rollout
 from oracle.rollout import segnn_step
 from oracle.segnn import SEGNNOracle, o3_transform
@@ -170,15 +170,126 @@ def test_rollout_equals_repeated_forward(hip_device, hidden, B, N):
         torch.testing.assert_close(tv[:, t].reshape(-1, 3), v, rtol=1e-5, atol=1e-6)
 
 
-def test_non_fc_graph_rejected(hip_device):
-    model = make_model(16, 1, hip_device)
+def graph_forward(model, pos, vel, mass, ei, B, N, device, with_batch=True):
     g = Graph()
-    g.pos = torch.zeros(10, 3, device=hip_device)
-    g.vel = torch.ones(10, 3, device=hip_device)
-    g.mass = torch.ones(10, 1, device=hip_device)
-    g.edge_index = G.fc_edge_index(2, 5, hip_device).flip(0)
-    with pytest.raises(NotImplementedError):
-        model(g)
+    g.pos = torch.tensor(pos, dtype=torch.float32, device=device)
+    g.vel = torch.tensor(vel, dtype=torch.float32, device=device)
+    g.mass = torch.tensor(mass, dtype=torch.float32, device=device)
+    g.edge_index = torch.as_tensor(np.asarray(ei), dtype=torch.int64, device=device)
+    if with_batch:
+        g.batch = torch.arange(B, device=device).repeat_interleave(N)
+    with torch.no_grad():
+        return model(g).double().cpu().numpy()
+
+
+def test_fc_graph_in_any_edge_order(hip_device):
+    """A fully-connected edge_index in another order (reversed, shuffled) is a general graph with
+    the same edge set: the graph path must give the fully-connected result."""
+    model = make_model(32, 2, hip_device).eval()
+    B, N = 6, 5
+    pos, vel, mass = states(B, N, seed=11)
+    ref = gpu_forward(model, pos, vel, mass, B, N, hip_device)
+    ei = fc_edge_index(B, N)
+    for e2 in (ei[:, ::-1].copy(), ei[:, np.random.default_rng(1).permutation(ei.shape[1])]):
+        np.testing.assert_allclose(graph_forward(model, pos, vel, mass, e2, B, N, hip_device), ref,
+                                   rtol=1e-5, atol=1e-6)
+
+
+def test_invalid_graph_rejected(hip_device):
+    """Self-loops, edges between systems and duplicate edges are outside the native graph model."""
+    import nbody_amd._lib as L
+    model = make_model(16, 1, hip_device)
+    B, N = 2, 5
+    pos, vel, mass = states(B, N)
+    ei = knn_edge_index(pos, B, N, 2)
+    bad = [np.concatenate([ei, [[3], [3]]], 1),          # self-loop
+           np.concatenate([ei, [[0], [7]]], 1),          # across systems
+           np.concatenate([ei, ei[:, :1]], 1)]           # duplicate
+    for e in bad:
+        with pytest.raises(L.NbxError):
+            graph_forward(model, pos, vel, mass, e, B, N, hip_device)
+    with pytest.raises(NotImplementedError):              # kNN edge count, no batch vector
+        graph_forward(model, pos, vel, mass, ei, B, N, hip_device, with_batch=False)
+
+
+@pytest.mark.parametrize("hidden,layers,B,N,k,training", [
+    (32, 2, 8, 5, 1, True), (32, 2, 8, 5, 2, True), (64, 3, 8, 5, 3, False), (192, 6, 16, 5, 2, True),
+    (24, 2, 4, 7, 3, True), (192, 2, 4, 20, 6, True)])
+def test_knn_graph_forward_matches_oracle(hip_device, hidden, layers, B, N, k, training):
+    """build_graph_with_knn's kNN branch (num_neighbors < N-1): messages source -> target, nodes
+    without incoming edges (k = 1 leaves some), node attributes averaged over incoming edges, the
+    message BatchNorm over the real edges."""
+    model = make_model(hidden, layers, hip_device)
+    model.train(training)
+    params = params_of(model)
+    pos, vel, mass = states(B, N, seed=12)
+    ei = knn_edge_index(pos, B, N, k)
+    om = SEGNNOracle(hidden_features=hidden, num_layers=layers)
+    x, ea, na, amf = o3_transform(pos, vel, mass, ei)
+    ref, stats = om.forward(params, x, ei, ea, na, amf, training=training)
+    got = graph_forward(model, pos, vel, mass, ei, B, N, hip_device)
+    assert_close_cols(got, ref)
+    if training:
+        sd = model.state_dict()
+        for key, v in stats.items():
+            np.testing.assert_allclose(sd[key].double().cpu().numpy(), v, rtol=1e-4, atol=1e-6)
+
+
+def test_knn_graph_forward_c2_width(hip_device):
+    """C2 widths (hidden 192, 6 layers) over B = 512 systems of a 3-NN graph vs the oracle."""
+    model = make_model(192, 6, hip_device, perturb_bn=False).train()
+    B, N = 512, 5
+    pos, vel, mass = states(B, N, seed=13)
+    ei = knn_edge_index(pos, B, N, 3)
+    om = SEGNNOracle(hidden_features=192, num_layers=6)
+    x, ea, na, amf = o3_transform(pos, vel, mass, ei)
+    ref, _ = om.forward(params_of(model), x, ei, ea, na, amf, training=True)
+    assert_close_cols(graph_forward(model, pos, vel, mass, ei, B, N, hip_device), ref)
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_knn_rollout_matches_oracle(hip_device, k):
+    """rollout(num_neighbors=k): each frame's kNN graph rebuilt on the device
+    (infer_self_feed.py:121-123) vs the oracle loop over build_graph_with_knn."""
+    model = make_model(32, 2, hip_device).train()
+    params = params_of(model)
+    B, N, T = 4, 5, 6
+    pos, vel, mass = states(B, N, seed=14)
+    loc0, vel0, m0 = pos.reshape(B, N, 3), vel.reshape(B, N, 3), mass.reshape(B, N, 1)
+    om = SEGNNOracle(hidden_features=32, num_layers=2)
+    rl, rv = oracle_rollout(segnn_step(om, params, num_neighbors=k), loc0, vel0, np.zeros_like(loc0), m0, T)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = model.rollout(t(loc0), t(vel0), t(m0), T, num_neighbors=k)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    for s in range(1, T):
+        assert_close(tp[:, s], rl[:, s], rel=2e-4 * s)
+        assert_close(tv[:, s], rv[:, s], rel=2e-4 * s)
+    assert ((tp - rl) ** 2).mean() <= 1e-5
+
+
+def test_knn_rollout_equals_repeated_forward(hip_device):
+    """rollout(num_neighbors=2) is the self-feed loop over forward() on build_graph_with_knn graphs."""
+    model = make_model(64, 2, hip_device).train()
+    B, N, T, k = 64, 5, 4, 2
+    pos, vel, mass = states(B, N, seed=15)
+    sd0 = {key: v.clone() for key, v in model.state_dict().items()}
+    loc = torch.tensor(pos.reshape(B, N, 3), dtype=torch.float32, device=hip_device)
+    ve = torch.tensor(vel.reshape(B, N, 3), dtype=torch.float32, device=hip_device)
+    ma = torch.tensor(mass.reshape(B, N, 1), dtype=torch.float32, device=hip_device)
+    tp, tv = model.rollout(loc, ve, ma, T, num_neighbors=k)
+    model.load_state_dict(sd0)
+    l, v = loc.reshape(-1, 3).clone(), ve.reshape(-1, 3).clone()
+    for s in range(1, T):
+        g = Graph()
+        g.pos, g.vel, g.mass = l, v, ma.reshape(-1, 1)
+        g.edge_index = G.build_graph_with_knn(l, B, N, hip_device, k)
+        g.batch = torch.arange(B, device=hip_device).repeat_interleave(N)
+        with torch.no_grad():
+            out = model(g)
+        l = l + out[:, :3]
+        v = out[:, 3:].contiguous()
+        torch.testing.assert_close(tp[:, s].reshape(-1, 3), l, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(tv[:, s].reshape(-1, 3), v, rtol=1e-5, atol=1e-6)
 
 
 def test_forward_deterministic_c2(hip_device):
