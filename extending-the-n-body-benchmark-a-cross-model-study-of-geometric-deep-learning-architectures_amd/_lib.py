@@ -138,6 +138,10 @@ _SIGNATURES = {
                                                   ctypes.POINTER(c_sz)]),
     "nbx_ponita_forward": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,
                                           c_p, c_sz, c_p]),
+    "nbx_ponita_forward_graph": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
+                                                c_i64, c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_ponita_rollout_knn": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
+                                              c_i32, c_i64, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_ponita_forward_timed": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                                 c_p, c_sz, c_p, c_f * 8, c_i32 * 8, c_d * 8, c_d * 8,
                                                 ctypes.POINTER(c_f)]),

@@ -52,6 +52,7 @@ struct LinProb {
     // message from src(d, q) = system base + (q < d ? q : q + 1);
     // Y[(d*O + o), n] = sum_q acc[(d, o, q), n] * X[(src(d, q)*O + o), n]
     int conv_G, conv_O, conv_nodes;  // slots per (d,o) (power of two <= 32), orientations, N
+    const int* conv_slot;            // general graphs: [V][G] source (local index) per slot, -1 padding; null = FC
     const float* conv_x;             // [V*O][ldx]
     int conv_ldx;
     int blocks_per_chunk;
@@ -339,9 +340,9 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
                 const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 const int q = row & (G - 1), dq = row / G, d = dq / O, o = dq - d * O;
                 const int dl = d % NN;
-                xoff[e] = (row < P.rows && q < NN - 1)
-                              ? ((d - dl + (q < dl ? q : q + 1)) * O + o) * P.conv_ldx
-                              : -1;
+                const int sq = row >= P.rows ? -1
+                               : P.conv_slot ? P.conv_slot[d * G + q] : (q < NN - 1 ? (q < dl ? q : q + 1) : -1);
+                xoff[e] = sq >= 0 ? ((d - dl + sq) * O + o) * P.conv_ldx : -1;
             }
 #pragma unroll
             for (int j = 0; j < NT; ++j) {

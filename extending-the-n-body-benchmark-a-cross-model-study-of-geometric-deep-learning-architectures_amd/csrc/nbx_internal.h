@@ -73,4 +73,10 @@ constexpr float kSH_C1 = 0.4886025119029199f;    // sqrt(3/(4 pi))
 constexpr float kC_SILU = 1.6791767923989418f;   // normalize2mom(SiLU)
 constexpr float kC_SIGMOID = 1.8467055342154763f; // normalize2mom(sigmoid)
 
+// csrc/graph.hip: general graphs as per-destination slot tables (SEGNN, PONITA)
+int graph_slots_from_edges(const int64_t* ei, int64_t E, int64_t V, int N, int G, unsigned long long* adj, int* slot,
+                           float* deg, int* err, hipStream_t st);
+int graph_slots_from_knn(const float* pos, int64_t V, int N, int G, int k, unsigned long long* adj, int* slot,
+                         float* deg, int* err, hipStream_t st);
+
 }  // namespace nbx

@@ -9,7 +9,8 @@
 // destination-major with G = next_pow2(N-1) slots per node and the orientation in between:
 // row (d, o, q) -> (d*O + o)*G + q, so the G messages a (d, o) fibre point receives are
 // consecutive rows of one MFMA tile and the aggregation is an in-register sum (lin.h
-// LIN_CONV).  Per forward:
+// LIN_CONV).  General graphs (kNN, any simple within-system edge_index): SLOT [V][G] names the
+// source of each slot (csrc/graph.hip), -1 padding.  Per forward:
 //   attr    : P16[(d,o,q)] = poly3(rel . ori_o, |rel - (rel . ori_o) ori_o|)       (14 of 16)
 //   basis   : KB = GELU(GELU(P16 Wb1' + b) Wb2' + b)        cached for all layers (E*O x Bk)
 //   fibre   : FK_l = GELU(GELU(poly3(ori_o . ori_p) Wf1' + b) Wf2' + b) Wfk_l'  (O*O x L*C)
@@ -38,7 +39,7 @@ unsigned g1(int64_t n) { return (unsigned)nbx::ceil_div(n > 0 ? n : 1, 256); }
 
 // invariant_attr_r3s2_fiber_bundle (separable) + PolynomialFeatures(3) per edge slot.
 __global__ void po_attr_kernel(const float* __restrict__ pos, const float* __restrict__ ori, int64_t R, int N, int O,
-                               int G, float* __restrict__ P16) {
+                               int G, float* __restrict__ P16, const int* __restrict__ slot) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= R) return;
     const int q = (int)(r % G);
@@ -48,9 +49,10 @@ __global__ void po_attr_kernel(const float* __restrict__ pos, const float* __res
     float f[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) f[i] = 0.f;
-    if (q < N - 1) {
-        const int dl = (int)(d % N);
-        const int64_t s = d - dl + (q < dl ? q : q + 1);
+    const int dl = (int)(d % N);
+    const int sq = slot ? slot[d * G + q] : (q < N - 1 ? (q < dl ? q : q + 1) : -1);
+    if (sq >= 0) {
+        const int64_t s = d - dl + sq;
         const float rx = pos[3 * s] - pos[3 * d], ry = pos[3 * s + 1] - pos[3 * d + 1],
                     rz = pos[3 * s + 2] - pos[3 * d + 2];
         const float ox = ori[3 * o], oy = ori[3 * o + 1], oz = ori[3 * o + 2];
@@ -259,6 +261,10 @@ struct PoDims {
 
 struct PoWs {
     float *P16, *B1H1, *KB, *FP, *FB1, *FKB, *FK, *X, *X1, *XN, *RO, *out;
+    int* SLOT;                 // general graphs: [V*G] source per slot
+    float* DEG;                // [V] in-degree (unused by the model: FiberBundleConv sums)
+    unsigned long long* ADJ;   // [V]
+    int* ERR;                  // [64]
 };
 
 int next_pow2(int x) {
@@ -298,6 +304,10 @@ size_t po_carve(PoWs* ws, void* base, const PoDims& d) {
     w.XN = take(VO * d.C);
     w.RO = take(VO * 2);
     w.out = take((size_t)d.V * 6);
+    w.SLOT = (int*)take((size_t)d.V * d.G);
+    w.DEG = take((size_t)d.V);
+    w.ADJ = (unsigned long long*)take((size_t)d.V * 2);
+    w.ERR = (int*)take(64);
     if (ws) *ws = w;
     return (off + 255) & ~size_t(255);
 }
@@ -679,7 +689,7 @@ enum PoKind : int { PK_CONV = 0, PK_LIN1 = 1, PK_LIN2 = 2, PK_BASIS = 3, PK_FIBE
 
 int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* vel, const float* mass,
                     const PoDims& d, float* out, double* mom, const PoWs& ws, hipStream_t st,
-                    nbx::LaunchTimer* tm = nullptr) {
+                    nbx::LaunchTimer* tm = nullptr, const int* slot = nullptr) {
     using nbx::LinProb;
     const int O = d.O, C = d.C, Bk = d.Bk, L = d.L;
     const int64_t VO = d.V * O;
@@ -688,7 +698,7 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
     const double f4 = 4.0;
     // ---- invariants, kernel bases (shared by all layers), lift
     hipLaunchKernelGGL(po_attr_kernel, dim3(g1(d.R)), dim3(256), 0, st, pos, w->ori_grid, d.R, (int)d.N, O, (int)d.G,
-                       ws.P16);
+                       ws.P16, slot);
     hipLaunchKernelGGL(po_fattr_kernel, dim3(g1(OO)), dim3(256), 0, st, w->ori_grid, O, ws.FP);
     hipLaunchKernelGGL(po_lift_kernel, dim3(g1(VO * C)), dim3(256), 0, st, mass, vel, w->ori_grid, w->embed_w, d.V, O,
                        C, ws.X);
@@ -722,6 +732,7 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             p.conv_G = (int)d.G;
             p.conv_O = O;
             p.conv_nodes = (int)d.N;
+            p.conv_slot = slot;
             p.conv_x = ws.X;
             p.conv_ldx = C;
             if (int rc = nbx::timed(tm, st, PK_CONV, 2.0 * Ev * Bk * C + 2.0 * Ev * C,
@@ -887,6 +898,52 @@ extern "C" int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float
                        (int64_t)0, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     for (int64_t f = 1; f < num_frames; ++f) {
         if (int rc = po_forward_impl(w, pos, vel, mass, d, ws.out, nullptr, ws, st)) return rc;
+        hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
+                           f, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
+    }
+    NBX_LAUNCH_CHECK("ponita rollout");
+    return NBX_OK;
+}
+
+extern "C" int nbx_ponita_forward_graph(const nbx_ponita_weights* w, const float* pos, const float* vel,
+                                        const float* mass, int64_t B, int64_t N, const int64_t* edge_index,
+                                        int64_t num_edges, float* out, double* calib_moments, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+    PoDims d;
+    PoWs ws;
+    if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
+    NBX_CHECK_ARG(num_edges >= 0 && (num_edges == 0 || edge_index), "nbx_ponita_forward_graph: bad edge_index");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = nbx::graph_slots_from_edges(edge_index, num_edges, d.V, (int)N, (int)d.G, ws.ADJ, ws.SLOT, ws.DEG,
+                                             ws.ERR, st))
+        return rc;
+    return po_forward_impl(w, pos, vel, mass, d, out, calib_moments, ws, st, nullptr, ws.SLOT);
+}
+
+extern "C" int nbx_ponita_rollout_knn(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass,
+                                      int64_t B, int64_t N, int64_t num_frames, int32_t flags, int64_t num_neighbors,
+                                      float* traj_pos, float* traj_vel, void* workspace, size_t workspace_bytes,
+                                      void* stream) {
+    if (num_neighbors < 0) num_neighbors = N - 1;   // the reference's None
+    NBX_CHECK_ARG(num_neighbors < N, "Graph cannot have more neighbors than there are nodes in simulation - 1");
+    if (num_neighbors == N - 1)   // build_graph_with_knn returns the fully-connected pattern
+        return nbx_ponita_rollout(w, pos, vel, mass, B, N, num_frames, flags, traj_pos, traj_vel, workspace,
+                                  workspace_bytes, stream);
+    NBX_CHECK_ARG(num_neighbors >= 1, "nbx_ponita_rollout_knn: num_neighbors must be >= 1");
+    PoDims d;
+    PoWs ws;
+    if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
+    NBX_CHECK_ARG(num_frames >= 1, "nbx_ponita_rollout_knn: num_frames >= 1");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t V = d.V;
+    hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
+                       (int64_t)0, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
+    for (int64_t f = 1; f < num_frames; ++f) {
+        // each frame's kNN graph from its positions (infer_self_feed.py:137-142)
+        if (int rc = nbx::graph_slots_from_knn(pos, V, (int)N, (int)d.G, (int)num_neighbors, ws.ADJ, ws.SLOT, ws.DEG,
+                                               ws.ERR, st))
+            return rc;
+        if (int rc = po_forward_impl(w, pos, vel, mass, d, ws.out, nullptr, ws, st, nullptr, ws.SLOT)) return rc;
         hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
                            f, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     }

@@ -55,3 +55,36 @@ def build_graph_with_knn(loc, batch_size, num_nodes, device, num_neighbors):
                                              batch_size, num_nodes, k, _lib.dev_ptr(ei), _lib.stream_ptr(loc.device)),
                "nbx_knn_edge_index")
     return ei.to(device)
+
+
+def system_layout(graph, num_nodes: int, num_edges: int, device):
+    """(B, N, fully_connected) of a batched graph of equal-size systems, for the native models.
+    N comes from ``graph.nbx_system_size`` (this package's dataloaders), else from ``graph.batch``
+    (the reference's graphs: arange(B).repeat_interleave(N)), else from a fully-connected edge
+    count (E = V (N-1)).  ``fully_connected``: the edge set is every ordered pair of a system."""
+    V, E = int(num_nodes), int(num_edges)
+    if V == 0:
+        raise ValueError("empty graph")
+    N = getattr(graph, "nbx_system_size", None)
+    batch = getattr(graph, "batch", None)
+    if N is not None:
+        N = int(N)
+    elif batch is not None and batch.numel() == V:
+        b = batch.to(device)
+        B = int(b.max().item()) + 1
+        if V % B or not torch.equal(b, torch.arange(B, device=device).repeat_interleave(V // B)):
+            raise NotImplementedError("native models need contiguous systems of equal size")
+        N = V // B
+    else:
+        n = E // V + 1
+        if E != V * (n - 1) or V % n:
+            raise NotImplementedError("native models need systems of equal size: pass graph.batch for "
+                                      "graphs that are not fully connected")
+        N = n
+    if V % N:
+        raise NotImplementedError("native models need systems of equal size")
+    B = V // N
+    fc = E == V * (N - 1)
+    if fc and getattr(graph, "nbx_system_size", None) is None:
+        fc = torch.equal(graph.edge_index.to(device), _fc_edge_index_shared(B, N, device))
+    return B, N, fc

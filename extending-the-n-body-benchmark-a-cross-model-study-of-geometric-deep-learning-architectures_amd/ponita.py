@@ -332,19 +332,18 @@ class PONITA_NBODY(nn.Module):
 
     # ------------------------------------------------------------ forward
     def forward(self, graph):
+        """graph: pos, vec / vel, x / mass, edge_index (build_graph_with_knn: fully connected, its kNN
+        graphs or any simple graph inside equal-size systems; ``batch`` for the latter)."""
         pos = graph.pos
         device = pos.device
         V = pos.shape[0]
-        N = getattr(graph, "nbx_system_size", None)
-        if N is None:
-            from .segnn import SEGNN
-            B, N = SEGNN.infer_system_size(V, graph.edge_index.shape[1])
-            from .graph import _fc_edge_index_shared as fc_edge_index
-            if not torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device)):
-                raise NotImplementedError("native PONITA needs the fully-connected edge_index")
+        ei = getattr(graph, "edge_index", None)
+        if ei is None:   # this package's own calls: fully connected systems of nbx_system_size nodes
+            N = int(graph.nbx_system_size)
+            B, fc = V // N, True
         else:
-            N = int(N)
-            B = V // N
+            from .graph import system_layout
+            B, N, fc = system_layout(graph, V, ei.shape[1], device)
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
         x = getattr(graph, "x", None)
         if x is None:
@@ -357,31 +356,58 @@ class PONITA_NBODY(nn.Module):
         ws = self._workspace(W, B, N, device)
         calib = self._needs_callibration()
         mom = torch.zeros(6 * W.num_layers, dtype=torch.float64, device=device) if calib else None
-        _lib.check(_lib.lib().nbx_ponita_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                                 _lib.dev_ptr(out), _lib.dev_ptr(mom) if calib else None,
-                                                 _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
-                   "nbx_ponita_forward")
+        if fc:
+            _lib.check(_lib.lib().nbx_ponita_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                     _lib.dev_ptr(out), _lib.dev_ptr(mom) if calib else None,
+                                                     _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                       "nbx_ponita_forward")
+        else:
+            e = ei.to(device=device, dtype=torch.int64).contiguous()
+            _lib.check(_lib.lib().nbx_ponita_forward_graph(
+                W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(e), e.shape[1],
+                _lib.dev_ptr(out), _lib.dev_ptr(mom) if calib else None, _lib.dev_ptr(ws), ws.numel(),
+                _lib.stream_ptr(device)), "nbx_ponita_forward_graph")
         if calib:
             self._callibrate(mom, V * self.num_ori * self.hidden_dim)
         return out.to(pos.dtype)
 
     @torch.no_grad()
-    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False):
+    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False, num_neighbors=None):
         """Self-feed loop (infer_self_feed.py:131-147,182-194) device-resident:
         loc/vel [B,N,3], mass [B,N,1] -> trajectories [B, T, N, 3] each, frame 0 =
         the initial state.  A model still owing its one-time calibration runs one
         calibrating forward on the initial state first, as the reference's first
         step would.  ``absolute``: pos = pred[:, :3] (targets other than "pos_dt+vel",
-        infer_self_feed.py:185-186) instead of pos += pred[:, :3]."""
+        infer_self_feed.py:185-186) instead of pos += pred[:, :3].  ``num_neighbors``: each frame's
+        graph is build_graph_with_knn's kNN graph of its positions (None / N-1: fully connected)."""
         flags = _lib.ROLLOUT_ABSOLUTE if absolute else 0
         device = loc.device
         B, N, _ = loc.shape
+        knn = num_neighbors is not None and int(num_neighbors) != N - 1
+        if knn and int(num_neighbors) >= N:
+            raise ValueError("Graph cannot have more neighbors than there are nodes in simulation - 1")
+
+        def run(p_, v_, T, tp_, tv_):
+            if knn:
+                _lib.check(_lib.lib().nbx_ponita_rollout_knn(
+                    W, _lib.dev_ptr(p_), _lib.dev_ptr(v_), _lib.dev_ptr(m), B, N, T, flags, int(num_neighbors),
+                    _lib.dev_ptr(tp_), _lib.dev_ptr(tv_), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                    "nbx_ponita_rollout_knn")
+            else:
+                _lib.check(_lib.lib().nbx_ponita_rollout(
+                    W, _lib.dev_ptr(p_), _lib.dev_ptr(v_), _lib.dev_ptr(m), B, N, T, flags, _lib.dev_ptr(tp_),
+                    _lib.dev_ptr(tv_), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)), "nbx_ponita_rollout")
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
         p, v, m = f(loc), f(vel), f(mass.reshape(B * N))
         if self._needs_callibration():
             g = type("G", (), {})()
-            g.pos, g.vec, g.x, g.nbx_system_size = p.reshape(-1, 3), v.reshape(-1, 1, 3), m.reshape(-1, 1), N
-            g.edge_index = None
+            g.pos, g.vec, g.x = p.reshape(-1, 3), v.reshape(-1, 1, 3), m.reshape(-1, 1)
+            if knn:
+                from .graph import build_graph_with_knn
+                g.edge_index = build_graph_with_knn(g.pos, B, N, device, int(num_neighbors))
+                g.batch = torch.arange(B, device=device).repeat_interleave(N)
+            else:
+                g.nbx_system_size, g.edge_index = N, None
             first = self.forward(g)
         else:
             first = None
@@ -390,10 +416,7 @@ class PONITA_NBODY(nn.Module):
         W = self._weights(device)
         ws = self._workspace(W, B, N, device)
         if first is None:
-            _lib.check(_lib.lib().nbx_ponita_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                                     num_frames, flags, _lib.dev_ptr(tp), _lib.dev_ptr(tv),
-                                                     _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
-                       "nbx_ponita_rollout")
+            run(p, v, num_frames, tp, tv)
             return tp, tv
         # frame 1 came from the calibrating forward; the rest from the calibrated weights
         tp[:, 0], tv[:, 0] = p, v
@@ -403,9 +426,6 @@ class PONITA_NBODY(nn.Module):
         v = first[:, 3:].reshape(B, N, 3).contiguous()
         rp = torch.empty(B, num_frames - 1, N, 3, device=device, dtype=torch.float32)
         rv = torch.empty_like(rp)
-        _lib.check(_lib.lib().nbx_ponita_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                                 num_frames - 1, flags, _lib.dev_ptr(rp), _lib.dev_ptr(rv),
-                                                 _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
-                   "nbx_ponita_rollout")
+        run(p, v, num_frames - 1, rp, rv)
         tp[:, 1:], tv[:, 1:] = rp, rv
         return tp, tv

@@ -435,31 +435,6 @@ class SEGNN(nn.Module):
             raise NotImplementedError("native SEGNN needs fully-connected systems of equal size")
         return num_nodes // n, n
 
-    def _graph_layout(self, graph, V, E, device):
-        """(B, N, fully_connected) of a batched graph of equal-size systems.  N comes from
-        ``graph.nbx_system_size`` (this package's dataloaders), else from ``graph.batch`` (the
-        reference's graphs: arange(B).repeat_interleave(N)), else from a fully-connected edge count."""
-        N = getattr(graph, "nbx_system_size", None)
-        batch = getattr(graph, "batch", None)
-        if N is not None:
-            N = int(N)
-        elif batch is not None and batch.numel() == V:
-            b = batch.to(device)
-            B = int(b.max().item()) + 1
-            if V % B or not torch.equal(b, torch.arange(B, device=device).repeat_interleave(V // B)):
-                raise NotImplementedError("native SEGNN needs contiguous systems of equal size")
-            N = V // B
-        else:
-            B, N = self.infer_system_size(V, E)
-        if V % N:
-            raise NotImplementedError("native SEGNN needs systems of equal size")
-        B = V // N
-        fc = E == V * (N - 1)
-        if fc and getattr(graph, "nbx_system_size", None) is None:
-            from .graph import _fc_edge_index_shared as fc_edge_index
-            fc = torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device))
-        return B, N, fc
-
     def forward(self, graph):
         """graph: pos [V,3], vel [V,3], mass [V,1], edge_index (build_graph_with_knn: the
         fully-connected pattern, its kNN graphs, or any simple graph inside equal-size systems),
@@ -468,7 +443,8 @@ class SEGNN(nn.Module):
         device = pos.device
         V = pos.shape[0]
         edge_index = graph.edge_index
-        B, N, fc = self._graph_layout(graph, V, edge_index.shape[1], device)
+        from .graph import system_layout
+        B, N, fc = system_layout(graph, V, edge_index.shape[1], device)
         out_dtype = pos.dtype
         if out_dtype != torch.float32 and not self._warned_dtype:
             warnings.warn("SEGNN HIP path computes in fp32; inputs are cast", stacklevel=2)

@@ -408,6 +408,22 @@ int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float* vel, cons
                        int64_t num_nodes, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                        size_t workspace_bytes, void* stream);
 
+/* General graphs (ABI 8), as nbx_segnn_forward_graph: nbx_ponita_forward on `edge_index` (int64
+ * [2][num_edges], row = source, col = target, e.g. build_graph_with_knn's kNN branch,
+ * infer_self_feed.py:137-142): FiberBundleConv sums the messages of a node's incoming edges, a node
+ * without any receives zero.  Edges must join different nodes of one system, without duplicates
+ * (NBX_E_INVAL otherwise); synchronises `stream` once. */
+int nbx_ponita_forward_graph(const nbx_ponita_weights* w, const float* pos, const float* vel, const float* mass,
+                             int64_t batch_size, int64_t num_nodes, const int64_t* edge_index, int64_t num_edges,
+                             float* out, double* calib_moments, void* workspace, size_t workspace_bytes, void* stream);
+
+/* nbx_ponita_rollout with the reference's num_neighbors: each frame's kNN graph built on the device
+ * (contract of nbx_segnn_rollout_knn). */
+int nbx_ponita_rollout_knn(const nbx_ponita_weights* w, float* pos, float* vel, const float* mass,
+                           int64_t batch_size, int64_t num_nodes, int64_t num_frames, int32_t flags,
+                           int64_t num_neighbors, float* traj_pos, float* traj_vel, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * EquiformerV2 (models/equiformer_v2/architecture/equiformer_v2_nbody.py:57-575 on the tuple
  * branch of helper_scripts/infer_self_feed.py:178-181, eval mode) — fp32.

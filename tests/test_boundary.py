@@ -233,6 +233,33 @@ def test_run_inference_layout(tmp_path, fake_sim):
         I.run_inference("painn", None, model=_ConstModel(), dataset=ds, device="cpu")
 
 
+class _KnnModel(_ConstModel):
+    """Stand-in whose rollout takes the reference's num_neighbors (the native SEGNN / PONITA do)."""
+
+    def rollout(self, loc, vel, mass, T, num_neighbors=None):
+        self.k = num_neighbors
+        return super().rollout(loc, vel, mass, T)
+
+
+def test_run_inference_routes_num_neighbors(tmp_path, fake_sim):
+    """infer_self_feed.py:58,121-123,137-139: segnn / ponita build each frame's graph with
+    build_graph_with_knn(num_neighbors): k < N-1 reaches the model's kNN rollout, k >= N raises
+    the reference's ValueError, a model without kNN support refuses loudly; egnn_mc's branch
+    ignores num_neighbors."""
+    ds = D.GravityDatasetOtf(batch_size=2, sim_length=60, num_nodes=3, device="cpu", data_path=str(tmp_path / "s"),
+                             double_precision=True)
+    kw = dict(device="cpu", max_rollout_steps=3, dataset=ds)
+    for mt in ("segnn", "ponita"):
+        m = _KnnModel()
+        I.run_inference(mt, None, model=m, save_dir=str(tmp_path / mt), num_neighbors=1, **kw)
+        assert m.k == 1
+        with pytest.raises(ValueError):
+            I.run_inference(mt, None, model=_KnnModel(), save_dir=str(tmp_path / mt), num_neighbors=3, **kw)
+        with pytest.raises(NotImplementedError):
+            I.run_inference(mt, None, model=_ConstModel(), save_dir=str(tmp_path / mt), num_neighbors=1, **kw)
+    I.run_inference("egnn_mc", None, model=_ConstModel(), save_dir=str(tmp_path / "e"), num_neighbors=1, **kw)
+
+
 def test_energy_oracle_small_case():
     loc = np.array([[[[0, 0, 0], [3, 4, 0]]]], dtype=float)
     vel = np.array([[[[1, 0, 0], [0, 2, 0]]]], dtype=float)

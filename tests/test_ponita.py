@@ -257,6 +257,93 @@ def test_gpu_rollout_equals_repeated_forward(hip_device):
         assert torch.equal(tv[:, k].reshape(-1, 3), v)
 
 
+def knn_graph(pos, vel, mass, ei, B, N, device):
+    gr = Graph()
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
+    gr.pos, gr.vec, gr.x = t(pos).reshape(-1, 3), t(vel).reshape(-1, 1, 3), t(mass).reshape(-1, 1)
+    gr.edge_index = torch.as_tensor(np.asarray(ei), dtype=torch.int64, device=device)
+    gr.batch = torch.arange(B, device=device).repeat_interleave(N)
+    gr.rel_pos = gr.pos[gr.edge_index[0]] - gr.pos[gr.edge_index[1]]
+    return gr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N,k,hidden,layers,num_ori", [(8, 5, 1, 32, 2, 12), (8, 5, 2, 64, 2, 20),
+                                                         (16, 5, 3, 128, 3, 20), (2, 20, 6, 32, 2, 12)])
+def test_gpu_knn_graph_forward_matches_oracle(hip_device, B, N, k, hidden, layers, num_ori):
+    """build_graph_with_knn's kNN branch (infer_self_feed.py:137-142 with num_neighbors < N-1):
+    FiberBundleConv sums over each node's incoming edges (k = 1 leaves nodes with none)."""
+    from oracle.graph import knn_edge_index
+    m = make(hidden, layers, num_ori=num_ori).to(hip_device)
+    m.eval()
+    rng = np.random.default_rng(4)
+    pos, vel = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3))
+    mass = rng.uniform(0.5, 1.5, (B * N, 1))
+    ei = knn_edge_index(pos, B, N, k)
+    ref = op.forward(oracle_params(m), mass, vel[:, None, :], ei, pos[ei[0]] - pos[ei[1]],
+                     m.model.ori_grid.double().cpu().numpy(), layers)
+    with torch.no_grad():
+        out = m(knn_graph(pos, vel, mass, ei, B, N, hip_device)).double().cpu().numpy()
+    assert np.abs(out - ref).max() <= 2e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_fc_graph_in_any_edge_order(hip_device):
+    """The fully-connected edge set in another order takes the general-graph path: same result."""
+    m = make(32, 2).to(hip_device)
+    m.eval()
+    B, N = 6, 5
+    rng = np.random.default_rng(5)
+    pos, vel, mass = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3)), np.ones((B * N, 1))
+    with torch.no_grad():
+        ref = m(gpu_graph(pos, vel, mass, B, N, hip_device)).double().cpu().numpy()
+        ei = fc_edge_index(B, N)[:, np.random.default_rng(6).permutation(B * N * (N - 1))]
+        out = m(knn_graph(pos, vel, mass, ei, B, N, hip_device)).double().cpu().numpy()
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [2, 3])
+def test_gpu_knn_rollout_matches_oracle(hip_device, k):
+    """rollout(num_neighbors=k): each frame's kNN graph rebuilt on the device vs the oracle loop."""
+    B, N, T = 16, 5, 5
+    m = make(64, 3).to(hip_device)
+    m.eval()
+    rng = np.random.default_rng(7)
+    loc, vel = rng.standard_normal((B, N, 3)), rng.standard_normal((B, N, 3)) * 0.1
+    mass = np.ones((B, N, 1))
+    params = oracle_params(m)
+    grid = m.model.ori_grid.double().cpu().numpy()
+    rl, rv = oracle_rollout(ponita_step(params, grid, 3, num_neighbors=k), loc, vel, np.zeros_like(loc), mass, T)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
+    tp, tv = m.rollout(t(loc), t(vel), t(mass), T, num_neighbors=k)
+    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    assert ((tp - rl) ** 2).mean() + ((tv - rv) ** 2).mean() <= 1e-5
+    for s in range(T):
+        tol = 2e-4 * (s + 1)
+        assert np.abs(tp[:, s] - rl[:, s]).max() <= tol * np.abs(rl[:, s]).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_knn_rollout_calibrates_on_first_frame(hip_device):
+    """A model owing its calibration runs the calibrating forward on the first frame's kNN graph,
+    then the kNN rollout: equal to calibrating by hand on that graph and rolling out."""
+    B, N, T, k = 8, 5, 4, 2
+    rng = np.random.default_rng(8)
+    loc = torch.tensor(rng.standard_normal((B, N, 3)), dtype=torch.float32, device=hip_device)
+    vel = torch.tensor(rng.standard_normal((B, N, 3)) * 0.1, dtype=torch.float32, device=hip_device)
+    mass = torch.ones(B, N, 1, device=hip_device)
+    a, b = make(32, 2).to(hip_device), make(32, 2).to(hip_device)
+    tp, tv = a.rollout(loc, vel, mass, T, num_neighbors=k)
+    ei = G.build_graph_with_knn(loc.reshape(-1, 3), B, N, hip_device, k)
+    with torch.no_grad():
+        first = b(knn_graph(loc.reshape(-1, 3).cpu().numpy(), vel.reshape(-1, 3).cpu().numpy(),
+                            mass.reshape(-1, 1).cpu().numpy(), ei.cpu().numpy(), B, N, hip_device))
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        torch.testing.assert_close(va, vb, msg=ka)
+    torch.testing.assert_close(tp[:, 1].reshape(-1, 3), loc.reshape(-1, 3) + first[:, :3])
+
+
 @pytest.mark.gpu
 def test_gpu_c3_full_batch_slices_match_oracle(hip_device):
     """C3 at its full size (hidden 128, 6 layers, 20 orientations, basis 128, B = 4096:
