@@ -65,59 +65,77 @@ __device__ void et_gemm(const float* X, int rows, int ldx, int K, const float* _
     __syncthreads();
 }
 
-// dX[r][k] (+)= sum_n dZ[r][n] W[k][n]
+// dX[r][k] (+)= sum_n dZ[r][n] W[k][n] (n < Nc; Nc, ldz, ldw multiples of 4, rows 16-byte aligned).
+// Thread = one output column k (of RS row ranges when K < 512): W row k is read once, 32 columns at
+// a time into registers, and every dZ float4 is an LDS broadcast (all lanes of a wave read the same
+// row); 4 rows per pass give 4 independent FMA chains.
 __device__ void et_gemm_t(const float* dZ, int rows, int ldz, int Nc, const float* __restrict__ W, int ldw, int K,
                           float* dX, int ldx, bool accumulate) {
-    const int rg = (rows + RB - 1) / RB;
-    for (int o = threadIdx.x; o < rg * K; o += ET_THREADS) {
-        const int g = o / K, k = o - g * K, r0 = g * RB;
+    const int RS = K >= ET_THREADS ? 1 : ET_THREADS / K;
+    for (int t = threadIdx.x; t < K * RS; t += ET_THREADS) {
+        const int k = t % K, part = t / K;
+        const int ra = rows * part / RS, rb = rows * (part + 1) / RS;
         const float* w = W + (size_t)k * ldw;
-        float v[RB];
-        const float* z[RB];
+        for (int c0 = 0; c0 < Nc; c0 += 32) {
+            float4 wr[8];
 #pragma unroll
-        for (int j = 0; j < RB; ++j) {
-            v[j] = 0.f;
-            z[j] = dZ + (r0 + j < rows ? r0 + j : r0) * ldz;
-        }
-        // Nc, ldz and ldw are multiples of 4 and the rows 16-byte aligned: float4 along n
-#pragma unroll 4
-        for (int n = 0; n < Nc; n += 4) {
-            const float4 ww = *reinterpret_cast<const float4*>(w + n);
+            for (int i = 0; i < 8; ++i)
+                wr[i] = c0 + 4 * i < Nc ? *reinterpret_cast<const float4*>(w + c0 + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r0 = ra; r0 < rb; r0 += 4) {
+                float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < RB; ++j) {
-                const float4 zz = *reinterpret_cast<const float4*>(z[j] + n);
-                v[j] = fmaf(zz.x, ww.x, fmaf(zz.y, ww.y, fmaf(zz.z, ww.z, fmaf(zz.w, ww.w, v[j]))));
+                for (int i = 0; i < 8; ++i) {
+                    if (c0 + 4 * i >= Nc) break;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = r0 + j < rb ? r0 + j : rb - 1;
+                        const float4 z = *reinterpret_cast<const float4*>(dZ + r * ldz + c0 + 4 * i);
+                        v[j] = fmaf(z.x, wr[i].x, fmaf(z.y, wr[i].y, fmaf(z.z, wr[i].z, fmaf(z.w, wr[i].w, v[j]))));
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = r0 + j;
+                    if (r >= rb) break;
+                    float* o = dX + r * ldx + k;
+                    *o = (accumulate || c0 > 0) ? *o + v[j] : v[j];
+                }
             }
-        }
-#pragma unroll
-        for (int j = 0; j < RB; ++j) {
-            const int r = r0 + j;
-            if (r >= rows) break;
-            dX[r * ldx + k] = accumulate ? dX[r * ldx + k] + v[j] : v[j];
         }
     }
     __syncthreads();
 }
 
-// G[k][n] += sum_r X[r][k] dZ[r][n] (k < K), gb[n] += sum_r dZ[r][n]; G / gb global (this
-// workgroup's partial slice), X / dZ in LDS or global; a thread owns RB consecutive k of one n
+// G[k][n] += sum_r X[r][k] dZ[r][n] (k < K), gb[n] += sum_r dZ[r][n]; G / gb global (this workgroup's
+// partial slice), X / dZ in LDS or global (K, Nc, ldx, ldz, ldg multiples of 4, rows 16-byte aligned).
+// Thread = a 4 x 4 block of G: per row one float4 of X and one of dZ feed 16 FMAs.
 __device__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* dZ, int ldz, int Nc, float* G, int ldg,
                          float* gb) {
-    const int kg = (K + RB - 1) / RB;
-    for (int o = threadIdx.x; o < kg * Nc; o += ET_THREADS) {
-        const int g = o / Nc, n = o - g * Nc, k0 = g * RB;
-        float v[RB];
+    const int kq = K >> 2, nq = Nc >> 2;
+    for (int o = threadIdx.x; o < kq * nq; o += ET_THREADS) {
+        const int kb = o / nq, nb = o - kb * nq, k0 = 4 * kb, n0 = 4 * nb;
+        float4 a[4];
 #pragma unroll
-        for (int j = 0; j < RB; ++j) v[j] = 0.f;
+        for (int i = 0; i < 4; ++i) a[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int r = 0; r < rows; ++r) {
-            const float z = dZ[r * ldz + n];
-            const float* x = X + r * ldx + k0;
+            const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + k0);
+            const float4 z = *reinterpret_cast<const float4*>(dZ + r * ldz + n0);
+            const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-            for (int j = 0; j < RB; ++j) v[j] = fmaf(k0 + j < K ? x[j] : 0.f, z, v[j]);
+            for (int i = 0; i < 4; ++i) {
+                a[i].x = fmaf(xs[i], z.x, a[i].x);
+                a[i].y = fmaf(xs[i], z.y, a[i].y);
+                a[i].z = fmaf(xs[i], z.z, a[i].z);
+                a[i].w = fmaf(xs[i], z.w, a[i].w);
+            }
         }
 #pragma unroll
-        for (int j = 0; j < RB; ++j)
-            if (k0 + j < K) G[(size_t)(k0 + j) * ldg + n] += v[j];
+        for (int i = 0; i < 4; ++i) {
+            float4* g = reinterpret_cast<float4*>(G + (size_t)(k0 + i) * ldg + n0);
+            float4 c = *g;
+            c.x += a[i].x; c.y += a[i].y; c.z += a[i].z; c.w += a[i].w;
+            *g = c;
+        }
     }
     if (gb)
         for (int n = threadIdx.x; n < Nc; n += ET_THREADS) {
@@ -126,6 +144,88 @@ __device__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* 
             gb[n] += v;
         }
     __syncthreads();
+}
+
+// Register-resident forward product for Nc = HT output columns (HT = 32, 64, 128), K % 4 == 0,
+// K <= 2 HT + 8, W input-major [K][HT]: wave w owns columns [4 CGW w, 4 CGW (w + 1)), lane = (column
+// group cg, K-slice sl); the lane's weights (its 4 columns of rows 4 (sl + SL j) .. + 3) are loaded
+// once into registers and serve every row; per row the K-slices are summed with xor shuffles over the
+// slice bits of the lane id, and slice 0 writes the row's 4 outputs.
+template <int HT>
+__device__ void et_gemm_r(const float* X, int rows, int ldx, int K, const float* __restrict__ W,
+                          const float* __restrict__ b, float* Y, int ldy, int act, float* Zs) {
+    constexpr int CGW = HT / 32, SL = 64 / CGW;
+    constexpr int KB = ((2 * HT + 8) / 4 + SL - 1) / SL;   // float4 K-blocks per lane
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int cg = lane % CGW, sl = lane / CGW;
+    const int n0 = (wave * CGW + cg) * 4;
+    const int kq = K >> 2;
+    float4 w[KB][4];
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+        const int kb = sl + SL * j;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w[j][i] = kb < kq ? *reinterpret_cast<const float4*>(W + (size_t)(4 * kb + i) * HT + n0)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float4 bias = b ? *reinterpret_cast<const float4*>(b + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r0 = 0; r0 < rows; r0 += 4) {
+        float4 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+            const int kb = sl + SL * j;
+            if (kb >= kq) break;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int r = r0 + rr < rows ? r0 + rr : rows - 1;
+                const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + 4 * kb);
+                acc[rr].x = fmaf(x.x, w[j][0].x, fmaf(x.y, w[j][1].x, fmaf(x.z, w[j][2].x, fmaf(x.w, w[j][3].x, acc[rr].x))));
+                acc[rr].y = fmaf(x.x, w[j][0].y, fmaf(x.y, w[j][1].y, fmaf(x.z, w[j][2].y, fmaf(x.w, w[j][3].y, acc[rr].y))));
+                acc[rr].z = fmaf(x.x, w[j][0].z, fmaf(x.y, w[j][1].z, fmaf(x.z, w[j][2].z, fmaf(x.w, w[j][3].z, acc[rr].z))));
+                acc[rr].w = fmaf(x.x, w[j][0].w, fmaf(x.y, w[j][1].w, fmaf(x.z, w[j][2].w, fmaf(x.w, w[j][3].w, acc[rr].w))));
+            }
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int o = CGW; o < 64; o <<= 1) {
+                acc[rr].x += __shfl_xor(acc[rr].x, o);
+                acc[rr].y += __shfl_xor(acc[rr].y, o);
+                acc[rr].z += __shfl_xor(acc[rr].z, o);
+                acc[rr].w += __shfl_xor(acc[rr].w, o);
+            }
+        if (sl == 0)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int r = r0 + rr;
+                if (r >= rows) break;
+                const float4 z = make_float4(acc[rr].x + bias.x, acc[rr].y + bias.y, acc[rr].z + bias.z, acc[rr].w + bias.w);
+                if (Zs) *reinterpret_cast<float4*>(Zs + r * HT + n0) = z;
+                *reinterpret_cast<float4*>(Y + r * ldy + n0) =
+                    act == 1 ? make_float4(et_silu(z.x), et_silu(z.y), et_silu(z.z), et_silu(z.w)) : z;
+            }
+    }
+    __syncthreads();
+}
+
+// forward product: the register-resident form at H = 32 / 64 / 128 (HT), the generic one otherwise
+template <int HT>
+__device__ inline void et_fwd(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
+                              const float* __restrict__ b, int Nc, float* Y, int ldy, int act, float* Zs) {
+    if constexpr (HT > 0) et_gemm_r<HT>(X, rows, ldx, K, W, b, Y, ldy, act, Zs);
+    else et_gemm(X, rows, ldx, K, W, ldw, b, Nc, Y, ldy, act, Zs);
+}
+
+// out[r] = sum_k X[r][k] w[k * ws] for rows r: one wave per row, lanes over k, shuffle sum
+__device__ inline float et_wave_dot(const float* x, const float* __restrict__ w, int ws, int K) {
+    float v = 0.f;
+    for (int k = threadIdx.x & 63; k < K; k += 64) v = fmaf(x[k], w[(size_t)k * ws], v);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
 struct EgnnTrain {
@@ -184,7 +284,8 @@ __host__ __device__ inline SaveOff save_off(int N, int H, int L) {
     const int E = N * (N - 1);
     SaveOff s;
     s.hin = 0; s.cin = s.hin + (int64_t)N * H; s.ze1 = s.cin + 4LL * N; s.zef = s.ze1 + (int64_t)E * H;
-    s.zc1 = s.zef + (int64_t)E * H; s.u = s.zc1 + (int64_t)E * H; s.zv1 = s.u + E; s.zn1 = s.zv1 + (int64_t)N * H;
+    s.zc1 = s.zef + (int64_t)E * H; s.u = s.zc1 + (int64_t)E * H; s.zv1 = s.u + ((E + 3) & ~3);
+    s.zn1 = s.zv1 + (int64_t)N * H;   // (every block starts 16-byte aligned: float4 access)
     s.agg = s.zn1 + (int64_t)N * H;
     s.layer = s.agg + (int64_t)N * H;
     s.hfin = L * s.layer; s.cfin = s.hfin + (int64_t)N * H;
@@ -193,7 +294,7 @@ __host__ __device__ inline SaveOff save_off(int N, int H, int L) {
 }
 __host__ __device__ inline int64_t save_floats(int N, int H, int L, int heads) {
     const SaveOff s = save_off(N, H, L);
-    return s.cfin + 4LL * N + heads * s.head;
+    return (s.cfin + 4LL * N + heads * s.head + 3) & ~3LL;
 }
 
 // LDS (floats), E = N (N - 1): X [E][2H+8] | dX [E][2H+8] | A B C [E][H] | n0..n4 [N][2H] | small
@@ -301,9 +402,10 @@ __device__ void edge_input(const EgnnTrain& P, const Lds& s, const float* h) {
     __syncthreads();
 }
 
+template <int HT>
 __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTrain P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int N = P.N, deg = N - 1, E = N * deg, H = P.H, LX = 2 * H + 8;
+    const int N = P.N, deg = N - 1, E = N * deg, H = HT > 0 ? HT : P.H, LX = 2 * H + 8;
     const Lds s = carve_lds(lds, N, H);
     const int64_t sys = blockIdx.x;
     const SaveOff so = save_off(N, H, P.L);
@@ -326,20 +428,20 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
         for (int o = threadIdx.x; o < 4 * N; o += ET_THREADS) sl[so.cin + o] = s.coord[o];
         geometry(P, s);
         edge_input(P, s, h);
-        et_gemm(s.X, E, LX, LX, P.blob + w.e0, H, P.blob + w.e0b, H, s.A, H, 1, sl + so.ze1);    // E1
-        et_gemm(s.A, E, H, H, P.blob + w.e1, H, P.blob + w.e1b, H, s.Bq, H, 1, sl + so.zef);      // EF
-        et_gemm(s.Bq, E, H, H, P.blob + w.c0, H, P.blob + w.c0b, H, s.A, H, 1, sl + so.zc1);      // C1
-        for (int e = threadIdx.x; e < E; e += ET_THREADS) {                                        // coord head
-            float u = 0.f;
-            for (int n = 0; n < H; ++n) u = fmaf(s.A[e * H + n], P.blob[w.c1w + n], u);
-            sl[so.u + e] = u;
-            s.cd[e] = P.use_tanh ? tanhf(u) : u;
+        et_fwd<HT>(s.X, E, LX, LX, P.blob + w.e0, H, P.blob + w.e0b, H, s.A, H, 1, sl + so.ze1);    // E1
+        et_fwd<HT>(s.A, E, H, H, P.blob + w.e1, H, P.blob + w.e1b, H, s.Bq, H, 1, sl + so.zef);      // EF
+        et_fwd<HT>(s.Bq, E, H, H, P.blob + w.c0, H, P.blob + w.c0b, H, s.A, H, 1, sl + so.zc1);      // C1
+        for (int e = threadIdx.x >> 6; e < E; e += ET_THREADS / 64) {                              // coord head
+            const float u = et_wave_dot(s.A + e * H, P.blob + w.c1w, 1, H);
+            if ((threadIdx.x & 63) == 0) {
+                sl[so.u + e] = u;
+                s.cd[e] = P.use_tanh ? tanhf(u) : u;
+            }
         }
-        et_gemm(h, N, H, H, P.blob + w.v0, H, P.blob + w.v0b, H, s.n1, H, 1, sl + so.zv1);        // V1
-        for (int i = threadIdx.x; i < N; i += ET_THREADS) {
-            float v = P.blob[w.v1b];
-            for (int n = 0; n < H; ++n) v = fmaf(s.n1[i * H + n], P.blob[w.v1w + n], v);
-            s.vd[i] = v;
+        et_fwd<HT>(h, N, H, H, P.blob + w.v0, H, P.blob + w.v0b, H, s.n1, H, 1, sl + so.zv1);        // V1
+        for (int i = threadIdx.x >> 6; i < N; i += ET_THREADS / 64) {
+            const float v = et_wave_dot(s.n1 + i * H, P.blob + w.v1w, 1, H);
+            if ((threadIdx.x & 63) == 0) s.vd[i] = P.blob[w.v1b] + v;
         }
         for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {                                   // [h | mean EF]
             const int i = o / H, n = o - i * H;
@@ -351,9 +453,9 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
             s.n2[i * 2 * H + H + n] = a;
         }
         __syncthreads();
-        et_gemm(s.n2, N, 2 * H, 2 * H, P.blob + w.n0, H, P.blob + w.n0b, H, s.n3, H, 1, sl + so.zn1);   // N1
+        et_fwd<HT>(s.n2, N, 2 * H, 2 * H, P.blob + w.n0, H, P.blob + w.n0b, H, s.n3, H, 1, sl + so.zn1);   // N1
         float* hn = h == s.n0 ? s.n4 : s.n0;
-        et_gemm(s.n3, N, H, H, P.blob + w.n1, H, P.blob + w.n1b, H, hn, H, 0, nullptr);
+        et_fwd<HT>(s.n3, N, H, H, P.blob + w.n1, H, P.blob + w.n1b, H, hn, H, 0, nullptr);
         for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {   // coord_model + velocity term
             const int i = o / 3, k = o - 3 * i;
             float a = 0.f;
@@ -386,21 +488,21 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
     for (int t = 0; t < P.heads; ++t) {
         const HeadOff w = head_off(H, P.L, t);
         float* sh = sv + so.cfin + 4 * N + t * so.head;
-        et_gemm(s.X, N, LH, LH, P.blob + w.w0, H, P.blob + w.b0, H, s.n1, H, 1, sh + so.zg1);
-        et_gemm(s.n1, N, H, H, P.blob + w.w1, H, P.blob + w.b1, H, s.n2, H, 1, sh + so.zg2);
-        for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {
+        et_fwd<HT>(s.X, N, LH, LH, P.blob + w.w0, H, P.blob + w.b0, H, s.n1, H, 1, sh + so.zg1);
+        et_fwd<HT>(s.n1, N, H, H, P.blob + w.w1, H, P.blob + w.b1, H, s.n2, H, 1, sh + so.zg2);
+        for (int o = threadIdx.x >> 6; o < 3 * N; o += ET_THREADS / 64) {
             const int i = o / 3, k = o - 3 * i;
-            float v = P.blob[w.b2 + k];
-            for (int n = 0; n < H; ++n) v = fmaf(s.n2[i * H + n], P.blob[w.w2 + 4 * n + k], v);
-            P.out[(sys * N + i) * 3 * P.heads + 3 * t + k] = v;
+            const float v = et_wave_dot(s.n2 + i * H, P.blob + w.w2 + k, 4, H);
+            if ((threadIdx.x & 63) == 0) P.out[(sys * N + i) * 3 * P.heads + 3 * t + k] = P.blob[w.b2 + k] + v;
         }
         __syncthreads();
     }
 }
 
+template <int HT>
 __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTrain P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int N = P.N, deg = N - 1, E = N * deg, H = P.H, LX = 2 * H + 8, LH = H + 8;
+    const int N = P.N, deg = N - 1, E = N * deg, H = HT > 0 ? HT : P.H, LX = 2 * H + 8, LH = H + 8;
     const Lds s = carve_lds(lds, N, H);
     const SaveOff so = save_off(N, H, P.L);
     float* G = P.gpart + (int64_t)blockIdx.x * P.blob_floats;
@@ -667,6 +769,18 @@ int check_train(const nbx_egnn_weights* w, int64_t B, int64_t N) {
 
 constexpr int TRAIN_GROUPS = 64;   // backward workgroups (partial gradient slices)
 
+int set_lds_attr() {
+    static bool done = false;
+    if (done) return NBX_OK;
+    for (const void* k : {(const void*)egnn_train_fwd_kernel<0>, (const void*)egnn_train_fwd_kernel<32>,
+                          (const void*)egnn_train_fwd_kernel<64>, (const void*)egnn_train_fwd_kernel<128>,
+                          (const void*)egnn_train_bwd_kernel<0>, (const void*)egnn_train_bwd_kernel<32>,
+                          (const void*)egnn_train_bwd_kernel<64>, (const void*)egnn_train_bwd_kernel<128>})
+        NBX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    done = true;
+    return NBX_OK;
+}
+
 }  // namespace
 
 extern "C" int nbx_egnn_train_workspace_bytes(const nbx_egnn_weights* w, int64_t B, int64_t N, size_t* bytes) {
@@ -692,15 +806,13 @@ extern "C" int nbx_egnn_train_forward(const nbx_egnn_weights* w, const float* po
     p.save_floats = save_floats((int)N, w->hidden, w->num_layers, w->num_heads);
     p.out = out;
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
-    static bool attr = false;
-    if (!attr) {
-        NBX_HIP(hipFuncSetAttribute((const void*)egnn_train_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
-        NBX_HIP(hipFuncSetAttribute((const void*)egnn_train_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
-        attr = true;
+    if (int rc = set_lds_attr()) return rc;
+    switch (w->hidden) {
+        case 32: hipLaunchKernelGGL(egnn_train_fwd_kernel<32>, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p); break;
+        case 64: hipLaunchKernelGGL(egnn_train_fwd_kernel<64>, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p); break;
+        case 128: hipLaunchKernelGGL(egnn_train_fwd_kernel<128>, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p); break;
+        default: hipLaunchKernelGGL(egnn_train_fwd_kernel<0>, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p);
     }
-    hipLaunchKernelGGL(egnn_train_fwd_kernel, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }
@@ -726,7 +838,13 @@ extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* p
     const int G = (int)(B < TRAIN_GROUPS ? B : TRAIN_GROUPS);
     NBX_HIP(hipMemsetAsync(p.gpart, 0, sizeof(float) * (size_t)G * p.blob_floats, st));
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
-    hipLaunchKernelGGL(egnn_train_bwd_kernel, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p);
+    if (int rc = set_lds_attr()) return rc;
+    switch (w->hidden) {
+        case 32: hipLaunchKernelGGL(egnn_train_bwd_kernel<32>, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p); break;
+        case 64: hipLaunchKernelGGL(egnn_train_bwd_kernel<64>, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p); break;
+        case 128: hipLaunchKernelGGL(egnn_train_bwd_kernel<128>, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p); break;
+        default: hipLaunchKernelGGL(egnn_train_bwd_kernel<0>, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p);
+    }
     NBX_HIP(hipGetLastError());
     hipLaunchKernelGGL(egnn_grad_reduce_kernel, dim3((unsigned)((p.blob_floats + 255) / 256)), dim3(256), 0, st, p.gpart,
                        G, p.blob_floats, grad_blob);

@@ -161,9 +161,11 @@ class EGNNMultiChannel(nn.Module):
         """The input-major weight blob of the persistent per-system kernel (include/nbx.h).
         ``differentiable``: built from the parameters with autograd-tracked ops, so a gradient
         of the blob (nbx_egnn_train_backward) flows back to every parameter."""
-        H = self.hidden_node_dim
-        f = dict(device=device, dtype=torch.float32)
         src = (lambda w: w) if differentiable else (lambda w: w.detach())
+        return self._blob_from(src, dict(device=device, dtype=torch.float32))
+
+    def _blob_from(self, src, f):
+        H = self.hidden_node_dim
 
         def t(w, rows=None, cols=None):          # nn.Linear [out][in] -> [in][out], zero-padded
             x = src(w).to(**f).T
@@ -224,6 +226,46 @@ class EGNNMultiChannel(nn.Module):
             self._ws = torch.empty(n.value, dtype=torch.uint8, device=device)
         return self._ws
 
+    # ------------------------------------------------------------ training blob
+    def _train_layout(self, device):
+        """(params, index, blob_floats): the parameters the blob holds, in a fixed order, and the blob
+        position of every element of their flattened concatenation -- persist_blob's layout traced
+        once with element ids, so a training step packs the blob with one scatter and maps the blob
+        gradient back onto the parameters with one gather."""
+        key = (device, tuple((tuple(q.shape), q.dtype) for q in self.parameters()))
+        if getattr(self, "_tlayout", None) is not None and self._tlayout[0] == key:
+            return self._tlayout[1:]
+        params = list(self.parameters())
+        ids, base = {}, 1
+        for q in params:
+            ids[id(q)] = torch.arange(base, base + q.numel(), dtype=torch.float64).reshape(q.shape)
+            base += q.numel()
+        tagged = self._blob_from(lambda w: ids[id(w)], dict(device="cpu", dtype=torch.float64)).to(torch.int64)
+        pos = torch.nonzero(tagged).reshape(-1)
+        elem = tagged[pos] - 1                       # flat parameter element at each blob position
+        index = torch.full((base - 1,), -1, dtype=torch.int64)
+        index[elem] = pos
+        used, off = [], 0
+        for q in params:
+            sl = index[off:off + q.numel()]
+            if bool((sl >= 0).all()):
+                used.append((q, sl))
+            elif bool((sl >= 0).any()):
+                raise RuntimeError("persist blob holds part of a parameter")
+            off += q.numel()
+        idx = torch.cat([sl for _, sl in used]).to(device)
+        self._tlayout = (key, [q for q, _ in used], idx, int(tagged.numel()))
+        return self._tlayout[1:]
+
+    def _train_weights(self, blob):
+        """The weight struct of the training entry points: the model's flags and the blob."""
+        W = _lib.EgnnWeights()
+        W.hidden, W.num_layers, W.num_heads = self.hidden_node_dim, self.num_layers, len(self.heads)
+        W.recurrent, W.norm_diff, W.use_tanh = int(self.recurrent), int(self.norm_diff), int(self.use_tanh)
+        W.coords_weight = float(self.coords_weight)
+        W.persist_blob = blob.data_ptr()
+        return W
+
     # ------------------------------------------------------------ forward
     def _trainable(self, N: int) -> bool:
         """Shapes the native training step covers (csrc/egnn_train.hip check_train): 2 <= N <= 8
@@ -254,9 +296,10 @@ class EGNNMultiChannel(nn.Module):
         if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()) and self._trainable(N):
             # training step (trainer.py:233-358): the native forward keeps its activations and
             # loss.backward() runs the native backward (csrc/egnn_train.hip)
-            W = self._weights(device)
-            blob = self.persist_blob(device, differentiable=True)
-            return _EgnnTrainFn.apply(blob, W, p, v, m, B, N).to(pos.dtype)
+            if self._native_reason:
+                raise NotImplementedError(self._native_reason)
+            params, idx, nblob = self._train_layout(device)
+            return _EgnnTrainFn.apply(self, idx, nblob, p, v, m, B, N, *params).to(pos.dtype)
         out = torch.empty(V, 3 * len(self.heads), device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(B, N, device)
@@ -286,13 +329,17 @@ class EGNNMultiChannel(nn.Module):
 
 class _EgnnTrainFn(torch.autograd.Function):
     """Native training forward / backward of EGNNMultiChannel (include/nbx.h
-    nbx_egnn_train_forward / nbx_egnn_train_backward): input = the differentiable weight blob,
-    output = pred [V, 3 heads]; backward returns dL/dblob, which autograd maps onto the parameters
-    through EGNNMultiChannel.persist_blob(differentiable=True)."""
+    nbx_egnn_train_forward / nbx_egnn_train_backward).  Inputs: the parameters the weight blob
+    holds; forward scatters them into the blob (one launch) and runs the native forward, output =
+    pred [V, 3 heads]; backward runs the native backward to dL/dblob and gathers it back onto the
+    parameters (one launch)."""
 
     @staticmethod
-    def forward(ctx, blob, W, pos, vel, mass, B, N):
+    def forward(ctx, model, idx, nblob, pos, vel, mass, B, N, *params):
         device = pos.device
+        flat = torch.cat([q.detach().reshape(-1).to(torch.float32) for q in params])
+        blob = torch.zeros(nblob, device=device, dtype=torch.float32).index_copy_(0, idx, flat)
+        W = model._train_weights(blob)
         n = _lib.c_sz()
         _lib.check(_lib.lib().nbx_egnn_train_workspace_bytes(W, B, N, n), "nbx_egnn_train_workspace_bytes")
         ws = torch.empty(n.value, dtype=torch.uint8, device=device)
@@ -300,9 +347,9 @@ class _EgnnTrainFn(torch.autograd.Function):
         _lib.check(_lib.lib().nbx_egnn_train_forward(W, _lib.dev_ptr(pos), _lib.dev_ptr(vel), _lib.dev_ptr(mass), B, N,
                                                      _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
                                                      _lib.stream_ptr(device)), "nbx_egnn_train_forward")
-        ctx.W, ctx.B, ctx.N, ctx.ws = W, B, N, ws
+        ctx.W, ctx.B, ctx.N, ctx.ws, ctx.blob, ctx.idx = W, B, N, ws, blob, idx
+        ctx.shapes = [(q.shape, q.dtype) for q in params]
         ctx.save_for_backward(pos, vel, mass)
-        ctx.blob_shape = blob.shape
         return out
 
     @staticmethod
@@ -310,10 +357,16 @@ class _EgnnTrainFn(torch.autograd.Function):
         pos, vel, mass = ctx.saved_tensors
         device = pos.device
         g = grad_out.detach().to(device=device, dtype=torch.float32).contiguous()
-        grad_blob = torch.empty(ctx.blob_shape, device=device, dtype=torch.float32)
+        grad_blob = torch.empty_like(ctx.blob)
         _lib.check(_lib.lib().nbx_egnn_train_backward(ctx.W, _lib.dev_ptr(pos), _lib.dev_ptr(vel), _lib.dev_ptr(mass),
                                                       ctx.B, ctx.N, _lib.dev_ptr(g), _lib.dev_ptr(grad_blob),
                                                       _lib.dev_ptr(ctx.ws), ctx.ws.numel(),
                                                       _lib.stream_ptr(device)), "nbx_egnn_train_backward")
-        ctx.ws = None
-        return grad_blob, None, None, None, None, None, None
+        flat = grad_blob.index_select(0, ctx.idx)
+        grads, off = [], 0
+        for shape, dtype in ctx.shapes:
+            k = shape.numel()
+            grads.append(flat[off:off + k].view(shape).to(dtype))
+            off += k
+        ctx.ws = ctx.blob = None
+        return (None,) * 8 + tuple(grads)

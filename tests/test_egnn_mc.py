@@ -212,6 +212,25 @@ def test_gpu_training_step_c1_shape(hip_device):
     assert any(not torch.equal(p0, p1) for p0, p1 in zip(before, model.parameters()))
 
 
+
+def test_training_blob_index_map():
+    """The training step packs the persist blob with one scatter of the flattened parameters and
+    maps the blob gradient back with one gather (EGNNMultiChannel._train_layout): the scatter must
+    reproduce persist_blob exactly and the gather must be its adjoint (every parameter element read
+    from its own blob slot, the padding never)."""
+    torch.manual_seed(3)
+    m = make(hidden=32, layers=2, dtype=torch.float32)
+    params, idx, nblob = m._train_layout("cpu")
+    flat = torch.cat([q.detach().reshape(-1) for q in params])
+    blob = torch.zeros(nblob).index_copy_(0, idx, flat)
+    torch.testing.assert_close(blob, m.persist_blob("cpu"), rtol=0, atol=0)
+    assert idx.unique().numel() == idx.numel() == sum(q.numel() for q in m.parameters())
+    g = torch.randn(nblob)
+    ref = torch.autograd.grad(m.persist_blob("cpu", differentiable=True), params, g)
+    got = g.index_select(0, idx)
+    torch.testing.assert_close(got, torch.cat([r.reshape(-1) for r in ref]), rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("tag", ["h32", "h64"])
 def test_torch_restatement_matches_reference_gradients(golden, tag):
     """oracle/egnn_mc_torch.py (the CPU baseline of bench.py --model egnn_mc_train) reproduces the
