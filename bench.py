@@ -371,7 +371,8 @@ def bench_egnn_train(a, rank, world, device, P):
     """one training step of the reference trainer (trainer.py:233-358, standard
     precision): zero_grad, native forward (activations kept), MSE loss, loss.backward() -> native
     backward (csrc/egnn_train.hip), gradient all-reduce over ranks (data parallel, RCCL), clip to
-    norm 1, Adam step.  C1 widths (6 x 128), N=5, batch 64 per rank ("weak")."""
+    norm 1, AdamW step + LambdaLR (trainer.py:170-194).  C1 widths (6 x 128), N=5, batch 64 per
+    rank ("weak")."""
     from nbody_amd.egnn_mc import EGNNMultiChannel
     B, N = a.batch or 64, 5
     torch.manual_seed(0)
@@ -390,7 +391,12 @@ def bench_egnn_train(a, rank, world, device, P):
     g.edge_index = fc_edge_index(B, N, device)
     g.nbx_system_size = N
     target = t(rng.standard_normal((B * N, 6)) * 0.1)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    # Trainer.create_optimizer / create_lr_scheduler (trainer.py:170-194): AdamW(weight_decay 1e-8,
+    # betas (0.9, 0.98), eps 1e-9) under the LambdaLR warmup schedule; the update as one fused launch
+    opt = torch.optim.AdamW(model.parameters(), lr=1.0, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9,
+                            fused=True)
+    sched = torch.optim.lr_scheduler.LambdaLR(
+        opt, lambda s: 128 ** -0.5 * min(max(s, 1) ** -0.5, max(s, 1) * 1000 ** -1.5))
     params = list(model.parameters())
 
     def train_step():
@@ -398,8 +404,9 @@ def bench_egnn_train(a, rank, world, device, P):
         loss = torch.nn.functional.mse_loss(model(g), target)
         loss.backward()
         P.allreduce_gradients(params)   # data parallel over RCCL (one bucket at C1); no-op on one rank
-        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        torch.nn.utils.clip_grad_norm_(params, 1.0, foreach=True)
         opt.step()
+        sched.step()
         return loss
 
     for _ in range(max(a.warmup, 1)):
@@ -412,13 +419,13 @@ def bench_egnn_train(a, rank, world, device, P):
     loss, elapsed = timed_region(work, device, P)
     value = a.steps / elapsed * world
     result = {
-        "metric": "EGNN-MC training steps/sec (C1 widths, forward + backward + Adam)", "value": round(value, 3),
+        "metric": "EGNN-MC training steps/sec (C1 widths, forward + backward + AdamW)", "value": round(value, 3),
         "unit": "train steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (GravitySim frame-0 initial states, random targets, seeded random-init weights)",
         "config": {"workload": "SURVEY 8(f)4: EGNN-MC 6 x 128 training step, N=5, batch 64 per GPU, MSE loss, "
-                               "grad-norm clip 1, Adam", "model": "EGNN-MC", "global_batch": B * world,
+                               "grad-norm clip 1, AdamW + LambdaLR (trainer.py:170-194)", "model": "EGNN-MC", "global_batch": B * world,
                    "seq_len": a.steps, "parallelism": f"dp{world}"},
         "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
                      "kernel": "egnn_train_fwd_kernel / egnn_train_bwd_kernel: one workgroup per system",
@@ -427,7 +434,7 @@ def bench_egnn_train(a, rank, world, device, P):
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import egnn_mc_torch as OT
         Pc = {k: v.detach().double().cpu().clone().requires_grad_(True) for k, v in model.named_parameters()}
-        optc = torch.optim.Adam(list(Pc.values()), lr=1e-4)
+        optc = torch.optim.AdamW(list(Pc.values()), lr=1e-4, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9)
         pc, vc, mc = (torch.from_numpy(x.reshape(-1, w)).double() for x, w in ((loc, 3), (vel, 3), (mass, 1)))
         tc = target.double().cpu()
         steps = 10

@@ -15,7 +15,10 @@
 //   tanh), ZV1 ZN1 AGG [N][H]; after the layers: h [N][H], coord [N][4], per head ZG1 ZG2 [N][H].
 // Weight gradients of one workgroup accumulate into its own slice of a partial buffer
 // [G][blob] (systems g, g + G, ...); a second kernel sums the G slices (deterministic order).
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "nbx_internal.h"
 
@@ -36,7 +39,7 @@ constexpr int RB = 4;
 
 // Y[r][n] = b[n] + sum_k X[r][k] W[k][n] (W input-major [K][ldw]); Zs (global, optional) gets the
 // pre-activation; Y gets act(.) with act 1 = SiLU.  X / Y in LDS.  All threads call.
-__device__ void et_gemm(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
+__device__ __forceinline__ void et_gemm(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
                         const float* __restrict__ b, int Nc, float* Y, int ldy, int act, float* Zs) {
     const int rg = (rows + RB - 1) / RB;
     for (int o = threadIdx.x; o < rg * Nc; o += ET_THREADS) {
@@ -69,22 +72,24 @@ __device__ void et_gemm(const float* X, int rows, int ldx, int K, const float* _
 // Thread = one output column k (of RS row ranges when K < 512): W row k is read once, 32 columns at
 // a time into registers, and every dZ float4 is an LDS broadcast (all lanes of a wave read the same
 // row); 4 rows per pass give 4 independent FMA chains.
-__device__ void et_gemm_t(const float* dZ, int rows, int ldz, int Nc, const float* __restrict__ W, int ldw, int K,
+constexpr int ET_TC = 4;   // float4 columns of W per register chunk
+__device__ __forceinline__ void et_gemm_t(const float* dZ, int rows, int ldz, int Nc, const float* __restrict__ W, int ldw, int K,
                           float* dX, int ldx, bool accumulate) {
     const int RS = K >= ET_THREADS ? 1 : ET_THREADS / K;
     for (int t = threadIdx.x; t < K * RS; t += ET_THREADS) {
         const int k = t % K, part = t / K;
         const int ra = rows * part / RS, rb = rows * (part + 1) / RS;
         const float* w = W + (size_t)k * ldw;
-        for (int c0 = 0; c0 < Nc; c0 += 32) {
-            float4 wr[8];
+        for (int c0 = 0; c0 < Nc; c0 += 4 * ET_TC) {
+            float4 wr[ET_TC];
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < ET_TC; ++i)
                 wr[i] = c0 + 4 * i < Nc ? *reinterpret_cast<const float4*>(w + c0 + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
             for (int r0 = ra; r0 < rb; r0 += 4) {
                 float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
+                for (int i = 0; i < ET_TC; ++i) {
                     if (c0 + 4 * i >= Nc) break;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -109,8 +114,8 @@ __device__ void et_gemm_t(const float* dZ, int rows, int ldz, int Nc, const floa
 // G[k][n] += sum_r X[r][k] dZ[r][n] (k < K), gb[n] += sum_r dZ[r][n]; G / gb global (this workgroup's
 // partial slice), X / dZ in LDS or global (K, Nc, ldx, ldz, ldg multiples of 4, rows 16-byte aligned).
 // Thread = a 4 x 4 block of G: per row one float4 of X and one of dZ feed 16 FMAs.
-__device__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* dZ, int ldz, int Nc, float* G, int ldg,
-                         float* gb) {
+__device__ __forceinline__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* dZ, int ldz, int Nc, float* G, int ldg,
+                         float* gb, bool first) {
     const int kq = K >> 2, nq = Nc >> 2;
     for (int o = threadIdx.x; o < kq * nq; o += ET_THREADS) {
         const int kb = o / nq, nb = o - kb * nq, k0 = 4 * kb, n0 = 4 * nb;
@@ -132,95 +137,156 @@ __device__ void et_wgrad(const float* X, int rows, int ldx, int K, const float* 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float4* g = reinterpret_cast<float4*>(G + (size_t)(k0 + i) * ldg + n0);
-            float4 c = *g;
-            c.x += a[i].x; c.y += a[i].y; c.z += a[i].z; c.w += a[i].w;
-            *g = c;
+            if (first) {   // the workgroup's first system writes its slice (no read-modify-write latency)
+                *g = a[i];
+            } else {
+                float4 c = *g;
+                c.x += a[i].x; c.y += a[i].y; c.z += a[i].z; c.w += a[i].w;
+                *g = c;
+            }
         }
     }
     if (gb)
         for (int n = threadIdx.x; n < Nc; n += ET_THREADS) {
             float v = 0.f;
             for (int r = 0; r < rows; ++r) v += dZ[r * ldz + n];
-            gb[n] += v;
+            gb[n] = first ? v : gb[n] + v;
         }
     __syncthreads();
 }
 
-// Register-resident forward product for Nc = HT output columns (HT = 32, 64, 128), K % 4 == 0,
-// K <= 2 HT + 8, W input-major [K][HT]: wave w owns columns [4 CGW w, 4 CGW (w + 1)), lane = (column
-// group cg, K-slice sl); the lane's weights (its 4 columns of rows 4 (sl + SL j) .. + 3) are loaded
-// once into registers and serve every row; per row the K-slices are summed with xor shuffles over the
-// slice bits of the lane id, and slice 0 writes the row's 4 outputs.
-template <int HT>
-__device__ void et_gemm_r(const float* X, int rows, int ldx, int K, const float* __restrict__ W,
-                          const float* __restrict__ b, float* Y, int ldy, int act, float* Zs) {
-    constexpr int CGW = HT / 32, SL = 64 / CGW;
-    constexpr int KB = ((2 * HT + 8) / 4 + SL - 1) / SL;   // float4 K-blocks per lane
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int cg = lane % CGW, sl = lane / CGW;
-    const int n0 = (wave * CGW + cg) * 4;
-    const int kq = K >> 2;
+// Sum over the 16 lanes of a DPP row; every lane of the row gets the total (4 VALU adds, no LDS).
+__device__ __forceinline__ float et_row_sum16(float v) {
+    auto dpp = [](float x, int ctrl) -> float {
+        switch (ctrl) {   // (the control must be a compile-time constant)
+            case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, true));
+            case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, true));
+            case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, true));
+            default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, true));
+        }
+    };
+    v += dpp(v, 0);   // quad_perm [1,0,3,2]
+    v += dpp(v, 1);   // quad_perm [2,3,0,1]: quad sums
+    v += dpp(v, 2);   // row_half_mirror: sums of 8
+    v += dpp(v, 3);   // row_mirror: sums of 16
+    return v;
+}
+
+// One 16-column tile of a register-resident product: Y[r][c0 + c] = sum_q A[r][q] B(q, c0 + c) over the
+// contraction q < Q (Q % 4 == 0) for all rows, where lane = (slice sl = lane & 15, column group
+// cg = lane >> 4) holds B for its 4 columns and the contraction blocks qb = sl + 16 j in registers
+// (loaded once), reads A rows as LDS float4 broadcasts, and the 16 slices of a column group (one DPP
+// row) are summed with et_row_sum16; lane sl of the row then owns output (row r0 + sl / 4, column
+// 4 cg + sl % 4) of the 4-row pass.  TRANS = false: B(q, n) = W[q][n] (W input-major [Q][ldw]);
+// TRANS = true: B(q, n) = W[n][q] (W [ncols][ldw], the transposed product of the backward).
+template <int KB, bool TRANS, class Epi>
+__device__ __forceinline__ void et_tile(const float* A, int rows, int lda, int Q, const float* __restrict__ W, int ldw,
+                                        int c0, int ncols, Epi epi) {
+    const int lane = threadIdx.x & 63, sl = lane & 15, cg = lane >> 4;
+    const int n0 = c0 + 4 * cg;
+    const int qq = Q >> 2;
     float4 w[KB][4];
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
-        const int kb = sl + SL * j;
+        const int qb = sl + 16 * j;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            w[j][i] = kb < kq ? *reinterpret_cast<const float4*>(W + (size_t)(4 * kb + i) * HT + n0)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    const float4 bias = b ? *reinterpret_cast<const float4*>(b + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r0 = 0; r0 < rows; r0 += 4) {
-        float4 acc[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int j = 0; j < KB; ++j) {
-            const int kb = sl + SL * j;
-            if (kb >= kq) break;
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int r = r0 + rr < rows ? r0 + rr : rows - 1;
-                const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + 4 * kb);
-                acc[rr].x = fmaf(x.x, w[j][0].x, fmaf(x.y, w[j][1].x, fmaf(x.z, w[j][2].x, fmaf(x.w, w[j][3].x, acc[rr].x))));
-                acc[rr].y = fmaf(x.x, w[j][0].y, fmaf(x.y, w[j][1].y, fmaf(x.z, w[j][2].y, fmaf(x.w, w[j][3].y, acc[rr].y))));
-                acc[rr].z = fmaf(x.x, w[j][0].z, fmaf(x.y, w[j][1].z, fmaf(x.z, w[j][2].z, fmaf(x.w, w[j][3].z, acc[rr].z))));
-                acc[rr].w = fmaf(x.x, w[j][0].w, fmaf(x.y, w[j][1].w, fmaf(x.z, w[j][2].w, fmaf(x.w, w[j][3].w, acc[rr].w))));
+        for (int i = 0; i < 4; ++i) {
+            if (qb >= qq) { w[j][i] = make_float4(0.f, 0.f, 0.f, 0.f); continue; }
+            if constexpr (!TRANS) {
+                w[j][i] = *reinterpret_cast<const float4*>(W + (size_t)(4 * qb + i) * ldw + n0);
+            } else {   // w[j][i] = (W[n0][4qb + i], W[n0 + 1][4qb + i], ...): 4 column rows, transposed
+                const int n = n0 + i < ncols ? n0 + i : ncols - 1;
+                w[j][i] = *reinterpret_cast<const float4*>(W + (size_t)n * ldw + 4 * qb);
             }
         }
+    }
+    for (int r0 = 0; r0 < rows; r0 += 4) {
+        float acc[4][4];
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-            for (int o = CGW; o < 64; o <<= 1) {
-                acc[rr].x += __shfl_xor(acc[rr].x, o);
-                acc[rr].y += __shfl_xor(acc[rr].y, o);
-                acc[rr].z += __shfl_xor(acc[rr].z, o);
-                acc[rr].w += __shfl_xor(acc[rr].w, o);
-            }
-        if (sl == 0)
+            for (int c = 0; c < 4; ++c) acc[rr][c] = 0.f;
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+            const int qb = sl + 16 * j;
+            if (qb >= qq) break;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int r = r0 + rr;
-                if (r >= rows) break;
-                const float4 z = make_float4(acc[rr].x + bias.x, acc[rr].y + bias.y, acc[rr].z + bias.z, acc[rr].w + bias.w);
-                if (Zs) *reinterpret_cast<float4*>(Zs + r * HT + n0) = z;
-                *reinterpret_cast<float4*>(Y + r * ldy + n0) =
-                    act == 1 ? make_float4(et_silu(z.x), et_silu(z.y), et_silu(z.z), et_silu(z.w)) : z;
+                const int r = r0 + rr < rows ? r0 + rr : rows - 1;
+                const float4 x = *reinterpret_cast<const float4*>(A + r * lda + 4 * qb);
+                if constexpr (!TRANS) {
+                    // w[j][i] = W[4qb + i][n0 .. n0 + 3]
+                    acc[rr][0] = fmaf(x.x, w[j][0].x, fmaf(x.y, w[j][1].x, fmaf(x.z, w[j][2].x, fmaf(x.w, w[j][3].x, acc[rr][0]))));
+                    acc[rr][1] = fmaf(x.x, w[j][0].y, fmaf(x.y, w[j][1].y, fmaf(x.z, w[j][2].y, fmaf(x.w, w[j][3].y, acc[rr][1]))));
+                    acc[rr][2] = fmaf(x.x, w[j][0].z, fmaf(x.y, w[j][1].z, fmaf(x.z, w[j][2].z, fmaf(x.w, w[j][3].z, acc[rr][2]))));
+                    acc[rr][3] = fmaf(x.x, w[j][0].w, fmaf(x.y, w[j][1].w, fmaf(x.z, w[j][2].w, fmaf(x.w, w[j][3].w, acc[rr][3]))));
+                } else {
+                    // w[j][c] = W[n0 + c][4qb .. 4qb + 3]
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        acc[rr][c] = fmaf(x.x, w[j][c].x, fmaf(x.y, w[j][c].y, fmaf(x.z, w[j][c].z, fmaf(x.w, w[j][c].w, acc[rr][c]))));
+                }
             }
+        }
+        float mine = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float t = et_row_sum16(acc[rr][c]);
+                mine = sl == 4 * rr + c ? t : mine;
+            }
+        const int r = r0 + (sl >> 2), n = n0 + (sl & 3);
+        if (r < rows && n < ncols) epi(r, n, mine);
     }
+}
+
+// forward product, H = HT in {32, 64, 128}: Y = act(X W + b) (W input-major [K][HT], K % 4 == 0,
+// K <= 2 HT + 8); wave w computes the 16-column tiles w, w + 8, ...
+template <int HT>
+__device__ __forceinline__ void et_gemm_r(const float* X, int rows, int ldx, int K, const float* __restrict__ W,
+                                          const float* __restrict__ b, float* Y, int ldy, int act, float* Zs) {
+    constexpr int KB = ((2 * HT + 8) / 4 + 15) / 16;
+    for (int t = threadIdx.x >> 6; t < HT / 16; t += ET_THREADS / 64)
+        et_tile<KB, false>(X, rows, ldx, K, W, HT, 16 * t, HT, [&](int r, int n, float v) {
+            const float z = v + (b ? b[n] : 0.f);
+            if (Zs) Zs[r * HT + n] = z;
+            Y[r * ldy + n] = act == 1 ? et_silu(z) : z;
+        });
+    __syncthreads();
+}
+
+// backward transposed product, H = HT: dX[r][k] (+)= sum_n dZ[r][n] W[k][n] (n < HT, k < K)
+template <int HT>
+__device__ __forceinline__ void et_gemm_t_r(const float* dZ, int rows, int ldz, const float* __restrict__ W, int K,
+                                            float* dX, int ldx, bool accumulate) {
+    constexpr int KB = (HT / 4 + 15) / 16;
+    for (int t = threadIdx.x >> 6; t < (K + 15) / 16; t += ET_THREADS / 64)
+        et_tile<KB, true>(dZ, rows, ldz, HT, W, HT, 16 * t, K, [&](int r, int k, float v) {
+            float* o = dX + r * ldx + k;
+            *o = accumulate ? *o + v : v;
+        });
     __syncthreads();
 }
 
 // forward product: the register-resident form at H = 32 / 64 / 128 (HT), the generic one otherwise
 template <int HT>
-__device__ inline void et_fwd(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
+__device__ __forceinline__ void et_fwd(const float* X, int rows, int ldx, int K, const float* __restrict__ W, int ldw,
                               const float* __restrict__ b, int Nc, float* Y, int ldy, int act, float* Zs) {
     if constexpr (HT > 0) et_gemm_r<HT>(X, rows, ldx, K, W, b, Y, ldy, act, Zs);
     else et_gemm(X, rows, ldx, K, W, ldw, b, Nc, Y, ldy, act, Zs);
 }
 
+// transposed product: the register-resident form at H = HT, the generic one otherwise
+template <int HT>
+__device__ __forceinline__ void et_bwd(const float* dZ, int rows, int ldz, int Nc, const float* __restrict__ W, int ldw,
+                                       int K, float* dX, int ldx, bool accumulate) {
+    if constexpr (HT > 0) et_gemm_t_r<HT>(dZ, rows, ldz, W, K, dX, ldx, accumulate);
+    else et_gemm_t(dZ, rows, ldz, Nc, W, ldw, K, dX, ldx, accumulate);
+}
+
 // out[r] = sum_k X[r][k] w[k * ws] for rows r: one wave per row, lanes over k, shuffle sum
-__device__ inline float et_wave_dot(const float* x, const float* __restrict__ w, int ws, int K) {
+__device__ __forceinline__ float et_wave_dot(const float* x, const float* __restrict__ w, int ws, int K) {
     float v = 0.f;
     for (int k = threadIdx.x & 63; k < K; k += 64) v = fmaf(x[k], w[(size_t)k * ws], v);
 #pragma unroll
@@ -240,6 +306,29 @@ struct EgnnTrain {
     const float* dout;      // backward: dL/dout [B N][3 heads]
     float* gpart;           // backward: [G][blob_floats] partial weight gradients (zeroed by the host)
     int64_t blob_floats;
+    unsigned long long* dbg;   // NBX_ET_DEBUG: per-workgroup phase clocks [grid][16] (tuning only)
+};
+
+// phase clocks of thread 0 (NBX_ET_DEBUG; every phase ends at a workgroup barrier)
+struct EtClock {
+    unsigned long long last, acc[16];
+    __device__ void start(const EgnnTrain& P) {
+        if (P.dbg && threadIdx.x == 0) {
+            last = clock64();
+            for (int i = 0; i < 16; ++i) acc[i] = 0;
+        }
+    }
+    __device__ void tick(const EgnnTrain& P, int i) {
+        if (P.dbg && threadIdx.x == 0) {
+            const unsigned long long t = clock64();
+            acc[i] += t - last;
+            last = t;
+        }
+    }
+    __device__ void flush(const EgnnTrain& P) {
+        if (P.dbg && threadIdx.x == 0)
+            for (int i = 0; i < 16; ++i) P.dbg[blockIdx.x * 16 + i] = acc[i];
+    }
 };
 
 // blob offsets (include/nbx.h): embedding [2][H] + b[H]; per layer e0 [2H+8][H] e0b e1 [H][H] e1b
@@ -410,6 +499,8 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
     const int64_t sys = blockIdx.x;
     const SaveOff so = save_off(N, H, P.L);
     float* sv = P.save + sys * P.save_floats;
+    EtClock ck;
+    ck.start(P);
     load_system(P, s, sys);
     // embedding: x = [|vel|, mass] (Linear 2 -> H)
     float* h = s.n0;
@@ -428,9 +519,12 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
         for (int o = threadIdx.x; o < 4 * N; o += ET_THREADS) sl[so.cin + o] = s.coord[o];
         geometry(P, s);
         edge_input(P, s, h);
+        ck.tick(P, 0);
         et_fwd<HT>(s.X, E, LX, LX, P.blob + w.e0, H, P.blob + w.e0b, H, s.A, H, 1, sl + so.ze1);    // E1
         et_fwd<HT>(s.A, E, H, H, P.blob + w.e1, H, P.blob + w.e1b, H, s.Bq, H, 1, sl + so.zef);      // EF
+        ck.tick(P, 1);
         et_fwd<HT>(s.Bq, E, H, H, P.blob + w.c0, H, P.blob + w.c0b, H, s.A, H, 1, sl + so.zc1);      // C1
+        ck.tick(P, 2);
         for (int e = threadIdx.x >> 6; e < E; e += ET_THREADS / 64) {                              // coord head
             const float u = et_wave_dot(s.A + e * H, P.blob + w.c1w, 1, H);
             if ((threadIdx.x & 63) == 0) {
@@ -438,7 +532,9 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
                 s.cd[e] = P.use_tanh ? tanhf(u) : u;
             }
         }
+        ck.tick(P, 3);
         et_fwd<HT>(h, N, H, H, P.blob + w.v0, H, P.blob + w.v0b, H, s.n1, H, 1, sl + so.zv1);        // V1
+        ck.tick(P, 4);
         for (int i = threadIdx.x >> 6; i < N; i += ET_THREADS / 64) {
             const float v = et_wave_dot(s.n1 + i * H, P.blob + w.v1w, 1, H);
             if ((threadIdx.x & 63) == 0) s.vd[i] = P.blob[w.v1b] + v;
@@ -453,9 +549,11 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
             s.n2[i * 2 * H + H + n] = a;
         }
         __syncthreads();
+        ck.tick(P, 5);
         et_fwd<HT>(s.n2, N, 2 * H, 2 * H, P.blob + w.n0, H, P.blob + w.n0b, H, s.n3, H, 1, sl + so.zn1);   // N1
         float* hn = h == s.n0 ? s.n4 : s.n0;
         et_fwd<HT>(s.n3, N, H, H, P.blob + w.n1, H, P.blob + w.n1b, H, hn, H, 0, nullptr);
+        ck.tick(P, 6);
         for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) {   // coord_model + velocity term
             const int i = o / 3, k = o - 3 * i;
             float a = 0.f;
@@ -470,6 +568,7 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
         __syncthreads();
         for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) s.coord[4 * (o / 3) + o % 3] += s.tmp[o];
         __syncthreads();
+        ck.tick(P, 7);
         h = hn;
     }
     for (int o = threadIdx.x; o < N * H; o += ET_THREADS) sv[so.hfin + o] = h[o];
@@ -497,6 +596,8 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_fwd_kernel(const EgnnTr
         }
         __syncthreads();
     }
+    ck.tick(P, 8);
+    ck.flush(P);
 }
 
 template <int HT>
@@ -506,7 +607,10 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
     const Lds s = carve_lds(lds, N, H);
     const SaveOff so = save_off(N, H, P.L);
     float* G = P.gpart + (int64_t)blockIdx.x * P.blob_floats;
+    EtClock ck;
+    ck.start(P);
     for (int64_t sys = blockIdx.x; sys < P.B; sys += gridDim.x) {
+        const bool first = sys == blockIdx.x;
         const float* sv = P.save + sys * P.save_floats;
         load_system(P, s, sys);
         for (int o = threadIdx.x; o < 3 * N * P.heads; o += ET_THREADS) s.dpred[o] = P.dout[sys * N * 3 * P.heads + o];
@@ -556,16 +660,17 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
                 s.n3[o] = v * et_dsilu(sh[so.zg2 + o]);
             }
             __syncthreads();
-            et_wgrad(s.n1, N, H, H, s.n3, H, H, G + w.w1, H, G + w.b1);
-            et_gemm_t(s.n3, N, H, H, P.blob + w.w1, H, H, s.n4, H, false);   // dG1 -> n4
+            et_wgrad(s.n1, N, H, H, s.n3, H, H, G + w.w1, H, G + w.b1, first);
+            et_bwd<HT>(s.n3, N, H, H, P.blob + w.w1, H, H, s.n4, H, false);   // dG1 -> n4
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) s.n4[o] *= et_dsilu(sh[so.zg1 + o]);   // dZG1
             __syncthreads();
-            et_wgrad(s.X, N, LH, LH, s.n4, H, H, G + w.w0, H, G + w.b0);
-            et_gemm_t(s.n4, N, H, H, P.blob + w.w0, H, LH, s.dX, LH, false);   // dXh [N][H+8]
+            et_wgrad(s.X, N, LH, LH, s.n4, H, H, G + w.w0, H, G + w.b0, first);
+            et_bwd<HT>(s.n4, N, H, H, P.blob + w.w0, H, LH, s.dX, LH, false);   // dXh [N][H+8]
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) dh[o] += s.dX[(o / H) * LH + o % H];
             for (int o = threadIdx.x; o < 3 * N; o += ET_THREADS) s.dcoord[o] += s.dX[(o / 3) * LH + H + o % 3];
             __syncthreads();
         }
+        ck.tick(P, 0);
         // ---- layers, last to first
         for (int l = P.L - 1; l >= 0; --l) {
             const LayerOff w = layer_off(H, l);
@@ -601,6 +706,7 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
                 s.dcd[e] = dc;
             }
             __syncthreads();
+            ck.tick(P, 1);
             // (b) node_mlp: dhn = dh; N1 = silu(ZN1) -> n2; Xn = [hin, AGG] -> n3 (2H wide)
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
                 const int i = o / H, n = o - i * H;
@@ -609,19 +715,20 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
                 s.n3[i * 2 * H + H + n] = sl[so.agg + o];
             }
             __syncthreads();
-            et_wgrad(s.n2, N, H, H, dh, H, H, G + w.n1, H, G + w.n1b);
-            et_gemm_t(dh, N, H, H, P.blob + w.n1, H, H, s.n4, H, false);   // dN1 -> n4
+            et_wgrad(s.n2, N, H, H, dh, H, H, G + w.n1, H, G + w.n1b, first);
+            et_bwd<HT>(dh, N, H, H, P.blob + w.n1, H, H, s.n4, H, false);   // dN1 -> n4
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) s.n4[o] *= et_dsilu(sl[so.zn1 + o]);   // dZN1
             __syncthreads();
-            et_wgrad(s.n3, N, 2 * H, 2 * H, s.n4, H, H, G + w.n0, H, G + w.n0b);
+            et_wgrad(s.n3, N, 2 * H, 2 * H, s.n4, H, H, G + w.n0, H, G + w.n0b, first);
             // dXn = dZN1 Wn0^T -> n2 ([N][2H]); dh_in = (recurrent ? dh : 0) + dXn[:, :H]; dAGG = dXn[:, H:]
-            et_gemm_t(s.n4, N, H, H, P.blob + w.n0, H, 2 * H, s.n2, 2 * H, false);
+            et_bwd<HT>(s.n4, N, H, H, P.blob + w.n0, H, 2 * H, s.n2, 2 * H, false);
             float* dhin = s.n3;   // [N][H] (n3 is free again)
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {
                 const int i = o / H, n = o - i * H;
                 dhin[o] = (P.recurrent ? dh[o] : 0.f) + s.n2[i * 2 * H + n];
             }
             __syncthreads();
+            ck.tick(P, 2);
             // (c) coord_mlp_vel: dV1 = dvd w_v1; gw_v1, gb_v1; dZV1 -> n4; dh_in += dZV1 Wv0^T
             for (int n = threadIdx.x; n < H; n += ET_THREADS) {
                 float v = 0.f;
@@ -638,8 +745,9 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
                 s.n4[o] = s.dvd[i] * P.blob[w.v1w + n] * et_dsilu(sl[so.zv1 + o]);
             }
             __syncthreads();
-            et_wgrad(hin, N, H, H, s.n4, H, H, G + w.v0, H, G + w.v0b);
-            et_gemm_t(s.n4, N, H, H, P.blob + w.v0, H, H, dhin, H, true);
+            et_wgrad(hin, N, H, H, s.n4, H, H, G + w.v0, H, G + w.v0b, first);
+            et_bwd<HT>(s.n4, N, H, H, P.blob + w.v0, H, H, dhin, H, true);
+            ck.tick(P, 3);
             // (d) coord_mlp: dU = dcd (1 - cd^2); C1 = silu(ZC1) -> A; EF = silu(ZEF) -> Bq
             for (int o = threadIdx.x; o < E * H; o += ET_THREADS) {
                 s.A[o] = et_silu(sl[so.zc1 + o]);
@@ -658,8 +766,11 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
                 s.Cq[o] = s.dcd[e] * P.blob[w.c1w + n] * et_dsilu(sl[so.zc1 + o]);
             }
             __syncthreads();
-            et_wgrad(s.Bq, E, H, H, s.Cq, H, H, G + w.c0, H, G + w.c0b);
-            et_gemm_t(s.Cq, E, H, H, P.blob + w.c0, H, H, s.A, H, false);   // dEF -> A
+            ck.tick(P, 4);
+            et_wgrad(s.Bq, E, H, H, s.Cq, H, H, G + w.c0, H, G + w.c0b, first);
+            ck.tick(P, 5);
+            et_bwd<HT>(s.Cq, E, H, H, P.blob + w.c0, H, H, s.A, H, false);   // dEF -> A
+            ck.tick(P, 6);
             // (e) dEF += dAGG[row] / deg
             for (int o = threadIdx.x; o < E * H; o += ET_THREADS) {
                 const int e = o / H, n = o - e * H;
@@ -672,15 +783,21 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
                 s.Bq[o] = et_silu(sl[so.ze1 + o]);
             }
             __syncthreads();
-            et_wgrad(s.Bq, E, H, H, s.Cq, H, H, G + w.e1, H, G + w.e1b);
-            et_gemm_t(s.Cq, E, H, H, P.blob + w.e1, H, H, s.A, H, false);   // dE1 -> A
+            ck.tick(P, 7);
+            et_wgrad(s.Bq, E, H, H, s.Cq, H, H, G + w.e1, H, G + w.e1b, first);
+            ck.tick(P, 5);
+            et_bwd<HT>(s.Cq, E, H, H, P.blob + w.e1, H, H, s.A, H, false);   // dE1 -> A
+            ck.tick(P, 6);
             for (int o = threadIdx.x; o < E * H; o += ET_THREADS) s.A[o] *= et_dsilu(sl[so.ze1 + o]);   // dZE1
             __syncthreads();
             edge_input(P, s, hin);                                         // X (for gWe0)
-            et_wgrad(s.X, E, LX, LX, s.A, H, H, G + w.e0, H, G + w.e0b);
+            ck.tick(P, 8);
+            et_wgrad(s.X, E, LX, LX, s.A, H, H, G + w.e0, H, G + w.e0b, first);
+            ck.tick(P, 9);
             // dX = dZE1 We0^T, only the columns that carry gradient: [0, 2H] (h_row, h_col, radial);
             // ddn still lives in the first 3E floats of s.dX, so the product goes to s.X (X is done)
-            et_gemm_t(s.A, E, H, H, P.blob + w.e0, H, 2 * H + 1, s.X, LX, false);
+            et_bwd<HT>(s.A, E, H, H, P.blob + w.e0, H, 2 * H + 1, s.X, LX, false);
+            ck.tick(P, 10);
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) {   // dh_in[row] / dh_in[col] sums
                 const int i = o / H, n = o - i * H;
                 float v = 0.f;
@@ -722,6 +839,7 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
             }
             for (int o = threadIdx.x; o < N * H; o += ET_THREADS) dh[o] = dhin[o];
             __syncthreads();
+            ck.tick(P, 11);
         }
         // ---- embedding: h0 = b + |vel| w[0] + mass w[1]
         for (int n = threadIdx.x; n < H; n += ET_THREADS) {
@@ -738,6 +856,8 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
         }
         __syncthreads();
     }
+    ck.tick(P, 12);
+    ck.flush(P);
 }
 
 // grad[i] = sum_g part[g][i]
@@ -747,6 +867,29 @@ __global__ void egnn_grad_reduce_kernel(const float* __restrict__ part, int G, i
     float v = 0.f;
     for (int g = 0; g < G; ++g) v += part[(int64_t)g * n + i];
     grad[i] = v;
+}
+
+// NBX_ET_DEBUG=1: per-workgroup phase clocks of the training kernels, averaged to stderr (tuning only)
+unsigned long long* et_dbg_buf() {
+    static const bool on = getenv("NBX_ET_DEBUG") != nullptr;
+    static unsigned long long* buf = nullptr;
+    if (on && !buf && hipMalloc(&buf, sizeof(unsigned long long) * 16 * 4096) != hipSuccess) buf = nullptr;
+    return on ? buf : nullptr;
+}
+
+int et_dbg_dump(const char* what, unsigned long long* dbg, int grid, hipStream_t st) {
+    if (!dbg) return NBX_OK;
+    std::vector<unsigned long long> h((size_t)grid * 16);
+    NBX_HIP(hipStreamSynchronize(st));
+    NBX_HIP(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    fprintf(stderr, "et_debug %s (avg clocks per workgroup):", what);
+    for (int i = 0; i < 16; ++i) {
+        double a = 0;
+        for (int g = 0; g < grid; ++g) a += (double)h[(size_t)g * 16 + i];
+        if (a > 0) fprintf(stderr, " [%d] %.0f", i, a / grid);
+    }
+    fprintf(stderr, "\n");
+    return NBX_OK;
 }
 
 int64_t blob_floats(const nbx_egnn_weights* w) {
@@ -805,6 +948,7 @@ extern "C" int nbx_egnn_train_forward(const nbx_egnn_weights* w, const float* po
     p.save = static_cast<float*>(workspace);
     p.save_floats = save_floats((int)N, w->hidden, w->num_layers, w->num_heads);
     p.out = out;
+    p.dbg = et_dbg_buf();
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
     if (int rc = set_lds_attr()) return rc;
     switch (w->hidden) {
@@ -814,7 +958,7 @@ extern "C" int nbx_egnn_train_forward(const nbx_egnn_weights* w, const float* po
         default: hipLaunchKernelGGL(egnn_train_fwd_kernel<0>, dim3((unsigned)B), dim3(ET_THREADS), lds, (hipStream_t)stream, p);
     }
     NBX_HIP(hipGetLastError());
-    return NBX_OK;
+    return et_dbg_dump("forward", p.dbg, (int)B, (hipStream_t)stream);
 }
 
 extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* pos, const float* vel,
@@ -836,6 +980,7 @@ extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* p
     p.blob_floats = blob_floats(w);
     p.gpart = p.save + B * p.save_floats;
     const int G = (int)(B < TRAIN_GROUPS ? B : TRAIN_GROUPS);
+    p.dbg = et_dbg_buf();
     NBX_HIP(hipMemsetAsync(p.gpart, 0, sizeof(float) * (size_t)G * p.blob_floats, st));
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
     if (int rc = set_lds_attr()) return rc;
@@ -846,6 +991,7 @@ extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* p
         default: hipLaunchKernelGGL(egnn_train_bwd_kernel<0>, dim3((unsigned)G), dim3(ET_THREADS), lds, st, p);
     }
     NBX_HIP(hipGetLastError());
+    if (int rc = et_dbg_dump("backward", p.dbg, G, st)) return rc;
     hipLaunchKernelGGL(egnn_grad_reduce_kernel, dim3((unsigned)((p.blob_floats + 255) / 256)), dim3(256), 0, st, p.gpart,
                        G, p.blob_floats, grad_blob);
     NBX_HIP(hipGetLastError());

@@ -232,9 +232,10 @@ class EGNNMultiChannel(nn.Module):
         position of every element of their flattened concatenation -- persist_blob's layout traced
         once with element ids, so a training step packs the blob with one scatter and maps the blob
         gradient back onto the parameters with one gather."""
-        key = (device, tuple((tuple(q.shape), q.dtype) for q in self.parameters()))
-        if getattr(self, "_tlayout", None) is not None and self._tlayout[0] == key:
-            return self._tlayout[1:]
+        device = torch.device(device)
+        cached = getattr(self, "_tlayout", None)
+        if cached is not None and cached[0] == device:   # (reset by _apply: .to() / .float() / ...)
+            return cached[1:]
         params = list(self.parameters())
         ids, base = {}, 1
         for q in params:
@@ -254,8 +255,12 @@ class EGNNMultiChannel(nn.Module):
                 raise RuntimeError("persist blob holds part of a parameter")
             off += q.numel()
         idx = torch.cat([sl for _, sl in used]).to(device)
-        self._tlayout = (key, [q for q, _ in used], idx, int(tagged.numel()))
+        self._tlayout = (device, [q for q, _ in used], idx, int(tagged.numel()))
         return self._tlayout[1:]
+
+    def _apply(self, fn, *args, **kwargs):
+        self._tlayout = None   # parameters may be replaced
+        return super()._apply(fn, *args, **kwargs)
 
     def _train_weights(self, blob):
         """The weight struct of the training entry points: the model's flags and the blob."""

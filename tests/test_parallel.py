@@ -208,7 +208,7 @@ def _grad_worker(rank, world, port, q):
         sl = slice(8 * rank, 8 * rank + 8)
         torch.nn.functional.mse_loss(lin(x[sl]), y[sl]).backward()
         P.allreduce_gradients(lin.parameters(), bucket_bytes=100)   # several buckets
-        q.put((rank, [p.grad.clone() for p in lin.parameters()]))
+        q.put((rank, [p.grad.numpy().copy() for p in lin.parameters()]))   # by value: the sender exits
     finally:
         dist.destroy_process_group()
 
@@ -234,4 +234,4 @@ def test_allreduce_gradients_equals_full_batch_mean_over_gloo():
     torch.nn.functional.mse_loss(lin(x), y).backward()
     for r in range(world):
         for g, p in zip(res[r], lin.parameters()):
-            torch.testing.assert_close(g, p.grad, rtol=1e-12, atol=1e-14)
+            torch.testing.assert_close(torch.from_numpy(g), p.grad, rtol=1e-12, atol=1e-14)
