@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 9
+ABI_VERSION = 8
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
@@ -25,7 +25,7 @@ class SegnnLayer(ctypes.Structure):
         "node_pre_s_img", "node_pre_v_img", "node_pre_s_img_x3", "node_pre_v_img_x3", "msg1_amf", "msg1_bias", "msg2_img", "msg2_img_x3", "msg2_bias",
         "upd1_img", "upd1_img_x3", "upd1_bias", "upd2_img", "upd2_bias",
         "msg_bn_weight", "msg_bn_bias", "msg_bn_running_mean", "msg_bn_running_var",
-        "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var", "msg2_img16_x3")]
+        "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var")]
 
 
 # nbx_allreduce_fn: int (*)(double* buf, int64_t count, void* stream, void* ctx)

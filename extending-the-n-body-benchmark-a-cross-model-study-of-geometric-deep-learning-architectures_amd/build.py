@@ -27,8 +27,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
 # kernel's edge combination) runs beside MFMAs, where packed fp32 VALU costs extra cycles; with
 # SLP vectorisation off these files run 1.8 % more steps/s (measured, C2).
 # NBX_FILE_FLAGS="file.hip:-flag,-flag;..." adds more (A/B builds).
-FILE_FLAGS = {"segnn.hip": ["-fno-slp-vectorize"], "msg_pre.hip": ["-fno-slp-vectorize"],
-              "msg_fused.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"segnn.hip": ["-fno-slp-vectorize"], "msg_pre.hip": ["-fno-slp-vectorize"]}
 for _item in filter(None, os.environ.get("NBX_FILE_FLAGS", "").split(";")):
     _f, _fl = _item.split(":", 1)
     FILE_FLAGS.setdefault(_f, []).extend(_fl.split(","))

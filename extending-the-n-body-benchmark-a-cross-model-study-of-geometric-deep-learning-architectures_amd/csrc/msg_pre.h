@@ -57,35 +57,4 @@ struct MsgPreProb {
 inline int msg_pre_group(int N) { return (N >= 2 && N <= 16) ? (16 / N) * N : 0; }
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus = 256);
 
-// Whole message path of one layer in one kernel (msg_fused.hip): message_layer_1 (node GEMM +
-// edge combination + gate) AND message_layer_2 (+ gate, aggregation over each destination's
-// edges, message-BatchNorm sums), so M1 never leaves the chip.  A block owns one node group
-// (NG = msg_pre_group(N) nodes = whole systems, NG * G <= 64 edge rows) and walks the M input
-// channels in 32-channel slices: node GEMM of the slice (both 16-channel chunks) -> LDS,
-// edge combination -> the slice of M1 as bf16x3 MFMA A fragments in LDS, then message_layer_2's
-// K-slice accumulated into per-wave register tiles that persist over the slices.  Weights are
-// read from L2 in MFMA fragment order (node_pre x3 images, the CW = 16 msg2 x3 image); mul = 96,
-// 2 <= N <= 5, fully-connected graphs, atomic BatchNorm sums.
-struct MsgFusedProb {
-    const float* X;       // [4][V][M] (pre-BN values of the previous layer)
-    const void* Simg;     // node_pre_s bf16x3 image (CW = 16)
-    const void* Vimg;     // node_pre_v bf16x3 image (CW = 16)
-    const void* W2;       // msg2 bf16x3 image with CW = 16 chunks: sub-tiles s (2M), gate (2M), t (M), v (M)
-    const float* EG;      // [V*G][8]
-    const float* amf;     // [2][3M]
-    const float* bias1;   // [2M] message_layer_1 (s, gate)
-    const float* bias2;   // [2M] message_layer_2 (s, gate)
-    const float* NA;      // [V][4]
-    const float* xcoef;   // pending feature BN [sc_s | sc_v | sh] or null (identity)
-    BnSrc xbn;            // as MsgPreProb::xbn
-    float* AGG;           // [4][V][M] aggregated messages (pre message-BN)
-    float* AD;            // [V][M] a_v . na
-    double* bn_sums;      // [3][M] message-BN sums (fp64 atomics)
-    long V;
-    int N, G, M, NG;
-    unsigned long long* dbg;  // optional per-wave phase clocks (tuning only)
-};
-bool msg_fused_supported(int M, int N);
-int msg_fused_launch(MsgFusedProb& p, hipStream_t st);
-
 }  // namespace nbx

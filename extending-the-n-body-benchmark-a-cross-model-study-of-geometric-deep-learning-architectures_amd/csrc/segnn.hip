@@ -833,51 +833,6 @@ int run_msg_pre(nbx::MsgPreProb& p, hipStream_t st, KernelTiming* tm) {
     return NBX_OK;
 }
 
-// fused message path (msg_fused.hip): both message TPs in one launch; NBX_MSG_FUSED=0 keeps the
-// two-kernel path (A/B only)
-bool msg_fused_enabled() {
-    static const bool on = !(getenv("NBX_MSG_FUSED") && getenv("NBX_MSG_FUSED")[0] == '0');
-    return on;
-}
-
-int run_msg_fused(nbx::MsgFusedProb& p, hipStream_t st, KernelTiming* tm) {
-    static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
-    if (debug) {
-        p.dbg = tp_dbg_buf(st);
-        if (int rc = nbx::msg_fused_launch(p, st)) return rc;
-        const int blocks = (int)((p.V + p.NG - 1) / p.NG), n = blocks * 8;
-        std::vector<unsigned long long> h((size_t)n * 4);
-        NBX_HIP(hipStreamSynchronize(st));
-        NBX_HIP(hipMemcpy(h.data(), p.dbg, h.size() * 8, hipMemcpyDeviceToHost));
-        double s[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-        for (int i = 0; i < n; ++i)
-            for (int k = 0; k < 4; ++k) s[(i & 7) < 6 ? 0 : 1][k] += (double)h[(size_t)i * 4 + k];
-        const double nv = blocks * 6.0, ns = blocks * 2.0;
-        fprintf(stderr,
-                "tp_debug msg_fused blocks=%d vector waves: node=%.0f comb=%.0f mma=%.0f bar=%.0f | scalar waves: "
-                "node=%.0f comb=%.0f bar=%.0f (avg clocks per wave)\n",
-                blocks, s[0][0] / nv, s[0][1] / nv, s[0][2] / nv, s[0][3] / nv, s[1][0] / ns, s[1][1] / ns,
-                s[1][3] / ns);
-        return NBX_OK;
-    }
-    if (!tm) return nbx::msg_fused_launch(p, st);
-    hipEvent_t a, b;
-    NBX_HIP(hipEventCreate(&a));
-    NBX_HIP(hipEventCreate(&b));
-    tm->ev.push_back(a);
-    tm->ev.push_back(b);
-    nbx::armed_events() = {a, b};   // the launch below records the kernel's own begin / end
-    if (int rc = nbx::msg_fused_launch(p, st)) return rc;
-    NBX_HIP(nbx::disarm_events(st));
-    // reported as the message kind: node GEMM (2 * 4V * M * 6M) + message_layer_2
-    // (2 * V*G * (2M * 3M - M * M + 3 * M * M): the t part contracts only m_s)
-    const double V = (double)p.V, M = p.M, E = V * p.G;
-    tm->kind.push_back(nbx::TP_MSG);
-    tm->flops[nbx::TP_MSG] += 2.0 * 4.0 * V * M * 6.0 * M + 2.0 * E * (5.0 * M * M + 3.0 * M * M);
-    tm->launches[nbx::TP_MSG] += 1;
-    return NBX_OK;
-}
-
 template <int NS, int NV, int EPI, int CG>
 int run_tp16_pair(nbx::TpProb& p0, nbx::TpProb& p1, hipStream_t st, KernelTiming* tm) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
@@ -997,26 +952,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             NBX_LAUNCH_CHECK("bn_apply");
             xprev = nullptr;
         }
-        const bool msg_all = bn_atomic && msg_fused_enabled() && x3_enabled() && L.node_pre_s_img_x3 &&
-                             L.node_pre_v_img_x3 && L.msg2_img16_x3 && nbx::msg_fused_supported(M, (int)N);
-        if (msg_all) {
-            // message_layer_1 + message_layer_2 + aggregation + message-BN sums in one kernel
-            nbx::MsgFusedProb mf;
-            memset(&mf, 0, sizeof(mf));
-            mf.X = ws.X; mf.Simg = L.node_pre_s_img_x3; mf.Vimg = L.node_pre_v_img_x3; mf.W2 = L.msg2_img16_x3;
-            mf.EG = ws.EG; mf.amf = L.msg1_amf; mf.bias1 = L.msg1_bias; mf.bias2 = L.msg2_bias; mf.NA = ws.NA;
-            mf.xcoef = xprev;
-            if (l > 0) {
-                const nbx_segnn_layer& Lp = w->layers[l - 1];
-                mf.xbn = nbx::BnSrc{sums_of(l - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias, Lp.feat_bn_running_mean,
-                                    Lp.feat_bn_running_var, ws.coef_feat, cnt_nodes, w->bn_eps, w->bn_momentum,
-                                    w->training, 1};
-            }
-            mf.AGG = ws.AGG; mf.AD = ws.AD; mf.bn_sums = sums_of(l, 0);
-            mf.V = V; mf.N = (int)N; mf.G = (int)d.G; mf.M = M; mf.NG = nbx::msg_pre_group((int)N);
-            if (int rc = run_msg_fused(mf, st, tm)) return rc;
-            if (int rc = sync_bn(sums_of(l, 0))) return rc;
-        } else if (fused_msg) {
+        if (fused_msg) {
             // message_layer_1: node precomputation + edge combination + gate in one kernel
             nbx::MsgPreProb mp;
             memset(&mp, 0, sizeof(mp));
@@ -1067,7 +1003,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             NBX_LAUNCH_CHECK("msg1");
         }
         int wpc_msg = 1, cw_msg = 16;
-        if (!msg_all) {
+        {
             // message_layer_2 + gate + aggregation + message-BN partial sums
             nbx::TpProb p = tp_base((int)Ep, d);
             p.As = ws.M1S; p.lda_s = 2 * M; p.B = L.msg2_img;

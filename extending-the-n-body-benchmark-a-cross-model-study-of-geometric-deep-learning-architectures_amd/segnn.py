@@ -304,8 +304,6 @@ class SEGNN(nn.Module):
                 if stem == "msg2":
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 32, c32)
                     out[pre + stem + "_img_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c32)
-                    # CW = 16 chunks for the fused message kernel (msg_fused.hip)
-                    out[pre + stem + "_img16_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c16, 16)
                 else:
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 16, c16)
                     if stem == "upd1":

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 9
+#define NBX_ABI_VERSION 8
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -159,10 +159,6 @@ typedef struct nbx_segnn_layer {
     const float* feat_bn_bias;
     float* feat_bn_running_mean;
     float* feat_bn_running_var;
-    /* ABI 9: msg2's operand as a bf16x3 image with CW = 16 chunks (sub-tiles s, gate, t, v; the
-     * layout of upd1_img_x3), read by the fused message kernel (message_layer_1 + message_layer_2
-     * in one launch, mul 96, 2 <= N <= 5), or NULL (two-kernel message path) */
-    const void* msg2_img16_x3;
 } nbx_segnn_layer;
 
 typedef struct nbx_segnn_weights {
