@@ -20,6 +20,7 @@
 // -> two SO(2) GEMMs -> S2 activation + alpha kernel -> two GEMMs -> per-system node kernel
 // (segment softmax over the N-1 incoming edges, inverse rotation, sum, projection, residual, norm,
 // the whole FFN and the next norm), so node features make one HBM round trip per block.
+#include <cstdlib>
 #include <cstring>
 
 #include "lin.h"
@@ -466,6 +467,197 @@ __global__ __launch_bounds__(64) void eqv2_node_kernel(const NodeArgs A) {
     }
 }
 
+// NODE_BLOCK on NPW nodes per wave (lane = channel): the attention aggregation runs node by
+// node, then proj, the FFN's gate / so3_linear_1 and so3_linear_2 walk their weights once for
+// all NPW nodes (each weight load feeds NPW nodes' FMAs, so the chains of dependent L2 weight
+// reads that bound the one-node kernel are NPW times shorter).  Per node the arithmetic and its
+// order are those of eqv2_node_kernel<NODE_BLOCK>.  Needs KV <= 16.
+template <int NPW>
+__global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, int64_t V) {
+    __shared__ float s_alpha[64 * 8];
+    __shared__ float s_ag[NPW][9 * 16];
+    __shared__ float s_x[NPW][9 * 64];
+    __shared__ float s_gt[GF * 9], s_gf[GF * 9];
+    const int lane = threadIdx.x;
+    const int C = A.C, F = A.F, N = A.N, deg = N - 1, KV = A.nh * A.nv;
+    const int64_t node0 = (int64_t)blockIdx.x * NPW;
+    for (int i = lane; i < GF * 9; i += 64) {
+        s_gt[i] = A.gto[i];
+        s_gf[i] = A.gfrom[i];
+    }
+    const int c = lane < C ? lane : 0;
+    const bool on = lane < C;
+    // ---- attention aggregation, node by node (softmax over the N-1 incoming edges per head,
+    // values * alpha rotated back and summed) -> s_ag[n]
+#pragma unroll
+    for (int n = 0; n < NPW; ++n) {
+        const int64_t node = node0 + n;
+        __syncthreads();   // s_alpha of the previous node is consumed
+        if (node >= V) continue;
+        const int64_t sys = node / N;
+        const int t = (int)(node - sys * N);
+        auto edge_of = [&](int q) -> int64_t {
+            const int s = q < t ? q : q + 1;
+            return sys * N * deg + (int64_t)s * deg + (t < s ? t : t - 1);
+        };
+        if (lane < A.nh) {
+            float mx = -INFINITY;
+            for (int q = 0; q < deg; ++q) mx = fmaxf(mx, A.L[edge_of(q) * A.nh + lane]);
+            float sum = 0.f;
+            for (int q = 0; q < deg; ++q) {
+                const float ex = __expf(A.L[edge_of(q) * A.nh + lane] - mx);
+                s_alpha[q * 8 + lane] = ex;
+                sum += ex;
+            }
+            const float inv = 1.0f / (sum + 1e-16f);
+            for (int q = 0; q < deg; ++q) s_alpha[q * 8 + lane] *= inv;
+        }
+        __syncthreads();
+        const int G = 64 / KV, k = lane % KV, qg = lane / KV, hd = k / A.nv;
+        float agg[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int q = qg; q < deg; q += G) {
+            const int64_t e = edge_of(q);
+            const float a = s_alpha[q * 8 + hd];
+            const float* v0 = A.V0 + e * A.ldv0 + k;
+            const float* vr = A.V1 + 2 * e * A.ldv1 + k;
+            const float* vi = vr + A.ldv1;
+            const float m0 = v0[0] * a, m1 = v0[KV] * a, m2 = v0[2 * KV] * a;
+            const float re1 = (vr[0] - vi[2 * KV]) * a, re2 = (vr[KV] - vi[3 * KV]) * a;
+            const float im1 = (vi[0] + vr[2 * KV]) * a, im2 = (vi[KV] + vr[3 * KV]) * a;
+            const float* D = A.rot + e * ROT;
+            agg[0] += m0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) agg[1 + j] += D[j] * im1 + D[3 + j] * m1 + D[6 + j] * re1;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) agg[4 + j] += kRescale2 * (D[9 + j] * im2 + D[14 + j] * m2 + D[19 + j] * re2);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+            for (int o = KV; o < 64; o <<= 1) agg[i] += __shfl_xor(agg[i], o);
+        if (lane < KV)
+#pragma unroll
+            for (int i = 0; i < 9; ++i) s_ag[n][i * KV + lane] = agg[i];
+    }
+    __syncthreads();
+    // ---- proj (SO3_LinearV2 nh nv -> C), residual, norm_2 -> s_x[n]
+    float x[NPW][9];
+    {
+        float y[NPW][9];
+#pragma unroll
+        for (int n = 0; n < NPW; ++n)
+#pragma unroll
+            for (int i = 0; i < 9; ++i) y[n][i] = 0.f;
+        for (int kk = 0; kk < KV; ++kk) {
+            const float w0 = A.proj_t[kk * C + c], w1 = A.proj_t[(KV + kk) * C + c], w2 = A.proj_t[(2 * KV + kk) * C + c];
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) {
+                y[n][0] += s_ag[n][kk] * w0;
+#pragma unroll
+                for (int i = 1; i < 4; ++i) y[n][i] += s_ag[n][i * KV + kk] * w1;
+#pragma unroll
+                for (int i = 4; i < 9; ++i) y[n][i] += s_ag[n][i * KV + kk] * w2;
+            }
+        }
+        const float pb = A.proj_b[c];
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            const int64_t node = node0 + n < V ? node0 + n : V - 1;
+            y[n][0] += pb;
+            const float* xo = A.X + node * 9 * C + c;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) x[n][i] = xo[i * C] + y[n][i];
+            float xn[9];
+            rms_norm(x[n], xn, A.norm2_w, A.norm2_b, c, on, C);
+            if (on)
+#pragma unroll
+                for (int i = 0; i < 9; ++i) s_x[n][i * C + c] = xn[i];
+        }
+    }
+    __syncthreads();
+    // ---- FFN: gating + so3_linear_1, S2 activation on the grid -> s_x[n] (reused), so3_linear_2
+    {
+        const bool fon = lane < F;
+        const int f = fon ? lane : 0;
+        float gate[NPW], h[NPW][9];
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            gate[n] = A.gate_b[f];
+            h[n][0] = A.lin1_b[f];
+#pragma unroll
+            for (int i = 1; i < 9; ++i) h[n][i] = 0.f;
+        }
+        for (int cc = 0; cc < C; ++cc) {
+            const float wg = A.gate_t[cc * F + f], w0 = A.lin1_t[cc * F + f], w1 = A.lin1_t[(C + cc) * F + f],
+                        w2 = A.lin1_t[(2 * C + cc) * F + f];
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) {
+                gate[n] += s_x[n][cc] * wg;
+                h[n][0] += s_x[n][cc] * w0;
+#pragma unroll
+                for (int i = 1; i < 4; ++i) h[n][i] += s_x[n][i * C + cc] * w1;
+#pragma unroll
+                for (int i = 4; i < 9; ++i) h[n][i] += s_x[n][i * C + cc] * w2;
+            }
+        }
+        __syncthreads();   // s_x is rewritten with the activation below
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            float o[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int p = 0; p < GF; ++p) {
+                float gv = 0.f;
+#pragma unroll
+                for (int i = 0; i < 9; ++i) gv += s_gt[p * 9 + i] * h[n][i];
+                const float sg = silu(gv);
+#pragma unroll
+                for (int i = 0; i < 9; ++i) o[i] += s_gf[p * 9 + i] * sg;
+            }
+            o[0] = silu(gate[n]);
+            if (fon)
+#pragma unroll
+                for (int i = 0; i < 9; ++i) s_x[n][i * F + f] = o[i];
+        }
+    }
+    __syncthreads();
+    {
+        float h2[NPW][9];
+        const float b2 = A.lin2_b[c];
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            h2[n][0] = b2;
+#pragma unroll
+            for (int i = 1; i < 9; ++i) h2[n][i] = 0.f;
+        }
+        for (int ff = 0; ff < F; ++ff) {
+            const float w0 = A.lin2_t[ff * C + c], w1 = A.lin2_t[(F + ff) * C + c], w2 = A.lin2_t[(2 * F + ff) * C + c];
+#pragma unroll
+            for (int n = 0; n < NPW; ++n) {
+                h2[n][0] += s_x[n][ff] * w0;
+#pragma unroll
+                for (int i = 1; i < 4; ++i) h2[n][i] += s_x[n][i * F + ff] * w1;
+#pragma unroll
+                for (int i = 4; i < 9; ++i) h2[n][i] += s_x[n][i * F + ff] * w2;
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < NPW; ++n) {
+            const int64_t node = node0 + n;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) x[n][i] += h2[n][i];
+            float xn[9];
+            rms_norm(x[n], xn, A.nnorm_w, A.nnorm_b, c, on, C);
+            if (node < V && on) {
+                float* xw = A.X + node * 9 * C + c;
+                float* xnw = A.XN + node * 9 * C + c;
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    xw[i * C] = x[n][i];
+                    xnw[i * C] = xn[i];
+                }
+            }
+        }
+    }
+}
+
 struct EqWs {
     float *rot, *H2, *A0, *A1, *Y0, *Y1, *Z0, *Z1, *L, *V0, *V1, *X, *XN, *out;
     int* zn;
@@ -690,7 +882,14 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         a.nnorm_w = last ? w->norm_w : w->blocks[l + 1].norm1_w;
         a.nnorm_b = last ? w->norm_b : w->blocks[l + 1].norm1_b;
         TScope ts(6, st, node_fl, node_by);
-        hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)(B * N)), dim3(64), 0, st, a);
+        // two nodes per wave (measured at C4: 98.7 us against 100.4-101.1 us for one node per wave and
+        // 139 us for four, whose 158 VGPRs cut the occupancy); NBX_EQ_NPW=1 keeps the one-node kernel
+        static const int npw = getenv("NBX_EQ_NPW") ? atoi(getenv("NBX_EQ_NPW")) : 2;
+        const int64_t V = B * N;
+        if (npw == 2 && w->num_heads * w->value_channels <= 16)
+            hipLaunchKernelGGL(eqv2_node_block_kernel<2>, dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
+        else
+            hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)V), dim3(64), 0, st, a);
         NBX_LAUNCH_CHECK("eqv2 node block");
     }
     if (int rc = attention_edges(w, w->force, ws, B, N, st)) return rc;

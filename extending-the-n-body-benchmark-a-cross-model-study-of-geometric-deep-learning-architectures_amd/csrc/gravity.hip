@@ -9,24 +9,45 @@
 
 namespace {
 
+// r^-1/2 for r2 > 0: the hardware v_rsq_f64 estimate refined by one Newton step,
+// y1 = y0 + y0/2 (1 - r2 y0^2) (4 fp64 ops; the estimate's relative error squares to the ulp
+// level).  OCML's rsqrt adds special-case classification and a second correction: about 12 ops,
+// 40 % of the pair interaction's instructions.
+__device__ inline double rsqrt_nr(double r2) {
+    const double y0 = __builtin_amdgcn_rsq(r2);
+    const double e = fma(-r2 * y0, y0, 1.0);
+    return fma(0.5 * y0, e, y0);
+}
+
 // a_i = G * sum_j ((x_j - x_i) * r^-3) * m_j, r^2 = |x_j - x_i|^2 + eps^2 (synthetic_sim.py:318-340).
 // Bodies sit in LDS as (x, y, z, m) double4 (two broadcast ds_read_b128 per partner);
-// r^-3 = rsqrt(r^2)^3 with the correctly-rounded-to-1-ulp OCML fp64 rsqrt instead of a
-// sqrt + divide (the reference's pow(r^2, -1.5) is itself ulp-different from both).
-__device__ inline void accel_from_lds(const double4* __restrict__ sp, int N, double xi, double yi, double zi,
-                                      double G, double soft2, double& ax, double& ay, double& az) {
-    double sx = 0.0, sy = 0.0, sz = 0.0;
+// r^-3 = rsqrt(r^2)^3 instead of a sqrt + divide (the reference's pow(r^2, -1.5) is itself
+// ulp-different from both).
+template <bool SOFT>
+__device__ inline void accel_sum(const double4* __restrict__ sp, int N, double xi, double yi, double zi, double soft2,
+                                 double& sx, double& sy, double& sz) {
 #pragma unroll 4
     for (int j = 0; j < N; ++j) {
         const double4 p = sp[j];
         const double dx = p.x - xi, dy = p.y - yi, dz = p.z - zi;
         const double r2 = dx * dx + dy * dy + dz * dz + soft2;
-        const double ri = rsqrt(r2);
-        const double w = r2 > 0.0 ? (ri * ri * ri) * p.w : 0.0;
+        const double ri = rsqrt_nr(r2);
+        // softened (eps > 0): r2 > 0 for every pair, the self term is 0 * finite; unsoftened: the
+        // self term (r2 = 0) is skipped
+        const double w = SOFT ? (ri * ri * ri) * p.w : (r2 > 0.0 ? (ri * ri * ri) * p.w : 0.0);
         sx += dx * w;
         sy += dy * w;
         sz += dz * w;
     }
+}
+
+__device__ inline void accel_from_lds(const double4* __restrict__ sp, int N, double xi, double yi, double zi,
+                                      double G, double soft2, double& ax, double& ay, double& az) {
+    double sx = 0.0, sy = 0.0, sz = 0.0;
+    if (soft2 > 0.0)
+        accel_sum<true>(sp, N, xi, yi, zi, soft2, sx, sy, sz);
+    else
+        accel_sum<false>(sp, N, xi, yi, zi, soft2, sx, sy, sz);
     ax = G * sx;
     ay = G * sy;
     az = G * sz;
