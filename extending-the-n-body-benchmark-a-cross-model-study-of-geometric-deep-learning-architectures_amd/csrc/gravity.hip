@@ -31,7 +31,7 @@ __device__ inline void accel_sum(const double4* __restrict__ sp, int N, double x
     for (int j = 0; j < N; ++j) {
         const double4 p = sp[j];
         const double dx = p.x - xi, dy = p.y - yi, dz = p.z - zi;
-        const double r2 = dx * dx + dy * dy + dz * dz + soft2;
+        const double r2 = fma(dz, dz, fma(dy, dy, fma(dx, dx, soft2)));   // 3 fp64 ops
         const double ri = rsqrt_nr(r2);
         // softened (eps > 0): r2 > 0 for every pair, the self term is 0 * finite; unsoftened: the
         // self term (r2 = 0) is skipped
