@@ -102,6 +102,16 @@ def bench_segnn(a, rank, world, device, P):
     B, N = a.batch or BATCH, NBODY
     torch.manual_seed(0)
     model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS, lmax_h=1).to(device).float().train()
+    # BatchNorm statistics: "batch" = per-rank batch statistics (the reference's
+    # train-mode rollout on each rank's own B systems), "sync" = batch statistics over every rank's
+    # systems (12 RCCL all-reduces of [3][96] fp64 sums per step), "running" = running statistics
+    bn_desc = {"batch": "batch statistics per rank (reference train-mode rollout)",
+               "sync": "batch statistics over all ranks (SyncBN: 12 all-reduces per step)",
+               "running": "running statistics (no batch reduction)"}[a.bn_mode]
+    if a.bn_mode == "running":
+        model.bn_mode = "running"
+    elif a.bn_mode == "sync" and world > 1:
+        model.enable_sync_batchnorm()
     loc, vel, mass = initial_states(B, N, rank * B)
     loc_d = torch.tensor(loc, dtype=torch.float32, device=device)
     vel_d = torch.tensor(vel, dtype=torch.float32, device=device)
@@ -175,7 +185,7 @@ def bench_segnn(a, rank, world, device, P):
         "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights)",
         "config": {"workload": "C2: SEGNN lmax_h=1 hidden=192 layers=6, N=5, batch=1024 per GPU, self-feed rollout",
                    "model": "SEGNN", "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}",
-                   "bn_mode": "batch statistics per rank (reference train-mode rollout)"},
+                   "bn_mode": bn_desc},
         "trajectory_steps_per_s": round(value * B, 1),
         "survey_formulation_tflops": round(value * SURVEY_GFLOP_PER_STEP / 1e3, 3),
         "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": round(achieved_tflops, 3),
@@ -625,6 +635,8 @@ def main():
                     choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "eqv2", "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--bn-mode", default="batch", choices=["batch", "sync", "running"],
+                    help="SEGNN BatchNorm statistics: per-rank batch (default), all-rank SyncBN, running")
     a = ap.parse_args()
     defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5), "eqv2": (20, 2),
                 "gravity": (1000, 100)}

@@ -141,6 +141,11 @@ class SEGNN(nn.Module):
         self._warned_dtype = False
         self._bn_group = None        # SyncBN process group (enable_sync_batchnorm)
         self._bn_hook = None
+        # BatchNorm statistics of the native forward / rollout (SURVEY §8(e) bn_mode): None follows
+        # self.training like the reference module (train() -> batch statistics, the reference's
+        # rollout semantics, infer_self_feed.py never calls eval()); "batch" / "running" force
+        # batch statistics (running stats updated) / the running statistics
+        self.bn_mode = None
 
     # ------------------------------------------------------------ reference API
     def get_model_size(self):
@@ -354,11 +359,17 @@ class SEGNN(nn.Module):
         self._packed = (self._param_version(), W, P, shadows)
         return W
 
+    def _bn_batch(self):
+        """True when the native path uses (and updates) batch statistics (bn_mode, else self.training)."""
+        if self.bn_mode not in (None, "batch", "running"):
+            raise ValueError(f"bn_mode must be None, 'batch' or 'running' (got {self.bn_mode!r})")
+        return self.training if self.bn_mode is None else self.bn_mode == "batch"
+
     def _weights(self, device):
         if self._packed is None or self._packed[0] != self._param_version():
             self.pack_weights(device)
         W = self._packed[1]
-        W.training = 1 if self.training else 0
+        W.training = 1 if self._bn_batch() else 0
         return W
 
     # ------------------------------------------------------------ SyncBN (multi-GPU)
@@ -392,7 +403,7 @@ class SEGNN(nn.Module):
 
     def _arm_sync(self, W, B, device):
         """Point the weight struct's hook at the SyncBN callback (or clear it) for one call."""
-        if self._bn_group is None or not self.training:
+        if self._bn_group is None or not self._bn_batch():
             W.bn_allreduce = _lib.ALLREDUCE_FN()
             W.bn_global_batch = 0
             return
@@ -409,7 +420,7 @@ class SEGNN(nn.Module):
             sh.copy_(buf)
 
     def _bn_sync_out(self):
-        if self.training:
+        if self._bn_batch():
             for buf, sh in self._packed[3]:
                 buf.copy_(sh)
 
@@ -495,7 +506,7 @@ class SEGNN(nn.Module):
                 _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
                 "nbx_segnn_rollout")
         else:
-            if self._bn_group is not None and self.training:
+            if self._bn_group is not None and self._bn_batch():
                 raise NotImplementedError("SyncBN rollouts need fully-connected graphs")
             _lib.check(_lib.lib().nbx_segnn_rollout_knn(
                 W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames, flags,

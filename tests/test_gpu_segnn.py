@@ -389,3 +389,27 @@ def test_forward_mul128_repeats_and_matches_oracle(hip_device):
     Bs = 24
     ref, _ = oracle_forward(model, params_of(model), pos[:Bs * N], vel[:Bs * N], mass[:Bs * N], Bs, N, False)
     assert_close_cols(gpu_forward(model, pos[:Bs * N], vel[:Bs * N], mass[:Bs * N], Bs, N, hip_device), ref)
+
+
+def test_bn_mode_overrides_module_mode(hip_device):
+    """SEGNN.bn_mode: "running" on a train() module is the eval() forward and leaves the
+    running statistics alone; "batch" on an eval() module is the train() forward."""
+    B, N = 32, 5
+    pos, vel, mass = states(B, N, seed=7)
+    model = make_model(64, 2, hip_device)
+    before = {k: v.clone() for k, v in model.state_dict().items() if "running" in k}
+    ref_eval = gpu_forward(model.eval(), pos, vel, mass, B, N, hip_device)
+    model.train()
+    model.bn_mode = "running"
+    got = gpu_forward(model, pos, vel, mass, B, N, hip_device)
+    np.testing.assert_array_equal(got, ref_eval)
+    for k, v in model.state_dict().items():
+        if "running" in k:
+            assert torch.equal(v, before[k]), k
+    model.bn_mode = None
+    ref_train = gpu_forward(model.train(), pos, vel, mass, B, N, hip_device)
+    for k, v in before.items():   # restore the running statistics the train-mode forward updated
+        model.state_dict()[k].copy_(v)
+    model.eval()
+    model.bn_mode = "batch"
+    np.testing.assert_allclose(gpu_forward(model, pos, vel, mass, B, N, hip_device), ref_train, rtol=1e-6, atol=1e-7)

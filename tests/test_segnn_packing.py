@@ -159,3 +159,19 @@ def test_state_dict_layout_matches_oracle():
     sd = {k: tuple(v.shape) for k, v in model.state_dict().items() if "output_mask" not in k}
     assert sd == om.param_shapes()
     assert sum(p.numel() for p in model.parameters()) == 1_947_552
+
+
+def test_bn_mode_switch():
+    """SEGNN.bn_mode (SURVEY §8(e) bn_mode={batch,running}): None follows train()/eval() like the
+    reference module; "batch" / "running" override it; anything else is rejected."""
+    import pytest
+    import nbody_amd.segnn as S
+    m = S.SEGNN(hidden_features=16, num_layers=1)
+    assert m.train()._bn_batch() and not m.eval()._bn_batch()
+    m.bn_mode = "batch"
+    assert m.eval()._bn_batch()
+    m.bn_mode = "running"
+    assert not m.train()._bn_batch()
+    m.bn_mode = "sync"
+    with pytest.raises(ValueError):
+        m._bn_batch()
