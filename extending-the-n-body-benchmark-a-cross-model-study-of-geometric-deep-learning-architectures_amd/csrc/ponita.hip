@@ -369,6 +369,47 @@ __device__ inline float gelu_nb(float x) {
     return 0.5f * x * (u >= 0.f ? 2.0f - ec : ec);
 }
 
+// kernel-basis MLP layer 1 (ponita_pg.py:92-98 basis_fn[1] + GELU, K = 16 polynomial features):
+// Y[r, c] = GELU(sum_k P16[r, k] W[c, k] + b[c]).  K is tiny, so this is a streaming write of the
+// [E O][C] hidden activation (839 MB at C3), not a GEMM: thread = (row, 4 channels) with its 64
+// weights and 4 biases in registers for every row it visits (persistent grid), the row's 16
+// features read as four float4 (shared by the row's C / 4 lanes through L1), one float4 store.
+// (The generic lin_kernel ran it at 2.1 TB/s; OCML's branchy erff made this kernel VALU-bound.)  W: [C][32] (basis1_t), features 14-31 zero-padded.
+__global__ __launch_bounds__(256) void po_basis1_kernel(const float* __restrict__ P16, const float* __restrict__ W,
+                                                        const float* __restrict__ b, int64_t rows, int C,
+                                                        float* __restrict__ Y) {
+    const int CQ = C >> 2;
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int q = (int)(t % CQ);
+    const int64_t r0 = t / CQ, rstride = (int64_t)gridDim.x * blockDim.x / CQ;
+    float w[4][16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            const float4 v = *reinterpret_cast<const float4*>(W + (size_t)(4 * q + j) * 32 + 4 * k4);
+            w[j][4 * k4] = v.x; w[j][4 * k4 + 1] = v.y; w[j][4 * k4 + 2] = v.z; w[j][4 * k4 + 3] = v.w;
+        }
+    const float4 bb = *reinterpret_cast<const float4*>(b + 4 * q);
+    for (int64_t r = r0; r < rows; r += rstride) {
+        float x[16];
+        const float4* pr = reinterpret_cast<const float4*>(P16 + r * 16);
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            const float4 v = pr[k4];
+            x[4 * k4] = v.x; x[4 * k4 + 1] = v.y; x[4 * k4 + 2] = v.z; x[4 * k4 + 3] = v.w;
+        }
+        float y[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) y[j] = fmaf(x[k], w[j][k], y[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = gelu_nb(y[j]);   // branch-free exact-erf GELU (3.8e-7 max error)
+        *reinterpret_cast<float4*>(Y + r * C + 4 * q) = float4{y[0], y[1], y[2], y[3]};
+    }
+}
+
 struct FfnProb {
     const float* XN;      // [rows][C] LayerNorm output (GEMM 1 input)
     float* X;             // [rows][C] residual in, layer output (in place)
@@ -719,8 +760,15 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
     NBX_LAUNCH_CHECK("ponita prep");
     {
         LinProb p = nbx::lin_dense(ws.P16, 16, 16, (int)d.R, w->basis1_t, 32, C, w->basis1_b, ws.B1H1, C);
-        if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * 14 * C, Ev * f4 * (16 + C),
-                                [&] { return lin_auto<nbx::ACT_GELU>(p, st); }))
+        // layer 1 as a streaming kernel (NBX_PO_BASIS1=0: the generic GEMM, A/B only)
+        static const bool b1s = !(getenv("NBX_PO_BASIS1") && getenv("NBX_PO_BASIS1")[0] == '0');
+        if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * 14 * C, Ev * f4 * (16 + C), [&] {
+                if (!b1s) return lin_auto<nbx::ACT_GELU>(p, st);
+                const int64_t threads = std::min<int64_t>(d.R * (C / 4), (int64_t)256 * 8 * 256);
+                hipLaunchKernelGGL(po_basis1_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                                   ws.P16, w->basis1_t, w->basis1_b, d.R, C, ws.B1H1);
+                return (int)NBX_OK;
+            }))
             return rc;
         LinProb q = nbx::lin_dense(ws.B1H1, C, C, (int)d.R, w->basis2_t, kp(C), Bk, w->basis2_b, ws.KB, Bk);
         q.Wx3 = w->basis2_img_x3;
