@@ -212,6 +212,60 @@ def test_gpu_training_step_c1_shape(hip_device):
     assert any(not torch.equal(p0, p1) for p0, p1 in zip(before, model.parameters()))
 
 
+@pytest.mark.gpu
+def test_gpu_training_step_hip_graph_matches_eager(hip_device):
+    """bench.py's training line replays the whole step (forward, backward, clip, fused AdamW with
+    a device-resident lr) as one HIP graph; five graph-path steps (three eager warm-up steps on a
+    side stream, then two replays) land on the same weights as five eager steps."""
+    B, N, K, W = 16, 5, 5, 3
+    rng = np.random.default_rng(5)
+    gr = Graph()
+    gr.pos = torch.tensor(rng.standard_normal((B * N, 3)), dtype=torch.float32, device=hip_device)
+    gr.vel = torch.tensor(rng.standard_normal((B * N, 3)) * 0.5, dtype=torch.float32, device=hip_device)
+    gr.mass = torch.ones(B * N, 1, device=hip_device)
+    gr.edge_index = G.fc_edge_index(B, N, hip_device)
+    gr.nbx_system_size = N  # skips the host-side edge_index check, which cannot run under capture
+    tgt = torch.tensor(rng.standard_normal((B * N, 6)) * 0.1, dtype=torch.float32, device=hip_device)
+
+    def run(graph):
+        torch.manual_seed(0)
+        model = make(64, 4, torch.float32).to(hip_device)
+        params = list(model.parameters())
+        opt = torch.optim.AdamW(params, lr=1e-3, fused=True, capturable=graph)
+        if graph:
+            for grp in opt.param_groups:
+                grp["lr"] = torch.tensor(1e-3, dtype=torch.float32, device=hip_device)
+
+        def body():
+            opt.zero_grad(set_to_none=not graph)
+            loss = torch.nn.functional.mse_loss(model(gr), tgt)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(params, 1.0, foreach=True)
+            opt.step()
+            return loss
+
+        if not graph:
+            for _ in range(K):
+                body()
+            return params
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(W):
+                body()
+        torch.cuda.current_stream().wait_stream(side)
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg):
+            body()
+        for _ in range(K - W):
+            cg.replay()
+        torch.cuda.synchronize()
+        return params
+
+    for pe, pg in zip(run(False), run(True)):
+        assert torch.allclose(pe, pg, rtol=1e-5, atol=1e-6), (pe - pg).abs().max().item()
+
+
 
 def test_training_blob_index_map():
     """The training step packs the persist blob with one scatter of the flattened parameters and
