@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 8
+ABI_VERSION = 9
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
@@ -123,6 +123,10 @@ _SIGNATURES = {
                                         c_p]),
     "nbx_egnn_rollout": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p,
                                         c_p, c_sz, c_p]),
+    "nbx_egnn_forward_graph": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p,
+                                              c_p, c_p, c_sz, c_p]),
+    "nbx_egnn_rollout_knn": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32,
+                                            c_i64, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_egnn_train_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "nbx_egnn_train_forward": (ctypes.c_int, [ctypes.POINTER(EgnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_sz,
                                               c_p]),

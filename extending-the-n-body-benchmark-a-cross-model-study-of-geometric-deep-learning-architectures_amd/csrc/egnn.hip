@@ -138,6 +138,9 @@ struct EgnnPersist {
     int absolute;
     float* traj_pos; float* traj_vel;            // [B][frames][N][3]
     float* out;                                  // [B N][3 heads]
+    int knn;                                     // 0: fully connected; k >= 1: k edges per row node
+    const int* nbr;                              // [B N][k] local neighbour of each edge (forward on a
+                                                 // given graph); nullptr with knn: kNN of each frame
 };
 
 __device__ inline float ep_silu(float x) { return x / (1.0f + __expf(-x)); }
@@ -223,15 +226,20 @@ __global__ __launch_bounds__(EP_THREADS, 1) void egnn_persist_kernel(const EgnnP
     float* cdot = diff + 3 * EP_EMAX;            // [E]
     float* vdot = cdot + EP_EMAX;                // [N]
     float* pred = vdot + EP_NMAX;                // [N][6]
+    int* snbr = reinterpret_cast<int*>(pred + 6 * EP_NMAX);   // [E]: kNN graphs, col of edge (i, q) = snbr[i k + q]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int N = P.N, deg = N - 1, E = N * deg;
+    const int N = P.N, deg = P.knn > 0 ? P.knn : N - 1, E = N * deg;
     const int64_t sys = blockIdx.x;
     const float* emb_i = P.blob;
     const float* emb_b = emb_i + 2 * H;
     const float* layer0 = emb_b + H;
     const float* head0 = layer0 + (size_t)P.L * LAYER;
     auto erow = [&](int e) { return e / deg; };
-    auto ecol = [&](int e) { const int i = e / deg, j = e - i * deg; return j < i ? j : j + 1; };
+    auto ecol = [&](int e) {
+        if (P.knn > 0) return snbr[e];
+        const int i = e / deg, j = e - i * deg;
+        return j < i ? j : j + 1;
+    };
 
     for (int i = tid; i < 3 * N; i += EP_THREADS) {
         pos0[i] = P.pos[sys * N * 3 + i];
@@ -248,6 +256,33 @@ __global__ __launch_bounds__(EP_THREADS, 1) void egnn_persist_kernel(const EgnnP
     if (P.frames >= 1) write_frame(0);
     const int64_t steps = P.frames >= 1 ? P.frames - 1 : 1;
     for (int64_t f = 1; f <= steps; ++f) {
+        // ---- graph (egnn_mc_n_body_dataloader.py:13-28): the given kNN table, or build_graph_with_knn
+        // of this frame's positions (utils/build_fully_connected_graph.py:42-80): node i's k nearest
+        // others by (fp64 distance, index), the first pick (self) dropped -- graph.hip's selection
+        if (P.knn > 0) {
+            if (P.nbr) {
+                for (int e = tid; e < E; e += EP_THREADS) snbr[e] = P.nbr[sys * E + e];
+            } else if (tid < N) {
+                double d[EP_NMAX];
+                const double xi = pos0[3 * tid], yi = pos0[3 * tid + 1], zi = pos0[3 * tid + 2];
+                for (int j = 0; j < N; ++j) {
+                    const double dx = xi - (double)pos0[3 * j], dy = yi - (double)pos0[3 * j + 1],
+                                 dz = zi - (double)pos0[3 * j + 2];
+                    d[j] = sqrt(dx * dx + dy * dy + dz * dz);
+                }
+                unsigned taken = 0;
+                for (int s = 0; s <= deg; ++s) {
+                    int best = -1;
+                    for (int j = 0; j < N; ++j) {
+                        if ((taken >> j) & 1u) continue;
+                        if (best < 0 || d[j] < d[best]) best = j;
+                    }
+                    taken |= 1u << best;
+                    if (s > 0) snbr[tid * deg + s - 1] = best;
+                }
+            }
+            __syncthreads();
+        }
         // ---- preprocess_batch (egnn_mc_n_body_dataloader.py:8-56): x = [|vel|, mass], edge_attr
         for (int o = tid; o < N * H; o += EP_THREADS) {
             const int i = o / H, n = o - i * H;
@@ -401,7 +436,7 @@ size_t ep_lds_bytes(int H) {
     const int S = EP_THREADS / 64;
     const size_t fl = (size_t)EP_EMAX * (2 * H + 8) + EP_EMAX * H + 2 * EP_NMAX * H + EP_NMAX * 2 * H +
                       (size_t)S * EP_RC * H + 3 * 3 * EP_NMAX + EP_NMAX + 4 * EP_EMAX + 3 * EP_EMAX + EP_EMAX +
-                      EP_NMAX + 6 * EP_NMAX;
+                      EP_NMAX + 6 * EP_NMAX + EP_EMAX;
     return fl * 4;
 }
 
@@ -426,9 +461,10 @@ int ep_launch_h(const EgnnPersist& p, int64_t B, hipStream_t st) {
 }
 
 int ep_launch(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t B, int64_t N,
-              int64_t frames, int absolute, float* traj_pos, float* traj_vel, float* out, hipStream_t st) {
+              int64_t frames, int absolute, float* traj_pos, float* traj_vel, float* out, hipStream_t st,
+              int knn = 0, const int* nbr = nullptr) {
     EgnnPersist p{w->persist_blob, w->num_layers, (int)N, w->num_heads, w->recurrent, w->norm_diff, w->use_tanh,
-                  w->coords_weight, pos, vel, mass, frames, absolute, traj_pos, traj_vel, out};
+                  w->coords_weight, pos, vel, mass, frames, absolute, traj_pos, traj_vel, out, knn, nbr};
     switch (w->hidden) {
         case 32: return ep_launch_h<32>(p, B, st);
         case 64: return ep_launch_h<64>(p, B, st);
@@ -618,4 +654,45 @@ extern "C" int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* ve
     }
     NBX_LAUNCH_CHECK("egnn rollout");
     return NBX_OK;
+}
+
+// kNN graphs (egnn_mc_n_body_dataloader.py:13-28 hands the model build_graph_with_knn's
+// graph when args.num_neighbors < N - 1): the persistent kernel with an explicit neighbour table.
+namespace {
+int egnn_knn_check(const nbx_egnn_weights* w, int64_t N, int64_t k, const char* fn) {
+    NBX_CHECK_ARG(k >= 1 && k < N, "%s: need 1 <= num_neighbors < N (got %lld, N = %lld)", fn, (long long)k,
+                  (long long)N);
+    if (!ep_usable(w, N)) {
+        nbx::set_error("%s: kNN graphs run on the persistent kernel only (hidden 32 / 64 / 128, 2 <= N <= %d)", fn,
+                       EP_NMAX);
+        return NBX_E_UNSUPPORTED;
+    }
+    return NBX_OK;
+}
+}  // namespace
+
+extern "C" int nbx_egnn_forward_graph(const nbx_egnn_weights* w, const float* pos, const float* vel,
+                                      const float* mass, int64_t B, int64_t N, int64_t k, const int32_t* nbr,
+                                      float* out, void* workspace, size_t workspace_bytes, void* stream) {
+    EgnnWs ws;
+    if (int rc = egnn_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    if (k == N - 1 && !nbr) return nbx_egnn_forward(w, pos, vel, mass, B, N, out, workspace, workspace_bytes, stream);
+    if (int rc = egnn_knn_check(w, N, k, "nbx_egnn_forward_graph")) return rc;
+    NBX_CHECK_ARG(nbr != nullptr, "nbx_egnn_forward_graph: null neighbour table");
+    return ep_launch(w, const_cast<float*>(pos), const_cast<float*>(vel), mass, B, N, 0, 0, nullptr, nullptr, out,
+                     (hipStream_t)stream, (int)k, nbr);
+}
+
+extern "C" int nbx_egnn_rollout_knn(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t B,
+                                    int64_t N, int64_t num_frames, int32_t flags, int64_t k, float* traj_pos,
+                                    float* traj_vel, void* workspace, size_t workspace_bytes, void* stream) {
+    if (k == N - 1)
+        return nbx_egnn_rollout(w, pos, vel, mass, B, N, num_frames, flags, traj_pos, traj_vel, workspace,
+                                workspace_bytes, stream);
+    EgnnWs ws;
+    if (int rc = egnn_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    NBX_CHECK_ARG(num_frames >= 1 && w->num_heads == 2, "nbx_egnn_rollout_knn: needs 2 heads (pos_dt, vel), frames >= 1");
+    if (int rc = egnn_knn_check(w, N, k, "nbx_egnn_rollout_knn")) return rc;
+    return ep_launch(w, pos, vel, mass, B, N, num_frames, flags & NBX_ROLLOUT_ABSOLUTE, traj_pos, traj_vel, nullptr,
+                     (hipStream_t)stream, (int)k, nullptr);
 }

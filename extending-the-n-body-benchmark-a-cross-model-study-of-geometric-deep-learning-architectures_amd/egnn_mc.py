@@ -284,21 +284,17 @@ class EGNNMultiChannel(nn.Module):
         pos = graph.pos
         device = pos.device
         V = pos.shape[0]
-        N = getattr(graph, "nbx_system_size", None)
-        if N is None:
-            from .segnn import SEGNN
-            B, N = SEGNN.infer_system_size(V, graph.edge_index.shape[1])
-            from .graph import _fc_edge_index_shared as fc_edge_index
-            if not torch.equal(graph.edge_index.to(device), fc_edge_index(B, N, device)):
-                raise NotImplementedError("native EGNN-MC needs the fully-connected edge_index")
-        else:
-            N = int(N)
-            B = V // N
+        from .graph import system_layout
+        # (graph.nbx_system_size, set by this package's dataloaders for fully-connected graphs, skips
+        # the host-side edge_index comparison: a captured training step needs that)
+        B, N, fc = system_layout(graph, V, graph.edge_index.shape[1], device)
+        knn = None if fc else self._knn_table(graph.edge_index, B, N, device)
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
         mass = getattr(graph, "mass", None)
         m = f(mass.reshape(-1)) if mass is not None else torch.ones(V, device=device)
         p, v = f(pos), f(graph.vel)
-        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()) and self._trainable(N):
+        if (knn is None and torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters())
+                and self._trainable(N)):
             # training step (trainer.py:233-358): the native forward keeps its activations and
             # loss.backward() runs the native backward (csrc/egnn_train.hip)
             if self._native_reason:
@@ -308,15 +304,49 @@ class EGNNMultiChannel(nn.Module):
         out = torch.empty(V, 3 * len(self.heads), device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(B, N, device)
-        _lib.check(_lib.lib().nbx_egnn_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                               _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
-                                               _lib.stream_ptr(device)), "nbx_egnn_forward")
+        if knn is None:
+            _lib.check(_lib.lib().nbx_egnn_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                   _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(),
+                                                   _lib.stream_ptr(device)), "nbx_egnn_forward")
+        else:
+            k, nbr = knn
+            _lib.check(_lib.lib().nbx_egnn_forward_graph(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                         k, _lib.dev_ptr(nbr), _lib.dev_ptr(out), _lib.dev_ptr(ws),
+                                                         ws.numel(), _lib.stream_ptr(device)),
+                       "nbx_egnn_forward_graph")
         return out.to(pos.dtype)
 
+    @staticmethod
+    def _knn_table(edge_index, B: int, N: int, device):
+        """(k, nbr int32 [B N][k]) of a graph with k edges at every row node, in row order (the kNN
+        graphs of build_graph_with_knn, build_fully_connected_graph.py:42-80, which
+        egnn_mc_n_body_dataloader.py:21-28 hands the model); nbr holds local column indices.
+        EGNN-MC aggregates at row = edge_index[0] (egnn_mc.py:127-128, 142-151), so other graphs
+        (ragged degrees) are refused.  (A grad-mode forward on such a graph returns the inference
+        result, as for shapes the native training step does not cover.)"""
+        V = B * N
+        ei = edge_index.to(device)
+        E = ei.shape[1]
+        k = E // V if V else 0
+        msg = ("native EGNN-MC runs the fully-connected graph or k < N-1 edges at every node, grouped by "
+               "row = edge_index[0] (build_graph_with_knn's kNN layout)")
+        if E != V * k or not 1 <= k < N - 1:
+            raise NotImplementedError(msg)
+        row, col = ei[0], ei[1]
+        if not torch.equal(row, torch.arange(V, device=device, dtype=row.dtype).repeat_interleave(k)):
+            raise NotImplementedError(msg)
+        local = col - torch.div(row, N, rounding_mode="floor") * N
+        if bool(((local < 0) | (local >= N)).any()):
+            raise NotImplementedError("native EGNN-MC: edges between systems")
+        return k, local.to(torch.int32).contiguous()
+
     @torch.no_grad()
-    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False):
+    def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False, num_neighbors=None):
         """Device-resident self-feed (infer_self_feed.py:161-194); ``absolute``: pos = pred[:, :3]
-        (targets other than "pos_dt+vel") instead of pos += pred[:, :3]."""
+        (targets other than "pos_dt+vel") instead of pos += pred[:, :3].  ``num_neighbors``: the
+        dataloader's kNN option (egnn_mc_n_body_dataloader.py:13-28): each frame's graph is the kNN
+        graph of that frame's positions, built inside the rollout kernel (None / N-1: fully
+        connected)."""
         device = loc.device
         B, N, _ = loc.shape
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous().clone()
@@ -325,10 +355,17 @@ class EGNNMultiChannel(nn.Module):
         tv = torch.empty_like(tp)
         W = self._weights(device)
         ws = self._workspace(B, N, device)
-        _lib.check(_lib.lib().nbx_egnn_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
-                                               num_frames, _lib.ROLLOUT_ABSOLUTE if absolute else 0,
-                                               _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws),
-                                               ws.numel(), _lib.stream_ptr(device)), "nbx_egnn_rollout")
+        flags = _lib.ROLLOUT_ABSOLUTE if absolute else 0
+        if num_neighbors is None or int(num_neighbors) == N - 1:
+            _lib.check(_lib.lib().nbx_egnn_rollout(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                   num_frames, flags, _lib.dev_ptr(tp), _lib.dev_ptr(tv),
+                                                   _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
+                       "nbx_egnn_rollout")
+        else:
+            _lib.check(_lib.lib().nbx_egnn_rollout_knn(W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N,
+                                                       num_frames, flags, int(num_neighbors), _lib.dev_ptr(tp),
+                                                       _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(),
+                                                       _lib.stream_ptr(device)), "nbx_egnn_rollout_knn")
         return tp, tv
 
 

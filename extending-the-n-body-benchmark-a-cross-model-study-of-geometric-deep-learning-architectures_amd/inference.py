@@ -208,6 +208,12 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
                 raise NotImplementedError(f"native {model_type} rollout: kNN graphs (num_neighbors < N-1) "
                                           "are not supported")
             knn = {"num_neighbors": int(num_neighbors)}
+    elif model_type == "egnn_mc":
+        # lines 161-170: the graph comes from dataloader.preprocess_batch, i.e. the dataloader's own
+        # args.num_neighbors (egnn_mc_n_body_dataloader.py:13-19: None / <= 0 / >= N: fully connected)
+        k = getattr(getattr(dataloader, "args", None), "num_neighbors", None)
+        if k is not None and 0 < int(k) < n_nodes - 1:
+            knn = {"num_neighbors": int(k)}
     num_steps = loc_actual.shape[1]
     if max_rollout_steps is not None:
         try:

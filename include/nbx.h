@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 8
+#define NBX_ABI_VERSION 9
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -307,6 +307,21 @@ int nbx_egnn_forward(const nbx_egnn_weights* w, const float* pos, const float* v
 int nbx_egnn_rollout(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
                      int64_t num_nodes, int64_t num_frames, int32_t flags, float* traj_pos, float* traj_vel, void* workspace,
                      size_t workspace_bytes, void* stream);
+
+/* kNN graphs (ABI 9; dataloaders/egnn_mc_n_body_dataloader.py:13-28 builds build_graph_with_knn's
+ * graph when args.num_neighbors < N - 1; EGNNMultiChannel aggregates at row = edge_index[0], so every
+ * node has exactly k edges).  nbx_egnn_forward_graph: nbx_egnn_forward on the graph whose edges
+ * (b N + i, b N + nbr[(b N + i) k + q]), q < k, are node i's (int32 local indices, [B N][k]);
+ * k == N - 1 with nbr == NULL is nbx_egnn_forward.  nbx_egnn_rollout_knn: nbx_egnn_rollout with
+ * every frame's graph the kNN graph of that frame's positions (k == N - 1: nbx_egnn_rollout).
+ * Both need 1 <= k < N and the persistent kernel's shapes (hidden 32 / 64 / 128, N <= 8), else
+ * NBX_E_INVAL / NBX_E_UNSUPPORTED. */
+int nbx_egnn_forward_graph(const nbx_egnn_weights* w, const float* pos, const float* vel, const float* mass,
+                           int64_t batch_size, int64_t num_nodes, int64_t k, const int32_t* nbr, float* out,
+                           void* workspace, size_t workspace_bytes, void* stream);
+int nbx_egnn_rollout_knn(const nbx_egnn_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
+                         int64_t num_nodes, int64_t num_frames, int32_t flags, int64_t k, float* traj_pos,
+                         float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
 
 /* EGNN-MC training step (trainer.py:233-358: pred = model(graph); loss.backward()), ABI 7.
  * nbx_egnn_train_forward runs the forward of `batch_size` fully-connected systems of 2..8 bodies
