@@ -416,7 +416,9 @@ def bench_egnn_train(a, rank, world, device, P):
     params = list(model.parameters())
 
     def step_body():
-        opt.zero_grad(set_to_none=not graph)   # captured: the gradients are static buffers
+        # (captured too: backward then allocates the gradients in the graph's pool, so replays
+        # rewrite the same buffers and no per-parameter fill / accumulate launches are recorded)
+        opt.zero_grad(set_to_none=True)
         loss = torch.nn.functional.mse_loss(model(g), target)
         loss.backward()
         P.allreduce_gradients(params)   # data parallel over RCCL (one bucket at C1); no-op on one rank

@@ -860,6 +860,14 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
     ck.flush(P);
 }
 
+// part = 0 as a kernel rather than hipMemsetAsync: the bench captures the whole training step in a
+// HIP graph, and back-to-back replays of a graph holding a memset node gave nondeterministic gradients
+// (a race between one replay's memset and the previous replay's reduction); kernel nodes stay ordered
+__global__ void egnn_zero_kernel(float* __restrict__ p, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = 0.f;
+}
+
 // grad[i] = sum_g part[g][i]
 __global__ void egnn_grad_reduce_kernel(const float* __restrict__ part, int G, int64_t n, float* __restrict__ grad) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -981,7 +989,7 @@ extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* p
     p.gpart = p.save + B * p.save_floats;
     const int G = (int)(B < TRAIN_GROUPS ? B : TRAIN_GROUPS);
     p.dbg = et_dbg_buf();
-    NBX_HIP(hipMemsetAsync(p.gpart, 0, sizeof(float) * (size_t)G * p.blob_floats, st));
+    hipLaunchKernelGGL(egnn_zero_kernel, dim3(4096), dim3(256), 0, st, p.gpart, (int64_t)G * p.blob_floats);
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
     if (int rc = set_lds_attr()) return rc;
     switch (w->hidden) {
