@@ -215,9 +215,9 @@ def test_gpu_training_step_c1_shape(hip_device):
 @pytest.mark.gpu
 def test_gpu_training_step_hip_graph_matches_eager(hip_device):
     """bench.py's training line replays the whole step (forward, backward, clip, fused AdamW with
-    a device-resident lr) as one HIP graph; five graph-path steps (three eager warm-up steps on a
-    side stream, then two replays) land on the same weights as five eager steps."""
-    B, N, K, W = 16, 5, 5, 3
+    a device-resident lr) as one HIP graph; twelve graph-path steps (three eager warm-up steps on a
+    side stream, then nine back-to-back replays) land on the same weights as twelve eager steps."""
+    B, N, K, W = 16, 5, 12, 3
     rng = np.random.default_rng(5)
     gr = Graph()
     gr.pos = torch.tensor(rng.standard_normal((B * N, 3)), dtype=torch.float32, device=hip_device)
