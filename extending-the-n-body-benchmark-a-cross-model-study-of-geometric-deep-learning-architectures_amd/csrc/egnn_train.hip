@@ -863,9 +863,9 @@ __global__ __launch_bounds__(ET_THREADS) void egnn_train_bwd_kernel(const EgnnTr
 // part = 0 as a kernel rather than hipMemsetAsync: the bench captures the whole training step in a
 // HIP graph, and back-to-back replays of a graph holding a memset node gave nondeterministic gradients
 // (a race between one replay's memset and the previous replay's reduction); kernel nodes stay ordered
-__global__ void egnn_zero_kernel(float* __restrict__ p, int64_t n) {
+__global__ void egnn_zero_kernel(float* __restrict__ p, int64_t n, float v) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        p[i] = 0.f;
+        p[i] = v;
 }
 
 // grad[i] = sum_g part[g][i]
@@ -989,7 +989,10 @@ extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* p
     p.gpart = p.save + B * p.save_floats;
     const int G = (int)(B < TRAIN_GROUPS ? B : TRAIN_GROUPS);
     p.dbg = et_dbg_buf();
-    hipLaunchKernelGGL(egnn_zero_kernel, dim3(4096), dim3(256), 0, st, p.gpart, (int64_t)G * p.blob_floats);
+    // NBX_ET_POISON=1 fills the slices with NaN instead (checks that every gradient element is written)
+    static const bool poison = getenv("NBX_ET_POISON") && getenv("NBX_ET_POISON")[0] == '1';
+    hipLaunchKernelGGL(egnn_zero_kernel, dim3(4096), dim3(256), 0, st, p.gpart, (int64_t)G * p.blob_floats,
+                       poison ? __builtin_nanf("") : 0.f);
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
     if (int rc = set_lds_attr()) return rc;
     switch (w->hidden) {
