@@ -245,7 +245,7 @@ def test_run_inference_routes_num_neighbors(tmp_path, fake_sim):
     """infer_self_feed.py:58,121-123,137-139: segnn / ponita build each frame's graph with
     build_graph_with_knn(num_neighbors): k < N-1 reaches the model's kNN rollout, k >= N raises
     the reference's ValueError, a model without kNN support refuses loudly; egnn_mc's branch
-    ignores num_neighbors."""
+    ignores num_neighbors and uses the dataloader's args.num_neighbors instead."""
     ds = D.GravityDatasetOtf(batch_size=2, sim_length=60, num_nodes=3, device="cpu", data_path=str(tmp_path / "s"),
                              double_precision=True)
     kw = dict(device="cpu", max_rollout_steps=3, dataset=ds)
@@ -258,6 +258,13 @@ def test_run_inference_routes_num_neighbors(tmp_path, fake_sim):
         with pytest.raises(NotImplementedError):
             I.run_inference(mt, None, model=_ConstModel(), save_dir=str(tmp_path / mt), num_neighbors=1, **kw)
     I.run_inference("egnn_mc", None, model=_ConstModel(), save_dir=str(tmp_path / "e"), num_neighbors=1, **kw)
+    # egnn_mc takes k from the dataloader (egnn_mc_n_body_dataloader.py:13-19): None / >= N-1 -> FC
+    import types
+    for k, want in ((1, 1), (None, None), (2, None), (0, None)):
+        m, dl = _KnnModel(), types.SimpleNamespace(args=types.SimpleNamespace(num_neighbors=k))
+        m.k = None
+        I.run_inference("egnn_mc", dl, model=m, save_dir=str(tmp_path / "e"), **kw)
+        assert m.k == want
 
 
 def test_energy_oracle_small_case():
