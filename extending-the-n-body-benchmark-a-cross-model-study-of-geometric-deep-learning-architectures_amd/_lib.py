@@ -12,7 +12,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 9
+ABI_VERSION = 10
+COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 MAX_LAYERS = 64
 
@@ -37,6 +38,7 @@ class SegnnWeights(ctypes.Structure):
                 ("bn_momentum", c_f)] + [(n, c_p) for n in (
                     "emb", "emb_bias", "pp1_img", "pp1_bias", "pp2")] + [
                 ("bn_allreduce", ALLREDUCE_FN), ("bn_allreduce_ctx", c_p), ("bn_global_batch", c_i64),
+                ("bn_comm", c_p), ("deterministic", c_i32), ("reserved0", c_i32),
                 ("layers", SegnnLayer * MAX_LAYERS)]
 
 
@@ -113,6 +115,10 @@ _SIGNATURES = {
                                           c_p, c_p, c_p, c_p]),
     "nbx_nbody_energies": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_i64, c_d, c_d, c_p, c_p, c_p, c_p, c_p]),
     "nbx_ks_2samp_stat": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "nbx_comm_unique_id": (ctypes.c_int, [c_p]),
+    "nbx_comm_init": (ctypes.c_int, [c_p, c_i32, c_i32, c_i32, ctypes.POINTER(c_p)]),
+    "nbx_comm_destroy": (ctypes.c_int, [c_p]),
+    "nbx_comm_allreduce_f64": (ctypes.c_int, [c_p, c_i64, c_p, c_p]),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),

@@ -73,7 +73,8 @@ def build(jobs: int = 8, verbose: bool = False, force: bool = False) -> str:
                 print(err, file=sys.stderr)
     _keep_device_asm()
     if cmds or not os.path.exists(LIB) or _needs(LIB, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
+        # librccl.so.1: csrc/comm.hip (under PyTorch the loader reuses torch's copy, same soname)
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl"])
     check_isa()
     return LIB
 

@@ -5,6 +5,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <string>
 
 #include "../../include/nbx.h"
@@ -78,5 +79,8 @@ int graph_slots_from_edges(const int64_t* ei, int64_t E, int64_t V, int N, int G
                            float* deg, int* err, hipStream_t st);
 int graph_slots_from_knn(const float* pos, int64_t V, int N, int G, int k, unsigned long long* adj, int* slot,
                          float* deg, int* err, hipStream_t st);
+
+// csrc/comm.hip: sum `count` doubles over the ranks of an RCCL communicator, in place, on `st`
+int comm_allreduce_f64(double* buf, int64_t count, void* comm, hipStream_t st);
 
 }  // namespace nbx

@@ -306,6 +306,42 @@ __global__ __launch_bounds__(BNF_THREADS) void bn_finalize_kernel(
     }
 }
 
+// Deterministic BatchNorm sums (nbx_segnn_weights.deterministic, and the SyncBN path of general
+// graphs): the producing kernel's partial rows [chunk][wpc][3][cw] are summed in a fixed order into
+// sums [3][M] (sum s, sum s^2 over the 0e channels, sum |v|^2 over the 1o channels) -- the layout
+// the atomic path accumulates -- so the consumers (or bn_coef_kernel) finalise from the same slot
+// and a SyncBN all-reduce can run between the two.
+__global__ __launch_bounds__(BNF_THREADS) void bn_reduce_kernel(const double* __restrict__ partial, int wpc, int cw,
+                                                               int M, double* __restrict__ sums) {
+    __shared__ double red[BNF_THREADS];
+    const int chunk = blockIdx.x, t = threadIdx.x;
+    const int ncol = 3 * cw, phases = BNF_THREADS / ncol;
+    const int col = t % ncol, ph = t / ncol;
+    double acc = 0.0;
+    if (ph < phases) {
+        const double* p = partial + (size_t)chunk * wpc * ncol + col;
+#pragma unroll 8
+        for (int i = ph; i < wpc; i += phases) acc += p[(size_t)i * ncol];
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (t < ncol) {
+        double a = 0.0;
+        for (int q = 0; q < phases; ++q) a += red[q * ncol + t];
+        const int st = t / cw, c = chunk * cw + (t - st * cw);
+        if (c < M) sums[st * M + c] = a;
+    }
+}
+
+// coefficients [sc_s | sc_v | sh] (and the running-stat update) from finalised sums, for the
+// consumers that read ws.coef_* (general graphs under SyncBN): one thread per (part, channel)
+__global__ void bn_coef_kernel(nbx::BnSrc b, int M) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 3 * M) return;
+    const int part = i / M, k = i - part * M;
+    (void)nbx::bn_coef(b, M, part, k, true);
+}
+
 // ---------------------------------------------------------------- update
 // message BatchNorm applied to the aggregate (BN is affine per channel, so
 // sum_j BN(m_ij) = scale * sum_j m_ij + deg * shift), then the update_layer_1
@@ -885,6 +921,7 @@ nbx::TpProb tp_base(int rows, const Dims& d) {
 // `edges` real edges in total.
 struct GraphSlots {
     double edges;
+    bool regular;   // every node is the source of the same number of edges (a kNN graph): SyncBN can scale counts
 };
 
 int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass, int64_t B,
@@ -912,24 +949,46 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // atomic BatchNorm statistics: the message BN is finalised by update_layer_1 (segmented input),
     // the feature BN of layers 0..L-2 by the next layer's message_layer_1, the last layer's by
     // pre_pool1 (segmented input); the sums are zeroed by the featurising kernel of the forward
-    const bool bn_atomic = bn_atomic_enabled() && fused_msg && seg_upd;
+    // consumer-finalised BatchNorm (the segmented path): the producers' sums land in a [3][M] slot per
+    // BN instance, by fp64 atomics (default) or, deterministic, as partial rows summed in a fixed order
+    // by bn_reduce_kernel (one small launch per BN instance)
+    const bool bn_slot = fused_msg && seg_upd && (w->deterministic || bn_atomic_enabled());
+    const bool bn_atomic = bn_slot && !w->deterministic;
     auto sums_of = [&](int l, int kind) { return ws.bn_sums + ((size_t)2 * l + kind) * 3 * M; };
-    // SyncBN (w->bn_allreduce): the batch statistics are reduced over every rank between the
-    // producing kernel and the finalising consumer, and normalised by the global counts
-    const bool sync = w->bn_allreduce != nullptr && w->training;
-    if (sync && !bn_atomic) {
-        nbx::set_error("segnn: SyncBN (bn_allreduce) needs the atomic BatchNorm path (mul 96 or 32, 2 <= N <= 16, "
-                       "fully-connected graphs)");
+    // SyncBN (w->bn_comm: an RCCL all-reduce the library enqueues itself; or the w->bn_allreduce hook):
+    // the batch statistics are summed over every rank between the producing kernel and the finalising
+    // consumer, and normalised by the global counts
+    const bool sync = (w->bn_comm != nullptr || w->bn_allreduce != nullptr) && w->training;
+    const int64_t Bg = sync && w->bn_global_batch > 0 ? w->bn_global_batch : B;
+    // general graphs: the real edge count (a kNN rollout's V k scales to the global batch under SyncBN)
+    const double cnt_nodes = (double)(Bg * N);
+    const double cnt_edges = gr ? gr->edges * ((double)Bg / (double)B) : (double)(Bg * N * (N - 1));
+    if (sync && gr && !gr->regular) {
+        nbx::set_error("segnn: SyncBN over a general edge_index needs a regular (kNN) graph");
         return NBX_E_UNSUPPORTED;
     }
-    const int64_t Bg = sync && w->bn_global_batch > 0 ? w->bn_global_batch : B;
-    const double cnt_nodes = (double)(Bg * N), cnt_edges = gr ? gr->edges : (double)(Bg * N * (N - 1));
     auto sync_bn = [&](double* sums) -> int {
         if (!sync) return NBX_OK;
+        if (w->bn_comm) return nbx::comm_allreduce_f64(sums, (int64_t)3 * M, w->bn_comm, st);
         if (w->bn_allreduce(sums, (int64_t)3 * M, (void*)st, w->bn_allreduce_ctx) != 0) {
             nbx::set_error("segnn: bn_allreduce hook failed");
             return NBX_E_HIP;
         }
+        return NBX_OK;
+    };
+    // non-atomic sums of the slot or general-graph paths: partial rows -> fixed-order reduction ->
+    // (SyncBN) all-reduce
+    auto reduce_sums = [&](int wpc, int cw, double* sums) -> int {
+        hipLaunchKernelGGL(bn_reduce_kernel, dim3((unsigned)nbx::ceil_div(M, cw)), dim3(BNF_THREADS), 0, st,
+                           ws.partial, wpc, cw, M, sums);
+        NBX_LAUNCH_CHECK("bn_reduce");
+        return sync_bn(sums);
+    };
+    // general-graph / non-segmented path under SyncBN: reduce, all-reduce, coefficients from the sums
+    auto finalize_sync = [&](int wpc, int cw, double* sums, const nbx::BnSrc& src) -> int {
+        if (int rc = reduce_sums(wpc, cw, sums)) return rc;
+        hipLaunchKernelGGL(bn_coef_kernel, dim3((unsigned)nbx::ceil_div(3 * M, 256)), dim3(256), 0, st, src, M);
+        NBX_LAUNCH_CHECK("bn_coef");
         return NBX_OK;
     };
     // (featurized: the previous rollout_pp2_kernel zeroed them)
@@ -960,7 +1019,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             mp.amf = L.msg1_amf; mp.bias = L.msg1_bias; mp.M1S = ws.M1S; mp.M1V = ws.M1V; mp.xcoef = xprev;
             mp.V = V; mp.N = (int)N; mp.G = (int)d.G; mp.M = M; mp.NG = nbx::msg_pre_group((int)N);
             mp.slot = slot;
-            if (bn_atomic && l > 0) {
+            if (bn_slot && l > 0) {
                 const nbx_segnn_layer& Lp = w->layers[l - 1];
                 mp.xbn = nbx::BnSrc{sums_of(l - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias, Lp.feat_bn_running_mean,
                                     Lp.feat_bn_running_var, ws.coef_feat, cnt_nodes, w->bn_eps, w->bn_momentum,
@@ -1018,14 +1077,24 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3)) return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
-                if (int rc = sync_bn(sums_of(l, 0))) return rc;
+                if (bn_atomic) {
+                    if (int rc = sync_bn(sums_of(l, 0))) return rc;
+                } else if (bn_slot) {
+                    if (int rc = reduce_sums(wpc_msg, cw_msg, sums_of(l, 0))) return rc;
+                }
             } else {
                 NBX_HIP(hipMemsetAsync(ws.AGG, 0, sizeof(float) * 4 * V * M, st));
                 NBX_HIP(hipMemsetAsync(ws.AD, 0, sizeof(float) * V * M, st));
                 NBX_HIP(hipMemsetAsync(ws.partial, 0, sizeof(double) * 48 * ((M + 15) / 16), st));
             }
         }
-        if (!bn_atomic) {
+        if (!bn_slot && sync) {
+            if (int rc = finalize_sync(wpc_msg, cw_msg, sums_of(l, 0),
+                                       nbx::BnSrc{sums_of(l, 0), L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
+                                                  L.msg_bn_running_var, ws.coef_msg, std::max(1.0, cnt_edges),
+                                                  w->bn_eps, w->bn_momentum, w->training, 1}))
+                return rc;
+        } else if (!bn_slot) {
             hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, cw_msg)), dim3(BNF_THREADS), 0, st,
                                ws.partial, wpc_msg, cw_msg, std::max(1.0, cnt_edges), M, w->training,
                                w->bn_eps, w->bn_momentum, L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
@@ -1042,7 +1111,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.seg_s[0] = ws.X; p.seg_s[1] = ws.AGG; p.seg_s[2] = ws.XD; p.seg_s[3] = ws.AD;
             p.seg_v[0] = ws.X + V * M; p.seg_v[1] = ws.AGG + V * M; p.seg_vplane = V * M;
             p.xcoef = xprev; p.mcoef = ws.coef_msg; p.deg = (float)(N - 1);
-            if (bn_atomic)
+            if (bn_slot)
                 p.mbn = nbx::BnSrc{sums_of(l, 0), L.msg_bn_weight, L.msg_bn_bias, L.msg_bn_running_mean,
                                    L.msg_bn_running_var, ws.coef_msg, cnt_edges, w->bn_eps,
                                    w->bn_momentum, w->training, 1};
@@ -1051,7 +1120,16 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.chunks = (M + 15) / 16;
             if (M == 96 && L.upd1_img_x3 && x3_enabled()) {
                 p.B = static_cast<const float*>(L.upd1_img_x3);
-                if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_X3>(p, st, tm)) return rc;
+                // A-ring depth (NBX_UPD1_PF, A/B): 3 = three B sets; > 3 = two B sets + the deeper ring
+                static const int upd1_pf = getenv("NBX_UPD1_PF") ? atoi(getenv("NBX_UPD1_PF")) : 3;
+                int rc;
+                switch (upd1_pf) {
+                    case 5: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 5, 1, SK_UPD1_SEG_X3>(p, st, tm); break;
+                    case 6: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 6, 1, SK_UPD1_SEG_X3>(p, st, tm); break;
+                    case 7: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 7, 1, SK_UPD1_SEG_X3>(p, st, tm); break;
+                    default: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_X3>(p, st, tm);
+                }
+                if (rc) return rc;
             } else if (M == 96) {
                 if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG>(p, st, tm)) return rc;
             } else {
@@ -1090,7 +1168,18 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             // update_layer_2: one 16-channel chunk per wave, full K (CG 1, KS 1; measured against CG 2 / KS 2,
             // CG 1 / KS 2, CG 2 / KS 1, CG 1 / KS 4: 15.1 vs 17.8 / 16.3 / 19.5 / 20.9 us). NBX_UPD2_VARIANT=CG*10+KS
             static const int upd2_var = getenv("NBX_UPD2_VARIANT") ? atoi(getenv("NBX_UPD2_VARIANT")) : 11;
-            if (upd2_var == 11) {
+            // A-ring depth (NBX_UPD2_PF, A/B): at C2 a wave owns one 16-row tile whose 15 A chunks
+            // (30 KB) stream from L2; PF = 16 issues them all before the weight staging
+            static const int upd2_pf = getenv("NBX_UPD2_PF") ? atoi(getenv("NBX_UPD2_PF")) : 3;
+            if (upd2_var == 11 && upd2_pf != 3 && M == 96 && static_enabled()) {
+                int rc;
+                switch (upd2_pf) {
+                    case 6: rc = run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 6, 1, SK_UPD2>(p, st, tm); break;
+                    case 9: rc = run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 9, 1, SK_UPD2>(p, st, tm); break;
+                    default: rc = run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 16, 1, SK_UPD2>(p, st, tm);
+                }
+                if (rc) return rc;
+            } else if (upd2_var == 11) {
                 if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             } else if (upd2_var == 12) {
                 if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
@@ -1102,13 +1191,24 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             }
             wpc_feat = p.waves_per_chunk;
-            if (int rc = sync_bn(sums_of(l, 1))) return rc;
+            if (bn_atomic) {
+                if (int rc = sync_bn(sums_of(l, 1))) return rc;
+            } else if (bn_slot) {
+                if (int rc = reduce_sums(wpc_feat, 16, sums_of(l, 1))) return rc;
+            }
         }
-        if (!bn_atomic)
+        if (!bn_slot && sync) {
+            if (int rc = finalize_sync(wpc_feat, 16, sums_of(l, 1),
+                                       nbx::BnSrc{sums_of(l, 1), L.feat_bn_weight, L.feat_bn_bias,
+                                                  L.feat_bn_running_mean, L.feat_bn_running_var, ws.coef_feat,
+                                                  cnt_nodes, w->bn_eps, w->bn_momentum, w->training, 1}))
+                return rc;
+        } else if (!bn_slot) {
             hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)nbx::ceil_div(M, 16)), dim3(BNF_THREADS), 0, st,
                                ws.partial, wpc_feat, 16, (double)V, M, w->training, w->bn_eps, w->bn_momentum,
                                L.feat_bn_weight, L.feat_bn_bias, L.feat_bn_running_mean, L.feat_bn_running_var,
                                ws.coef_feat);
+        }
     }
 
     // pre_pool1 (gate TP) and pre_pool2 (-> 2x1o)
@@ -1121,7 +1221,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.lda_s = 2 * M; p.lda_v = M;
         p.seg_s[0] = ws.X; p.seg_s[1] = ws.XD; p.seg_v[0] = ws.X + V * M; p.seg_vplane = V * M;
         p.xcoef = w->num_layers > 0 ? ws.coef_feat : nullptr;
-        if (bn_atomic && w->num_layers > 0) {
+        if (bn_slot && w->num_layers > 0) {
             const nbx_segnn_layer& Lp = w->layers[w->num_layers - 1];
             p.xbn = nbx::BnSrc{sums_of(w->num_layers - 1, 1), Lp.feat_bn_weight, Lp.feat_bn_bias,
                                Lp.feat_bn_running_mean, Lp.feat_bn_running_var, ws.coef_feat, cnt_nodes, w->bn_eps,
@@ -1250,7 +1350,7 @@ extern "C" int nbx_segnn_forward_graph(const nbx_segnn_weights* w, const float* 
     NBX_CHECK_ARG(num_edges >= 1 && edge_index != nullptr, "nbx_segnn_forward_graph: need at least one edge");
     hipStream_t st = (hipStream_t)stream;
     if (int rc = slots_from_edges(edge_index, num_edges, B, N, ws, st)) return rc;
-    const GraphSlots gr{(double)num_edges};
+    const GraphSlots gr{(double)num_edges, false};
     return forward_impl(w, pos, vel, mass, B, N, out, ws, st, nullptr, nullptr, false, &gr);
 }
 
@@ -1272,7 +1372,7 @@ extern "C" int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, flo
     hipLaunchKernelGGL(rollout_update_kernel, dim3((unsigned)nbx::ceil_div(V * 3, 256)), dim3(256), 0, st, pos, vel,
                        ws.out, V, (int)N, (int64_t)0, num_frames, traj_pos, traj_vel);
     NBX_LAUNCH_CHECK("rollout_update");
-    const GraphSlots gr{(double)(V * num_neighbors)};
+    const GraphSlots gr{(double)(V * num_neighbors), true};
     for (int64_t f = 1; f < num_frames; ++f) {
         // the graph is rebuilt from each frame's positions (infer_self_feed.py:121-123)
         if (int rc = slots_from_knn(pos, B, N, (int)num_neighbors, ws, st)) return rc;

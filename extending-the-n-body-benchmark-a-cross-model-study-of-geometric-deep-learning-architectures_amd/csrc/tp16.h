@@ -28,7 +28,7 @@ constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
 // `split`, P1 above): node_pre's scalar-row and vector-row GEMMs fill the chip together.
 template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, bool DUAL = false,
           class SK = DynSK>
-__global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
+__global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
     const bool second = DUAL && (int)blockIdx.x >= split;
     const TpProb& P = second ? P1 : P0;
     const int bidx = second ? (int)blockIdx.x - split : (int)blockIdx.x;
@@ -421,10 +421,15 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                         }
                     };
                     auto keep = [&](const bf16x8& v) { asm volatile("" ::"v"(v)); };
+                    // B (SrcB) fragment sets: three (item u in set u % 3, each kept live until item u+1's
+                    // MFMAs issued) or, with a deep A ring (PF > 3), two: the measured gfx950 hazard is on
+                    // SrcA only (a load over an MFMA's SrcB at 0 wait states is safe, tools/hazard), and
+                    // the 36 VGPRs saved hold the deeper A ring
+                    constexpr int NBS = PF > 3 ? 2 : 3;
                     slice_call([&](auto sc_) {
                         constexpr int lo = decltype(sc_)::value * SNIT / KS;
                         constexpr int n = (decltype(sc_)::value + 1) * SNIT / KS - lo;
-                        bf16x8 bx[3][CG][NS > 1 ? NS : 1][3];   // item u in set u % 3
+                        bf16x8 bx[NBS][CG][NS > 1 ? NS : 1][3];   // item u in set u % NBS
                         bf16x8 ax[3][3];
                         read_b(std::integral_constant<int, lo>{}, bx[0]);
                         static_for<0, n>([&](auto uc) {
@@ -432,12 +437,12 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                             if constexpr (u + PF - 1 < n)
                                 load_item(std::integral_constant<int, item + PF - 1>{}, rt, ring[(u + PF - 1) % PF]);
                             __builtin_amdgcn_sched_barrier(0);
-                            if constexpr (u + 1 < n) read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % 3]);
+                            if constexpr (u + 1 < n) read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % NBS]);
                             float av[8];
                             item_a(std::integral_constant<int, item>{}, ring[u % PF], av);
                             tp_split3(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]},
                                       ax[u % 3][0], ax[u % 3][1], ax[u % 3][2]);
-                            const bf16x8 (&b)[CG][NS > 1 ? NS : 1][3] = bx[u % 3];
+                            const bf16x8 (&b)[CG][NS > 1 ? NS : 1][3] = bx[u % NBS];
                             const bf16x8 (&a)[3] = ax[u % 3];
                             if constexpr (item < SK::K0) {
                                 constexpr int NA = 1 + (NS > 1 && item < SK::K1 ? 1 : 0) + (NS > 2 && item < SK::K2 ? 1 : 0);
@@ -476,12 +481,14 @@ __global__ __launch_bounds__(64 * WAVES, SK::PREC ? 1 : 2) void tp16_kernel(cons
                                                                    : 1;
 #pragma unroll
                                 for (int p3 = 0; p3 < 3; ++p3) keep(ax[pu][p3]);
+                                if constexpr (NBS == 3) {
 #pragma unroll
-                                for (int g = 0; g < CG; ++g)
+                                    for (int g = 0; g < CG; ++g)
 #pragma unroll
-                                    for (int j = 0; j < PNA; ++j)
+                                        for (int j = 0; j < PNA; ++j)
 #pragma unroll
-                                        for (int p3 = 0; p3 < 3; ++p3) keep(bx[pu][g][j][p3]);
+                                            for (int p3 = 0; p3 < 3; ++p3) keep(bx[pu][g][j][p3]);
+                                }
                             }
                             __builtin_amdgcn_sched_barrier(0);
                         });

@@ -111,7 +111,7 @@ class SEGNN(nn.Module):
 
     def __init__(self, input_irreps="2x1o + 1x0e", hidden_features=64, lmax_h=1, lmax_attr=1, num_layers=4,
                  output_irreps="2x1o", norm="batch", pool="avg", task="node", additional_message_irreps="2x0e",
-                 training_args=None):
+                 training_args=None, deterministic=False):
         super().__init__()
         if task != "node" or lmax_h != 1 or lmax_attr != 1 or norm != "batch":
             raise NotImplementedError("native SEGNN supports task='node', norm='batch', lmax_h = lmax_attr = 1")
@@ -141,6 +141,10 @@ class SEGNN(nn.Module):
         self._warned_dtype = False
         self._bn_group = None        # SyncBN process group (enable_sync_batchnorm)
         self._bn_hook = None
+        self._bn_comm = None         # RCCL communicator the library all-reduces on (nbx_comm_init)
+        # deterministic=True: train-mode BatchNorm sums reduced in a fixed order instead of fp64
+        # atomics, so repeated train-mode forwards / rollouts are bit-identical (include/nbx.h)
+        self.deterministic = bool(deterministic)
         # BatchNorm statistics of the native forward / rollout (SURVEY §8(e) bn_mode): None follows
         # self.training like the reference module (train() -> batch statistics, the reference's
         # rollout semantics, infer_self_feed.py never calls eval()); "batch" / "running" force
@@ -370,20 +374,49 @@ class SEGNN(nn.Module):
             self.pack_weights(device)
         W = self._packed[1]
         W.training = 1 if self._bn_batch() else 0
+        W.deterministic = 1 if self.deterministic else 0
         return W
 
     # ------------------------------------------------------------ SyncBN (multi-GPU)
-    def enable_sync_batchnorm(self, group=None):
+    def enable_sync_batchnorm(self, group=None, use_rccl=None):
         """Train-mode BatchNorm over the union of every rank's batch (the reference's
         single-process statistics, segnn.py:233-235,257-261,282-283, when the batch is sharded
         over ranks): after each producing kernel the [3][mul] fp64 sums of that BatchNorm are
-        all-reduced over ``group`` (torch.distributed; RCCL under the ``nccl`` backend) on the
-        launch stream and normalised by the global counts.  12 all-reduces per forward."""
+        all-reduced over the ranks on the launch stream and normalised by the global counts.
+        12 all-reduces per forward.
+
+        ``use_rccl`` (default: the group's backend is ``nccl``, i.e. RCCL): the library gets its own
+        RCCL communicator over the group's ranks (include/nbx.h nbx_comm_init; collective call) and
+        enqueues the all-reduces itself -- no host round trip per BatchNorm, so a sharded forward or
+        rollout can be captured into a HIP graph.  Otherwise (gloo) the library calls back into
+        ``torch.distributed.all_reduce`` on the group."""
         import torch.distributed as dist
+        self.disable_sync_batchnorm()
         self._bn_group = group if group is not None else dist.group.WORLD
+        if use_rccl is None:
+            use_rccl = dist.get_backend(self._bn_group) == "nccl"
+        if use_rccl:
+            import ctypes
+            ranks = dist.get_process_group_ranks(self._bn_group)
+            me = dist.get_rank(self._bn_group)
+            uid = [None]
+            if me == 0:
+                buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+                _lib.check(_lib.lib().nbx_comm_unique_id(buf), "nbx_comm_unique_id")
+                uid[0] = buf.raw
+            dist.broadcast_object_list(uid, src=ranks[0], group=self._bn_group)
+            comm = _lib.c_p()
+            dev = torch.cuda.current_device()
+            _lib.check(_lib.lib().nbx_comm_init(ctypes.create_string_buffer(uid[0], _lib.COMM_ID_BYTES), len(ranks),
+                                                me, dev, ctypes.byref(comm)), "nbx_comm_init")
+            self._bn_comm = comm
         return self
 
     def disable_sync_batchnorm(self):
+        if self._bn_comm is not None:
+            torch.cuda.synchronize()
+            _lib.check(_lib.lib().nbx_comm_destroy(self._bn_comm), "nbx_comm_destroy")
+            self._bn_comm = None
         self._bn_group = None
         return self
 
@@ -405,14 +438,21 @@ class SEGNN(nn.Module):
         """Point the weight struct's hook at the SyncBN callback (or clear it) for one call."""
         if self._bn_group is None or not self._bn_batch():
             W.bn_allreduce = _lib.ALLREDUCE_FN()
+            W.bn_comm = None
             W.bn_global_batch = 0
             return
         import torch.distributed as dist
-        if self._bn_hook is None:
-            self._bn_hook = _lib.ALLREDUCE_FN(self._allreduce_cb)
-        nb = torch.tensor([B], dtype=torch.int64, device=device)
+        if self._bn_comm is not None:
+            W.bn_comm = self._bn_comm
+            W.bn_allreduce = _lib.ALLREDUCE_FN()
+        else:
+            if self._bn_hook is None:
+                self._bn_hook = _lib.ALLREDUCE_FN(self._allreduce_cb)
+            W.bn_comm = None
+            W.bn_allreduce = self._bn_hook
+        on_dev = dist.get_backend(self._bn_group) == "nccl"
+        nb = torch.tensor([B], dtype=torch.int64, device=device if on_dev else "cpu")
         dist.all_reduce(nb, group=self._bn_group)
-        W.bn_allreduce = self._bn_hook
         W.bn_global_batch = int(nb.item())
 
     def _bn_sync_in(self):
@@ -506,8 +546,6 @@ class SEGNN(nn.Module):
                 _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
                 "nbx_segnn_rollout")
         else:
-            if self._bn_group is not None and self._bn_batch():
-                raise NotImplementedError("SyncBN rollouts need fully-connected graphs")
             _lib.check(_lib.lib().nbx_segnn_rollout_knn(
                 W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, num_frames, flags,
                 int(num_neighbors), _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(),

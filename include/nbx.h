@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 9
+#define NBX_ABI_VERSION 10
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -182,8 +182,30 @@ typedef struct nbx_segnn_weights {
     nbx_allreduce_fn bn_allreduce;
     void* bn_allreduce_ctx;
     int64_t bn_global_batch;
+    /* ABI 10.  bn_comm: an RCCL communicator from nbx_comm_init.  When non-NULL and training, the
+     * library enqueues the SyncBN all-reduce itself (ncclAllReduce of the [3][mul] fp64 sums on
+     * `stream`; takes precedence over bn_allreduce): no host round trip, graph-capturable.  Also
+     * available on general (kNN) graphs, through the fixed-order reduction below.
+     * deterministic: 1 = the BatchNorm batch sums are reduced from per-block partial rows in a fixed
+     * order (one small launch per BatchNorm) instead of fp64 atomics, so train-mode forwards and
+     * rollouts are bit-reproducible (measured cost: DESIGN.md §3.3); 0 = atomics (default). */
+    void* bn_comm;
+    int32_t deterministic;
+    int32_t reserved0;
     nbx_segnn_layer layers[NBX_SEGNN_MAX_LAYERS];
 } nbx_segnn_weights;
+
+/* RCCL communicators for nbx_segnn_weights.bn_comm (ABI 10), one process per GPU: rank 0 calls
+ * nbx_comm_unique_id, the id (NBX_COMM_ID_BYTES opaque bytes) travels to every rank over any
+ * channel (torch.distributed.broadcast_object_list), then every rank calls nbx_comm_init with its
+ * rank and HIP device (collective: blocks until all ranks arrive).  nbx_comm_allreduce_f64 sums
+ * `count` doubles in place on `stream`.  No reference counterpart: the reference runs one
+ * process on one GPU (SURVEY §2.1 "Parallelism strategies"). */
+#define NBX_COMM_ID_BYTES 128
+int nbx_comm_unique_id(void* id_out);
+int nbx_comm_init(const void* id, int32_t nranks, int32_t rank, int32_t device, void** comm_out);
+int nbx_comm_destroy(void* comm);
+int nbx_comm_allreduce_f64(double* buf, int64_t count, void* comm, void* stream);
 
 /* Bytes of device workspace nbx_segnn_forward / nbx_segnn_rollout need. */
 int nbx_segnn_workspace_bytes(int64_t batch_size, int64_t num_nodes, int32_t mul, size_t* bytes);
@@ -193,7 +215,8 @@ int nbx_segnn_workspace_bytes(int64_t batch_size, int64_t num_nodes, int32_t mul
  * pos/vel [B*N,3], mass [B*N] fp32 -> out [B*N, 6] = (2x1o: delta-pos, vel).
  * Train mode (w->training = 1): the BatchNorm batch statistics are fp64 sums accumulated
  * with device-scope atomics, so repeated calls can differ in the last float bits (eval mode
- * is bit-reproducible); the running statistics are updated in place as in the reference. */
+ * is bit-reproducible; w->deterministic = 1 makes train mode bit-reproducible too); the running
+ * statistics are updated in place as in the reference. */
 int nbx_segnn_forward(const nbx_segnn_weights* w, const float* pos, const float* vel, const float* mass,
                       int64_t batch_size, int64_t num_nodes, float* out, void* workspace, size_t workspace_bytes,
                       void* stream);

@@ -1,0 +1,83 @@
+"""Generate the long-horizon C2 SEGNN rollout fixture from the CPU oracle (build container).
+
+    python tests/golden/make_segnn_c2_long.py [--frames 121] [--scale 0.003] [--slice 64]
+
+Why a second C2 fixture: with random-init weights the C2 rollout of make_segnn_c2.py turns chaotic
+within ~5 steps (bodies flung to |pos| ~ 50, pairs passing within 1e-3 of each other), so north_star's
+"rollout MSE <= 1e-5 vs reference" can only be checked over that short horizon there.  This fixture
+keeps the C2 model and workload -- SEGNN lmax_h=1, hidden 192, 6 layers, N=5, B=1024, train-mode
+BatchNorm over the whole batch, GravitySim frame-0 initial states (seeds 0..1023) -- and scales the
+output layer ``pre_pool2`` (both 2x1o outputs: the position increment and the new velocity) by
+``--scale``, so every step moves a body by ~1e-3 of the inter-body spacing and the autoregressive
+map stays close to the identity.  That the dynamics are then NOT chaotic over the horizon is shown
+inside the fixture: the same oracle rollout computed entirely in fp32 arithmetic stays within MSE
+1e-7 of the fp64 one at every frame (``f32_mse_loc`` / ``f32_mse_vel``, over all 1024 systems).
+
+Stored: the fp32-rounded initial states of all 1024 systems (the device rollout needs the whole
+batch: train-mode BatchNorm couples the systems), every frame of the fp64 oracle rollout for the
+first ``--slice`` systems (fp64), the per-frame fp32-oracle MSEs over all systems, the scale and a
+weight checksum.  The oracle is the e3nn restatement oracle/segnn.py: parity vs e3nn itself is
+UNPINNED (e3nn is absent from this image).
+
+Output: tests/golden/segnn_c2_long.npz
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from make_segnn_c2 import HIDDEN, LAYERS, c2_model, initial_states, weight_checksum  # noqa: E402
+
+
+def scaled_model(scale):
+    model = c2_model()
+    with torch.no_grad():
+        model.pre_pool2.tp.weight.mul_(scale)
+    return model
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=121)
+    ap.add_argument("--scale", type=float, default=0.003)
+    ap.add_argument("--slice", type=int, default=64)
+    a = ap.parse_args()
+    from oracle.rollout import rollout, segnn_step
+    from oracle.segnn import SEGNNOracle
+    model = scaled_model(a.scale)
+    params = {k: t.double().numpy().copy() for k, t in model.state_dict().items()}
+    loc, vel, mass = initial_states()
+    loc, vel = loc.astype(np.float32).astype(np.float64), vel.astype(np.float32).astype(np.float64)
+    om = SEGNNOracle(hidden_features=HIDDEN, num_layers=LAYERS)
+    t0 = time.time()
+    tl, tv = rollout(segnn_step(om, dict(params), training=True), loc, vel, np.zeros_like(loc), mass, a.frames)
+    print(f"fp64 oracle rollout of {a.frames - 1} steps: {time.time() - t0:.1f} s", flush=True)
+    p32 = {k: v.astype(np.float32) for k, v in params.items()}
+    f32 = lambda x: x.astype(np.float32)
+    fl, fv = rollout(segnn_step(om, p32, training=True), f32(loc), f32(vel), f32(np.zeros_like(loc)), f32(mass),
+                     a.frames)
+    print(f"fp32 oracle rollout done: {time.time() - t0:.1f} s", flush=True)
+    mse_l = ((fl.astype(np.float64) - tl) ** 2).mean(axis=(0, 2, 3))
+    mse_v = ((fv.astype(np.float64) - tv) ** 2).mean(axis=(0, 2, 3))
+    for k in range(0, a.frames, 10):
+        print(f"frame {k}: fp32-oracle MSE loc {mse_l[k]:.3e} vel {mse_v[k]:.3e}; mean displacement "
+              f"{np.abs(tl[:, k] - tl[:, 0]).mean():.3e}")
+    print(f"max fp32-oracle MSE over the horizon: loc {mse_l.max():.3e}, vel {mse_v.max():.3e}")
+    S = a.slice
+    np.savez_compressed(os.path.join(HERE, "segnn_c2_long.npz"), loc0=loc, vel0=vel,
+                        traj_loc=tl[:S], traj_vel=tv[:S], f32_mse_loc=mse_l, f32_mse_vel=mse_v,
+                        scale=np.float64(a.scale), weight_checksum=np.float64(weight_checksum(model)))
+
+
+if __name__ == "__main__":
+    main()

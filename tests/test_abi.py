@@ -70,7 +70,7 @@ def test_struct_layout_matches_header():
     assert [f for f, _ in lib.SegnnWeights._fields_] == wf
     head = 3 * 4 + 2 * 4   # mul, num_layers, training, bn_eps, bn_momentum
     head = (head + 7) // 8 * 8
-    extra = 8 + 8          # bn_allreduce (function pointer), bn_global_batch (int64)
+    extra = 8 + 8 + 8      # bn_allreduce (function pointer), bn_global_batch (int64), deterministic + reserved0
     assert ctypes.sizeof(lib.SegnnWeights) == head + w_ptrs * 8 + extra + lib.MAX_LAYERS * layer_ptrs * 8
 
 

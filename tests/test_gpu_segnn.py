@@ -413,3 +413,38 @@ def test_bn_mode_overrides_module_mode(hip_device):
     model.eval()
     model.bn_mode = "batch"
     np.testing.assert_allclose(gpu_forward(model, pos, vel, mass, B, N, hip_device), ref_train, rtol=1e-6, atol=1e-7)
+
+
+def test_deterministic_train_mode_rollout_c2_bit_identical(hip_device):
+    """SEGNN(deterministic=True) (include/nbx.h nbx_segnn_weights.deterministic): the train-mode
+    BatchNorm sums are reduced from per-block partial rows in a fixed order instead of fp64 atomics,
+    so two C2 train-mode rollouts (hidden 192, 6 layers, B=1024, 8 frames) from the same state are
+    bit-identical, running statistics included; and they agree with the atomic path's forward."""
+    torch.manual_seed(0)
+    model = S.SEGNN(hidden_features=192, num_layers=6, deterministic=True).to(hip_device).train()
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    B, N, T = 1024, 5, 8
+    pos, vel, mass = states(B, N, seed=12)
+    t = lambda a: torch.tensor(a.reshape(B, N, -1), dtype=torch.float32, device=hip_device)
+    runs = []
+    for _ in range(2):
+        model.load_state_dict(sd0)
+        tp, tv = model.rollout(t(pos), t(vel), t(mass), T)
+        runs.append((tp.cpu().numpy(), tv.cpu().numpy(),
+                     {k: v.cpu().numpy() for k, v in model.state_dict().items() if "running" in k}))
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+    for k in runs[0][2]:
+        np.testing.assert_array_equal(runs[0][2][k], runs[1][2][k])
+    # the deterministic forward equals the atomic one up to the atomics' summation order
+    model.load_state_dict(sd0)
+    det = gpu_forward(model, pos, vel, mass, B, N, hip_device)
+    model.load_state_dict(sd0)
+    model.deterministic = False
+    atom = gpu_forward(model, pos, vel, mass, B, N, hip_device)
+    assert (np.abs(det - atom).max(0) <= 1e-6 * np.abs(det).max(0)).all()
+    model.load_state_dict(sd0)
+    model.deterministic = True
+    params = params_of(model)
+    ref, _ = oracle_forward(model, params, pos, vel, mass, B, N, True)
+    assert_close_cols(det, ref)

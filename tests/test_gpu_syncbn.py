@@ -28,13 +28,13 @@ def _inputs():
     return rng.standard_normal((B, N, 3)), rng.standard_normal((B, N, 3))
 
 
-def _model(device):
+def _model(device, deterministic=False):
     from nbody_amd.segnn import SEGNN
     torch.manual_seed(0)
-    return SEGNN(hidden_features=192, num_layers=6).to(device).train()
+    return SEGNN(hidden_features=192, num_layers=6, deterministic=deterministic).to(device).train()
 
 
-def _run(model, loc, vel, device):
+def _run(model, loc, vel, device, knn=None):
     import nbody_amd.graph as G
 
     class Graph:
@@ -51,21 +51,26 @@ def _run(model, loc, vel, device):
     stats = {k: v.cpu().numpy() for k, v in model.state_dict().items() if "running" in k}
     model.load_state_dict(sd0)
     t = lambda a: torch.tensor(a, dtype=torch.float32, device=device)
-    tp, tv = model.rollout(t(loc), t(vel), torch.ones(b, N, 1, device=device), T)
+    tp, tv = model.rollout(t(loc), t(vel), torch.ones(b, N, 1, device=device), T,
+                           **({"num_neighbors": knn} if knn else {}))
     return out, stats, tp.cpu().numpy(), tv.cpu().numpy()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, backend="gloo", deterministic=False, knn=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    if backend == "nccl":
+        torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
-        dev = torch.device("cuda:0")
         loc, vel = _inputs()
         sl = slice(rank * B // world, (rank + 1) * B // world)
-        model = _model(dev).enable_sync_batchnorm()
-        q.put((rank, _run(model, loc[sl], vel[sl], dev)))
+        model = _model(dev, deterministic).enable_sync_batchnorm()
+        assert (model._bn_comm is not None) == (backend == "nccl")
+        q.put((rank, _run(model, loc[sl], vel[sl], dev, knn)))
+        model.disable_sync_batchnorm()
     except Exception as e:  # surfaced by the parent
         q.put((rank, repr(e)))
     finally:
@@ -97,3 +102,57 @@ def test_syncbn_two_ranks_reproduce_full_batch(hip_device):
     # and without SyncBN the halves differ (per-rank statistics): the test is sensitive
     half = _run(_model(hip_device), loc[:B // 2], vel[:B // 2], hip_device)[0]
     assert np.abs(half - out[:B // 2 * N]).max() > 1e-3 * np.abs(out).max()
+
+
+def _spawn(world, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+    return res
+
+
+def test_syncbn_knn_rollout_two_ranks_reproduce_full_batch(hip_device):
+    """kNN graphs (num_neighbors=2 < N-1, infer_self_feed.py:121-123) under SyncBN: the general-graph
+    path reduces each BatchNorm's partial rows in a fixed order, all-reduces the sums and finalises
+    them (bn_reduce_kernel / bn_coef_kernel); two half-batch ranks reproduce the single-process
+    kNN rollout, whose message-BN count is the global V k."""
+    res = _spawn(2, knn=2)
+    loc, vel = _inputs()
+    _, _, tp, tv = _run(_model(hip_device), loc, vel, hip_device, knn=2)
+    np.testing.assert_allclose(np.concatenate([res[0][2], res[1][2]]), tp, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(np.concatenate([res[0][3], res[1][3]]), tv, rtol=1e-4, atol=1e-5)
+
+
+def test_syncbn_deterministic_two_ranks_bit_reproducible(hip_device):
+    """deterministic=True under SyncBN: fixed-order partial-row reductions, then the all-reduce; two
+    runs of the sharded forward + rollout are bit-identical and reproduce the full batch."""
+    a, b = _spawn(2, deterministic=True), _spawn(2, deterministic=True)
+    for r in (0, 1):
+        for i in (0, 2, 3):
+            np.testing.assert_array_equal(a[r][i], b[r][i])
+    loc, vel = _inputs()
+    out, _, tp, tv = _run(_model(hip_device, True), loc, vel, hip_device)
+    scale = np.abs(out).max(0)
+    assert (np.abs(np.concatenate([a[0][0], a[1][0]]) - out).max(0) <= 1e-5 * scale).all()
+    np.testing.assert_allclose(np.concatenate([a[0][2], a[1][2]]), tp, rtol=1e-4, atol=1e-5)
+
+
+def test_syncbn_rccl_communicator_single_rank(hip_device):
+    """The library-owned RCCL communicator (nbx_comm_init; enable_sync_batchnorm under the nccl
+    backend): the all-reduces are enqueued by libnbx on the launch stream.  One rank (the box has one
+    GPU; RCCL refuses two ranks on one device): the sum over one rank is the identity, so the
+    deterministic SyncBN forward and rollout equal the plain deterministic ones bit for bit."""
+    res = _spawn(1, backend="nccl", deterministic=True)
+    loc, vel = _inputs()
+    out, stats, tp, tv = _run(_model(hip_device, True), loc, vel, hip_device)
+    np.testing.assert_array_equal(res[0][0], out)
+    np.testing.assert_array_equal(res[0][2], tp)
+    np.testing.assert_array_equal(res[0][3], tv)
