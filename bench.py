@@ -403,7 +403,9 @@ def bench_egnn_train(a, rank, world, device, P):
     target = t(rng.standard_normal((B * N, 6)) * 0.1)
     # Trainer.create_optimizer / create_lr_scheduler (trainer.py:170-194): AdamW(weight_decay 1e-8,
     # betas (0.9, 0.98), eps 1e-9) under the LambdaLR warmup schedule; the update as one fused launch
-    graph = not a.eager
+    # one HIP graph per step on one GPU; with several ranks the gradient all-reduce (RCCL) would be
+    # recorded inside the graph, a path not yet validated on hardware: eager until it is
+    graph = not a.eager and world == 1
     opt = torch.optim.AdamW(model.parameters(), lr=1.0, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9,
                             fused=True, capturable=graph)
     sched = torch.optim.lr_scheduler.LambdaLR(
@@ -443,6 +445,7 @@ def bench_egnn_train(a, rank, world, device, P):
         def train_step():
             cg.replay()
             sched.step()
+            model.invalidate_weights()   # the replay's AdamW updated the parameters in place
             return static_loss
     else:
         def train_step():

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import Sequence
 
+import warnings
+
 import torch
 from torch import nn
 
@@ -212,6 +214,13 @@ class EGNNMultiChannel(nn.Module):
         self._packed = (self._param_version(), W, P)
         return W
 
+    def invalidate_weights(self):
+        """Drop the packed inference weights.  Call after updating the parameters in a way that does
+        not bump their version counters -- e.g. replays of a captured training step (HIP graph), whose
+        optimizer writes the parameters in place on the device."""
+        self._packed = None
+        return self
+
     def _weights(self, device):
         if self._native_reason:
             raise NotImplementedError(self._native_reason)
@@ -272,13 +281,23 @@ class EGNNMultiChannel(nn.Module):
         return W
 
     # ------------------------------------------------------------ forward
-    def _trainable(self, N: int) -> bool:
-        """Shapes the native training step covers (csrc/egnn_train.hip check_train): 2 <= N <= 8
-        within 160 KiB of LDS; elsewhere a grad-mode forward returns the inference result, which
-        carries no autograd graph (loss.backward() then fails loudly)."""
+    def _untrainable_reason(self, N: int):
+        """None if the native training step (csrc/egnn_train.hip check_train) covers systems of N
+        bodies, else why not: 2 <= N <= 8 within 160 KiB of LDS, hidden % 4 == 0, 1-2 heads."""
         H, E = self.hidden_node_dim, N * (N - 1)
         lds = 2 * E * (2 * H + 8) + 3 * E * H + 10 * N * H + 512 + 16 * E + 32 * N
-        return 2 <= N <= 8 and H % 4 == 0 and lds * 4 <= 160 * 1024 and 1 <= len(self.heads) <= 2
+        if not 2 <= N <= 8:
+            return f"systems of N = {N} bodies (the native training step needs 2 <= N <= 8)"
+        if H % 4:
+            return f"hidden {H} (the native training step needs hidden % 4 == 0)"
+        if lds * 4 > 160 * 1024:
+            return f"hidden {H} at N = {N} needs {lds * 4} bytes of LDS per system (> 160 KiB)"
+        if not 1 <= len(self.heads) <= 2:
+            return f"{len(self.heads)} output heads (the native training step needs 1 or 2)"
+        return None
+
+    def _trainable(self, N: int) -> bool:
+        return self._untrainable_reason(N) is None
 
     def forward(self, graph):
         pos = graph.pos
@@ -293,12 +312,23 @@ class EGNNMultiChannel(nn.Module):
         mass = getattr(graph, "mass", None)
         m = f(mass.reshape(-1)) if mass is not None else torch.ones(V, device=device)
         p, v = f(pos), f(graph.vel)
-        if (knn is None and torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters())
-                and self._trainable(N)):
+        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()):
             # training step (trainer.py:233-358): the native forward keeps its activations and
-            # loss.backward() runs the native backward (csrc/egnn_train.hip)
+            # loss.backward() runs the native backward (csrc/egnn_train.hip).  Inputs it does not
+            # cover raise here, instead of returning an inference result without an autograd graph
+            # (whose parameters AdamW would silently skip).
             if self._native_reason:
                 raise NotImplementedError(self._native_reason)
+            if knn is not None:
+                raise NotImplementedError("native EGNN-MC training step: kNN graphs (num_neighbors < N-1) are not "
+                                          "supported; the training forward runs fully-connected systems")
+            why = self._untrainable_reason(N)
+            if why:
+                raise NotImplementedError("native EGNN-MC training step: " + why)
+            if any(q.dtype == torch.float64 for q in self.parameters()) and not getattr(self, "_warned_f64", False):
+                warnings.warn("EGNN-MC native training computes in fp32: float64 parameters (double_precision "
+                              "datasets) are cast to fp32 for the step and the gradients cast back", stacklevel=2)
+                self._warned_f64 = True
             params, idx, nblob = self._train_layout(device)
             return _EgnnTrainFn.apply(self, idx, nblob, p, v, m, B, N, *params).to(pos.dtype)
         out = torch.empty(V, 3 * len(self.heads), device=device, dtype=torch.float32)
@@ -396,6 +426,10 @@ class _EgnnTrainFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
+        if ctx.ws is None:
+            raise RuntimeError("EGNN-MC native training step: backward ran twice through the same forward "
+                               "(retain_graph=True is not supported: the activations are released after the "
+                               "first backward)")
         pos, vel, mass = ctx.saved_tensors
         device = pos.device
         g = grad_out.detach().to(device=device, dtype=torch.float32).contiguous()

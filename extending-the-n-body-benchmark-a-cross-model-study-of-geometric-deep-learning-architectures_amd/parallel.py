@@ -16,8 +16,8 @@ __all__ = ["init_from_env", "shard_range", "all_gather_shards", "max_over_ranks"
            "allreduce_gradients"]
 
 
-def world() -> int:
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+def world(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
 def rank() -> int:
@@ -95,19 +95,26 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20) -> Non
     on one device (trainer.py:233-358); this is the multi-GPU form of its optimizer step."""
     if world() == 1:
         return
-    params = [q for q in params if q.grad is not None]
-    n = world()
-    i = 0
-    while i < len(params):
-        bucket, size = [], 0
-        while i < len(params) and (not bucket or size + params[i].grad.numel() * 4 <= bucket_bytes):
-            bucket.append(params[i])
-            size += params[i].grad.numel() * 4
-            i += 1
-        flat = torch.cat([q.grad.reshape(-1) for q in bucket])
-        dist.all_reduce(flat, group=group)
-        flat /= n
-        o = 0
-        for q in bucket:
-            q.grad.copy_(flat[o:o + q.numel()].view_as(q.grad))
-            o += q.numel()
+    n = world(group) if group is not None else world()
+    # buckets hold one gradient dtype each (the reference trains in float64 by default,
+    # config.yaml precision_mode: double) and are sized by that dtype's element size
+    by_dtype = {}
+    for q in params:
+        if q.grad is not None:
+            by_dtype.setdefault((q.grad.dtype, q.grad.device), []).append(q)
+    for plist in by_dtype.values():
+        esz = plist[0].grad.element_size()
+        i = 0
+        while i < len(plist):
+            bucket, size = [], 0
+            while i < len(plist) and (not bucket or size + plist[i].grad.numel() * esz <= bucket_bytes):
+                bucket.append(plist[i])
+                size += plist[i].grad.numel() * esz
+                i += 1
+            flat = torch.cat([q.grad.reshape(-1) for q in bucket])
+            dist.all_reduce(flat, group=group)
+            flat /= n
+            o = 0
+            for q in bucket:
+                q.grad.copy_(flat[o:o + q.numel()].view_as(q.grad))
+                o += q.numel()

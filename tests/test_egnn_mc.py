@@ -247,7 +247,7 @@ def test_gpu_training_step_hip_graph_matches_eager(hip_device):
         if not graph:
             for _ in range(K):
                 body()
-            return params
+            return params, model
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -257,13 +257,21 @@ def test_gpu_training_step_hip_graph_matches_eager(hip_device):
         cg = torch.cuda.CUDAGraph()
         with torch.cuda.graph(cg):
             body()
+        with torch.no_grad():
+            model(gr)              # packs the inference weights at their current (pre-replay) values
         for _ in range(K - W):
             cg.replay()
         torch.cuda.synchronize()
-        return params
+        model.invalidate_weights()   # replays update the parameters without bumping _version
+        return params, model
 
-    for pe, pg in zip(run(False), run(True)):
+    (pe_all, me), (pg_all, mg) = run(False), run(True)
+    for pe, pg in zip(pe_all, pg_all):
         assert torch.allclose(pe, pg, rtol=1e-5, atol=1e-6), (pe - pg).abs().max().item()
+    # a no-grad (inference) forward after the replays sees the replayed weights
+    with torch.no_grad():
+        oe_, og_ = me(gr), mg(gr)
+    assert torch.allclose(oe_, og_, rtol=1e-4, atol=1e-5), (oe_ - og_).abs().max().item()
 
 
 
@@ -379,3 +387,31 @@ def test_gpu_rollout_knn_equals_repeated_oracle_forward(hip_device):
         want_p, want_v = p + pred[:, :3], pred[:, 3:]
         assert np.abs(tp[:, f].reshape(-1, 3) - want_p).max() <= 2e-4 * np.abs(want_p).max() + 1e-5
         assert np.abs(tv[:, f].reshape(-1, 3) - want_v).max() <= 2e-4 * np.abs(want_v).max() + 1e-5
+
+
+def test_grad_mode_forward_refuses_uncovered_training_inputs():
+    """A grad-mode forward the native training step does not cover raises NotImplementedError with
+    the reason: a kNN graph (the egnn_mc dataloader's num_neighbors < N-1) and N = 9
+    bodies (the step holds a system's activations in LDS for 2 <= N <= 8).  Before, such a forward
+    returned the inference result without an autograd graph, so every parameter's .grad stayed None
+    and AdamW skipped them silently.  Host logic only: the refusal comes before any device call."""
+    from oracle.graph import knn_edge_index
+    model = make(32, 2, torch.float32)
+    rng = np.random.default_rng(3)
+    B, N, k = 2, 6, 2
+    pos, vel = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3))
+    g = Graph()
+    g.pos, g.vel = torch.tensor(pos, dtype=torch.float32), torch.tensor(vel, dtype=torch.float32)
+    g.mass = torch.ones(B * N, 1)
+    g.edge_index = torch.from_numpy(knn_edge_index(pos, B, N, k))
+    g.batch = torch.arange(B).repeat_interleave(N)
+    with pytest.raises(NotImplementedError, match="kNN"):
+        model(g)
+    N = 9
+    g.pos, g.vel = torch.zeros(B * N, 3), torch.ones(B * N, 3)
+    g.mass = torch.ones(B * N, 1)
+    g.edge_index = torch.from_numpy(__import__("oracle.graph", fromlist=["x"]).fc_edge_index(B, N))
+    g.batch = torch.arange(B).repeat_interleave(N)
+    g.nbx_system_size = N          # (fully connected: skips the device-side edge_index comparison)
+    with pytest.raises(NotImplementedError, match="N = 9"):
+        model(g)
