@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so") 
 ABI_VERSION = 10
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
+GEMM_TRANS_A, GEMM_TRANS_B = 1, 2
 MAX_LAYERS = 64
 
 c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double,
@@ -119,6 +120,23 @@ _SIGNATURES = {
     "nbx_comm_init": (ctypes.c_int, [c_p, c_i32, c_i32, c_i32, ctypes.POINTER(c_p)]),
     "nbx_comm_destroy": (ctypes.c_int, [c_p]),
     "nbx_comm_allreduce_f64": (ctypes.c_int, [c_p, c_i64, c_p, c_p]),
+    "nbx_gemm_f32_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "nbx_gemm_f32": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_p, c_sz, c_p]),
+    "nbx_tp_prep": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "nbx_tp_prep_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p, c_p]),
+    "nbx_tp_post": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_tp_post_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_colsum_workspace_bytes": (ctypes.c_int, [c_i64, c_i32, ctypes.POINTER(c_sz)]),
+    "nbx_colsum": (ctypes.c_int, [c_i64, c_i32, c_p, c_i64, c_p, c_i32, c_p, c_sz, c_p]),
+    "nbx_bn_train_workspace_bytes": (ctypes.c_int, [c_i64, c_i32, ctypes.POINTER(c_sz)]),
+    "nbx_bn_train_forward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p,
+                                            c_sz, c_p]),
+    "nbx_bn_train_backward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz,
+                                             c_p]),
+    "nbx_gather_rows": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p]),
+    "nbx_segment_sum": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_i32, c_p]),
+    "nbx_segnn_train_featurize": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                                 c_p, c_p]),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),

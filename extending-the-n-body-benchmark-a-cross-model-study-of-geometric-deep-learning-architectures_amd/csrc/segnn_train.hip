@@ -1,0 +1,681 @@
+// SEGNN training step (trainer.py:233-358: pred = model(graph); loss.backward()) —
+// the native operators the training forward and backward are composed of (fp32).
+//
+// Reference: models/segnn/segnn.py:150-304, models/segnn/o3_building_blocks.py:10-278, e3nn
+// BatchNorm / Gate / FullyConnectedTensorProduct.  Every O(3) tensor product of
+// SEGNN (l <= 1) is written in one canonical form:
+//   S_in  = [XS | sum_k XV[k] * Y3[:, k]]                     (rows x (Ks + Kv))
+//   Zs    = S_in Ws^T,  Zv[k] = XV[k] Wv^T                      (MFMA GEMMs)
+//   scalar outputs  OS = Zs[:, :Ms] + b                  (gated: c_silu SiLU(.))
+//   vector outputs  OV[k] = Y3[:, k] * Zs[:, NSc + w] + Zv[k]  (gated: * c_sig sigmoid(Zs[:, Ms + w] + b))
+// with the e3nn path constants and the SH prefactors folded into Ws / Wv on the host (segnn.py
+// train_matrices), so the training forward is: GEMM (nbx_gemm_f32), the TP pre / post elementwise
+// kernels, e3nn batch-statistic BatchNorm, and row gathers / segment sums for message passing; the
+// backward is the same operators transposed.  Reductions (bias / BatchNorm / weight gradients,
+// aggregation) run in a fixed order: the training step is bit-reproducible.
+#include <algorithm>
+#include <cstring>
+
+#include "nbx_internal.h"
+
+namespace {
+
+using nbx::kC_SIGMOID;
+using nbx::kC_SILU;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------- GEMM (fp32 MFMA)
+// C[m][n] (+)= sum_k A(m, k) B(k, n);  A(m, k) = TA ? A[k lda + m] : A[m lda + k],
+// B(k, n) = TB ? B[n ldb + k] : B[k ldb + n].  Block tile 64 x 64, K step 16, four waves of a 32 x 32
+// v_mfma_f32_32x32x2_f32 tile each; the next K tile is loaded into registers while the current one
+// is multiplied from LDS.  Split-K (gridDim.z > 1): each z writes its partial tile into `part`
+// [z][M][N]; gemm_reduce_kernel sums them in z order.
+constexpr int GB = 64, GK = 16, GT = 256;
+
+struct GemmArgs {
+    const float* A;
+    const float* B;
+    float* C;
+    float* part;
+    int64_t M, N, K, lda, ldb, ldc;
+    int64_t kchunk;   // K range per split
+    float beta;
+};
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
+    __shared__ float As[2][GK][GB + 4];
+    __shared__ float Bs[2][GK][GB + 4];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t m0 = (int64_t)blockIdx.y * GB, n0 = (int64_t)blockIdx.x * GB;
+    const int64_t k_lo = (int64_t)blockIdx.z * g.kchunk;
+    const int64_t k_hi = std::min<int64_t>(g.K, k_lo + g.kchunk);
+    const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+    float ra[4], rb[4];
+    // thread -> (tile row, k) of its four loads: contiguous global dimension along the thread index
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int r, k;
+            if (TA) { k = t >> 4; r = (t & 15) * 4 + j; }   // A stored [K][M]: m contiguous
+            else { r = t >> 2; k = (t & 3) * 4 + j; }        // A stored [M][K]: k contiguous
+            const int64_t gm = m0 + r, gk = k0 + k;
+            ra[j] = (gm < g.M && gk < k_hi) ? (TA ? g.A[gk * g.lda + gm] : g.A[gm * g.lda + gk]) : 0.f;
+            int c, kb;
+            if (TB) { c = t >> 2; kb = (t & 3) * 4 + j; }   // B stored [N][K]: k contiguous
+            else { kb = t >> 4; c = (t & 15) * 4 + j; }      // B stored [K][N]: n contiguous
+            const int64_t gn = n0 + c, gkb = k0 + kb;
+            rb[j] = (gn < g.N && gkb < k_hi) ? (TB ? g.B[gn * g.ldb + gkb] : g.B[gkb * g.ldb + gn]) : 0.f;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (TA) As[buf][t >> 4][(t & 15) * 4 + j] = ra[j];
+            else As[buf][(t & 3) * 4 + j][t >> 2] = ra[j];
+            if (TB) Bs[buf][(t & 3) * 4 + j][t >> 2] = rb[j];
+            else Bs[buf][t >> 4][(t & 15) * 4 + j] = rb[j];
+        }
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const int64_t nk = (k_hi - k_lo + GK - 1) / GK;
+    if (nk > 0) {
+        load(k_lo);
+        store(0);
+        __syncthreads();
+        for (int64_t it = 0; it < nk; ++it) {
+            const int buf = (int)(it & 1);
+            if (it + 1 < nk) load(k_lo + (it + 1) * GK);
+#pragma unroll
+            for (int kk = 0; kk < GK; kk += 2) {
+                const float a = As[buf][kk + (lane >> 5)][wm + (lane & 31)];
+                const float b = Bs[buf][kk + (lane >> 5)][wn + (lane & 31)];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+            }
+            if (it + 1 < nk) store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // 32x32 accumulator: register i -> row 8 (i / 4) + 4 (lane / 32) + i % 4, column lane % 32
+    const int64_t col = n0 + wn + (lane & 31);
+    if (col >= g.N) return;
+    const bool split = gridDim.z > 1;
+    float* out = split ? g.part + (int64_t)blockIdx.z * g.M * g.N : g.C;
+    const int64_t ld = split ? g.N : g.ldc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t row = m0 + wm + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
+        if (row >= g.M) continue;
+        float* p = out + row * ld + col;
+        *p = (!split && g.beta != 0.f) ? acc[i] + g.beta * *p : acc[i];
+    }
+}
+
+__global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, int64_t M, int64_t N,
+                                   float* __restrict__ C, int64_t ldc, float beta) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= M * N) return;
+    const int64_t r = i / N, c = i - r * N;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += part[(int64_t)z * M * N + i];
+    float* p = C + r * ldc + c;
+    *p = beta != 0.f ? s + beta * *p : s;
+}
+
+int gemm_splits(int64_t M, int64_t N, int64_t K) {
+    const int64_t tiles = ((M + GB - 1) / GB) * ((N + GB - 1) / GB);
+    if (tiles >= 128 || K < 1024) return 1;
+    int64_t s = std::min<int64_t>((256 + tiles - 1) / tiles, K / 512);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(s, 32));
+}
+
+// ---------------------------------------------------------------- TP pre / post
+__global__ void tp_prep_kernel(int64_t rows, int Ks, int Kv, const float* __restrict__ XS, int64_t ldxs,
+                               const float* __restrict__ XV, int64_t pvs, const float* __restrict__ Y3,
+                               float* __restrict__ S) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int W = Ks + Kv;
+    if (i >= rows * W) return;
+    const int64_t r = i / W;
+    const int c = (int)(i - r * W);
+    float v;
+    if (c < Ks) {
+        v = XS[r * ldxs + c];
+    } else {
+        const int j = c - Ks;
+        const float* y = Y3 + 3 * r;
+        v = XV[r * Kv + j] * y[0] + XV[pvs + r * Kv + j] * y[1] + XV[2 * pvs + r * Kv + j] * y[2];
+    }
+    S[i] = v;
+}
+
+// dXS = dS[:, :Ks] (written); dXV[k] += Y3[:, k] * dS[:, Ks:] (accumulated onto the GEMM part)
+__global__ void tp_prep_bwd_kernel(int64_t rows, int Ks, int Kv, const float* __restrict__ dS,
+                                   const float* __restrict__ Y3, float* __restrict__ dXS, int64_t lddxs,
+                                   float* __restrict__ dXV, int64_t pvs) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int W = Ks + Kv;
+    if (i >= rows * W) return;
+    const int64_t r = i / W;
+    const int c = (int)(i - r * W);
+    const float d = dS[i];
+    if (c < Ks) {
+        if (dXS) dXS[r * lddxs + c] = d;
+    } else {
+        const int j = c - Ks;
+        const float* y = Y3 + 3 * r;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dXV[k * pvs + r * Kv + j] += y[k] * d;
+    }
+}
+
+struct TpPost {
+    int64_t rows;
+    int Ms, Nt, gate;     // NSc = Ms + (gate ? Nt : 0) scalar columns of Zs, then Nt t columns
+    const float* Zs;      // [rows][NSc + Nt]
+    const float* Zv;      // [3][rows][Nt]
+    const float* Y3;      // [rows][3]
+    const float* bias;    // [NSc] or null
+    const float* RS;      // residual [rows][Ms] or null
+    const float* RV;      // residual [3][rows][Nt] or null
+    float* OS;            // [rows][Ms]
+    float* OV;            // [3][rows][Nt]
+    // backward
+    const float* dOS;
+    const float* dOV;
+    float* dZs;
+    float* dZv;
+};
+
+__device__ inline float sig_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ void tp_post_kernel(TpPost p) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int W = p.Ms + p.Nt;
+    if (i >= p.rows * W) return;
+    const int64_t r = i / W;
+    const int c = (int)(i - r * W);
+    const int nsc = p.Ms + (p.gate ? p.Nt : 0), ldz = nsc + p.Nt;
+    if (c < p.Ms) {
+        float x = p.Zs[r * ldz + c] + (p.bias ? p.bias[c] : 0.f);
+        if (p.gate) x = kC_SILU * x * sig_f(x);
+        if (p.RS) x += p.RS[r * p.Ms + c];
+        p.OS[r * p.Ms + c] = x;
+        return;
+    }
+    const int w = c - p.Ms;
+    const int64_t pv = p.rows * p.Nt;
+    const float t = p.Zs[r * ldz + nsc + w];
+    const float* y = p.Y3 + 3 * r;
+    const float g = p.gate ? kC_SIGMOID * sig_f(p.Zs[r * ldz + p.Ms + w] + p.bias[p.Ms + w]) : 1.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int64_t o = k * pv + r * p.Nt + w;
+        float v = g * (y[k] * t + p.Zv[o]);
+        if (p.RV) v += p.RV[o];
+        p.OV[o] = v;
+    }
+}
+
+__global__ void tp_post_bwd_kernel(TpPost p) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int W = p.Ms + p.Nt;
+    if (i >= p.rows * W) return;
+    const int64_t r = i / W;
+    const int c = (int)(i - r * W);
+    const int nsc = p.Ms + (p.gate ? p.Nt : 0), ldz = nsc + p.Nt;
+    if (c < p.Ms) {
+        const float d = p.dOS[r * p.Ms + c];
+        float dz = d;
+        if (p.gate) {
+            const float x = p.Zs[r * ldz + c] + p.bias[c];
+            const float s = sig_f(x);
+            dz = d * kC_SILU * s * (1.0f + x * (1.0f - s));
+        }
+        p.dZs[r * ldz + c] = dz;
+        return;
+    }
+    const int w = c - p.Ms;
+    const int64_t pv = p.rows * p.Nt;
+    const float t = p.Zs[r * ldz + nsc + w];
+    const float* y = p.Y3 + 3 * r;
+    float g = 1.f, dg = 0.f, sg = 0.f;
+    if (p.gate) {
+        sg = sig_f(p.Zs[r * ldz + p.Ms + w] + p.bias[p.Ms + w]);
+        g = kC_SIGMOID * sg;
+    }
+    float dt = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int64_t o = k * pv + r * p.Nt + w;
+        const float dov = p.dOV[o];
+        const float dv = g * dov;
+        p.dZv[o] = dv;
+        dt += y[k] * dv;
+        if (p.gate) dg += dov * (y[k] * t + p.Zv[o]);
+    }
+    p.dZs[r * ldz + nsc + w] = dt;
+    if (p.gate) p.dZs[r * ldz + p.Ms + w] = dg * kC_SIGMOID * sg * (1.0f - sg);
+}
+
+// ---------------------------------------------------------------- column sums (bias gradients)
+// out[c] = sum_r X[r][c], fixed order: blocks of CS_ROWS rows -> partial rows -> one pass
+constexpr int CS_ROWS = 256;
+__global__ void colsum_partial_kernel(int64_t rows, int cols, const float* __restrict__ X, int64_t ld,
+                                      double* __restrict__ part) {
+    const int c = blockIdx.y * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS, r1 = std::min<int64_t>(rows, r0 + CS_ROWS);
+    double s = 0.0;
+    for (int64_t r = r0; r < r1; ++r) s += X[r * ld + c];
+    part[(int64_t)blockIdx.x * cols + c] = s;
+}
+
+__global__ void colsum_final_kernel(int nb, int cols, const double* __restrict__ part, float* __restrict__ out,
+                                    int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += part[(int64_t)b * cols + c];
+    out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+// ---------------------------------------------------------------- e3nn BatchNorm, batch statistics
+// S [rows][M] (0e channels), V [3][rows][M] (1o channels).  Forward partial sums per block of BN_ROWS
+// rows: (sum s, sum s^2, sum |v|^2); backward: (sum dy_s, sum dy_s * xhat, sum dy_v . v).
+constexpr int BN_ROWS = 128;
+__global__ void bn_partial_kernel(int64_t rows, int M, const float* __restrict__ S, const float* __restrict__ V,
+                                  const float* __restrict__ dS, const float* __restrict__ dV,
+                                  const float* __restrict__ save, double* __restrict__ part) {
+    const int c = blockIdx.y * blockDim.x + threadIdx.x;
+    if (c >= M) return;
+    const int64_t r0 = (int64_t)blockIdx.x * BN_ROWS, r1 = std::min<int64_t>(rows, r0 + BN_ROWS);
+    const int64_t pv = rows * M;
+    double a = 0.0, b = 0.0, e = 0.0;
+    if (!dS) {
+        for (int64_t r = r0; r < r1; ++r) {
+            const double s = S[r * M + c];
+            a += s;
+            b += s * s;
+            const float v0 = V[r * M + c], v1 = V[pv + r * M + c], v2 = V[2 * pv + r * M + c];
+            e += (double)v0 * v0 + (double)v1 * v1 + (double)v2 * v2;
+        }
+    } else {
+        const float mu = save[c], inv = save[M + c];
+        for (int64_t r = r0; r < r1; ++r) {
+            const double d = dS[r * M + c];
+            a += d;
+            b += d * (double)((S[r * M + c] - mu) * inv);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) e += (double)dV[k * pv + r * M + c] * V[k * pv + r * M + c];
+        }
+    }
+    double* p = part + (int64_t)blockIdx.x * 3 * M;
+    p[c] = a;
+    p[M + c] = b;
+    p[2 * M + c] = e;
+}
+
+// save [3][M] = (mu, 1/sqrt(var + eps), 1/sqrt(n + eps)); running stats r <- (1 - m) r + m stat
+__global__ void bn_stats_kernel(int nb, int64_t rows, int M, const double* __restrict__ part, float eps,
+                                float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
+                                float* __restrict__ save) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= M) return;
+    double a = 0.0, b = 0.0, e = 0.0;
+    for (int i = 0; i < nb; ++i) {
+        const double* p = part + (int64_t)i * 3 * M;
+        a += p[c];
+        b += p[M + c];
+        e += p[2 * M + c];
+    }
+    const double mu = a / rows;
+    double var = b / rows - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const double n = e / (3.0 * rows);
+    save[c] = (float)mu;
+    save[M + c] = (float)(1.0 / sqrt(var + (double)eps));
+    save[2 * M + c] = (float)(1.0 / sqrt(n + (double)eps));
+    if (rmean) {
+        rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mu;
+        rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)var;
+        rvar[M + c] = (1.0f - momentum) * rvar[M + c] + momentum * (float)n;
+    }
+}
+
+__global__ void bn_apply_train_kernel(int64_t rows, int M, const float* __restrict__ S, const float* __restrict__ V,
+                                      const float* __restrict__ save, const float* __restrict__ weight,
+                                      const float* __restrict__ bias, float* __restrict__ OS, float* __restrict__ OV) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= rows * M) return;
+    const int c = (int)(i % M);
+    const int64_t pv = rows * M;
+    OS[i] = (S[i] - save[c]) * save[M + c] * weight[c] + bias[c];
+    const float sv = save[2 * M + c] * weight[M + c];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) OV[k * pv + i] = V[k * pv + i] * sv;
+}
+
+// sums [3][M] of the backward partials -> (dS, dV) and the parameter gradients
+__global__ void bn_bwd_apply_kernel(int64_t rows, int M, const float* __restrict__ S, const float* __restrict__ V,
+                                    const float* __restrict__ save, const float* __restrict__ weight,
+                                    const double* __restrict__ sums, const float* __restrict__ dOS,
+                                    const float* __restrict__ dOV, float* __restrict__ dS, float* __restrict__ dV) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= rows * M) return;
+    const int c = (int)(i % M);
+    const int64_t pv = rows * M;
+    const float mu = save[c], inv = save[M + c], invv = save[2 * M + c];
+    const float mdy = (float)(sums[c] / rows), mdyx = (float)(sums[M + c] / rows);
+    const float xh = (S[i] - mu) * inv;
+    dS[i] = weight[c] * inv * (dOS[i] - mdy - xh * mdyx);
+    const float wv = weight[M + c];
+    const float cv = (float)(sums[2 * M + c] / (3.0 * rows)) * invv * invv;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dV[k * pv + i] = wv * invv * (dOV[k * pv + i] - V[k * pv + i] * cv);
+}
+
+__global__ void bn_param_grad_kernel(int nb, int M, const double* __restrict__ part, const float* __restrict__ save,
+                                     double* __restrict__ sums, float* __restrict__ dweight,
+                                     float* __restrict__ dbias) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= M) return;
+    double a = 0.0, b = 0.0, e = 0.0;
+    for (int i = 0; i < nb; ++i) {
+        const double* p = part + (int64_t)i * 3 * M;
+        a += p[c];
+        b += p[M + c];
+        e += p[2 * M + c];
+    }
+    sums[c] = a;
+    sums[M + c] = b;
+    sums[2 * M + c] = e;
+    dbias[c] = (float)a;
+    dweight[c] = (float)b;
+    dweight[M + c] = (float)(e * save[2 * M + c]);
+}
+
+// ---------------------------------------------------------------- gathers and segment sums
+// out[r][c] = in[idx[r]][c] per plane
+__global__ void gather_rows_kernel(int64_t n, int cols, const int* __restrict__ idx, const float* __restrict__ in,
+                                   int64_t ldi, int64_t psi, float* __restrict__ out, int64_t ldo, int64_t pso,
+                                   int planes) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n * cols) return;
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    const int64_t s = idx[r];
+    for (int k = 0; k < planes; ++k) out[k * pso + r * ldo + c] = in[k * psi + s * ldi + c];
+}
+
+// out[n][c] (+)= sum_{j in [ptr[n], ptr[n+1])} in[eid[j]][c] per plane, in CSR order
+__global__ void segment_sum_kernel(int64_t n, int cols, const int* __restrict__ ptr, const int* __restrict__ eid,
+                                   const float* __restrict__ in, int64_t ldi, int64_t psi, float* __restrict__ out,
+                                   int64_t ldo, int64_t pso, int planes, int accumulate) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n * cols) return;
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    const int j0 = ptr[r], j1 = ptr[r + 1];
+    for (int k = 0; k < planes; ++k) {
+        float s = 0.f;
+        for (int j = j0; j < j1; ++j) s += in[k * psi + (int64_t)eid[j] * ldi + c];
+        float* o = out + k * pso + r * ldo + c;
+        *o = accumulate ? *o + s : s;
+    }
+}
+
+// ---------------------------------------------------------------- featurisation (no gradient)
+// O3Transform (o3_building_blocks.py:231-278) + catch_isolated_nodes (segnn.py:136-148) on an edge
+// list: rel = pos[src] - pos[dst]; node attribute = mean over the incoming edges (dst CSR) of
+// SH(rel) + SH(vel), column 0 forced to 1 -> na3 = its l=1 part [V][3];  embedding input
+// XS0 = |vel| [V], XV0 [3][V][2] = (pos - mean_xyz(pos), vel) per component; edges:
+// rhat [E][3], amf [E][2] = (|rel|, m_src m_dst).
+constexpr float kSH1 = nbx::kSH_C1;
+__global__ void train_featurize_kernel(int64_t V, int64_t E, const float* __restrict__ pos,
+                                       const float* __restrict__ vel, const float* __restrict__ mass,
+                                       const int* __restrict__ src, const int* __restrict__ dst,
+                                       const int* __restrict__ dptr, const int* __restrict__ deid,
+                                       float* __restrict__ na3, float* __restrict__ xs0, float* __restrict__ xv0,
+                                       float* __restrict__ rhat, float* __restrict__ amf) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < E) {
+        const int64_t s = src[i], d = dst[i];
+        const float rx = pos[3 * s] - pos[3 * d], ry = pos[3 * s + 1] - pos[3 * d + 1];
+        const float rz = pos[3 * s + 2] - pos[3 * d + 2];
+        const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+        const float inv = 1.0f / fmaxf(dist, 1e-12f);
+        rhat[3 * i] = rx * inv;
+        rhat[3 * i + 1] = ry * inv;
+        rhat[3 * i + 2] = rz * inv;
+        amf[2 * i] = dist;
+        amf[2 * i + 1] = mass[s] * mass[d];
+    }
+    if (i < V) {
+        const float px = pos[3 * i], py = pos[3 * i + 1], pz = pos[3 * i + 2];
+        float ax = 0.f, ay = 0.f, az = 0.f;
+        const int j0 = dptr[i], j1 = dptr[i + 1];
+        for (int j = j0; j < j1; ++j) {
+            const int64_t s = src[deid[j]];
+            const float rx = pos[3 * s] - px, ry = pos[3 * s + 1] - py, rz = pos[3 * s + 2] - pz;
+            const float inv = 1.0f / fmaxf(sqrtf(rx * rx + ry * ry + rz * rz), 1e-12f);
+            ax += kSH1 * rx * inv; ay += kSH1 * ry * inv; az += kSH1 * rz * inv;
+        }
+        const float cnt = (float)(j1 - j0);
+        const float ic = cnt > 0.f ? 1.0f / cnt : 0.f;
+        const float vx = vel[3 * i], vy = vel[3 * i + 1], vz = vel[3 * i + 2];
+        const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
+        const float vd = 1.0f / fmaxf(vn, 1e-12f);
+        na3[3 * i] = ax * ic + kSH1 * vx * vd;
+        na3[3 * i + 1] = ay * ic + kSH1 * vy * vd;
+        na3[3 * i + 2] = az * ic + kSH1 * vz * vd;
+        xs0[i] = vn;
+        const float mp = (px + py + pz) / 3.0f;   // pos.mean(1): mean over xyz (reference quirk)
+        const float pc[3] = {px - mp, py - mp, pz - mp}, vv[3] = {vx, vy, vz};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            xv0[(k * V + i) * 2] = pc[k];
+            xv0[(k * V + i) * 2 + 1] = vv[k];
+        }
+    }
+}
+
+unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+}  // namespace
+
+// ======================================================================== C ABI (include/nbx.h)
+extern "C" int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes) {
+    NBX_CHECK_ARG(bytes != nullptr && M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_workspace_bytes: bad arguments");
+    const int s = gemm_splits(M, N, K);
+    *bytes = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+    return NBX_OK;
+}
+
+extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                            const float* B, int64_t ldb, float* C, int64_t ldc, float beta, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+    NBX_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32: negative size");
+    NBX_CHECK_ARG(beta == 0.f || beta == 1.f, "nbx_gemm_f32: beta must be 0 or 1");
+    if (M == 0 || N == 0) return NBX_OK;
+    NBX_CHECK_ARG(A && B && C, "nbx_gemm_f32: null operand");
+    const bool ta = flags & NBX_GEMM_TRANS_A, tb = flags & NBX_GEMM_TRANS_B;
+    NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N, "nbx_gemm_f32: leading dimension too small");
+    const int splits = gemm_splits(M, N, K);
+    const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+    NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
+                  workspace_bytes, need);
+    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta};
+    g.kchunk = (g.kchunk + GK - 1) / GK * GK;
+    const dim3 grid((unsigned)((N + GB - 1) / GB), (unsigned)((M + GB - 1) / GB), (unsigned)splits);
+    hipStream_t st = (hipStream_t)stream;
+    if (ta && tb) hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(GT), 0, st, g);
+    else if (ta) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(GT), 0, st, g);
+    else if (tb) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(GT), 0, st, g);
+    else hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(GT), 0, st, g);
+    NBX_LAUNCH_CHECK("gemm_f32");
+    if (splits > 1) {
+        hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,
+                           N, C, ldc, beta);
+        NBX_LAUNCH_CHECK("gemm_reduce");
+    }
+    return NBX_OK;
+}
+
+extern "C" int nbx_tp_prep(int64_t rows, int32_t Ks, int32_t Kv, const float* XS, int64_t ldxs, const float* XV,
+                           const float* Y3, float* S, void* stream) {
+    NBX_CHECK_ARG(rows >= 0 && Ks >= 0 && Kv >= 0 && ldxs >= Ks, "nbx_tp_prep: bad sizes");
+    if (rows == 0 || Ks + Kv == 0) return NBX_OK;
+    hipLaunchKernelGGL(tp_prep_kernel, dim3(nblk(rows * (Ks + Kv))), dim3(256), 0, (hipStream_t)stream, rows, Ks, Kv,
+                       XS, ldxs, XV, rows * Kv, Y3, S);
+    NBX_LAUNCH_CHECK("tp_prep");
+    return NBX_OK;
+}
+
+extern "C" int nbx_tp_prep_backward(int64_t rows, int32_t Ks, int32_t Kv, const float* dS, const float* Y3,
+                                    float* dXS, int64_t lddxs, float* dXV, void* stream) {
+    NBX_CHECK_ARG(rows >= 0 && Ks >= 0 && Kv >= 0, "nbx_tp_prep_backward: bad sizes");
+    if (rows == 0 || Ks + Kv == 0) return NBX_OK;
+    NBX_CHECK_ARG(Kv == 0 || dXV, "nbx_tp_prep_backward: null dXV");
+    hipLaunchKernelGGL(tp_prep_bwd_kernel, dim3(nblk(rows * (Ks + Kv))), dim3(256), 0, (hipStream_t)stream, rows, Ks,
+                       Kv, dS, Y3, dXS, lddxs, dXV, rows * Kv);
+    NBX_LAUNCH_CHECK("tp_prep_backward");
+    return NBX_OK;
+}
+
+extern "C" int nbx_tp_post(int64_t rows, int32_t Ms, int32_t Nt, int32_t gate, const float* Zs, const float* Zv,
+                           const float* Y3, const float* bias, const float* RS, const float* RV, float* OS, float* OV,
+                           void* stream) {
+    NBX_CHECK_ARG(rows >= 0 && Ms >= 0 && Nt >= 0, "nbx_tp_post: bad sizes");
+    NBX_CHECK_ARG(!gate || (bias && Ms > 0 && Nt > 0), "nbx_tp_post: a gated TP needs scalars, gates and a bias");
+    if (rows == 0 || Ms + Nt == 0) return NBX_OK;
+    TpPost p{rows, Ms, Nt, gate, Zs, Zv, Y3, bias, RS, RV, OS, OV, nullptr, nullptr, nullptr, nullptr};
+    hipLaunchKernelGGL(tp_post_kernel, dim3(nblk(rows * (Ms + Nt))), dim3(256), 0, (hipStream_t)stream, p);
+    NBX_LAUNCH_CHECK("tp_post");
+    return NBX_OK;
+}
+
+extern "C" int nbx_tp_post_backward(int64_t rows, int32_t Ms, int32_t Nt, int32_t gate, const float* Zs,
+                                    const float* Zv, const float* Y3, const float* bias, const float* dOS,
+                                    const float* dOV, float* dZs, float* dZv, void* stream) {
+    NBX_CHECK_ARG(rows >= 0 && Ms >= 0 && Nt >= 0, "nbx_tp_post_backward: bad sizes");
+    NBX_CHECK_ARG(!gate || (bias && Ms > 0 && Nt > 0), "nbx_tp_post_backward: a gated TP needs a bias");
+    if (rows == 0 || Ms + Nt == 0) return NBX_OK;
+    TpPost p{rows, Ms, Nt, gate, Zs, Zv, Y3, bias, nullptr, nullptr, nullptr, nullptr, dOS, dOV, dZs, dZv};
+    hipLaunchKernelGGL(tp_post_bwd_kernel, dim3(nblk(rows * (Ms + Nt))), dim3(256), 0, (hipStream_t)stream, p);
+    NBX_LAUNCH_CHECK("tp_post_backward");
+    return NBX_OK;
+}
+
+extern "C" int nbx_colsum_workspace_bytes(int64_t rows, int32_t cols, size_t* bytes) {
+    NBX_CHECK_ARG(bytes && rows >= 0 && cols >= 0, "nbx_colsum_workspace_bytes: bad arguments");
+    *bytes = (size_t)std::max<int64_t>(1, (rows + CS_ROWS - 1) / CS_ROWS) * cols * sizeof(double);
+    return NBX_OK;
+}
+
+extern "C" int nbx_colsum(int64_t rows, int32_t cols, const float* X, int64_t ld, float* out, int32_t accumulate,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+    NBX_CHECK_ARG(rows >= 0 && cols >= 0 && ld >= cols, "nbx_colsum: bad sizes");
+    if (cols == 0) return NBX_OK;
+    const int nb = (int)std::max<int64_t>(1, (rows + CS_ROWS - 1) / CS_ROWS);
+    NBX_CHECK_ARG(workspace && workspace_bytes >= (size_t)nb * cols * sizeof(double), "nbx_colsum: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    double* part = (double*)workspace;
+    if (rows == 0) {
+        NBX_HIP(hipMemsetAsync(part, 0, (size_t)cols * sizeof(double), st));
+    } else {
+        hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)nb, (unsigned)((cols + 255) / 256)), dim3(256), 0, st,
+                           rows, cols, X, ld, part);
+        NBX_LAUNCH_CHECK("colsum_partial");
+    }
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(nblk(cols)), dim3(256), 0, st, nb, cols, part, out, accumulate);
+    NBX_LAUNCH_CHECK("colsum_final");
+    return NBX_OK;
+}
+
+extern "C" int nbx_bn_train_workspace_bytes(int64_t rows, int32_t M, size_t* bytes) {
+    NBX_CHECK_ARG(bytes && rows >= 0 && M >= 0, "nbx_bn_train_workspace_bytes: bad arguments");
+    *bytes = ((size_t)std::max<int64_t>(1, (rows + BN_ROWS - 1) / BN_ROWS) + 1) * 3 * M * sizeof(double);
+    return NBX_OK;
+}
+
+extern "C" int nbx_bn_train_forward(int64_t rows, int32_t M, const float* S, const float* V, const float* weight,
+                                    const float* bias, float* running_mean, float* running_var, float eps,
+                                    float momentum, float* save, float* OS, float* OV, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+    NBX_CHECK_ARG(rows > 0 && M > 0, "nbx_bn_train_forward: need rows > 0 and M > 0");
+    const int nb = (int)((rows + BN_ROWS - 1) / BN_ROWS);
+    NBX_CHECK_ARG(workspace && workspace_bytes >= (size_t)(nb + 1) * 3 * M * sizeof(double),
+                  "nbx_bn_train_forward: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    double* part = (double*)workspace;
+    const unsigned cb = (unsigned)((M + 127) / 128);
+    hipLaunchKernelGGL(bn_partial_kernel, dim3((unsigned)nb, cb), dim3(128), 0, st, rows, M, S, V, nullptr, nullptr,
+                       nullptr, part);
+    NBX_LAUNCH_CHECK("bn_partial");
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk(M)), dim3(256), 0, st, nb, rows, M, part, eps, momentum, running_mean,
+                       running_var, save);
+    NBX_LAUNCH_CHECK("bn_stats");
+    hipLaunchKernelGGL(bn_apply_train_kernel, dim3(nblk(rows * M)), dim3(256), 0, st, rows, M, S, V, save, weight, bias,
+                       OS, OV);
+    NBX_LAUNCH_CHECK("bn_apply_train");
+    return NBX_OK;
+}
+
+extern "C" int nbx_bn_train_backward(int64_t rows, int32_t M, const float* S, const float* V, const float* weight,
+                                     const float* save, const float* dOS, const float* dOV, float* dS, float* dV,
+                                     float* dweight, float* dbias, void* workspace, size_t workspace_bytes,
+                                     void* stream) {
+    NBX_CHECK_ARG(rows > 0 && M > 0, "nbx_bn_train_backward: need rows > 0 and M > 0");
+    const int nb = (int)((rows + BN_ROWS - 1) / BN_ROWS);
+    NBX_CHECK_ARG(workspace && workspace_bytes >= (size_t)(nb + 1) * 3 * M * sizeof(double),
+                  "nbx_bn_train_backward: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    double* part = (double*)workspace;
+    double* sums = part + (size_t)nb * 3 * M;
+    const unsigned cb = (unsigned)((M + 127) / 128);
+    hipLaunchKernelGGL(bn_partial_kernel, dim3((unsigned)nb, cb), dim3(128), 0, st, rows, M, S, V, dOS, dOV, save, part);
+    NBX_LAUNCH_CHECK("bn_partial(bwd)");
+    hipLaunchKernelGGL(bn_param_grad_kernel, dim3(nblk(M)), dim3(256), 0, st, nb, M, part, save, sums, dweight, dbias);
+    NBX_LAUNCH_CHECK("bn_param_grad");
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(rows * M)), dim3(256), 0, st, rows, M, S, V, save, weight, sums,
+                       dOS, dOV, dS, dV);
+    NBX_LAUNCH_CHECK("bn_bwd_apply");
+    return NBX_OK;
+}
+
+extern "C" int nbx_gather_rows(int64_t n, int32_t cols, const int32_t* idx, const float* in, int64_t ld_in,
+                               int64_t plane_in, float* out, int64_t ld_out, int64_t plane_out, int32_t planes,
+                               void* stream) {
+    NBX_CHECK_ARG(n >= 0 && cols >= 0 && planes >= 1 && ld_in >= cols && ld_out >= cols, "nbx_gather_rows: bad sizes");
+    if (n == 0 || cols == 0) return NBX_OK;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(nblk(n * cols)), dim3(256), 0, (hipStream_t)stream, n, cols, idx, in,
+                       ld_in, plane_in, out, ld_out, plane_out, planes);
+    NBX_LAUNCH_CHECK("gather_rows");
+    return NBX_OK;
+}
+
+extern "C" int nbx_segment_sum(int64_t n, int32_t cols, const int32_t* ptr, const int32_t* eid, const float* in,
+                               int64_t ld_in, int64_t plane_in, float* out, int64_t ld_out, int64_t plane_out,
+                               int32_t planes, int32_t accumulate, void* stream) {
+    NBX_CHECK_ARG(n >= 0 && cols >= 0 && planes >= 1 && ld_in >= cols && ld_out >= cols, "nbx_segment_sum: bad sizes");
+    if (n == 0 || cols == 0) return NBX_OK;
+    hipLaunchKernelGGL(segment_sum_kernel, dim3(nblk(n * cols)), dim3(256), 0, (hipStream_t)stream, n, cols, ptr, eid, in,
+                       ld_in, plane_in, out, ld_out, plane_out, planes, accumulate);
+    NBX_LAUNCH_CHECK("segment_sum");
+    return NBX_OK;
+}
+
+extern "C" int nbx_segnn_train_featurize(int64_t V, int64_t E, const float* pos, const float* vel, const float* mass,
+                                         const int32_t* src, const int32_t* dst, const int32_t* dst_ptr,
+                                         const int32_t* dst_eid, float* na3, float* xs0, float* xv0, float* rhat,
+                                         float* amf, void* stream) {
+    NBX_CHECK_ARG(V >= 1 && E >= 0, "nbx_segnn_train_featurize: bad sizes");
+    hipLaunchKernelGGL(train_featurize_kernel, dim3(nblk(std::max(V, E))), dim3(256), 0, (hipStream_t)stream, V, E, pos,
+                       vel, mass, src, dst, dst_ptr, dst_eid, na3, xs0, xv0, rhat, amf);
+    NBX_LAUNCH_CHECK("segnn_train_featurize");
+    return NBX_OK;
+}

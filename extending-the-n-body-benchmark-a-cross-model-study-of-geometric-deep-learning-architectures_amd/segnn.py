@@ -225,6 +225,59 @@ class SEGNN(nn.Module):
         P["pp2"] = vec(torch.stack([Ws[:, 0], Ws[:, 1], Wv[:, 0], Wv[:, 1]]))
         return P
 
+    def train_matrices(self, device):
+        """The operands of the training step's canonical tensor products (include/nbx.h "SEGNN
+        training step"; segnn_train.py), built from the e3nn parameters with differentiable torch
+        ops: ``<tp>_s`` = Ws [NSc + Nt][Ks + Kv], ``<tp>_v`` = Wv [Nt][Kv], ``<tp>_bias``.  Same
+        constants as packed_matrices; message_layer_1 unfactored, its input being
+        [x_i s | x_j s | amf | x_i v . rhat | x_j v . rhat] and [x_i v | x_j v] per edge."""
+        M = self.mul
+        f32 = dict(device=device, dtype=torch.float32)
+
+        def views(tpmod):
+            return [w.to(**f32)[:, 0, :] for w in tpmod.tp.weight_views()]   # [mul1, mul_out]
+
+        def T(x):
+            return x.t().contiguous()
+
+        z = lambda r, c: torch.zeros(r, c, **f32)
+        P = {}
+        Wa, Wb, Wc, Wd = views(self.embedding_layer)          # S_in = [|v| | pos_c . na | vel . na]
+        P["emb_s"] = T(torch.cat([torch.stack([Wc[0], Wb[0] * INV_SQRT3, Wb[1] * INV_SQRT3]),
+                                  torch.stack([Wd[0], Wd[0] * 0, Wd[0] * 0])], 1))
+        P["emb_v"] = T(Wa)
+        P["emb_bias"] = self.embedding_layer.biases.to(**f32)
+        for li, layer in enumerate(self.layers):
+            p = f"layers.{li}."
+            WA0, WA1, WB0, WB1, WC0, WC1, WD0, WD1, WE0, WE1 = views(layer.message_layer_1)
+            s_blk = torch.cat([SH_C0 * WA0, SH_C0 * WC0, SH_C0 * WE0, SH_C1 * INV_SQRT3 * WB1, SH_C1 * INV_SQRT3 * WD1])
+            t_blk = torch.cat([SH_C1 * WA1, SH_C1 * WC1, SH_C1 * WE1, z(2 * M, M)])
+            P[p + "msg1_s"] = T(torch.cat([s_blk, t_blk], 1))
+            P[p + "msg1_v"] = T(torch.cat([SH_C0 * WB0, SH_C0 * WD0]))
+            P[p + "msg1_bias"] = layer.message_layer_1.biases.to(**f32)
+            W1, W2, W3, W4 = views(layer.message_layer_2)
+            P[p + "msg2_s"] = T(torch.cat([torch.cat([SH_C0 * W1, SH_C1 * INV_SQRT3 * W4]),
+                                           torch.cat([SH_C1 * W2, z(M, M)])], 1))
+            P[p + "msg2_v"] = T(SH_C0 * W3)
+            P[p + "msg2_bias"] = layer.message_layer_2.biases.to(**f32)
+            Xs0, Xs1, Xv0, Xv1, As0, As1, Av0, Av1 = views(layer.update_layer_1)
+            P[p + "upd1_s"] = T(torch.cat([torch.cat([Xs0, As0, INV_SQRT3 * Xv1, INV_SQRT3 * Av1]),
+                                           torch.cat([Xs1, As1, z(2 * M, M)])], 1))
+            P[p + "upd1_v"] = T(torch.cat([Xv0, Av0]))
+            P[p + "upd1_bias"] = layer.update_layer_1.biases.to(**f32)
+            U1, U2, U3, U4 = views(layer.update_layer_2)
+            P[p + "upd2_s"] = T(torch.cat([torch.cat([U1, INV_SQRT3 * U4]), torch.cat([U2, z(M, M)])], 1))
+            P[p + "upd2_v"] = T(U3)
+            P[p + "upd2_bias"] = layer.update_layer_2.biases.to(**f32)
+        P1, P2, P3, P4 = views(self.pre_pool1)
+        P["pp1_s"] = T(torch.cat([torch.cat([P1, INV_SQRT3 * P4]), torch.cat([P2, z(M, M)])], 1))
+        P["pp1_v"] = T(P3)
+        P["pp1_bias"] = self.pre_pool1.biases.to(**f32)
+        Ws, Wv = views(self.pre_pool2)
+        P["pp2_s"] = T(torch.cat([Ws, z(M, 2)]))
+        P["pp2_v"] = T(Wv)
+        return P
+
     # ------------------------------------------------------------ LDS images (include/nbx.h)
     @staticmethod
     def frag_image(subs, vec, cw: int, chunks: int) -> torch.Tensor:
@@ -503,6 +556,14 @@ class SEGNN(nn.Module):
         self._check_params(device)
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
         p, v, m = f(pos), f(graph.vel), f(graph.mass.reshape(-1))
+        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()):
+            # training step (trainer.py:233-358): the forward runs on the native training operators
+            # with autograd (segnn_train.py), so loss.backward() reaches every parameter
+            if self._bn_group is not None and self._bn_batch():
+                raise NotImplementedError("native SEGNN training step: SyncBN is not supported (per-rank "
+                                          "BatchNorm statistics, data-parallel gradients)")
+            from . import segnn_train
+            return segnn_train.train_forward(self, p, v, m, edge_index).to(out_dtype)
         out = torch.empty(V, 6, device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(B, N, device)

@@ -1,0 +1,314 @@
+"""SEGNN training step on the native operators.
+
+The reference trains SEGNN with ``pred = model(graph); loss.backward(); optimizer.step()``
+(trainer.py:233-358) in train mode (batch-statistic BatchNorm, segnn.py:233-235,257-261).  Here a
+grad-mode ``SEGNN.forward`` (segnn.py) runs :func:`train_forward`: the forward of
+models/segnn/segnn.py:150-304 composed of the libnbx training operators (include/nbx.h "SEGNN
+training step", csrc/segnn_train.hip) inside ``torch.autograd.Function`` s whose backward passes
+call the same library, so ``loss.backward()`` lands on every ``nn.Parameter`` of the reference's
+module tree (tensor-product weights, biases, BatchNorm weight / bias):
+
+* every O(3) tensor product (o3_building_blocks.py:10-203) = ``_TPFn``: tp_prep, two MFMA GEMMs
+  (scalar rows, vector component planes), tp_post (bias, e3nn Gate, residual); backward: tp_post
+  backward, four GEMMs (input and weight gradients), a column sum (bias), tp_prep backward;
+* e3nn BatchNorm with batch statistics = ``_BNFn`` (fixed-order fp64 reductions, the running
+  statistics updated in place like the reference module);
+* message passing (x_i = x[dst], x_j = x[src], aggr="add" at edge_index[1]) = ``_GatherFn`` /
+  ``_SegSumFn`` over CSR tables of the edges by destination and by source (deterministic).
+
+The weight operands come from the e3nn parameters through differentiable torch ops
+(``SEGNN.train_matrices``), so the gradient of the packed operands flows back to the parameters.
+Arithmetic is fp32 (a float64 module is cast for the step, like its fp32 inference path).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+_f32 = torch.float32
+
+
+def _dp(t):
+    return _lib.dev_ptr(t) if t is not None else None
+
+
+def _st(t):
+    return _lib.stream_ptr(t.device)
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def gemm(flags, M, N, K, A, lda, B, ldb, C, ldc, beta=0.0):
+    """C = op(A) op(B) (+ C) through nbx_gemm_f32 (include/nbx.h)."""
+    L = _lib.lib()
+    n = _lib.c_sz()
+    _lib.check(L.nbx_gemm_f32_workspace_bytes(M, N, K, ctypes.byref(n)), "nbx_gemm_f32_workspace_bytes")
+    ws = _ws(n.value, C.device) if n.value else None
+    _lib.check(L.nbx_gemm_f32(flags, M, N, K, _dp(A), lda, _dp(B), ldb, _dp(C), ldc, float(beta), _dp(ws),
+                              n.value, _st(C)), "nbx_gemm_f32")
+    return C
+
+
+def colsum(X, rows, cols, ld, out, accumulate=False):
+    L = _lib.lib()
+    n = _lib.c_sz()
+    _lib.check(L.nbx_colsum_workspace_bytes(rows, cols, ctypes.byref(n)), "nbx_colsum_workspace_bytes")
+    ws = _ws(n.value, out.device)
+    _lib.check(L.nbx_colsum(rows, cols, _dp(X), ld, _dp(out), int(accumulate), _dp(ws), n.value, _st(out)),
+               "nbx_colsum")
+    return out
+
+
+class _TPFn(torch.autograd.Function):
+    """One O(3) tensor product in the canonical form of include/nbx.h ("SEGNN training step").
+    XS [rows][Ks], XV [3][rows][Kv] (or None), Y3 [rows][3]; Ws [NSc + Nt][Ks + Kv], Wv [Nt][Kv];
+    bias [NSc] or None; residuals RS [rows][Ms] / RV [3][rows][Nt] or None.  Returns (OS, OV)."""
+
+    @staticmethod
+    def forward(ctx, XS, XV, Y3, Ws, Wv, bias, RS, RV, Ms, Nt, gate):
+        L = _lib.lib()
+        dev = XS.device
+        rows, Ks = XS.shape
+        Kv = XV.shape[2] if XV is not None else 0
+        nsc = Ms + (Nt if gate else 0)
+        S = torch.empty(rows, Ks + Kv, device=dev, dtype=_f32)
+        _lib.check(L.nbx_tp_prep(rows, Ks, Kv, _dp(XS), Ks, _dp(XV), _dp(Y3), _dp(S), _st(S)), "nbx_tp_prep")
+        Zs = torch.empty(rows, nsc + Nt, device=dev, dtype=_f32)
+        gemm(_lib.GEMM_TRANS_B, rows, nsc + Nt, Ks + Kv, S, Ks + Kv, Ws, Ks + Kv, Zs, nsc + Nt)
+        Zv = torch.empty(3, rows, Nt, device=dev, dtype=_f32)
+        if Kv:
+            gemm(_lib.GEMM_TRANS_B, 3 * rows, Nt, Kv, XV, Kv, Wv, Kv, Zv, Nt)
+        else:
+            Zv.zero_()
+        OS = torch.empty(rows, Ms, device=dev, dtype=_f32)
+        OV = torch.empty(3, rows, Nt, device=dev, dtype=_f32)
+        _lib.check(L.nbx_tp_post(rows, Ms, Nt, int(gate), _dp(Zs), _dp(Zv), _dp(Y3), _dp(bias), _dp(RS), _dp(RV),
+                                 _dp(OS), _dp(OV), _st(OS)), "nbx_tp_post")
+        ctx.save_for_backward(S, XV, Y3, Ws, Wv, bias, Zs, Zv)
+        ctx.dims = (rows, Ks, Kv, Ms, Nt, nsc, int(gate), RS is not None, RV is not None)
+        return OS, OV
+
+    @staticmethod
+    def backward(ctx, dOS, dOV):
+        L = _lib.lib()
+        S, XV, Y3, Ws, Wv, bias, Zs, Zv = ctx.saved_tensors
+        rows, Ks, Kv, Ms, Nt, nsc, gate, has_rs, has_rv = ctx.dims
+        dev = S.device
+        dOS = dOS.contiguous() if dOS is not None else torch.zeros(rows, Ms, device=dev, dtype=_f32)
+        dOV = dOV.contiguous() if dOV is not None else torch.zeros(3, rows, Nt, device=dev, dtype=_f32)
+        dZs = torch.empty_like(Zs)
+        dZv = torch.empty_like(Zv)
+        _lib.check(L.nbx_tp_post_backward(rows, Ms, Nt, gate, _dp(Zs), _dp(Zv), _dp(Y3), _dp(bias), _dp(dOS),
+                                          _dp(dOV), _dp(dZs), _dp(dZv), _st(dZs)), "nbx_tp_post_backward")
+        dbias = None
+        if bias is not None and ctx.needs_input_grad[5]:
+            dbias = colsum(dZs, rows, nsc, nsc + Nt, torch.empty(nsc, device=dev, dtype=_f32))
+        dWs = dWv = None
+        if ctx.needs_input_grad[3]:
+            dWs = gemm(_lib.GEMM_TRANS_A, nsc + Nt, Ks + Kv, rows, dZs, nsc + Nt, S, Ks + Kv,
+                       torch.empty(nsc + Nt, Ks + Kv, device=dev, dtype=_f32), Ks + Kv)
+        if Kv and ctx.needs_input_grad[4]:
+            dWv = gemm(_lib.GEMM_TRANS_A, Nt, Kv, 3 * rows, dZv, Nt, XV, Kv,
+                       torch.empty(Nt, Kv, device=dev, dtype=_f32), Kv)
+        dXS = dXV = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            dS = gemm(0, rows, Ks + Kv, nsc + Nt, dZs, nsc + Nt, Ws, Ks + Kv,
+                      torch.empty(rows, Ks + Kv, device=dev, dtype=_f32), Ks + Kv)
+            dXS = torch.empty(rows, Ks, device=dev, dtype=_f32)
+            if Kv:
+                dXV = gemm(0, 3 * rows, Kv, Nt, dZv, Nt, Wv, Kv, torch.empty(3, rows, Kv, device=dev, dtype=_f32), Kv)
+            _lib.check(L.nbx_tp_prep_backward(rows, Ks, Kv, _dp(dS), _dp(Y3), _dp(dXS), Ks, _dp(dXV), _st(dS)),
+                       "nbx_tp_prep_backward")
+        return (dXS, dXV, None, dWs, dWv, dbias, dOS if has_rs else None, dOV if has_rv else None, None, None, None)
+
+
+def tp(XS, XV, Y3, Ws, Wv, bias, Ms, Nt, gate, RS=None, RV=None):
+    f = lambda t: t.contiguous() if t is not None else None
+    return _TPFn.apply(f(XS), f(XV), f(Y3), f(Ws), f(Wv), f(bias), f(RS), f(RV), Ms, Nt, gate)
+
+
+class _BNFn(torch.autograd.Function):
+    """e3nn BatchNorm with batch statistics of (S [rows][M], V [3][rows][M]); the running statistics
+    (fp32 tensors rm [M], rv [2M]) are updated in place."""
+
+    @staticmethod
+    def forward(ctx, S, V, weight, bias, rm, rv, eps, momentum):
+        L = _lib.lib()
+        rows, M = S.shape
+        dev = S.device
+        n = _lib.c_sz()
+        _lib.check(L.nbx_bn_train_workspace_bytes(rows, M, ctypes.byref(n)), "nbx_bn_train_workspace_bytes")
+        ws = _ws(n.value, dev)
+        save = torch.empty(3, M, device=dev, dtype=_f32)
+        OS, OV = torch.empty_like(S), torch.empty_like(V)
+        _lib.check(L.nbx_bn_train_forward(rows, M, _dp(S), _dp(V), _dp(weight), _dp(bias), _dp(rm), _dp(rv),
+                                          float(eps), float(momentum), _dp(save), _dp(OS), _dp(OV), _dp(ws), n.value,
+                                          _st(S)), "nbx_bn_train_forward")
+        ctx.save_for_backward(S, V, weight, save)
+        ctx.wsb = n.value
+        return OS, OV
+
+    @staticmethod
+    def backward(ctx, dOS, dOV):
+        L = _lib.lib()
+        S, V, weight, save = ctx.saved_tensors
+        rows, M = S.shape
+        dev = S.device
+        dOS = dOS.contiguous() if dOS is not None else torch.zeros_like(S)
+        dOV = dOV.contiguous() if dOV is not None else torch.zeros_like(V)
+        ws = _ws(ctx.wsb, dev)
+        dS, dV = torch.empty_like(S), torch.empty_like(V)
+        dw = torch.empty(2 * M, device=dev, dtype=_f32)
+        db = torch.empty(M, device=dev, dtype=_f32)
+        _lib.check(L.nbx_bn_train_backward(rows, M, _dp(S), _dp(V), _dp(weight), _dp(save), _dp(dOS), _dp(dOV),
+                                           _dp(dS), _dp(dV), _dp(dw), _dp(db), _dp(ws), ctx.wsb, _st(dS)),
+                   "nbx_bn_train_backward")
+        return dS, dV, dw, db, None, None, None, None
+
+
+class Graph:
+    """Index tables of one edge list: src / dst int32 [E] and CSRs of the edges by destination and by
+    source (ptr [V + 1], eid [E]), built on the device without a host synchronisation."""
+
+    def __init__(self, edge_index, V, device):
+        ei = edge_index.to(device=device, dtype=torch.int64)
+        self.V, self.E = V, ei.shape[1]
+        self.src = ei[0].to(torch.int32).contiguous()
+        self.dst = ei[1].to(torch.int32).contiguous()
+        nodes = torch.arange(V + 1, device=device, dtype=torch.int64)
+        for name, key in (("d", ei[1]), ("s", ei[0])):
+            order = torch.argsort(key, stable=True)
+            ptr = torch.searchsorted(key[order].contiguous(), nodes).to(torch.int32).contiguous()
+            setattr(self, name + "ptr", ptr)
+            setattr(self, name + "eid", order.to(torch.int32).contiguous())
+
+
+class _GatherFn(torch.autograd.Function):
+    """out[e] = X[idx[e]] per plane (X [planes][V][C] or [V][C]); backward: segment sum over the
+    CSR of idx."""
+
+    @staticmethod
+    def forward(ctx, X, idx, ptr, eid):
+        planes = X.shape[0] if X.dim() == 3 else 1
+        V, C = X.shape[-2], X.shape[-1]
+        n = idx.shape[0]
+        out = torch.empty(*((planes,) if X.dim() == 3 else ()), n, C, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_gather_rows(n, C, _dp(idx), _dp(X), C, V * C, _dp(out), C, n * C, planes, _st(X)),
+                   "nbx_gather_rows")
+        ctx.save_for_backward(ptr, eid)
+        ctx.shape = (planes, V, C, n, X.dim())
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ptr, eid = ctx.saved_tensors
+        planes, V, C, n, nd = ctx.shape
+        dout = dout.contiguous()
+        dX = torch.empty(*((planes,) if nd == 3 else ()), V, C, device=dout.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_segment_sum(V, C, _dp(ptr), _dp(eid), _dp(dout), C, n * C, _dp(dX), C, V * C,
+                                              planes, 0, _st(dout)), "nbx_segment_sum")
+        return dX, None, None, None
+
+
+class _SegSumFn(torch.autograd.Function):
+    """out[v] = sum of Xe[e] over the edges e with idx[e] = v (CSR ptr / eid of idx); backward: gather."""
+
+    @staticmethod
+    def forward(ctx, Xe, idx, ptr, eid, V):
+        planes = Xe.shape[0] if Xe.dim() == 3 else 1
+        n, C = Xe.shape[-2], Xe.shape[-1]
+        out = torch.empty(*((planes,) if Xe.dim() == 3 else ()), V, C, device=Xe.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_segment_sum(V, C, _dp(ptr), _dp(eid), _dp(Xe), C, n * C, _dp(out), C, V * C, planes,
+                                              0, _st(Xe)), "nbx_segment_sum")
+        ctx.save_for_backward(idx)
+        ctx.shape = (planes, V, C, n, Xe.dim())
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx,) = ctx.saved_tensors
+        planes, V, C, n, nd = ctx.shape
+        dout = dout.contiguous()
+        dXe = torch.empty(*((planes,) if nd == 3 else ()), n, C, device=dout.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_gather_rows(n, C, _dp(idx), _dp(dout), C, V * C, _dp(dXe), C, n * C, planes,
+                                              _st(dout)), "nbx_gather_rows")
+        return dXe, None, None, None, None
+
+
+def featurize(pos, vel, mass, g: Graph):
+    """O3Transform + catch_isolated_nodes (no gradient): na3 [V][3], xs0 [V][1], xv0 [3][V][2],
+    rhat [E][3], amf [E][2]."""
+    dev = pos.device
+    V, E = g.V, g.E
+    na3 = torch.empty(V, 3, device=dev, dtype=_f32)
+    xs0 = torch.empty(V, 1, device=dev, dtype=_f32)
+    xv0 = torch.empty(3, V, 2, device=dev, dtype=_f32)
+    rhat = torch.empty(max(E, 1), 3, device=dev, dtype=_f32)
+    amf = torch.empty(max(E, 1), 2, device=dev, dtype=_f32)
+    _lib.check(_lib.lib().nbx_segnn_train_featurize(V, E, _dp(pos), _dp(vel), _dp(mass), _dp(g.src), _dp(g.dst),
+                                                    _dp(g.dptr), _dp(g.deid), _dp(na3), _dp(xs0), _dp(xv0),
+                                                    _dp(rhat), _dp(amf), _st(pos)), "nbx_segnn_train_featurize")
+    return na3, xs0, xv0, rhat[:E], amf[:E]
+
+
+def _batch_norm(model, bn, S, V, batch_stats):
+    """e3nn BatchNorm of the module ``bn`` (segnn.py BatchNorm): batch statistics through _BNFn (the
+    running statistics updated in place; fp32 shadows for a float64 module), else the running
+    statistics (an affine map, torch ops)."""
+    w, b = bn.weight.to(_f32), bn.bias.to(_f32)
+    M = S.shape[1]
+    if not batch_stats:
+        rm, rv = bn.running_mean.to(_f32), bn.running_var.to(_f32)
+        sc = w[:M] / torch.sqrt(rv[:M] + bn.eps)
+        return (S - rm) * sc + b, V * (w[M:] / torch.sqrt(rv[M:] + bn.eps))
+    rm, rv = bn.running_mean, bn.running_var
+    shadow = rm.dtype != _f32 or not rm.is_contiguous()
+    if shadow:
+        rm, rv = rm.to(_f32).contiguous(), rv.to(_f32).contiguous()
+    OS, OV = _BNFn.apply(S.contiguous(), V.contiguous(), w.contiguous(), b.contiguous(), rm, rv, bn.eps, bn.momentum)
+    if shadow:
+        with torch.no_grad():
+            bn.running_mean.copy_(rm)
+            bn.running_var.copy_(rv)
+    return OS, OV
+
+
+def train_forward(model, pos, vel, mass, edge_index):
+    """The SEGNN forward of segnn.py:150-189 with autograd through the native operators.
+    pos / vel [V, 3], mass [V] fp32 on the device; edge_index [2, E] (row = source, col = target).
+    Returns pred [V, 6] fp32."""
+    dev = pos.device
+    V = pos.shape[0]
+    g = Graph(edge_index, V, dev)
+    na3, xs0, xv0, rhat, amf = featurize(pos, vel, mass, g)
+    W = model.train_matrices(dev)
+    M = model.mul
+    batch_stats = model._bn_batch()
+    hs, hv = tp(xs0, xv0, na3, W["emb_s"], W["emb_v"], W["emb_bias"], M, M, 0)
+    for li, layer in enumerate(model.layers):
+        p = f"layers.{li}."
+        # message(x_i = x[dst], x_j = x[src], additional features) -> two gated TPs -> message BatchNorm
+        xd = _GatherFn.apply(hs, g.dst, g.dptr, g.deid)
+        xs = _GatherFn.apply(hs, g.src, g.sptr, g.seid)
+        vd = _GatherFn.apply(hv, g.dst, g.dptr, g.deid)
+        vs = _GatherFn.apply(hv, g.src, g.sptr, g.seid)
+        ms, mv = tp(torch.cat([xd, xs, amf], 1), torch.cat([vd, vs], 2), rhat, W[p + "msg1_s"], W[p + "msg1_v"],
+                    W[p + "msg1_bias"], M, M, 1)
+        ms, mv = tp(ms, mv, rhat, W[p + "msg2_s"], W[p + "msg2_v"], W[p + "msg2_bias"], M, M, 1)
+        ms, mv = _batch_norm(model, layer.message_norm, ms, mv, batch_stats)
+        # aggr="add" at edge_index[1]
+        a_s = _SegSumFn.apply(ms, g.dst, g.dptr, g.deid, V)
+        a_v = _SegSumFn.apply(mv, g.dst, g.dptr, g.deid, V)
+        # update: cat(x, agg) -> gated TP -> TP, x + update, feature BatchNorm
+        us, uv = tp(torch.cat([hs, a_s], 1), torch.cat([hv, a_v], 2), na3, W[p + "upd1_s"], W[p + "upd1_v"],
+                    W[p + "upd1_bias"], M, M, 1)
+        hs, hv = tp(us, uv, na3, W[p + "upd2_s"], W[p + "upd2_v"], W[p + "upd2_bias"], M, M, 0, RS=hs, RV=hv)
+        hs, hv = _batch_norm(model, layer.feature_norm, hs, hv, batch_stats)
+    hs, hv = tp(hs, hv, na3, W["pp1_s"], W["pp1_v"], W["pp1_bias"], M, M, 1)
+    _, ov = tp(hs, hv, na3, W["pp2_s"], W["pp2_v"], None, 0, 2, 0)
+    return ov.permute(1, 2, 0).reshape(V, 6)      # [V][(copy, xyz)]: 2x1o

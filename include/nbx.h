@@ -265,6 +265,80 @@ int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, co
 
 
 /* ------------------------------------------------------------------------
+ * SEGNN training step (ABI 10; SURVEY §8(f)4: trainer.py:233-358, pred = model(graph) with the
+ * train-mode BatchNorm of models/segnn/segnn.py:233-235, loss.backward()).  The training forward and
+ * backward are composed (segnn_train.py, autograd) of the operators below; every O(3) tensor product
+ * of SEGNN (o3_building_blocks.py:10-203) is one canonical form
+ *   S_in = [XS | sum_k XV[k] * Y3[:, k]],  Zs = S_in Ws^T,  Zv[k] = XV[k] Wv^T,
+ *   OS = Zs[:, :Ms] + b (gated: c_silu SiLU), OV[k] = Y3[:, k] Zs[:, NSc + w] + Zv[k]
+ *        (gated: times c_sig sigmoid(Zs[:, Ms + w] + b[Ms + w]); NSc = Ms (+ Nt gates))
+ * with e3nn's path constants and the SH prefactors folded into Ws / Wv (segnn.py train_matrices).
+ * Layouts: row-major, vector features as 3 component planes [3][rows][C].  All reductions run in a
+ * fixed order (bit-reproducible).  fp32. */
+
+/* C = op(A) op(B) (+ C if beta = 1), C [M][N] (ldc); op(A) [M][K]: A stored [M][K] (lda) or, with
+ * NBX_GEMM_TRANS_A, [K][M]; op(B) [K][N]: B stored [K][N] (ldb) or, with NBX_GEMM_TRANS_B, [N][K].
+ * fp32 MFMA (v_mfma_f32_32x32x2_f32), 64 x 64 tiles; small-M N, long-K products (weight gradients)
+ * split K over the workspace (nbx_gemm_f32_workspace_bytes) and sum the splits in order. */
+#define NBX_GEMM_TRANS_A 1
+#define NBX_GEMM_TRANS_B 2
+int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes);
+int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                 int64_t ldb, float* C, int64_t ldc, float beta, void* workspace, size_t workspace_bytes, void* stream);
+
+/* S_in [rows][Ks + Kv] from XS (rows x Ks, leading dimension ldxs), XV [3][rows][Kv], Y3 [rows][3];
+ * backward: dXS = dS[:, :Ks] (written when non-NULL), dXV[k] += Y3[:, k] dS[:, Ks:] (accumulated). */
+int nbx_tp_prep(int64_t rows, int32_t Ks, int32_t Kv, const float* XS, int64_t ldxs, const float* XV, const float* Y3,
+                float* S, void* stream);
+int nbx_tp_prep_backward(int64_t rows, int32_t Ks, int32_t Kv, const float* dS, const float* Y3, float* dXS,
+                         int64_t lddxs, float* dXV, void* stream);
+
+/* The TP epilogue: Zs [rows][NSc + Nt], Zv [3][rows][Nt] -> OS [rows][Ms], OV [3][rows][Nt] (+ the
+ * optional residuals RS / RV: x + update, segnn.py:303); gate = e3nn Gate(SiLU, sigmoid)
+ * (o3_building_blocks.py:187-203).  Backward: dOS, dOV -> dZs, dZv (the bias gradient is the column
+ * sum of dZs[:, :NSc], nbx_colsum). */
+int nbx_tp_post(int64_t rows, int32_t Ms, int32_t Nt, int32_t gate, const float* Zs, const float* Zv, const float* Y3,
+                const float* bias, const float* RS, const float* RV, float* OS, float* OV, void* stream);
+int nbx_tp_post_backward(int64_t rows, int32_t Ms, int32_t Nt, int32_t gate, const float* Zs, const float* Zv,
+                         const float* Y3, const float* bias, const float* dOS, const float* dOV, float* dZs, float* dZv,
+                         void* stream);
+
+/* out[c] (+)= sum over rows of X[r][c] (fixed order, fp64 partials). */
+int nbx_colsum_workspace_bytes(int64_t rows, int32_t cols, size_t* bytes);
+int nbx_colsum(int64_t rows, int32_t cols, const float* X, int64_t ld, float* out, int32_t accumulate, void* workspace,
+               size_t workspace_bytes, void* stream);
+
+/* e3nn BatchNorm with batch statistics (train mode) of M 0e channels S [rows][M]
+ * and M 1o channels V [3][rows][M]: OS = (S - mu) w / sqrt(var + eps) + b, OV = V w_v / sqrt(n + eps),
+ * n = mean over rows and components of V^2; running stats updated in place (momentum) when non-NULL;
+ * save [3][M] = (mu, 1/sqrt(var + eps), 1/sqrt(n + eps)) for the backward, which returns dS, dV and
+ * the parameter gradients dweight [2M] (0e then 1o), dbias [M]. */
+int nbx_bn_train_workspace_bytes(int64_t rows, int32_t M, size_t* bytes);
+int nbx_bn_train_forward(int64_t rows, int32_t M, const float* S, const float* V, const float* weight, const float* bias,
+                         float* running_mean, float* running_var, float eps, float momentum, float* save, float* OS,
+                         float* OV, void* workspace, size_t workspace_bytes, void* stream);
+int nbx_bn_train_backward(int64_t rows, int32_t M, const float* S, const float* V, const float* weight,
+                          const float* save, const float* dOS, const float* dOV, float* dS, float* dV, float* dweight,
+                          float* dbias, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Message passing (MessagePassing aggr="add", segnn.py:249): out[r] = in[idx[r]] per plane (x_i = x[dst],
+ * x_j = x[src]) and out[n] (+)= sum over j in [ptr[n], ptr[n+1]) of in[eid[j]] (a CSR of the edges by
+ * destination / source; the aggregation and the gathers' adjoint).  planes: component planes, strides
+ * plane_in / plane_out. */
+int nbx_gather_rows(int64_t n, int32_t cols, const int32_t* idx, const float* in, int64_t ld_in, int64_t plane_in,
+                    float* out, int64_t ld_out, int64_t plane_out, int32_t planes, void* stream);
+int nbx_segment_sum(int64_t n, int32_t cols, const int32_t* ptr, const int32_t* eid, const float* in, int64_t ld_in,
+                    int64_t plane_in, float* out, int64_t ld_out, int64_t plane_out, int32_t planes,
+                    int32_t accumulate, void* stream);
+
+/* O3Transform + catch_isolated_nodes on an edge list (src, dst int32 [E]; dst_ptr [V+1] / dst_eid [E]:
+ * the edges grouped by destination): na3 [V][3] (the l=1 node attribute), xs0 [V] = |vel|,
+ * xv0 [3][V][2] = (pos - mean_xyz(pos), vel), rhat [E][3], amf [E][2] = (|rel|, m_src m_dst). */
+int nbx_segnn_train_featurize(int64_t V, int64_t E, const float* pos, const float* vel, const float* mass,
+                              const int32_t* src, const int32_t* dst, const int32_t* dst_ptr, const int32_t* dst_eid,
+                              float* na3, float* xs0, float* xv0, float* rhat, float* amf, void* stream);
+
+/* ------------------------------------------------------------------------
  * EGNN-MC (models/egnn_mc/egnn_mc.py:45-295 with the preprocessing of
  * dataloaders/egnn_mc_n_body_dataloader.py:8-56) — fp32.
  *

@@ -161,7 +161,8 @@ def test_rollout_equals_repeated_forward(hip_device, hidden, B, N):
     for t in range(1, T):
         g = Graph()
         g.pos, g.vel, g.mass, g.edge_index = l, v, ma.reshape(-1, 1), G.fc_edge_index(B, N, hip_device)
-        out = model(g)
+        with torch.no_grad():   # the inference forward (grad mode runs the training forward)
+            out = model(g)
         l = l + out[:, :3]
         v = out[:, 3:].contiguous()
         # same arithmetic; the train-mode BatchNorm sums are fp64 atomics (arrival order varies:

@@ -100,3 +100,46 @@ def test_batchnorm_train_and_eval():
     np.testing.assert_allclose(rv, 0.9 + 0.1 * np.concatenate([s.var(0), n]))
     ye, _, _ = e3.batch_norm(x, ir, w, b, rm, rv, training=False)
     np.testing.assert_allclose(ye[:, :3], (s - rm) / np.sqrt(rv[:3] + 1e-5) * w[:3] + b, rtol=1e-12)
+
+
+def test_torch_oracle_matches_numpy_oracle():
+    """oracle/segnn_torch.py (the autograd reference of the training step) is the numpy oracle's
+    forward in torch: predictions and running statistics agree to fp64 rounding on fully-connected
+    and kNN graphs, and its gradients match central finite differences of the numpy oracle's loss."""
+    import torch
+    from oracle import segnn_torch as ST
+    from oracle.graph import fc_edge_index, knn_edge_index
+    from oracle.segnn import SEGNNOracle, init_params, o3_transform
+    om = SEGNNOracle(hidden_features=16, num_layers=2)
+    p = init_params(om, 1)
+    rng = np.random.default_rng(0)
+    B, N = 3, 5
+    pos, vel = rng.standard_normal((B * N, 3)), rng.standard_normal((B * N, 3))
+    mass = rng.uniform(0.5, 1.5, (B * N, 1))
+    for ei in (fc_edge_index(B, N), knn_edge_index(pos, B, N, 2)):
+        x, ea, na, amf = o3_transform(pos, vel, mass, ei)
+        ref, st = om.forward(p, x, ei, ea, na, amf, training=True)
+        P = {k: torch.tensor(v) for k, v in p.items()}
+        out, st2 = ST.forward(om, P, torch.tensor(pos), torch.tensor(vel), torch.tensor(mass), torch.tensor(ei), True)
+        np.testing.assert_allclose(out.numpy(), ref, rtol=1e-12, atol=1e-13)
+        for k in st:
+            np.testing.assert_allclose(st2[k].numpy(), st[k], rtol=1e-12, atol=1e-13)
+    # gradients vs finite differences of the numpy oracle's MSE loss, a few entries per kind
+    ei = fc_edge_index(B, N)
+    tgt = rng.standard_normal((B * N, 6))
+    _, _, grads, _ = ST.loss_and_grads(om, p, pos, vel, mass, ei, tgt)
+    x, ea, na, amf = o3_transform(pos, vel, mass, ei)
+
+    def loss(q):
+        return float(((om.forward(q, x, ei, ea, na, amf, training=True)[0] - tgt) ** 2).mean())
+    for key in ("layers.0.message_layer_1.tp.weight", "layers.1.update_layer_2.biases",
+                "layers.0.message_norm.weight", "layers.1.feature_norm.bias", "pre_pool2.tp.weight",
+                "embedding_layer.tp.weight"):
+        for j in (0, len(p[key]) // 2, len(p[key]) - 1):
+            h = 1e-6
+            qp, qm = dict(p), dict(p)
+            qp[key], qm[key] = p[key].copy(), p[key].copy()
+            qp[key][j] += h
+            qm[key][j] -= h
+            fd = (loss(qp) - loss(qm)) / (2 * h)
+            assert abs(fd - grads[key][j]) <= 1e-6 * max(1.0, abs(fd)), (key, j, fd, grads[key][j])
