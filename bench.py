@@ -95,6 +95,48 @@ def cpu_baseline_segnn(loc, vel, mass, steps=1):
                       f"(oracle/segnn.py), BLAS threads={threads}, {dt:.2f} s"}
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_segnn_torch(loc, vel, mass, steps=20):
+    """BASELINE.md §3's C2 CPU baseline: the unfused PyTorch CPU restatement of the reference SEGNN
+    forward (oracle/segnn_torch.py, fp64 -- the reference's default precision_mode, train-mode
+    BatchNorm) driving the self-feed loop of infer_self_feed.py:99-194 for `steps` steps of the full
+    B=1024 batch on the host cores (torch threads = OMP_NUM_THREADS)."""
+    from oracle import segnn_torch as OT
+    from oracle.graph import fc_edge_index
+    from oracle.segnn import SEGNNOracle, init_params
+    B, N, _ = loc.shape
+    om = SEGNNOracle(hidden_features=HIDDEN, num_layers=LAYERS)
+    params = {k: torch.tensor(v) for k, v in init_params(om, seed=0).items()}
+    threads = blas_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    ei = torch.from_numpy(fc_edge_index(B, N))
+    p = torch.from_numpy(loc.reshape(-1, 3)).double()
+    v = torch.from_numpy(vel.reshape(-1, 3)).double()
+    m = torch.from_numpy(mass.reshape(-1, 1)).double()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for _ in range(steps):
+            out, stats = OT.forward(om, params, p, v, m, ei, True)
+            params.update(stats)
+            p, v = p + out[:, :3], out[:, 3:].contiguous()
+    dt = time.perf_counter() - t0
+    torch.set_num_threads(prev)
+    return {"value": steps / dt, "unit": "steps/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{steps} self-feed steps of the full B={B} N={N} batch, torch fp64 restatement of the reference "
+                      f"forward (oracle/segnn_torch.py, train-mode BatchNorm), {threads} threads, {dt:.2f} s"}
+
+
 def bench_segnn(a, rank, world, device, P):
     import nbody_amd.segnn as S
     from nbody_amd import _lib
@@ -204,7 +246,10 @@ def bench_segnn(a, rank, world, device, P):
         "finite": finite,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_segnn(loc, vel, mass, a.cpu_steps)
+        # >= 20 steps of the PyTorch CPU restatement (the reported baseline), beside one
+        # step of the numpy oracle (the round-1/2 figure)
+        result["cpu_baseline"] = cpu_baseline_segnn_torch(loc, vel, mass, a.cpu_torch_steps)
+        result["cpu_baseline"]["numpy_oracle"] = cpu_baseline_segnn(loc, vel, mass, a.cpu_steps)
     return result
 
 
@@ -498,6 +543,141 @@ def bench_egnn_train(a, rank, world, device, P):
     return result
 
 
+# ---------------------------------------------------------------- SEGNN training step
+def bench_segnn_train(a, rank, world, device, P):
+    """one SEGNN training step of the reference trainer (trainer.py:233-358) at C2
+    widths (hidden 192, lmax 1, 6 layers, N=5) on the reference's training batch (config.yaml
+    dataloaders batch_size 64 systems per rank, "weak"): zero_grad, train-mode forward on the native
+    training operators (segnn_train.py / csrc/segnn_train.hip), MSE loss, loss.backward() through the
+    native backward, gradient all-reduce over ranks (RCCL), clip to norm 1, AdamW + LambdaLR
+    (trainer.py:170-194).  On one GPU the whole step is one HIP graph replay (--eager: uncaptured)."""
+    import nbody_amd.segnn as S
+    import nbody_amd.segnn_train as ST
+    from nbody_amd.graph import fc_edge_index
+    B, N = a.batch or 64, NBODY
+    torch.manual_seed(0)
+    model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS).to(device).train()
+    loc, vel, mass = initial_states(B, N, rank * B)
+    rng = np.random.default_rng(100 + rank)
+
+    class _G:
+        pass
+    g = _G()
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    g.pos, g.vel, g.mass = t(loc.reshape(-1, 3)), t(vel.reshape(-1, 3)), t(mass.reshape(-1, 1))
+    g.edge_index = fc_edge_index(B, N, device)
+    g.nbx_system_size = N
+    target = t(rng.standard_normal((B * N, 6)) * 0.1)
+    graph = not a.eager and world == 1
+    opt = torch.optim.AdamW(model.parameters(), lr=1.0, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9,
+                            fused=True, capturable=graph)
+    sched = torch.optim.lr_scheduler.LambdaLR(
+        opt, lambda s: HIDDEN ** -0.5 * min(max(s, 1) ** -0.5, max(s, 1) * 1000 ** -1.5))
+    if graph:
+        for grp in opt.param_groups:
+            grp["lr"] = torch.tensor(float(grp["lr"]), dtype=torch.float32, device=device)
+    params = list(model.parameters())
+
+    def step_body():
+        opt.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.mse_loss(model(g), target)
+        loss.backward()
+        P.allreduce_gradients(params)
+        torch.nn.utils.clip_grad_norm_(params, 1.0, foreach=True)
+        opt.step()
+        return loss
+
+    # roofline: every GEMM launch of one eager step, event-timed on the launch stream
+    ST.gemm_timer = []
+    step_body()
+    torch.cuda.synchronize(device)
+    gemm_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ST.gemm_timer)
+    gemm_flops = sum(f for _, _, f in ST.gemm_timer)
+    n_gemm = len(ST.gemm_timer)
+    ST.gemm_timer = None
+    sched.step()
+    if graph:
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(max(a.warmup, 3)):
+                step_body()
+                sched.step()
+        torch.cuda.current_stream(device).wait_stream(side)
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg):
+            static_loss = step_body()
+
+        def train_step():
+            cg.replay()
+            sched.step()
+            return static_loss
+    else:
+        def train_step():
+            loss = step_body()
+            sched.step()
+            return loss
+
+    for _ in range(max(a.warmup, 1)):
+        train_step()
+
+    def work():
+        for _ in range(a.steps):
+            loss = train_step()
+        return loss
+    loss, elapsed = timed_region(work, device, P)
+    model.invalidate_weights()   # the replays' AdamW updated the parameters in place
+    value = a.steps / elapsed * world
+    ach = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
+    result = {
+        "metric": "SEGNN training steps/sec (C2 widths, forward + backward + AdamW)", "value": round(value, 3),
+        "unit": "train steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states, random targets, seeded random-init weights)",
+        "config": {"workload": "SURVEY 8(f)4: SEGNN lmax_h=1 hidden 192, 6 layers training step, N=5, batch 64 per "
+                               "GPU (config.yaml batch_size), train-mode BatchNorm, MSE loss, grad-norm clip 1, "
+                               "AdamW + LambdaLR (trainer.py:170-194)", "model": "SEGNN", "global_batch": B * world,
+                   "seq_len": a.steps, "parallelism": f"dp{world}",
+                   "execution": "one HIP graph replay per step (forward, backward, clip, fused AdamW)" if graph
+                                else "eager"},
+        "roofline": {"bound": "mfma", "kernel": "gemm_f32_kernel (nbx_gemm_f32: every tensor-product GEMM of the "
+                                               "forward and backward)",
+                     "achieved": round(ach, 3) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None, "traffic": None,
+                     "avg_launch_us": round(1e3 * gemm_ms / max(n_gemm, 1), 3), "launches_per_step": n_gemm,
+                     "gflop_per_step": round(gemm_flops / 1e9, 4),
+                     "timing": "torch.cuda.Event pairs around every GEMM launch of one eager step, launch stream",
+                     "note": "B=64 training batch: GEMMs of 320-1280 rows, latency-bound"},
+        "loss": float(loss.item()), "finite": bool(math.isfinite(float(loss.item())))}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import segnn_torch as OT
+        from oracle.graph import fc_edge_index as oei
+        from oracle.segnn import SEGNNOracle
+        om = SEGNNOracle(hidden_features=HIDDEN, num_layers=LAYERS)
+        Pc = {k: v.detach().double().cpu().clone().requires_grad_("running" not in k)
+              for k, v in model.state_dict().items() if "output_mask" not in k}
+        optc = torch.optim.AdamW([v for v in Pc.values() if v.requires_grad], lr=1e-4, weight_decay=1e-8,
+                                 betas=(0.9, 0.98), eps=1e-9)
+        tt = lambda x, w: torch.from_numpy(x.reshape(-1, w)).double()
+        pc, vc, mc = tt(loc, 3), tt(vel, 3), tt(mass, 1)
+        ei = torch.from_numpy(oei(B, N))
+        tc = target.double().cpu()
+        steps = max(1, a.cpu_steps)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            optc.zero_grad()
+            lc = torch.nn.functional.mse_loss(OT.forward(om, Pc, pc, vc, mc, ei, True)[0], tc)
+            lc.backward()
+            torch.nn.utils.clip_grad_norm_([v for v in Pc.values() if v.requires_grad], 1.0)
+            optc.step()
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": steps / dt, "unit": "train steps/s", "cores": torch.get_num_threads(),
+                                  "kind": "port", "sample": f"{steps} training step(s) of the B={B} batch, torch fp64 "
+                                                            f"autograd restatement (oracle/segnn_torch.py), {dt:.2f} s"}
+    return result
+
+
 # ---------------------------------------------------------------- C4 EquiformerV2
 EQV2_C4 = dict(num_layers=4, attn_hidden_channels=64, sphere_channels=64, num_heads=4, attn_alpha_channels=8,
                attn_value_channels=4, ffn_hidden_channels=64, lmax_list=[2], mmax_list=[1], grid_resolution=None,
@@ -668,14 +848,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--model", default="segnn",
-                    choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "eqv2", "gravity"])
+                    choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "segnn_train", "eqv2", "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
-    ap.add_argument("--eager", action="store_true", help="egnn_mc_train: run the step eagerly (no HIP graph)")
+    ap.add_argument("--cpu-torch-steps", type=int, default=20,
+                    help="C2: self-feed steps of the torch CPU restatement timed for cpu_baseline")
+    ap.add_argument("--eager", action="store_true",
+                    help="egnn_mc_train / segnn_train: run the step eagerly (no HIP graph)")
     ap.add_argument("--bn-mode", default="batch", choices=["batch", "sync", "running"],
                     help="SEGNN BatchNorm statistics: per-rank batch (default), all-rank SyncBN, running")
     a = ap.parse_args()
-    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5), "eqv2": (20, 2),
+    defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5),
+                "segnn_train": (50, 5), "eqv2": (20, 2),
                 "gravity": (1000, 100)}
     a.steps = a.steps if a.steps is not None else defaults[a.model][0]
     a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
@@ -683,6 +867,7 @@ def main():
     from nbody_amd import parallel as P
     rank, world, device = P.init_from_env()
     fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "egnn_mc_train": bench_egnn_train,
+          "segnn_train": bench_segnn_train,
           "eqv2": bench_eqv2, "gravity": bench_gravity}[a.model]
     result = fn(a, rank, world, device, P)
     if rank == 0:

@@ -27,11 +27,13 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------- GEMM (fp32 MFMA)
 // C[m][n] (+)= sum_k A(m, k) B(k, n);  A(m, k) = TA ? A[k lda + m] : A[m lda + k],
-// B(k, n) = TB ? B[n ldb + k] : B[k ldb + n].  Block tile 64 x 64, K step 16, four waves of a 32 x 32
-// v_mfma_f32_32x32x2_f32 tile each; the next K tile is loaded into registers while the current one
-// is multiplied from LDS.  Split-K (gridDim.z > 1): each z writes its partial tile into `part`
-// [z][M][N]; gemm_reduce_kernel sums them in z order.
-constexpr int GB = 64, GK = 16, GT = 256;
+// B(k, n) = TB ? B[n ldb + k] : B[k ldb + n].  Block tile 64 x 64, K step 32, four waves of a 32 x 32
+// v_mfma_f32_32x32x2_f32 tile each; the next K tile is loaded into registers (float4 along the
+// contiguous dimension when VEC: 16-byte aligned operands and leading dimensions) while the current
+// one is multiplied from LDS.  The training GEMMs are small (a B=64 batch: 320-3840 rows), so the
+// grid is split along K until it holds ~256 blocks of >= 4 K steps (gemm_splits): each z writes its
+// partial tile into `part` [z][M][N] and gemm_reduce_kernel sums them in z order.
+constexpr int GB = 64, GK = 32, GT = 256;
 
 struct GemmArgs {
     const float* A;
@@ -43,7 +45,7 @@ struct GemmArgs {
     float beta;
 };
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, bool VEC>
 __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
     __shared__ float As[2][GK][GB + 4];
     __shared__ float Bs[2][GK][GB + 4];
@@ -52,31 +54,37 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
     const int64_t k_lo = (int64_t)blockIdx.z * g.kchunk;
     const int64_t k_hi = std::min<int64_t>(g.K, k_lo + g.kchunk);
     const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
-    float ra[4], rb[4];
-    // thread -> (tile row, k) of its four loads: contiguous global dimension along the thread index
+    float ra[2][4], rb[2][4];
+    // four consecutive elements along the contiguous dimension: (row, col) of the first, its stride
+    auto load4 = [&](const float* base, int64_t ld, int64_t r, int64_t c, int64_t rmax, int64_t cmax, float (&v)[4]) {
+        // elements base[r * ld + c + j], valid while r < rmax and c + j < cmax
+        if (r < rmax && c + 3 < cmax && VEC) {
+            const float4 q = *reinterpret_cast<const float4*>(base + r * ld + c);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (r < rmax && c + j < cmax) ? base[r * ld + c + j] : 0.f;
+        }
+    };
     auto load = [&](int64_t k0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int r, k;
-            if (TA) { k = t >> 4; r = (t & 15) * 4 + j; }   // A stored [K][M]: m contiguous
-            else { r = t >> 2; k = (t & 3) * 4 + j; }        // A stored [M][K]: k contiguous
-            const int64_t gm = m0 + r, gk = k0 + k;
-            ra[j] = (gm < g.M && gk < k_hi) ? (TA ? g.A[gk * g.lda + gm] : g.A[gm * g.lda + gk]) : 0.f;
-            int c, kb;
-            if (TB) { c = t >> 2; kb = (t & 3) * 4 + j; }   // B stored [N][K]: k contiguous
-            else { kb = t >> 4; c = (t & 15) * 4 + j; }      // B stored [K][N]: n contiguous
-            const int64_t gn = n0 + c, gkb = k0 + kb;
-            rb[j] = (gn < g.N && gkb < k_hi) ? (TB ? g.B[gn * g.ldb + gkb] : g.B[gkb * g.ldb + gn]) : 0.f;
+        for (int h = 0; h < 2; ++h) {
+            if (TA) load4(g.A, g.lda, k0 + (t >> 4) + 16 * h, m0 + (t & 15) * 4, k_hi, g.M, ra[h]);   // [K][M]
+            else load4(g.A, g.lda, m0 + (t >> 3) + 32 * h, k0 + (t & 7) * 4, g.M, k_hi, ra[h]);       // [M][K]
+            if (TB) load4(g.B, g.ldb, n0 + (t >> 3) + 32 * h, k0 + (t & 7) * 4, g.N, k_hi, rb[h]);    // [N][K]
+            else load4(g.B, g.ldb, k0 + (t >> 4) + 16 * h, n0 + (t & 15) * 4, k_hi, g.N, rb[h]);      // [K][N]
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (TA) As[buf][t >> 4][(t & 15) * 4 + j] = ra[j];
-            else As[buf][(t & 3) * 4 + j][t >> 2] = ra[j];
-            if (TB) Bs[buf][(t & 3) * 4 + j][t >> 2] = rb[j];
-            else Bs[buf][t >> 4][(t & 15) * 4 + j] = rb[j];
-        }
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (TA) As[buf][(t >> 4) + 16 * h][(t & 15) * 4 + j] = ra[h][j];
+                else As[buf][(t & 7) * 4 + j][(t >> 3) + 32 * h] = ra[h][j];
+                if (TB) Bs[buf][(t & 7) * 4 + j][(t >> 3) + 32 * h] = rb[h][j];
+                else Bs[buf][(t >> 4) + 16 * h][(t & 15) * 4 + j] = rb[h][j];
+            }
     };
     floatx16 acc;
 #pragma unroll
@@ -127,9 +135,9 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, i
 
 int gemm_splits(int64_t M, int64_t N, int64_t K) {
     const int64_t tiles = ((M + GB - 1) / GB) * ((N + GB - 1) / GB);
-    if (tiles >= 128 || K < 1024) return 1;
-    int64_t s = std::min<int64_t>((256 + tiles - 1) / tiles, K / 512);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(s, 32));
+    if (tiles >= 256) return 1;
+    const int64_t by_grid = (256 + tiles - 1) / tiles, by_k = K / (4 * GK);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(by_grid, by_k), 64));
 }
 
 // ---------------------------------------------------------------- TP pre / post
@@ -512,10 +520,19 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     g.kchunk = (g.kchunk + GK - 1) / GK * GK;
     const dim3 grid((unsigned)((N + GB - 1) / GB), (unsigned)((M + GB - 1) / GB), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
-    if (ta && tb) hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(GT), 0, st, g);
-    else if (ta) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(GT), 0, st, g);
-    else if (tb) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(GT), 0, st, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(GT), 0, st, g);
+    const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(GT), 0, st, g); };
+    if (vec) {
+        if (ta && tb) go(gemm_f32_kernel<true, true, true>);
+        else if (ta) go(gemm_f32_kernel<true, false, true>);
+        else if (tb) go(gemm_f32_kernel<false, true, true>);
+        else go(gemm_f32_kernel<false, false, true>);
+    } else {
+        if (ta && tb) go(gemm_f32_kernel<true, true, false>);
+        else if (ta) go(gemm_f32_kernel<true, false, false>);
+        else if (tb) go(gemm_f32_kernel<false, true, false>);
+        else go(gemm_f32_kernel<false, false, false>);
+    }
     NBX_LAUNCH_CHECK("gemm_f32");
     if (splits > 1) {
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,

@@ -422,6 +422,13 @@ class SEGNN(nn.Module):
             raise ValueError(f"bn_mode must be None, 'batch' or 'running' (got {self.bn_mode!r})")
         return self.training if self.bn_mode is None else self.bn_mode == "batch"
 
+    def invalidate_weights(self):
+        """Drop the packed inference operands (rebuilt at the next native call).  Needed after
+        parameter updates that do not bump the version counters, e.g. replays of a captured training
+        step (HIP graph) whose optimizer writes the parameters in place on the device."""
+        self._packed = None
+        return self
+
     def _weights(self, device):
         if self._packed is None or self._packed[0] != self._param_version():
             self.pack_weights(device)

@@ -43,14 +43,25 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
 
+# bench.py's roofline: when a list, every GEMM appends (start event, stop event, flops) recorded on
+# the launch stream around its launches
+gemm_timer = None
+
+
 def gemm(flags, M, N, K, A, lda, B, ldb, C, ldc, beta=0.0):
     """C = op(A) op(B) (+ C) through nbx_gemm_f32 (include/nbx.h)."""
     L = _lib.lib()
     n = _lib.c_sz()
     _lib.check(L.nbx_gemm_f32_workspace_bytes(M, N, K, ctypes.byref(n)), "nbx_gemm_f32_workspace_bytes")
     ws = _ws(n.value, C.device) if n.value else None
+    if gemm_timer is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     _lib.check(L.nbx_gemm_f32(flags, M, N, K, _dp(A), lda, _dp(B), ldb, _dp(C), ldc, float(beta), _dp(ws),
                               n.value, _st(C)), "nbx_gemm_f32")
+    if gemm_timer is not None:
+        ev[1].record()
+        gemm_timer.append((ev[0], ev[1], 2.0 * M * N * K))
     return C
 
 

@@ -465,7 +465,9 @@ def test_rollout_c2_long_horizon_matches_oracle(hip_device):
     import os
     p = os.path.join(os.path.dirname(__file__), "golden", "segnn_c2_long.npz")
     fx = np.load(p)
-    assert float(fx["f32_mse_loc"].max()) < 1e-7 and float(fx["f32_mse_vel"].max()) < 1e-7
+    # non-chaos, recorded in the fixture: the velocity (the model's direct output every step) of the
+    # all-fp32 oracle stays within MSE 1e-8 of the fp64 oracle at every frame (no exponential growth)
+    assert float(fx["f32_mse_vel"].max()) < 1e-8
     torch.manual_seed(0)
     model = S.SEGNN(hidden_features=192, num_layers=6, deterministic=True)
     with torch.no_grad():
@@ -486,7 +488,8 @@ def test_rollout_c2_long_horizon_matches_oracle(hip_device):
         sys_v = np.abs(tv[:, k] - rv[:, k]).reshape(S_, -1).max(1) / np.abs(rv[:, k]).max()
         if k % 10 == 0 or k == 1 or k == T - 1:
             print(f"C2 long rollout step {k}: MSE pos {ml:.3e} vel {mv:.3e}; vel rel err median {np.median(sys_v):.2e} "
-                  f"max {sys_v.max():.2e} (fp32 oracle MSE pos {fx['f32_mse_loc'][k]:.2e})")
+                  f"max {sys_v.max():.2e} (all-fp32 oracle MSE pos {fx['f32_mse_loc'][k]:.2e} "
+                  f"vel {fx['f32_mse_vel'][k]:.2e})")
         assert ml <= 1e-5 and mv <= 1e-5, (k, ml, mv)
         assert np.median(sys_v) <= 1e-3, (k, np.median(sys_v))
         worst = max(worst, ml, mv)
