@@ -156,3 +156,74 @@ def test_syncbn_rccl_communicator_single_rank(hip_device):
     np.testing.assert_array_equal(res[0][0], out)
     np.testing.assert_array_equal(res[0][2], tp)
     np.testing.assert_array_equal(res[0][3], tv)
+
+
+class _GtDataset:
+    """run_inference's dataset contract (batch_size, double_precision, target,
+    get_ground_truth_trajectories): system i of the global batch starts at GravitySim frame 0 of seed i,
+    whichever rank holds it (the reference draws unseeded trajectories; fixed seeds make the sharded and
+    the single-process rollouts comparable)."""
+
+    def __init__(self, B, T, N=5):
+        self.batch_size, self.double_precision, self.target = B, False, "pos_dt+vel"
+        self.T, self.N = T, N
+
+    def get_ground_truth_trajectories(self, batch_size=None, seeds=None, shard=None):
+        import torch.distributed as dist
+        from nbody_amd.parallel import shard_range
+        from oracle.gravity import initial_conditions
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        start, _ = shard_range(self.batch_size, rank, world) if batch_size != self.batch_size else (0, 0)
+        out = []
+        for i in range(batch_size):
+            p, v, _ = initial_conditions(self.N, start + i)
+            out.append((np.repeat(p[None], self.T, 0), np.repeat(v[None], self.T, 0), np.zeros((self.T, self.N, 3)),
+                        np.ones((self.N, 1))))
+        return out, {}
+
+
+def _inference_worker(rank, world, port, q, B, T, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import nbody_amd.inference as I
+        model = _model(torch.device("cuda:0"))
+        _, locs, vels = I.run_inference("segnn", None, model=model, dataset=_GtDataset(B, T), device="cuda:0",
+                                        save_dir=os.path.join(out_dir, f"r{rank}"), max_rollout_steps=T,
+                                        print_step=False)
+        q.put((rank, (locs[1], vels[1])))
+    except Exception as e:  # surfaced by the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_run_inference_native_segnn_matches_single_process(hip_device, tmp_path):
+    """run_inference sharded over two ranks (gloo, both on the box's GPU) with the native SEGNN rollout in
+    train mode: each rank rolls out its half of the batch with SyncBN (the reference's full-batch
+    BatchNorm statistics), one all-gather reassembles [2, B, T, N, 3]; the predictions equal the
+    single-process run_inference of the whole batch."""
+    import nbody_amd.inference as I
+    B, T = 48, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inference_worker, args=(r, 2, port, q, B, T, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert not isinstance(res[r], str), res[r]
+    _, locs, vels = I.run_inference("segnn", None, model=_model(hip_device), dataset=_GtDataset(B, T),
+                                    device=hip_device, save_dir=str(tmp_path / "single"), max_rollout_steps=T,
+                                    print_step=False)
+    for r in (0, 1):
+        np.testing.assert_allclose(res[r][0], locs[1], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(res[r][1], vels[1], rtol=1e-4, atol=1e-5)
+    assert np.abs(locs[1][:, 1:] - locs[1][:, :1]).max() > 1e-3    # the rollout moved the bodies

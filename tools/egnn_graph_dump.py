@@ -21,6 +21,18 @@ import nbody_amd.graph as G  # noqa: E402
 from nbody_amd.egnn_mc import EGNNMultiChannel  # noqa: E402
 
 
+def dump_graph(cg, path):
+    """hipGraphDebugDotPrint of the captured hipGraph_t (CUDAGraph(keep_graph=True).raw_cuda_graph())."""
+    import ctypes
+    try:
+        g = cg.raw_cuda_graph()
+        hip = ctypes.CDLL("libamdhip64.so")
+        rc = hip.hipGraphDebugDotPrint(ctypes.c_void_p(g), path.encode(), ctypes.c_uint(1 << 0 | 1 << 2 | 1 << 3))
+        print(f"hipGraphDebugDotPrint -> {rc}")
+    except Exception as e:   # diagnosis only
+        print(f"graph dump unavailable: {e!r}")
+
+
 def main(path):
     dev = torch.device("cuda:0")
     B, N, K, W = 64, 5, 12, 3
@@ -57,29 +69,38 @@ def main(path):
         losses = []
         if not graph:
             for _ in range(K):
-                losses.append(float(body()))
+                losses.append(float(body().detach()))
             return losses
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(W):
-                losses.append(float(body()))
+                losses.append(float(body().detach()))
         torch.cuda.current_stream().wait_stream(side)
-        cg = torch.cuda.CUDAGraph()
-        cg.enable_debug_mode()
+        try:
+            cg = torch.cuda.CUDAGraph(keep_graph=True)
+        except TypeError:
+            cg = torch.cuda.CUDAGraph()
         with torch.cuda.graph(cg):
             sl = body()
-        cg.debug_dump(path)
-        for _ in range(K - W):
+        dump_graph(cg, path)
+        # back-to-back replays, no host synchronisation in between (the r02 symptom's setting): each
+        # replay's loss is copied on the stream into its own slot
+        hist = torch.empty(K - W, device=dev)
+        for i in range(K - W):
             cg.replay()
-            losses.append(float(sl))   # (synchronises: one replay at a time, like the test)
-        return losses, cg
+            hist[i].copy_(sl.detach())
+        torch.cuda.synchronize()
+        return losses + hist.tolist(), cg
 
     eager = run(False)
     graphed, cg = run(True)
     print("eager  ", " ".join(f"{x:.9g}" for x in eager))
     print("graphed", " ".join(f"{x:.9g}" for x in graphed))
     print("max |diff| over the replays:", max(abs(a - b) for a, b in zip(eager, graphed)))
+    if not os.path.exists(path):
+        print("no graph dump written")
+        return
     txt = open(path).read()
     nodes = dict(re.findall(r'"?(\w+)"?\s*\[[^\]]*label="([^"]*)', txt))
     print(f"graph dump: {path}, {len(nodes)} nodes")
