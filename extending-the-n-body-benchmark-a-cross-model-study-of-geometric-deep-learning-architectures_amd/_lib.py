@@ -74,7 +74,7 @@ class PonitaLayer(ctypes.Structure):
 class PonitaWeights(ctypes.Structure):
     _fields_ = [(n, c_i32) for n in ("hidden", "basis_dim", "widening", "num_layers", "num_ori")] + [
         (n, c_p) for n in ("ori_grid", "basis1_t", "basis1_b", "basis2_t", "basis2_b", "fbasis1_t", "fbasis1_b",
-                           "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w", "basis2_img_x3")] + [
+                           "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w", "basis2_img_x3", "basis_ffn_img_x3")] + [
         ("layers", PonitaLayer * PONITA_MAX_LAYERS)]
 
 

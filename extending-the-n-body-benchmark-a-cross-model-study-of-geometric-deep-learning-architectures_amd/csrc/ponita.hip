@@ -411,30 +411,42 @@ __global__ __launch_bounds__(256) void po_basis1_kernel(const float* __restrict_
 }
 
 struct FfnProb {
-    const float* XN;      // [rows][C] LayerNorm output (GEMM 1 input)
-    float* X;             // [rows][C] residual in, layer output (in place)
+    const float* XN;      // [rows][ldi] GEMM 1 input: the LayerNorm output (ConvNext), P16 (kernel basis)
+    float* X;             // [rows][C] residual in, layer output (in place); the kernel basis KB (FFN_BASIS)
     const void* img;      // [F/32] slabs [W1 chunk | W2 chunk] (include/nbx.h ffn_img_x3)
     const float* b1;      // [F]
     const float* b2;      // [C]
     const float* scale;   // [C] layer_scale or null
     int64_t rows;
     int F;                // hidden width (multiple of 32, <= FFN_FMAX)
+    int ldi;              // GEMM 1 input row stride (floats); input columns >= ldi read as zeros
     unsigned long long* dbg;   // tuning only (NBX_PO_FFN_DEBUG): per-wave phase clocks [4]
 };
 constexpr int FFN_FMAX = 1024;
 
-template <int NT>   // NT = C / 32
+// MODE FFN_CONVNEXT: the ConvNext MLP, X = X + scale (W2 GELU(W1 XN + b1) + b2), input width NTI 32 =
+// output width NTO 32 = C.  MODE FFN_BASIS (r03): the kernel-basis MLP of ponita_pg.py:92-98,140-142,
+// KB = GELU(W2 GELU(W1 P16 + b1) + b2), input the 16 polynomial features (NTI = 1: one 32-deep K chunk,
+// columns 16-31 read as zeros against zero weights), output Bk = NTO 32 columns stored, so the [E O][C]
+// hidden activation (839 MB at C3) never reaches HBM.
+constexpr int FFN_CONVNEXT = 0, FFN_BASIS = 1;
+template <int NTI, int NTO, int MODE>
 __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb P) {
     using nbx::bf16x8;
     using nbx::floatx16;
-    constexpr int C = NT * 32;
-    constexpr int PART = NT * nbx::LIN_X3_BLK;   // floats of one chunk's W1 (or W2) blocks
-    constexpr int PW = PART / 256 / FFN_WAVES;    // DMA pieces per wave per part
-    static_assert(PART % (256 * FFN_WAVES) == 0, "po_ffn: a part must split evenly over the waves");
+    constexpr int NT = NTO;               // output column tiles (the scheduling groups' unit)
+    constexpr int C = NTO * 32;           // output width
+    constexpr int PART1 = NTI * nbx::LIN_X3_BLK;   // floats of one chunk's W1 blocks
+    constexpr int PART = NTO * nbx::LIN_X3_BLK;    // floats of one chunk's W2 blocks
+    constexpr int NP1 = PART1 / 256;               // W1 DMA pieces (1 KiB each) per chunk
+    constexpr int PW1 = (NP1 + FFN_WAVES - 1) / FFN_WAVES;
+    constexpr int PW = PART / 256 / FFN_WAVES;    // W2 DMA pieces per wave per part
+    static_assert(PART % (256 * FFN_WAVES) == 0, "po_ffn: a W2 part must split evenly over the waves");
+    static_assert(PART1 % 256 == 0, "po_ffn: a W1 part is whole DMA pieces");
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* ring1 = lds;                 // 3 x PART: W1 chunks (chunk c in slot c % 3)
-    float* ring2 = lds + 3 * PART;      // 3 x PART: W2 chunks
-    float* b1s = lds + 6 * PART;        // [F]
+    float* ring1 = lds;                 // 3 x PART1: W1 chunks (chunk c in slot c % 3)
+    float* ring2 = lds + 3 * PART1;     // 3 x PART: W2 chunks
+    float* b1s = ring2 + 3 * PART;      // [F]
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
     const int nj = P.F >> 5;
     const int64_t row0 = ((int64_t)blockIdx.x * FFN_WAVES + wave) * 32;
@@ -442,29 +454,31 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     const bool ok = row < P.rows;
     const float* img = reinterpret_cast<const float*>(P.img);
     const unsigned long long c0t = P.dbg ? clock64() : 0ull;
-    auto w1src = [&](int j) { return img + (size_t)j * 2 * PART; };
-    auto w2src = [&](int j) { return img + (size_t)j * 2 * PART + PART; };
+    auto w1src = [&](int j) { return img + (size_t)j * (PART1 + PART); };
+    auto w2src = [&](int j) { return img + (size_t)j * (PART1 + PART) + PART1; };
 
     // prologue: input rows (lane (row, h) holds k = 32 kc + 16 h + 8 m + i, the image K order), b1,
     // W1 chunks 0-2 and W2 chunk 0; W2 chunk 1 then goes in flight
-    bf16x8 ax[NT][3][2];
+    bf16x8 ax[NTI][3][2];
     {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.XN, (short)0, 0x7FFFFFF0, 0x00020000);
-        const uint32_t base = (uint32_t)(((ok ? row : 0) * C + 16 * h) * 4);
-        float4 a[NT][4];
+        const uint32_t base = (uint32_t)(((ok ? row : 0) * P.ldi + 16 * h) * 4);
+        float4 a[NTI][4];
 #pragma unroll
-        for (int kc = 0; kc < NT; ++kc)
+        for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < 4; ++q) {
+                const bool in = ok && 32 * kc + 16 * h + 4 * q < P.ldi;   // (ldi % 4 == 0)
                 a[kc][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs, ok ? base + (uint32_t)(kc * 128 + 16 * q) : 0x7FFFFFF0u, 0, 0));
+                                                          rs, in ? base + (uint32_t)(kc * 128 + 16 * q) : 0x7FFFFFF0u, 0, 0));
+            }
         float bv[FFN_FMAX / (64 * FFN_WAVES)];
 #pragma unroll
         for (int u = 0; u < FFN_FMAX / (64 * FFN_WAVES); ++u) {
             const int i = t + u * 64 * FFN_WAVES;
             bv[u] = i < P.F ? P.b1[i] : 0.f;
         }
-        for (int c = 0; c < 3 && c < nj; ++c) nbx::tp_dma_image<FFN_WAVES>(w1src(c), ring1 + c * PART, PART);
+        for (int c = 0; c < 3 && c < nj; ++c) nbx::tp_dma_image<FFN_WAVES>(w1src(c), ring1 + c * PART1, PART1);
         nbx::tp_dma_image<FFN_WAVES>(w2src(0), ring2, PART);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -473,14 +487,14 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
             if (i < P.F) b1s[i] = bv[u];
         }
 #pragma unroll
-        for (int kc = 0; kc < NT; ++kc) {
+        for (int kc = 0; kc < NTI; ++kc) {
             nbx::tp_split3(a[kc][0], a[kc][1], ax[kc][0][0], ax[kc][1][0], ax[kc][2][0]);
             nbx::tp_split3(a[kc][2], a[kc][3], ax[kc][0][1], ax[kc][1][1], ax[kc][2][1]);
         }
         // the input operands live in AGPRs for the whole loop (MFMA reads A/B from either file), which
         // leaves the architectural VGPRs to the weight fragments and the GELU arithmetic
 #pragma unroll
-        for (int kc = 0; kc < NT; ++kc)
+        for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
             for (int p3 = 0; p3 < 3; ++p3)
 #pragma unroll
@@ -499,16 +513,16 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     auto gemm1 = [&](const float* buf) {
         // all of the chunk's fragments are read first (one LDS latency per chunk, not per 6 MFMAs)
         const bf16x8* w1 = reinterpret_cast<const bf16x8*>(buf) + lane;
-        bf16x8 b[NT][2][3];
+        bf16x8 b[NTI][2][3];
 #pragma unroll
-        for (int kc = 0; kc < NT; ++kc)
+        for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
             for (int m = 0; m < 2; ++m)
 #pragma unroll
                 for (int p3 = 0; p3 < 3; ++p3) b[kc][m][p3] = w1[kc * (nbx::LIN_X3_BLK / 4) + m * 64 + p3 * 128];
         floatx16 g;
 #pragma unroll
-        for (int kc = 0; kc < NT; ++kc)
+        for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 const bf16x8(&a)[3][2] = ax[kc];
@@ -565,7 +579,7 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     floatx16 gq[2];
     bf16x8 hq[2][3][2];
     gq[0] = gemm1(ring1);                               // chunk 0
-    if (nj > 1) gq[1] = gemm1(ring1 + PART);           // chunk 1
+    if (nj > 1) gq[1] = gemm1(ring1 + PART1);          // chunk 1
     gelu_split(0, gq[0], hq[0]);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -580,6 +594,17 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
                                              (__attribute__((address_space(3))) void*)(dst + p * 256), 16, 0, 0);
         }
     };
+    // a W1 part (NP1 pieces, possibly fewer than one per wave per round): issued before the same
+    // iteration's W2 part, so the wait for all but W2's PW pieces covers it
+    auto dma_part1 = [&](const float* src, float* dst) {
+#pragma unroll
+        for (int i = 0; i < PW1; ++i) {
+            const int p = wave + i * FFN_WAVES;
+            if (p < NP1)
+                __builtin_amdgcn_global_load_lds((const void*)(src + p * 256 + lane * 4),
+                                                 (__attribute__((address_space(3))) void*)(dst + p * 256), 16, 0, 0);
+        }
+    };
     // iteration j; FULL: every step of the steady state (W1 chunk j + 3 and W2 chunk j + 2 exist), so
     // the body is one basic block the scheduling groups can interleave
     // SLOT: j % 3 when known at compile time (the steady state is unrolled by 6), else -1
@@ -589,11 +614,11 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
         constexpr int SLOT = decltype(slotc)::value;
         const int s0 = SLOT >= 0 ? SLOT : j % 3, s2 = SLOT >= 0 ? (SLOT + 2) % 3 : (j + 2) % 3;
         const bool d1 = FULL || j + 3 < nj, d2 = FULL || j + 2 < nj;
-        if (d1) dma_part(w1src(j + 3), ring1 + s0 * PART);
+        if (d1) dma_part1(w1src(j + 3), ring1 + s0 * PART1);
         if (d2) dma_part(w2src(j + 2), ring2 + s2 * PART);
         // gq[nxt] holds chunk j + 1's GEMM 1 result; gq[cur] receives chunk j + 2's
         if (FULL || j + 1 < nj) gelu_split(j + 1, gq[nxt], hq[nxt]);
-        if (FULL || j + 2 < nj) gq[cur] = gemm1(ring1 + s2 * PART);
+        if (FULL || j + 2 < nj) gq[cur] = gemm1(ring1 + s2 * PART1);
         gemm2(ring2 + s0 * PART, hq[cur]);
         if constexpr (FULL) {
             // GEMM 1's fragment reads first; its 12 NT MFMAs each followed by ~5 vector instructions
@@ -651,7 +676,10 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
             const float b = P.b2[col];
             const float sc = P.scale ? P.scale[col] : 1.f;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) tile[((e & 3) + 8 * (e >> 2) + 4 * h) * LDR + col] = sc * (acc[tt][e] + b);
+            for (int e = 0; e < 16; ++e) {
+                const float v = MODE == FFN_BASIS ? gelu_nb(acc[tt][e] + b) : sc * (acc[tt][e] + b);
+                tile[((e & 3) + 8 * (e >> 2) + 4 * h) * LDR + col] = v;
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's own tile: no cross-wave hand-off
         constexpr int F4 = 32 * C / 4 / 64;   // float4 per lane
@@ -659,8 +687,9 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
 #pragma unroll
         for (int i = 0; i < F4; ++i) {
             const int f = lane + 64 * i, rr = f / (C / 4), c4 = f % (C / 4);
-            res[i] = row0 + rr < P.rows ? *reinterpret_cast<const float4*>(P.X + (row0 + rr) * C + 4 * c4)
-                                        : float4{0.f, 0.f, 0.f, 0.f};
+            res[i] = MODE == FFN_CONVNEXT && row0 + rr < P.rows
+                         ? *reinterpret_cast<const float4*>(P.X + (row0 + rr) * C + 4 * c4)
+                         : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int i = 0; i < F4; ++i) {
@@ -677,17 +706,18 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     }
 }
 
-template <int NT>
+template <int NTI, int NTO, int MODE>
 int po_ffn_launch(const FfnProb& p, hipStream_t st) {
     if (p.rows <= 0) return NBX_OK;
     NBX_CHECK_ARG(p.F % 32 == 0 && p.F >= 32 && p.F <= FFN_FMAX && p.img && p.b1 && p.b2,
                   "po_ffn: 32 <= F <= %d, F %% 32 == 0, an image, b1 and b2 required", FFN_FMAX);
-    NBX_CHECK_ARG((double)p.rows * NT * 32 * 4.0 < 2147483632.0, "po_ffn: XN spans >= 2 GiB");
-    const size_t lds = (6 * (size_t)NT * nbx::LIN_X3_BLK + p.F) * 4;
+    NBX_CHECK_ARG((double)p.rows * p.ldi * 4.0 < 2147483632.0, "po_ffn: XN spans >= 2 GiB");
+    NBX_CHECK_ARG(p.ldi % 4 == 0 && p.ldi <= NTI * 32, "po_ffn: input stride must be a multiple of 4, <= %d", NTI * 32);
+    const size_t lds = (3 * (size_t)(NTI + NTO) * nbx::LIN_X3_BLK + p.F) * 4;
     NBX_CHECK_ARG(lds <= 160 * 1024, "po_ffn: %zu bytes of LDS", lds);
     static bool attr_set = false;
     if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)po_ffn_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        NBX_HIP(hipFuncSetAttribute((const void*)po_ffn_kernel<NTI, NTO, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024));
         attr_set = true;
     }
@@ -698,7 +728,7 @@ int po_ffn_launch(const FfnProb& p, hipStream_t st) {
     const size_t nw = (size_t)blocks * FFN_WAVES;
     if (debug && !dbg) NBX_HIP(hipMalloc(&dbg, nw * 4 * sizeof(unsigned long long)));
     q.dbg = debug ? dbg : nullptr;
-    hipLaunchKernelGGL(po_ffn_kernel<NT>, dim3(blocks), dim3(64 * FFN_WAVES), lds, st, q);
+    hipLaunchKernelGGL((po_ffn_kernel<NTI, NTO, MODE>), dim3(blocks), dim3(64 * FFN_WAVES), lds, st, q);
     NBX_HIP(hipGetLastError());
     if (debug) {   // tuning only: average clocks per wave of prologue / loop / loop-end waits / epilogue
         std::vector<unsigned long long> hb(nw * 4);
@@ -758,7 +788,16 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
     hipLaunchKernelGGL(po_lift_kernel, dim3(g1(VO * (C / 4))), dim3(256), 0, st, mass, vel, w->ori_grid, w->embed_w, d.V, O,
                        C, ws.X);
     NBX_LAUNCH_CHECK("ponita prep");
-    {
+    // both kernel-basis layers in one kernel when the weights carry the fused image (NBX_PO_BASIS_FUSED=0:
+    // the two-kernel path, A/B only)
+    static const bool basis_fused = !(getenv("NBX_PO_BASIS_FUSED") && getenv("NBX_PO_BASIS_FUSED")[0] == '0');
+    if (w->basis_ffn_img_x3 && basis_fused && (Bk == 128 || Bk == 64) && C % 32 == 0 && C <= FFN_FMAX) {
+        const FfnProb fb{ws.P16, ws.KB, w->basis_ffn_img_x3, w->basis1_b, w->basis2_b, nullptr, d.R, C, 16, nullptr};
+        if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * (14 * C + C * Bk), Ev * f4 * (16 + Bk), [&] {
+                return Bk == 128 ? po_ffn_launch<1, 4, FFN_BASIS>(fb, st) : po_ffn_launch<1, 2, FFN_BASIS>(fb, st);
+            }))
+            return rc;
+    } else {
         LinProb p = nbx::lin_dense(ws.P16, 16, 16, (int)d.R, w->basis1_t, 32, C, w->basis1_b, ws.B1H1, C);
         // layer 1 as a streaming kernel (NBX_PO_BASIS1=0: the generic GEMM, A/B only)
         static const bool b1s = !(getenv("NBX_PO_BASIS1") && getenv("NBX_PO_BASIS1")[0] == '0');
@@ -775,6 +814,8 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
         if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * C * Bk, Ev * f4 * (C + Bk),
                                 [&] { return lin_auto<nbx::ACT_GELU>(q, st); }))
             return rc;
+    }
+    {
         LinProb f1 = nbx::lin_dense(ws.FP, 4, 4, OO, w->fbasis1_t, 32, C, w->fbasis1_b, ws.FB1, C);
         if (int rc = lin_auto<nbx::ACT_GELU>(f1, st)) return rc;
         LinProb f2 = nbx::lin_dense(ws.FB1, C, C, OO, w->fbasis2_t, kp(C), Bk, w->fbasis2_b, ws.FKB, Bk);
@@ -831,9 +872,9 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
         if (Ly.ffn_img_x3 && po_x3_enabled() && (C == 64 || C == 128) && d.mlp % 32 == 0 && d.mlp <= FFN_FMAX) {
             // ConvNext MLP fused (linear_1 + GELU + linear_2 + layer_scale + residual): the hidden
             // activation stays in registers (po_ffn_kernel)
-            const FfnProb fp{ws.XN, ws.X, Ly.ffn_img_x3, Ly.lin1_b, Ly.lin2_b, Ly.layer_scale, VO, d.mlp, nullptr};
+            const FfnProb fp{ws.XN, ws.X, Ly.ffn_img_x3, Ly.lin1_b, Ly.lin2_b, Ly.layer_scale, VO, d.mlp, C, nullptr};
             if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * 2.0 * VO * C * d.mlp, (double)VO * f4 * 3 * C, [&] {
-                    return C == 128 ? po_ffn_launch<4>(fp, st) : po_ffn_launch<2>(fp, st);
+                    return C == 128 ? po_ffn_launch<4, 4, FFN_CONVNEXT>(fp, st) : po_ffn_launch<2, 2, FFN_CONVNEXT>(fp, st);
                 }))
                 return rc;
         } else {   // ConvNext MLP with the residual in the epilogue

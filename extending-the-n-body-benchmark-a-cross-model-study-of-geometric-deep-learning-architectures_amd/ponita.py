@@ -249,6 +249,9 @@ class PONITA_NBODY(nn.Module):
                     img = P[name]
                     P[name] = img.reshape(img.shape[0], W.shape[1] // 32, -1).transpose(0, 1).contiguous()
         C = m.hidden_dim
+        # the kernel-basis MLP as one fused kernel (csrc/ponita.hip po_ffn_kernel FFN_BASIS)
+        if C % 32 == 0 and C <= 1024 and m.basis_dim in (64, 128) and P["basis1_t"].shape[1] == 32:
+            P["basis_ffn_img_x3"] = self._ffn_image(P["basis1_t"], P["basis2_t"])
         for i in range(len(m.interaction_layers)):
             p = f"layers.{i}."
             if C in (64, 128) and P[p + "lin1_t"].shape[0] % 32 == 0:
@@ -288,6 +291,7 @@ class PONITA_NBODY(nn.Module):
                      "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w"):
             setattr(W, name, P[name].data_ptr())
         W.basis2_img_x3 = P["basis2_img_x3"].data_ptr() if "basis2_img_x3" in P else None
+        W.basis_ffn_img_x3 = P["basis_ffn_img_x3"].data_ptr() if "basis_ffn_img_x3" in P else None
         for i in range(W.num_layers):
             L = W.layers[i]
             for name, _ in L._fields_:

@@ -490,6 +490,11 @@ typedef struct nbx_ponita_weights {
     const float* fiber_t;
     const float* embed_w;
     const void* basis2_img_x3;   /* optional bf16x3 image of basis2_t (as the layer images) */
+    /* optional (ABI 10): both kernel-basis layers in one kernel (hidden width = hidden, basis_dim 64 or
+     * 128): per 32-wide hidden chunk one slab [basis1_t rows of the chunk | basis2_t columns of the
+     * chunk, K order permuted], the ffn_img_x3 layout with one 32-deep input chunk; the [E O][hidden]
+     * activation between the layers never reaches HBM */
+    const void* basis_ffn_img_x3;
     nbx_ponita_layer layers[NBX_PONITA_MAX_LAYERS];
 } nbx_ponita_weights;
 
