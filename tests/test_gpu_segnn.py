@@ -455,19 +455,20 @@ def test_rollout_c2_long_horizon_matches_oracle(hip_device):
     """north_star "rollout MSE <= 1e-5 vs reference" over a long C2 horizon (120 steps): the C2 model
     and workload (hidden 192, 6 layers, N=5, B=1024, train-mode BatchNorm over the whole batch,
     GravitySim frame-0 states) with pre_pool2 scaled so each step moves a body by ~1e-3 of the
-    inter-body spacing (tests/golden/make_segnn_c2_long.py).  The fixture proves these dynamics are
-    not chaotic over the horizon: the oracle computed entirely in fp32 stays within MSE 1e-7 of the
-    fp64 oracle at every frame.  The device rollout runs with deterministic BatchNorm
-    (SEGNN(deterministic=True)); per frame over the fixture's 64-system slice:
-      * MSE(device, fp64 oracle) <= 1e-5 for positions and velocities (north_star), printed;
-      * the position MSE within 10x that of the all-fp32 oracle (the device path is measured 10-1000x
-        closer to fp64 than a plain fp32 computation of the same algorithm)."""
+    inter-body spacing (tests/golden/make_segnn_c2_long.py).  The fixture proves the horizon is
+    predictable: the fp64 oracle started one fp32 ulp away (another valid fp32 rounding of the same
+    state) stays within MSE 1e-7 of the fp64 oracle at every frame (max 5.9e-9 at frame 120).  The
+    device rollout runs with deterministic BatchNorm (SEGNN(deterministic=True)); per frame over the
+    fixture's 64-system slice:
+      * MSE(device, fp64 oracle) <= 1e-5 for positions and velocities (north_star), printed beside the
+        one-ulp sensitivity (measured: the device error is at that level);
+      * the position MSE within 10x that of the all-fp32 oracle (measured 10-1000x closer to fp64)."""
     import os
     p = os.path.join(os.path.dirname(__file__), "golden", "segnn_c2_long.npz")
     fx = np.load(p)
-    # non-chaos, recorded in the fixture: the velocity (the model's direct output every step) of the
-    # all-fp32 oracle stays within MSE 1e-8 of the fp64 oracle at every frame (no exponential growth)
-    assert float(fx["f32_mse_vel"].max()) < 1e-8
+    # predictability, recorded in the fixture: the fp64 oracle rollout from initial states one fp32 ulp
+    # away stays within MSE 1e-7 of the fp64 oracle at every frame
+    assert float(fx["pert_mse_loc"].max()) < 1e-7 and float(fx["pert_mse_vel"].max()) < 1e-7
     torch.manual_seed(0)
     model = S.SEGNN(hidden_features=192, num_layers=6, deterministic=True)
     with torch.no_grad():
@@ -488,8 +489,8 @@ def test_rollout_c2_long_horizon_matches_oracle(hip_device):
         sys_v = np.abs(tv[:, k] - rv[:, k]).reshape(S_, -1).max(1) / np.abs(rv[:, k]).max()
         if k % 10 == 0 or k == 1 or k == T - 1:
             print(f"C2 long rollout step {k}: MSE pos {ml:.3e} vel {mv:.3e}; vel rel err median {np.median(sys_v):.2e} "
-                  f"max {sys_v.max():.2e} (all-fp32 oracle MSE pos {fx['f32_mse_loc'][k]:.2e} "
-                  f"vel {fx['f32_mse_vel'][k]:.2e})")
+                  f"max {sys_v.max():.2e} (one-ulp input change: MSE pos {fx['pert_mse_loc'][k]:.2e} vel "
+                  f"{fx['pert_mse_vel'][k]:.2e}; all-fp32 oracle MSE pos {fx['f32_mse_loc'][k]:.2e})")
         assert ml <= 1e-5 and mv <= 1e-5, (k, ml, mv)
         # and at least as close to fp64 as the same algorithm computed in fp32 arithmetic
         assert ml <= 10.0 * fx["f32_mse_loc"][k] + 1e-13, (k, ml, fx["f32_mse_loc"][k])
