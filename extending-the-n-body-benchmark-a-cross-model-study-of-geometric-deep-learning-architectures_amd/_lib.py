@@ -12,10 +12,11 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 10
+ABI_VERSION = 11
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B = 1, 2
+ACT_NONE, ACT_GELU = 0, 1
 MAX_LAYERS = 64
 
 c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double,
@@ -137,6 +138,16 @@ _SIGNATURES = {
     "nbx_segment_sum": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_i32, c_p]),
     "nbx_segnn_train_featurize": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                                  c_p, c_p]),
+    "nbx_ponita_train_featurize": (ctypes.c_int, [c_i64, c_i64, c_i32] + [c_p] * 10),
+    "nbx_bias_act": (ctypes.c_int, [c_i64, c_i32, c_p, c_i64, c_p, c_i32, c_p, c_i64, c_p]),
+    "nbx_bias_act_backward": (ctypes.c_int, [c_i64, c_i32, c_p, c_i64, c_p, c_i32, c_p, c_p, c_p]),
+    "nbx_po_message": (ctypes.c_int, [c_i64, c_i32, c_i32] + [c_p] * 7),
+    "nbx_po_message_backward": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32] + [c_p] * 10),
+    "nbx_po_fiber_conv": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_po_fiber_conv_workspace_bytes": (ctypes.c_int, [c_i64, c_i32, c_i32, ctypes.POINTER(c_sz)]),
+    "nbx_po_fiber_conv_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_layernorm_forward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "nbx_layernorm_backward": (ctypes.c_int, [c_i64, c_i32] + [c_p] * 7),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),

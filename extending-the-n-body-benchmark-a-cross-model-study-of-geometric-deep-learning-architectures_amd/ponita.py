@@ -355,6 +355,21 @@ class PONITA_NBODY(nn.Module):
         m = f(x.reshape(V))
         vel = graph.vec if getattr(graph, "vec", None) is not None else graph.vel
         p, v = f(pos), f(vel.reshape(V, 3))
+        if torch.is_grad_enabled() and any(t.requires_grad for t in self.parameters()):
+            # training step: native operators under autograd (ponita_train.py).  A model
+            # still owing its one-time calibration gets it first from a no-grad forward, as the
+            # reference's train.py:49-77 dummy forward does before the first optimiser step.
+            if self._native_reason:
+                raise NotImplementedError(self._native_reason)
+            self.model.materialize()
+            if self._needs_callibration():
+                with torch.no_grad():
+                    self.forward(graph)
+            from . import ponita_train
+            if ei is None:
+                from .graph import fc_edge_index
+                ei = fc_edge_index(B, N, device)
+            return ponita_train.train_forward(self, p, v, m, ei).to(pos.dtype)
         out = torch.empty(V, 6, device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(W, B, N, device)

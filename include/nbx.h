@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 10
+#define NBX_ABI_VERSION 11
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -337,6 +337,55 @@ int nbx_segment_sum(int64_t n, int32_t cols, const int32_t* ptr, const int32_t* 
 int nbx_segnn_train_featurize(int64_t V, int64_t E, const float* pos, const float* vel, const float* mass,
                               const int32_t* src, const int32_t* dst, const int32_t* dst_ptr, const int32_t* dst_eid,
                               float* na3, float* xs0, float* xv0, float* rhat, float* amf, void* stream);
+
+/* ------------------------------------------------------------------------
+ * PONITA training step (ABI 11; SURVEY §8(f)4: trainer.py:233-358 on PONITA_NBODY,
+ * models/ponita/models/ponita_pg.py:134-192, nn/conv.py:103-133, nn/convnext.py:18-32).  The training
+ * forward and backward (ponita_train.py, autograd) are composed of nbx_gemm_f32 (every nn.Linear),
+ * nbx_colsum (bias / LayerNorm parameter gradients), the CSRs of nbx_segment_sum's convention and
+ * the operators below, on the fibre-bundle layout: node rows [V][O][C], edge rows [E][O][*], fibre
+ * rows [O][O][*] (o major).  fp32; every reduction in a fixed order (bit-reproducible).
+ */
+#define NBX_ACT_NONE 0
+#define NBX_ACT_GELU 1   /* nn.GELU(): 0.5 x (1 + erf(x / sqrt 2)) */
+
+/* Invariants + degree-3 polynomial features (no gradient): attr [E*O][16] (16-byte aligned) =
+ * poly(r.o, |r - (r.o) o|) (14 features, 2 zero pads), r = pos[src] - pos[dst]; fiber [O*O][4] =
+ * (s, s^2, s^3, 0), s = o_p . o_o; lift [V*O][2] = (mass, vel . o). */
+int nbx_ponita_train_featurize(int64_t V, int64_t E, int32_t O, const float* pos, const float* vel, const float* mass,
+                               const float* ori_grid, const int32_t* src, const int32_t* dst, float* attr, float* fiber,
+                               float* lift, void* stream);
+
+/* Y[r][c] = act(Z[r][c] + bias[c]) (bias may be NULL); backward dZ = dY act'(Z + bias), dY / dZ
+ * contiguous [rows][cols]. */
+int nbx_bias_act(int64_t rows, int32_t cols, const float* Z, int64_t ldz, const float* bias, int32_t act, float* Y,
+                 int64_t ldy, void* stream);
+int nbx_bias_act_backward(int64_t rows, int32_t cols, const float* Z, int64_t ldz, const float* bias, int32_t act,
+                          const float* dY, float* dZ, void* stream);
+
+/* Separable spatial message, aggr "add" at edge_index[1]: X1[v][o][c] = sum over the edges e into v
+ * (dst CSR) of K[e][o][c] H[src_e][o][c].  Backward: dK[e] = dX1[dst_e] H[src_e] (NULL: skipped) and
+ * dH[u] = sum over the edges out of u (src CSR) of dX1[dst_e] K[e] (NULL: skipped). */
+int nbx_po_message(int64_t V, int32_t O, int32_t C, const int32_t* dst_ptr, const int32_t* dst_eid, const int32_t* src,
+                   const float* K, const float* H, float* X1, void* stream);
+int nbx_po_message_backward(int64_t V, int64_t E, int32_t O, int32_t C, const int32_t* src, const int32_t* dst,
+                            const int32_t* src_ptr, const int32_t* src_eid, const float* K, const float* H,
+                            const float* dX1, float* dK, float* dH, void* stream);
+
+/* Depth-wise fibre convolution X2[v][p][c] = (sum_o X1[v][o][c] FK[o][p][c]) / O + bias[c];
+ * backward dX1 (NULL: skipped) and dFK (summed over the nodes in fixed chunks; workspace). */
+int nbx_po_fiber_conv(int64_t V, int32_t O, int32_t C, const float* X1, const float* FK, const float* bias, float* X2,
+                      void* stream);
+int nbx_po_fiber_conv_workspace_bytes(int64_t V, int32_t O, int32_t C, size_t* bytes);
+int nbx_po_fiber_conv_backward(int64_t V, int32_t O, int32_t C, const float* X1, const float* FK, const float* dX2,
+                               float* dX1, float* dFK, void* workspace, size_t workspace_bytes, void* stream);
+
+/* LayerNorm over C <= 1024 channels (biased variance): save [2][rows] = (mean, 1/sqrt(var + eps));
+ * backward dX and G [rows][2C] = (dY xhat | dY), whose column sums are dweight | dbias. */
+int nbx_layernorm_forward(int64_t rows, int32_t C, const float* X, const float* weight, const float* bias, float eps,
+                          float* Y, float* save, void* stream);
+int nbx_layernorm_backward(int64_t rows, int32_t C, const float* X, const float* weight, const float* save,
+                           const float* dY, float* dX, float* G, void* stream);
 
 /* ------------------------------------------------------------------------
  * EGNN-MC (models/egnn_mc/egnn_mc.py:45-295 with the preprocessing of
