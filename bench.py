@@ -21,6 +21,8 @@ Secondary configurations (not the headline; same JSON shape):
   --model eqv2     C4: EquiformerV2 (config.yaml widths), N=20, batch 256 per rank ("weak").
   --model egnn_mc_train  SURVEY 8(f)4: EGNN-MC training step (C1 widths, forward + backward + Adam,
                    gradients all-reduced over ranks), batch 64 per rank ("weak").
+  --model segnn_train / ponita_train  SURVEY 8(f)4: SEGNN (C2 widths) / PONITA (config.yaml: 128 x 8)
+                   training step, batch 64 per rank ("weak").
   --model gravity  C5: ground-truth integrator, 10 000 systems x N=100, --steps
                    KDK steps (sample_freq 10), systems sharded over the ranks ("strong").
 
@@ -544,35 +546,19 @@ def bench_egnn_train(a, rank, world, device, P):
 
 
 # ---------------------------------------------------------------- SEGNN training step
-def bench_segnn_train(a, rank, world, device, P):
-    """SURVEY §8(f)4: one SEGNN training step of the reference trainer (trainer.py:233-358) at C2
-    widths (hidden 192, lmax 1, 6 layers, N=5) on the reference's training batch (config.yaml
-    dataloaders batch_size 64 systems per rank, "weak"): zero_grad, train-mode forward on the native
-    training operators (segnn_train.py / csrc/segnn_train.hip), MSE loss, loss.backward() through the
-    native backward, gradient all-reduce over ranks (RCCL), clip to norm 1, AdamW + LambdaLR
-    (trainer.py:170-194).  On one GPU the whole step is one HIP graph replay (--eager: uncaptured)."""
-    import nbody_amd.segnn as S
+def train_loop(a, world, device, P, model, forward, target, model_size):
+    """The reference trainer's step (trainer.py:170-194,233-358): zero_grad, forward, MSE loss,
+    loss.backward(), gradient all-reduce over ranks (RCCL), clip to norm 1, AdamW (weight decay 1e-8,
+    betas (0.9, 0.98), eps 1e-9) + LambdaLR (factor 1, warmup 1000, model_size^-0.5).  One eager step
+    first (it also performs any one-time calibration) with every nbx_gemm_f32 launch event-timed for
+    the roofline; on one GPU the step is then captured as one HIP graph (--eager: uncaptured).
+    Returns (last loss, timed seconds, (gemm ms, gemm flops, gemm launches) of one step, graph?)."""
     import nbody_amd.segnn_train as ST
-    from nbody_amd.graph import fc_edge_index
-    B, N = a.batch or 64, NBODY
-    torch.manual_seed(0)
-    model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS).to(device).train()
-    loc, vel, mass = initial_states(B, N, rank * B)
-    rng = np.random.default_rng(100 + rank)
-
-    class _G:
-        pass
-    g = _G()
-    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
-    g.pos, g.vel, g.mass = t(loc.reshape(-1, 3)), t(vel.reshape(-1, 3)), t(mass.reshape(-1, 1))
-    g.edge_index = fc_edge_index(B, N, device)
-    g.nbx_system_size = N
-    target = t(rng.standard_normal((B * N, 6)) * 0.1)
     graph = not a.eager and world == 1
     opt = torch.optim.AdamW(model.parameters(), lr=1.0, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9,
                             fused=True, capturable=graph)
     sched = torch.optim.lr_scheduler.LambdaLR(
-        opt, lambda s: HIDDEN ** -0.5 * min(max(s, 1) ** -0.5, max(s, 1) * 1000 ** -1.5))
+        opt, lambda s: model_size ** -0.5 * min(max(s, 1) ** -0.5, max(s, 1) * 1000 ** -1.5))
     if graph:
         for grp in opt.param_groups:
             grp["lr"] = torch.tensor(float(grp["lr"]), dtype=torch.float32, device=device)
@@ -580,7 +566,7 @@ def bench_segnn_train(a, rank, world, device, P):
 
     def step_body():
         opt.zero_grad(set_to_none=True)
-        loss = torch.nn.functional.mse_loss(model(g), target)
+        loss = torch.nn.functional.mse_loss(forward(), target)
         loss.backward()
         P.allreduce_gradients(params)
         torch.nn.utils.clip_grad_norm_(params, 1.0, foreach=True)
@@ -591,9 +577,8 @@ def bench_segnn_train(a, rank, world, device, P):
     ST.gemm_timer = []
     step_body()
     torch.cuda.synchronize(device)
-    gemm_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ST.gemm_timer)
-    gemm_flops = sum(f for _, _, f in ST.gemm_timer)
-    n_gemm = len(ST.gemm_timer)
+    gemm = (sum(e0.elapsed_time(e1) for e0, e1, _ in ST.gemm_timer), sum(f for _, _, f in ST.gemm_timer),
+            len(ST.gemm_timer))
     ST.gemm_timer = None
     sched.step()
     if graph:
@@ -626,8 +611,37 @@ def bench_segnn_train(a, rank, world, device, P):
             loss = train_step()
         return loss
     loss, elapsed = timed_region(work, device, P)
+    return loss, elapsed, gemm, graph
+
+
+def bench_segnn_train(a, rank, world, device, P):
+    """SURVEY §8(f)4: one SEGNN training step of the reference trainer (trainer.py:233-358) at C2
+    widths (hidden 192, lmax 1, 6 layers, N=5) on the reference's training batch (config.yaml
+    dataloaders batch_size 64 systems per rank, "weak"): zero_grad, train-mode forward on the native
+    training operators (segnn_train.py / csrc/segnn_train.hip), MSE loss, loss.backward() through the
+    native backward, gradient all-reduce over ranks (RCCL), clip to norm 1, AdamW + LambdaLR
+    (trainer.py:170-194).  On one GPU the whole step is one HIP graph replay (--eager: uncaptured)."""
+    import nbody_amd.segnn as S
+    import nbody_amd.segnn_train as ST
+    from nbody_amd.graph import fc_edge_index
+    B, N = a.batch or 64, NBODY
+    torch.manual_seed(0)
+    model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS).to(device).train()
+    loc, vel, mass = initial_states(B, N, rank * B)
+    rng = np.random.default_rng(100 + rank)
+
+    class _G:
+        pass
+    g = _G()
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    g.pos, g.vel, g.mass = t(loc.reshape(-1, 3)), t(vel.reshape(-1, 3)), t(mass.reshape(-1, 1))
+    g.edge_index = fc_edge_index(B, N, device)
+    g.nbx_system_size = N
+    target = t(rng.standard_normal((B * N, 6)) * 0.1)
+    loss, elapsed, gemm, graph = train_loop(a, world, device, P, model, lambda: model(g), target, HIDDEN)
     model.invalidate_weights()   # the replays' AdamW updated the parameters in place
     value = a.steps / elapsed * world
+    gemm_ms, gemm_flops, n_gemm = gemm
     ach = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
     result = {
         "metric": "SEGNN training steps/sec (C2 widths, forward + backward + AdamW)", "value": round(value, 3),
@@ -675,6 +689,88 @@ def bench_segnn_train(a, rank, world, device, P):
         result["cpu_baseline"] = {"value": steps / dt, "unit": "train steps/s", "cores": torch.get_num_threads(),
                                   "kind": "port", "sample": f"{steps} training step(s) of the B={B} batch, torch fp64 "
                                                             f"autograd restatement (oracle/segnn_torch.py), {dt:.2f} s"}
+    return result
+
+
+PONITA_TRAIN = dict(hidden_dim=128, layers=8, num_ori=20, basis_dim=128)   # config.yaml models.ponita
+
+
+def bench_ponita_train(a, rank, world, device, P):
+    """one PONITA training step of the reference trainer (trainer.py:233-358) at the
+    reference's PONITA training configuration (config.yaml: hidden 128, 8 layers, 20 orientations,
+    basis 128, batch_size 64 systems of N=5 per rank, num_neighbors 4 = fully connected; "weak"):
+    zero_grad, forward on the native training operators (ponita_train.py / csrc/ponita_train.hip +
+    nbx_gemm_f32), MSE loss, loss.backward() through the native backward, gradient all-reduce over
+    ranks, clip, AdamW + LambdaLR.  The one-time FiberBundleConv calibration happens in the first
+    (untimed) step's no-grad forward, as the reference's train.py:49-77 dummy forward."""
+    import nbody_amd.ponita as PO
+    B, N = a.batch or 64, NBODY
+    torch.manual_seed(0)
+    model = PO.PONITA_NBODY(**PONITA_TRAIN).to(device).train()
+    model.model.materialize()
+    loc, vel, mass = initial_states(B, N, rank * B)
+    rng = np.random.default_rng(200 + rank)
+    from nbody_amd.graph import build_graph_with_knn
+
+    class _G:
+        pass
+    g = _G()
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    g.pos, g.vec, g.x = t(loc.reshape(-1, 3)), t(vel.reshape(-1, 1, 3)), t(mass.reshape(-1, 1))
+    g.edge_index = build_graph_with_knn(g.pos, B, N, device, N - 1)
+    g.nbx_system_size = N        # no host synchronisation inside the captured step
+    target = t(rng.standard_normal((B * N, 6)) * 0.1)
+    loss, elapsed, gemm, graph = train_loop(a, world, device, P, model, lambda: model(g), target,
+                                            model.get_model_size())
+    gemm_ms, gemm_flops, n_gemm = gemm
+    value = a.steps / elapsed * world
+    ach = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
+    result = {
+        "metric": "PONITA training steps/sec (reference training config, forward + backward + AdamW)",
+        "value": round(value, 3), "unit": "train steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states, random targets, seeded random-init weights)",
+        "config": {"workload": "SURVEY 8(f)4: PONITA hidden 128, 8 layers, 20 orientations, basis 128 training "
+                               "step, N=5, batch 64 per GPU (config.yaml), MSE loss, grad-norm clip 1, AdamW + "
+                               "LambdaLR (trainer.py:170-194)", "model": "PONITA", "global_batch": B * world,
+                   "seq_len": a.steps, "parallelism": f"dp{world}",
+                   "execution": "one HIP graph replay per step (forward, backward, clip, fused AdamW)" if graph
+                                else "eager"},
+        "roofline": {"bound": "mfma", "kernel": "gemm_f32_kernel (nbx_gemm_f32: every nn.Linear of the forward and "
+                                               "backward)",
+                     "achieved": round(ach, 3) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None, "traffic": None,
+                     "avg_launch_us": round(1e3 * gemm_ms / max(n_gemm, 1), 3), "launches_per_step": n_gemm,
+                     "gflop_per_step": round(gemm_flops / 1e9, 4),
+                     "timing": "torch.cuda.Event pairs around every GEMM launch of one eager step, launch stream"},
+        "loss": float(loss.item()), "finite": bool(math.isfinite(float(loss.item())))}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import ponita_torch as OT
+        Pc = {k: v.detach().double().cpu().clone().requires_grad_(not (k.endswith("callibrated") or
+                                                                       k.endswith("ori_grid")))
+              for k, v in model.state_dict().items()}
+        learn = [v for v in Pc.values() if v.requires_grad]
+        optc = torch.optim.AdamW(learn, lr=1e-4, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9)
+        pc = torch.from_numpy(loc.reshape(-1, 3))
+        vc, mc = torch.from_numpy(vel.reshape(-1, 1, 3)), torch.from_numpy(mass.reshape(-1, 1))
+        ei = g.edge_index.cpu()
+        grid = Pc["model.ori_grid"]
+        tc = target.double().cpu()
+        steps = max(1, a.cpu_steps)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            optc.zero_grad()
+            lc = torch.nn.functional.mse_loss(
+                OT.forward(Pc, mc, vc, ei, pc[ei[0]] - pc[ei[1]], grid, PONITA_TRAIN["layers"]), tc)
+            lc.backward()
+            torch.nn.utils.clip_grad_norm_(learn, 1.0)
+            optc.step()
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": steps / dt, "unit": "train steps/s", "cores": torch.get_num_threads(),
+                                  "kind": "port", "sample": f"{steps} training step(s) of the B={B} batch, torch fp64 "
+                                                            f"autograd restatement (oracle/ponita_torch.py; the "
+                                                            f"reference trains PONITA in float64), {dt:.2f} s"}
     return result
 
 
@@ -848,7 +944,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--model", default="segnn",
-                    choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "segnn_train", "eqv2", "gravity"])
+                    choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "segnn_train", "ponita_train", "eqv2",
+                             "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-torch-steps", type=int, default=20,
@@ -859,7 +956,7 @@ def main():
                     help="SEGNN BatchNorm statistics: per-rank batch (default), all-rank SyncBN, running")
     a = ap.parse_args()
     defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5),
-                "segnn_train": (50, 5), "eqv2": (20, 2),
+                "segnn_train": (50, 5), "ponita_train": (30, 3), "eqv2": (20, 2),
                 "gravity": (1000, 100)}
     a.steps = a.steps if a.steps is not None else defaults[a.model][0]
     a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
@@ -867,7 +964,7 @@ def main():
     from nbody_amd import parallel as P
     rank, world, device = P.init_from_env()
     fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "egnn_mc_train": bench_egnn_train,
-          "segnn_train": bench_segnn_train,
+          "segnn_train": bench_segnn_train, "ponita_train": bench_ponita_train,
           "eqv2": bench_eqv2, "gravity": bench_gravity}[a.model]
     result = fn(a, rank, world, device, P)
     if rank == 0:
