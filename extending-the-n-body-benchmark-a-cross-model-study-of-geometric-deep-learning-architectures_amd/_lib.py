@@ -16,7 +16,7 @@ ABI_VERSION = 11
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B = 1, 2
-ACT_NONE, ACT_GELU = 0, 1
+ACT_NONE, ACT_GELU, ACT_SILU, ACT_SLRELU = 0, 1, 2, 3
 MAX_LAYERS = 64
 
 c_i64, c_i32, c_f, c_d, c_p, c_sz = (ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double,
@@ -148,6 +148,15 @@ _SIGNATURES = {
     "nbx_po_fiber_conv_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_layernorm_forward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "nbx_layernorm_backward": (ctypes.c_int, [c_i64, c_i32] + [c_p] * 7),
+    "nbx_eqv2_train_edges": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, ctypes.c_uint64, c_i32, c_p, c_p, c_p, c_p,
+                                            c_p]),
+    "nbx_eqv2_rotate": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p]),
+    "nbx_eqv2_s2_act": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_eqv2_s2_act_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_segment_softmax": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_segment_softmax_backward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_eqv2_rms_norm": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "nbx_eqv2_rms_norm_backward": (ctypes.c_int, [c_i64, c_i32] + [c_p] * 7),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),

@@ -924,6 +924,30 @@ int eqv2_prepare(const nbx_eqv2_weights* w, int64_t B, int64_t N, void* ws_ptr, 
     return NBX_OK;
 }
 
+// ---- training step (eqv2_train.py): the reduced Wigner rows of every edge as a dense [7][9] block
+// (rows l = 0; l = 1, m = -1, 0, 1; l = 2, m = -1, 0, 1 — the |m| <= mmax = 1 coefficients in l-primary
+// order, so3.py:30-115; columns the 9 l-primary coefficients) and |pos_src - pos_dst|, from the same
+// edge records the inference path uses (eqv2_edge_kernel).
+__global__ void eqv2_dsel_kernel(int64_t E, const float* __restrict__ rot, float* __restrict__ dsel,
+                                 float* __restrict__ dist) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const float* r = rot + e * ROT;
+    float* d = dsel + e * 63;
+#pragma unroll
+    for (int i = 0; i < 63; ++i) d[i] = 0.f;
+    d[0] = 1.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) d[(1 + a) * 9 + 1 + b] = r[3 * a + b];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 5; ++b) d[(4 + a) * 9 + 4 + b] = r[9 + 5 * a + b];
+    dist[e] = r[24];
+}
+
 }  // namespace
 
 extern "C" int nbx_eqv2_workspace_bytes(const nbx_eqv2_weights* w, int64_t B, int64_t N, size_t* bytes) {
@@ -997,5 +1021,20 @@ extern "C" int nbx_eqv2_rollout(const nbx_eqv2_weights* w, float* pos, float* ve
                            f, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     }
     NBX_LAUNCH_CHECK("eqv2 rollout");
+    return NBX_OK;
+}
+
+extern "C" int nbx_eqv2_train_edges(int64_t B, int64_t N, const float* pos, const float* mass, const float* gauge,
+                                    uint64_t seed, int32_t num_elements, float* rot_scratch, float* dsel, float* dist,
+                                    int32_t* zn, void* stream) {
+    NBX_CHECK_ARG(B >= 1 && N >= 2 && num_elements >= 1, "nbx_eqv2_train_edges: bad sizes");
+    NBX_CHECK_ARG(pos && mass && rot_scratch && dsel && dist && zn, "nbx_eqv2_train_edges: null operand");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t V = B * N, E = V * (N - 1);
+    hipLaunchKernelGGL(eqv2_edge_kernel, dim3(g1(std::max(V, E))), dim3(256), 0, st, pos, mass, gauge, seed,
+                       (uint64_t)0, V, (int)N, num_elements, rot_scratch, zn);
+    NBX_LAUNCH_CHECK("eqv2 train edge");
+    hipLaunchKernelGGL(eqv2_dsel_kernel, dim3(g1(E)), dim3(256), 0, st, E, rot_scratch, dsel, dist);
+    NBX_LAUNCH_CHECK("eqv2 dsel");
     return NBX_OK;
 }

@@ -82,6 +82,23 @@ __device__ __forceinline__ float gelu_grad(float x) {
     return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
 
+// nn.SiLU (EquiformerV2 radial function / gates) and SmoothLeakyReLU(0.2) = 0.6 x + 0.4 x (2 sigmoid(x) - 1)
+// (equiformer_v2 activation.py; the attention logits)
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float act_f(int act, float x) {
+    if (act == NBX_ACT_GELU) return gelu_f(x);
+    if (act == NBX_ACT_SILU) return x * sigm(x);
+    if (act == NBX_ACT_SLRELU) return 0.2f * x + 0.8f * x * sigm(x);
+    return x;
+}
+__device__ __forceinline__ float act_grad(int act, float x) {
+    if (act == NBX_ACT_GELU) return gelu_grad(x);
+    const float s = sigm(x);
+    if (act == NBX_ACT_SILU) return s + x * s * (1.0f - s);
+    if (act == NBX_ACT_SLRELU) return 0.2f + 0.8f * (s + x * s * (1.0f - s));
+    return 1.0f;
+}
+
 // Y[r][c] = act(Z[r][c] + bias[c])
 __global__ void bias_act_kernel(int64_t rows, int cols, const float* __restrict__ Z, int64_t ldz,
                                 const float* __restrict__ bias, int act, float* __restrict__ Y, int64_t ldy) {
@@ -89,9 +106,7 @@ __global__ void bias_act_kernel(int64_t rows, int cols, const float* __restrict_
     if (i >= rows * cols) return;
     const int64_t r = i / cols;
     const int c = (int)(i - r * cols);
-    float z = Z[r * ldz + c] + (bias ? bias[c] : 0.f);
-    if (act == NBX_ACT_GELU) z = gelu_f(z);
-    Y[r * ldy + c] = z;
+    Y[r * ldy + c] = act_f(act, Z[r * ldz + c] + (bias ? bias[c] : 0.f));
 }
 
 // dZ[r][c] = dY[r][c] act'(Z[r][c] + bias[c])   (dY, dZ contiguous [rows][cols])
@@ -102,9 +117,7 @@ __global__ void bias_act_bwd_kernel(int64_t rows, int cols, const float* __restr
     if (i >= rows * cols) return;
     const int64_t r = i / cols;
     const int c = (int)(i - r * cols);
-    float g = dY[i];
-    if (act == NBX_ACT_GELU) g *= gelu_grad(Z[r * ldz + c] + (bias ? bias[c] : 0.f));
-    dZ[i] = g;
+    dZ[i] = act == NBX_ACT_NONE ? dY[i] : dY[i] * act_grad(act, Z[r * ldz + c] + (bias ? bias[c] : 0.f));
 }
 
 // ---------------------------------------------------------------- spatial message (separable conv)
@@ -315,7 +328,7 @@ extern "C" int nbx_ponita_train_featurize(int64_t V, int64_t E, int32_t O, const
 extern "C" int nbx_bias_act(int64_t rows, int32_t cols, const float* Z, int64_t ldz, const float* bias, int32_t act,
                             float* Y, int64_t ldy, void* stream) {
     NBX_CHECK_ARG(rows >= 0 && cols >= 0 && ldz >= cols && ldy >= cols, "nbx_bias_act: bad sizes");
-    NBX_CHECK_ARG(act == NBX_ACT_NONE || act == NBX_ACT_GELU, "nbx_bias_act: unknown activation %d", act);
+    NBX_CHECK_ARG(act >= NBX_ACT_NONE && act <= NBX_ACT_SLRELU, "nbx_bias_act: unknown activation %d", act);
     if (rows == 0 || cols == 0) return NBX_OK;
     hipLaunchKernelGGL(bias_act_kernel, dim3(nblk(rows * cols)), dim3(256), 0, (hipStream_t)stream, rows, cols, Z, ldz,
                        bias, act, Y, ldy);
@@ -326,7 +339,8 @@ extern "C" int nbx_bias_act(int64_t rows, int32_t cols, const float* Z, int64_t 
 extern "C" int nbx_bias_act_backward(int64_t rows, int32_t cols, const float* Z, int64_t ldz, const float* bias,
                                      int32_t act, const float* dY, float* dZ, void* stream) {
     NBX_CHECK_ARG(rows >= 0 && cols >= 0 && ldz >= cols, "nbx_bias_act_backward: bad sizes");
-    NBX_CHECK_ARG(act == NBX_ACT_NONE || act == NBX_ACT_GELU, "nbx_bias_act_backward: unknown activation %d", act);
+    NBX_CHECK_ARG(act >= NBX_ACT_NONE && act <= NBX_ACT_SLRELU, "nbx_bias_act_backward: unknown activation %d",
+                  act);
     if (rows == 0 || cols == 0) return NBX_OK;
     hipLaunchKernelGGL(bias_act_bwd_kernel, dim3(nblk(rows * cols)), dim3(256), 0, (hipStream_t)stream, rows, cols, Z,
                        ldz, bias, act, dY, dZ);

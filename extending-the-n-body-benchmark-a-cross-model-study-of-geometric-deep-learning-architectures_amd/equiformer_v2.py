@@ -490,10 +490,17 @@ class EquiformerV2_nbody(nn.Module):
             g = f(gauge)
             if g.shape != (V * (N - 1), 3):
                 raise ValueError("gauge must be [B*N*(N-1), 3]")
+        seed = (int(self.gauge_seed) * 0x100000001B3 + self._calls) & 0xFFFFFFFFFFFFFFFF
+        if torch.is_grad_enabled() and any(t.requires_grad for t in self.parameters()):
+            # training step: native operators under autograd (eqv2_train.py)
+            if self._native_reason:
+                raise NotImplementedError(self._native_reason)
+            from . import eqv2_train
+            self._calls += 1
+            return eqv2_train.train_forward(self, p, vv, q, B, N, g, seed).to(pos.dtype)
         out = torch.empty(V, 6, device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(W, B, N, device)
-        seed = (int(self.gauge_seed) * 0x100000001B3 + self._calls) & 0xFFFFFFFFFFFFFFFF
         self._calls += 1
         _lib.check(_lib.lib().nbx_eqv2_forward(W, _lib.dev_ptr(p), _lib.dev_ptr(vv), _lib.dev_ptr(q), B, N,
                                                _lib.dev_ptr(g) if g is not None else None, seed, _lib.dev_ptr(out),

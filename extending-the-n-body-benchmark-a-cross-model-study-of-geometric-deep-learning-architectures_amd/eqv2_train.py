@@ -1,0 +1,323 @@
+"""EquiformerV2 training step on the native operators.
+
+The reference trains EquiformerV2_nbody with ``pred = model(data); loss.backward();
+optimizer.step()`` (trainer.py:233-358).  Here a grad-mode ``EquiformerV2_nbody.forward``
+(equiformer_v2.py) runs :func:`train_forward`: the forward of
+models/equiformer_v2/architecture/equiformer_v2_nbody.py:428-575 (lmax 2, mmax 1, separable S2
+activations, rms_norm_sh) composed of libnbx operators inside ``torch.autograd.Function`` s whose
+backward passes call the same library, so ``loss.backward()`` reaches every ``nn.Parameter`` the
+reference's forward uses:
+
+* every nn.Linear / SO3_LinearV2 degree / SO(2) ``fc`` = ``ponita_train._LinFn`` (nbx_gemm_f32 +
+  nbx_bias_act), every LayerNorm = ``_LayerNormFn``, SiLU / SmoothLeakyReLU = ``_ActFn``;
+* SO3_Rotation.rotate / rotate_inv = ``_RotateFn`` (nbx_eqv2_rotate; adjoint pair);
+* the separable S2 activation's grid round trip = ``_S2Fn`` (nbx_eqv2_s2_act);
+* the attention softmax over edge_index[1] = ``_SoftmaxFn`` (nbx_segment_softmax);
+* EquivariantRMSNormArraySphericalHarmonicsV2 = ``_RMSNormFn`` (nbx_eqv2_rms_norm);
+* gathers x[edge_index[0 / 1]], embedding lookups and the aggregation = ``segnn_train._GatherFn`` /
+  ``_SegSumFn`` over CSR tables (no atomics).
+
+Edge frames come from ``nbx_eqv2_train_edges`` (the inference path's frames and gauge draws).
+Reshapes, concatenations, the SO(2) complex combine, the radial weighting of the messages and the
+dropout masks (alpha dropout, GraphDropPath: transformer_block.py:342-343,686-706, drop.py:51-68,
+train mode, torch's RNG) are torch glue.  Arithmetic is fp32 (a float64 module is cast for the step).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .ponita_train import _LayerNormFn, linear
+from .segnn_train import Graph, _GatherFn, _SegSumFn, _dp, _st, colsum
+
+_f32 = torch.float32
+AVG_DEGREE = 23.395238876342773          # equiformer_v2_nbody.py:36
+# reduced (|m| <= 1) coefficients, l-primary: (0,0) (1,-1) (1,0) (1,1) (2,-1) (2,0) (2,1); m-primary
+# order of SO2_Convolution (so3.py:30-115 CoefficientMappingModule): m = 0 (l = 0, 1, 2), m = +1
+# (l = 1, 2), m = -1 (l = 1, 2)
+M_PRIMARY = [0, 2, 5, 3, 6, 1, 4]
+L_PRIMARY = [M_PRIMARY.index(i) for i in range(7)]
+
+
+class _ActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, act):
+        X = X.contiguous()
+        rows, cols = X.shape[0], X.numel() // max(X.shape[0], 1)
+        Y = torch.empty_like(X)
+        _lib.check(_lib.lib().nbx_bias_act(rows, cols, _dp(X), cols, None, act, _dp(Y), cols, _st(X)), "nbx_bias_act")
+        ctx.save_for_backward(X)
+        ctx.act = act
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        (X,) = ctx.saved_tensors
+        rows, cols = X.shape[0], X.numel() // max(X.shape[0], 1)
+        dY = dY.contiguous()
+        dX = torch.empty_like(X)
+        _lib.check(_lib.lib().nbx_bias_act_backward(rows, cols, _dp(X), cols, None, ctx.act, _dp(dY), _dp(dX),
+                                                    _st(dX)), "nbx_bias_act_backward")
+        return dX, None
+
+
+def act(X, kind):
+    return _ActFn.apply(X, kind)
+
+
+class _RotateFn(torch.autograd.Function):
+    """rotate (inverse = 0): [E][9][C] -> [E][7][C]; rotate_inv (inverse = 1): [E][7][C] -> [E][9][C]."""
+
+    @staticmethod
+    def forward(ctx, X, D, inverse, rescale):
+        E, _, C = X.shape
+        X = X.contiguous()
+        out = torch.empty(E, 9 if inverse else 7, C, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rotate(E, C, _dp(D), _dp(X), X.shape[1] * C, _dp(out), inverse, rescale,
+                                              _st(X)), "nbx_eqv2_rotate")
+        ctx.save_for_backward(D)
+        ctx.mode = (inverse, rescale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dY):
+        (D,) = ctx.saved_tensors
+        inverse, rescale = ctx.mode
+        dY = dY.contiguous()
+        E, _, C = dY.shape
+        dX = torch.empty(E, 7 if inverse else 9, C, device=dY.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rotate(E, C, _dp(D), _dp(dY), dY.shape[1] * C, _dp(dX), 1 - inverse, rescale,
+                                              _st(dY)), "nbx_eqv2_rotate")
+        return dX, None, None, None
+
+
+class _S2Fn(torch.autograd.Function):
+    """Separable S2 activation's grid part of X [rows][I][H] with T / F [P][I]."""
+
+    @staticmethod
+    def forward(ctx, X, T, F):
+        X = X.contiguous()
+        rows, I, H = X.shape
+        out = torch.empty_like(X)
+        _lib.check(_lib.lib().nbx_eqv2_s2_act(rows, I, T.shape[0], H, _dp(T), _dp(F), _dp(X), _dp(out), _st(X)),
+                   "nbx_eqv2_s2_act")
+        ctx.save_for_backward(X, T, F)
+        return out
+
+    @staticmethod
+    def backward(ctx, dY):
+        X, T, F = ctx.saved_tensors
+        rows, I, H = X.shape
+        dY = dY.contiguous()
+        dX = torch.empty_like(X)
+        _lib.check(_lib.lib().nbx_eqv2_s2_act_backward(rows, I, T.shape[0], H, _dp(T), _dp(F), _dp(X), _dp(dY),
+                                                       _dp(dX), _st(dX)), "nbx_eqv2_s2_act_backward")
+        return dX, None, None
+
+
+class _SoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, g):
+        logits = logits.contiguous()
+        nh = logits.shape[1]
+        alpha = torch.empty_like(logits)
+        _lib.check(_lib.lib().nbx_segment_softmax(g.V, nh, _dp(g.dptr), _dp(g.deid), _dp(logits), _dp(alpha),
+                                                  _st(logits)), "nbx_segment_softmax")
+        ctx.save_for_backward(alpha)
+        ctx.g = g
+        return alpha
+
+    @staticmethod
+    def backward(ctx, dA):
+        (alpha,) = ctx.saved_tensors
+        g = ctx.g
+        dA = dA.contiguous()
+        dL = torch.empty_like(alpha)
+        _lib.check(_lib.lib().nbx_segment_softmax_backward(g.V, alpha.shape[1], _dp(g.dptr), _dp(g.deid), _dp(alpha),
+                                                           _dp(dA), _dp(dL), _st(dA)), "nbx_segment_softmax_backward")
+        return dL, None
+
+
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, w, b, eps):
+        X = X.contiguous()
+        V, _, C = X.shape
+        Y = torch.empty_like(X)
+        save = torch.empty(2, V, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rms_norm(V, C, _dp(X), _dp(w), _dp(b), float(eps), _dp(Y), _dp(save), _st(X)),
+                   "nbx_eqv2_rms_norm")
+        ctx.save_for_backward(X, w, save)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        X, w, save = ctx.saved_tensors
+        V, _, C = X.shape
+        dY = dY.contiguous()
+        dX = torch.empty_like(X)
+        G = torch.empty(V, 4 * C, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rms_norm_backward(V, C, _dp(X), _dp(w), _dp(save), _dp(dY), _dp(dX), _dp(G),
+                                                         _st(dX)), "nbx_eqv2_rms_norm_backward")
+        dwb = colsum(G, V, 4 * C, 4 * C, torch.empty(4 * C, device=X.device, dtype=_f32))
+        return dX, dwb[:3 * C].view(3, C), dwb[3 * C:], None
+
+
+def _f(t):
+    return t.to(_f32).contiguous()
+
+
+def gather(X, idx_graph, which):
+    """Rows X[idx] (X [rows][...]) through a CSR of the index (``which``: "s" = the graph's sources,
+    "d" = its destinations)."""
+    g = idx_graph
+    idx = g.src if which == "s" else g.dst
+    ptr, eid = (g.sptr, g.seid) if which == "s" else (g.dptr, g.deid)
+    shape = X.shape
+    out = _GatherFn.apply(X.reshape(shape[0], -1).contiguous(), idx, ptr, eid)
+    return out.view(idx.shape[0], *shape[1:])
+
+
+class _Step:
+    """Per-forward state: the graph, edge frames, distance expansion and dropout settings."""
+
+    def __init__(self, model, pos, vel, charges, B, N, gauge, seed):
+        dev = pos.device
+        self.m, self.B, self.N = model, B, N
+        V, E = B * N, B * N * (N - 1)
+        self.V, self.E = V, E
+        rot = torch.empty(max(E, 1), 32, device=dev, dtype=_f32)
+        self.D = torch.empty(max(E, 1), 7, 9, device=dev, dtype=_f32)
+        dist = torch.empty(max(E, 1), device=dev, dtype=_f32)
+        zn = torch.empty(V, device=dev, dtype=torch.int32)
+        _lib.check(_lib.lib().nbx_eqv2_train_edges(B, N, _dp(pos), _dp(charges), _dp(gauge), seed,
+                                                   model.max_num_elements, _dp(rot), _dp(self.D), _dp(dist), _dp(zn),
+                                                   _st(pos)), "nbx_eqv2_train_edges")
+        from .graph import fc_edge_index
+        self.g = Graph(fc_edge_index(B, N, dev), V, dev)
+        zl = zn.long()
+        ze = torch.stack([zl[self.g.src.long()], zl[self.g.dst.long()]])
+        self.gz = Graph(ze, model.max_num_elements, dev)          # CSRs of the edges' source / target elements
+        self.gn = Graph(torch.stack([zl, zl]), model.max_num_elements, dev)   # of the nodes' elements
+        self.dexp = linear(dist[:E, None], model.distance_expansion.weight, model.distance_expansion.bias)
+        self.training = model.training
+        self.batch = torch.arange(B, device=dev).repeat_interleave(N)
+        ga, gf = model.SO3_grid[2][1], model.SO3_grid[2][2]
+        self.grid_attn = (_f(ga.to_grid_mat.reshape(-1, 7)), _f(ga.from_grid_mat.reshape(-1, 7)))
+        self.grid_ffn = (_f(gf.to_grid_mat.reshape(-1, 9)), _f(gf.from_grid_mat.reshape(-1, 9)))
+
+    # ---------------------------------------------------------------- building blocks
+    def x_edge(self, mod):
+        s = gather(_f(mod.source_embedding.weight), self.gz, "s")
+        t = gather(_f(mod.target_embedding.weight), self.gz, "d")
+        return torch.cat([self.dexp, s, t], 1)
+
+    @staticmethod
+    def rad_func(rad, x):
+        """RadialFunction: Linear, LayerNorm, SiLU, Linear, LayerNorm, SiLU, Linear."""
+        net = rad.net
+        h = linear(x, net[0].weight, net[0].bias)
+        h = act(_LayerNormFn.apply(h, _f(net[1].weight), _f(net[1].bias), net[1].eps), _lib.ACT_SILU)
+        h = linear(h, net[3].weight, net[3].bias)
+        h = act(_LayerNormFn.apply(h, _f(net[4].weight), _f(net[4].bias), net[4].eps), _lib.ACT_SILU)
+        return linear(h, net[6].weight, net[6].bias)
+
+    def so2_conv(self, conv, x, x_edge, cout, n_extra=0):
+        """SO2_Convolution (so2_ops.py:78-156) of x [E][7][cin] (l-primary) -> ([E][7][cout], extra)."""
+        E, _, cin = x.shape
+        xm = x[:, M_PRIMARY]
+        rad = self.rad_func(conv.rad_func, x_edge) if x_edge is not None else None
+        x0 = xm[:, :3].reshape(E, 3 * cin)
+        if rad is not None:
+            x0 = x0 * rad[:, :3 * cin]
+        y0 = linear(x0, conv.fc_m0.weight, conv.fc_m0.bias)
+        extra, y0 = y0[:, :n_extra], y0[:, n_extra:].reshape(E, 3, cout)
+        x1 = xm[:, 3:7].reshape(E, 2, 2 * cin)
+        if rad is not None:
+            x1 = x1 * rad[:, None, 3 * cin:5 * cin]
+        y = linear(x1.reshape(2 * E, 2 * cin), conv.so2_m_conv[0].fc.weight).view(E, 2, 4 * cout)
+        xr, xi = y[..., :2 * cout], y[..., 2 * cout:]
+        y1 = torch.stack([xr[:, 0] - xi[:, 1], xr[:, 1] + xi[:, 0]], 1).reshape(E, 4, cout)
+        return torch.cat([y0, y1], 1)[:, L_PRIMARY], extra
+
+    @staticmethod
+    def so3_linear(lin, x):
+        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][9][cin]."""
+        V, _, cin = x.shape
+        W = lin.weight
+        y0 = linear(x[:, 0], W[0], lin.bias).view(V, 1, -1)
+        y1 = linear(x[:, 1:4].reshape(3 * V, cin), W[1]).view(V, 3, -1)
+        y2 = linear(x[:, 4:9].reshape(5 * V, cin), W[2]).view(V, 5, -1)
+        return torch.cat([y0, y1, y2], 1)
+
+    @staticmethod
+    def rms_norm(norm, x):
+        return _RMSNormFn.apply(x, _f(norm.affine_weight), _f(norm.affine_bias), norm.eps)
+
+    def drop_path(self, x):
+        """GraphDropPath (drop.py:51-68): one Bernoulli keep / (1 - p) per system, train mode."""
+        p = self.m.drop_path_rate
+        if not self.training or p == 0.0:
+            return x
+        keep = torch.empty(self.B, 1, 1, device=x.device, dtype=x.dtype).bernoulli_(1.0 - p) / (1.0 - p)
+        return x * keep[self.batch]
+
+    # ---------------------------------------------------------------- layers
+    def attention(self, A, x, cout):
+        """SO2EquivariantGraphAttention (transformer_block.py:226-370) of x [V][9][C] -> [V][9][cout]."""
+        m, g, E, V = self.m, self.g, self.E, self.V
+        nh, na, nv, H = m.num_heads, m.attn_alpha_channels, m.attn_value_channels, m.attn_hidden_channels
+        x_edge = self.x_edge(A)
+        xs, xd = gather(x, g, "s"), gather(x, g, "d")
+        msg = _RotateFn.apply(torch.cat([xs, xd], 2), self.D, 0, 0)
+        msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
+        gating, a_in = extra[:, nh * na:], extra[:, :nh * na]
+        msg = torch.cat([act(gating.contiguous(), _lib.ACT_SILU)[:, None],
+                         _S2Fn.apply(msg, *self.grid_attn)[:, 1:]], 1)
+        msg, _ = self.so2_conv(A.so2_conv_2, msg, None, nh * nv)
+        a = _LayerNormFn.apply(a_in.reshape(E * nh, na).contiguous(), _f(A.alpha_norm.weight), _f(A.alpha_norm.bias),
+                               A.alpha_norm.eps)
+        a = act(a, _lib.ACT_SLRELU).view(E, nh, na)
+        logit = (a * _f(A.alpha_dot)).sum(-1)
+        alpha = _SoftmaxFn.apply(logit, g)
+        if self.training and m.alpha_drop > 0.0:
+            alpha = torch.nn.functional.dropout(alpha, m.alpha_drop, True)
+        msg = (msg.view(E, 7, nh, nv) * alpha[:, None, :, None]).reshape(E, 7, nh * nv)
+        rot = _RotateFn.apply(msg, self.D, 1, 1)
+        agg = _SegSumFn.apply(rot.reshape(E, 9 * nh * nv), g.dst, g.dptr, g.deid, V).view(V, 9, nh * nv)
+        return self.so3_linear(A.proj, agg)
+
+    def ffn(self, F, x):
+        """FeedForwardNetwork (transformer_block.py:473-530), separable S2 activation on SO3_Grid(2, 2)."""
+        gating = linear(x[:, 0], F.gating_linear.weight, F.gating_linear.bias, _lib.ACT_SILU)
+        h = self.so3_linear(F.so3_linear_1, x)
+        h = torch.cat([gating[:, None], _S2Fn.apply(h, *self.grid_ffn)[:, 1:]], 1)
+        return self.so3_linear(F.so3_linear_2, h)
+
+    def edge_degree(self):
+        """EdgeDegreeEmbedding (input_block.py:83-138): m = 0 radial coefficients rotated back and
+        summed over the incoming edges / AVG_DEGREE."""
+        ed, E, V, C = self.m.edge_degree_embedding, self.E, self.V, self.m.sphere_channels
+        r = self.rad_func(ed.rad_func, self.x_edge(ed)).view(E, 3, C)
+        z = r.new_zeros(E, 1, C)
+        red = torch.cat([r[:, 0:1], z, r[:, 1:2], z, z, r[:, 2:3], z], 1)         # m = 0 slots 0, 2, 5
+        y = _RotateFn.apply(red, self.D, 1, 1)
+        out = _SegSumFn.apply(y.reshape(E, 9 * C), self.g.dst, self.g.dptr, self.g.deid, V).view(V, 9, C)
+        return out / AVG_DEGREE
+
+
+def train_forward(model, pos, vel, charges, B, N, gauge=None, seed=0):
+    """equiformer_v2_nbody.py:428-575 with autograd through the native operators.  pos / vel [V, 3],
+    charges [V] fp32 on the device; gauge [E, 3] or None (device hash of ``seed``).  Returns [V, 6]."""
+    m = model
+    st = _Step(m, pos, vel, charges, B, N, gauge, seed)
+    V, C = st.V, m.sphere_channels
+    x0 = gather(_f(m.sphere_embedding.weight), st.gn, "s")                               # [V][C]
+    xv = linear(vel, m.velocity_embedding.weight, m.velocity_embedding.bias).view(V, 3, C)
+    x = torch.cat([x0[:, None], xv, x0.new_zeros(V, 5, C)], 1) + st.edge_degree()
+    for blk in m.blocks:
+        y = st.drop_path(st.attention(blk.ga, st.rms_norm(blk.norm_1, x), C)) + x
+        x = st.drop_path(st.ffn(blk.ffn, st.rms_norm(blk.norm_2, y))) + y
+    x = st.rms_norm(m.norm, x)
+    pred = st.attention(m.force_block, x, 2)
+    return torch.cat([pred[:, 1:4, 0], pred[:, 1:4, 1]], 1)

@@ -348,6 +348,8 @@ int nbx_segnn_train_featurize(int64_t V, int64_t E, const float* pos, const floa
  */
 #define NBX_ACT_NONE 0
 #define NBX_ACT_GELU 1   /* nn.GELU(): 0.5 x (1 + erf(x / sqrt 2)) */
+#define NBX_ACT_SILU 2   /* nn.SiLU(): x sigmoid(x) */
+#define NBX_ACT_SLRELU 3 /* SmoothLeakyReLU(0.2): 0.6 x + 0.4 x (2 sigmoid(x) - 1) */
 
 /* Invariants + degree-3 polynomial features (no gradient): attr [E*O][16] (16-byte aligned) =
  * poly(r.o, |r - (r.o) o|) (14 features, 2 zero pads), r = pos[src] - pos[dst]; fiber [O*O][4] =
@@ -386,6 +388,50 @@ int nbx_layernorm_forward(int64_t rows, int32_t C, const float* X, const float* 
                           float* Y, float* save, void* stream);
 int nbx_layernorm_backward(int64_t rows, int32_t C, const float* X, const float* weight, const float* save,
                            const float* dY, float* dX, float* G, void* stream);
+
+/* ------------------------------------------------------------------------
+ * EquiformerV2 training step (ABI 11; SURVEY §8(f)4: trainer.py:233-358 on EquiformerV2_nbody,
+ * equiformer_v2_nbody.py:392-575, lmax 2 / mmax 1).  The training forward and backward
+ * (eqv2_train.py, autograd) are composed of nbx_gemm_f32, nbx_bias_act (SiLU, SmoothLeakyReLU),
+ * nbx_layernorm_*, nbx_colsum, nbx_gather_rows / nbx_segment_sum and the operators below.  Layout:
+ * node irreps [V][9][C] (l-primary coefficients, channels contiguous), edge irreps [E][7][C] (the
+ * |m| <= 1 coefficients, l-primary), fully-connected edges in build_graph_with_knn order.
+ */
+
+/* Edge frames (edge_rot_mat.py:6-63 with the gauge draws of nbx_eqv2_forward: `gauge` [E][3] or the
+ * device hash of `seed`): dsel [E][7][9] = the |m| <= 1 rows of the block Wigner matrix
+ * (so3.py:485-531), dist [E] = |pos_src - pos_dst|, zn [V] = clamp(int(mass)); rot_scratch [E][32]. */
+int nbx_eqv2_train_edges(int64_t B, int64_t N, const float* pos, const float* mass, const float* gauge, uint64_t seed,
+                         int32_t num_elements, float* rot_scratch, float* dsel, float* dist, int32_t* zn, void* stream);
+
+/* SO3_Rotation.rotate (inverse = 0: out [E][7][C] = dsel in, in [E][9][C] with `ld_in` floats per edge)
+ * and rotate_inv (inverse = 1: out [E][9][C] = dsel^T in, in [E][7][C]); rescale = 1 multiplies the
+ * l = 2 block by sqrt(5/3) (get_rotate_inv_rescale, so3.py:160-185).  Each is the other's adjoint. */
+int nbx_eqv2_rotate(int64_t E, int32_t C, const float* dsel, const float* in, int64_t ld_in, float* out,
+                    int32_t inverse, int32_t rescale, void* stream);
+
+/* Separable S2 activation, grid part (activation.py:155-202): out[r][i][h] = sum_p F[p][i]
+ * SiLU(sum_j T[p][j] X[r][j][h]), X / out [rows][I][H], T / F [P][I] (SO3_Grid to / from grid
+ * matrices), I <= 9, P <= 64; backward dX from dOut. */
+int nbx_eqv2_s2_act(int64_t rows, int32_t I, int32_t P, int32_t H, const float* to_grid, const float* from_grid,
+                    const float* X, float* out, void* stream);
+int nbx_eqv2_s2_act_backward(int64_t rows, int32_t I, int32_t P, int32_t H, const float* to_grid,
+                             const float* from_grid, const float* X, const float* dOut, float* dX, void* stream);
+
+/* torch_geometric softmax of logits [E][nh] over edge_index[1] (dst CSR), + 1e-16 in the denominator
+ * (transformer_block.py:331-339), and its backward. */
+int nbx_segment_softmax(int64_t V, int32_t nh, const int32_t* dst_ptr, const int32_t* dst_eid, const float* logits,
+                        float* alpha, void* stream);
+int nbx_segment_softmax_backward(int64_t V, int32_t nh, const int32_t* dst_ptr, const int32_t* dst_eid,
+                                 const float* alpha, const float* dalpha, float* dlogits, void* stream);
+
+/* EquivariantRMSNormArraySphericalHarmonicsV2 (layer_norm.py:327-441, lmax 2, C <= 128) of X [V][9][C]:
+ * weight [3][C], bias [C]; save [2][V]; backward dX and G [V][4C] whose column sums are
+ * dweight [3][C] | dbias [C]. */
+int nbx_eqv2_rms_norm(int64_t V, int32_t C, const float* X, const float* weight, const float* bias, float eps, float* Y,
+                      float* save, void* stream);
+int nbx_eqv2_rms_norm_backward(int64_t V, int32_t C, const float* X, const float* weight, const float* save,
+                               const float* dY, float* dX, float* G, void* stream);
 
 /* ------------------------------------------------------------------------
  * EGNN-MC (models/egnn_mc/egnn_mc.py:45-295 with the preprocessing of
