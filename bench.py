@@ -21,8 +21,8 @@ Secondary configurations (not the headline; same JSON shape):
   --model eqv2     C4: EquiformerV2 (config.yaml widths), N=20, batch 256 per rank ("weak").
   --model egnn_mc_train  SURVEY 8(f)4: EGNN-MC training step (C1 widths, forward + backward + Adam,
                    gradients all-reduced over ranks), batch 64 per rank ("weak").
-  --model segnn_train / ponita_train  SURVEY 8(f)4: SEGNN (C2 widths) / PONITA (config.yaml: 128 x 8)
-                   training step, batch 64 per rank ("weak").
+  --model segnn_train / ponita_train / eqv2_train  SURVEY 8(f)4: SEGNN (C2 widths) / PONITA
+                   (config.yaml: 128 x 8) / EquiformerV2 (C4 widths, N=5) training step, batch 64 per rank.
   --model gravity  C5: ground-truth integrator, 10 000 systems x N=100, --steps
                    KDK steps (sample_freq 10), systems sharded over the ranks ("strong").
 
@@ -861,6 +861,74 @@ def bench_eqv2(a, rank, world, device, P):
     return result
 
 
+def bench_eqv2_train(a, rank, world, device, P):
+    """one EquiformerV2 training step of the reference trainer (trainer.py:233-358) at
+    the reference's EquiformerV2 training configuration (config.yaml: the C4 widths, batch_size 64
+    systems of N=5 per rank; the constructor's alpha_drop 0.1 / drop_path_rate 0.05 in train mode;
+    "weak"): zero_grad, forward on the native training operators (eqv2_train.py /
+    csrc/eqv2_train.hip + nbx_gemm_f32), MSE loss, loss.backward(), gradient all-reduce over ranks, clip,
+    AdamW + LambdaLR."""
+    from nbody_amd.equiformer_v2 import EquiformerV2_nbody
+    B, N = a.batch or 64, NBODY
+    torch.manual_seed(0)
+    model = EquiformerV2_nbody(**EQV2_C4).to(device).train()
+    loc, vel, mass = initial_states(B, N, rank * B)
+    rng = np.random.default_rng(300 + rank)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    pos, vv, q = t(loc.reshape(-1, 3)), t(vel.reshape(-1, 3)), t(mass.reshape(-1, 1))
+    batch = torch.arange(B, device=device).repeat_interleave(N)
+    gauge = t(rng.uniform(0, 1, (B * N * (N - 1), 3)))      # fixed gauges: no host-side counter in the graph
+    data = (pos, vv, torch.zeros_like(pos), q, pos)
+    target = t(rng.standard_normal((B * N, 6)) * 0.1)
+    import nbody_amd.eqv2_train as ET
+    fwd = lambda: ET.train_forward(model, pos, vv, q.reshape(-1), B, N, gauge, 0)
+    model(data, batch, gauge=gauge)          # the module's own entry point once (grad mode -> eqv2_train)
+    loss, elapsed, gemm, graph = train_loop(a, world, device, P, model, fwd, target, model.get_model_size())
+    gemm_ms, gemm_flops, n_gemm = gemm
+    value = a.steps / elapsed * world
+    ach = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
+    result = {
+        "metric": "EquiformerV2 training steps/sec (reference training config, forward + backward + AdamW)",
+        "value": round(value, 3), "unit": "train steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states, random targets and gauges, seeded random-init weights)",
+        "config": {"workload": "SURVEY 8(f)4: EquiformerV2 C4 widths (4 layers, sphere 64, lmax 2 / mmax 1) training "
+                               "step, N=5, batch 64 per GPU (config.yaml), alpha dropout 0.1 + drop path 0.05, MSE "
+                               "loss, grad-norm clip 1, AdamW + LambdaLR (trainer.py:170-194)",
+                   "model": "EquiformerV2", "global_batch": B * world, "seq_len": a.steps,
+                   "parallelism": f"dp{world}",
+                   "execution": "one HIP graph replay per step (forward, backward, clip, fused AdamW)" if graph
+                                else "eager"},
+        "roofline": {"bound": "mfma", "kernel": "gemm_f32_kernel (nbx_gemm_f32: every linear layer of the forward "
+                                               "and backward)",
+                     "achieved": round(ach, 3) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None, "traffic": None,
+                     "avg_launch_us": round(1e3 * gemm_ms / max(n_gemm, 1), 3), "launches_per_step": n_gemm,
+                     "gflop_per_step": round(gemm_flops / 1e9, 4),
+                     "timing": "torch.cuda.Event pairs around every GEMM launch of one eager step, launch stream"},
+        "loss": float(loss.item()), "finite": bool(math.isfinite(float(loss.item())))}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import equiformer_v2 as EQ
+        Pc = {k: v.detach().double().cpu().clone().requires_grad_() for k, v in model.named_parameters()}
+        optc = torch.optim.AdamW(list(Pc.values()), lr=1e-4, weight_decay=1e-8, betas=(0.9, 0.98), eps=1e-9)
+        gc, tc = gauge.double().cpu(), target.double().cpu()
+        steps = max(1, a.cpu_steps)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            optc.zero_grad()
+            lc = torch.nn.functional.mse_loss(EQ.forward(EQV2_C4, Pc, loc, vel, mass, B, N, gc), tc)
+            lc.backward()
+            torch.nn.utils.clip_grad_norm_(list(Pc.values()), 1.0)
+            optc.step()
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": steps / dt, "unit": "train steps/s", "cores": torch.get_num_threads(),
+                                  "kind": "port", "sample": f"{steps} training step(s) of the B={B} batch, torch fp64 "
+                                                            f"autograd of oracle/equiformer_v2.py (no dropout), "
+                                                            f"{dt:.2f} s"}
+    return result
+
+
 def cpu_baseline_eqv2(model, B_glob, B_s=128):
     from oracle import equiformer_v2 as EQ
     p = {k: v.detach().double().cpu() for k, v in model.named_parameters()}
@@ -945,7 +1013,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--model", default="segnn",
                     choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "segnn_train", "ponita_train", "eqv2",
-                             "gravity"])
+                             "eqv2_train", "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-torch-steps", type=int, default=20,
@@ -957,6 +1025,7 @@ def main():
     a = ap.parse_args()
     defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5),
                 "segnn_train": (50, 5), "ponita_train": (30, 3), "eqv2": (20, 2),
+                "eqv2_train": (30, 3),
                 "gravity": (1000, 100)}
     a.steps = a.steps if a.steps is not None else defaults[a.model][0]
     a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
@@ -964,7 +1033,7 @@ def main():
     from nbody_amd import parallel as P
     rank, world, device = P.init_from_env()
     fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "egnn_mc_train": bench_egnn_train,
-          "segnn_train": bench_segnn_train, "ponita_train": bench_ponita_train,
+          "segnn_train": bench_segnn_train, "ponita_train": bench_ponita_train, "eqv2_train": bench_eqv2_train,
           "eqv2": bench_eqv2, "gravity": bench_gravity}[a.model]
     result = fn(a, rank, world, device, P)
     if rank == 0:
