@@ -1,19 +1,21 @@
 #!/bin/bash
 # rocprofv3 kernel summaries + HBM PMC passes for the bench lines (one rocprofv3 run per pass,
 # each under its own time limit; stops at the first failure).  Usage:
-#   bash scripts/profile_models.sh [models...]     (default: segnn ponita egnn_mc egnn_mc_train segnn_train eqv2 gravity)
+#   bash scripts/profile_models.sh [models...]     (default: segnn ponita egnn_mc egnn_mc_train segnn_train ponita_train eqv2_train eqv2 gravity)
 # Output: gpurun_out/prof/<model>/{stats,fetch,write}/ and gpurun_out/prof/<model>_summary.md,
 #         gpurun_out/prof/pmc_<model>.json (per-kernel HBM bytes per launch)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 export TMPDIR=/tmp
-MODELS="${*:-segnn ponita egnn_mc egnn_mc_train segnn_train eqv2 gravity}"
+MODELS="${*:-segnn ponita egnn_mc egnn_mc_train segnn_train ponita_train eqv2_train eqv2 gravity}"
 declare -A ARGS=(
   [segnn]="--model segnn --steps 20 --warmup 2 --no-cpu-baseline"
   [ponita]="--model ponita --steps 4 --warmup 1 --no-cpu-baseline"
   [egnn_mc]="--model egnn_mc --steps 50 --warmup 5 --no-cpu-baseline"
   [egnn_mc_train]="--model egnn_mc_train --steps 20 --warmup 3 --no-cpu-baseline"
   [segnn_train]="--model segnn_train --steps 10 --warmup 2 --no-cpu-baseline"
+  [ponita_train]="--model ponita_train --steps 10 --warmup 2 --no-cpu-baseline"
+  [eqv2_train]="--model eqv2_train --steps 10 --warmup 2 --no-cpu-baseline"
   [eqv2]="--model eqv2 --steps 5 --warmup 1 --no-cpu-baseline"
   [gravity]="--model gravity --steps 200 --warmup 10 --no-cpu-baseline"
 )
