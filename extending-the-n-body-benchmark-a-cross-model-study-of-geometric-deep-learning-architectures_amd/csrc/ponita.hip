@@ -853,7 +853,10 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             const int PR = std::max(1, std::min(O, (int)(fk_lds / ((size_t)O * C * 4))));
             const int R = (O + PR - 1) / PR;
             const int npi = PO_FIB_THREADS / (C / 4);
-            const int gx = (int)std::min<int64_t>((d.V + npi - 1) / npi, std::max(1, 1024 / R));
+            // NBX_PO_FIB_BLOCKS: total workgroups over all ranges (A/B; the ranges of one node group sit on
+            // the same XCD since gx % 8 == 0, so co-resident ranges share X1 through that XCD's L2)
+            static const int fib_blocks = getenv("NBX_PO_FIB_BLOCKS") ? atoi(getenv("NBX_PO_FIB_BLOCKS")) : 1024;
+            const int gx = (int)std::min<int64_t>((d.V + npi - 1) / npi, std::max(1, fib_blocks / R));
             const size_t lds = (size_t)O * PR * C * 4;
             auto kern = O <= 20 ? po_fiber_ln_kernel<20, 4> : po_fiber_ln_kernel<PO_OMAX, 2>;
             if (lds > 64 * 1024) {
