@@ -155,7 +155,7 @@ def bench_segnn(a, rank, world, device, P):
     if a.bn_mode == "running":
         model.bn_mode = "running"
     elif a.bn_mode == "sync" and world > 1:
-        model.enable_sync_batchnorm()
+        model.enable_sync_batchnorm(global_batch=B * world)
     loc, vel, mass = initial_states(B, N, rank * B)
     loc_d = torch.tensor(loc, dtype=torch.float32, device=device)
     vel_d = torch.tensor(vel, dtype=torch.float32, device=device)

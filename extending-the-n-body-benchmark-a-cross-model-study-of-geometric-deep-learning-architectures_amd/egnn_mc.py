@@ -17,6 +17,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from .train_dispatch import use_training_path
 
 __all__ = ["EGNNMultiChannel"]
 
@@ -312,7 +313,7 @@ class EGNNMultiChannel(nn.Module):
         mass = getattr(graph, "mass", None)
         m = f(mass.reshape(-1)) if mass is not None else torch.ones(V, device=device)
         p, v = f(pos), f(graph.vel)
-        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()):
+        if use_training_path(self):   # train_dispatch.py: autograd on + trainable params
             # training step (trainer.py:233-358): the native forward keeps its activations and
             # loss.backward() runs the native backward (csrc/egnn_train.hip).  Inputs it does not
             # cover raise here, instead of returning an inference result without an autograd graph

@@ -24,6 +24,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from .train_dispatch import use_training_path
 from . import so3
 
 __all__ = ["EquiformerV2_nbody"]
@@ -491,7 +492,7 @@ class EquiformerV2_nbody(nn.Module):
             if g.shape != (V * (N - 1), 3):
                 raise ValueError("gauge must be [B*N*(N-1), 3]")
         seed = (int(self.gauge_seed) * 0x100000001B3 + self._calls) & 0xFFFFFFFFFFFFFFFF
-        if torch.is_grad_enabled() and any(t.requires_grad for t in self.parameters()):
+        if use_training_path(self):   # train_dispatch.py: autograd on + trainable params
             # training step: native operators under autograd (eqv2_train.py)
             if self._native_reason:
                 raise NotImplementedError(self._native_reason)

@@ -262,6 +262,16 @@ class _Step:
         keep = torch.empty(self.B, 1, 1, device=x.device, dtype=x.dtype).bernoulli_(1.0 - p) / (1.0 - p)
         return x * keep[self.batch]
 
+    def proj_drop(self, x):
+        """EquivariantDropoutArraySphericalHarmonics(drop_graph=False) (drop.py:121-146), applied to the
+        attention and FFN outputs (transformer_block.py:690-706): one keep / (1 - p) per (node, channel),
+        shared by all coefficients, train mode."""
+        p = self.m.proj_drop
+        if not self.training or p == 0.0:
+            return x
+        mask = torch.nn.functional.dropout(x.new_ones(x.shape[0], 1, x.shape[2]), p, True)
+        return x * mask
+
     # ---------------------------------------------------------------- layers
     def attention(self, A, x, cout):
         """SO2EquivariantGraphAttention (transformer_block.py:226-370) of x [V][9][C] -> [V][9][cout]."""
@@ -280,8 +290,8 @@ class _Step:
         a = act(a, _lib.ACT_SLRELU).view(E, nh, na)
         logit = (a * _f(A.alpha_dot)).sum(-1)
         alpha = _SoftmaxFn.apply(logit, g)
-        if self.training and m.alpha_drop > 0.0:
-            alpha = torch.nn.functional.dropout(alpha, m.alpha_drop, True)
+        if self.training and A.alpha_drop > 0.0:   # the module's own rate: the force block's is 0
+            alpha = torch.nn.functional.dropout(alpha, A.alpha_drop, True)    # (equiformer_v2_nbody.py:362)
         msg = (msg.view(E, 7, nh, nv) * alpha[:, None, :, None]).reshape(E, 7, nh * nv)
         rot = _RotateFn.apply(msg, self.D, 1, 1)
         agg = _SegSumFn.apply(rot.reshape(E, 9 * nh * nv), g.dst, g.dptr, g.deid, V).view(V, 9, nh * nv)
@@ -316,8 +326,8 @@ def train_forward(model, pos, vel, charges, B, N, gauge=None, seed=0):
     xv = linear(vel, m.velocity_embedding.weight, m.velocity_embedding.bias).view(V, 3, C)
     x = torch.cat([x0[:, None], xv, x0.new_zeros(V, 5, C)], 1) + st.edge_degree()
     for blk in m.blocks:
-        y = st.drop_path(st.attention(blk.ga, st.rms_norm(blk.norm_1, x), C)) + x
-        x = st.drop_path(st.ffn(blk.ffn, st.rms_norm(blk.norm_2, y))) + y
+        y = st.proj_drop(st.drop_path(st.attention(blk.ga, st.rms_norm(blk.norm_1, x), C))) + x
+        x = st.proj_drop(st.drop_path(st.ffn(blk.ffn, st.rms_norm(blk.norm_2, y)))) + y
     x = st.rms_norm(m.norm, x)
     pred = st.attention(m.force_block, x, 2)
     return torch.cat([pred[:, 1:4, 0], pred[:, 1:4, 1]], 1)

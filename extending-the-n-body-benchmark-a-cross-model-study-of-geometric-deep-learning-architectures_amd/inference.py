@@ -238,7 +238,7 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
     kw.update(knn)
     sync = shard and hasattr(model, "enable_sync_batchnorm") and model.training
     if sync:
-        model.enable_sync_batchnorm()
+        model.enable_sync_batchnorm(global_batch=batch_size)   # no per-call batch-size collective
     try:
         tp, tv = model.rollout(loc0, vel0, mass0, num_steps, **kw)
     finally:

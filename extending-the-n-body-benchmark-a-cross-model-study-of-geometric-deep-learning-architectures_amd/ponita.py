@@ -25,6 +25,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from .train_dispatch import use_training_path
 
 __all__ = ["PONITA_NBODY", "PonitaFiberBundle", "uniform_grid_s2"]
 
@@ -355,7 +356,7 @@ class PONITA_NBODY(nn.Module):
         m = f(x.reshape(V))
         vel = graph.vec if getattr(graph, "vec", None) is not None else graph.vel
         p, v = f(pos), f(vel.reshape(V, 3))
-        if torch.is_grad_enabled() and any(t.requires_grad for t in self.parameters()):
+        if use_training_path(self):   # train_dispatch.py: autograd on + trainable params
             # training step: native operators under autograd (ponita_train.py).  A model
             # still owing its one-time calibration gets it first from a no-grad forward, as the
             # reference's train.py:49-77 dummy forward does before the first optimiser step.

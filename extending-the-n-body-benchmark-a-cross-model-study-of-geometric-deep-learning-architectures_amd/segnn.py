@@ -14,16 +14,26 @@ from __future__ import annotations
 
 import math
 import warnings
+import weakref
 
 import torch
 import torch.nn as nn
 
 from . import _lib
+from .train_dispatch import use_training_path
 from .o3 import FullyConnectedTensorProduct, Irreps, weight_balanced_irreps
 
 SH_C0 = 1.0 / math.sqrt(4.0 * math.pi)
 SH_C1 = math.sqrt(3.0 / (4.0 * math.pi))
 INV_SQRT3 = 1.0 / math.sqrt(3.0)
+
+
+def _destroy_comm(comm):
+    """Release a library RCCL communicator (after the device has drained the work enqueued on it)."""
+    try:
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(_lib.lib().nbx_comm_destroy(comm), "nbx_comm_destroy")
 
 
 class O3TensorProduct(nn.Module):
@@ -140,6 +150,8 @@ class SEGNN(nn.Module):
         self._ws = None
         self._warned_dtype = False
         self._bn_group = None        # SyncBN process group (enable_sync_batchnorm)
+        self._bn_global_batch = None
+        self._bn_comm_fin = None
         self._bn_hook = None
         self._bn_comm = None         # RCCL communicator the library all-reduces on (nbx_comm_init)
         # deterministic=True: train-mode BatchNorm sums reduced in a fixed order instead of fp64
@@ -438,7 +450,7 @@ class SEGNN(nn.Module):
         return W
 
     # ------------------------------------------------------------ SyncBN (multi-GPU)
-    def enable_sync_batchnorm(self, group=None, use_rccl=None):
+    def enable_sync_batchnorm(self, group=None, use_rccl=None, global_batch=None):
         """Train-mode BatchNorm over the union of every rank's batch (the reference's
         single-process statistics, segnn.py:233-235,257-261,282-283, when the batch is sharded
         over ranks): after each producing kernel the [3][mul] fp64 sums of that BatchNorm are
@@ -447,12 +459,18 @@ class SEGNN(nn.Module):
 
         ``use_rccl`` (default: the group's backend is ``nccl``, i.e. RCCL): the library gets its own
         RCCL communicator over the group's ranks (include/nbx.h nbx_comm_init; collective call) and
-        enqueues the all-reduces itself -- no host round trip per BatchNorm, so a sharded forward or
-        rollout can be captured into a HIP graph.  Otherwise (gloo) the library calls back into
-        ``torch.distributed.all_reduce`` on the group."""
+        enqueues the all-reduces itself -- no host round trip per BatchNorm.  Otherwise (gloo) the
+        library calls back into ``torch.distributed.all_reduce`` on the group.
+
+        ``global_batch``: the number of systems summed over the group's ranks.  When given, a forward
+        or rollout makes no collective and no host synchronisation of its own (with RCCL the call can
+        then be captured into a HIP graph); it must stay the union of the ranks' batches for every
+        call until SyncBN is re-enabled.  When None, every call all-reduces the local batch size
+        first (one small collective plus a ``.item()``)."""
         import torch.distributed as dist
         self.disable_sync_batchnorm()
         self._bn_group = group if group is not None else dist.group.WORLD
+        self._bn_global_batch = None if global_batch is None else int(global_batch)
         if use_rccl is None:
             use_rccl = dist.get_backend(self._bn_group) == "nccl"
         if use_rccl:
@@ -470,14 +488,16 @@ class SEGNN(nn.Module):
             _lib.check(_lib.lib().nbx_comm_init(ctypes.create_string_buffer(uid[0], _lib.COMM_ID_BYTES), len(ranks),
                                                 me, dev, ctypes.byref(comm)), "nbx_comm_init")
             self._bn_comm = comm
+            # a model dropped without disable_sync_batchnorm() still releases its communicator
+            self._bn_comm_fin = weakref.finalize(self, _destroy_comm, comm)
         return self
 
     def disable_sync_batchnorm(self):
         if self._bn_comm is not None:
-            torch.cuda.synchronize()
-            _lib.check(_lib.lib().nbx_comm_destroy(self._bn_comm), "nbx_comm_destroy")
-            self._bn_comm = None
+            self._bn_comm_fin()      # synchronise, nbx_comm_destroy (runs once)
+            self._bn_comm, self._bn_comm_fin = None, None
         self._bn_group = None
+        self._bn_global_batch = None
         return self
 
     def _allreduce_cb(self, buf, count, stream, ctx):
@@ -510,6 +530,11 @@ class SEGNN(nn.Module):
                 self._bn_hook = _lib.ALLREDUCE_FN(self._allreduce_cb)
             W.bn_comm = None
             W.bn_allreduce = self._bn_hook
+        if self._bn_global_batch is not None:
+            if B > self._bn_global_batch:
+                raise ValueError(f"SyncBN: local batch {B} exceeds global_batch {self._bn_global_batch}")
+            W.bn_global_batch = self._bn_global_batch
+            return
         on_dev = dist.get_backend(self._bn_group) == "nccl"
         nb = torch.tensor([B], dtype=torch.int64, device=device if on_dev else "cpu")
         dist.all_reduce(nb, group=self._bn_group)
@@ -563,7 +588,7 @@ class SEGNN(nn.Module):
         self._check_params(device)
         f = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()
         p, v, m = f(pos), f(graph.vel), f(graph.mass.reshape(-1))
-        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()):
+        if use_training_path(self):   # train_dispatch.py: autograd on + trainable params
             # training step (trainer.py:233-358): the forward runs on the native training operators
             # with autograd (segnn_train.py), so loss.backward() reaches every parameter
             if self._bn_group is not None and self._bn_batch():

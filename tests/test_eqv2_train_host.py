@@ -114,3 +114,32 @@ def test_train_forward_composition_matches_oracle(torch_ops):
     assert set(grads) == set(rg)
     for k in rg:
         torch.testing.assert_close(grads[k], rg[k], rtol=1e-10, atol=1e-12, msg=k)
+
+
+def test_train_forward_dropout_sites(torch_ops, monkeypatch):
+    """Train-mode dropouts of the composition: alpha dropout at each block's own rate and never in the
+    force block (equiformer_v2_nbody.py:362 builds it with alpha_drop=0.0), proj_drop after the
+    attention and after the FFN of every block (transformer_block.py:690-706), none in eval mode."""
+    calls = []
+    real = torch.nn.functional.dropout
+
+    def spy(x, p=0.5, training=True, inplace=False):
+        calls.append((tuple(x.shape), p, training))
+        return real(x, p, training, inplace)
+    monkeypatch.setattr(torch.nn.functional, "dropout", spy)
+    torch.manual_seed(0)
+    m = EquiformerV2_nbody(**CFG, alpha_drop=0.1, drop_path_rate=0.0, proj_drop=0.2).double()
+    B, N = 2, 4
+    rng = np.random.default_rng(1)
+    loc = torch.tensor(rng.standard_normal((B * N, 3)))
+    vel = torch.tensor(rng.standard_normal((B * N, 3))) * 0.3
+    mass = torch.ones(B * N, dtype=torch.float64)
+    gauge = torch.tensor(rng.uniform(0, 1, (B * N * (N - 1), 3)))
+    out = T.train_forward(m.train(), loc, vel, mass, B, N, gauge, 0)
+    E, V, C, nh = B * N * (N - 1), B * N, CFG["sphere_channels"], CFG["num_heads"]
+    per_block = [((E, nh), 0.1, True), ((V, 1, C), 0.2, True), ((V, 1, C), 0.2, True)]
+    assert calls == per_block * CFG["num_layers"], calls
+    assert torch.isfinite(out).all()
+    calls.clear()
+    T.train_forward(m.eval(), loc, vel, mass, B, N, gauge, 0)
+    assert calls == []

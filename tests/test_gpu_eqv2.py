@@ -43,8 +43,9 @@ def run(m, loc, vel, mass, gauge, device):
     t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32, device=device).reshape(B * N, -1)
     batch = torch.arange(B, device=device).repeat_interleave(N)
     pos = t(loc)
-    out = m((pos, t(vel), torch.zeros_like(pos), t(mass), pos), batch,
-            gauge=torch.as_tensor(np.asarray(gauge), dtype=torch.float32, device=device))
+    with torch.no_grad():   # the fused inference kernels (a grad-mode forward runs the training composition)
+        out = m((pos, t(vel), torch.zeros_like(pos), t(mass), pos), batch,
+                gauge=torch.as_tensor(np.asarray(gauge), dtype=torch.float32, device=device))
     torch.cuda.synchronize()
     return out.double().cpu().numpy()
 

@@ -193,6 +193,7 @@ def test_training_step_bit_reproducible_and_eval_matches_inference(hip_device):
     gg = torch.as_tensor(gauge, device=hip_device)
     with torch.no_grad():
         inf = m((pos, t(vel), torch.zeros_like(pos), t(mass), pos), batch, gauge=gg)
+    m.native_train = True    # explicit: an eval-mode grad forward runs the training composition
     tr = m((pos, t(vel), torch.zeros_like(pos), t(mass), pos), batch, gauge=gg)
     assert tr.requires_grad
     torch.testing.assert_close(tr.detach(), inf, rtol=2e-5, atol=2e-6)

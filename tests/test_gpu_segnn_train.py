@@ -212,6 +212,7 @@ def test_training_steps_with_adamw_decrease_loss(hip_device):
     g.pos, g.vel, g.mass, g.edge_index = t(pos), t(vel), t(mass), G.fc_edge_index(B, N, hip_device)
     with torch.no_grad():
         inf = model(g)
+    model.native_train = True    # explicit: an eval-mode grad forward runs the training composition
     with torch.enable_grad():
         tr = model(g)       # eval-mode training forward: running statistics, same weights
     torch.testing.assert_close(inf, tr.detach(), rtol=1e-4, atol=1e-5)

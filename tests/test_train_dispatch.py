@@ -1,0 +1,54 @@
+"""The forward's path rule (train_dispatch.py): training composition only when autograd records and
+parameters are trainable; an eval()-mode grad forward warns once; ``native_train`` overrides it.
+Reference behaviour it serves: trainer.py:233-358 (train mode, grad) and trainer.py:417 (validation
+under torch.no_grad())."""
+import warnings
+
+import pytest
+import torch
+
+from nbody_amd.egnn_mc import EGNNMultiChannel
+from nbody_amd.train_dispatch import NativePathWarning, use_training_path
+
+
+def _model():
+    return EGNNMultiChannel(num_layers=1, hidden_node_dim=8, hidden_edge_dim=8, hidden_coord_dim=8, target_names=["pos_dt", "vel"])
+
+
+def test_train_mode_grad_takes_training_path():
+    m = _model().train()
+    assert use_training_path(m)
+    with torch.no_grad():
+        assert not use_training_path(m)
+
+
+def test_frozen_parameters_take_fused_path():
+    m = _model().train()
+    for p in m.parameters():
+        p.requires_grad_(False)
+    assert not use_training_path(m)
+
+
+def test_eval_grad_warns_once():
+    m = _model().eval()
+    with pytest.warns(NativePathWarning):
+        assert use_training_path(m)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert use_training_path(m)
+
+
+def test_explicit_override():
+    m = _model().eval()
+    m.native_train = True
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert use_training_path(m)
+    with torch.no_grad():
+        assert not use_training_path(m)
+    m.native_train = False
+    assert not use_training_path(m.train())
+    m.native_train = "yes"
+    with pytest.raises(ValueError):
+        use_training_path(m)
+    assert "native_train" not in m.state_dict()
