@@ -170,6 +170,19 @@ def bench_segnn(a, rank, world, device, P):
         return tp
     tp, elapsed = timed_region(work, device, P)
     finite = bool(torch.isfinite(tp).all().item())
+    # diagnostic (outside the timed region): host time to enqueue one rollout of the same length
+    # against its device completion, and the device time of the rollout kernels alone (events)
+    torch.cuda.synchronize(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    h0 = time.perf_counter()
+    e0.record()
+    model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
+    e1.record()
+    h1 = time.perf_counter()
+    torch.cuda.synchronize(device)
+    h2 = time.perf_counter()
+    diag = {"host_enqueue_ms": round(1e3 * (h1 - h0), 3), "host_to_done_ms": round(1e3 * (h2 - h0), 3),
+            "device_event_ms": round(e0.elapsed_time(e1), 3)}
 
     # live roofline of the dominant kernel: HIP events around every launch of the
     # fused tensor-product kernels of a few forwards, on the launch stream, split by kind
@@ -245,7 +258,7 @@ def bench_segnn(a, rank, world, device, P):
                                             if x3 else None),
                      "timing": "hipExtLaunchKernel start/stop events (kernel execution interval)",
                      "fused_tp_share_of_forward": round(sum(ms_k) / fwd_ms, 3), "per_kind": per_kind},
-        "finite": finite,
+        "finite": finite, "rollout_timing": diag,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         # >= 20 steps of the PyTorch CPU restatement (the reported baseline), beside one

@@ -1,6 +1,7 @@
 """Generate the long-horizon C2 SEGNN rollout fixture from the CPU oracle (build container).
 
     python tests/golden/make_segnn_c2_long.py [--frames 121] [--scale 0.002] [--slice 64] [--add-perturbed]
+                                              [--add-perturbed-traj]
 
 Why a second C2 fixture: with random-init weights the C2 rollout of make_segnn_c2.py turns chaotic
 within ~5 steps (bodies flung to |pos| ~ 50, pairs passing within 1e-3 of each other), so north_star's
@@ -61,9 +62,13 @@ def main():
     ap.add_argument("--slice", type=int, default=64)
     ap.add_argument("--add-perturbed", action="store_true",
                     help="add the one-ulp sensitivity (pert_mse_*) to an existing fixture")
+    ap.add_argument("--add-perturbed-traj", action="store_true",
+                    help="add the one-ulp-perturbed fp64 trajectories of the slice (pert_loc / pert_vel)")
     a = ap.parse_args()
     if a.add_perturbed:
         return add_perturbed()
+    if a.add_perturbed_traj:
+        return add_perturbed_traj()
     from oracle.rollout import rollout, segnn_step
     from oracle.segnn import SEGNNOracle
     model = scaled_model(a.scale)
@@ -119,6 +124,63 @@ def add_perturbed():
     for k in range(0, T, 10):
         print(f"frame {k}: one-ulp sensitivity MSE loc {fx['pert_mse_loc'][k]:.3e} vel {fx['pert_mse_vel'][k]:.3e}")
     print(f"max over the horizon: loc {fx['pert_mse_loc'].max():.3e} vel {fx['pert_mse_vel'].max():.3e}")
+    np.savez_compressed(path, **fx)
+
+
+def torch_rollout(params, loc, vel, mass, T):
+    """The fp64 train-mode self-feed (infer_self_feed.py:182-194, target pos_dt+vel) on the torch
+    restatement oracle/segnn_torch.py (equal to oracle/segnn.py to ~1e-16 per forward, and several
+    times faster on the CPU); running statistics carried from step to step."""
+    from oracle import segnn_torch as OT
+    from oracle.graph import fc_edge_index
+    from oracle.segnn import SEGNNOracle
+    om = SEGNNOracle(hidden_features=HIDDEN, num_layers=LAYERS)
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in params.items()}
+    Bn, Nn = loc.shape[:2]
+    ei = torch.from_numpy(fc_edge_index(Bn, Nn))
+    p = torch.tensor(loc.reshape(-1, 3), dtype=torch.float64)
+    v = torch.tensor(vel.reshape(-1, 3), dtype=torch.float64)
+    m = torch.tensor(mass.reshape(-1, 1), dtype=torch.float64)
+    locs, vels = [p.clone()], [v.clone()]
+    with torch.no_grad():
+        for k in range(T - 1):
+            out, stats = OT.forward(om, P, p, v, m, ei, True)
+            P.update(stats)
+            p, v = p + out[:, :3], out[:, 3:].contiguous()
+            locs.append(p.clone())
+            vels.append(v.clone())
+            if k % 10 == 0:
+                print(f"  step {k + 1}/{T - 1}", flush=True)
+    st = lambda xs: torch.stack(xs, 1).reshape(Bn, Nn, T, 3).permute(0, 2, 1, 3).numpy()
+    return st(locs), st(vels)
+
+
+def add_perturbed_traj():
+    """Store the one-ulp-perturbed fp64 trajectories of the slice (``pert_loc`` / ``pert_vel``), so that
+    the device test can normalise any error measure (velocities, displacements pos - pos0, per-system
+    relative errors) by the same measure of the reference's own one-ulp sensitivity.  Also re-runs the
+    unperturbed rollout on the torch oracle and records its largest difference from the stored numpy
+    trajectory (``torch_vs_numpy_max``: the two oracles' ~1e-16 per-step disagreement amplified by the
+    horizon), which must stay far below the perturbed rollout's distance."""
+    path = os.path.join(HERE, "segnn_c2_long.npz")
+    fx = dict(np.load(path))
+    model = scaled_model(float(fx["scale"]))
+    assert abs(weight_checksum(model) - float(fx["weight_checksum"])) <= 1e-9 * float(fx["weight_checksum"])
+    params = {k: t.double().numpy().copy() for k, t in model.state_dict().items()}
+    loc, vel = fx["loc0"], fx["vel0"]
+    _, _, mass = initial_states()
+    T, S = fx["traj_loc"].shape[1], fx["traj_loc"].shape[0]
+    up = lambda x: np.nextafter(x.astype(np.float32), np.float32(np.inf)).astype(np.float64)
+    t0 = time.time()
+    tl, tv = torch_rollout(params, loc, vel, mass, T)
+    d = max(np.abs(tl[:S] - fx["traj_loc"]).max(), np.abs(tv[:S] - fx["traj_vel"]).max())
+    print(f"torch fp64 rollout: {time.time() - t0:.1f} s; max |torch - numpy| over the slice {d:.3e}", flush=True)
+    pl, pv = torch_rollout(params, up(loc), up(vel), mass, T)
+    print(f"perturbed torch fp64 rollout: {time.time() - t0:.1f} s", flush=True)
+    pm = ((pl[:S] - fx["traj_loc"]) ** 2).mean(axis=(0, 2, 3))
+    print(f"pert MSE (torch) vs stored pert_mse_loc: max ratio {np.max(pm[1:] / fx['pert_mse_loc'][1:]):.3f}")
+    fx["pert_loc"], fx["pert_vel"] = pl[:S], pv[:S]
+    fx["torch_vs_numpy_max"] = np.float64(d)
     np.savez_compressed(path, **fx)
 
 
