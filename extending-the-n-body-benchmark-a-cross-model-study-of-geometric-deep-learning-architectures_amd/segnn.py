@@ -94,6 +94,29 @@ class BatchNorm(nn.Module):
         self.register_buffer("running_var", torch.ones(self.irreps.num_irreps))
 
 
+class _TrainPackFn(torch.autograd.Function):
+    """SEGNN._train_layout's gather: (layout, *flat tensor-product weights) -> the operand tensors."""
+
+    @staticmethod
+    def forward(ctx, L, *weights):
+        flat = torch.cat([w.reshape(-1).to(torch.float32) for w in weights] +
+                         [torch.zeros(1, device=L["src"].device, dtype=torch.float32)])
+        buf = flat.index_select(0, L["src"]).mul_(L["scale"])
+        ctx.L = L
+        ctx.meta = [(w.dtype, w.shape) for w in weights]
+        return tuple(buf[o:o + math.prod(sh)].view(sh) for o, sh in L["slots"].values())
+
+    @staticmethod
+    def backward(ctx, *grads):
+        L = ctx.L
+        parts = [g.reshape(-1) if g is not None else torch.zeros(math.prod(sh), device=L["src"].device)
+                 for g, (o, sh) in zip(grads, L["slots"].values())]
+        dbuf = torch.cat(parts).mul_(L["scale"])
+        dflat = torch.zeros(L["total"], device=dbuf.device, dtype=torch.float32)
+        dflat.index_put_((L["live_src"],), dbuf.index_select(0, L["live_pos"]))   # unique targets
+        return (None,) + tuple(d.view(sh).to(dt) for d, (dt, sh) in zip(dflat.split(L["sizes"]), ctx.meta))
+
+
 class SEGNNLayer(nn.Module):
     """segnn.py:192-304 (PyG MessagePassing, aggr="add", node_dim=-2)."""
 
@@ -148,6 +171,7 @@ class SEGNN(nn.Module):
             raise NotImplementedError(f"hidden irreps {hidden_irreps} outside the native path (mul % 4 == 0)")
         self._packed = None
         self._ws = None
+        self._tlayout = None         # training operand layout (_train_layout)
         self._warned_dtype = False
         self._bn_group = None        # SyncBN process group (enable_sync_batchnorm)
         self._bn_global_batch = None
@@ -237,17 +261,20 @@ class SEGNN(nn.Module):
         P["pp2"] = vec(torch.stack([Ws[:, 0], Ws[:, 1], Wv[:, 0], Wv[:, 1]]))
         return P
 
-    def train_matrices(self, device):
+    def train_matrices(self, device, weights=None, dtype=torch.float32):
         """The operands of the training step's canonical tensor products (include/nbx.h "SEGNN
         training step"; segnn_train.py), built from the e3nn parameters with differentiable torch
         ops: ``<tp>_s`` = Ws [NSc + Nt][Ks + Kv], ``<tp>_v`` = Wv [Nt][Kv], ``<tp>_bias``.  Same
         constants as packed_matrices; message_layer_1 unfactored, its input being
-        [x_i s | x_j s | amf | x_i v . rhat | x_j v . rhat] and [x_i v | x_j v] per edge."""
+        [x_i s | x_j s | amf | x_i v . rhat | x_j v . rhat] and [x_i v | x_j v] per edge.
+        ``weights``: {id(O3TensorProduct): flat weight} in place of the modules' own (the layout
+        trace of :meth:`train_operands`)."""
         M = self.mul
-        f32 = dict(device=device, dtype=torch.float32)
+        f32 = dict(device=device, dtype=dtype)
 
         def views(tpmod):
-            return [w.to(**f32)[:, 0, :] for w in tpmod.tp.weight_views()]   # [mul1, mul_out]
+            w = None if weights is None else weights[id(tpmod)]
+            return [v.to(**f32)[:, 0, :] for v in tpmod.tp.weight_views(w)]   # [mul1, mul_out]
 
         def T(x):
             return x.t().contiguous()
@@ -288,6 +315,67 @@ class SEGNN(nn.Module):
         Ws, Wv = views(self.pre_pool2)
         P["pp2_s"] = T(torch.cat([Ws, z(M, 2)]))
         P["pp2_v"] = T(Wv)
+        return P
+
+    def _train_layout(self, device):
+        """The map from the concatenated tensor-product weights to every operand of
+        :meth:`train_matrices`, traced once (the layout depends on the module structure only):
+        operand element i = scale[i] * flat[src[i]], or 0 (src = the appended zero slot).  Every
+        weight element feeds at most one operand element, so the backward is a scatter."""
+        if self._tlayout is not None and self._tlayout["device"] == device:
+            return self._tlayout
+        tps = [m for m in self.modules() if isinstance(m, O3TensorProduct)]
+        sizes = [m.tp.weight.numel() for m in tps]
+        total = sum(sizes)
+        ids, ones, off = {}, {}, 0
+        for m, n in zip(tps, sizes):
+            ids[id(m)] = torch.arange(off + 1, off + n + 1, dtype=torch.float64)   # 1-based: 0 = no source
+            ones[id(m)] = torch.ones(n, dtype=torch.float64)
+            off += n
+        cpu = torch.device("cpu")
+        with torch.no_grad():
+            Pi = self.train_matrices(cpu, ids, torch.float64)
+            Po = self.train_matrices(cpu, ones, torch.float64)
+        keys = [k for k in Pi if not k.endswith("_bias")]
+        src, scale, slots = [], [], {}
+        pos = 0
+        for k in keys:
+            vi, vo = Pi[k].reshape(-1), Po[k].reshape(-1)
+            live = vo != 0
+            idx = torch.where(live, torch.round(vi / torch.where(live, vo, torch.ones_like(vo))), torch.zeros_like(vi))
+            if not torch.equal(idx * vo, torch.where(live, vi, torch.zeros_like(vi))) and \
+                    not torch.allclose(idx * vo, vi, rtol=1e-12, atol=0):
+                raise RuntimeError(f"SEGNN training operand {k} is not a scaled copy of the weights")
+            src.append(torch.where(live, idx - 1, torch.full_like(idx, total)).long())
+            scale.append(torch.where(live, vo, torch.zeros_like(vo)))
+            slots[k] = (pos, tuple(Pi[k].shape))
+            pos += vi.numel()
+        src, scale = torch.cat(src), torch.cat(scale)
+        live = src < total
+        if torch.unique(src[live]).numel() != int(live.sum()):
+            raise RuntimeError("SEGNN training operands: a weight element feeds two operand elements")
+        self._tlayout = {"device": device, "tps": tps, "sizes": sizes, "slots": slots,
+                         "src": src.to(device), "scale": scale.to(device=device, dtype=torch.float32),
+                         "live_pos": torch.nonzero(live).reshape(-1).to(device),
+                         "live_src": src[live].to(device), "total": total}
+        return self._tlayout
+
+    def train_operands(self, device):
+        """:meth:`train_matrices` as one gather: the concatenated tensor-product weights -> every
+        operand (scale x weight), and in the backward one scatter of the operand gradients back
+        (_TrainPackFn).  Equal to train_matrices element for element (a product by the same
+        constant); a few launches instead of hundreds of small differentiable torch ops."""
+        L = self._train_layout(device)
+        outs = _TrainPackFn.apply(L, *[m.tp.weight for m in L["tps"]])
+        P = dict(zip(L["slots"], outs))
+        f32 = dict(device=device, dtype=torch.float32)
+        P["emb_bias"] = self.embedding_layer.biases.to(**f32)
+        for li, layer in enumerate(self.layers):
+            p = f"layers.{li}."
+            for name, mod in (("msg1", layer.message_layer_1), ("msg2", layer.message_layer_2),
+                              ("upd1", layer.update_layer_1), ("upd2", layer.update_layer_2)):
+                P[p + name + "_bias"] = mod.biases.to(**f32)
+        P["pp1_bias"] = self.pre_pool1.biases.to(**f32)
         return P
 
     # ------------------------------------------------------------ LDS images (include/nbx.h)

@@ -16,8 +16,9 @@ module tree (tensor-product weights, biases, BatchNorm weight / bias):
 * message passing (x_i = x[dst], x_j = x[src], aggr="add" at edge_index[1]) = ``_GatherFn`` /
   ``_SegSumFn`` over CSR tables of the edges by destination and by source (deterministic).
 
-The weight operands come from the e3nn parameters through differentiable torch ops
-(``SEGNN.train_matrices``), so the gradient of the packed operands flows back to the parameters.
+The weight operands come from the e3nn parameters through one traced gather (``SEGNN.train_operands``:
+every operand element is a constant times one weight element, the layout of ``SEGNN.train_matrices``),
+whose backward scatters the operand gradients back onto the parameters.
 Arithmetic is fp32 (a float64 module is cast for the step, like its fp32 inference path).
 """
 from __future__ import annotations
@@ -297,7 +298,7 @@ def train_forward(model, pos, vel, mass, edge_index):
     V = pos.shape[0]
     g = Graph(edge_index, V, dev)
     na3, xs0, xv0, rhat, amf = featurize(pos, vel, mass, g)
-    W = model.train_matrices(dev)
+    W = model.train_operands(dev)
     M = model.mul
     batch_stats = model._bn_batch()
     hs, hv = tp(xs0, xv0, na3, W["emb_s"], W["emb_v"], W["emb_bias"], M, M, 0)
