@@ -68,6 +68,8 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
     const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void*)P.As, (short)0, 0x7FFFFFF0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV =
         __builtin_amdgcn_make_buffer_rsrc((void*)(NV ? P.Av : P.As), (short)0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsSeg = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(SK::SEG > 0 ? P.seg_base : P.As), (short)0, 0x7FFFFFF0, 0x00020000);
     auto load_a = [&](int rt, int i, float4 (&a)[2]) {
         // branch-free: both the scalar- and the vector-chunk offsets are computed and selected,
         // so one pair of loads is issued from one code path; chunks outside [c_lo, c_hi) (ring
@@ -111,16 +113,16 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
         constexpr int kc = sc ? item : v - plane * SK::KV;
         const int row = rt_ * 16 + c16;
         if constexpr (SK::SEG > 0) {
-            // segment q of width M = (K0 / SEG) chunks (scalar) or (KV / (SEG / 2)) chunks (vector)
+            // segment q of width M = (K0 / SEG) chunks (scalar) or (KV / (SEG / 2)) chunks (vector);
+            // one resource over all segments (seg_base), the segment / plane as the scalar offset
             constexpr int cps = sc ? SK::K0 / SK::SEG : SK::KV / (SK::SEG / 2);
             constexpr int q = kc / cps, kk = (kc - q * cps) * 32;
             const int k = kk + 8 * qd;
             const bool ok = row < P.rows;
-            const float* base = sc ? P.seg_s[q] : P.seg_v[q] + (size_t)plane * P.seg_vplane;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFF0, 0x00020000);
+            const uint32_t soff = sc ? P.seg_boff[q] : P.seg_boff[4 + q] + (uint32_t)(plane * P.seg_vplane * 4);
             const uint32_t off = ok ? (uint32_t)(((size_t)row * P.M + k) * 4) : 0x7FFFFFF0u;
-            a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-            a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off + 16 : off, 0, 0));
+            a[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsSeg, off, soff, 0));
+            a[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsSeg, ok ? off + 16 : off, soff, 0));
         } else {
             const int k = kc * 32 + 8 * qd;
             const bool ok = row < P.rows && k < (sc ? P.K[0] : P.Kv);
@@ -803,9 +805,35 @@ int tp16_check_static(const TpProb& p) {
     return NBX_OK;
 }
 
+// segmented input (StatSK SEG > 0): one buffer resource over every segment -- the lowest segment
+// pointer and each segment's byte offset from it (all segments live in one workspace)
+inline int tp16_seg_prepare(TpProb& p) {
+    if (!p.seg_s[0]) return NBX_OK;
+    const float* ptrs[6] = {p.seg_s[0], p.seg_s[1], p.seg_s[2], p.seg_s[3], p.seg_v[0], p.seg_v[1]};
+    const float* base = nullptr;
+    for (const float* q : ptrs)
+        if (q && (!base || q < base)) base = q;
+    p.seg_base = base;
+    for (int i = 0; i < 6; ++i) {
+        const long long off = ptrs[i] ? (long long)((const char*)ptrs[i] - (const char*)base) : 0;
+        const long long end = off + (long long)(i >= 4 ? 3 : 1) * p.seg_vplane * 4;
+        if (end >= 0x7FFFFFF0LL) {
+            set_error("tp16: segmented input spans >= 2 GiB (32-bit buffer offsets)");
+            return NBX_E_UNSUPPORTED;
+        }
+        p.seg_boff[i] = (unsigned)off;
+    }
+    return NBX_OK;
+}
+
 template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, bool DUAL, class SK = DynSK>
 int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
     if (b0 + b1 == 0) return NBX_OK;
+    if constexpr (SK::SEG > 0) {
+        if (int rc = tp16_seg_prepare(p0)) return rc;
+        if (DUAL)
+            if (int rc = tp16_seg_prepare(p1)) return rc;
+    }
     if (int rc = tp16_check_static<SK>(p0)) return rc;
     if (DUAL)
         if (int rc = tp16_check_static<SK>(p1)) return rc;

@@ -136,6 +136,11 @@ struct TpProb {
     const float* seg_s[4];
     const float* seg_v[2];
     long seg_vplane;
+    // (set by the tp16 launcher) one buffer resource for all segments: the lowest segment pointer,
+    // and each segment's byte offset from it (seg_s 0-3, seg_v 4-5) passed as the load's soffset,
+    // so the kernel holds one 4-SGPR resource instead of one per (segment, plane)
+    const float* seg_base;
+    unsigned seg_boff[6];
     const float* mcoef;
     BnSrc mbn;           // SEG = 4 with mbn.sums: message BN finalised here from atomic sums (mcoef unused)
     BnSrc xbn;           // SEG > 0 with xbn.sums: pending feature BN finalised here (the segment table's

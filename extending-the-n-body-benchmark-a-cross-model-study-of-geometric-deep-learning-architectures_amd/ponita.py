@@ -319,7 +319,17 @@ class PONITA_NBODY(nn.Module):
 
     # ------------------------------------------------------------ calibration
     def _needs_callibration(self):
-        return self.training and any(not bool(L.conv.callibrated) for L in self.model.interaction_layers)
+        if not self.training:
+            return False
+        # the flags are device buffers: their value is cached per (pointer, version), so a steady-state
+        # call (e.g. inside a captured training step) makes no host synchronisation
+        flags = [L.conv.callibrated for L in self.model.interaction_layers]
+        key = tuple((f.data_ptr(), f._version) for f in flags)
+        cached = getattr(self, "_calib_cache", None)
+        if cached is None or cached[0] != key:
+            cached = (key, any(not bool(f) for f in flags))
+            self._calib_cache = cached
+        return cached[1]
 
     @torch.no_grad()
     def _callibrate(self, moments, n):
