@@ -30,6 +30,7 @@
 #include "tp16.h"
 #include "tp_fused.h"
 #include "msg_pre.h"
+#include "upd_vec.h"
 
 namespace {
 
@@ -679,6 +680,7 @@ using SK_UPD1 = nbx::StatSK<12, 12, 6, 6>;
 using SK_UPD1_32 = nbx::StatSK<4, 4, 2, 2>;
 using SK_UPD1_SEG = nbx::StatSK<12, 12, 6, 6, 4>;
 using SK_UPD1_SEG_X3 = nbx::StatSKX3<12, 12, 6, 6, 4>;
+using SK_UPD1S_SEG_X3 = nbx::StatSKX3<12, 12, 6, 0, 4>;   // split form: the 0e items only (upd_vec.h)
 using SK_UPD1_32_SEG = nbx::StatSK<4, 4, 2, 2, 4>;
 using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
 using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
@@ -825,9 +827,27 @@ int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
     k += NV ? 3.0 * p.Kv : 0.0;
-    tm->kind.push_back(EPI);
-    tm->flops[EPI] += 2.0 * p.rows * 16.0 * p.chunks * k;
-    tm->launches[EPI] += 1;
+    // the split update_layer_1 (GATE_VRAW + upd_vec_kernel) is timed as the update_layer_1 kind; its
+    // two launches count as one launch of the kind
+    constexpr int kind = EPI == nbx::TP_GATE_VRAW ? (int)nbx::TP_GATE_NODE : EPI;
+    tm->kind.push_back(kind);
+    tm->flops[kind] += 2.0 * p.rows * 16.0 * p.chunks * k;
+    tm->launches[kind] += 1;
+    return NBX_OK;
+}
+
+int run_upd_vec(const nbx::UpdVecProb& p, hipStream_t st, KernelTiming* tm) {
+    if (!tm) return nbx::upd_vec_launch(p, st);
+    hipEvent_t a, b;
+    NBX_HIP(hipEventCreate(&a));
+    NBX_HIP(hipEventCreate(&b));
+    tm->ev.push_back(a);
+    tm->ev.push_back(b);
+    nbx::armed_events() = {a, b};
+    if (int rc = nbx::upd_vec_launch(p, st)) return rc;
+    NBX_HIP(nbx::disarm_events(st));
+    tm->kind.push_back(nbx::TP_GATE_NODE);
+    tm->flops[nbx::TP_GATE_NODE] += 2.0 * 3.0 * p.V * 2.0 * p.M * p.M;
     return NBX_OK;
 }
 
@@ -1118,7 +1138,27 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
-            if (M == 96 && L.upd1_img_x3 && x3_enabled()) {
+            // split form (upd_vec.h): the 1o GEMM of all channels, then the 0e GEMM + gate
+            // (NBX_UPD1_SPLIT=0: the combined kernel, A/B only)
+            static const bool upd1_split = !getenv("NBX_UPD1_SPLIT") || atoi(getenv("NBX_UPD1_SPLIT")) != 0;
+            if (M == 96 && L.upd1_img_x3 && x3_enabled() && upd1_split) {
+                const int kc_s = (4 * M + 31) / 32, kc_t = (2 * M + 31) / 32, kc_v = (2 * M + 31) / 32;
+                const int stride = (2 * kc_s + kc_t + kc_v) * 768;   // floats per bf16x3 chunk image
+                nbx::UpdVecProb vp;
+                memset(&vp, 0, sizeof(vp));
+                vp.xv = ws.X + V * M; vp.av = ws.AGG + V * M;
+                vp.img = static_cast<const float*>(L.upd1_img_x3);
+                vp.img_stride = stride; vp.vec_off = (2 * kc_s + kc_t) * 768;
+                vp.xcoef = xprev; vp.mcoef = ws.coef_msg; vp.mbn = p.mbn;
+                vp.out = ws.U1V; vp.V = V; vp.M = M;
+                if (int rc = run_upd_vec(vp, st, tm)) return rc;
+                p.B = static_cast<const float*>(L.upd1_img_x3);
+                p.img_stride = stride;
+                p.Kv = 0;
+                p.Av = ws.U1V; p.lda_v = M; p.plane_stride = V * M;
+                p.mbn = nbx::BnSrc{};   // finalised by upd_vec_kernel's block 0 into ws.coef_msg
+                if (int rc = run_tp16_w<3, 0, nbx::TP_GATE_VRAW, 1, 8, 3, 1, SK_UPD1S_SEG_X3>(p, st, tm)) return rc;
+            } else if (M == 96 && L.upd1_img_x3 && x3_enabled()) {
                 p.B = static_cast<const float*>(L.upd1_img_x3);
                 // A-ring depth (NBX_UPD1_PF, A/B): 3 = three B sets; > 3 = two B sets + the deeper ring
                 static const int upd1_pf = getenv("NBX_UPD1_PF") ? atoi(getenv("NBX_UPD1_PF")) : 3;

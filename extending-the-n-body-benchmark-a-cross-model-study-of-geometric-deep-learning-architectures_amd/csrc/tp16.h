@@ -211,6 +211,23 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
             // their latency hides under the MFMAs (not after the last chunk)
             float rres[EPI == TP_RESID ? CG : 1][4][4];
             float rna[4][3];
+            float rvr[EPI == TP_GATE_VRAW ? CG : 1][4][3];   // GATE_VRAW: the rows' 1o pre-gate values
+            if constexpr (EPI == TP_GATE_VRAW) {
+                const int row0p = rt * 16 + 4 * qd;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int row = row0p + jj;
+                    const bool rok = rt < row_tiles && row < P.rows;
+#pragma unroll
+                    for (int g = 0; g < CG; ++g) {
+                        const int ch = (cgroup * CG + g) * 16 + c16;
+                        const bool ok = rok && ch < P.M;
+                        const size_t o = (size_t)row * P.lda_v + ch;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) rvr[g][jj][k] = ok ? P.Av[(size_t)k * P.plane_stride + o] : 0.f;
+                    }
+                }
+            }
             if constexpr (EPI == TP_RESID) {
                 const int row0p = rt * 16 + 4 * qd;
 #pragma unroll
@@ -664,6 +681,26 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
                         P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
                     }
+                } else if constexpr (EPI == TP_GATE_VRAW) {
+                    const bool live = ch < M;
+                    const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int row = row0 + jj;
+                        if (!live || row >= P.rows) continue;
+                        const float* na = P.geom + (size_t)row * 4;
+                        const float hs = kC_SILU * tp_silu(acc[g][0][jj] + ba);
+                        const float gg = kC_SIGMOID * tp_sigmoid(acc[g][1][jj] + bg);
+                        const float tt = acc[g][2][jj];
+                        const float h0 = gg * (na[1] * tt + rvr[g][jj][0]);
+                        const float h1 = gg * (na[2] * tt + rvr[g][jj][1]);
+                        const float h2 = gg * (na[3] * tt + rvr[g][jj][2]);
+                        P.out_s[(size_t)row * 2 * M + ch] = hs;
+                        P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
+                        P.out_v[(size_t)row * M + ch] = h0;
+                        P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
+                        P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
+                    }
                 } else if constexpr (EPI == TP_RESID) {
                     const bool live = ch < M;
                     const float b = live ? P.bias[ch] : 0.f;
@@ -796,8 +833,10 @@ int tp16_check_static(const TpProb& p) {
             set_error("tp16: segmented pre_pool input needs mul %% 32 == 0 and the segment pointers");
             return NBX_E_INVAL;
         }
-        if (SK::SEG == 4 && (p.M * 4 != SK::K0 * 32 || p.M * 2 != SK::KV * 32 || !p.seg_s[0] || !p.seg_s[1] ||
-                             !p.seg_s[2] || !p.seg_s[3] || !p.seg_v[0] || !p.seg_v[1] || !p.mcoef)) {
+        // (KV = 0: the scalar items only, update_layer_1's split form -- upd_vec.h)
+        if (SK::SEG == 4 && (p.M * 4 != SK::K0 * 32 || (SK::KV && p.M * 2 != SK::KV * 32) || !p.seg_s[0] ||
+                             !p.seg_s[1] || !p.seg_s[2] || !p.seg_s[3] || (SK::KV && (!p.seg_v[0] || !p.seg_v[1])) ||
+                             (!p.mcoef && !p.mbn.sums))) {
             set_error("tp16: segmented update input needs mul %% 32 == 0 and all segment pointers");
             return NBX_E_INVAL;
         }

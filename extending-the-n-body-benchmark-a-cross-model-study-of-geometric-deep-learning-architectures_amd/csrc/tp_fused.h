@@ -28,7 +28,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3 };
+// TP_GATE_VRAW (tp16, NV = 0): the gated node epilogue of TP_GATE_NODE with the 1o pre-gate values
+// read from Av ([3][rows][lda_v], planes plane_stride apart: upd_vec_kernel's v_raw) instead of the
+// kernel's own vector accumulators (upd_vec.h)
+enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3, TP_GATE_VRAW = 4 };
 
 // BatchNorm statistics accumulated by the producing kernel with device-scope fp64 atomics
 // ([3][M]: sum s and sum s^2 over the 0e channels, sum |v|^2 over the 1o channels) and
