@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 11
+ABI_VERSION = 12
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B = 1, 2
@@ -123,6 +123,8 @@ _SIGNATURES = {
     "nbx_comm_allreduce_f64": (ctypes.c_int, [c_p, c_i64, c_p, c_p]),
     "nbx_gemm_f32_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "nbx_gemm_f32": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_p, c_sz, c_p]),
+    "nbx_gemm_f32_batched_workspace_bytes": (ctypes.c_int, [c_i32, c_p, ctypes.POINTER(c_sz)]),
+    "nbx_gemm_f32_batched": (ctypes.c_int, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_tp_prep": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "nbx_tp_prep_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p, c_p]),
     "nbx_tp_post": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),

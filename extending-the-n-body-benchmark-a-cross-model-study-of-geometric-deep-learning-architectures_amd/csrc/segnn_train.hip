@@ -45,13 +45,14 @@ struct GemmArgs {
     float beta;
 };
 
+// one 64 x 64 output tile (bx, by) of K split bz of nz (the body of gemm_f32_kernel and of the
+// grouped gemm_f32_batched_kernel)
 template <bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
-    __shared__ float As[2][GK][GB + 4];
-    __shared__ float Bs[2][GK][GB + 4];
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int nz, float (&As)[2][GK][GB + 4],
+                                          float (&Bs)[2][GK][GB + 4]) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t m0 = (int64_t)blockIdx.y * GB, n0 = (int64_t)blockIdx.x * GB;
-    const int64_t k_lo = (int64_t)blockIdx.z * g.kchunk;
+    const int64_t m0 = (int64_t)by * GB, n0 = (int64_t)bx * GB;
+    const int64_t k_lo = (int64_t)bz * g.kchunk;
     const int64_t k_hi = std::min<int64_t>(g.K, k_lo + g.kchunk);
     const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
     float ra[2][4], rb[2][4];
@@ -110,8 +111,8 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
     // 32x32 accumulator: register i -> row 8 (i / 4) + 4 (lane / 32) + i % 4, column lane % 32
     const int64_t col = n0 + wn + (lane & 31);
     if (col >= g.N) return;
-    const bool split = gridDim.z > 1;
-    float* out = split ? g.part + (int64_t)blockIdx.z * g.M * g.N : g.C;
+    const bool split = nz > 1;
+    float* out = split ? g.part + (int64_t)bz * g.M * g.N : g.C;
     const int64_t ld = split ? g.N : g.ldc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -120,6 +121,74 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
         float* p = out + row * ld + col;
         *p = (!split && g.beta != 0.f) ? acc[i] + g.beta * *p : acc[i];
     }
+}
+
+template <bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
+    __shared__ float As[2][GK][GB + 4];
+    __shared__ float Bs[2][GK][GB + 4];
+    gemm_tile<TA, TB, VEC>(g, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.z, As, Bs);
+}
+
+// Up to GMAXP independent GEMMs in one launch (a tensor product's scalar-row and vector-plane GEMMs,
+// its four backward GEMMs): block b belongs to the problem whose block range holds it; the operand
+// orders (TA, TB) and the float4 path are per problem (block-uniform branches).
+constexpr int GMAXP = 4;
+struct GemmBatch {
+    GemmArgs g[GMAXP];
+    int mode[GMAXP];      // bit 0 TA, bit 1 TB, bit 2 VEC
+    int tx[GMAXP], ty[GMAXP], nz[GMAXP];
+    int first[GMAXP + 1];
+    int count;
+};
+
+__global__ __launch_bounds__(GT) void gemm_f32_batched_kernel(GemmBatch b) {
+    __shared__ float As[2][GK][GB + 4];
+    __shared__ float Bs[2][GK][GB + 4];
+    const int blk = (int)blockIdx.x;
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < GMAXP; ++i)
+        if (i < b.count && blk >= b.first[i]) p = i;
+    const int local = blk - b.first[p], txy = b.tx[p] * b.ty[p];
+    const int bz = local / txy, r = local - bz * txy, by = r / b.tx[p], bx = r - by * b.tx[p];
+    const GemmArgs& g = b.g[p];
+    switch (b.mode[p]) {
+        case 0: gemm_tile<false, false, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 1: gemm_tile<true, false, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 2: gemm_tile<false, true, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 3: gemm_tile<true, true, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 4: gemm_tile<false, false, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 5: gemm_tile<true, false, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 6: gemm_tile<false, true, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        default: gemm_tile<true, true, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
+    }
+}
+
+// the split-K sums of every split problem of a batch in one launch (z order, as gemm_reduce_kernel)
+struct ReduceBatch {
+    const float* part[GMAXP];
+    float* C[GMAXP];
+    int64_t M[GMAXP], N[GMAXP], ldc[GMAXP];
+    int splits[GMAXP];
+    float beta[GMAXP];
+    int64_t first[GMAXP + 1];   // first element of each problem in the flattened index
+    int count;
+};
+
+__global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= b.first[b.count]) return;
+    int p = 0;
+#pragma unroll
+    for (int q = 1; q < GMAXP; ++q)
+        if (q < b.count && i >= b.first[q]) p = q;
+    const int64_t e = i - b.first[p], N = b.N[p], MN = b.M[p] * N;
+    const int64_t r = e / N, c = e - r * N;
+    float s = 0.f;
+    for (int z = 0; z < b.splits[p]; ++z) s += b.part[p][(int64_t)z * MN + e];
+    float* q = b.C[p] + r * b.ldc[p] + c;
+    *q = b.beta[p] != 0.f ? s + b.beta[p] * *q : s;
 }
 
 __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, int64_t M, int64_t N,
@@ -571,6 +640,76 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,
                            N, C, ldc, beta);
         NBX_LAUNCH_CHECK("gemm_reduce");
+    }
+    return NBX_OK;
+}
+
+extern "C" int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes) {
+    NBX_CHECK_ARG(bytes != nullptr && dims != nullptr && count >= 1 && count <= GMAXP,
+                  "nbx_gemm_f32_batched_workspace_bytes: bad arguments (count 1..%d)", GMAXP);
+    size_t n = 0;
+    for (int i = 0; i < count; ++i) {
+        const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
+        NBX_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_batched_workspace_bytes: negative size");
+        const int s = gemm_splits(M, N, K);
+        if (s > 1) n += ((size_t)s * M * N + 63) / 64 * 64;
+    }
+    *bytes = n * sizeof(float);
+    return NBX_OK;
+}
+
+extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
+                                    const float* const* B, float* const* C, const float* beta, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+    NBX_CHECK_ARG(count >= 1 && count <= GMAXP && flags && dims && A && B && C && beta,
+                  "nbx_gemm_f32_batched: bad arguments (count 1..%d)", GMAXP);
+    GemmBatch gb;
+    memset(&gb, 0, sizeof(gb));
+    ReduceBatch rb;
+    memset(&rb, 0, sizeof(rb));
+    int blocks = 0, nred = 0;
+    size_t ws_off = 0;
+    for (int i = 0; i < count; ++i) {
+        const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
+        const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
+        const bool ta = flags[i] & NBX_GEMM_TRANS_A, tb = flags[i] & NBX_GEMM_TRANS_B;
+        NBX_CHECK_ARG(M > 0 && N > 0 && K >= 0, "nbx_gemm_f32_batched: problem %d: sizes must be positive", i);
+        NBX_CHECK_ARG(beta[i] == 0.f || beta[i] == 1.f, "nbx_gemm_f32_batched: beta must be 0 or 1");
+        NBX_CHECK_ARG(A[i] && B[i] && C[i], "nbx_gemm_f32_batched: null operand");
+        NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N,
+                      "nbx_gemm_f32_batched: leading dimension too small");
+        const int splits = gemm_splits(M, N, K);
+        float* part = nullptr;
+        if (splits > 1) {
+            const size_t need = ((size_t)splits * M * N + 63) / 64 * 64;
+            NBX_CHECK_ARG(workspace && (ws_off + need) * sizeof(float) <= workspace_bytes,
+                          "nbx_gemm_f32_batched: workspace too small");
+            part = (float*)workspace + ws_off;
+            ws_off += need;
+            rb.part[nred] = part; rb.C[nred] = C[i]; rb.M[nred] = M; rb.N[nred] = N; rb.ldc[nred] = ldc;
+            rb.splits[nred] = splits; rb.beta[nred] = beta[i]; rb.first[nred + 1] = rb.first[nred] + M * N;
+            ++nred;
+        }
+        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i]};
+        g.kchunk = (g.kchunk + GK - 1) / GK * GK;
+        const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+        gb.g[i] = g;
+        gb.mode[i] = (ta ? 1 : 0) | (tb ? 2 : 0) | (vec ? 4 : 0);
+        gb.tx[i] = (int)((N + GB - 1) / GB);
+        gb.ty[i] = (int)((M + GB - 1) / GB);
+        gb.nz[i] = splits;
+        gb.first[i] = blocks;
+        blocks += gb.tx[i] * gb.ty[i] * splits;
+        gb.first[i + 1] = blocks;
+    }
+    gb.count = count;
+    rb.count = nred;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(gemm_f32_batched_kernel, dim3((unsigned)blocks), dim3(GT), 0, st, gb);
+    NBX_LAUNCH_CHECK("gemm_f32_batched");
+    if (nred) {
+        hipLaunchKernelGGL(gemm_reduce_batched_kernel, dim3(nblk(rb.first[nred])), dim3(256), 0, st, rb);
+        NBX_LAUNCH_CHECK("gemm_reduce_batched");
     }
     return NBX_OK;
 }

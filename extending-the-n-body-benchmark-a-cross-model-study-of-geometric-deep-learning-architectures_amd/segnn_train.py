@@ -66,6 +66,33 @@ def gemm(flags, M, N, K, A, lda, B, ldb, C, ldc, beta=0.0):
     return C
 
 
+def gemm_batched(problems):
+    """Up to 4 independent GEMMs ``(flags, M, N, K, A, lda, B, ldb, C, ldc, beta)`` in one launch
+    (nbx_gemm_f32_batched: each result bit-identical to nbx_gemm_f32).  Returns the C tensors."""
+    problems = [p for p in problems if p[1] > 0 and p[2] > 0]
+    if not problems:
+        return []
+    L = _lib.lib()
+    n = len(problems)
+    flags = (ctypes.c_int32 * n)(*[int(p[0]) for p in problems])
+    dims = (ctypes.c_int64 * (6 * n))(*[int(v) for p in problems for v in (p[1], p[2], p[3], p[5], p[7], p[9])])
+    ptr = lambda i: (ctypes.c_void_p * n)(*[_dp(p[i]) for p in problems])
+    beta = (ctypes.c_float * n)(*[float(p[10]) for p in problems])
+    nb = _lib.c_sz()
+    _lib.check(L.nbx_gemm_f32_batched_workspace_bytes(n, dims, ctypes.byref(nb)), "nbx_gemm_f32_batched_workspace_bytes")
+    C = problems[0][8]
+    ws = _ws(nb.value, C.device) if nb.value else None
+    if gemm_timer is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    _lib.check(L.nbx_gemm_f32_batched(n, flags, dims, ptr(4), ptr(6), ptr(8), beta, _dp(ws), nb.value, _st(C)),
+               "nbx_gemm_f32_batched")
+    if gemm_timer is not None:
+        ev[1].record()
+        gemm_timer.append((ev[0], ev[1], sum(2.0 * p[1] * p[2] * p[3] for p in problems)))
+    return [p[8] for p in problems]
+
+
 def colsum(X, rows, cols, ld, out, accumulate=False):
     L = _lib.lib()
     n = _lib.c_sz()
@@ -91,11 +118,11 @@ class _TPFn(torch.autograd.Function):
         S = torch.empty(rows, Ks + Kv, device=dev, dtype=_f32)
         _lib.check(L.nbx_tp_prep(rows, Ks, Kv, _dp(XS), Ks, _dp(XV), _dp(Y3), _dp(S), _st(S)), "nbx_tp_prep")
         Zs = torch.empty(rows, nsc + Nt, device=dev, dtype=_f32)
-        gemm(_lib.GEMM_TRANS_B, rows, nsc + Nt, Ks + Kv, S, Ks + Kv, Ws, Ks + Kv, Zs, nsc + Nt)
         Zv = torch.empty(3, rows, Nt, device=dev, dtype=_f32)
-        if Kv:
-            gemm(_lib.GEMM_TRANS_B, 3 * rows, Nt, Kv, XV, Kv, Wv, Kv, Zv, Nt)
-        else:
+        # the scalar-row and the vector-plane GEMM in one launch
+        gemm_batched([(_lib.GEMM_TRANS_B, rows, nsc + Nt, Ks + Kv, S, Ks + Kv, Ws, Ks + Kv, Zs, nsc + Nt, 0.0)] +
+                     ([(_lib.GEMM_TRANS_B, 3 * rows, Nt, Kv, XV, Kv, Wv, Kv, Zv, Nt, 0.0)] if Kv else []))
+        if not Kv:
             Zv.zero_()
         OS = torch.empty(rows, Ms, device=dev, dtype=_f32)
         OV = torch.empty(3, rows, Nt, device=dev, dtype=_f32)
@@ -120,20 +147,26 @@ class _TPFn(torch.autograd.Function):
         dbias = None
         if bias is not None and ctx.needs_input_grad[5]:
             dbias = colsum(dZs, rows, nsc, nsc + Nt, torch.empty(nsc, device=dev, dtype=_f32))
-        dWs = dWv = None
+        # the (up to) four backward GEMMs -- weight gradients and input gradients -- in one launch
+        probs = []
+        dWs = dWv = dS = None
         if ctx.needs_input_grad[3]:
-            dWs = gemm(_lib.GEMM_TRANS_A, nsc + Nt, Ks + Kv, rows, dZs, nsc + Nt, S, Ks + Kv,
-                       torch.empty(nsc + Nt, Ks + Kv, device=dev, dtype=_f32), Ks + Kv)
+            dWs = torch.empty(nsc + Nt, Ks + Kv, device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A, nsc + Nt, Ks + Kv, rows, dZs, nsc + Nt, S, Ks + Kv, dWs, Ks + Kv, 0.0))
         if Kv and ctx.needs_input_grad[4]:
-            dWv = gemm(_lib.GEMM_TRANS_A, Nt, Kv, 3 * rows, dZv, Nt, XV, Kv,
-                       torch.empty(Nt, Kv, device=dev, dtype=_f32), Kv)
+            dWv = torch.empty(Nt, Kv, device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A, Nt, Kv, 3 * rows, dZv, Nt, XV, Kv, dWv, Kv, 0.0))
         dXS = dXV = None
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            dS = gemm(0, rows, Ks + Kv, nsc + Nt, dZs, nsc + Nt, Ws, Ks + Kv,
-                      torch.empty(rows, Ks + Kv, device=dev, dtype=_f32), Ks + Kv)
+        need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        if need_x:
+            dS = torch.empty(rows, Ks + Kv, device=dev, dtype=_f32)
+            probs.append((0, rows, Ks + Kv, nsc + Nt, dZs, nsc + Nt, Ws, Ks + Kv, dS, Ks + Kv, 0.0))
             dXS = torch.empty(rows, Ks, device=dev, dtype=_f32)
             if Kv:
-                dXV = gemm(0, 3 * rows, Kv, Nt, dZv, Nt, Wv, Kv, torch.empty(3, rows, Kv, device=dev, dtype=_f32), Kv)
+                dXV = torch.empty(3, rows, Kv, device=dev, dtype=_f32)
+                probs.append((0, 3 * rows, Kv, Nt, dZv, Nt, Wv, Kv, dXV, Kv, 0.0))
+        gemm_batched(probs)
+        if need_x:
             _lib.check(L.nbx_tp_prep_backward(rows, Ks, Kv, _dp(dS), _dp(Y3), _dp(dXS), Ks, _dp(dXV), _st(dS)),
                        "nbx_tp_prep_backward")
         return (dXS, dXV, None, dWs, dWv, dbias, dOS if has_rs else None, dOV if has_rv else None, None, None, None)

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 11
+#define NBX_ABI_VERSION 12
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -283,6 +283,15 @@ int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, co
 #define NBX_GEMM_TRANS_A 1
 #define NBX_GEMM_TRANS_B 2
 int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes);
+/* ABI 12.  Up to 4 independent nbx_gemm_f32 problems in one launch (plus one launch for every split-K
+ * sum): problem i has flags[i], dims[6 i ..] = (M, N, K, lda, ldb, ldc), A[i], B[i], C[i], beta[i]
+ * (0 or 1), each with the operand layouts, blocking and split-K order of nbx_gemm_f32, so its result
+ * is bit-identical.  Host arrays; workspace from nbx_gemm_f32_batched_workspace_bytes.  Replaces the
+ * separate launches of one tensor product's GEMMs in the training step (segnn_train.py). */
+int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes);
+int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
+                         const float* const* B, float* const* C, const float* beta, void* workspace,
+                         size_t workspace_bytes, void* stream);
 int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
                  int64_t ldb, float* C, int64_t ldc, float beta, void* workspace, size_t workspace_bytes, void* stream);
 
