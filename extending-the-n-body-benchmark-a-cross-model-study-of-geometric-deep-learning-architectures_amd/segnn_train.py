@@ -285,6 +285,52 @@ class _SegSumFn(torch.autograd.Function):
         return dXe, None, None, None, None
 
 
+class _MsgInputFn(torch.autograd.Function):
+    """message_layer_1's per-edge input without concatenation kernels: x[dst] and x[src] gathered
+    straight into the column slices of one buffer, plus a constant tail (amf).  hs [V][M] ->
+    [E][2M + T] = [hs[dst] | hs[src] | tail]; hv [3][V][M] -> [3][E][2M] = [hv[dst] | hv[src]].
+    Backward: two segment sums per input (over the destination / source CSR), the second
+    accumulating, read from the column slices of the contiguous output gradient."""
+
+    @staticmethod
+    def forward(ctx, hs, hv, tail, g):
+        L = _lib.lib()
+        V, M = hs.shape
+        E, T = g.E, tail.shape[1]
+        st = _st(hs)
+        S = torch.empty(E, 2 * M + T, device=hs.device, dtype=_f32)
+        Vv = torch.empty(3, E, 2 * M, device=hs.device, dtype=_f32)
+        for j, idx in enumerate((g.dst, g.src)):
+            _lib.check(L.nbx_gather_rows(E, M, _dp(idx), _dp(hs), M, V * M, _dp(S[:, j * M:]), 2 * M + T, 0, 1, st),
+                       "nbx_gather_rows")
+            _lib.check(L.nbx_gather_rows(E, M, _dp(idx), _dp(hv), M, V * M, _dp(Vv[:, :, j * M:]), 2 * M, E * 2 * M, 3,
+                                         st), "nbx_gather_rows")
+        S[:, 2 * M:].copy_(tail)
+        ctx.g, ctx.dims = g, (V, M, T)
+        return S, Vv
+
+    @staticmethod
+    def backward(ctx, dS, dVv):
+        L = _lib.lib()
+        g = ctx.g
+        V, M, T = ctx.dims
+        E = g.E
+        dhs = dhv = None
+        if dS is not None:
+            dS = dS.contiguous()
+            dhs = torch.empty(V, M, device=dS.device, dtype=_f32)
+            for j, (ptr, eid) in enumerate(((g.dptr, g.deid), (g.sptr, g.seid))):
+                _lib.check(L.nbx_segment_sum(V, M, _dp(ptr), _dp(eid), _dp(dS[:, j * M:]), 2 * M + T, 0, _dp(dhs), M,
+                                             V * M, 1, j, _st(dS)), "nbx_segment_sum")
+        if dVv is not None:
+            dVv = dVv.contiguous()
+            dhv = torch.empty(3, V, M, device=dVv.device, dtype=_f32)
+            for j, (ptr, eid) in enumerate(((g.dptr, g.deid), (g.sptr, g.seid))):
+                _lib.check(L.nbx_segment_sum(V, M, _dp(ptr), _dp(eid), _dp(dVv[:, :, j * M:]), 2 * M, E * 2 * M,
+                                             _dp(dhv), M, V * M, 3, j, _st(dVv)), "nbx_segment_sum")
+        return dhs, dhv, None, None
+
+
 def featurize(pos, vel, mass, g: Graph):
     """O3Transform + catch_isolated_nodes (no gradient): na3 [V][3], xs0 [V][1], xv0 [3][V][2],
     rhat [E][3], amf [E][2]."""
@@ -338,12 +384,8 @@ def train_forward(model, pos, vel, mass, edge_index):
     for li, layer in enumerate(model.layers):
         p = f"layers.{li}."
         # message(x_i = x[dst], x_j = x[src], additional features) -> two gated TPs -> message BatchNorm
-        xd = _GatherFn.apply(hs, g.dst, g.dptr, g.deid)
-        xs = _GatherFn.apply(hs, g.src, g.sptr, g.seid)
-        vd = _GatherFn.apply(hv, g.dst, g.dptr, g.deid)
-        vs = _GatherFn.apply(hv, g.src, g.sptr, g.seid)
-        ms, mv = tp(torch.cat([xd, xs, amf], 1), torch.cat([vd, vs], 2), rhat, W[p + "msg1_s"], W[p + "msg1_v"],
-                    W[p + "msg1_bias"], M, M, 1)
+        xin, vin = _MsgInputFn.apply(hs.contiguous(), hv.contiguous(), amf, g)   # [x_i | x_j | amf], [v_i | v_j]
+        ms, mv = tp(xin, vin, rhat, W[p + "msg1_s"], W[p + "msg1_v"], W[p + "msg1_bias"], M, M, 1)
         ms, mv = tp(ms, mv, rhat, W[p + "msg2_s"], W[p + "msg2_v"], W[p + "msg2_bias"], M, M, 1)
         ms, mv = _batch_norm(model, layer.message_norm, ms, mv, batch_stats)
         # aggr="add" at edge_index[1]
