@@ -36,6 +36,12 @@ def _dp(t):
     return _lib.dev_ptr(t) if t is not None else None
 
 
+def _at(t, offset):
+    """Device pointer of element `offset` of the contiguous fp32 tensor t (column slices passed to the
+    strided operators with their own leading dimension)."""
+    return _lib.dev_ptr(t) + 4 * int(offset)
+
+
 def _st(t):
     return _lib.stream_ptr(t.device)
 
@@ -301,9 +307,9 @@ class _MsgInputFn(torch.autograd.Function):
         S = torch.empty(E, 2 * M + T, device=hs.device, dtype=_f32)
         Vv = torch.empty(3, E, 2 * M, device=hs.device, dtype=_f32)
         for j, idx in enumerate((g.dst, g.src)):
-            _lib.check(L.nbx_gather_rows(E, M, _dp(idx), _dp(hs), M, V * M, _dp(S[:, j * M:]), 2 * M + T, 0, 1, st),
+            _lib.check(L.nbx_gather_rows(E, M, _dp(idx), _dp(hs), M, V * M, _at(S, j * M), 2 * M + T, 0, 1, st),
                        "nbx_gather_rows")
-            _lib.check(L.nbx_gather_rows(E, M, _dp(idx), _dp(hv), M, V * M, _dp(Vv[:, :, j * M:]), 2 * M, E * 2 * M, 3,
+            _lib.check(L.nbx_gather_rows(E, M, _dp(idx), _dp(hv), M, V * M, _at(Vv, j * M), 2 * M, E * 2 * M, 3,
                                          st), "nbx_gather_rows")
         S[:, 2 * M:].copy_(tail)
         ctx.g, ctx.dims = g, (V, M, T)
@@ -320,13 +326,13 @@ class _MsgInputFn(torch.autograd.Function):
             dS = dS.contiguous()
             dhs = torch.empty(V, M, device=dS.device, dtype=_f32)
             for j, (ptr, eid) in enumerate(((g.dptr, g.deid), (g.sptr, g.seid))):
-                _lib.check(L.nbx_segment_sum(V, M, _dp(ptr), _dp(eid), _dp(dS[:, j * M:]), 2 * M + T, 0, _dp(dhs), M,
+                _lib.check(L.nbx_segment_sum(V, M, _dp(ptr), _dp(eid), _at(dS, j * M), 2 * M + T, 0, _dp(dhs), M,
                                              V * M, 1, j, _st(dS)), "nbx_segment_sum")
         if dVv is not None:
             dVv = dVv.contiguous()
             dhv = torch.empty(3, V, M, device=dVv.device, dtype=_f32)
             for j, (ptr, eid) in enumerate(((g.dptr, g.deid), (g.sptr, g.seid))):
-                _lib.check(L.nbx_segment_sum(V, M, _dp(ptr), _dp(eid), _dp(dVv[:, :, j * M:]), 2 * M, E * 2 * M,
+                _lib.check(L.nbx_segment_sum(V, M, _dp(ptr), _dp(eid), _at(dVv, j * M), 2 * M, E * 2 * M,
                                              _dp(dhv), M, V * M, 3, j, _st(dVv)), "nbx_segment_sum")
         return dhs, dhv, None, None
 
