@@ -668,10 +668,12 @@ def bench_segnn_train(a, rank, world, device, P):
                    "seq_len": a.steps, "parallelism": f"dp{world}",
                    "execution": "one HIP graph replay per step (forward, backward, clip, fused AdamW)" if graph
                                 else "eager"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_f32_kernel (nbx_gemm_f32: every tensor-product GEMM of the "
-                                               "forward and backward)",
+        "roofline": {"bound": "mfma", "kernel": "gemm_f32_batched_kernel (nbx_gemm_f32_batched: every tensor-product "
+                                               "GEMM of the forward and backward, grouped per tensor product)",
                      "achieved": round(ach, 3) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None, "traffic": None,
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None,
+                     "traffic": pmc_traffic("(anonymous namespace)::gemm_f32_batched_kernel((anonymous namespace)::"
+                                            "GemmBatch)", "segnn_train"),
                      "avg_launch_us": round(1e3 * gemm_ms / max(n_gemm, 1), 3), "launches_per_step": n_gemm,
                      "gflop_per_step": round(gemm_flops / 1e9, 4),
                      "timing": "torch.cuda.Event pairs around every GEMM launch of one eager step, launch stream",

@@ -1138,9 +1138,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
-            // split form (upd_vec.h): the 1o GEMM of all channels, then the 0e GEMM + gate
-            // (NBX_UPD1_SPLIT=0: the combined kernel, A/B only)
-            static const bool upd1_split = !getenv("NBX_UPD1_SPLIT") || atoi(getenv("NBX_UPD1_SPLIT")) != 0;
+            // split form (upd_vec.h; NBX_UPD1_SPLIT=1, A/B only): the 1o GEMM of all channels, then the
+            // 0e GEMM + gate.  Measured r04 (profiles/r04/segnn_upd1_split_summary.md): 10.8 + 15.0 us
+            // against 22.7-24 us for the combined kernel -- the second launch's staging and fill / drain
+            // cost more than the VALU the split saves, so the combined kernel stays the default
+            static const bool upd1_split = getenv("NBX_UPD1_SPLIT") && atoi(getenv("NBX_UPD1_SPLIT")) != 0;
             if (M == 96 && L.upd1_img_x3 && x3_enabled() && upd1_split) {
                 const int kc_s = (4 * M + 31) / 32, kc_t = (2 * M + 31) / 32, kc_v = (2 * M + 31) / 32;
                 const int stride = (2 * kc_s + kc_t + kc_v) * 768;   // floats per bf16x3 chunk image

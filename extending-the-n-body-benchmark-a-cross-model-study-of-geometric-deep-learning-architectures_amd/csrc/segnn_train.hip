@@ -344,19 +344,17 @@ __global__ void tp_post_bwd_kernel(TpPost p) {
 // the block's CS_ROWS in fp64 and the 4 wave sums are added in a fixed order through LDS.  Small row
 // blocks keep many blocks in flight at the training batch (320-1280 rows): the first version's
 // 256-row serial loop per thread ran 10 blocks and took ~60 us per call.
-constexpr int CS_ROWS = 32;
+constexpr int CS_ROWS = 32;   // rows per partial block at the training batch (more rows: cs_rows)
 __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t rows, int cols, const float* __restrict__ X,
-                                                             int64_t ld, double* __restrict__ part) {
+                                                             int64_t ld, int rpb, double* __restrict__ part) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.y * 64 + lane;
-    const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
+    const int64_t r0 = (int64_t)blockIdx.x * rpb;
     double s = 0.0;
     if (c < cols) {
-#pragma unroll
-        for (int i = w; i < CS_ROWS; i += 4) {
-            const int64_t r = r0 + i;
-            if (r < rows) s += (double)X[r * ld + c];
-        }
+        const int64_t r1 = std::min<int64_t>(rows, r0 + rpb);
+#pragma unroll 4
+        for (int64_t r = r0 + w; r < r1; r += 4) s += (double)X[r * ld + c];
     }
     __shared__ double red[4][64];
     red[w][lane] = s;
@@ -365,14 +363,30 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t rows, int c
         part[(int64_t)blockIdx.x * cols + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-__global__ void colsum_final_kernel(int nb, int cols, const double* __restrict__ part, float* __restrict__ out,
-                                    int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cols) return;
+// rows per partial block: CS_ROWS, or more once that would give over 256 partial rows (large
+// operands, e.g. PONITA's edge-orientation rows), so the final pass stays short
+int cs_rows(int64_t rows) {
+    const int64_t r = std::max<int64_t>(CS_ROWS, (rows + 255) / 256);
+    return (int)((r + 3) / 4 * 4);
+}
+
+// the partial rows summed in a fixed order: 4 waves x 64 columns, wave w takes partials w, w + 4, ...
+__global__ __launch_bounds__(256) void colsum_final_kernel(int nb, int cols, const double* __restrict__ part,
+                                                           float* __restrict__ out, int accumulate) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     double s = 0.0;
-#pragma unroll 8
-    for (int b = 0; b < nb; ++b) s += part[(int64_t)b * cols + c];
-    out[c] = accumulate ? out[c] + (float)s : (float)s;
+    if (c < cols) {
+#pragma unroll 4
+        for (int b = w; b < nb; b += 4) s += part[(int64_t)b * cols + c];
+    }
+    __shared__ double red[4][64];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && c < cols) {
+        const double t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        out[c] = accumulate ? out[c] + (float)t : (float)t;
+    }
 }
 
 // ---------------------------------------------------------------- e3nn BatchNorm, batch statistics
@@ -761,7 +775,8 @@ extern "C" int nbx_tp_post_backward(int64_t rows, int32_t Ms, int32_t Nt, int32_
 
 extern "C" int nbx_colsum_workspace_bytes(int64_t rows, int32_t cols, size_t* bytes) {
     NBX_CHECK_ARG(bytes && rows >= 0 && cols >= 0, "nbx_colsum_workspace_bytes: bad arguments");
-    *bytes = (size_t)std::max<int64_t>(1, (rows + CS_ROWS - 1) / CS_ROWS) * cols * sizeof(double);
+    const int rpb = cs_rows(rows);
+    *bytes = (size_t)std::max<int64_t>(1, (rows + rpb - 1) / rpb) * cols * sizeof(double);
     return NBX_OK;
 }
 
@@ -769,7 +784,8 @@ extern "C" int nbx_colsum(int64_t rows, int32_t cols, const float* X, int64_t ld
                           void* workspace, size_t workspace_bytes, void* stream) {
     NBX_CHECK_ARG(rows >= 0 && cols >= 0 && ld >= cols, "nbx_colsum: bad sizes");
     if (cols == 0) return NBX_OK;
-    const int nb = (int)std::max<int64_t>(1, (rows + CS_ROWS - 1) / CS_ROWS);
+    const int rpb = cs_rows(rows);
+    const int nb = (int)std::max<int64_t>(1, (rows + rpb - 1) / rpb);
     NBX_CHECK_ARG(workspace && workspace_bytes >= (size_t)nb * cols * sizeof(double), "nbx_colsum: workspace too small");
     hipStream_t st = (hipStream_t)stream;
     double* part = (double*)workspace;
@@ -777,10 +793,11 @@ extern "C" int nbx_colsum(int64_t rows, int32_t cols, const float* X, int64_t ld
         NBX_HIP(hipMemsetAsync(part, 0, (size_t)cols * sizeof(double), st));
     } else {
         hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)nb, (unsigned)((cols + 63) / 64)), dim3(256), 0, st,
-                           rows, cols, X, ld, part);
+                           rows, cols, X, ld, rpb, part);
         NBX_LAUNCH_CHECK("colsum_partial");
     }
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(nblk(cols)), dim3(256), 0, st, nb, cols, part, out, accumulate);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0, st, nb, cols, part, out,
+                       accumulate);
     NBX_LAUNCH_CHECK("colsum_final");
     return NBX_OK;
 }

@@ -28,7 +28,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .segnn_train import Graph, colsum, gemm, _dp, _st, _ws
+from .segnn_train import Graph, colsum, gemm, gemm_batched, _dp, _st, _ws
 
 _f32 = torch.float32
 
@@ -68,13 +68,15 @@ class _LinFn(torch.autograd.Function):
         db = dW = dX = None
         if b is not None and ctx.needs_input_grad[2]:
             db = colsum(dZ, rows, N, N, torch.empty(N, device=dev, dtype=_f32))
+        probs = []   # the weight and the input gradient GEMMs in one launch (nbx_gemm_f32_batched)
         if ctx.needs_input_grad[1]:
-            dW = gemm(_lib.GEMM_TRANS_A, N, K, rows, dZ, N, X, ldx, torch.empty(N, K, device=dev, dtype=_f32), K)
+            dW = torch.empty(N, K, device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A, N, K, rows, dZ, N, X, ldx, dW, K, 0.0))
         if ctx.needs_input_grad[0]:
-            dX = torch.zeros(rows, ldx, device=dev, dtype=_f32) if ldx != K else None
-            out = dX if dX is not None else torch.empty(rows, K, device=dev, dtype=_f32)
-            gemm(0, rows, K, N, dZ, N, W, K, out, ldx)
-            dX = out
+            dX = torch.zeros(rows, ldx, device=dev, dtype=_f32) if ldx != K else torch.empty(rows, K, device=dev,
+                                                                                              dtype=_f32)
+            probs.append((0, rows, K, N, dZ, N, W, K, dX, ldx, 0.0))
+        gemm_batched(probs)
         return dX, dW, db, None, None
 
 
