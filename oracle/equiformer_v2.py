@@ -21,7 +21,7 @@ Follows (all under models/equiformer_v2/architecture/):
   SmoothLeakyReLU                               activation.py:62-202
 * torch_geometric.utils.softmax                 segment softmax over edge_index[1] (+1e-16)
 
-Supported: lmax_list = [lmax <= 2], one resolution, use_atom_edge_embedding and not shared,
+Supported: lmax_list = [lmax <= 6] (e3nn_so3.LMAX_SUPPORTED), one resolution, use_atom_edge_embedding and not shared,
 use_m_share_rad False, distance_function "projection", use_sep_s2_act (the C4 configuration).
 ``p`` maps the reference state-dict keys to float64 tensors.
 """
@@ -115,9 +115,10 @@ def so3_linear(p, key, x, lmax):
 def rms_norm_sh(p, key, x, lmax, eps=1e-5):
     """EquivariantRMSNormArraySphericalHarmonicsV2 (centering, std_balance_degrees)."""
     x = torch.cat([x[:, :1] - x[:, :1].mean(-1, keepdim=True), x[:, 1:]], 1)
-    # balance_degree_weight is a float32 buffer (torch.zeros in the default dtype), cast with the model
-    bal = torch.tensor([1.0 / (2 * l + 1) / (lmax + 1) for l in range(lmax + 1) for _ in range(2 * l + 1)],
-                       dtype=torch.float32).to(x.dtype)
+    # balance_degree_weight is a float32 buffer (torch.zeros in the default dtype): 1 / (2l + 1) rounded to
+    # float32, then divided by lmax + 1 in float32 (layer_norm.py:370-378), cast with the model
+    bal = (torch.tensor([1.0 / (2 * l + 1) for l in range(lmax + 1) for _ in range(2 * l + 1)], dtype=torch.float32)
+           / (lmax + 1)).to(x.dtype)
     nrm = torch.einsum("nic,i->nc", x * x, bal).mean(-1)
     s = (nrm + eps) ** -0.5
     lidx = torch.tensor([l for l in range(lmax + 1) for _ in range(2 * l + 1)])

@@ -82,3 +82,58 @@ def test_rotation_conventions():
         lhs = E.sh_component(l, torch.einsum("nij,kj->nki", R, u))
         rhs = torch.einsum("nij,kj->nki", D, E.sh_component(l, u))
         assert torch.allclose(lhs, rhs, atol=1e-13)
+
+
+# ---------------------------------------------------------------- lmax > 2 (reference default degrees)
+Z6 = np.load(os.path.join(HERE, "golden", "eqv2_l6.npz"))
+STATE6 = json.load(open(os.path.join(HERE, "golden", "eqv2_l6_state.json")))
+
+
+def params6(tag):
+    return {k: torch.from_numpy(param_value(k, STATE6[tag]["keys"][k])).float().double()
+            for k in STATE6[tag]["params"]}
+
+
+def test_wigner_l6_matches_reference_jd():
+    """The closed-form harmonics' Wigner-D (oracle/e3nn_so3.py, any l <= 6) equals the reference's
+    Jd.pt-based wigner_D (SO3_Rotation(6).set_wigner) block by block."""
+    R = torch.from_numpy(Z6["wigner6/rot"])
+    D = torch.from_numpy(Z6["wigner6/D"])
+    np.testing.assert_allclose(EQ.wigner(R, 6).numpy(), D.numpy(), rtol=0, atol=1e-12)
+
+
+def test_general_harmonics_reduce_to_the_explicit_ones():
+    u = torch.nn.functional.normalize(torch.randn(40, 3, dtype=torch.float64), dim=-1)
+    for l in range(3):
+        np.testing.assert_allclose(E.sh_general(l, u).numpy(), E.sh_component(l, u).numpy(), rtol=0, atol=1e-14)
+
+
+def test_grid_round_trip_exact_l6():
+    for lmax in range(3, 7):
+        rb, ra = 2 * (lmax + 1), 2 * (lmax + 1) + 1
+        to, fr = E.ToS2Grid(lmax, (rb, ra), dtype=torch.float64), E.FromS2Grid((rb, ra), lmax, dtype=torch.float64)
+        tm = torch.einsum("mbi,am->bai", to.shb, to.sha)
+        fm = torch.einsum("am,mbi->bai", fr.sha, fr.shb)
+        np.testing.assert_allclose(torch.einsum("bai,bak->ik", fm, tm).numpy(), np.eye((lmax + 1) ** 2), atol=1e-12)
+
+
+def test_grid_matrices_l6_match_reference_construction():
+    for l in range(7):
+        for m in range(l + 1):
+            to, fr = EQ.grid_mats(l, m)
+            np.testing.assert_allclose(to.numpy(), Z6[f"grid/{l}{m}/to"], rtol=0, atol=1e-14)
+            np.testing.assert_allclose(fr.numpy(), Z6[f"grid/{l}{m}/from"], rtol=0, atol=1e-14)
+
+
+@pytest.mark.parametrize("tag", ["l6", "l4"])
+def test_forward_lmax_gt2_matches_reference(tag):
+    """The oracle at the reference's default degrees (lmax 6, mmax 2) and at lmax 4 / mmax 3 equals the
+    reference model's own float64 forward (tests/golden/make_eqv2_l6.py)."""
+    cfg = STATE6[tag]["config"]
+    loc, vel, mass = Z6[f"{tag}/loc"], Z6[f"{tag}/vel"], Z6[f"{tag}/mass"]
+    B, N = loc.shape[:2]
+    acts = {}
+    pred = EQ.forward(cfg, params6(tag), loc, vel, mass, B, N, Z6[f"{tag}/gauge"], acts=acts)
+    np.testing.assert_allclose(pred.numpy(), Z6[f"{tag}/f64/pred"], rtol=1e-9, atol=1e-10)
+    for k in ("edge_degree", "block0", "final_norm"):
+        np.testing.assert_allclose(acts[k].numpy(), Z6[f"{tag}/f64/{k}"], rtol=1e-9, atol=1e-10)
