@@ -853,9 +853,11 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             const int PR = std::max(1, std::min(O, (int)(fk_lds / ((size_t)O * C * 4))));
             const int R = (O + PR - 1) / PR;
             const int npi = PO_FIB_THREADS / (C / 4);
-            // NBX_PO_FIB_BLOCKS: total workgroups over all ranges (A/B; the ranges of one node group sit on
-            // the same XCD since gx % 8 == 0, so co-resident ranges share X1 through that XCD's L2)
-            static const int fib_blocks = getenv("NBX_PO_FIB_BLOCKS") ? atoi(getenv("NBX_PO_FIB_BLOCKS")) : 1024;
+            // NBX_PO_FIB_BLOCKS: total workgroups over all ranges (the ranges of one node group sit on the
+            // same XCD since gx % 8 == 0, so co-resident ranges share X1 through that XCD's L2).  Measured
+            // (profiles/r04/ponita_fib_ab): 1024 -> 181 us / 989 MB, 512 -> 169 us / 762 MB, 256 -> 261 us /
+            // 610 MB per launch; fewer groups re-read less but 256 no longer fills the chip
+            static const int fib_blocks = getenv("NBX_PO_FIB_BLOCKS") ? atoi(getenv("NBX_PO_FIB_BLOCKS")) : 512;
             const int gx = (int)std::min<int64_t>((d.V + npi - 1) / npi, std::max(1, fib_blocks / R));
             const size_t lds = (size_t)O * PR * C * 4;
             auto kern = O <= 20 ? po_fiber_ln_kernel<20, 4> : po_fiber_ln_kernel<PO_OMAX, 2>;
