@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 12
+ABI_VERSION = 13
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B = 1, 2
@@ -159,6 +159,13 @@ _SIGNATURES = {
     "nbx_segment_softmax_backward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
     "nbx_eqv2_rms_norm": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "nbx_eqv2_rms_norm_backward": (ctypes.c_int, [c_i64, c_i32] + [c_p] * 7),
+    "nbx_eqv2_edges": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, ctypes.c_uint64, c_i64, c_i32, c_p, c_p, c_p, c_p]),
+    "nbx_eqv2_wigner_table_floats": (ctypes.c_int, [c_i32, ctypes.POINTER(c_i64)]),
+    "nbx_eqv2_dsel_floats": (ctypes.c_int, [c_i32, c_i32, ctypes.POINTER(c_i64)]),
+    "nbx_eqv2_wigner": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
+    "nbx_eqv2_rotate_general": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p]),
+    "nbx_eqv2_rms_norm_general": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "nbx_eqv2_rms_norm_general_backward": (ctypes.c_int, [c_i64, c_i32, c_i32] + [c_p] * 7),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),
     "nbx_segnn_forward": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_p,
                                          c_p, c_sz, c_p]),

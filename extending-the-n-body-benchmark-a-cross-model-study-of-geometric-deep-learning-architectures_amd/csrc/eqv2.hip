@@ -933,6 +933,8 @@ __global__ void eqv2_dsel_kernel(int64_t E, const float* __restrict__ rot, float
     const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (e >= E) return;
     const float* r = rot + e * ROT;
+    dist[e] = r[24];
+    if (!dsel) return;                                // nbx_eqv2_edges: frames and distances only
     float* d = dsel + e * 63;
 #pragma unroll
     for (int i = 0; i < 63; ++i) d[i] = 0.f;
@@ -945,7 +947,6 @@ __global__ void eqv2_dsel_kernel(int64_t E, const float* __restrict__ rot, float
     for (int a = 0; a < 3; ++a)
 #pragma unroll
         for (int b = 0; b < 5; ++b) d[(4 + a) * 9 + 4 + b] = r[9 + 5 * a + b];
-    dist[e] = r[24];
 }
 
 }  // namespace
@@ -1036,5 +1037,20 @@ extern "C" int nbx_eqv2_train_edges(int64_t B, int64_t N, const float* pos, cons
     NBX_LAUNCH_CHECK("eqv2 train edge");
     hipLaunchKernelGGL(eqv2_dsel_kernel, dim3(g1(E)), dim3(256), 0, st, E, rot_scratch, dsel, dist);
     NBX_LAUNCH_CHECK("eqv2 dsel");
+    return NBX_OK;
+}
+
+extern "C" int nbx_eqv2_edges(int64_t B, int64_t N, const float* pos, const float* mass, const float* gauge,
+                              uint64_t seed, int64_t frame, int32_t num_elements, float* rot_scratch, float* dist,
+                              int32_t* zn, void* stream) {
+    NBX_CHECK_ARG(B >= 1 && N >= 2 && num_elements >= 1 && frame >= 0, "nbx_eqv2_edges: bad sizes");
+    NBX_CHECK_ARG(pos && mass && rot_scratch && dist && zn, "nbx_eqv2_edges: null operand");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t V = B * N, E = V * (N - 1);
+    hipLaunchKernelGGL(eqv2_edge_kernel, dim3(g1(std::max(V, E))), dim3(256), 0, st, pos, mass, gauge, seed,
+                       (uint64_t)frame, V, (int)N, num_elements, rot_scratch, zn);
+    NBX_LAUNCH_CHECK("eqv2 edges");
+    hipLaunchKernelGGL(eqv2_dsel_kernel, dim3(g1(E)), dim3(256), 0, st, E, rot_scratch, nullptr, dist);
+    NBX_LAUNCH_CHECK("eqv2 edge distances");
     return NBX_OK;
 }

@@ -69,17 +69,21 @@ __global__ void eqv2_rotate_kernel(int64_t E, int C, const float* __restrict__ D
 }
 
 // ---------------------------------------------------------------- separable S2 activation (grid part)
-// out[r][i][h] = sum_p F[p][i] SiLU(sum_j T[p][j] x[r][j][h]) for the I <= 9 coefficients of a row and
-// P <= 64 grid points; backward dx[r][j][h] = sum_p T[p][j] SiLU'(t_p) sum_i F[p][i] dout[r][i][h].
-constexpr int S2_MAXI = 9, S2_MAXP = 64;
+// out[r][i][h] = sum_p F[p][i] SiLU(sum_j T[p][j] x[r][j][h]) for the I coefficients of a row and P
+// grid points; backward dx[r][j][h] = sum_p T[p][j] SiLU'(t_p) sum_i F[p][i] dout[r][i][h].  T and F
+// sit in LDS (2 P I floats: 82 KB at lmax 6, SO3_Grid(6, 6) = 14 x 15 points); a thread keeps one
+// (row, channel)'s coefficients in registers (MAXI = 9 up to lmax 2, 49 up to lmax 6).
+constexpr int S2_MAXI = 49, S2_MAXP = 256;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-template <bool BWD>
+template <int MAXI, bool BWD>
 __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P, int H, const float* __restrict__ T,
                                                       const float* __restrict__ F, const float* __restrict__ X,
                                                       const float* __restrict__ dOut, float* __restrict__ out) {
-    __shared__ float sT[S2_MAXP * S2_MAXI], sF[S2_MAXP * S2_MAXI];
+    extern __shared__ float s2_lds[];
+    float* sT = s2_lds;
+    float* sF = s2_lds + P * I;
     for (int k = threadIdx.x; k < P * I; k += blockDim.x) {
         sT[k] = T[k];
         sF[k] = F[k];
@@ -90,9 +94,9 @@ __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P
     const int64_t r = g / H;
     const int h = (int)(g - r * H);
     const int64_t base = r * I * H + h;
-    float x[S2_MAXI], d[S2_MAXI], o[S2_MAXI];
+    float x[MAXI], d[MAXI], o[MAXI];
 #pragma unroll
-    for (int i = 0; i < S2_MAXI; ++i) {
+    for (int i = 0; i < MAXI; ++i) {
         x[i] = i < I ? X[base + (int64_t)i * H] : 0.f;
         d[i] = (BWD && i < I) ? dOut[base + (int64_t)i * H] : 0.f;
         o[i] = 0.f;
@@ -102,28 +106,39 @@ __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P
         const float* fp = sF + p * I;
         float t = 0.f;
 #pragma unroll
-        for (int i = 0; i < S2_MAXI; ++i)
+        for (int i = 0; i < MAXI; ++i)
             if (i < I) t += tp[i] * x[i];
         const float s = sigm(t);
         if (!BWD) {
             const float a = t * s;
 #pragma unroll
-            for (int i = 0; i < S2_MAXI; ++i)
+            for (int i = 0; i < MAXI; ++i)
                 if (i < I) o[i] += fp[i] * a;
         } else {
             float gsum = 0.f;
 #pragma unroll
-            for (int i = 0; i < S2_MAXI; ++i)
+            for (int i = 0; i < MAXI; ++i)
                 if (i < I) gsum += fp[i] * d[i];
             const float dt = gsum * (s + t * s * (1.0f - s));
 #pragma unroll
-            for (int i = 0; i < S2_MAXI; ++i)
+            for (int i = 0; i < MAXI; ++i)
                 if (i < I) o[i] += tp[i] * dt;
         }
     }
 #pragma unroll
-    for (int i = 0; i < S2_MAXI; ++i)
+    for (int i = 0; i < MAXI; ++i)
         if (i < I) out[base + (int64_t)i * H] = o[i];
+}
+
+template <bool BWD>
+int s2_launch(int64_t rows, int I, int P, int H, const float* T, const float* F, const float* X, const float* dOut,
+              float* out, hipStream_t st) {
+    const size_t lds = 2 * (size_t)P * I * sizeof(float);
+    auto kern = I <= 9 ? eqv2_s2_kernel<9, BWD> : eqv2_s2_kernel<S2_MAXI, BWD>;
+    if (lds > 64 * 1024)
+        NBX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3(nblk(rows * H)), dim3(256), lds, st, rows, I, P, H, T, F, X, dOut, out);
+    return NBX_OK;
 }
 
 // ---------------------------------------------------------------- segment softmax over edge_index[1]
@@ -305,8 +320,7 @@ extern "C" int nbx_eqv2_s2_act(int64_t rows, int32_t I, int32_t P, int32_t H, co
     NBX_CHECK_ARG(rows >= 0 && I >= 1 && I <= S2_MAXI && P >= 1 && P <= S2_MAXP && H >= 1,
                   "nbx_eqv2_s2_act: need I <= %d coefficients, P <= %d grid points", S2_MAXI, S2_MAXP);
     if (rows == 0) return NBX_OK;
-    hipLaunchKernelGGL(eqv2_s2_kernel<false>, dim3(nblk(rows * H)), dim3(256), 0, (hipStream_t)stream, rows, I, P, H,
-                       to_grid, from_grid, X, nullptr, out);
+    if (int rc = s2_launch<false>(rows, I, P, H, to_grid, from_grid, X, nullptr, out, (hipStream_t)stream)) return rc;
     NBX_LAUNCH_CHECK("eqv2_s2_act");
     return NBX_OK;
 }
@@ -317,8 +331,7 @@ extern "C" int nbx_eqv2_s2_act_backward(int64_t rows, int32_t I, int32_t P, int3
     NBX_CHECK_ARG(rows >= 0 && I >= 1 && I <= S2_MAXI && P >= 1 && P <= S2_MAXP && H >= 1,
                   "nbx_eqv2_s2_act_backward: need I <= %d coefficients, P <= %d grid points", S2_MAXI, S2_MAXP);
     if (rows == 0) return NBX_OK;
-    hipLaunchKernelGGL(eqv2_s2_kernel<true>, dim3(nblk(rows * H)), dim3(256), 0, (hipStream_t)stream, rows, I, P, H,
-                       to_grid, from_grid, X, dOut, dX);
+    if (int rc = s2_launch<true>(rows, I, P, H, to_grid, from_grid, X, dOut, dX, (hipStream_t)stream)) return rc;
     NBX_LAUNCH_CHECK("eqv2_s2_act_backward");
     return NBX_OK;
 }

@@ -222,8 +222,9 @@ class _EdgeDegreeEmbedding(nn.Module):
 # ----------------------------------------------------------------------------- the model
 class EquiformerV2_nbody(nn.Module):
     """EquiformerV2_nbody (equiformer_v2_nbody.py:57-389): constructor arguments and defaults of the
-    reference; the native forward covers its C4 / inference configurations (include/nbx.h,
-    EquiformerV2 section)."""
+    reference; the fused forward covers its C4 / inference configurations (include/nbx.h,
+    EquiformerV2 section), the composed one (eqv2_train.py) every single-resolution lmax <= 6
+    including the constructor default lmax 6 / mmax 2."""
 
     def __init__(self, device=None, use_pbc=False, regress_forces=True, otf_graph=True, max_neighbors=5,
                  max_radius=4096, max_num_elements=90, num_layers=12, attn_hidden_channels=128, sphere_channels=128,
@@ -267,8 +268,26 @@ class EquiformerV2_nbody(nn.Module):
         if num_layers > _lib.EQV2_MAX_LAYERS:
             reasons.append(f"num_layers <= {_lib.EQV2_MAX_LAYERS}")
         self._native_reason = ("native EquiformerV2 needs " + "; ".join(reasons)) if reasons else None
-        if reasons and (max(lmax_list) > so3.LMAX or len(lmax_list) != 1):
-            raise NotImplementedError(self._native_reason)
+        # the composed path (eqv2_train.py on the general-degree operators, csrc/eqv2_general.hip) runs
+        # every single-resolution lmax <= 6 with the reference's default module choices
+        general = []
+        if len(lmax_list) != 1 or len(mmax_list) != 1:
+            general.append("one resolution (len(lmax_list) == 1)")
+        elif not 0 <= mmax_list[0] <= lmax_list[0] <= so3.LMAX:
+            general.append(f"0 <= mmax <= lmax <= {so3.LMAX}")
+        if norm_type != "rms_norm_sh" or distance_function != "projection" or grid_resolution is not None:
+            general.append('norm_type "rms_norm_sh", distance_function "projection", default grid resolution')
+        if (not use_atom_edge_embedding or share_atom_edge_embedding or use_m_share_rad or use_s2_act_attn
+                or use_gate_act or use_grid_mlp or not use_sep_s2_act or not use_attn_renorm):
+            general.append("per-module atom edge embeddings, separable S2 activations, attention re-norm")
+        if edge_channels > 1024 or attn_alpha_channels > 1024:
+            general.append("edge / alpha channels <= 1024")
+        self._general_reason = ("EquiformerV2 needs " + "; ".join(general)) if general else None
+        if self._general_reason:
+            raise NotImplementedError(self._general_reason)
+        self.layout = so3.Layout(lmax_list[0], mmax_list[0])
+        self.force_general_ops = False    # route even lmax 2 / mmax 1 through the general operators (tests)
+        self._wtab = None
 
         C, He = sphere_channels, edge_channels
         self.num_resolutions = len(self.lmax_list)
@@ -465,6 +484,27 @@ class EquiformerV2_nbody(nn.Module):
             self._ws = torch.empty(n.value, dtype=torch.uint8, device=device)
         return self._ws
 
+    def uses_general_ops(self):
+        """True when the composed path runs on the general-degree operators (nbx_eqv2_wigner /
+        rotate_general / rms_norm_general) instead of the lmax 2 / mmax 1 ones."""
+        return ((self.layout.lmax, self.layout.mmax) != (2, 1) or self.sphere_channels > 128
+                or bool(self.force_general_ops))
+
+    def wigner_table(self, device):
+        """so3.wigner_table(lmax) on ``device`` (the probe constants of nbx_eqv2_wigner), cached."""
+        if self._wtab is None or self._wtab.device != device:
+            n = _lib.c_i64()
+            _lib.check(_lib.lib().nbx_eqv2_wigner_table_floats(self.layout.lmax, n), "nbx_eqv2_wigner_table_floats")
+            t = so3.wigner_table(self.layout.lmax)
+            if n.value and t.numel() != n.value:
+                raise RuntimeError("EquiformerV2: Wigner table size disagrees with the library")
+            self._wtab = t.to(device)
+        return self._wtab
+
+    def _composed(self, p, vv, q, B, N, g, seed, frame=0):
+        from . import eqv2_train
+        return eqv2_train.train_forward(self, p, vv, q, B, N, g, seed, frame)
+
     # ------------------------------------------------------------ forward
     def forward(self, data, batch=None, gauge=None):
         """equiformer_v2_nbody.py:392-575 -> [B*N, 6] (delta pos | vel)."""
@@ -494,11 +534,14 @@ class EquiformerV2_nbody(nn.Module):
         seed = (int(self.gauge_seed) * 0x100000001B3 + self._calls) & 0xFFFFFFFFFFFFFFFF
         if use_training_path(self):   # train_dispatch.py: autograd on + trainable params
             # training step: native operators under autograd (eqv2_train.py)
-            if self._native_reason:
-                raise NotImplementedError(self._native_reason)
-            from . import eqv2_train
             self._calls += 1
-            return eqv2_train.train_forward(self, p, vv, q, B, N, g, seed).to(pos.dtype)
+            return self._composed(p, vv, q, B, N, g, seed).to(pos.dtype)
+        if self._native_reason:
+            # no fused kernels for this configuration (e.g. the reference default lmax 6 / mmax 2):
+            # the same native operators, composed, without autograd
+            self._calls += 1
+            with torch.no_grad():
+                return self._composed(p, vv, q, B, N, g, seed).to(pos.dtype)
         out = torch.empty(V, 6, device=device, dtype=torch.float32)
         W = self._weights(device)
         ws = self._workspace(W, B, N, device)
@@ -518,6 +561,19 @@ class EquiformerV2_nbody(nn.Module):
         p, v, m = f(loc), f(vel), f(mass.reshape(B * N))
         tp = torch.empty(B, num_frames, N, 3, device=device, dtype=torch.float32)
         tv = torch.empty_like(tp)
+        if self._native_reason:
+            # composed path: frame f draws its gauges from (seed, f - 1) as nbx_eqv2_rollout does
+            if seed is None:
+                seed = (int(self.gauge_seed) * 0x100000001B3 + self._calls) & 0xFFFFFFFFFFFFFFFF
+                self._calls += 1
+            tp[:, 0], tv[:, 0] = p, v
+            p, v = p.reshape(B * N, 3), v.reshape(B * N, 3)
+            for f in range(1, num_frames):
+                pred = self._composed(p, v, m, B, N, None, int(seed), f - 1)
+                p = pred[:, :3].contiguous() if absolute else p + pred[:, :3]
+                v = pred[:, 3:].contiguous()
+                tp[:, f], tv[:, f] = p.view(B, N, 3), v.view(B, N, 3)
+            return tp, tv
         W = self._weights(device)
         ws = self._workspace(W, B, N, device)
         if seed is None:

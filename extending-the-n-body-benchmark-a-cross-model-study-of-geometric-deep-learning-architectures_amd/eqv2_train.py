@@ -3,21 +3,25 @@
 The reference trains EquiformerV2_nbody with ``pred = model(data); loss.backward();
 optimizer.step()`` (trainer.py:233-358).  Here a grad-mode ``EquiformerV2_nbody.forward``
 (equiformer_v2.py) runs :func:`train_forward`: the forward of
-models/equiformer_v2/architecture/equiformer_v2_nbody.py:428-575 (lmax 2, mmax 1, separable S2
-activations, rms_norm_sh) composed of libnbx operators inside ``torch.autograd.Function`` s whose
+models/equiformer_v2/architecture/equiformer_v2_nbody.py:428-575 (any single resolution lmax <= 6,
+separable S2 activations, rms_norm_sh) composed of libnbx operators inside ``torch.autograd.Function`` s whose
 backward passes call the same library, so ``loss.backward()`` reaches every ``nn.Parameter`` the
 reference's forward uses:
 
 * every nn.Linear / SO3_LinearV2 degree / SO(2) ``fc`` = ``ponita_train._LinFn`` (nbx_gemm_f32 +
   nbx_bias_act), every LayerNorm = ``_LayerNormFn``, SiLU / SmoothLeakyReLU = ``_ActFn``;
-* SO3_Rotation.rotate / rotate_inv = ``_RotateFn`` (nbx_eqv2_rotate; adjoint pair);
+* SO3_Rotation.rotate / rotate_inv = ``_RotateFn`` (nbx_eqv2_rotate, lmax 2 / mmax 1) or
+  ``_RotateGFn`` (nbx_eqv2_rotate_general with the nbx_eqv2_wigner rows, any lmax <= 6); adjoint pairs;
 * the separable S2 activation's grid round trip = ``_S2Fn`` (nbx_eqv2_s2_act);
 * the attention softmax over edge_index[1] = ``_SoftmaxFn`` (nbx_segment_softmax);
-* EquivariantRMSNormArraySphericalHarmonicsV2 = ``_RMSNormFn`` (nbx_eqv2_rms_norm);
+* EquivariantRMSNormArraySphericalHarmonicsV2 = ``_RMSNormFn`` (nbx_eqv2_rms_norm, lmax 2) or
+  ``_RMSNormGFn`` (nbx_eqv2_rms_norm_general);
 * gathers x[edge_index[0 / 1]], embedding lookups and the aggregation = ``segnn_train._GatherFn`` /
   ``_SegSumFn`` over CSR tables (no atomics).
 
-Edge frames come from ``nbx_eqv2_train_edges`` (the inference path's frames and gauge draws).
+Edge frames come from ``nbx_eqv2_train_edges`` / ``nbx_eqv2_edges`` (the inference path's frames and
+gauge draws).  Without autograd the same composition is the inference forward of the configurations
+the fused kernels do not cover (EquiformerV2_nbody.forward / rollout).
 Reshapes, concatenations, the SO(2) complex combine, the radial weighting of the messages and the
 dropout masks (alpha dropout, GraphDropPath: transformer_block.py:342-343,686-706, drop.py:51-68,
 train mode, torch's RNG) are torch glue.  Arithmetic is fp32 (a float64 module is cast for the step).
@@ -26,17 +30,12 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, so3
 from .ponita_train import _LayerNormFn, linear
 from .segnn_train import Graph, _GatherFn, _SegSumFn, _dp, _st, colsum
 
 _f32 = torch.float32
 AVG_DEGREE = 23.395238876342773          # equiformer_v2_nbody.py:36
-# reduced (|m| <= 1) coefficients, l-primary: (0,0) (1,-1) (1,0) (1,1) (2,-1) (2,0) (2,1); m-primary
-# order of SO2_Convolution (so3.py:30-115 CoefficientMappingModule): m = 0 (l = 0, 1, 2), m = +1
-# (l = 1, 2), m = -1 (l = 1, 2)
-M_PRIMARY = [0, 2, 5, 3, 6, 1, 4]
-L_PRIMARY = [M_PRIMARY.index(i) for i in range(7)]
 
 
 class _ActFn(torch.autograd.Function):
@@ -89,6 +88,34 @@ class _RotateFn(torch.autograd.Function):
         _lib.check(_lib.lib().nbx_eqv2_rotate(E, C, _dp(D), _dp(dY), dY.shape[1] * C, _dp(dX), 1 - inverse, rescale,
                                               _st(dY)), "nbx_eqv2_rotate")
         return dX, None, None, None
+
+
+class _RotateGFn(torch.autograd.Function):
+    """General degrees: rotate (inverse = 0) [E][(lmax+1)^2][C] -> [E][R][C], rotate_inv (inverse = 1)
+    [E][R][C] -> [E][(lmax+1)^2][C] with the kept Wigner rows D [E][S]."""
+
+    @staticmethod
+    def forward(ctx, X, D, lay, inverse, rescale):
+        E, _, C = X.shape
+        X = X.contiguous()
+        out = torch.empty(E, lay.n_full if inverse else lay.n_red, C, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rotate_general(E, C, lay.lmax, lay.mmax, _dp(D), _dp(X), X.shape[1] * C,
+                                                      _dp(out), inverse, rescale, _st(X)), "nbx_eqv2_rotate_general")
+        ctx.save_for_backward(D)
+        ctx.mode = (lay, inverse, rescale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dY):
+        (D,) = ctx.saved_tensors
+        lay, inverse, rescale = ctx.mode
+        dY = dY.contiguous()
+        E, _, C = dY.shape
+        dX = torch.empty(E, lay.n_red if inverse else lay.n_full, C, device=dY.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rotate_general(E, C, lay.lmax, lay.mmax, _dp(D), _dp(dY), dY.shape[1] * C,
+                                                      _dp(dX), 1 - inverse, rescale, _st(dY)),
+                   "nbx_eqv2_rotate_general")
+        return dX, None, None, None, None
 
 
 class _S2Fn(torch.autograd.Function):
@@ -163,6 +190,34 @@ class _RMSNormFn(torch.autograd.Function):
         return dX, dwb[:3 * C].view(3, C), dwb[3 * C:], None
 
 
+class _RMSNormGFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, w, b, eps, lmax):
+        X = X.contiguous()
+        V, _, C = X.shape
+        Y = torch.empty_like(X)
+        save = torch.empty(2, V, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rms_norm_general(V, lmax, C, _dp(X), _dp(w), _dp(b), float(eps), _dp(Y),
+                                                        _dp(save), _st(X)), "nbx_eqv2_rms_norm_general")
+        ctx.save_for_backward(X, w, save)
+        ctx.lmax = lmax
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        X, w, save = ctx.saved_tensors
+        V, _, C = X.shape
+        L1 = ctx.lmax + 1
+        dY = dY.contiguous()
+        dX = torch.empty_like(X)
+        G = torch.empty(V, (L1 + 1) * C, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rms_norm_general_backward(V, ctx.lmax, C, _dp(X), _dp(w), _dp(save), _dp(dY),
+                                                                 _dp(dX), _dp(G), _st(dX)),
+                   "nbx_eqv2_rms_norm_general_backward")
+        dwb = colsum(G, V, (L1 + 1) * C, (L1 + 1) * C, torch.empty((L1 + 1) * C, device=X.device, dtype=_f32))
+        return dX, dwb[:L1 * C].view(L1, C), dwb[L1 * C:], None, None
+
+
 def _f(t):
     return t.to(_f32).contiguous()
 
@@ -181,18 +236,31 @@ def gather(X, idx_graph, which):
 class _Step:
     """Per-forward state: the graph, edge frames, distance expansion and dropout settings."""
 
-    def __init__(self, model, pos, vel, charges, B, N, gauge, seed):
+    def __init__(self, model, pos, vel, charges, B, N, gauge, seed, frame=0):
         dev = pos.device
         self.m, self.B, self.N = model, B, N
         V, E = B * N, B * N * (N - 1)
         self.V, self.E = V, E
+        lay = self.lay = model.layout
+        self.general = model.uses_general_ops()
         rot = torch.empty(max(E, 1), 32, device=dev, dtype=_f32)
-        self.D = torch.empty(max(E, 1), 7, 9, device=dev, dtype=_f32)
         dist = torch.empty(max(E, 1), device=dev, dtype=_f32)
         zn = torch.empty(V, device=dev, dtype=torch.int32)
-        _lib.check(_lib.lib().nbx_eqv2_train_edges(B, N, _dp(pos), _dp(charges), _dp(gauge), seed,
-                                                   model.max_num_elements, _dp(rot), _dp(self.D), _dp(dist), _dp(zn),
-                                                   _st(pos)), "nbx_eqv2_train_edges")
+        if self.general:
+            self.D = torch.empty(max(E, 1), lay.dsel_floats, device=dev, dtype=_f32)
+            _lib.check(_lib.lib().nbx_eqv2_edges(B, N, _dp(pos), _dp(charges), _dp(gauge), seed, frame,
+                                                 model.max_num_elements, _dp(rot), _dp(dist), _dp(zn), _st(pos)),
+                       "nbx_eqv2_edges")
+            _lib.check(_lib.lib().nbx_eqv2_wigner(E, lay.lmax, lay.mmax, _dp(rot), 32,
+                                                  _dp(model.wigner_table(dev)), _dp(self.D), _st(pos)),
+                       "nbx_eqv2_wigner")
+        else:
+            if frame:
+                raise ValueError("frame > 0 needs the general operators")
+            self.D = torch.empty(max(E, 1), 7, 9, device=dev, dtype=_f32)
+            _lib.check(_lib.lib().nbx_eqv2_train_edges(B, N, _dp(pos), _dp(charges), _dp(gauge), seed,
+                                                       model.max_num_elements, _dp(rot), _dp(self.D), _dp(dist),
+                                                       _dp(zn), _st(pos)), "nbx_eqv2_train_edges")
         from .graph import fc_edge_index
         self.g = Graph(fc_edge_index(B, N, dev), V, dev)
         zl = zn.long()
@@ -202,9 +270,24 @@ class _Step:
         self.dexp = linear(dist[:E, None], model.distance_expansion.weight, model.distance_expansion.bias)
         self.training = model.training
         self.batch = torch.arange(B, device=dev).repeat_interleave(N)
-        ga, gf = model.SO3_grid[2][1], model.SO3_grid[2][2]
-        self.grid_attn = (_f(ga.to_grid_mat.reshape(-1, 7)), _f(ga.from_grid_mat.reshape(-1, 7)))
-        self.grid_ffn = (_f(gf.to_grid_mat.reshape(-1, 9)), _f(gf.from_grid_mat.reshape(-1, 9)))
+        ga, gf = model.SO3_grid[lay.lmax][lay.mmax], model.SO3_grid[lay.lmax][lay.lmax]
+        nr, nf = lay.n_red, lay.n_full
+        self.grid_attn = (_f(ga.to_grid_mat.reshape(-1, nr)), _f(ga.from_grid_mat.reshape(-1, nr)))
+        self.grid_ffn = (_f(gf.to_grid_mat.reshape(-1, nf)), _f(gf.from_grid_mat.reshape(-1, nf)))
+        dev_idx = lambda v: torch.tensor(v, device=dev, dtype=torch.long)
+        self.perm, self.inv_perm, self.m0 = dev_idx(lay.perm), dev_idx(lay.inv_perm), dev_idx(lay.m0)
+
+    def rotate(self, x):
+        """SO3_Rotation.rotate (so3.py:485-505): [E][(lmax+1)^2][C] -> the kept rows [E][R][C]."""
+        if self.general:
+            return _RotateGFn.apply(x, self.D, self.lay, 0, 0)
+        return _RotateFn.apply(x, self.D, 0, 0)
+
+    def rotate_inv(self, y):
+        """SO3_Rotation.rotate_inv with get_rotate_inv_rescale (so3.py:507-531)."""
+        if self.general:
+            return _RotateGFn.apply(y, self.D, self.lay, 1, 1)
+        return _RotateFn.apply(y, self.D, 1, 1)
 
     # ---------------------------------------------------------------- building blocks
     def x_edge(self, mod):
@@ -223,35 +306,44 @@ class _Step:
         return linear(h, net[6].weight, net[6].bias)
 
     def so2_conv(self, conv, x, x_edge, cout, n_extra=0):
-        """SO2_Convolution (so2_ops.py:78-156) of x [E][7][cin] (l-primary) -> ([E][7][cout], extra)."""
+        """SO2_Convolution (so2_ops.py:78-156) of x [E][R][cin] (kept coefficients, l-primary) ->
+        ([E][R][cout], extra): m-primary order (CoefficientMappingModule), the m = 0 block through
+        fc_m0, every m > 0 pair (+m, -m) through its SO2_m_Convolution as a complex product."""
         E, _, cin = x.shape
-        xm = x[:, M_PRIMARY]
+        lay = self.lay
+        xm = x[:, self.perm]
         rad = self.rad_func(conv.rad_func, x_edge) if x_edge is not None else None
-        x0 = xm[:, :3].reshape(E, 3 * cin)
+        n0 = lay.m_size[0]
+        x0 = xm[:, :n0].reshape(E, n0 * cin)
         if rad is not None:
-            x0 = x0 * rad[:, :3 * cin]
+            x0 = x0 * rad[:, :n0 * cin]
         y0 = linear(x0, conv.fc_m0.weight, conv.fc_m0.bias)
-        extra, y0 = y0[:, :n_extra], y0[:, n_extra:].reshape(E, 3, cout)
-        x1 = xm[:, 3:7].reshape(E, 2, 2 * cin)
-        if rad is not None:
-            x1 = x1 * rad[:, None, 3 * cin:5 * cin]
-        y = linear(x1.reshape(2 * E, 2 * cin), conv.so2_m_conv[0].fc.weight).view(E, 2, 4 * cout)
-        xr, xi = y[..., :2 * cout], y[..., 2 * cout:]
-        y1 = torch.stack([xr[:, 0] - xi[:, 1], xr[:, 1] + xi[:, 0]], 1).reshape(E, 4, cout)
-        return torch.cat([y0, y1], 1)[:, L_PRIMARY], extra
+        extra, y0 = y0[:, :n_extra], y0[:, n_extra:].reshape(E, n0, cout)
+        outs, off, roff = [y0], n0, n0 * cin
+        for m in range(1, lay.mmax + 1):
+            nm = lay.m_size[m]
+            xmm = xm[:, off:off + 2 * nm].reshape(E, 2, nm * cin)
+            if rad is not None:
+                xmm = xmm * rad[:, None, roff:roff + nm * cin]
+            y = linear(xmm.reshape(2 * E, nm * cin), conv.so2_m_conv[m - 1].fc.weight).view(E, 2, 2 * nm * cout)
+            xr, xi = y[..., :nm * cout], y[..., nm * cout:]
+            outs.append(torch.stack([xr[:, 0] - xi[:, 1], xr[:, 1] + xi[:, 0]], 1).reshape(E, 2 * nm, cout))
+            off, roff = off + 2 * nm, roff + nm * cin
+        return torch.cat(outs, 1)[:, self.inv_perm], extra
 
-    @staticmethod
-    def so3_linear(lin, x):
-        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][9][cin]."""
+    def so3_linear(self, lin, x):
+        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin]."""
         V, _, cin = x.shape
         W = lin.weight
-        y0 = linear(x[:, 0], W[0], lin.bias).view(V, 1, -1)
-        y1 = linear(x[:, 1:4].reshape(3 * V, cin), W[1]).view(V, 3, -1)
-        y2 = linear(x[:, 4:9].reshape(5 * V, cin), W[2]).view(V, 5, -1)
-        return torch.cat([y0, y1, y2], 1)
+        ys = [linear(x[:, 0], W[0], lin.bias).view(V, 1, -1)]
+        for l in range(1, self.lay.lmax + 1):
+            n = 2 * l + 1
+            ys.append(linear(x[:, l * l:l * l + n].reshape(n * V, cin), W[l]).view(V, n, -1))
+        return torch.cat(ys, 1)
 
-    @staticmethod
-    def rms_norm(norm, x):
+    def rms_norm(self, norm, x):
+        if self.general:
+            return _RMSNormGFn.apply(x, _f(norm.affine_weight), _f(norm.affine_bias), norm.eps, self.lay.lmax)
         return _RMSNormFn.apply(x, _f(norm.affine_weight), _f(norm.affine_bias), norm.eps)
 
     def drop_path(self, x):
@@ -279,7 +371,7 @@ class _Step:
         nh, na, nv, H = m.num_heads, m.attn_alpha_channels, m.attn_value_channels, m.attn_hidden_channels
         x_edge = self.x_edge(A)
         xs, xd = gather(x, g, "s"), gather(x, g, "d")
-        msg = _RotateFn.apply(torch.cat([xs, xd], 2), self.D, 0, 0)
+        msg = self.rotate(torch.cat([xs, xd], 2))
         msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
         gating, a_in = extra[:, nh * na:], extra[:, :nh * na]
         msg = torch.cat([act(gating.contiguous(), _lib.ACT_SILU)[:, None],
@@ -292,13 +384,14 @@ class _Step:
         alpha = _SoftmaxFn.apply(logit, g)
         if self.training and A.alpha_drop > 0.0:   # the module's own rate: the force block's is 0
             alpha = torch.nn.functional.dropout(alpha, A.alpha_drop, True)    # (equiformer_v2_nbody.py:362)
-        msg = (msg.view(E, 7, nh, nv) * alpha[:, None, :, None]).reshape(E, 7, nh * nv)
-        rot = _RotateFn.apply(msg, self.D, 1, 1)
-        agg = _SegSumFn.apply(rot.reshape(E, 9 * nh * nv), g.dst, g.dptr, g.deid, V).view(V, 9, nh * nv)
+        nr, nf = self.lay.n_red, self.lay.n_full
+        msg = (msg.view(E, nr, nh, nv) * alpha[:, None, :, None]).reshape(E, nr, nh * nv)
+        rot = self.rotate_inv(msg)
+        agg = _SegSumFn.apply(rot.reshape(E, nf * nh * nv), g.dst, g.dptr, g.deid, V).view(V, nf, nh * nv)
         return self.so3_linear(A.proj, agg)
 
     def ffn(self, F, x):
-        """FeedForwardNetwork (transformer_block.py:473-530), separable S2 activation on SO3_Grid(2, 2)."""
+        """FeedForwardNetwork (transformer_block.py:473-530), separable S2 activation on SO3_Grid(lmax, lmax)."""
         gating = linear(x[:, 0], F.gating_linear.weight, F.gating_linear.bias, _lib.ACT_SILU)
         h = self.so3_linear(F.so3_linear_1, x)
         h = torch.cat([gating[:, None], _S2Fn.apply(h, *self.grid_ffn)[:, 1:]], 1)
@@ -308,23 +401,25 @@ class _Step:
         """EdgeDegreeEmbedding (input_block.py:83-138): m = 0 radial coefficients rotated back and
         summed over the incoming edges / AVG_DEGREE."""
         ed, E, V, C = self.m.edge_degree_embedding, self.E, self.V, self.m.sphere_channels
-        r = self.rad_func(ed.rad_func, self.x_edge(ed)).view(E, 3, C)
-        z = r.new_zeros(E, 1, C)
-        red = torch.cat([r[:, 0:1], z, r[:, 1:2], z, z, r[:, 2:3], z], 1)         # m = 0 slots 0, 2, 5
-        y = _RotateFn.apply(red, self.D, 1, 1)
-        out = _SegSumFn.apply(y.reshape(E, 9 * C), self.g.dst, self.g.dptr, self.g.deid, V).view(V, 9, C)
+        lay = self.lay
+        r = self.rad_func(ed.rad_func, self.x_edge(ed)).view(E, lay.m_size[0], C)
+        red = r.new_zeros(E, lay.n_red, C).index_copy(1, self.m0, r)             # the m = 0 slots
+        y = self.rotate_inv(red)
+        out = _SegSumFn.apply(y.reshape(E, lay.n_full * C), self.g.dst, self.g.dptr, self.g.deid,
+                              V).view(V, lay.n_full, C)
         return out / AVG_DEGREE
 
 
-def train_forward(model, pos, vel, charges, B, N, gauge=None, seed=0):
+def train_forward(model, pos, vel, charges, B, N, gauge=None, seed=0, frame=0):
     """equiformer_v2_nbody.py:428-575 with autograd through the native operators.  pos / vel [V, 3],
-    charges [V] fp32 on the device; gauge [E, 3] or None (device hash of ``seed``).  Returns [V, 6]."""
+    charges [V] fp32 on the device; gauge [E, 3] or None (device hash of ``seed`` and ``frame``).
+    Returns [V, 6]."""
     m = model
-    st = _Step(m, pos, vel, charges, B, N, gauge, seed)
+    st = _Step(m, pos, vel, charges, B, N, gauge, seed, frame)
     V, C = st.V, m.sphere_channels
     x0 = gather(_f(m.sphere_embedding.weight), st.gn, "s")                               # [V][C]
     xv = linear(vel, m.velocity_embedding.weight, m.velocity_embedding.bias).view(V, 3, C)
-    x = torch.cat([x0[:, None], xv, x0.new_zeros(V, 5, C)], 1) + st.edge_degree()
+    x = torch.cat([x0[:, None], xv, x0.new_zeros(V, st.lay.n_full - 4, C)], 1) + st.edge_degree()
     for blk in m.blocks:
         y = st.proj_drop(st.drop_path(st.attention(blk.ga, st.rms_norm(blk.norm_1, x), C))) + x
         x = st.proj_drop(st.drop_path(st.ffn(blk.ffn, st.rms_norm(blk.norm_2, y)))) + y

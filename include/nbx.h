@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 12
+#define NBX_ABI_VERSION 13
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -421,7 +421,7 @@ int nbx_eqv2_rotate(int64_t E, int32_t C, const float* dsel, const float* in, in
 
 /* Separable S2 activation, grid part (activation.py:155-202): out[r][i][h] = sum_p F[p][i]
  * SiLU(sum_j T[p][j] X[r][j][h]), X / out [rows][I][H], T / F [P][I] (SO3_Grid to / from grid
- * matrices), I <= 9, P <= 64; backward dX from dOut. */
+ * matrices), I <= 49, P <= 256 (ABI 13; lmax 6: SO3_Grid(6, 6) has 14 x 15 points); backward dX from dOut. */
 int nbx_eqv2_s2_act(int64_t rows, int32_t I, int32_t P, int32_t H, const float* to_grid, const float* from_grid,
                     const float* X, float* out, void* stream);
 int nbx_eqv2_s2_act_backward(int64_t rows, int32_t I, int32_t P, int32_t H, const float* to_grid,
@@ -441,6 +441,46 @@ int nbx_eqv2_rms_norm(int64_t V, int32_t C, const float* X, const float* weight,
                       float* save, void* stream);
 int nbx_eqv2_rms_norm_backward(int64_t V, int32_t C, const float* X, const float* weight, const float* save,
                                const float* dY, float* dX, float* G, void* stream);
+
+/* ------------------------------------------------------------------------
+ * EquiformerV2 at general degrees (ABI 13; lmax <= 6, mmax <= lmax: the reference constructor's
+ * default lmax_list = [6], mmax_list = [2], equiformer_v2_nbody.py:122-123).  The composed forward
+ * and training step (eqv2_train.py) use these with the operators above.  Layout: node irreps
+ * [V][(lmax+1)^2][C] (l-primary), edge irreps [E][R][C] with the R kept (|m| <= mmax) coefficients
+ * (l-primary, coefficient_idx of so3.py:117-157), dsel [E][S]: per degree l the kept rows of D^l,
+ * [2 min(l, mmax)+1][2l+1], back to back (S from nbx_eqv2_dsel_floats).
+ */
+
+/* nbx_eqv2_train_edges without the lmax-2 rows and with the gauge counter's frame index (the draws
+ * of nbx_eqv2_rollout's frame `frame`): rot_scratch [E][32] (R, the edge frame, in floats 0..8),
+ * dist [E], zn [V]. */
+int nbx_eqv2_edges(int64_t B, int64_t N, const float* pos, const float* mass, const float* gauge, uint64_t seed,
+                   int64_t frame, int32_t num_elements, float* rot_scratch, float* dist, int32_t* zn, void* stream);
+
+/* Sizes: the probe table of nbx_eqv2_wigner (host-built: so3.py wigner_table) and S. */
+int nbx_eqv2_wigner_table_floats(int32_t lmax, int64_t* floats);
+int nbx_eqv2_dsel_floats(int32_t lmax, int32_t mmax, int64_t* floats);
+
+/* Kept Wigner rows of every edge frame (SO3_Rotation.set_wigner, so3.py:485-531; Y(R u) = D(R) Y(u)
+ * in e3nn's basis): R = rot[e * ld_rot + 0..8] (rows), D^0 = 1, D^1 = R, D^l = [Y^l(R u_k)]_k P_l from
+ * the table's probe vectors u_k and P_l = pinv([Y^l(u_k)]_k). */
+int nbx_eqv2_wigner(int64_t E, int32_t lmax, int32_t mmax, const float* rot, int64_t ld_rot, const float* table,
+                    float* dsel, void* stream);
+
+/* rotate (inverse = 0: out [E][R][C] = dsel in, in [E][(lmax+1)^2][C] with ld_in floats per edge) and
+ * rotate_inv (inverse = 1: out [E][(lmax+1)^2][C] = dsel^T in, in [E][R][C]); rescale = 1 multiplies
+ * degree l > mmax by float32(sqrt((2l+1)/(2 mmax+1))) (get_rotate_inv_rescale, so3.py:160-185), so
+ * each direction with the same rescale is the other's adjoint. */
+int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel, const float* in,
+                            int64_t ld_in, float* out, int32_t inverse, int32_t rescale, void* stream);
+
+/* EquivariantRMSNormArraySphericalHarmonicsV2 (layer_norm.py:327-441) of X [V][(lmax+1)^2][C], any C:
+ * weight [lmax+1][C], bias [C], balance weights float32(1/(2l+1)) / (lmax+1); save [2][V]; backward
+ * dX and G [V][(lmax+2) C] whose column sums are dweight [lmax+1][C] | dbias [C]. */
+int nbx_eqv2_rms_norm_general(int64_t V, int32_t lmax, int32_t C, const float* X, const float* weight,
+                              const float* bias, float eps, float* Y, float* save, void* stream);
+int nbx_eqv2_rms_norm_general_backward(int64_t V, int32_t lmax, int32_t C, const float* X, const float* weight,
+                                       const float* save, const float* dY, float* dX, float* G, void* stream);
 
 /* ------------------------------------------------------------------------
  * EGNN-MC (models/egnn_mc/egnn_mc.py:45-295 with the preprocessing of

@@ -45,6 +45,13 @@ def _rotate(X, D, inverse, rescale):
     return torch.bmm(D.transpose(1, 2) * (EQ.Layout(2, 1).rescale[None] if rescale else 1.0), X)
 
 
+def _rotate_general(X, D, lay, inverse, rescale):
+    """nbx_eqv2_rotate_general on dense kept rows D [E][R][(lmax+1)^2]."""
+    if not inverse:
+        return torch.bmm(D, X)
+    return torch.bmm(D.transpose(1, 2) * (EQ.Layout(lay.lmax, lay.mmax).rescale[None] if rescale else 1.0), X)
+
+
 def _s2(X, Tm, Fm):
     t = torch.einsum("pi,zic->zpc", Tm, X)
     return torch.einsum("pi,zpc->zic", Fm, t * torch.sigmoid(t))
@@ -70,13 +77,20 @@ def torch_ops(monkeypatch):
     monkeypatch.setattr(T, "_SoftmaxFn", _fn(_softmax))
     monkeypatch.setattr(T, "_RMSNormFn", _fn(lambda X, w, b, eps: EQ.rms_norm_sh(
         {"n.affine_weight": w, "n.affine_bias": b}, "n", X, 2, eps)))
+    monkeypatch.setattr(T, "_RotateGFn", _fn(_rotate_general))
+    monkeypatch.setattr(T, "_RMSNormGFn", _fn(lambda X, w, b, eps, lmax: EQ.rms_norm_sh(
+        {"n.affine_weight": w, "n.affine_bias": b}, "n", X, lmax, eps)))
     monkeypatch.setattr(T, "_SegSumFn", _fn(lambda X, idx, p, e, V: torch.zeros(V, X.shape[1], dtype=X.dtype)
                                              .index_add(0, idx.long(), X)))
 
-    def step_init(self, model, pos, vel, charges, B, N, gauge, seed):
+    def step_init(self, model, pos, vel, charges, B, N, gauge, seed, frame=0):
         self.m, self.B, self.N, self.V, self.E = model, B, N, B * N, B * N * (N - 1)
-        ctx = EQ.Ctx(CFG, dict(model.state_dict()), pos, vel, charges, B, N, gauge)
-        self.D = ctx.D[:, EQ.Layout(2, 1).sel, :]
+        lay = self.lay = model.layout
+        self.general = model.uses_general_ops()
+        cfg = dict(lmax_list=model.lmax_list, mmax_list=model.mmax_list)
+        ctx = EQ.Ctx(cfg, dict(model.state_dict()), pos, vel, charges, B, N, gauge)
+        self.D = ctx.D[:, EQ.Layout(lay.lmax, lay.mmax).sel, :]
+        self.perm, self.inv_perm, self.m0 = (torch.tensor(v) for v in (lay.perm, lay.inv_perm, lay.m0))
         z = ctx.z
         self.g = _G(torch.stack([ctx.src, ctx.dst]), self.V)
         self.gz = _G(torch.stack([z[ctx.src], z[ctx.dst]]), model.max_num_elements)
@@ -84,15 +98,23 @@ def torch_ops(monkeypatch):
         self.dexp = _lin(ctx.dist[:, None], model.distance_expansion.weight, model.distance_expansion.bias)
         self.training = model.training
         self.batch = torch.arange(B).repeat_interleave(N)
-        ta, fa = EQ.grid_mats(2, 1)
-        tf, ff = EQ.grid_mats(2, 2)
-        self.grid_attn, self.grid_ffn = (ta.reshape(-1, 7), fa.reshape(-1, 7)), (tf.reshape(-1, 9), ff.reshape(-1, 9))
+        ta, fa = EQ.grid_mats(lay.lmax, lay.mmax)
+        tf, ff = EQ.grid_mats(lay.lmax, lay.lmax)
+        nr, nf = lay.n_red, lay.n_full
+        self.grid_attn, self.grid_ffn = (ta.reshape(-1, nr), fa.reshape(-1, nr)), (tf.reshape(-1, nf), ff.reshape(-1, nf))
     monkeypatch.setattr(T._Step, "__init__", step_init)
 
 
-def test_train_forward_composition_matches_oracle(torch_ops):
+@pytest.mark.parametrize("lmax,mmax,general", [(2, 1, False), (2, 1, True), (6, 2, True), (4, 3, True), (3, 0, True)])
+def test_train_forward_composition_matches_oracle(torch_ops, lmax, mmax, general):
+    """The composition's host logic (coefficient orders, SO(2) blocks per m, per-degree SO3_LinearV2,
+    m = 0 edge-degree slots, grids) at lmax 2 on the specialised and the general operators and at
+    lmax 3-6 (the reference default lmax 6 / mmax 2) on the general ones."""
     torch.manual_seed(0)
-    m = EquiformerV2_nbody(**CFG, alpha_drop=0.0, drop_path_rate=0.0).double()
+    cfg = dict(CFG, lmax_list=[lmax], mmax_list=[mmax])
+    m = EquiformerV2_nbody(**cfg, alpha_drop=0.0, drop_path_rate=0.0).double()
+    m.force_general_ops = general
+    assert m.uses_general_ops() == general
     with torch.no_grad():
         for k, p in m.named_parameters():
             if k.endswith("bias") or "affine" in k or "norm" in k:
@@ -107,7 +129,7 @@ def test_train_forward_composition_matches_oracle(torch_ops):
     (got ** 2).sum().backward()
     grads = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
     P = {k: p.detach().clone().requires_grad_() for k, p in m.named_parameters()}
-    ref = EQ.forward(CFG, P, loc, vel, mass, B, N, gauge)
+    ref = EQ.forward(cfg, P, loc, vel, mass, B, N, gauge)
     (ref ** 2).sum().backward()
     torch.testing.assert_close(got.detach(), ref.detach(), rtol=0, atol=1e-13)
     rg = {k: v.grad for k, v in P.items() if v.grad is not None}
