@@ -145,7 +145,8 @@ def bench_segnn(a, rank, world, device, P):
 
     B, N = a.batch or BATCH, NBODY
     torch.manual_seed(0)
-    model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS, lmax_h=1).to(device).float().train()
+    model = S.SEGNN(hidden_features=HIDDEN, num_layers=LAYERS, lmax_h=1,
+                    deterministic=a.deterministic_bn).to(device).float().train()
     # BatchNorm statistics: "batch" = per-rank batch statistics (the reference's
     # train-mode rollout on each rank's own B systems), "sync" = batch statistics over every rank's
     # systems (12 RCCL all-reduces of [3][96] fp64 sums per step), "running" = running statistics
@@ -242,7 +243,7 @@ def bench_segnn(a, rank, world, device, P):
         "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights)",
         "config": {"workload": "C2: SEGNN lmax_h=1 hidden=192 layers=6, N=5, batch=1024 per GPU, self-feed rollout",
                    "model": "SEGNN", "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}",
-                   "bn_mode": bn_desc},
+                   "bn_mode": bn_desc, "bn_sums": "fixed order" if a.deterministic_bn else "fp64 atomics"},
         "trajectory_steps_per_s": round(value * B, 1),
         "survey_formulation_tflops": round(value * SURVEY_GFLOP_PER_STEP / 1e3, 3),
         "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": round(achieved_tflops, 3),
@@ -944,14 +945,52 @@ def bench_eqv2_train(a, rank, world, device, P):
     return result
 
 
-def cpu_baseline_eqv2(model, B_glob, B_s=128):
+def bench_eqv2_l6(a, rank, world, device, P):
+    """The reference constructor's default degrees (lmax_list [6], mmax_list [2],
+    equiformer_v2_nbody.py:122-123) at the C4 widths: self-feed rollout on the composed native path
+    (eqv2_train.py on csrc/eqv2_general.hip + the generic operators; no fused kernels exist for
+    these degrees), N=20, batch 64 per GPU, device-hash edge gauges."""
+    from nbody_amd.equiformer_v2 import EquiformerV2_nbody
+    B, N = a.batch or 64, 20
+    cfg = dict(EQV2_C4, lmax_list=[6], mmax_list=[2])
+    torch.manual_seed(0)
+    model = EquiformerV2_nbody(**cfg).to(device).eval()
+    loc, vel, mass = initial_states(B, N, rank * B)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
+    loc_d, vel_d, mass_d = t(loc), t(vel), t(mass)
+    model.rollout(loc_d, vel_d, mass_d, max(a.warmup, 1) + 1, seed=1)
+
+    def work():
+        tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1, seed=2)
+        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
+        return tp
+    tp, elapsed = timed_region(work, device, P)
+    value = a.steps / elapsed * world
+    result = {
+        "metric": "self-feed rollout steps/sec, EquiformerV2 lmax 6 / mmax 2 N=20 batch=64", "value": round(value, 3),
+        "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GravitySim frame-0 initial states N=20, seeded random-init weights, device-hash edge gauges)",
+        "config": {"workload": "EquiformerV2 at the reference default degrees lmax [6] / mmax [2], C4 widths "
+                               "(4 layers, sphere 64, attn hidden 64, 4 heads, ffn 64, edge 64), N=20, batch 64 per GPU, "
+                               "composed native operators",
+                   "model": "EquiformerV2", "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}"},
+        "trajectory_steps_per_s": round(value * B, 1), "roofline": None,
+        "finite": bool(torch.isfinite(tp).all().item())}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_eqv2(model, B, B_s=8, cfg=cfg)
+    return result
+
+
+def cpu_baseline_eqv2(model, B_glob, B_s=128, cfg=EQV2_C4):
     from oracle import equiformer_v2 as EQ
     p = {k: v.detach().double().cpu() for k, v in model.named_parameters()}
     loc, vel, mass = initial_states(B_s, 20, 0)
     g = np.random.default_rng(0).uniform(0, 1, (B_s * 20 * 19, 3))
     threads = torch.get_num_threads()
     t0 = time.perf_counter()
-    EQ.forward(EQV2_C4, p, loc, vel, mass, B_s, 20, g)
+    EQ.forward(cfg, p, loc, vel, mass, B_s, 20, g)
     dt = time.perf_counter() - t0
     return {"value": 1.0 / (dt * B_glob / B_s), "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": f"1 forward of B={B_s} systems with the torch fp64 CPU oracle (oracle/equiformer_v2.py), "
@@ -1028,19 +1067,21 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--model", default="segnn",
                     choices=["segnn", "ponita", "egnn_mc", "egnn_mc_train", "segnn_train", "ponita_train", "eqv2",
-                             "eqv2_train", "gravity"])
+                             "eqv2_train", "eqv2_l6", "gravity"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-torch-steps", type=int, default=20,
                     help="C2: self-feed steps of the torch CPU restatement timed for cpu_baseline")
     ap.add_argument("--eager", action="store_true",
                     help="egnn_mc_train / segnn_train: run the step eagerly (no HIP graph)")
+    ap.add_argument("--deterministic-bn", action="store_true",
+                    help="segnn: fixed-order BatchNorm sums (bit-reproducible) instead of fp64 atomics")
     ap.add_argument("--bn-mode", default="batch", choices=["batch", "sync", "running"],
                     help="SEGNN BatchNorm statistics: per-rank batch (default), all-rank SyncBN, running")
     a = ap.parse_args()
     defaults = {"segnn": (200, 20), "ponita": (20, 2), "egnn_mc": (100, 10), "egnn_mc_train": (50, 5),
                 "segnn_train": (50, 5), "ponita_train": (30, 3), "eqv2": (20, 2),
-                "eqv2_train": (30, 3),
+                "eqv2_train": (30, 3), "eqv2_l6": (5, 1),
                 "gravity": (1000, 100)}
     a.steps = a.steps if a.steps is not None else defaults[a.model][0]
     a.warmup = a.warmup if a.warmup is not None else defaults[a.model][1]
@@ -1049,7 +1090,7 @@ def main():
     rank, world, device = P.init_from_env()
     fn = {"segnn": bench_segnn, "ponita": bench_ponita, "egnn_mc": bench_egnn, "egnn_mc_train": bench_egnn_train,
           "segnn_train": bench_segnn_train, "ponita_train": bench_ponita_train, "eqv2_train": bench_eqv2_train,
-          "eqv2": bench_eqv2, "gravity": bench_gravity}[a.model]
+          "eqv2": bench_eqv2, "eqv2_l6": bench_eqv2_l6, "gravity": bench_gravity}[a.model]
     result = fn(a, rank, world, device, P)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -274,8 +274,11 @@ class _Step:
         nr, nf = lay.n_red, lay.n_full
         self.grid_attn = (_f(ga.to_grid_mat.reshape(-1, nr)), _f(ga.from_grid_mat.reshape(-1, nr)))
         self.grid_ffn = (_f(gf.to_grid_mat.reshape(-1, nf)), _f(gf.from_grid_mat.reshape(-1, nf)))
-        dev_idx = lambda v: torch.tensor(v, device=dev, dtype=torch.long)
-        self.perm, self.inv_perm, self.m0 = dev_idx(lay.perm), dev_idx(lay.inv_perm), dev_idx(lay.m0)
+        # coefficient index tables, built once per device (no host-to-device copy inside a captured step)
+        cache = model.__dict__.setdefault("_eqv2_index_cache", {})
+        if dev not in cache:
+            cache[dev] = tuple(torch.tensor(v, device=dev, dtype=torch.long) for v in (lay.perm, lay.inv_perm, lay.m0))
+        self.perm, self.inv_perm, self.m0 = cache[dev]
 
     def rotate(self, x):
         """SO3_Rotation.rotate (so3.py:485-505): [E][(lmax+1)^2][C] -> the kept rows [E][R][C]."""

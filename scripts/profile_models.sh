@@ -17,6 +17,7 @@ declare -A ARGS=(
   [ponita_train]="--model ponita_train --steps 10 --warmup 2 --no-cpu-baseline"
   [eqv2_train]="--model eqv2_train --steps 10 --warmup 2 --no-cpu-baseline"
   [eqv2]="--model eqv2 --steps 5 --warmup 1 --no-cpu-baseline"
+  [eqv2_l6]="--model eqv2_l6 --steps 3 --warmup 1 --no-cpu-baseline"
   [gravity]="--model gravity --steps 200 --warmup 10 --no-cpu-baseline"
 )
 mkdir -p gpurun_out/prof
