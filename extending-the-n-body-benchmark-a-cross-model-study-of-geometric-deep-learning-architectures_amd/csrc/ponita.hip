@@ -219,6 +219,105 @@ __global__ __launch_bounds__(PO_FIB_THREADS, MINW) void po_fiber_ln_kernel(
     }
 }
 
+// One-pass variant: X1 is read from HBM exactly once.  A block walks node tiles (npi nodes of C/4
+// lanes each); for every tile it keeps X1[d, :, c..c+3] in registers and runs through ALL the
+// orientation ranges, the FK slices streaming through two LDS buffers: range k+1's slice is DMA-ed
+// (global_load_lds, 16 B per lane, no registers) into the other buffer while range k is computed,
+// one barrier per range.  The slices are re-fetched per tile from L2 (FK is 200 KB, L2-resident),
+// so HBM sees X1 once and XN once: the algorithmic traffic.  LDS slice layout [o][pl][C/4] float4
+// with the range's own width pn (so the DMA destination is linear).
+template <int OMAX, int MINW, int NT = PO_FIB_THREADS>
+__global__ __launch_bounds__(NT, MINW) void po_fiber_ln1_kernel(
+    const float* __restrict__ X1, const float* __restrict__ FK, int ldfk, const float* __restrict__ cbias,
+    const float* __restrict__ nw, const float* __restrict__ nb, int64_t V, int O, int C, int PR, int slice4,
+    float* __restrict__ XN, double* __restrict__ mom) {
+    extern __shared__ __attribute__((aligned(16))) float fks[];
+    __shared__ double red[16];
+    const int CG = C >> 2, npi = NT / CG;
+    const int t = threadIdx.x, ns = t / CG, cg = t - ns * CG, c = 4 * cg;
+    const int wave = t >> 6, lane = t & 63;
+    const int R = (O + PR - 1) / PR;
+    float4* fk4 = reinterpret_cast<float4*>(fks);
+    // DMA range r's slice into buffer b: element i = (o pn + pl) CG + q <- FK row (o O + p0 + pl), float4 q
+    auto dma = [&](int r, int b) {
+        const int p0 = r * PR, pn = min(PR, O - p0), n = O * pn * CG, per_o = pn * CG;
+        for (int piece = wave; piece * 64 < n; piece += NT / 64) {
+            int i = piece * 64 + lane;
+            i = i < n ? i : n - 1;                        // tail lanes re-read a valid element
+            const int o = i / per_o, rr = i - o * per_o, pl = rr / CG, q = rr - pl * CG;
+            __builtin_amdgcn_global_load_lds((const void*)(FK + (size_t)(o * O + p0 + pl) * ldfk + 4 * q),
+                                             (__attribute__((address_space(3))) void*)(fk4 + b * slice4 + piece * 64),
+                                             16, 0, 0);
+        }
+    };
+    const float4 cb = *reinterpret_cast<const float4*>(cbias + c);
+    const float4 w4 = *reinterpret_cast<const float4*>(nw + c);
+    const float4 b4 = *reinterpret_cast<const float4*>(nb + c);
+    const float invO = 1.0f / (float)O, invC = 1.0f / (float)C;
+    double s1 = 0.0, s2 = 0.0;
+    const int64_t first = (int64_t)blockIdx.x * npi, step_d = (int64_t)gridDim.x * npi;
+    if (first < V) dma(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int bsel = 0;                         // LDS buffer holding the current range
+    for (int64_t d0 = first; d0 < V; d0 += step_d) {
+        const int64_t d = d0 + ns;
+        const bool active = d < V;
+        float4 x[OMAX];
+        const float* x1 = X1 + (size_t)(active ? d : 0) * O * C + c;
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o)
+            x[o] = (o < O) ? *reinterpret_cast<const float4*>(x1 + (size_t)o * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool more_tiles = d0 + step_d < V;
+        for (int r = 0; r < R; ++r) {
+            if (r + 1 < R || more_tiles) dma(r + 1 < R ? r + 1 : 0, bsel ^ 1);   // the next step's slice
+            const int p0 = r * PR, pn = min(PR, O - p0);
+            const float4* sl = fk4 + bsel * slice4;
+            for (int pl = 0; pl < pn; ++pl) {
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int o = 0; o < OMAX; ++o) {
+                    if (o < O) {
+                        const float4 f = sl[(o * pn + pl) * CG + cg];
+                        a.x += x[o].x * f.x;
+                        a.y += x[o].y * f.y;
+                        a.z += x[o].z * f.z;
+                        a.w += x[o].w * f.w;
+                    }
+                }
+                a.x *= invO; a.y *= invO; a.z *= invO; a.w *= invO;
+                if (mom && active) {
+                    s1 += (double)a.x + (double)a.y + (double)a.z + (double)a.w;
+                    s2 += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+                }
+                const float y0 = a.x + cb.x, y1 = a.y + cb.y, y2 = a.z + cb.z, y3 = a.w + cb.w;
+                float s = y0 + y1 + y2 + y3;
+                for (int off = CG >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off);
+                const float mu = s * invC;
+                const float e0 = y0 - mu, e1 = y1 - mu, e2 = y2 - mu, e3 = y3 - mu;
+                float v = e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+                for (int off = CG >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off);
+                const float rs = 1.0f / sqrtf(v * invC + 1e-5f);
+                if (active)
+                    *reinterpret_cast<float4*>(XN + ((size_t)d * O + p0 + pl) * C + c) =
+                        make_float4(e0 * rs * w4.x + b4.x, e1 * rs * w4.y + b4.y, e2 * rs * w4.z + b4.z,
+                                    e3 * rs * w4.w + b4.w);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            bsel ^= 1;
+        }
+    }
+    if (mom) {
+        s1 = block_sum_double(s1, red);
+        s2 = block_sum_double(s2, red);
+        if (threadIdx.x == 0) {
+            atomicAdd(&mom[0], s1);
+            atomicAdd(&mom[1], s2);
+        }
+    }
+}
+
 // read_out_layers[l]: RO[row, k] (+)= X[row] . Wro[k] + bro[k], k < 2; C/4 lanes per row
 __global__ void po_readout_kernel(const float* __restrict__ X, const float* __restrict__ Wro,
                                   const float* __restrict__ bro, int64_t rows, int C, int first,
@@ -858,6 +957,43 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             // (profiles/r04/ponita_fib_ab): 1024 -> 181 us / 989 MB, 512 -> 169 us / 762 MB, 256 -> 261 us /
             // 610 MB per launch; fewer groups re-read less but 256 no longer fills the chip
             static const int fib_blocks = getenv("NBX_PO_FIB_BLOCKS") ? atoi(getenv("NBX_PO_FIB_BLOCKS")) : 512;
+            // po_fiber_ln1_kernel (default; NBX_PO_FIB_ONEPASS=0 selects the range-split kernel below): X1
+            // read once, FK slices double-buffered through LDS-DMA.  Measured (profiles/r04/ponita_fib_onepass):
+            // 450 MB per launch (1.07x algorithmic) in 184 us against the range-split kernel's 762 MB in
+            // 167 us; C3 steps/s equal within run-to-run noise (103.55 vs 103.51).  256-thread blocks,
+            // 16-20 KiB slices and 1024-2048 blocks measured slower (219-287 us)
+            static const bool onepass = !getenv("NBX_PO_FIB_ONEPASS") || atoi(getenv("NBX_PO_FIB_ONEPASS")) != 0;
+            static const size_t fk1_lds = getenv("NBX_PO_FK1_LDS") ? (size_t)atol(getenv("NBX_PO_FK1_LDS")) : 32 * 1024;
+            const int PR1 = std::max(1, std::min(O, (int)(fk1_lds / ((size_t)O * C * 4))));
+            if (onepass && O <= 20 && C % 4 == 0 && PO_FIB_THREADS % (C / 4) == 0) {
+                static const int fib1_blocks =
+                    getenv("NBX_PO_FIB1_BLOCKS") ? atoi(getenv("NBX_PO_FIB1_BLOCKS")) : 512;
+                int gx1;
+                const int slice4 = (O * PR1 * (C / 4) + 63) / 64 * 64;     // whole DMA pieces
+                const size_t lds1 = 2 * (size_t)slice4 * 16;
+                // NBX_PO_FIB1_W: waves per EU the register budget targets (4: <= 128 VGPRs, two blocks per CU)
+                static const int fib1_w = getenv("NBX_PO_FIB1_W") ? atoi(getenv("NBX_PO_FIB1_W")) : 4;
+                // NBX_PO_FIB1_NT: threads per block (256: more, smaller blocks interleave the per-range barriers)
+                static const int fib1_nt = getenv("NBX_PO_FIB1_NT") ? atoi(getenv("NBX_PO_FIB1_NT")) : 512;
+                const int nt1 = (fib1_nt == 256 && 256 % (C / 4) == 0) ? 256 : 512;
+                const int npi1 = nt1 / (C / 4);
+                gx1 = (int)std::min<int64_t>((d.V + npi1 - 1) / npi1, std::max(1, fib1_blocks));
+                auto k1 = nt1 == 256 ? (fib1_w >= 4 ? po_fiber_ln1_kernel<20, 4, 256> : po_fiber_ln1_kernel<20, 2, 256>)
+                                     : (fib1_w >= 4 ? po_fiber_ln1_kernel<20, 4> : po_fiber_ln1_kernel<20, 2>);
+                NBX_CHECK_ARG(lds1 <= 160 * 1024, "ponita: one-pass fibre kernel needs %zu bytes of LDS", lds1);
+                if (lds1 > 64 * 1024)
+                    NBX_HIP(hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)lds1));
+                if (int rc = nbx::timed(tm, st, PK_FIBER, 2.0 * VO * O * C, (double)VO * C * f4 * 2, [&] {
+                        hipLaunchKernelGGL(k1, dim3(gx1), dim3(nt1), lds1, st, ws.X1,
+                                           ws.FK + (size_t)l * C, L * C, Ly.conv_bias, Ly.norm_w, Ly.norm_b, d.V,
+                                           O, C, PR1, slice4, ws.XN, mom ? mom + 6 * l + 4 : nullptr);
+                        return (int)NBX_OK;
+                    }))
+                    return rc;
+                goto fiber_done;
+            }
+            {
             const int gx = (int)std::min<int64_t>((d.V + npi - 1) / npi, std::max(1, fib_blocks / R));
             const size_t lds = (size_t)O * PR * C * 4;
             auto kern = O <= 20 ? po_fiber_ln_kernel<20, 4> : po_fiber_ln_kernel<PO_OMAX, 2>;
@@ -873,6 +1009,8 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
                     return (int)NBX_OK;
                 }))
                 return rc;
+            }
+        fiber_done:;
         }
         if (Ly.ffn_img_x3 && po_x3_enabled() && (C == 64 || C == 128) && d.mlp % 32 == 0 && d.mlp <= FFN_FMAX) {
             // ConvNext MLP fused (linear_1 + GELU + linear_2 + layer_scale + residual): the hidden
