@@ -535,6 +535,49 @@ __global__ void gather_rows_kernel(int64_t n, int cols, const int* __restrict__ 
     for (int k = 0; k < planes; ++k) out[k * pso + r * ldo + c] = in[k * psi + s * ldi + c];
 }
 
+// out[n][c] (+)= sum_{j in [ptr[n], ptr[n+1])} in[eid[j]][c] per plane, fixed order: one block of 4
+// waves per (segment, 64-column slice), lane = column; wave w sums the w-th quarter of the segment
+// in CSR order with its row loads issued 8 at a time (long segments -- an embedding-table gradient
+// has ~E / #elements rows per segment -- were a serial chain of dependent L2 round trips), then
+// the 4 partials are added in wave order through LDS
+__global__ __launch_bounds__(256) void segment_sum4_kernel(int64_t n, int cols, const int* __restrict__ ptr,
+                                                          const int* __restrict__ eid, const float* __restrict__ in,
+                                                          int64_t ldi, int64_t psi, float* __restrict__ out,
+                                                          int64_t ldo, int64_t pso, int planes, int accumulate) {
+    __shared__ float part[4][64];
+    const int slices = (cols + 63) >> 6;
+    const int64_t r = blockIdx.x / slices;
+    const int c = (int)(blockIdx.x - r * slices) * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+    const int j0 = ptr[r], j1 = ptr[r + 1], len = j1 - j0, q = (len + 3) >> 2;
+    const int a = j0 + min(len, w * q), b = j0 + min(len, (w + 1) * q);
+    const bool live = c < cols;
+    for (int k = 0; k < planes; ++k) {
+        const float* src = in + k * psi + (live ? c : 0);
+        float s = 0.f;
+        int j = a;
+        for (; j + 8 <= b; j += 8) {
+            int e[8];
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) e[u] = eid[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)e[u] * ldi];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; j < b; ++j) s += src[(int64_t)eid[j] * ldi];
+        part[w][threadIdx.x & 63] = s;
+        __syncthreads();
+        if (w == 0 && live) {
+            const int l = threadIdx.x & 63;
+            const float t = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+            float* o = out + k * pso + r * ldo + c;
+            *o = accumulate ? *o + t : t;
+        }
+        __syncthreads();
+    }
+}
+
 // out[n][c] (+)= sum_{j in [ptr[n], ptr[n+1])} in[eid[j]][c] per plane, in CSR order
 __global__ void segment_sum_kernel(int64_t n, int cols, const int* __restrict__ ptr, const int* __restrict__ eid,
                                    const float* __restrict__ in, int64_t ldi, int64_t psi, float* __restrict__ out,
@@ -869,8 +912,15 @@ extern "C" int nbx_segment_sum(int64_t n, int32_t cols, const int32_t* ptr, cons
                                int32_t planes, int32_t accumulate, void* stream) {
     NBX_CHECK_ARG(n >= 0 && cols >= 0 && planes >= 1 && ld_in >= cols && ld_out >= cols, "nbx_segment_sum: bad sizes");
     if (n == 0 || cols == 0) return NBX_OK;
-    hipLaunchKernelGGL(segment_sum_kernel, dim3(nblk(n * cols)), dim3(256), 0, (hipStream_t)stream, n, cols, ptr, eid, in,
-                       ld_in, plane_in, out, ld_out, plane_out, planes, accumulate);
+    // NBX_SEGSUM_SERIAL=1: the thread-per-(segment, column) sequential kernel (A/B)
+    static const bool serial = getenv("NBX_SEGSUM_SERIAL") && atoi(getenv("NBX_SEGSUM_SERIAL")) != 0;
+    if (serial)
+        hipLaunchKernelGGL(segment_sum_kernel, dim3(nblk(n * cols)), dim3(256), 0, (hipStream_t)stream, n, cols, ptr, eid,
+                           in, ld_in, plane_in, out, ld_out, plane_out, planes, accumulate);
+    else
+        hipLaunchKernelGGL(segment_sum4_kernel, dim3((unsigned)(n * ((cols + 63) / 64))), dim3(256), 0,
+                           (hipStream_t)stream, n, cols, ptr, eid, in, ld_in, plane_in, out, ld_out, plane_out, planes,
+                           accumulate);
     NBX_LAUNCH_CHECK("segment_sum");
     return NBX_OK;
 }

@@ -48,6 +48,10 @@ class _ArrayUnpickler(pickle.Unpickler):
         raise pickle.UnpicklingError(f"refusing to load {module}.{name} from a simulation cache")
 
 
+def _log(msg):
+    print(f"[GravityDatasetOtf] {msg}")
+
+
 def load_cached_simulations(path):
     with open(path, "rb") as f:
         return _ArrayUnpickler(io.BytesIO(f.read())).load()
@@ -116,82 +120,93 @@ class GravityDatasetOtf:
         return batch_data, self.get_serializable_attributes()
 
     def _load_more_batches(self):
-        future_batch, _ = self.get_ground_truth_trajectories()
-        self.data_queue.append(future_batch)
-        self.unused_indices_queue.append(list(range(future_batch[0][0].shape[0] - 1)))
+        """Integrate a fresh batch, queue it (all its frame pairs unused) and optionally cache it."""
+        batch, _ = self.get_ground_truth_trajectories()
+        self._enqueue(batch)
         if self.cache_data:
-            self._save_simulations(future_batch)
+            self._save_simulations(batch)
 
     # ------------------------------------------------------------ cache
     def _cache_folder(self):
         return f"{self.data_path}/{self.cached_folder_name}"
 
+    @staticmethod
+    def _pickles(folder):
+        return [fn for fn in os.listdir(folder) if fn.endswith(".pkl")]
+
     def _save_simulations(self, data):
+        """Next free integer file name in the cache folder (<k>.pkl, k = 1 + the largest present)."""
         folder = self._cache_folder()
         os.makedirs(folder, exist_ok=True)
-        pickled = [fn for fn in os.listdir(folder) if fn[-4:] == ".pkl"]
-        file_name = "0.pkl" if not pickled else f"{max(int(fn[:-4]) for fn in pickled) + 1}.pkl"
-        file_name = f"{folder}/{file_name}"
-        save_cached_simulations(file_name, data)
-        print(f"simulation is saved into {file_name}")
+        taken = [int(fn[:-4]) for fn in self._pickles(folder)]
+        path = f"{folder}/{max(taken) + 1 if taken else 0}.pkl"
+        save_cached_simulations(path, data)
+        _log(f"cached {len(data)} trajectories -> {path}")
 
     def _load_saved_simulations(self, index):
-        print(f"Loading cached simulations from {self.cached_folder_name}")
+        """Queue cache file number ``index`` (sorted file names); when the folder is missing or the
+        files are used up, switch to generation for good (cache_index = -1)."""
         folder = self._cache_folder()
-        if not os.path.exists(folder):
-            print(f"No cached simulations found at {folder}")
+        files = sorted(self._pickles(folder)) if os.path.exists(folder) else None
+        if files is None or index >= len(files):
+            _log(f"simulation cache {self.cached_folder_name}: "
+                 + ("folder missing" if files is None else f"all {len(files)} files used") + "; generating")
             self.cache_index = -1
             self._load_more_batches()
             return
-        pickled = sorted(fn for fn in os.listdir(folder) if fn[-4:] == ".pkl")
-        if index > len(pickled) - 1:
-            print("Ran out of cached simulations")
-            self.cache_index = -1
-            self._load_more_batches()
-            return
-        print(f"Loading pregenerated simulation index {index}")
-        self._push_simulations_into_data_queue(load_cached_simulations(f"{folder}/{pickled[index]}"))
+        _log(f"simulation cache {self.cached_folder_name}: reading file {index} ({files[index]})")
+        self._enqueue(load_cached_simulations(f"{folder}/{files[index]}"))
         self.cache_index += 1
 
-    def _push_simulations_into_data_queue(self, data):
-        self.data_queue.append(data)
-        self.unused_indices_queue.append(list(range(data[0][0].shape[0] - 1)))
+    def _enqueue(self, batch):
+        frames = batch[0][0].shape[0]
+        self.data_queue.append(batch)
+        self.unused_indices_queue.append(list(range(frames - 1)))   # frame_0 candidates (frame_T = frame_0 + 1)
+
+    # kept for callers of the reference's name
+    _push_simulations_into_data_queue = _enqueue
 
     def _get_cached_folder_name(self):
         return hashlib.sha256(json.dumps(self.locals, sort_keys=True).encode()).hexdigest()
 
     # ------------------------------------------------------------ samples
+    # target -> y from the batch arrays (loc / vel / force [B, T, N, 3]) and the frame pair; the first
+    # two index the batch's FIRST axis with the frame number, exactly as the reference does
+    _TARGETS = {
+        "pos": lambda loc, vel, force, f0, fT: loc[fT],
+        "force": lambda loc, vel, force, f0, fT: force[fT],
+        "pos_dt+vel_dt": lambda loc, vel, force, f0, fT: np.concatenate((loc[fT] - loc[f0], vel[fT] - vel[f0]), axis=1),
+        "pos_dt+vel": lambda loc, vel, force, f0, fT: np.concatenate((loc[:, fT] - loc[:, f0], vel[:, fT]), axis=2),
+        "pos+vel": lambda loc, vel, force, f0, fT: np.concatenate((loc[:, fT], vel[:, fT]), axis=2),
+        "pos_com+vel": lambda loc, vel, force, f0, fT: np.concatenate(
+            (loc[fT] - np.mean(loc[f0], axis=0)[None, :], vel[fT]), axis=1),
+    }
+
+    def _advance_queue(self):
+        """The head batch has no unused frame pair left: drop it; if the queue is then empty, refill
+        it from the cache (while it lasts) or by generating."""
+        _log("head simulation batch exhausted; moving to the next one")
+        del self.data_queue[0], self.unused_indices_queue[0]
+        if not self.unused_indices_queue:
+            _log("simulation queue empty; refilling")
+            if self.cache_index == -1:
+                self._load_more_batches()
+            else:
+                self._load_saved_simulations(self.cache_index)
+
     def __getitem__(self, _):
-        if len(self.unused_indices_queue[0]) == 0:
-            print("No more unused indices in this simulation. Using next simulation batch")
-            self.data_queue.pop(0)
-            self.unused_indices_queue.pop(0)
-            if len(self.unused_indices_queue) == 0:
-                print("no more simulations in queue. Loading new simulation batch")
-                if self.cache_index != -1:
-                    self._load_saved_simulations(self.cache_index)
-                else:
-                    self._load_more_batches()
+        """One random unused frame pair (frame_0, frame_0 + 1) of the head batch (random.choice, then
+        removed): (loc, vel, force at frame_0 [B, N, 3], mass, target)."""
+        if not self.unused_indices_queue[0]:
+            self._advance_queue()
         loc, vel, force, mass = (np.array(x) for x in zip(*self.data_queue[0]))
-        frame_0 = random.choice(self.unused_indices_queue[0])
-        frame_T = frame_0 + 1
-        self.unused_indices_queue[0].remove(frame_0)
-        if self.target == "pos":
-            y = loc[frame_T]
-        elif self.target == "force":
-            y = force[frame_T]
-        elif self.target == "pos_dt+vel_dt":
-            y = np.concatenate((loc[frame_T] - loc[frame_0], vel[frame_T] - vel[frame_0]), axis=1)
-        elif self.target == "pos_dt+vel":
-            y = np.concatenate((loc[:, frame_T] - loc[:, frame_0], vel[:, frame_T]), axis=2)
-        elif self.target == "pos+vel":
-            y = np.concatenate((loc[:, frame_T], vel[:, frame_T]), axis=2)
-        elif self.target == "pos_com+vel":
-            com = np.mean(loc[frame_0], axis=0)
-            y = np.concatenate((loc[frame_T] - com[None, :], vel[frame_T]), axis=1)
-        else:
+        f0 = random.choice(self.unused_indices_queue[0])
+        self.unused_indices_queue[0].remove(f0)
+        make = self._TARGETS.get(self.target)
+        if make is None:
             raise Exception(f"Wrong target {self.target}")
-        return (torch.tensor(loc[:, frame_0]), torch.tensor(vel[:, frame_0]), torch.tensor(force[:, frame_0]),
+        y = make(loc, vel, force, f0, f0 + 1)
+        return (torch.tensor(loc[:, f0]), torch.tensor(vel[:, f0]), torch.tensor(force[:, f0]),
                 torch.tensor(mass), torch.tensor(y))
 
     def get_serializable_attributes(self):

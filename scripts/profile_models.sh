@@ -15,7 +15,7 @@ declare -A ARGS=(
   [egnn_mc_train]="--model egnn_mc_train --steps 20 --warmup 3 --no-cpu-baseline"
   [segnn_train]="--model segnn_train --steps 10 --warmup 2 --no-cpu-baseline"
   [ponita_train]="--model ponita_train --steps 10 --warmup 2 --no-cpu-baseline"
-  [eqv2_train]="--model eqv2_train --steps 10 --warmup 2 --no-cpu-baseline"
+  [eqv2_train]="--model eqv2_train --steps 10 --warmup 2 --no-cpu-baseline --eager"
   [eqv2]="--model eqv2 --steps 5 --warmup 1 --no-cpu-baseline"
   [eqv2_l6]="--model eqv2_l6 --steps 3 --warmup 1 --no-cpu-baseline"
   [gravity]="--model gravity --steps 200 --warmup 10 --no-cpu-baseline"
