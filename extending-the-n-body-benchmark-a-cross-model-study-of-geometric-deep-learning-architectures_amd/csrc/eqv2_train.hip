@@ -71,9 +71,9 @@ __global__ void eqv2_rotate_kernel(int64_t E, int C, const float* __restrict__ D
 // ---------------------------------------------------------------- separable S2 activation (grid part)
 // out[r][i][h] = sum_p F[p][i] SiLU(sum_j T[p][j] x[r][j][h]) for the I coefficients of a row and P
 // grid points; backward dx[r][j][h] = sum_p T[p][j] SiLU'(t_p) sum_i F[p][i] dout[r][i][h].  T and F
-// sit in LDS (2 P I floats: 82 KB at lmax 6, SO3_Grid(6, 6) = 14 x 15 points); a thread keeps one
+// sit in LDS (2 P I4 floats, I padded to 4: 87 KB at lmax 6, SO3_Grid(6, 6) = 14 x 15 points); a thread keeps one
 // (row, channel)'s coefficients in registers (MAXI = 9 up to lmax 2, 49 up to lmax 6).
-constexpr int S2_MAXI = 49, S2_MAXP = 256;
+constexpr int S2_MAXI = 49, S2_MAXP = 240;   // LDS: 2 x 240 x 52 floats = 99.8 KB
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
@@ -81,12 +81,18 @@ template <int MAXI, bool BWD>
 __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P, int H, const float* __restrict__ T,
                                                       const float* __restrict__ F, const float* __restrict__ X,
                                                       const float* __restrict__ dOut, float* __restrict__ out) {
-    extern __shared__ float s2_lds[];
-    float* sT = s2_lds;
-    float* sF = s2_lds + P * I;
-    for (int k = threadIdx.x; k < P * I; k += blockDim.x) {
-        sT[k] = T[k];
-        sF[k] = F[k];
+    // T / F rows padded to a multiple of 4 coefficients with zeros and read as float4: the lanes of a
+    // wave share one row, so each ds_read_b128 is a broadcast feeding four FMAs (one b32 read per FMA
+    // left the kernel LDS-issue bound)
+    constexpr int M4 = (MAXI + 3) / 4;
+    extern __shared__ __attribute__((aligned(16))) float s2_lds[];
+    const int I4 = (I + 3) >> 2;
+    float4* sT = reinterpret_cast<float4*>(s2_lds);
+    float4* sF = sT + P * I4;
+    for (int k = threadIdx.x; k < P * I4 * 4; k += blockDim.x) {
+        const int p = k / (I4 * 4), i = k - p * I4 * 4;
+        s2_lds[k] = i < I ? T[p * I + i] : 0.f;
+        s2_lds[P * I4 * 4 + k] = i < I ? F[p * I + i] : 0.f;
     }
     __syncthreads();
     const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -94,47 +100,59 @@ __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P
     const int64_t r = g / H;
     const int h = (int)(g - r * H);
     const int64_t base = r * I * H + h;
-    float x[MAXI], d[MAXI], o[MAXI];
+    float x[4 * M4], d[4 * M4], o[4 * M4];
 #pragma unroll
-    for (int i = 0; i < MAXI; ++i) {
+    for (int i = 0; i < 4 * M4; ++i) {
         x[i] = i < I ? X[base + (int64_t)i * H] : 0.f;
         d[i] = (BWD && i < I) ? dOut[base + (int64_t)i * H] : 0.f;
         o[i] = 0.f;
     }
     for (int p = 0; p < P; ++p) {
-        const float* tp = sT + p * I;
-        const float* fp = sF + p * I;
+        const float4* tp = sT + p * I4;
+        const float4* fp = sF + p * I4;
         float t = 0.f;
 #pragma unroll
-        for (int i = 0; i < MAXI; ++i)
-            if (i < I) t += tp[i] * x[i];
+        for (int q = 0; q < M4; ++q)
+            if (q < I4) {
+                const float4 v = tp[q];
+                t += v.x * x[4 * q] + v.y * x[4 * q + 1] + v.z * x[4 * q + 2] + v.w * x[4 * q + 3];
+            }
         const float s = sigm(t);
         if (!BWD) {
             const float a = t * s;
 #pragma unroll
-            for (int i = 0; i < MAXI; ++i)
-                if (i < I) o[i] += fp[i] * a;
+            for (int q = 0; q < M4; ++q)
+                if (q < I4) {
+                    const float4 v = fp[q];
+                    o[4 * q] += v.x * a; o[4 * q + 1] += v.y * a; o[4 * q + 2] += v.z * a; o[4 * q + 3] += v.w * a;
+                }
         } else {
             float gsum = 0.f;
 #pragma unroll
-            for (int i = 0; i < MAXI; ++i)
-                if (i < I) gsum += fp[i] * d[i];
+            for (int q = 0; q < M4; ++q)
+                if (q < I4) {
+                    const float4 v = fp[q];
+                    gsum += v.x * d[4 * q] + v.y * d[4 * q + 1] + v.z * d[4 * q + 2] + v.w * d[4 * q + 3];
+                }
             const float dt = gsum * (s + t * s * (1.0f - s));
 #pragma unroll
-            for (int i = 0; i < MAXI; ++i)
-                if (i < I) o[i] += tp[i] * dt;
+            for (int q = 0; q < M4; ++q)
+                if (q < I4) {
+                    const float4 v = tp[q];
+                    o[4 * q] += v.x * dt; o[4 * q + 1] += v.y * dt; o[4 * q + 2] += v.z * dt; o[4 * q + 3] += v.w * dt;
+                }
         }
     }
 #pragma unroll
-    for (int i = 0; i < MAXI; ++i)
+    for (int i = 0; i < 4 * M4; ++i)
         if (i < I) out[base + (int64_t)i * H] = o[i];
 }
 
 template <bool BWD>
 int s2_launch(int64_t rows, int I, int P, int H, const float* T, const float* F, const float* X, const float* dOut,
               float* out, hipStream_t st) {
-    const size_t lds = 2 * (size_t)P * I * sizeof(float);
-    auto kern = I <= 9 ? eqv2_s2_kernel<9, BWD> : eqv2_s2_kernel<S2_MAXI, BWD>;
+    const size_t lds = 2 * (size_t)P * ((I + 3) / 4 * 4) * sizeof(float);
+    auto kern = I <= 9 ? eqv2_s2_kernel<9, BWD> : I <= 32 ? eqv2_s2_kernel<32, BWD> : eqv2_s2_kernel<S2_MAXI, BWD>;
     if (lds > 64 * 1024)
         NBX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, dim3(nblk(rows * H)), dim3(256), lds, st, rows, I, P, H, T, F, X, dOut, out);

@@ -421,7 +421,7 @@ int nbx_eqv2_rotate(int64_t E, int32_t C, const float* dsel, const float* in, in
 
 /* Separable S2 activation, grid part (activation.py:155-202): out[r][i][h] = sum_p F[p][i]
  * SiLU(sum_j T[p][j] X[r][j][h]), X / out [rows][I][H], T / F [P][I] (SO3_Grid to / from grid
- * matrices), I <= 49, P <= 256 (ABI 13; lmax 6: SO3_Grid(6, 6) has 14 x 15 points); backward dX from dOut. */
+ * matrices), I <= 49, P <= 240 (ABI 13; lmax 6: SO3_Grid(6, 6) has 14 x 15 points); backward dX from dOut. */
 int nbx_eqv2_s2_act(int64_t rows, int32_t I, int32_t P, int32_t H, const float* to_grid, const float* from_grid,
                     const float* X, float* out, void* stream);
 int nbx_eqv2_s2_act_backward(int64_t rows, int32_t I, int32_t P, int32_t H, const float* to_grid,
