@@ -289,13 +289,15 @@ def pmc_traffic(kernel_name, model=None):
 # rocprofv3 names at C3 with the bf16x3 images (ponita.hip lin_auto: PREC = 1, NT by the image's LDS size;
 # the ConvNext MLP fused into po_ffn_kernel; kind 2 (linear_2 alone) only runs on the unfused path)
 PONITA_KIND_NAMES = ["void nbx::lin_kernel<4, 0, 1, 1>(nbx::LinProb)",
-                     "void (anonymous namespace)::po_ffn_kernel<4>((anonymous namespace)::FfnProb)",
-                     "void nbx::lin_rp_kernel<4, 0>(nbx::LinRpProb)", "void nbx::lin_kernel<4, 2, 0, 1>(nbx::LinProb)",
-                     "void (anonymous namespace)::po_fiber_ln_kernel<20, 4>(float const*, float const*, int, "
-                     "float const*, float const*, float const*, long, int, int, int, float*, double*)"]
+                     "void (anonymous namespace)::po_ffn_kernel<4, 4, 0>((anonymous namespace)::FfnProb)",
+                     "void nbx::lin_rp_kernel<4, 0>(nbx::LinRpProb)",
+                     "void (anonymous namespace)::po_ffn_kernel<1, 4, 1>((anonymous namespace)::FfnProb)",
+                     "void (anonymous namespace)::po_fiber_ln1_kernel<20, 4, 512>(float const*, float const*, int, "
+                     "float const*, float const*, float const*, long, int, int, int, int, float*, double*)"]
 PONITA_KIND_ROLES = ["FiberBundleConv spatial kernel GEMM + gather/aggregate epilogue",
                      "ConvNext MLP fused (linear_1 + GELU + linear_2 + layer_scale + residual, hidden in registers)",
-                     "ConvNext linear_2 + layer_scale + residual (unfused path only)", "kernel basis MLP (2 GEMMs)",
+                     "ConvNext linear_2 + layer_scale + residual (unfused path only)",
+                     "kernel basis MLP (both layers fused, po_ffn_kernel FFN_BASIS)",
                      "fibre conv + bias + LayerNorm"]
 
 
