@@ -124,10 +124,12 @@ __device__ __forceinline__ float inv_rescale(int l, int mmax) {
 
 // MODE 0 (rotate):     out [E][R][C]          = D_sel in (x rescale), in [E][(lmax+1)^2][C] (ld_in per edge)
 // MODE 1 (rotate_inv): out [E][(lmax+1)^2][C] = D_sel^T in (x rescale), in [E][R][C] (ld_in per edge)
+// order (nullable): the edge-side row of kept coefficient k (l-primary) is order[k] -- e.g. the
+// m-primary order of SO2_Convolution, so the SO(2) blocks read contiguous rows without a permutation
 template <int MODE>
 __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax, int S, int R,
                                            const float* __restrict__ D, const float* __restrict__ in, int64_t ld_in,
-                                           float* __restrict__ out, int rescale) {
+                                           float* __restrict__ out, int rescale, const int* __restrict__ order) {
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (t >= E * C) return;
     const int64_t e = t / C;
@@ -150,12 +152,12 @@ __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax,
 #pragma unroll
                 for (int j = 0; j < GN_MAX; ++j)
                     if (j < n) a += di[j] * v[j];
-                o[(int64_t)(roff + i) * C] = s * a;
+                o[(int64_t)(order ? order[roff + i] : roff + i) * C] = s * a;
             }
         } else {
             float v[GN_MAX];
 #pragma unroll
-            for (int i = 0; i < GN_MAX; ++i) v[i] = i < kl ? x[(int64_t)(roff + i) * C] : 0.f;
+            for (int i = 0; i < GN_MAX; ++i) v[i] = i < kl ? x[(int64_t)(order ? order[roff + i] : roff + i) * C] : 0.f;
             for (int j = 0; j < n; ++j) {
                 float a = 0.f;
 #pragma unroll
@@ -309,7 +311,7 @@ extern "C" int nbx_eqv2_wigner(int64_t E, int32_t lmax, int32_t mmax, const floa
 
 extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel,
                                        const float* in, int64_t ld_in, float* out, int32_t inverse, int32_t rescale,
-                                       void* stream) {
+                                       const int32_t* order, void* stream) {
     NBX_CHECK_ARG(E >= 0 && C >= 1 && mmax >= 0 && mmax <= lmax && lmax <= GL_MAX,
                   "nbx_eqv2_rotate_general: need C >= 1, 0 <= mmax <= lmax <= %d", GL_MAX);
     const int R = kept_rows(lmax, mmax), K = (lmax + 1) * (lmax + 1);
@@ -320,10 +322,10 @@ extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32
     const int S = dsel_floats(lmax, mmax);
     if (inverse)
         hipLaunchKernelGGL(eqv2_rotate_general_kernel<1>, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R,
-                           dsel, in, ld_in, out, rescale);
+                           dsel, in, ld_in, out, rescale, order);
     else
         hipLaunchKernelGGL(eqv2_rotate_general_kernel<0>, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R,
-                           dsel, in, ld_in, out, rescale);
+                           dsel, in, ld_in, out, rescale, order);
     NBX_LAUNCH_CHECK("eqv2_rotate_general");
     return NBX_OK;
 }

@@ -92,30 +92,32 @@ class _RotateFn(torch.autograd.Function):
 
 class _RotateGFn(torch.autograd.Function):
     """General degrees: rotate (inverse = 0) [E][(lmax+1)^2][C] -> [E][R][C], rotate_inv (inverse = 1)
-    [E][R][C] -> [E][(lmax+1)^2][C] with the kept Wigner rows D [E][S]."""
+    [E][R][C] -> [E][(lmax+1)^2][C] with the kept Wigner rows D [E][S]; ``order`` (int32 [R] or None):
+    the [E][R][C] row of each kept coefficient (the m-primary order of the SO(2) convolutions)."""
 
     @staticmethod
-    def forward(ctx, X, D, lay, inverse, rescale):
+    def forward(ctx, X, D, lay, inverse, rescale, order=None):
         E, _, C = X.shape
         X = X.contiguous()
         out = torch.empty(E, lay.n_full if inverse else lay.n_red, C, device=X.device, dtype=_f32)
         _lib.check(_lib.lib().nbx_eqv2_rotate_general(E, C, lay.lmax, lay.mmax, _dp(D), _dp(X), X.shape[1] * C,
-                                                      _dp(out), inverse, rescale, _st(X)), "nbx_eqv2_rotate_general")
-        ctx.save_for_backward(D)
+                                                      _dp(out), inverse, rescale, _dp(order), _st(X)),
+                   "nbx_eqv2_rotate_general")
+        ctx.save_for_backward(D, order)
         ctx.mode = (lay, inverse, rescale)
         return out
 
     @staticmethod
     def backward(ctx, dY):
-        (D,) = ctx.saved_tensors
+        D, order = ctx.saved_tensors
         lay, inverse, rescale = ctx.mode
         dY = dY.contiguous()
         E, _, C = dY.shape
         dX = torch.empty(E, lay.n_red if inverse else lay.n_full, C, device=dY.device, dtype=_f32)
         _lib.check(_lib.lib().nbx_eqv2_rotate_general(E, C, lay.lmax, lay.mmax, _dp(D), _dp(dY), dY.shape[1] * C,
-                                                      _dp(dX), 1 - inverse, rescale, _st(dY)),
+                                                      _dp(dX), 1 - inverse, rescale, _dp(order), _st(dY)),
                    "nbx_eqv2_rotate_general")
-        return dX, None, None, None, None
+        return dX, None, None, None, None, None
 
 
 class _S2Fn(torch.autograd.Function):
@@ -272,24 +274,32 @@ class _Step:
         self.batch = torch.arange(B, device=dev).repeat_interleave(N)
         ga, gf = model.SO3_grid[lay.lmax][lay.mmax], model.SO3_grid[lay.lmax][lay.lmax]
         nr, nf = lay.n_red, lay.n_full
-        self.grid_attn = (_f(ga.to_grid_mat.reshape(-1, nr)), _f(ga.from_grid_mat.reshape(-1, nr)))
-        self.grid_ffn = (_f(gf.to_grid_mat.reshape(-1, nf)), _f(gf.from_grid_mat.reshape(-1, nf)))
         # coefficient index tables, built once per device (no host-to-device copy inside a captured step)
         cache = model.__dict__.setdefault("_eqv2_index_cache", {})
         if dev not in cache:
-            cache[dev] = tuple(torch.tensor(v, device=dev, dtype=torch.long) for v in (lay.perm, lay.inv_perm, lay.m0))
-        self.perm, self.inv_perm, self.m0 = cache[dev]
+            cache[dev] = tuple(torch.tensor(v, device=dev, dtype=torch.long) for v in (lay.perm, lay.inv_perm, lay.m0)) \
+                + (torch.tensor(lay.inv_perm, device=dev, dtype=torch.int32),)
+        self.perm, self.inv_perm, self.m0, self.order = cache[dev]
+        # general operators: edge irreps stay in the m-primary order of the SO(2) convolutions end to end
+        # (the rotation writes / reads rows through `order`, the attention grid's columns are permuted
+        # once), so no feature permutation runs per convolution; the lmax-2 operators work l-primary
+        self.mprimary = self.general
+        ta, fa = ga.to_grid_mat.reshape(-1, nr), ga.from_grid_mat.reshape(-1, nr)
+        if self.mprimary:
+            ta, fa = ta[:, self.perm.to(ta.device)], fa[:, self.perm.to(fa.device)]
+        self.grid_attn = (_f(ta), _f(fa))
+        self.grid_ffn = (_f(gf.to_grid_mat.reshape(-1, nf)), _f(gf.from_grid_mat.reshape(-1, nf)))
 
     def rotate(self, x):
         """SO3_Rotation.rotate (so3.py:485-505): [E][(lmax+1)^2][C] -> the kept rows [E][R][C]."""
         if self.general:
-            return _RotateGFn.apply(x, self.D, self.lay, 0, 0)
+            return _RotateGFn.apply(x, self.D, self.lay, 0, 0, self.order)
         return _RotateFn.apply(x, self.D, 0, 0)
 
     def rotate_inv(self, y):
         """SO3_Rotation.rotate_inv with get_rotate_inv_rescale (so3.py:507-531)."""
         if self.general:
-            return _RotateGFn.apply(y, self.D, self.lay, 1, 1)
+            return _RotateGFn.apply(y, self.D, self.lay, 1, 1, self.order)
         return _RotateFn.apply(y, self.D, 1, 1)
 
     # ---------------------------------------------------------------- building blocks
@@ -314,7 +324,7 @@ class _Step:
         fc_m0, every m > 0 pair (+m, -m) through its SO2_m_Convolution as a complex product."""
         E, _, cin = x.shape
         lay = self.lay
-        xm = x[:, self.perm]
+        xm = x if self.mprimary else x[:, self.perm]
         rad = self.rad_func(conv.rad_func, x_edge) if x_edge is not None else None
         n0 = lay.m_size[0]
         x0 = xm[:, :n0].reshape(E, n0 * cin)
@@ -332,7 +342,8 @@ class _Step:
             xr, xi = y[..., :nm * cout], y[..., nm * cout:]
             outs.append(torch.stack([xr[:, 0] - xi[:, 1], xr[:, 1] + xi[:, 0]], 1).reshape(E, 2 * nm, cout))
             off, roff = off + 2 * nm, roff + nm * cin
-        return torch.cat(outs, 1)[:, self.inv_perm], extra
+        out = torch.cat(outs, 1)
+        return (out if self.mprimary else out[:, self.inv_perm]), extra
 
     def so3_linear(self, lin, x):
         """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin]."""
@@ -406,7 +417,10 @@ class _Step:
         ed, E, V, C = self.m.edge_degree_embedding, self.E, self.V, self.m.sphere_channels
         lay = self.lay
         r = self.rad_func(ed.rad_func, self.x_edge(ed)).view(E, lay.m_size[0], C)
-        red = r.new_zeros(E, lay.n_red, C).index_copy(1, self.m0, r)             # the m = 0 slots
+        if self.mprimary:                                                      # m = 0 rows come first
+            red = torch.cat([r, r.new_zeros(E, lay.n_red - lay.m_size[0], C)], 1)
+        else:
+            red = r.new_zeros(E, lay.n_red, C).index_copy(1, self.m0, r)         # the m = 0 slots
         y = self.rotate_inv(red)
         out = _SegSumFn.apply(y.reshape(E, lay.n_full * C), self.g.dst, self.g.dptr, self.g.deid,
                               V).view(V, lay.n_full, C)

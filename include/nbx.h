@@ -470,9 +470,12 @@ int nbx_eqv2_wigner(int64_t E, int32_t lmax, int32_t mmax, const float* rot, int
 /* rotate (inverse = 0: out [E][R][C] = dsel in, in [E][(lmax+1)^2][C] with ld_in floats per edge) and
  * rotate_inv (inverse = 1: out [E][(lmax+1)^2][C] = dsel^T in, in [E][R][C]); rescale = 1 multiplies
  * degree l > mmax by float32(sqrt((2l+1)/(2 mmax+1))) (get_rotate_inv_rescale, so3.py:160-185), so
- * each direction with the same rescale is the other's adjoint. */
+ * each direction with the same rescale is the other's adjoint.  order [R] (nullable): the row of the
+ * [E][R][C] side that holds kept coefficient k (l-primary) -- the m-primary order of SO2_Convolution
+ * (so3.py:30-115 to_m) keeps the SO(2) blocks contiguous. */
 int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel, const float* in,
-                            int64_t ld_in, float* out, int32_t inverse, int32_t rescale, void* stream);
+                            int64_t ld_in, float* out, int32_t inverse, int32_t rescale, const int32_t* order,
+                            void* stream);
 
 /* EquivariantRMSNormArraySphericalHarmonicsV2 (layer_norm.py:327-441) of X [V][(lmax+1)^2][C], any C:
  * weight [lmax+1][C], bias [C], balance weights float32(1/(2l+1)) / (lmax+1); save [2][V]; backward

@@ -45,10 +45,18 @@ def _rotate(X, D, inverse, rescale):
     return torch.bmm(D.transpose(1, 2) * (EQ.Layout(2, 1).rescale[None] if rescale else 1.0), X)
 
 
-def _rotate_general(X, D, lay, inverse, rescale):
-    """nbx_eqv2_rotate_general on dense kept rows D [E][R][(lmax+1)^2]."""
+def _rotate_general(X, D, lay, inverse, rescale, order=None):
+    """nbx_eqv2_rotate_general on dense kept rows D [E][R][(lmax+1)^2]; the [E][R] side's row of kept
+    coefficient k is order[k] (None: k)."""
     if not inverse:
-        return torch.bmm(D, X)
+        y = torch.bmm(D, X)
+        if order is not None:
+            out = torch.empty_like(y)
+            out[:, order.long()] = y
+            return out
+        return y
+    if order is not None:
+        X = X[:, order.long()]
     return torch.bmm(D.transpose(1, 2) * (EQ.Layout(lay.lmax, lay.mmax).rescale[None] if rescale else 1.0), X)
 
 
@@ -91,6 +99,8 @@ def torch_ops(monkeypatch):
         ctx = EQ.Ctx(cfg, dict(model.state_dict()), pos, vel, charges, B, N, gauge)
         self.D = ctx.D[:, EQ.Layout(lay.lmax, lay.mmax).sel, :]
         self.perm, self.inv_perm, self.m0 = (torch.tensor(v) for v in (lay.perm, lay.inv_perm, lay.m0))
+        self.order = torch.tensor(lay.inv_perm, dtype=torch.int32)
+        self.mprimary = self.general
         z = ctx.z
         self.g = _G(torch.stack([ctx.src, ctx.dst]), self.V)
         self.gz = _G(torch.stack([z[ctx.src], z[ctx.dst]]), model.max_num_elements)
@@ -101,7 +111,10 @@ def torch_ops(monkeypatch):
         ta, fa = EQ.grid_mats(lay.lmax, lay.mmax)
         tf, ff = EQ.grid_mats(lay.lmax, lay.lmax)
         nr, nf = lay.n_red, lay.n_full
-        self.grid_attn, self.grid_ffn = (ta.reshape(-1, nr), fa.reshape(-1, nr)), (tf.reshape(-1, nf), ff.reshape(-1, nf))
+        ta, fa = ta.reshape(-1, nr), fa.reshape(-1, nr)
+        if self.mprimary:
+            ta, fa = ta[:, self.perm], fa[:, self.perm]
+        self.grid_attn, self.grid_ffn = (ta, fa), (tf.reshape(-1, nf), ff.reshape(-1, nf))
     monkeypatch.setattr(T._Step, "__init__", step_init)
 
 

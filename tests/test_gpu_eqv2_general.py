@@ -129,6 +129,13 @@ def test_general_operators_match_torch(hip_device, lmax, mmax):
     _close(got_i, ref_i, 1e-5, "rotate_inv")
     _close(xd.grad, x.grad, 1e-5, "rotate adjoint")
     _close(yd.grad, y.grad, 1e-5, "rotate_inv adjoint")
+    # the m-primary row order of the SO(2) convolutions: rows permuted, values unchanged
+    order = torch.tensor(lay.inv_perm, dtype=torch.int32, device=dev)
+    perm = torch.tensor(lay.perm, device=dev)
+    with torch.no_grad():
+        torch.testing.assert_close(T._RotateGFn.apply(xd, D, lay, 0, 0, order), got_r[:, perm], rtol=0, atol=0)
+        torch.testing.assert_close(T._RotateGFn.apply(yd[:, perm].contiguous(), D, lay, 1, 1, order), got_i,
+                                   rtol=0, atol=0)
     for mm, I in ((mmax, lay.n_red), (lmax, lay.n_full)):
         to, fr = EQ.grid_mats(lmax, mm)
         h = torch.randn(E, I, C, dtype=torch.float64, requires_grad=True)
