@@ -136,6 +136,11 @@ _SIGNATURES = {
                                             c_sz, c_p]),
     "nbx_bn_train_backward": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz,
                                              c_p]),
+    "nbx_bn_train_sums": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_bn_train_apply": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p,
+                                          c_p]),
+    "nbx_bn_train_param_grads": (ctypes.c_int, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "nbx_bn_train_backward_apply": (ctypes.c_int, [c_i64, c_i32] + [c_p] * 10),
     "nbx_gather_rows": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p]),
     "nbx_segment_sum": (ctypes.c_int, [c_i64, c_i32, c_p, c_p, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_i32, c_p]),
     "nbx_segnn_train_featurize": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,

@@ -442,11 +442,12 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(int64_t rows, int M, co
 }
 
 // save [3][M] = (mu, 1/sqrt(var + eps), 1/sqrt(n + eps)); running stats r <- (1 - m) r + m stat
-__global__ void bn_stats_kernel(int nb, int64_t rows, int M, const double* __restrict__ part, float eps,
+__global__ void bn_stats_kernel(int nb, int64_t rows_arg, int M, const double* __restrict__ part, float eps,
                                 float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
-                                float* __restrict__ save) {
+                                float* __restrict__ save, const double* __restrict__ count) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= M) return;
+    const double rows = count ? *count : (double)rows_arg;   // SyncBN: the all-reduced row count
     double a = 0.0, b = 0.0, e = 0.0;
 #pragma unroll 8
     for (int i = 0; i < nb; ++i) {
@@ -486,19 +487,39 @@ __global__ void bn_apply_train_kernel(int64_t rows, int M, const float* __restri
 __global__ void bn_bwd_apply_kernel(int64_t rows, int M, const float* __restrict__ S, const float* __restrict__ V,
                                     const float* __restrict__ save, const float* __restrict__ weight,
                                     const double* __restrict__ sums, const float* __restrict__ dOS,
-                                    const float* __restrict__ dOV, float* __restrict__ dS, float* __restrict__ dV) {
+                                    const float* __restrict__ dOV, float* __restrict__ dS, float* __restrict__ dV,
+                                    const double* __restrict__ count) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= rows * M) return;
     const int c = (int)(i % M);
     const int64_t pv = rows * M;
+    const double n = count ? *count : (double)rows;           // SyncBN: means over every rank's rows
     const float mu = save[c], inv = save[M + c], invv = save[2 * M + c];
-    const float mdy = (float)(sums[c] / rows), mdyx = (float)(sums[M + c] / rows);
+    const float mdy = (float)(sums[c] / n), mdyx = (float)(sums[M + c] / n);
     const float xh = (S[i] - mu) * inv;
     dS[i] = weight[c] * inv * (dOS[i] - mdy - xh * mdyx);
     const float wv = weight[M + c];
-    const float cv = (float)(sums[2 * M + c] / (3.0 * rows)) * invv * invv;
+    const float cv = (float)(sums[2 * M + c] / (3.0 * n)) * invv * invv;
 #pragma unroll
     for (int k = 0; k < 3; ++k) dV[k * pv + i] = wv * invv * (dOV[k * pv + i] - V[k * pv + i] * cv);
+}
+
+// fixed-order sum of the per-block partials into sums [3][M] (+ sums[3M] = rows when count_slot)
+__global__ void bn_sum_kernel(int nb, int64_t rows, int M, const double* __restrict__ part, double* __restrict__ sums) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0) sums[3 * M] = (double)rows;
+    if (c >= M) return;
+    double a = 0.0, b = 0.0, e = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < nb; ++i) {
+        const double* p = part + (int64_t)i * 3 * M;
+        a += p[c];
+        b += p[M + c];
+        e += p[2 * M + c];
+    }
+    sums[c] = a;
+    sums[M + c] = b;
+    sums[2 * M + c] = e;
 }
 
 __global__ void bn_param_grad_kernel(int nb, int M, const double* __restrict__ part, const float* __restrict__ save,
@@ -866,7 +887,7 @@ extern "C" int nbx_bn_train_forward(int64_t rows, int32_t M, const float* S, con
                        nullptr, part);
     NBX_LAUNCH_CHECK("bn_partial");
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk(M)), dim3(256), 0, st, nb, rows, M, part, eps, momentum, running_mean,
-                       running_var, save);
+                       running_var, save, (const double*)nullptr);
     NBX_LAUNCH_CHECK("bn_stats");
     hipLaunchKernelGGL(bn_apply_train_kernel, dim3(nblk(rows * M)), dim3(256), 0, st, rows, M, S, V, save, weight, bias,
                        OS, OV);
@@ -891,8 +912,60 @@ extern "C" int nbx_bn_train_backward(int64_t rows, int32_t M, const float* S, co
     hipLaunchKernelGGL(bn_param_grad_kernel, dim3(nblk(M)), dim3(256), 0, st, nb, M, part, save, sums, dweight, dbias);
     NBX_LAUNCH_CHECK("bn_param_grad");
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(rows * M)), dim3(256), 0, st, rows, M, S, V, save, weight, sums,
-                       dOS, dOV, dS, dV);
+                       dOS, dOV, dS, dV, (const double*)nullptr);
     NBX_LAUNCH_CHECK("bn_bwd_apply");
+    return NBX_OK;
+}
+
+// ---- SyncBN training (sharded train-mode BatchNorm): the caller all-reduces the sums between the calls
+extern "C" int nbx_bn_train_sums(int64_t rows, int32_t M, const float* S, const float* V, const float* dOS,
+                                 const float* dOV, const float* save, double* sums, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+    NBX_CHECK_ARG(rows > 0 && M > 0 && sums, "nbx_bn_train_sums: need rows > 0, M > 0 and sums");
+    NBX_CHECK_ARG(!dOS == !dOV && (!dOS || save), "nbx_bn_train_sums: the backward sums need dOS, dOV and save");
+    const int nb = (int)((rows + BN_ROWS - 1) / BN_ROWS);
+    NBX_CHECK_ARG(workspace && workspace_bytes >= (size_t)(nb + 1) * 3 * M * sizeof(double),
+                  "nbx_bn_train_sums: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    double* part = (double*)workspace;
+    hipLaunchKernelGGL(bn_partial_kernel, dim3((unsigned)nb, (unsigned)((M + 63) / 64)), dim3(256), 0, st, rows, M, S, V,
+                       dOS, dOV, save, part);
+    NBX_LAUNCH_CHECK("bn_partial(sums)");
+    hipLaunchKernelGGL(bn_sum_kernel, dim3(nblk(M)), dim3(256), 0, st, nb, rows, M, part, sums);
+    NBX_LAUNCH_CHECK("bn_sum");
+    return NBX_OK;
+}
+
+extern "C" int nbx_bn_train_apply(int64_t rows, int32_t M, const float* S, const float* V, const float* weight,
+                                  const float* bias, const double* sums, float* running_mean, float* running_var,
+                                  float eps, float momentum, float* save, float* OS, float* OV, void* stream) {
+    NBX_CHECK_ARG(rows > 0 && M > 0 && sums, "nbx_bn_train_apply: need rows > 0, M > 0 and sums");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk(M)), dim3(256), 0, st, 1, rows, M, sums, eps, momentum, running_mean,
+                       running_var, save, sums + 3 * M);
+    NBX_LAUNCH_CHECK("bn_stats(sync)");
+    hipLaunchKernelGGL(bn_apply_train_kernel, dim3(nblk(rows * M)), dim3(256), 0, st, rows, M, S, V, save, weight, bias,
+                       OS, OV);
+    NBX_LAUNCH_CHECK("bn_apply_train(sync)");
+    return NBX_OK;
+}
+
+extern "C" int nbx_bn_train_param_grads(int32_t M, const float* save, const double* local_sums, double* scratch,
+                                        float* dweight, float* dbias, void* stream) {
+    NBX_CHECK_ARG(M > 0 && save && local_sums && scratch && dweight && dbias, "nbx_bn_train_param_grads: bad arguments");
+    hipLaunchKernelGGL(bn_param_grad_kernel, dim3(nblk(M)), dim3(256), 0, (hipStream_t)stream, 1, M, local_sums, save,
+                       scratch, dweight, dbias);
+    NBX_LAUNCH_CHECK("bn_param_grad(sync)");
+    return NBX_OK;
+}
+
+extern "C" int nbx_bn_train_backward_apply(int64_t rows, int32_t M, const float* S, const float* V,
+                                           const float* weight, const float* save, const double* sums,
+                                           const float* dOS, const float* dOV, float* dS, float* dV, void* stream) {
+    NBX_CHECK_ARG(rows > 0 && M > 0 && sums, "nbx_bn_train_backward_apply: need rows > 0, M > 0 and sums");
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(rows * M)), dim3(256), 0, (hipStream_t)stream, rows, M, S, V, save,
+                       weight, sums, dOS, dOV, dS, dV, sums + 3 * M);
+    NBX_LAUNCH_CHECK("bn_bwd_apply(sync)");
     return NBX_OK;
 }
 

@@ -679,9 +679,8 @@ class SEGNN(nn.Module):
         if use_training_path(self):   # train_dispatch.py: autograd on + trainable params
             # training step (trainer.py:233-358): the forward runs on the native training operators
             # with autograd (segnn_train.py), so loss.backward() reaches every parameter
-            if self._bn_group is not None and self._bn_batch():
-                raise NotImplementedError("native SEGNN training step: SyncBN is not supported (per-rank "
-                                          "BatchNorm statistics, data-parallel gradients)")
+            # with enable_sync_batchnorm() the step's batch statistics span every rank of the group
+            # (segnn_train._SyncBNFn: one all-reduce of the fp64 sums per BatchNorm, forward and backward)
             from . import segnn_train
             return segnn_train.train_forward(self, p, v, m, edge_index).to(out_dtype)
         out = torch.empty(V, 6, device=device, dtype=torch.float32)

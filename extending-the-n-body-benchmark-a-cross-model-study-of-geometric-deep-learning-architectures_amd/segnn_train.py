@@ -222,6 +222,60 @@ class _BNFn(torch.autograd.Function):
         return dS, dV, dw, db, None, None, None, None
 
 
+class _SyncBNFn(torch.autograd.Function):
+    """_BNFn with the batch statistics of every rank of ``group`` (sharded train-mode BatchNorm): the
+    local fixed-order sums [3M + 1] (with the row count) are all-reduced between nbx_bn_train_sums and
+    nbx_bn_train_apply; the backward all-reduces (sum dy, sum dy xhat, sum dy_v . v) the same way, while
+    dweight / dbias come from the local sums (the data-parallel gradient all-reduce sums them)."""
+
+    @staticmethod
+    def forward(ctx, S, V, weight, bias, rm, rv, eps, momentum, group):
+        import torch.distributed as dist
+        L = _lib.lib()
+        rows, M = S.shape
+        dev = S.device
+        n = _lib.c_sz()
+        _lib.check(L.nbx_bn_train_workspace_bytes(rows, M, ctypes.byref(n)), "nbx_bn_train_workspace_bytes")
+        ws = _ws(n.value, dev)
+        sums = torch.empty(3 * M + 1, device=dev, dtype=torch.float64)
+        _lib.check(L.nbx_bn_train_sums(rows, M, _dp(S), _dp(V), None, None, None, _dp(sums), _dp(ws), n.value, _st(S)),
+                   "nbx_bn_train_sums")
+        dist.all_reduce(sums, group=group)
+        save = torch.empty(3, M, device=dev, dtype=_f32)
+        OS, OV = torch.empty_like(S), torch.empty_like(V)
+        _lib.check(L.nbx_bn_train_apply(rows, M, _dp(S), _dp(V), _dp(weight), _dp(bias), _dp(sums), _dp(rm), _dp(rv),
+                                        float(eps), float(momentum), _dp(save), _dp(OS), _dp(OV), _st(S)),
+                   "nbx_bn_train_apply")
+        ctx.save_for_backward(S, V, weight, save)
+        ctx.wsb, ctx.group = n.value, group
+        return OS, OV
+
+    @staticmethod
+    def backward(ctx, dOS, dOV):
+        import torch.distributed as dist
+        L = _lib.lib()
+        S, V, weight, save = ctx.saved_tensors
+        rows, M = S.shape
+        dev = S.device
+        dOS = dOS.contiguous() if dOS is not None else torch.zeros_like(S)
+        dOV = dOV.contiguous() if dOV is not None else torch.zeros_like(V)
+        ws = _ws(ctx.wsb, dev)
+        local = torch.empty(3 * M + 1, device=dev, dtype=torch.float64)
+        _lib.check(L.nbx_bn_train_sums(rows, M, _dp(S), _dp(V), _dp(dOS), _dp(dOV), _dp(save), _dp(local), _dp(ws),
+                                       ctx.wsb, _st(S)), "nbx_bn_train_sums")
+        dw = torch.empty(2 * M, device=dev, dtype=_f32)
+        db = torch.empty(M, device=dev, dtype=_f32)
+        scratch = torch.empty(3 * M, device=dev, dtype=torch.float64)
+        _lib.check(L.nbx_bn_train_param_grads(M, _dp(save), _dp(local), _dp(scratch), _dp(dw), _dp(db), _st(S)),
+                   "nbx_bn_train_param_grads")
+        dist.all_reduce(local, group=ctx.group)
+        dS, dV = torch.empty_like(S), torch.empty_like(V)
+        _lib.check(L.nbx_bn_train_backward_apply(rows, M, _dp(S), _dp(V), _dp(weight), _dp(save), _dp(local),
+                                                 _dp(dOS), _dp(dOV), _dp(dS), _dp(dV), _st(S)),
+                   "nbx_bn_train_backward_apply")
+        return dS, dV, dw, db, None, None, None, None, None
+
+
 class Graph:
     """Index tables of one edge list: src / dst int32 [E] and CSRs of the edges by destination and by
     source (ptr [V + 1], eid [E]), built on the device without a host synchronisation."""
@@ -367,7 +421,13 @@ def _batch_norm(model, bn, S, V, batch_stats):
     shadow = rm.dtype != _f32 or not rm.is_contiguous()
     if shadow:
         rm, rv = rm.to(_f32).contiguous(), rv.to(_f32).contiguous()
-    OS, OV = _BNFn.apply(S.contiguous(), V.contiguous(), w.contiguous(), b.contiguous(), rm, rv, bn.eps, bn.momentum)
+    group = getattr(model, "_bn_group", None)
+    if group is not None:    # SyncBN (enable_sync_batchnorm): statistics of the whole sharded batch
+        OS, OV = _SyncBNFn.apply(S.contiguous(), V.contiguous(), w.contiguous(), b.contiguous(), rm, rv, bn.eps,
+                                 bn.momentum, group)
+    else:
+        OS, OV = _BNFn.apply(S.contiguous(), V.contiguous(), w.contiguous(), b.contiguous(), rm, rv, bn.eps,
+                             bn.momentum)
     if shadow:
         with torch.no_grad():
             bn.running_mean.copy_(rm)

@@ -330,6 +330,25 @@ int nbx_bn_train_backward(int64_t rows, int32_t M, const float* S, const float* 
                           const float* save, const float* dOS, const float* dOV, float* dS, float* dV, float* dweight,
                           float* dbias, void* workspace, size_t workspace_bytes, void* stream);
 
+/* SyncBN training step (sharded train-mode BatchNorm; the reference trains on one device, so the
+ * statistics of a sharded step are those of the whole global batch): nbx_bn_train_sums writes
+ * sums [3M + 1] fp64 -- the forward sums (sum s, sum s^2, sum |v|^2) when dOS / dOV are NULL, the
+ * backward sums (sum dy_s, sum dy_s xhat, sum dy_v . v) otherwise -- and sums[3M] = rows; the caller
+ * all-reduces them over the ranks (one collective of 3M + 1 doubles); nbx_bn_train_apply /
+ * nbx_bn_train_backward_apply then normalise / back-propagate with the all-reduced sums and count.
+ * nbx_bn_train_param_grads: dweight / dbias from the LOCAL backward sums (the data-parallel gradient
+ * all-reduce sums them over the ranks); scratch [3M] doubles. */
+int nbx_bn_train_sums(int64_t rows, int32_t M, const float* S, const float* V, const float* dOS, const float* dOV,
+                      const float* save, double* sums, void* workspace, size_t workspace_bytes, void* stream);
+int nbx_bn_train_apply(int64_t rows, int32_t M, const float* S, const float* V, const float* weight, const float* bias,
+                       const double* sums, float* running_mean, float* running_var, float eps, float momentum,
+                       float* save, float* OS, float* OV, void* stream);
+int nbx_bn_train_param_grads(int32_t M, const float* save, const double* local_sums, double* scratch, float* dweight,
+                             float* dbias, void* stream);
+int nbx_bn_train_backward_apply(int64_t rows, int32_t M, const float* S, const float* V, const float* weight,
+                                const float* save, const double* sums, const float* dOS, const float* dOV, float* dS,
+                                float* dV, void* stream);
+
 /* Message passing (MessagePassing aggr="add", segnn.py:249): out[r] = in[idx[r]] per plane (x_i = x[dst],
  * x_j = x[src]) and out[n] (+)= sum over j in [ptr[n], ptr[n+1]) of in[eid[j]] (a CSR of the edges by
  * destination / source; the aggregation and the gathers' adjoint).  planes: component planes, strides

@@ -227,3 +227,92 @@ def test_sharded_run_inference_native_segnn_matches_single_process(hip_device, t
         np.testing.assert_allclose(res[r][0], locs[1], rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(res[r][1], vels[1], rtol=1e-4, atol=1e-5)
     assert np.abs(locs[1][:, 1:] - locs[1][:, :1]).max() > 1e-3    # the rollout moved the bodies
+
+
+def _train_inputs(b, seed=5):
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal((b, N, 3)), rng.standard_normal((b, N, 3)) * 0.3,
+            rng.integers(1, 4, (b, N, 1)).astype(np.float64), rng.standard_normal((b * N, 6)) * 0.1)
+
+
+def _train_step(model, loc, vel, mass, tgt, device):
+    """One grad-mode forward (the native training operators) + MSE loss + backward -> (pred, loss,
+    grads, running stats)."""
+    import nbody_amd.graph as G
+
+    class Graph:
+        pass
+    b = loc.shape[0]
+    g = Graph()
+    g.pos = torch.tensor(loc.reshape(-1, 3), dtype=torch.float32, device=device)
+    g.vel = torch.tensor(vel.reshape(-1, 3), dtype=torch.float32, device=device)
+    g.mass = torch.tensor(mass.reshape(-1, 1), dtype=torch.float32, device=device)
+    g.edge_index = G.fc_edge_index(b, N, device)
+    model.zero_grad(set_to_none=True)
+    pred = model(g)
+    loss = torch.nn.functional.mse_loss(pred, torch.tensor(tgt, dtype=torch.float32, device=device))
+    loss.backward()
+    grads = {k: p.grad.double().cpu().numpy() for k, p in model.named_parameters() if p.grad is not None}
+    stats = {k: v.double().cpu().numpy() for k, v in model.state_dict().items() if "running" in k}
+    return pred.detach().double().cpu().numpy(), float(loss), grads, stats
+
+
+def _train_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    from nbody_amd.segnn import SEGNN
+    dev = torch.device("cuda:0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        loc, vel, mass, tgt = _train_inputs(B)
+        sl = slice(rank * B // world, (rank + 1) * B // world)
+        torch.manual_seed(0)
+        model = SEGNN(hidden_features=64, num_layers=3).to(dev).train().enable_sync_batchnorm()
+        pred, loss, grads, stats = _train_step(model, loc[sl], vel[sl], mass[sl], tgt[sl.start * N:sl.stop * N], dev)
+        from nbody_amd.parallel import allreduce_gradients
+        allreduce_gradients(list(model.parameters()))             # data-parallel average
+        avg = {k: p.grad.double().cpu().numpy() for k, p in model.named_parameters() if p.grad is not None}
+        q.put((rank, (pred, loss, avg, stats)))
+        model.disable_sync_batchnorm()
+    except Exception as e:  # surfaced by the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_syncbn_training_step_two_ranks_reproduce_full_batch(hip_device):
+    """Sharded SEGNN training step with SyncBN (segnn_train._SyncBNFn: nbx_bn_train_sums -> all-reduce of
+    the fp64 sums and row count -> nbx_bn_train_apply, and the same for the backward sums): two gloo
+    ranks on half batches each, gradients averaged over the ranks, reproduce the single-process
+    full-batch step -- predictions, the (equal-halves) mean loss, every parameter gradient and the
+    running statistics (the reference trains on one device with the statistics of the whole batch,
+    trainer.py:233-358)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert not isinstance(res[r], str), res[r]
+    from nbody_amd.segnn import SEGNN
+    loc, vel, mass, tgt = _train_inputs(B)
+    torch.manual_seed(0)
+    model = SEGNN(hidden_features=64, num_layers=3).to(hip_device).train()
+    pred, loss, grads, stats = _train_step(model, loc, vel, mass, tgt, hip_device)
+    got = np.concatenate([res[0][0], res[1][0]])
+    scale = np.abs(pred).max(0)
+    assert (np.abs(got - pred).max(0) <= 1e-5 * scale + 1e-7).all(), np.abs(got - pred).max(0) / scale
+    assert abs(0.5 * (res[0][1] + res[1][1]) - loss) <= 1e-5 * abs(loss)
+    for k, g in grads.items():
+        for r in (0, 1):   # both ranks hold the averaged gradient
+            e = np.abs(res[r][2][k] - g).max()
+            assert e <= 2e-4 * np.abs(g).max() + 1e-7, (k, e, np.abs(g).max())
+    for k, v in stats.items():
+        for r in (0, 1):
+            np.testing.assert_allclose(res[r][3][k], v, rtol=1e-5, atol=1e-7)
