@@ -254,7 +254,7 @@ def _train_step(model, loc, vel, mass, tgt, device):
     loss.backward()
     grads = {k: p.grad.double().cpu().numpy() for k, p in model.named_parameters() if p.grad is not None}
     stats = {k: v.double().cpu().numpy() for k, v in model.state_dict().items() if "running" in k}
-    return pred.detach().double().cpu().numpy(), float(loss), grads, stats
+    return pred.detach().double().cpu().numpy(), float(loss.detach()), grads, stats
 
 
 def _train_worker(rank, world, port, q):
