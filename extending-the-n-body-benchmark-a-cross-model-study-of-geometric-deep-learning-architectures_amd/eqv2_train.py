@@ -278,8 +278,9 @@ class _Step:
         cache = model.__dict__.setdefault("_eqv2_index_cache", {})
         if dev not in cache:
             cache[dev] = tuple(torch.tensor(v, device=dev, dtype=torch.long) for v in (lay.perm, lay.inv_perm, lay.m0)) \
-                + (torch.tensor(lay.inv_perm, device=dev, dtype=torch.int32),)
-        self.perm, self.inv_perm, self.m0, self.order = cache[dev]
+                + (torch.tensor(lay.inv_perm, device=dev, dtype=torch.int32),
+                   torch.tensor([-1.0, 1.0], device=dev, dtype=_f32).view(1, 2, 1))
+        self.perm, self.inv_perm, self.m0, self.order, self.sign = cache[dev]
         # general operators: edge irreps stay in the m-primary order of the SO(2) convolutions end to end
         # (the rotation writes / reads rows through `order`, the attention grid's columns are permuted
         # once), so no feature permutation runs per convolution; the lmax-2 operators work l-primary
@@ -319,40 +320,47 @@ class _Step:
         return linear(h, net[6].weight, net[6].bias)
 
     def so2_conv(self, conv, x, x_edge, cout, n_extra=0):
-        """SO2_Convolution (so2_ops.py:78-156) of x [E][R][cin] (kept coefficients, l-primary) ->
-        ([E][R][cout], extra): m-primary order (CoefficientMappingModule), the m = 0 block through
-        fc_m0, every m > 0 pair (+m, -m) through its SO2_m_Convolution as a complex product."""
+        """SO2_Convolution (so2_ops.py:78-156) of x [E][R][cin] (kept coefficients) -> ([E][R][cout], extra):
+        m-primary order (CoefficientMappingModule), the m = 0 block through fc_m0, every m > 0 pair
+        (+m, -m) through its SO2_m_Convolution as a complex product.  The per-order blocks are taken
+        with one torch.split (one backward op instead of a zero-fill + copy per slice)."""
         E, _, cin = x.shape
         lay = self.lay
         xm = x if self.mprimary else x[:, self.perm]
-        rad = self.rad_func(conv.rad_func, x_edge) if x_edge is not None else None
         n0 = lay.m_size[0]
-        x0 = xm[:, :n0].reshape(E, n0 * cin)
+        parts = torch.split(xm, [n0] + [2 * lay.m_size[m] for m in range(1, lay.mmax + 1)], dim=1)
+        rad = self.rad_func(conv.rad_func, x_edge) if x_edge is not None else None
+        rparts = torch.split(rad, [n0 * cin] + [lay.m_size[m] * cin for m in range(1, lay.mmax + 1)], dim=1) \
+            if rad is not None else None
+        x0 = parts[0].reshape(E, n0 * cin)
         if rad is not None:
-            x0 = x0 * rad[:, :n0 * cin]
+            x0 = x0 * rparts[0]
         y0 = linear(x0, conv.fc_m0.weight, conv.fc_m0.bias)
-        extra, y0 = y0[:, :n_extra], y0[:, n_extra:].reshape(E, n0, cout)
-        outs, off, roff = [y0], n0, n0 * cin
+        extra, y0 = torch.split(y0, [n_extra, n0 * cout], dim=1)
+        outs = [y0.reshape(E, n0, cout)]
         for m in range(1, lay.mmax + 1):
             nm = lay.m_size[m]
-            xmm = xm[:, off:off + 2 * nm].reshape(E, 2, nm * cin)
+            xmm = parts[m].reshape(E, 2, nm * cin)
             if rad is not None:
-                xmm = xmm * rad[:, None, roff:roff + nm * cin]
-            y = linear(xmm.reshape(2 * E, nm * cin), conv.so2_m_conv[m - 1].fc.weight).view(E, 2, 2 * nm * cout)
-            xr, xi = y[..., :nm * cout], y[..., nm * cout:]
-            outs.append(torch.stack([xr[:, 0] - xi[:, 1], xr[:, 1] + xi[:, 0]], 1).reshape(E, 2 * nm, cout))
-            off, roff = off + 2 * nm, roff + nm * cin
+                xmm = xmm * rparts[m][:, None]
+            y = linear(xmm.reshape(2 * E, nm * cin), conv.so2_m_conv[m - 1].fc.weight).view(E, 2, 2, nm * cout)
+            xr, xi = y.unbind(2)         # [E][row (+m, -m)][nm cout]: real / imaginary halves of fc
+            # (+m, -m) outputs = (xr[+m] - xi[-m], xr[-m] + xi[+m])
+            outs.append((xr + xi.flip(1) * self.sign).reshape(E, 2 * nm, cout))
         out = torch.cat(outs, 1)
         return (out if self.mprimary else out[:, self.inv_perm]), extra
 
-    def so3_linear(self, lin, x):
-        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin]."""
+    def so3_linear(self, lin, x, parts=None):
+        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin];
+        ``parts``: x already split by degree."""
         V, _, cin = x.shape
         W = lin.weight
-        ys = [linear(x[:, 0], W[0], lin.bias).view(V, 1, -1)]
+        if parts is None:
+            parts = torch.split(x, [2 * l + 1 for l in range(self.lay.lmax + 1)], dim=1)
+        ys = [linear(parts[0].reshape(V, cin), W[0], lin.bias).view(V, 1, -1)]
         for l in range(1, self.lay.lmax + 1):
             n = 2 * l + 1
-            ys.append(linear(x[:, l * l:l * l + n].reshape(n * V, cin), W[l]).view(V, n, -1))
+            ys.append(linear(parts[l].reshape(n * V, cin), W[l]).view(V, n, -1))
         return torch.cat(ys, 1)
 
     def rms_norm(self, norm, x):
@@ -387,9 +395,9 @@ class _Step:
         xs, xd = gather(x, g, "s"), gather(x, g, "d")
         msg = self.rotate(torch.cat([xs, xd], 2))
         msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
-        gating, a_in = extra[:, nh * na:], extra[:, :nh * na]
-        msg = torch.cat([act(gating.contiguous(), _lib.ACT_SILU)[:, None],
-                         _S2Fn.apply(msg, *self.grid_attn)[:, 1:]], 1)
+        a_in, gating = torch.split(extra, [nh * na, H], dim=1)
+        s2 = torch.split(_S2Fn.apply(msg, *self.grid_attn), [1, msg.shape[1] - 1], dim=1)[1]
+        msg = torch.cat([act(gating.contiguous(), _lib.ACT_SILU)[:, None], s2], 1)
         msg, _ = self.so2_conv(A.so2_conv_2, msg, None, nh * nv)
         a = _LayerNormFn.apply(a_in.reshape(E * nh, na).contiguous(), _f(A.alpha_norm.weight), _f(A.alpha_norm.bias),
                                A.alpha_norm.eps)
@@ -406,9 +414,12 @@ class _Step:
 
     def ffn(self, F, x):
         """FeedForwardNetwork (transformer_block.py:473-530), separable S2 activation on SO3_Grid(lmax, lmax)."""
-        gating = linear(x[:, 0], F.gating_linear.weight, F.gating_linear.bias, _lib.ACT_SILU)
-        h = self.so3_linear(F.so3_linear_1, x)
-        h = torch.cat([gating[:, None], _S2Fn.apply(h, *self.grid_ffn)[:, 1:]], 1)
+        parts = torch.split(x, [2 * l + 1 for l in range(self.lay.lmax + 1)], dim=1)
+        gating = linear(parts[0].reshape(x.shape[0], -1), F.gating_linear.weight, F.gating_linear.bias,
+                        _lib.ACT_SILU)
+        h = self.so3_linear(F.so3_linear_1, x, parts)
+        s2 = torch.split(_S2Fn.apply(h, *self.grid_ffn), [1, h.shape[1] - 1], dim=1)[1]
+        h = torch.cat([gating[:, None], s2], 1)
         return self.so3_linear(F.so3_linear_2, h)
 
     def edge_degree(self):
@@ -442,4 +453,4 @@ def train_forward(model, pos, vel, charges, B, N, gauge=None, seed=0, frame=0):
         x = st.proj_drop(st.drop_path(st.ffn(blk.ffn, st.rms_norm(blk.norm_2, y)))) + y
     x = st.rms_norm(m.norm, x)
     pred = st.attention(m.force_block, x, 2)
-    return torch.cat([pred[:, 1:4, 0], pred[:, 1:4, 1]], 1)
+    return pred[:, 1:4, :2].transpose(1, 2).reshape(V, 6)     # (force l = 1 | velocity l = 1)

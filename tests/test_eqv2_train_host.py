@@ -100,6 +100,7 @@ def torch_ops(monkeypatch):
         self.D = ctx.D[:, EQ.Layout(lay.lmax, lay.mmax).sel, :]
         self.perm, self.inv_perm, self.m0 = (torch.tensor(v) for v in (lay.perm, lay.inv_perm, lay.m0))
         self.order = torch.tensor(lay.inv_perm, dtype=torch.int32)
+        self.sign = torch.tensor([-1.0, 1.0], dtype=torch.float64).view(1, 2, 1)
         self.mprimary = self.general
         z = ctx.z
         self.g = _G(torch.stack([ctx.src, ctx.dst]), self.V)
