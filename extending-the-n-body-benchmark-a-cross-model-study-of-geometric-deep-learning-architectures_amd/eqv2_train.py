@@ -354,7 +354,7 @@ class _Step:
         """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin];
         ``parts``: x already split by degree."""
         V, _, cin = x.shape
-        W = lin.weight
+        W = lin.weight.unbind(0)      # per-degree weights (one stack in the backward, not a select each)
         if parts is None:
             parts = torch.split(x, [2 * l + 1 for l in range(self.lay.lmax + 1)], dim=1)
         ys = [linear(parts[0].reshape(V, cin), W[0], lin.bias).view(V, 1, -1)]
