@@ -487,8 +487,9 @@ class EquiformerV2_nbody(nn.Module):
     def uses_general_ops(self):
         """True when the composed path runs on the general-degree operators (nbx_eqv2_wigner /
         rotate_general / rms_norm_general) instead of the lmax 2 / mmax 1 ones."""
+        import os
         return ((self.layout.lmax, self.layout.mmax) != (2, 1) or self.sphere_channels > 128
-                or bool(self.force_general_ops))
+                or bool(self.force_general_ops) or os.environ.get("NBX_EQV2_GENERAL", "0") == "1")
 
     def wigner_table(self, device):
         """so3.wigner_table(lmax) on ``device`` (the probe constants of nbx_eqv2_wigner), cached."""

@@ -264,7 +264,11 @@ class _Step:
                                                        model.max_num_elements, _dp(rot), _dp(self.D), _dp(dist),
                                                        _dp(zn), _st(pos)), "nbx_eqv2_train_edges")
         from .graph import fc_edge_index
-        self.g = Graph(fc_edge_index(B, N, dev), V, dev)
+        # the fully-connected graph's index tables depend on (B, N) only: built once per shape and device
+        gcache = model.__dict__.setdefault("_eqv2_fc_graphs", {})
+        if (B, N, dev) not in gcache:
+            gcache[(B, N, dev)] = Graph(fc_edge_index(B, N, dev), V, dev)
+        self.g = gcache[(B, N, dev)]
         zl = zn.long()
         ze = torch.stack([zl[self.g.src.long()], zl[self.g.dst.long()]])
         self.gz = Graph(ze, model.max_num_elements, dev)          # CSRs of the edges' source / target elements
