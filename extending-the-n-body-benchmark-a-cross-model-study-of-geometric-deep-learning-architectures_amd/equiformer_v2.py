@@ -286,7 +286,12 @@ class EquiformerV2_nbody(nn.Module):
         if self._general_reason:
             raise NotImplementedError(self._general_reason)
         self.layout = so3.Layout(lmax_list[0], mmax_list[0])
-        self.force_general_ops = False    # route even lmax 2 / mmax 1 through the general operators (tests)
+        # composed path at lmax 2 / mmax 1: the general-degree operators (default; measured 7 % faster in
+        # the training step, profiles/r04/eqv2_train_glue) or the lmax-2 ones (specialised_ops = True,
+        # or NBX_EQV2_SPECIALISED=1)
+        import os
+        self.specialised_ops = os.environ.get("NBX_EQV2_SPECIALISED", "0") == "1"
+        self.force_general_ops = False
         self._wtab = None
 
         C, He = sphere_channels, edge_channels
@@ -486,10 +491,10 @@ class EquiformerV2_nbody(nn.Module):
 
     def uses_general_ops(self):
         """True when the composed path runs on the general-degree operators (nbx_eqv2_wigner /
-        rotate_general / rms_norm_general) instead of the lmax 2 / mmax 1 ones."""
-        import os
-        return ((self.layout.lmax, self.layout.mmax) != (2, 1) or self.sphere_channels > 128
-                or bool(self.force_general_ops) or os.environ.get("NBX_EQV2_GENERAL", "0") == "1")
+        rotate_general / rms_norm_general, m-primary edge irreps) instead of the lmax 2 / mmax 1 ones:
+        always outside lmax 2 / mmax 1 and C <= 128, and there unless ``specialised_ops`` is set."""
+        lmax2 = (self.layout.lmax, self.layout.mmax) == (2, 1) and self.sphere_channels <= 128
+        return not lmax2 or bool(self.force_general_ops) or not self.specialised_ops
 
     def wigner_table(self, device):
         """so3.wigner_table(lmax) on ``device`` (the probe constants of nbx_eqv2_wigner), cached."""

@@ -127,7 +127,7 @@ def test_train_forward_composition_matches_oracle(torch_ops, lmax, mmax, general
     torch.manual_seed(0)
     cfg = dict(CFG, lmax_list=[lmax], mmax_list=[mmax])
     m = EquiformerV2_nbody(**cfg, alpha_drop=0.0, drop_path_rate=0.0).double()
-    m.force_general_ops = general
+    m.specialised_ops = not general
     assert m.uses_general_ops() == general
     with torch.no_grad():
         for k, p in m.named_parameters():

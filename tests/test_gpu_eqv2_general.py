@@ -258,13 +258,16 @@ def test_training_step_gradients_match_oracle(hip_device, cfg, B, N):
 
 
 def test_general_operators_at_lmax2_agree_with_the_specialised_ones(hip_device):
-    """lmax 2 / mmax 1 through the general operators (force_general_ops) vs the specialised lmax-2
-    operators (training composition) and the fused inference kernels, same weights and gauges."""
+    """lmax 2 / mmax 1 through the general operators (the composed path's default) vs the specialised
+    lmax-2 operators (specialised_ops = True) and the fused inference kernels, same weights and gauges."""
     B, N = 3, 6
     loc, vel, mass, gauge, tgt = _inputs(B, N, seed=11)
-    spec = _train_step(_model(SMALL2, hip_device, seed=5), loc, vel, mass, gauge, tgt, hip_device)
+    ms = _model(SMALL2, hip_device, seed=5)
+    ms.specialised_ops = True
+    assert not ms.uses_general_ops()
+    spec = _train_step(ms, loc, vel, mass, gauge, tgt, hip_device)
     mg = _model(SMALL2, hip_device, seed=5)
-    mg.force_general_ops = True
+    assert mg.uses_general_ops()          # the default at lmax 2 / mmax 1 too
     gen = _train_step(mg, loc, vel, mass, gauge, tgt, hip_device)
     np.testing.assert_allclose(gen[1], spec[1], rtol=2e-5, atol=2e-6)
     for k, r in spec[2].items():
