@@ -32,6 +32,11 @@ def init_from_env(backend=None):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rk = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (several ranks on one GPU): NBX_LOCAL_DEVICE pins every rank to one device,
+    # NBX_DIST_BACKEND overrides the backend (gloo: RCCL refuses two ranks on one device)
+    if os.environ.get("NBX_LOCAL_DEVICE") is not None:
+        local = int(os.environ["NBX_LOCAL_DEVICE"])
+    backend = backend or os.environ.get("NBX_DIST_BACKEND") or None
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
