@@ -32,8 +32,15 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // contiguous dimension when VEC: 16-byte aligned operands and leading dimensions) while the current
 // one is multiplied from LDS.  The training GEMMs are small (a B=64 batch: 320-3840 rows), so the
 // grid is split along K until it holds ~256 blocks of >= 4 K steps (gemm_splits): each z writes its
-// partial tile into `part` [z][M][N] and gemm_reduce_kernel sums them in z order.
-constexpr int GB = 64, GK = 32, GT = 256;
+// partial tile into `part` [z][M][N] and gemm_reduce_kernel sums them in z order.  An opt-in variant
+// (T = 32, gemm_tile_size) uses 32 x 32 tiles of one wave when the 64 x 64 grid would not fill the chip.
+constexpr int GB = 64, GK = 32;
+
+template <int T>
+struct GemmCfg {
+    static constexpr int THREADS = (T / 32) * (T / 32) * 64;   // one wave per 32 x 32 quadrant
+    static constexpr int H = T * GK / (THREADS * 4);            // float4 groups per thread per operand
+};
 
 struct GemmArgs {
     const float* A;
@@ -47,15 +54,16 @@ struct GemmArgs {
 
 // one 64 x 64 output tile (bx, by) of K split bz of nz (the body of gemm_f32_kernel and of the
 // grouped gemm_f32_batched_kernel)
-template <bool TA, bool TB, bool VEC>
-__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int nz, float (&As)[2][GK][GB + 4],
-                                          float (&Bs)[2][GK][GB + 4]) {
+template <bool TA, bool TB, bool VEC, int T = GB>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int nz, float (&As)[2][GK][T + 4],
+                                          float (&Bs)[2][GK][T + 4]) {
+    constexpr int THREADS = GemmCfg<T>::THREADS, H = GemmCfg<T>::H, Q4 = T / 4;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t m0 = (int64_t)by * GB, n0 = (int64_t)bx * GB;
+    const int64_t m0 = (int64_t)by * T, n0 = (int64_t)bx * T;
     const int64_t k_lo = (int64_t)bz * g.kchunk;
     const int64_t k_hi = std::min<int64_t>(g.K, k_lo + g.kchunk);
     const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
-    float ra[2][4], rb[2][4];
+    float ra[H][4], rb[H][4];
     // four consecutive elements along the contiguous dimension: (row, col) of the first, its stride
     auto load4 = [&](const float* base, int64_t ld, int64_t r, int64_t c, int64_t rmax, int64_t cmax, float (&v)[4]) {
         // elements base[r * ld + c + j], valid while r < rmax and c + j < cmax
@@ -67,25 +75,30 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
             for (int j = 0; j < 4; ++j) v[j] = (r < rmax && c + j < cmax) ? base[r * ld + c + j] : 0.f;
         }
     };
+    // float4 group q = t + THREADS h of a K step: [M][K] / [N][K] operands row q / 8, k 4 (q % 8);
+    // [K][M] / [K][N] operands k q / Q4, column 4 (q % Q4)
     auto load = [&](int64_t k0) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (TA) load4(g.A, g.lda, k0 + (t >> 4) + 16 * h, m0 + (t & 15) * 4, k_hi, g.M, ra[h]);   // [K][M]
-            else load4(g.A, g.lda, m0 + (t >> 3) + 32 * h, k0 + (t & 7) * 4, g.M, k_hi, ra[h]);       // [M][K]
-            if (TB) load4(g.B, g.ldb, n0 + (t >> 3) + 32 * h, k0 + (t & 7) * 4, g.N, k_hi, rb[h]);    // [N][K]
-            else load4(g.B, g.ldb, k0 + (t >> 4) + 16 * h, n0 + (t & 15) * 4, k_hi, g.N, rb[h]);      // [K][N]
+        for (int h = 0; h < H; ++h) {
+            const int q = t + THREADS * h;
+            if (TA) load4(g.A, g.lda, k0 + q / Q4, m0 + (q % Q4) * 4, k_hi, g.M, ra[h]);   // [K][M]
+            else load4(g.A, g.lda, m0 + (q >> 3), k0 + (q & 7) * 4, g.M, k_hi, ra[h]);    // [M][K]
+            if (TB) load4(g.B, g.ldb, n0 + (q >> 3), k0 + (q & 7) * 4, g.N, k_hi, rb[h]); // [N][K]
+            else load4(g.B, g.ldb, k0 + q / Q4, n0 + (q % Q4) * 4, k_hi, g.N, rb[h]);      // [K][N]
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < H; ++h) {
+            const int q = t + THREADS * h;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (TA) As[buf][(t >> 4) + 16 * h][(t & 15) * 4 + j] = ra[h][j];
-                else As[buf][(t & 7) * 4 + j][(t >> 3) + 32 * h] = ra[h][j];
-                if (TB) Bs[buf][(t & 7) * 4 + j][(t >> 3) + 32 * h] = rb[h][j];
-                else Bs[buf][(t >> 4) + 16 * h][(t & 15) * 4 + j] = rb[h][j];
+                if (TA) As[buf][q / Q4][(q % Q4) * 4 + j] = ra[h][j];
+                else As[buf][(q & 7) * 4 + j][q >> 3] = ra[h][j];
+                if (TB) Bs[buf][(q & 7) * 4 + j][q >> 3] = rb[h][j];
+                else Bs[buf][q / Q4][(q % Q4) * 4 + j] = rb[h][j];
             }
+        }
     };
     floatx16 acc;
 #pragma unroll
@@ -123,11 +136,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
 }
 
-template <bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs g) {
-    __shared__ float As[2][GK][GB + 4];
-    __shared__ float Bs[2][GK][GB + 4];
-    gemm_tile<TA, TB, VEC>(g, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.z, As, Bs);
+template <bool TA, bool TB, bool VEC, int T = GB>
+__global__ __launch_bounds__(GemmCfg<T>::THREADS) void gemm_f32_kernel(GemmArgs g) {
+    __shared__ float As[2][GK][T + 4];
+    __shared__ float Bs[2][GK][T + 4];
+    gemm_tile<TA, TB, VEC, T>(g, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.z, As, Bs);
 }
 
 // Up to GMAXP independent GEMMs in one launch (a tensor product's scalar-row and vector-plane GEMMs,
@@ -142,9 +155,10 @@ struct GemmBatch {
     int count;
 };
 
-__global__ __launch_bounds__(GT) void gemm_f32_batched_kernel(GemmBatch b) {
-    __shared__ float As[2][GK][GB + 4];
-    __shared__ float Bs[2][GK][GB + 4];
+template <int T>
+__global__ __launch_bounds__(GemmCfg<T>::THREADS) void gemm_f32_batched_kernel(GemmBatch b) {
+    __shared__ float As[2][GK][T + 4];
+    __shared__ float Bs[2][GK][T + 4];
     const int blk = (int)blockIdx.x;
     int p = 0;
 #pragma unroll
@@ -154,14 +168,14 @@ __global__ __launch_bounds__(GT) void gemm_f32_batched_kernel(GemmBatch b) {
     const int bz = local / txy, r = local - bz * txy, by = r / b.tx[p], bx = r - by * b.tx[p];
     const GemmArgs& g = b.g[p];
     switch (b.mode[p]) {
-        case 0: gemm_tile<false, false, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        case 1: gemm_tile<true, false, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        case 2: gemm_tile<false, true, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        case 3: gemm_tile<true, true, false>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        case 4: gemm_tile<false, false, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        case 5: gemm_tile<true, false, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        case 6: gemm_tile<false, true, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
-        default: gemm_tile<true, true, true>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 0: gemm_tile<false, false, false, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 1: gemm_tile<true, false, false, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 2: gemm_tile<false, true, false, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 3: gemm_tile<true, true, false, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 4: gemm_tile<false, false, true, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 5: gemm_tile<true, false, true, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        case 6: gemm_tile<false, true, true, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
+        default: gemm_tile<true, true, true, T>(g, bx, by, bz, b.nz[p], As, Bs); break;
     }
 }
 
@@ -202,8 +216,18 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, i
     *p = beta != 0.f ? s + beta * *p : s;
 }
 
-int gemm_splits(int64_t M, int64_t N, int64_t K) {
-    const int64_t tiles = ((M + GB - 1) / GB) * ((N + GB - 1) / GB);
+int64_t gemm_tiles(int64_t M, int64_t N, int T) { return ((M + T - 1) / T) * ((N + T - 1) / T); }
+
+// 32 when NBX_GEMM_TILE32=1 and the launch's 64 x 64 grid (tiles64, summed over its problems) holds
+// fewer than 256 tiles.  Off by default: measured slower on every training step (r04 A/B, DESIGN
+// §3.6: a one-wave block halves the waves per CU that LDS admits, and split-K already fills the chip)
+int gemm_tile_size(int64_t tiles64) {
+    static const bool on = getenv("NBX_GEMM_TILE32") && atoi(getenv("NBX_GEMM_TILE32")) != 0;
+    return on && tiles64 < 256 ? 32 : GB;
+}
+
+int gemm_splits(int64_t M, int64_t N, int64_t K, int T) {
+    const int64_t tiles = gemm_tiles(M, N, T);
     if (tiles >= 256) return 1;
     const int64_t by_grid = (256 + tiles - 1) / tiles, by_k = K / (4 * GK);
     return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(by_grid, by_k), 64));
@@ -678,7 +702,7 @@ unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n
 // ======================================================================== C ABI (include/nbx.h)
 extern "C" int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes) {
     NBX_CHECK_ARG(bytes != nullptr && M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_workspace_bytes: bad arguments");
-    const int s = gemm_splits(M, N, K);
+    const int s = gemm_splits(M, N, K, gemm_tile_size(gemm_tiles(M, N, GB)));
     *bytes = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
     return NBX_OK;
 }
@@ -692,27 +716,33 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     NBX_CHECK_ARG(A && B && C, "nbx_gemm_f32: null operand");
     const bool ta = flags & NBX_GEMM_TRANS_A, tb = flags & NBX_GEMM_TRANS_B;
     NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N, "nbx_gemm_f32: leading dimension too small");
-    const int splits = gemm_splits(M, N, K);
+    const int T = gemm_tile_size(gemm_tiles(M, N, GB));
+    const int splits = gemm_splits(M, N, K, T);
     const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
     NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
                   workspace_bytes, need);
     GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta};
     g.kchunk = (g.kchunk + GK - 1) / GK * GK;
-    const dim3 grid((unsigned)((N + GB - 1) / GB), (unsigned)((M + GB - 1) / GB), (unsigned)splits);
+    const dim3 grid((unsigned)((N + T - 1) / T), (unsigned)((M + T - 1) / T), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
     const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(GT), 0, st, g); };
-    if (vec) {
-        if (ta && tb) go(gemm_f32_kernel<true, true, true>);
-        else if (ta) go(gemm_f32_kernel<true, false, true>);
-        else if (tb) go(gemm_f32_kernel<false, true, true>);
-        else go(gemm_f32_kernel<false, false, true>);
-    } else {
-        if (ta && tb) go(gemm_f32_kernel<true, true, false>);
-        else if (ta) go(gemm_f32_kernel<true, false, false>);
-        else if (tb) go(gemm_f32_kernel<false, true, false>);
-        else go(gemm_f32_kernel<false, false, false>);
-    }
+    auto launch = [&](auto tile) {
+        constexpr int TT = decltype(tile)::value;
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(GemmCfg<TT>::THREADS), 0, st, g); };
+        if (vec) {
+            if (ta && tb) go(gemm_f32_kernel<true, true, true, TT>);
+            else if (ta) go(gemm_f32_kernel<true, false, true, TT>);
+            else if (tb) go(gemm_f32_kernel<false, true, true, TT>);
+            else go(gemm_f32_kernel<false, false, true, TT>);
+        } else {
+            if (ta && tb) go(gemm_f32_kernel<true, true, false, TT>);
+            else if (ta) go(gemm_f32_kernel<true, false, false, TT>);
+            else if (tb) go(gemm_f32_kernel<false, true, false, TT>);
+            else go(gemm_f32_kernel<false, false, false, TT>);
+        }
+    };
+    if (T == 32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, GB>{});
     NBX_LAUNCH_CHECK("gemm_f32");
     if (splits > 1) {
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,
@@ -726,10 +756,13 @@ extern "C" int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t
     NBX_CHECK_ARG(bytes != nullptr && dims != nullptr && count >= 1 && count <= GMAXP,
                   "nbx_gemm_f32_batched_workspace_bytes: bad arguments (count 1..%d)", GMAXP);
     size_t n = 0;
+    int64_t tiles64 = 0;
+    for (int i = 0; i < count; ++i) tiles64 += gemm_tiles(dims[6 * i], dims[6 * i + 1], GB);
+    const int T = gemm_tile_size(tiles64);
     for (int i = 0; i < count; ++i) {
         const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
         NBX_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_batched_workspace_bytes: negative size");
-        const int s = gemm_splits(M, N, K);
+        const int s = gemm_splits(M, N, K, T);
         if (s > 1) n += ((size_t)s * M * N + 63) / 64 * 64;
     }
     *bytes = n * sizeof(float);
@@ -747,6 +780,9 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
     memset(&rb, 0, sizeof(rb));
     int blocks = 0, nred = 0;
     size_t ws_off = 0;
+    int64_t tiles64 = 0;
+    for (int i = 0; i < count; ++i) tiles64 += gemm_tiles(dims[6 * i], dims[6 * i + 1], GB);
+    const int T = gemm_tile_size(tiles64);
     for (int i = 0; i < count; ++i) {
         const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
         const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
@@ -756,7 +792,7 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
         NBX_CHECK_ARG(A[i] && B[i] && C[i], "nbx_gemm_f32_batched: null operand");
         NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N,
                       "nbx_gemm_f32_batched: leading dimension too small");
-        const int splits = gemm_splits(M, N, K);
+        const int splits = gemm_splits(M, N, K, T);
         float* part = nullptr;
         if (splits > 1) {
             const size_t need = ((size_t)splits * M * N + 63) / 64 * 64;
@@ -773,8 +809,8 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
         const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
         gb.g[i] = g;
         gb.mode[i] = (ta ? 1 : 0) | (tb ? 2 : 0) | (vec ? 4 : 0);
-        gb.tx[i] = (int)((N + GB - 1) / GB);
-        gb.ty[i] = (int)((M + GB - 1) / GB);
+        gb.tx[i] = (int)((N + T - 1) / T);
+        gb.ty[i] = (int)((M + T - 1) / T);
         gb.nz[i] = splits;
         gb.first[i] = blocks;
         blocks += gb.tx[i] * gb.ty[i] * splits;
@@ -783,7 +819,10 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
     gb.count = count;
     rb.count = nred;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(gemm_f32_batched_kernel, dim3((unsigned)blocks), dim3(GT), 0, st, gb);
+    if (T == 32)
+        hipLaunchKernelGGL(gemm_f32_batched_kernel<32>, dim3((unsigned)blocks), dim3(GemmCfg<32>::THREADS), 0, st, gb);
+    else
+        hipLaunchKernelGGL(gemm_f32_batched_kernel<GB>, dim3((unsigned)blocks), dim3(GemmCfg<GB>::THREADS), 0, st, gb);
     NBX_LAUNCH_CHECK("gemm_f32_batched");
     if (nred) {
         hipLaunchKernelGGL(gemm_reduce_batched_kernel, dim3(nblk(rb.first[nred])), dim3(256), 0, st, rb);
