@@ -50,6 +50,7 @@ struct GemmArgs {
     int64_t M, N, K, lda, ldb, ldc;
     int64_t kchunk;   // K range per split
     float beta;
+    int ones;         // NBX_GEMM_B_ONES: op(B)'s last column (n = N - 1) is ones, not memory
 };
 
 // one 64 x 64 output tile (bx, by) of K split bz of nz (the body of gemm_f32_kernel and of the
@@ -83,8 +84,16 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
             const int q = t + THREADS * h;
             if (TA) load4(g.A, g.lda, k0 + q / Q4, m0 + (q % Q4) * 4, k_hi, g.M, ra[h]);   // [K][M]
             else load4(g.A, g.lda, m0 + (q >> 3), k0 + (q & 7) * 4, g.M, k_hi, ra[h]);    // [M][K]
-            if (TB) load4(g.B, g.ldb, n0 + (q >> 3), k0 + (q & 7) * 4, g.N, k_hi, rb[h]); // [N][K]
-            else load4(g.B, g.ldb, k0 + q / Q4, n0 + (q % Q4) * 4, k_hi, g.N, rb[h]);      // [K][N]
+            const int64_t bn = TB ? n0 + (q >> 3) : n0 + (q % Q4) * 4, bk = TB ? k0 + (q & 7) * 4 : k0 + q / Q4;
+            if (TB) load4(g.B, g.ldb, bn, bk, g.N - g.ones, k_hi, rb[h]);   // [N][K]
+            else load4(g.B, g.ldb, bk, bn, k_hi, g.N - g.ones, rb[h]);      // [K][N]
+            if (g.ones && n0 + T >= g.N) {   // the appended column of ones (block-uniform test)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool one = TB ? (bn == g.N - 1 && bk + j < k_hi) : (bn + j == g.N - 1 && bk < k_hi);
+                    if (one) rb[h][j] = 1.f;
+                }
+            }
         }
     };
     auto store = [&](int buf) {
@@ -715,13 +724,16 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     if (M == 0 || N == 0) return NBX_OK;
     NBX_CHECK_ARG(A && B && C, "nbx_gemm_f32: null operand");
     const bool ta = flags & NBX_GEMM_TRANS_A, tb = flags & NBX_GEMM_TRANS_B;
-    NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N, "nbx_gemm_f32: leading dimension too small");
+    const int ones = (flags & NBX_GEMM_B_ONES) ? 1 : 0;
+    NBX_CHECK_ARG(!ones || N >= 1, "nbx_gemm_f32: NBX_GEMM_B_ONES needs N >= 1");
+    NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N,
+                  "nbx_gemm_f32: leading dimension too small");
     const int T = gemm_tile_size(gemm_tiles(M, N, GB));
     const int splits = gemm_splits(M, N, K, T);
     const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
     NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
                   workspace_bytes, need);
-    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta};
+    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones};
     g.kchunk = (g.kchunk + GK - 1) / GK * GK;
     const dim3 grid((unsigned)((N + T - 1) / T), (unsigned)((M + T - 1) / T), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
@@ -787,10 +799,11 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
         const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
         const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
         const bool ta = flags[i] & NBX_GEMM_TRANS_A, tb = flags[i] & NBX_GEMM_TRANS_B;
+        const int ones = (flags[i] & NBX_GEMM_B_ONES) ? 1 : 0;
         NBX_CHECK_ARG(M > 0 && N > 0 && K >= 0, "nbx_gemm_f32_batched: problem %d: sizes must be positive", i);
         NBX_CHECK_ARG(beta[i] == 0.f || beta[i] == 1.f, "nbx_gemm_f32_batched: beta must be 0 or 1");
         NBX_CHECK_ARG(A[i] && B[i] && C[i], "nbx_gemm_f32_batched: null operand");
-        NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N,
+        NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N,
                       "nbx_gemm_f32_batched: leading dimension too small");
         const int splits = gemm_splits(M, N, K, T);
         float* part = nullptr;
@@ -804,7 +817,7 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
             rb.splits[nred] = splits; rb.beta[nred] = beta[i]; rb.first[nred + 1] = rb.first[nred] + M * N;
             ++nred;
         }
-        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i]};
+        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i], ones};
         g.kchunk = (g.kchunk + GK - 1) / GK * GK;
         const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
         gb.g[i] = g;

@@ -28,7 +28,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .segnn_train import Graph, colsum, gemm, gemm_batched, _dp, _st, _ws
+from .segnn_train import Graph, colsum, gemm, gemm_batched, _BIAS_COLSUM, _dp, _st, _ws
 
 _f32 = torch.float32
 
@@ -66,12 +66,19 @@ class _LinFn(torch.autograd.Function):
             _lib.check(L.nbx_bias_act_backward(rows, N, _dp(Z), N, _dp(b), act, _dp(dY), _dp(dZ), _st(dZ)),
                        "nbx_bias_act_backward")
         db = dW = dX = None
-        if b is not None and ctx.needs_input_grad[2]:
+        want_b = b is not None and ctx.needs_input_grad[2]
+        if want_b and _BIAS_COLSUM:
             db = colsum(dZ, rows, N, N, torch.empty(N, device=dev, dtype=_f32))
-        probs = []   # the weight and the input gradient GEMMs in one launch (nbx_gemm_f32_batched)
-        if ctx.needs_input_grad[1]:
-            dW = torch.empty(N, K, device=dev, dtype=_f32)
-            probs.append((_lib.GEMM_TRANS_A, N, K, rows, dZ, N, X, ldx, dW, K, 0.0))
+            want_b = False
+        # the weight and the input gradient GEMMs in one launch (nbx_gemm_f32_batched); the bias gradient
+        # (column sums of dZ) is the last column of the weight gradient against X extended by ones
+        probs = []
+        if ctx.needs_input_grad[1] or want_b:
+            dWe = torch.empty(N, K + 1, device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES, N, K + 1, rows, dZ, N, X, ldx, dWe, K + 1, 0.0))
+            dW = dWe[:, :K] if ctx.needs_input_grad[1] else None
+            if want_b:
+                db = dWe[:, K]
         if ctx.needs_input_grad[0]:
             dX = torch.zeros(rows, ldx, device=dev, dtype=_f32) if ldx != K else torch.empty(rows, K, device=dev,
                                                                                               dtype=_f32)

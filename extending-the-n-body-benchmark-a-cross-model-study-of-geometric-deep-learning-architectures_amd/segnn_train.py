@@ -24,6 +24,7 @@ Arithmetic is fp32 (a float64 module is cast for the step, like its fp32 inferen
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -49,6 +50,10 @@ def _st(t):
 def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
+
+# NBX_BIAS_COLSUM=1: bias gradients by nbx_colsum (two launches each) instead of the ones column of the
+# weight-gradient GEMM (A/B only)
+_BIAS_COLSUM = os.environ.get("NBX_BIAS_COLSUM", "0") == "1"
 
 # bench.py's roofline: when a list, every GEMM appends (start event, stop event, flops) recorded on
 # the launch stream around its launches
@@ -151,14 +156,23 @@ class _TPFn(torch.autograd.Function):
         _lib.check(L.nbx_tp_post_backward(rows, Ms, Nt, gate, _dp(Zs), _dp(Zv), _dp(Y3), _dp(bias), _dp(dOS),
                                           _dp(dOV), _dp(dZs), _dp(dZv), _st(dZs)), "nbx_tp_post_backward")
         dbias = None
-        if bias is not None and ctx.needs_input_grad[5]:
+        want_b = bias is not None and ctx.needs_input_grad[5]
+        if want_b and _BIAS_COLSUM:
             dbias = colsum(dZs, rows, nsc, nsc + Nt, torch.empty(nsc, device=dev, dtype=_f32))
-        # the (up to) four backward GEMMs -- weight gradients and input gradients -- in one launch
+            want_b = False
+        # the (up to) four backward GEMMs -- weight gradients and input gradients -- in one launch; the
+        # bias gradient (column sums of dZs[:, :NSc]) is the last column of the weight-gradient GEMM
+        # against S_in extended by a column of ones (NBX_GEMM_B_ONES)
         probs = []
         dWs = dWv = dS = None
-        if ctx.needs_input_grad[3]:
-            dWs = torch.empty(nsc + Nt, Ks + Kv, device=dev, dtype=_f32)
-            probs.append((_lib.GEMM_TRANS_A, nsc + Nt, Ks + Kv, rows, dZs, nsc + Nt, S, Ks + Kv, dWs, Ks + Kv, 0.0))
+        if ctx.needs_input_grad[3] or want_b:
+            W1 = Ks + Kv + 1
+            dWe = torch.empty(nsc + Nt, W1, device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES, nsc + Nt, W1, rows, dZs, nsc + Nt, S, Ks + Kv,
+                          dWe, W1, 0.0))
+            dWs = dWe[:, :Ks + Kv] if ctx.needs_input_grad[3] else None
+            if want_b:
+                dbias = dWe[:nsc, Ks + Kv]
         if Kv and ctx.needs_input_grad[4]:
             dWv = torch.empty(Nt, Kv, device=dev, dtype=_f32)
             probs.append((_lib.GEMM_TRANS_A, Nt, Kv, 3 * rows, dZv, Nt, XV, Kv, dWv, Kv, 0.0))

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 13
+#define NBX_ABI_VERSION 14
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -282,6 +282,9 @@ int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, co
  * split K over the workspace (nbx_gemm_f32_workspace_bytes) and sum the splits in order. */
 #define NBX_GEMM_TRANS_A 1
 #define NBX_GEMM_TRANS_B 2
+/* op(B) gains a last column of ones (n = N - 1 reads 1, not memory; B holds N - 1 columns): C's last
+ * column is then the row sums of op(A) -- a bias gradient from the weight-gradient GEMM (ABI 14) */
+#define NBX_GEMM_B_ONES 4
 int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes);
 /* ABI 12.  Up to 4 independent nbx_gemm_f32 problems in one launch (plus one launch for every split-K
  * sum): problem i has flags[i], dims[6 i ..] = (M, N, K, lda, ldb, ldc), A[i], B[i], C[i], beta[i]

@@ -41,6 +41,36 @@ def test_gemm_f32_matches_torch(hip_device, flags, M, N, K, beta):
     assert err <= 2e-6 * (A.abs() @ B.abs()).max().item() + 1e-6, err
 
 
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K,ldb_pad", [(70, 34, 45, 0), (130, 289, 3840, 3), (96, 65, 1280, 0), (5, 1, 7, 1)])
+def test_gemm_f32_ones_column(hip_device, flags, M, N, K, ldb_pad):
+    """NBX_GEMM_B_ONES: op(B) [K][N - 1] from memory plus a last column of ones, so C's last column is the
+    row sums of op(A) (the bias gradient of a weight-gradient GEMM); single and batched launches agree
+    bit for bit, and the memory past op(B)'s N - 1 columns is never read."""
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N - 1, generator=g, dtype=torch.float64)
+    ref = torch.cat([A @ B, A.sum(1, keepdim=True)], 1)
+    As = A.t().contiguous() if flags & 1 else A
+    # B stored with padding columns / rows filled with NaN: reading them would poison C
+    Bs = B.t().contiguous() if flags & 2 else B
+    ldb = Bs.shape[1] + ldb_pad
+    Bp = torch.full((Bs.shape[0] + 1, ldb), float("nan"), dtype=torch.float64)
+    Bp[:Bs.shape[0], :Bs.shape[1]] = Bs
+    d = lambda x: x.to(device=hip_device, dtype=torch.float32).contiguous()
+    Ad, Bd = d(As), d(Bp)
+    C = torch.full((M, N), 7.0, device=hip_device)
+    f = flags | _lib.GEMM_B_ONES
+    T.gemm(f, M, N, K, Ad, As.shape[1], Bd, ldb, C, N)
+    Cb = torch.full((M, N), 7.0, device=hip_device)
+    T.gemm_batched([(f, M, N, K, Ad, As.shape[1], Bd, ldb, Cb, N, 0.0)])
+    torch.cuda.synchronize()
+    assert torch.isfinite(C).all()
+    err = (C.double().cpu() - ref).abs().max().item()
+    assert err <= 2e-6 * (A.abs() @ torch.cat([B.abs(), torch.ones(K, 1, dtype=torch.float64)], 1)).max().item() + 1e-6
+    assert torch.equal(C, Cb)
+
+
 def test_gemm_f32_batched_equals_single(hip_device):
     """nbx_gemm_f32_batched (up to 4 GEMMs in one launch + one split-K sum launch) is bit-identical to
     nbx_gemm_f32 on each problem: mixed storage orders, split and unsplit shapes, beta 0 and 1."""
