@@ -71,6 +71,10 @@ struct LinProb {
     // (one column chunk), eps 1e-5 (EquiformerV2 RadialFunction hidden layers)
     const float* ln_w;
     const float* ln_b;
+    // set by lin_launch: block b runs logical block (b % 8) * (nblocks / 8) + b / 8, so the blocks of a
+    // contiguous row range share one XCD (b % 8) and its L2 -- the gathering LIN_CONV epilogue then
+    // fetches a system's source rows into one L2 instead of one per neighbouring block
+    int xcd_remap;
 };
 
 constexpr int LIN_WAVES = 8, LIN_THREADS = 64 * LIN_WAVES;
@@ -95,8 +99,9 @@ constexpr int LIN_X3_BLK = 1536;   // floats of one (column tile, 32-deep chunk)
 template <int NT, int ACT, int EPI = LIN_STORE, int PREC = 0>
 __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int chunk = blockIdx.x / P.blocks_per_chunk;
-    const int blk = blockIdx.x - chunk * P.blocks_per_chunk;
+    const int bid = P.xcd_remap ? ((int)blockIdx.x & 7) * ((int)gridDim.x >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+    const int chunk = bid / P.blocks_per_chunk;
+    const int blk = bid - chunk * P.blocks_per_chunk;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
     const int pitch = ((P.Ktot + 31) & ~31) + 4;
     const int n0 = chunk * NT * 32;
@@ -468,6 +473,12 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     if (bpc > max_bpc) bpc = max_bpc;
     if (bpc < 1) bpc = 1;
     p.blocks_per_chunk = bpc;
+    // XCD-grouped block order for the gathering epilogues (a bijection only when the grid is a
+    // multiple of 8 blocks; NBX_LIN_XCD=0 keeps the plain order, A/B)
+    static const bool xcd = !(getenv("NBX_LIN_XCD") && getenv("NBX_LIN_XCD")[0] == '0');
+    // (LIN_CONV only: C3's spatial conv 1.64 -> 1.39 GB per launch at the same time; EquiformerV2's
+    // LIN_EQMSG measured 1 % slower with it, profiles/r04/lin_xcd_ab)
+    p.xcd_remap = (xcd && EPI == LIN_CONV && (p.chunks * bpc) % 8 == 0) ? 1 : 0;
     static bool attr_set = false;
     if (!attr_set) {
         NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT, EPI, PREC>,
