@@ -1,7 +1,7 @@
 // A20-A22 — GravitySim softened-gravity leapfrog (datasets/nbody/dataset/synthetic_sim.py:305-420), fp64.
 //
-// Layout: one thread per body, floor(256/N) systems per 256-thread workgroup
-// (one system per workgroup when N > 256).  The current positions of the
+// Layout: one thread per body, the systems per workgroup (<= 1024 threads) that waste the fewest
+// lanes (launch_geometry: N = 100 -> 10 systems, 1000 of 1024 lanes).  The current positions of the
 // workgroup's systems live in LDS; the whole T-step KDK loop runs inside the
 // kernel, so HBM only sees the initial state, the sampled frames and the final
 // state.  Per step each body does N softened interactions (FP64 VALU bound).
@@ -76,7 +76,10 @@ __global__ void gravity_accel_kernel(const double* __restrict__ pos, const doubl
     acc[(s * N + i) * 3 + 2] = az;
 }
 
-__global__ void gravity_sample_kernel(double* __restrict__ pos, double* __restrict__ vel,
+// OCC: minimum resident 1024-thread workgroups per CU the register allocation must allow (2: <= 64
+// VGPRs, 8 waves per SIMD to hide the rsq / LDS latency of the pair loop; 1: the compiler's choice)
+template <int OCC>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4 * OCC))) void gravity_sample_kernel(double* __restrict__ pos, double* __restrict__ vel,
                                       const double* __restrict__ mass, int64_t S, int N, int spb, int64_t T,
                                       int64_t freq, double dt, double G, double soft2, double* __restrict__ pos_save,
                                       double* __restrict__ vel_save, double* __restrict__ force_save) {
@@ -199,9 +202,16 @@ extern "C" int nbx_gravity_sample(double* pos, double* vel, const double* mass, 
     int spb, threads;
     launch_geometry(N, spb, threads);
     const size_t lds = sizeof(double4) * spb * N;
-    hipLaunchKernelGGL(gravity_sample_kernel, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
-                       (hipStream_t)stream, pos, vel, mass, S, (int)N, spb, T, sample_freq, dt, G,
-                       softening * softening, pos_save, vel_save, force_save);
+    // NBX_GRAV_OCC=1: the compiler's register allocation (one workgroup per CU at N = 100), A/B
+    static const bool occ2 = !(getenv("NBX_GRAV_OCC") && getenv("NBX_GRAV_OCC")[0] == '1');
+    if (occ2)
+        hipLaunchKernelGGL(gravity_sample_kernel<2>, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
+                           (hipStream_t)stream, pos, vel, mass, S, (int)N, spb, T, sample_freq, dt, G,
+                           softening * softening, pos_save, vel_save, force_save);
+    else
+        hipLaunchKernelGGL(gravity_sample_kernel<1>, dim3((unsigned)nbx::ceil_div(S, spb)), dim3(threads), lds,
+                           (hipStream_t)stream, pos, vel, mass, S, (int)N, spb, T, sample_freq, dt, G,
+                           softening * softening, pos_save, vel_save, force_save);
     NBX_LAUNCH_CHECK("gravity_sample_kernel");
     return NBX_OK;
 }
