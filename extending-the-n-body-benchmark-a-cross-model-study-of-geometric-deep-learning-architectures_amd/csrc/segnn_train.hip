@@ -197,7 +197,35 @@ struct ReduceBatch {
     float beta[GMAXP];
     int64_t first[GMAXP + 1];   // first element of each problem in the flattened index
     int count;
+    int serial;
 };
+
+// sum_z part[z * MN + e] for z = 0 .. splits - 1, added in z order (bit-identical to the plain loop)
+// with the loads issued 8 at a time: a serial load -> add chain paid one full memory latency per split
+__device__ __forceinline__ float splitk_sum(const float* __restrict__ part, int splits, int64_t MN, int64_t e,
+                                            bool serial) {
+    float s = 0.f;
+    if (serial) {   // NBX_SPLITK_SERIAL=1: the plain loop (A/B)
+        for (int z = 0; z < splits; ++z) s += part[(int64_t)z * MN + e];
+        return s;
+    }
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(z + u) * MN + e];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    float v[7];
+    const int rem = splits - z;
+#pragma unroll
+    for (int u = 0; u < 7; ++u) v[u] = u < rem ? part[(int64_t)(z + u) * MN + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+        if (u < rem) s += v[u];
+    return s;
+}
 
 __global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -208,21 +236,24 @@ __global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
         if (q < b.count && i >= b.first[q]) p = q;
     const int64_t e = i - b.first[p], N = b.N[p], MN = b.M[p] * N;
     const int64_t r = e / N, c = e - r * N;
-    float s = 0.f;
-    for (int z = 0; z < b.splits[p]; ++z) s += b.part[p][(int64_t)z * MN + e];
+    const float s = splitk_sum(b.part[p], b.splits[p], MN, e, b.serial);
     float* q = b.C[p] + r * b.ldc[p] + c;
     *q = b.beta[p] != 0.f ? s + b.beta[p] * *q : s;
 }
 
 __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, int64_t M, int64_t N,
-                                   float* __restrict__ C, int64_t ldc, float beta) {
+                                   float* __restrict__ C, int64_t ldc, float beta, int serial) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= M * N) return;
     const int64_t r = i / N, c = i - r * N;
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += part[(int64_t)z * M * N + i];
+    const float s = splitk_sum(part, splits, M * N, i, serial);
     float* p = C + r * ldc + c;
     *p = beta != 0.f ? s + beta * *p : s;
+}
+
+bool splitk_serial() {
+    static const bool v = getenv("NBX_SPLITK_SERIAL") && atoi(getenv("NBX_SPLITK_SERIAL")) != 0;
+    return v;
 }
 
 int64_t gemm_tiles(int64_t M, int64_t N, int T) { return ((M + T - 1) / T) * ((N + T - 1) / T); }
@@ -758,7 +789,7 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     NBX_LAUNCH_CHECK("gemm_f32");
     if (splits > 1) {
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,
-                           N, C, ldc, beta);
+                           N, C, ldc, beta, (int)splitk_serial());
         NBX_LAUNCH_CHECK("gemm_reduce");
     }
     return NBX_OK;
@@ -831,6 +862,7 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
     }
     gb.count = count;
     rb.count = nred;
+    rb.serial = splitk_serial() ? 1 : 0;
     hipStream_t st = (hipStream_t)stream;
     if (T == 32)
         hipLaunchKernelGGL(gemm_f32_batched_kernel<32>, dim3((unsigned)blocks), dim3(GemmCfg<32>::THREADS), 0, st, gb);

@@ -19,5 +19,9 @@ tail -3 $out/smoke.log
 echo "[$(date +%T)] bench (default)"
 timeout -k 10 600 python bench.py > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
 grep '^{' $out/bench.log | tail -1 | cut -c1-400
+if [ -n "${AB_ENV:-}" ]; then
+  echo "[$(date +%T)] training A/B ($AB_ENV)"
+  ROUNDS=${ROUNDS:-1} MODELS="${AB_MODELS:-segnn_train ponita_train}" bash scripts/ab_train_env.sh || exit 1
+fi
 [ -n "${NO_PROFILE:-}" ] && exit 0
-bash scripts/profile_models.sh ${PROFILE_MODELS:-ponita gravity segnn_train}
+bash scripts/profile_models.sh ${PROFILE_MODELS:-ponita gravity}
