@@ -152,6 +152,44 @@ __global__ __launch_bounds__(256) void eqv2_radial_kernel(const float* __restric
     }
 }
 
+// softmax over a node's deg incoming edges for head `lane` (segment softmax + 1e-16, PyG): alpha[q] ->
+// sal[q * 8 + lane].  Up to 32 edges the logits are loaded in one predicated batch into registers (the
+// loop form waited one memory latency per edge, twice); the arithmetic and its order are unchanged.
+template <class EdgeOf>
+__device__ __forceinline__ void edge_softmax(const float* __restrict__ L, int nh, int lane, int deg, EdgeOf edge_of,
+                                             float* sal) {
+    if (deg <= 32) {
+        float lv[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) lv[q] = q < deg ? L[edge_of(q) * nh + lane] : -INFINITY;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) mx = fmaxf(mx, lv[q]);
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < 32; ++q)
+            if (q < deg) {
+                lv[q] = __expf(lv[q] - mx);
+                sum += lv[q];
+            }
+        const float inv = 1.0f / (sum + 1e-16f);
+#pragma unroll
+        for (int q = 0; q < 32; ++q)
+            if (q < deg) sal[q * 8 + lane] = lv[q] * inv;
+        return;
+    }
+    float mx = -INFINITY;
+    for (int q = 0; q < deg; ++q) mx = fmaxf(mx, L[edge_of(q) * nh + lane]);
+    float sum = 0.f;
+    for (int q = 0; q < deg; ++q) {
+        const float ex = __expf(L[edge_of(q) * nh + lane] - mx);
+        sal[q * 8 + lane] = ex;
+        sum += ex;
+    }
+    const float inv = 1.0f / (sum + 1e-16f);
+    for (int q = 0; q < deg; ++q) sal[q * 8 + lane] *= inv;
+}
+
 // ---- separable S2 activation of the so2_conv_1 output + attention logits
 // (transformer_block.py:287-339; activation.py:155-202; so2_ops.py:61-75 complex combine):
 // one wave per edge, lane = hidden channel.
@@ -165,6 +203,10 @@ struct S2Args {
     float* Z0; float* Z1; float* L;
 };
 
+// NA: attn_alpha_channels as a compile-time count (8 at C4, 16), so the head's alpha row and LayerNorm
+// parameters are loaded in one batch; 0 = run-time count (a serial load per element: the lanes h < nh
+// of every wave waited ~3 NA memory latencies, which bounded the kernel)
+template <int NA>
 __global__ __launch_bounds__(256) void eqv2_s2act_kernel(const S2Args A) {
     // one thread per (edge, hidden channel); the grid matrices are read with uniform addresses
     // (scalar loads, SGPR operands): no LDS traffic in the 18-point loop
@@ -209,23 +251,50 @@ __global__ __launch_bounds__(256) void eqv2_s2act_kernel(const S2Args A) {
     z1[3 * H] = o[4];
     if (h < A.nh) {   // alpha_norm (LayerNorm), SmoothLeakyReLU(0.2), alpha_dot for head h
         const float* xa = y0 + h * A.na;
-        float xs[16];
-        float mu = 0.f;
-        for (int k = 0; k < A.na; ++k) {
-            xs[k] = xa[k];
-            mu += xs[k];
+        if constexpr (NA > 0) {
+            float xs[NA], w[NA], b[NA], d[NA];
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                xs[k] = xa[k];
+                w[k] = A.an_w[k];
+                b[k] = A.an_b[k];
+                d[k] = A.adot[h * NA + k];
+            }
+            float mu = 0.f;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) mu += xs[k];
+            mu /= NA;
+            float var = 0.f;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) var += (xs[k] - mu) * (xs[k] - mu);
+            const float rs = 1.0f / sqrtf(var / NA + 1e-5f);
+            float lg = 0.f;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const float y = (xs[k] - mu) * rs * w[k] + b[k];
+                const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                lg += (0.6f * y + 0.4f * y * (2.0f * sg - 1.0f)) * d[k];
+            }
+            A.L[e * A.nh + h] = lg;
+        } else {
+            float xs[16];
+            float mu = 0.f;
+            for (int k = 0; k < A.na; ++k) {
+                xs[k] = xa[k];
+                mu += xs[k];
+            }
+            mu /= A.na;
+            float var = 0.f;
+            for (int k = 0; k < A.na; ++k) var += (xs[k] - mu) * (xs[k] - mu);
+            const float rs = 1.0f / sqrtf(var / A.na + 1e-5f);
+            float lg = 0.f;
+            for (int k = 0; k < A.na; ++k) {
+                const float y = (xs[k] - mu) * rs * A.an_w[k] + A.an_b[k];
+                const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                lg += (0.6f * y + 0.4f * y * (2.0f * sg - 1.0f)) * A.adot[h * A.na + k];
+            }
+            A.L[e * A.nh + h] = lg;
         }
-        mu /= A.na;
-        float var = 0.f;
-        for (int k = 0; k < A.na; ++k) var += (xs[k] - mu) * (xs[k] - mu);
-        const float rs = 1.0f / sqrtf(var / A.na + 1e-5f);
-        float lg = 0.f;
-        for (int k = 0; k < A.na; ++k) {
-            const float y = (xs[k] - mu) * rs * A.an_w[k] + A.an_b[k];
-            const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-y));
-            lg += (0.6f * y + 0.4f * y * (2.0f * sg - 1.0f)) * A.adot[h * A.na + k];
-        }
-        A.L[e * A.nh + h] = lg;
     }
 }
 
@@ -329,18 +398,7 @@ __global__ __launch_bounds__(64) void eqv2_node_kernel(const NodeArgs A) {
             // ---- attention: softmax over the N-1 incoming edges per head
             const int KV = A.nh * A.nv;
             float* sal = s_alpha;
-            if (active && lane < A.nh) {
-                float mx = -INFINITY;
-                for (int q = 0; q < deg; ++q) mx = fmaxf(mx, A.L[edge_of(q) * A.nh + lane]);
-                float sum = 0.f;
-                for (int q = 0; q < deg; ++q) {
-                    const float ex = __expf(A.L[edge_of(q) * A.nh + lane] - mx);
-                    sal[q * 8 + lane] = ex;
-                    sum += ex;
-                }
-                const float inv = 1.0f / (sum + 1e-16f);
-                for (int q = 0; q < deg; ++q) sal[q * 8 + lane] *= inv;
-            }
+            if (active && lane < A.nh) edge_softmax(A.L, A.nh, lane, deg, edge_of, sal);
             __syncthreads();
             // ---- values * alpha, rotated back (Wigner^T with the l = 2 rescale), summed over edges
             const int G = 64 / KV, k = lane % KV, qg = lane / KV, hd = k / A.nv;
@@ -472,7 +530,8 @@ __global__ __launch_bounds__(64) void eqv2_node_kernel(const NodeArgs A) {
 // all NPW nodes (each weight load feeds NPW nodes' FMAs, so the chains of dependent L2 weight
 // reads that bound the one-node kernel are NPW times shorter).  Per node the arithmetic and its
 // order are those of eqv2_node_kernel<NODE_BLOCK>.  Needs KV <= 16.
-template <int NPW>
+// NB_ROWS: weight rows per load batch (4: 124 VGPRs, four waves per SIMD; 8: 190 VGPRs)
+template <int NPW, int NB_ROWS = 4>
 __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, int64_t V) {
     __shared__ float s_alpha[64 * 8];
     __shared__ float s_ag[NPW][9 * 16];
@@ -500,18 +559,7 @@ __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, i
             const int s = q < t ? q : q + 1;
             return sys * N * deg + (int64_t)s * deg + (t < s ? t : t - 1);
         };
-        if (lane < A.nh) {
-            float mx = -INFINITY;
-            for (int q = 0; q < deg; ++q) mx = fmaxf(mx, A.L[edge_of(q) * A.nh + lane]);
-            float sum = 0.f;
-            for (int q = 0; q < deg; ++q) {
-                const float ex = __expf(A.L[edge_of(q) * A.nh + lane] - mx);
-                s_alpha[q * 8 + lane] = ex;
-                sum += ex;
-            }
-            const float inv = 1.0f / (sum + 1e-16f);
-            for (int q = 0; q < deg; ++q) s_alpha[q * 8 + lane] *= inv;
-        }
+        if (lane < A.nh) edge_softmax(A.L, A.nh, lane, deg, edge_of, s_alpha);
         __syncthreads();
         const int G = 64 / KV, k = lane % KV, qg = lane / KV, hd = k / A.nv;
         float agg[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -547,16 +595,36 @@ __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, i
         for (int n = 0; n < NPW; ++n)
 #pragma unroll
             for (int i = 0; i < 9; ++i) y[n][i] = 0.f;
-        for (int kk = 0; kk < KV; ++kk) {
-            const float w0 = A.proj_t[kk * C + c], w1 = A.proj_t[(KV + kk) * C + c], w2 = A.proj_t[(2 * KV + kk) * C + c];
+        // weight loops in groups of NB_ROWS rows: the group's weight loads are issued together into
+        // registers before its FMAs (one L2 round trip per group instead of per row or two); the
+        // accumulation order is unchanged
+        auto proj_rows = [&](int k0, auto nrows) {
+            constexpr int R = decltype(nrows)::value;
+            float w0[R], w1[R], w2[R];
 #pragma unroll
-            for (int n = 0; n < NPW; ++n) {
-                y[n][0] += s_ag[n][kk] * w0;
-#pragma unroll
-                for (int i = 1; i < 4; ++i) y[n][i] += s_ag[n][i * KV + kk] * w1;
-#pragma unroll
-                for (int i = 4; i < 9; ++i) y[n][i] += s_ag[n][i * KV + kk] * w2;
+            for (int u = 0; u < R; ++u) {
+                const int kk = k0 + u;
+                w0[u] = A.proj_t[kk * C + c];
+                w1[u] = A.proj_t[(KV + kk) * C + c];
+                w2[u] = A.proj_t[(2 * KV + kk) * C + c];
             }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int kk = k0 + u;
+#pragma unroll
+                for (int n = 0; n < NPW; ++n) {
+                    y[n][0] += s_ag[n][kk] * w0[u];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) y[n][i] += s_ag[n][i * KV + kk] * w1[u];
+#pragma unroll
+                    for (int i = 4; i < 9; ++i) y[n][i] += s_ag[n][i * KV + kk] * w2[u];
+                }
+            }
+        };
+        {
+            int k0 = 0;
+            for (; k0 + NB_ROWS <= KV; k0 += NB_ROWS) proj_rows(k0, std::integral_constant<int, NB_ROWS>{});
+            for (; k0 < KV; ++k0) proj_rows(k0, std::integral_constant<int, 1>{});
         }
         const float pb = A.proj_b[c];
 #pragma unroll
@@ -586,18 +654,35 @@ __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, i
 #pragma unroll
             for (int i = 1; i < 9; ++i) h[n][i] = 0.f;
         }
-        for (int cc = 0; cc < C; ++cc) {
-            const float wg = A.gate_t[cc * F + f], w0 = A.lin1_t[cc * F + f], w1 = A.lin1_t[(C + cc) * F + f],
-                        w2 = A.lin1_t[(2 * C + cc) * F + f];
+        auto lin1_rows = [&](int c0, auto nrows) {
+            constexpr int R = decltype(nrows)::value;
+            float wg[R], w0[R], w1[R], w2[R];
 #pragma unroll
-            for (int n = 0; n < NPW; ++n) {
-                gate[n] += s_x[n][cc] * wg;
-                h[n][0] += s_x[n][cc] * w0;
-#pragma unroll
-                for (int i = 1; i < 4; ++i) h[n][i] += s_x[n][i * C + cc] * w1;
-#pragma unroll
-                for (int i = 4; i < 9; ++i) h[n][i] += s_x[n][i * C + cc] * w2;
+            for (int u = 0; u < R; ++u) {
+                const int cc = c0 + u;
+                wg[u] = A.gate_t[cc * F + f];
+                w0[u] = A.lin1_t[cc * F + f];
+                w1[u] = A.lin1_t[(C + cc) * F + f];
+                w2[u] = A.lin1_t[(2 * C + cc) * F + f];
             }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int cc = c0 + u;
+#pragma unroll
+                for (int n = 0; n < NPW; ++n) {
+                    gate[n] += s_x[n][cc] * wg[u];
+                    h[n][0] += s_x[n][cc] * w0[u];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) h[n][i] += s_x[n][i * C + cc] * w1[u];
+#pragma unroll
+                    for (int i = 4; i < 9; ++i) h[n][i] += s_x[n][i * C + cc] * w2[u];
+                }
+            }
+        };
+        {
+            int c0 = 0;
+            for (; c0 + NB_ROWS <= C; c0 += NB_ROWS) lin1_rows(c0, std::integral_constant<int, NB_ROWS>{});
+            for (; c0 < C; ++c0) lin1_rows(c0, std::integral_constant<int, 1>{});
         }
         __syncthreads();   // s_x is rewritten with the activation below
 #pragma unroll
@@ -627,16 +712,33 @@ __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, i
 #pragma unroll
             for (int i = 1; i < 9; ++i) h2[n][i] = 0.f;
         }
-        for (int ff = 0; ff < F; ++ff) {
-            const float w0 = A.lin2_t[ff * C + c], w1 = A.lin2_t[(F + ff) * C + c], w2 = A.lin2_t[(2 * F + ff) * C + c];
+        auto lin2_rows = [&](int f0, auto nrows) {
+            constexpr int R = decltype(nrows)::value;
+            float w0[R], w1[R], w2[R];
 #pragma unroll
-            for (int n = 0; n < NPW; ++n) {
-                h2[n][0] += s_x[n][ff] * w0;
-#pragma unroll
-                for (int i = 1; i < 4; ++i) h2[n][i] += s_x[n][i * F + ff] * w1;
-#pragma unroll
-                for (int i = 4; i < 9; ++i) h2[n][i] += s_x[n][i * F + ff] * w2;
+            for (int u = 0; u < R; ++u) {
+                const int ff = f0 + u;
+                w0[u] = A.lin2_t[ff * C + c];
+                w1[u] = A.lin2_t[(F + ff) * C + c];
+                w2[u] = A.lin2_t[(2 * F + ff) * C + c];
             }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int ff = f0 + u;
+#pragma unroll
+                for (int n = 0; n < NPW; ++n) {
+                    h2[n][0] += s_x[n][ff] * w0[u];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) h2[n][i] += s_x[n][i * F + ff] * w1[u];
+#pragma unroll
+                    for (int i = 4; i < 9; ++i) h2[n][i] += s_x[n][i * F + ff] * w2[u];
+                }
+            }
+        };
+        {
+            int f0 = 0;
+            for (; f0 + NB_ROWS <= F; f0 += NB_ROWS) lin2_rows(f0, std::integral_constant<int, NB_ROWS>{});
+            for (; f0 < F; ++f0) lin2_rows(f0, std::integral_constant<int, 1>{});
         }
 #pragma unroll
         for (int n = 0; n < NPW; ++n) {
@@ -814,7 +916,14 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
              Aw.alpha_dot, nh, w->alpha_channels, H, E, ws.Z0, ws.Z1, ws.L};
     {
         TScope ts(4, st, 2.0 * e * H * GA * 14, f4 * e * (n0r + 8 * H + 7 * H + nh));
-        hipLaunchKernelGGL(eqv2_s2act_kernel, dim3(g1(E * H)), dim3(256), 0, st, s);
+        // NBX_EQV2_S2_NA0=1: the run-time alpha count (A/B)
+        static const bool rt = getenv("NBX_EQV2_S2_NA0") && getenv("NBX_EQV2_S2_NA0")[0] == '1';
+        if (!rt && s.na == 8)
+            hipLaunchKernelGGL(eqv2_s2act_kernel<8>, dim3(g1(E * H)), dim3(256), 0, st, s);
+        else if (!rt && s.na == 16)
+            hipLaunchKernelGGL(eqv2_s2act_kernel<16>, dim3(g1(E * H)), dim3(256), 0, st, s);
+        else
+            hipLaunchKernelGGL(eqv2_s2act_kernel<0>, dim3(g1(E * H)), dim3(256), 0, st, s);
         NBX_LAUNCH_CHECK("eqv2 s2act");
     }
     {
@@ -887,7 +996,16 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         static const int npw = getenv("NBX_EQ_NPW") ? atoi(getenv("NBX_EQ_NPW")) : 2;
         const int64_t V = B * N;
         if (npw == 2 && w->num_heads * w->value_channels <= 16)
-            hipLaunchKernelGGL(eqv2_node_block_kernel<2>, dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
+        {
+            // NBX_EQ_NB: weight rows per load batch (A/B: 1, 4, 8)
+            static const int nb = getenv("NBX_EQ_NB") ? atoi(getenv("NBX_EQ_NB")) : 4;
+            if (nb == 8)
+                hipLaunchKernelGGL((eqv2_node_block_kernel<2, 8>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
+            else if (nb == 1)
+                hipLaunchKernelGGL((eqv2_node_block_kernel<2, 1>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
+            else
+                hipLaunchKernelGGL((eqv2_node_block_kernel<2, 4>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
+        }
         else
             hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)V), dim3(64), 0, st, a);
         NBX_LAUNCH_CHECK("eqv2 node block");
