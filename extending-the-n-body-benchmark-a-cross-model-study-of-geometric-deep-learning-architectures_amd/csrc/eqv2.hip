@@ -530,8 +530,8 @@ __global__ __launch_bounds__(64) void eqv2_node_kernel(const NodeArgs A) {
 // all NPW nodes (each weight load feeds NPW nodes' FMAs, so the chains of dependent L2 weight
 // reads that bound the one-node kernel are NPW times shorter).  Per node the arithmetic and its
 // order are those of eqv2_node_kernel<NODE_BLOCK>.  Needs KV <= 16.
-// NB_ROWS: weight rows per load batch (4: 124 VGPRs, four waves per SIMD; 8: 190 VGPRs)
-template <int NPW, int NB_ROWS = 4>
+// NB_ROWS: weight rows per load batch (1: the default, 121 VGPRs; 4: 124 VGPRs; 8: 190 VGPRs)
+template <int NPW, int NB_ROWS = 1>
 __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, int64_t V) {
     __shared__ float s_alpha[64 * 8];
     __shared__ float s_ag[NPW][9 * 16];
@@ -997,14 +997,15 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
         const int64_t V = B * N;
         if (npw == 2 && w->num_heads * w->value_channels <= 16)
         {
-            // NBX_EQ_NB: weight rows per load batch (A/B: 1, 4, 8)
-            static const int nb = getenv("NBX_EQ_NB") ? atoi(getenv("NBX_EQ_NB")) : 4;
+            // NBX_EQ_NB: weight rows per load batch (A/B: 1, 4, 8; measured at C4: 237.0 / 236.3, 234.8 /
+            // 235.2, 226.8 / 228.7 steps/s -- the compiler's own schedule of one row per step is best)
+            static const int nb = getenv("NBX_EQ_NB") ? atoi(getenv("NBX_EQ_NB")) : 1;
             if (nb == 8)
                 hipLaunchKernelGGL((eqv2_node_block_kernel<2, 8>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
-            else if (nb == 1)
-                hipLaunchKernelGGL((eqv2_node_block_kernel<2, 1>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
-            else
+            else if (nb == 4)
                 hipLaunchKernelGGL((eqv2_node_block_kernel<2, 4>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
+            else
+                hipLaunchKernelGGL((eqv2_node_block_kernel<2, 1>), dim3((unsigned)((V + 1) / 2)), dim3(64), 0, st, a, V);
         }
         else
             hipLaunchKernelGGL(eqv2_node_kernel<NODE_BLOCK>, dim3((unsigned)V), dim3(64), 0, st, a);
