@@ -48,6 +48,14 @@ HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0         # MI355X_MICROARCH.md: BF16 MFMA, dense (~2.5 PF)
 X3_TERMS = 6                           # bf16x3 split: bf16 MFMA products per fp32 product
+SPLIT_TERMS = {1: 6, 2: 3}             # 16-bit MFMA products per fp32 product: bf16x3, fp16x2
+
+
+def segnn_split_prec():
+    """The SEGNN split-precision path the library selects (csrc/segnn.hip split_prec)."""
+    if os.environ.get("NBX_X3") == "0" or os.environ.get("NBX_SPLIT", "")[:1] == "0":
+        return 0
+    return 1 if os.environ.get("NBX_SPLIT", "")[:1] in ("x", "1") else 2
 FP64_VALU_PEAK_TFLOPS = 78.6           # MI355X spec (SURVEY §8d); no f64 MFMA used by the integrator
 SURVEY_GFLOP_PER_STEP = 67.73          # SURVEY §8(d): algorithmic work of the reference formulation
 
@@ -206,17 +214,17 @@ def bench_segnn(a, rank, world, device, P):
             n_k[k] += kn[k]
             fl_k[k] += kfl[k]
         fwd_ms += tot.value
-    # rocprofv3 names of the four timed launch kinds at C2 (csrc/segnn.hip::forward_impl)
-    x3 = os.environ.get("NBX_X3") != "0"
-    names = [("void nbx::msg_pre_kernel<true, 3>(nbx::MsgPreProb)" if x3 else
-              "void nbx::msg_pre_kernel<false, 0>(nbx::MsgPreProb)"),
-             ("void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSKX3<6, 6, 3, 3, 0> >(nbx::TpProb)" if x3 else
-              "void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::StatSK<6, 6, 3, 3, 0> >(nbx::TpProb)"),
-             ("void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSKX3<12, 12, 6, 6, 4> >(nbx::TpProb, "
-              "nbx::TpProb, int)" if x3 else
-              "void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::StatSK<12, 12, 6, 6, 4> >(nbx::TpProb, "
-              "nbx::TpProb, int)"),
-             "void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, nbx::StatSK<6, 3, 0, 3, 0> >(nbx::TpProb, nbx::TpProb, int)"]
+    # rocprofv3 names of the four timed launch kinds at C2 (csrc/segnn.hip::forward_impl, split_prec):
+    # 2 = fp16x2 images (default), 1 = bf16x3 (NBX_SPLIT=x3), 0 = fp32 MFMA (NBX_X3=0)
+    prec = segnn_split_prec()
+    sk = {2: "StatSKH2", 1: "StatSKX3", 0: "StatSK"}[prec]
+    names = [f"void nbx::msg_pre_kernel<{prec}, {3 if prec else 0}>(nbx::MsgPreProb)",
+             f"void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::{sk}<6, 6, 3, 3, 0> >(nbx::TpProb)",
+             f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::{sk}<12, 12, 6, 6, 4> >(nbx::TpProb, "
+             "nbx::TpProb, int)",
+             f"void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, nbx::{'StatSKH2' if prec == 2 else 'StatSK'}"
+             "<6, 3, 0, 3, 0> >(nbx::TpProb, nbx::TpProb, int)"]
+    x3 = prec != 0
     roles = ["message_layer_1: node GEMM + edge combination + gate (flops: the node GEMM)",
              "message_layer_2 + gate + aggregation + BN sums",
              "update_layer_1 + gate (the kind's average includes pre_pool1, once per forward)",
@@ -252,11 +260,13 @@ def bench_segnn(a, rank, world, device, P):
                      "avg_launch_us": round(dom_avg_s * 1e6, 3), "gflop_per_launch": round(dom_flops / 1e9, 4),
                      # achieved / frac: fp32-accurate GEMM flops against the fp32 MFMA peak; the
                      # split-precision path executes them as X3_TERMS bf16 MFMA products each
-                     "mfma_path": ("bf16x3 split (fp32-accurate), v_mfma_f32_*_bf16" if x3 else
-                                   "fp32, v_mfma_f32_*_f32"),
-                     "executed_bf16_tflops": round(achieved_tflops * X3_TERMS, 2) if x3 else None,
-                     "executed_bf16_frac": (round(achieved_tflops * X3_TERMS / BF16_MFMA_PEAK_TFLOPS, 4)
-                                            if x3 else None),
+                     "mfma_path": {2: "fp16x2 split (fp32-accurate), v_mfma_f32_*_f16",
+                                   1: "bf16x3 split (fp32-accurate), v_mfma_f32_*_bf16",
+                                   0: "fp32, v_mfma_f32_*_f32"}[prec],
+                     # the 16-bit MFMA products actually issued (bf16x3: 6, fp16x2: 3 per fp32 product)
+                     "executed_16bit_tflops": round(achieved_tflops * SPLIT_TERMS[prec], 2) if x3 else None,
+                     "executed_16bit_frac": (round(achieved_tflops * SPLIT_TERMS[prec] / BF16_MFMA_PEAK_TFLOPS, 4)
+                                             if x3 else None),
                      "timing": "hipExtLaunchKernel start/stop events (kernel execution interval)",
                      "fused_tp_share_of_forward": round(sum(ms_k) / fwd_ms, 3), "per_kind": per_kind},
         "finite": finite, "rollout_timing": diag,

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 14
+ABI_VERSION = 15
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B, GEMM_B_ONES = 1, 2, 4
@@ -28,7 +28,9 @@ class SegnnLayer(ctypes.Structure):
         "node_pre_s_img", "node_pre_v_img", "node_pre_s_img_x3", "node_pre_v_img_x3", "msg1_amf", "msg1_bias", "msg2_img", "msg2_img_x3", "msg2_bias",
         "upd1_img", "upd1_img_x3", "upd1_bias", "upd2_img", "upd2_bias",
         "msg_bn_weight", "msg_bn_bias", "msg_bn_running_mean", "msg_bn_running_var",
-        "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var")]
+        "feat_bn_weight", "feat_bn_bias", "feat_bn_running_mean", "feat_bn_running_var",
+        "node_pre_s_img_h2", "node_pre_v_img_h2", "msg2_img_h2", "upd1_img_h2", "upd2_img_h2")] + [
+        (n, c_f) for n in ("node_pre_h2_descale", "msg2_h2_descale", "upd1_h2_descale", "upd2_h2_descale")]
 
 
 # nbx_allreduce_fn: int (*)(double* buf, int64_t count, void* stream, void* ctx)
@@ -41,6 +43,7 @@ class SegnnWeights(ctypes.Structure):
                     "emb", "emb_bias", "pp1_img", "pp1_bias", "pp2")] + [
                 ("bn_allreduce", ALLREDUCE_FN), ("bn_allreduce_ctx", c_p), ("bn_global_batch", c_i64),
                 ("bn_comm", c_p), ("deterministic", c_i32), ("reserved0", c_i32),
+                ("pp1_img_h2", c_p), ("pp1_h2_descale", c_f), ("reserved1", c_i32),
                 ("layers", SegnnLayer * MAX_LAYERS)]
 
 

@@ -93,8 +93,8 @@ def _keep_device_asm():
 
 def check_isa():
     """The gfx950 hazard ROCm 7.2 does not pad (DESIGN.md "gfx950 MFMA SrcA hazard"): a load
-    issued right after a v_mfma_f32_16x16x32_bf16 into that MFMA's SrcA registers.  Any
-    occurrence in the built kernels fails the build."""
+    issued right after a v_mfma_f32_16x16x32_bf16 (or its fp16 twin) into that MFMA's SrcA
+    registers.  Any occurrence in the built kernels fails the build."""
     import glob as _g
     from importlib import import_module
     scan = import_module(__package__ + ".isa_scan" if __package__ else "isa_scan").scan
@@ -103,7 +103,7 @@ def check_isa():
         msg = "\n".join(f"{os.path.basename(p)}:{no} [{fn}] {ld} <- SrcA of line {pno}: {mf}"
                         for p, fn, no, ld, pno, mf, _, _ in hits)
         raise RuntimeError("gfx950 MFMA SrcA hazard in the built kernels (a load into the SrcA registers of the "
-                           "v_mfma_f32_16x16x32_bf16 issued just before it):\n" + msg)
+                           "v_mfma_f32_16x16x32_bf16 / _f16 issued just before it):\n" + msg)
 
 
 if __name__ == "__main__":

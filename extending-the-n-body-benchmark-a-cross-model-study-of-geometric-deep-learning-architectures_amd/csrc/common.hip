@@ -1,4 +1,8 @@
 // Error plumbing and version query for the C ABI.
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "nbx_internal.h"
 
 namespace nbx {
@@ -17,6 +21,18 @@ void set_error(const char* fmt, ...) {
 int hip_error(hipError_t e, const char* where) {
     set_error("%s failed: %s", where, hipGetErrorString(e));
     return NBX_E_HIP;
+}
+
+int lds_limit_160k(const void* kernel) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    NBX_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({kernel, dev})) return NBX_OK;
+    NBX_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    done.insert({kernel, dev});
+    return NBX_OK;
 }
 
 }  // namespace nbx

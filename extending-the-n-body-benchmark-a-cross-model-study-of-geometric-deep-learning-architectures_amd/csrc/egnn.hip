@@ -449,12 +449,7 @@ bool ep_usable(const nbx_egnn_weights* w, int64_t N) {
 template <int H>
 int ep_launch_h(const EgnnPersist& p, int64_t B, hipStream_t st) {
     const size_t lds = ep_lds_bytes(H);
-    static bool attr = false;
-    if (!attr) {
-        NBX_HIP(hipFuncSetAttribute((const void*)egnn_persist_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
-        attr = true;
-    }
+    NBX_LDS_160K(egnn_persist_kernel<H>);
     hipLaunchKernelGGL(egnn_persist_kernel<H>, dim3((unsigned)B), dim3(EP_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;

@@ -921,14 +921,11 @@ int check_train(const nbx_egnn_weights* w, int64_t B, int64_t N) {
 constexpr int TRAIN_GROUPS = 64;   // backward workgroups (partial gradient slices)
 
 int set_lds_attr() {
-    static bool done = false;
-    if (done) return NBX_OK;
     for (const void* k : {(const void*)egnn_train_fwd_kernel<0>, (const void*)egnn_train_fwd_kernel<32>,
                           (const void*)egnn_train_fwd_kernel<64>, (const void*)egnn_train_fwd_kernel<128>,
                           (const void*)egnn_train_bwd_kernel<0>, (const void*)egnn_train_bwd_kernel<32>,
                           (const void*)egnn_train_bwd_kernel<64>, (const void*)egnn_train_bwd_kernel<128>})
-        NBX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    done = true;
+        NBX_LDS_160K(k);
     return NBX_OK;
 }
 

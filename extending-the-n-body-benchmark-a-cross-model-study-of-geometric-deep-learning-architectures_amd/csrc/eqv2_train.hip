@@ -154,11 +154,7 @@ int s2_launch(int64_t rows, int I, int P, int H, const float* T, const float* F,
     const size_t lds = 2 * (size_t)P * ((I + 3) / 4 * 4) * sizeof(float);
     const int which = I <= 9 ? 0 : I <= 32 ? 1 : 2;
     auto kern = which == 0 ? eqv2_s2_kernel<9, BWD> : which == 1 ? eqv2_s2_kernel<32, BWD> : eqv2_s2_kernel<S2_MAXI, BWD>;
-    static size_t granted[3] = {64 * 1024, 64 * 1024, 64 * 1024};   // per instantiation: raise the limit once
-    if (lds > granted[which]) {
-        NBX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        granted[which] = 160 * 1024;
-    }
+    if (lds > 64 * 1024) NBX_LDS_160K(kern);
     hipLaunchKernelGGL(kern, dim3(nblk(rows * H)), dim3(256), lds, st, rows, I, P, H, T, F, X, dOut, out);
     return NBX_OK;
 }

@@ -479,12 +479,7 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
     // (LIN_CONV only: C3's spatial conv 1.64 -> 1.39 GB per launch at the same time; EquiformerV2's
     // LIN_EQMSG measured 1 % slower with it, profiles/r04/lin_xcd_ab)
     p.xcd_remap = (xcd && EPI == LIN_CONV && (p.chunks * bpc) % 8 == 0) ? 1 : 0;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)lin_kernel<NT, ACT, EPI, PREC>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    NBX_LDS_160K((lin_kernel<NT, ACT, EPI, PREC>));
     hipLaunchKernelGGL((lin_kernel<NT, ACT, EPI, PREC>), dim3(p.chunks * bpc), dim3(LIN_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
@@ -657,12 +652,7 @@ int lin_rp_launch(const LinRpProb& p, hipStream_t st) {
         return NBX_E_UNSUPPORTED;
     }
     const size_t lds = (NTILES <= 5 ? 3 : 2) * (size_t)NTILES * LIN_X3_BLK * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)lin_rp_kernel<NTILES, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
-        attr_set = true;
-    }
+    NBX_LDS_160K((lin_rp_kernel<NTILES, ACT>));
     const unsigned blocks = (unsigned)((p.rows + 32 * RP_WAVES - 1) / (32 * RP_WAVES));
     hipLaunchKernelGGL((lin_rp_kernel<NTILES, ACT>), dim3(blocks), dim3(64 * RP_WAVES), lds, st, p);
     NBX_HIP(hipGetLastError());

@@ -46,7 +46,8 @@ struct MsgPreProb {
     int chunks;          // ceil(M / 16)
     int per_chunk;       // persistent blocks per chunk
     int img_floats;      // F = 6 * ceil(M/32) * 512 (x3: * 768)
-    int x3;              // node GEMM on the split-precision bf16x3 MFMA path
+    int prec;            // node GEMM: 0 fp32 MFMA, 1 bf16x3 images, 2 fp16x2 images (descaled by bscale)
+    float bscale;        // fp16x2: the factor that undoes the images' power-of-two weight scale
     int xcd_group;       // block id -> (chunk, slab) so a slab's chunk blocks share one XCD (per_chunk % 8 == 0)
     unsigned long long* dbg;  // optional per-wave phase clocks (tuning only)
     int diag;                 // tuning only: 1 = edge waves idle (timing of the GEMM side alone)

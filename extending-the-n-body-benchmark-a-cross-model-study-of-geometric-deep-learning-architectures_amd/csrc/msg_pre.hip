@@ -14,7 +14,7 @@ constexpr int MP_THREADS = 512;
 // channel quads of row r are stored XOR-swizzled by (r >> 2) & 3 instead, which keeps the GEMM
 // waves' stores -- lane quarters hold rows 4 apart -- on distinct banks and the edge waves'
 // float4 reads whole)
-template <bool X3> struct MpEx {
+template <bool X3> struct MpEx {   // X3: any split-precision node GEMM (bf16x3 or fp16x2)
     static constexpr int RS = X3 ? 16 : 20, PART = 16 * RS, EX = 4 * 6 * PART;
 };
 
@@ -22,8 +22,11 @@ template <bool X3> struct MpEx {
 // v_mfma_f32_16x16x32_bf16 whose A fragment -- lane quarter qd holds k = 8 qd + j -- is exactly
 // the X chunk a lane loads)
 // (X3 runs a static schedule over KCT = ceil(M / 32) K chunks)
-template <bool X3, int KCT = 0>
-__global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const MsgPreProb P) {
+// (PREC 2: the fp16x2 images and v_mfma_f32_16x16x32_f16, 3 terms instead of 6; the node GEMM
+// results are descaled by P.bscale as they are parked in the exchange)
+template <int PREC, int KCT = 0>
+__global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const MsgPreProb P) {
+    constexpr bool X3 = PREC != 0;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
     constexpr int MP_RS = MpEx<X3>::RS, MP_PART = MpEx<X3>::PART, MP_EX = MpEx<X3>::EX;
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int col = X3 ? (c16 & 3) | (((c16 >> 2) ^ qd) << 2) : c16;   // row (4 qd + jj) >> 2 = qd
-                    ex[j * MP_PART + (4 * qd + jj) * MP_RS + col] = acc[j][jj];
+                    ex[j * MP_PART + (4 * qd + jj) * MP_RS + col] = PREC == 2 ? acc[j][jj] * P.bscale : acc[j][jj];
                 }
         };
         if (gemm_wave) {
@@ -141,14 +144,16 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                     // registers last read by chunk kc-1's MFMAs -- at least 18 MFMAs (288 cycles)
                     // earlier, so no pending MFMA's operands are refilled (msg_pre.hip history:
                     // LDS returns overwriting the operands of a pending MFMA corrupted groups).
-                    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
-                    const bf16x8* bimg = reinterpret_cast<const bf16x8*>(img) + lane;
-                    bf16x8 bx[2][6][3], ax[2][3];
-                    auto read_b = [&](int kc, bf16x8 (&bb)[6][3]) {
+                    using SP = SplitP<PREC>;
+                    using SPT = typename SP::T;
+                    constexpr int NP = SP::NP, NT = SP::NT;
+                    const SPT* bimg = reinterpret_cast<const SPT*>(img) + lane;
+                    SPT bx[2][6][NP], ax[2][NP];
+                    auto read_b = [&](int kc, SPT (&bb)[6][NP]) {
 #pragma unroll
                         for (int j = 0; j < 6; ++j)
 #pragma unroll
-                            for (int p3 = 0; p3 < 3; ++p3) bb[j][p3] = bimg[(j * KCT + kc) * 192 + p3 * 64];
+                            for (int p3 = 0; p3 < NP; ++p3) bb[j][p3] = bimg[(j * KCT + kc) * (NP * 64) + p3 * 64];
                     };
                     read_b(0, bx[0]);
                     static_for<0, KCT>([&](auto kcc) {
@@ -166,22 +171,21 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
                                         fmaf(sc0.z, abuf[kc][0].z, sh0.z), fmaf(sc0.w, abuf[kc][0].w, sh0.w)};
                         const float4 v1{fmaf(sc1.x, abuf[kc][1].x, sh1.x), fmaf(sc1.y, abuf[kc][1].y, sh1.y),
                                         fmaf(sc1.z, abuf[kc][1].z, sh1.z), fmaf(sc1.w, abuf[kc][1].w, sh1.w)};
-                        tp_split3(v0, v1, ax[kc & 1][0], ax[kc & 1][1], ax[kc & 1][2]);
-                        const bf16x8 (&a)[3] = ax[kc & 1];
-                        const bf16x8 (&b)[6][3] = bx[kc & 1];
+                        SP::split(v0, v1, ax[kc & 1]);
+                        const SPT (&a)[NP] = ax[kc & 1];
+                        const SPT (&b)[6][NP] = bx[kc & 1];
                         __builtin_amdgcn_sched_barrier(0);
+                        // terms [0, NT/2): then the next chunk's B reads go out under terms [NT/2, NT)
 #pragma unroll
-                        for (int tt = 0; tt < 3; ++tt)
+                        for (int tt = 0; tt < NT / 2; ++tt)
 #pragma unroll
-                            for (int j = 0; j < 6; ++j)
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], b[j][TB[tt]], acc[j], 0, 0, 0);
+                            for (int j = 0; j < 6; ++j) acc[j] = mfma16x16(a[SP::TA[tt]], b[j][SP::TB[tt]], acc[j]);
                         __builtin_amdgcn_sched_barrier(0);
                         if constexpr (kc + 1 < KCT) read_b(kc + 1, bx[(kc + 1) & 1]);
 #pragma unroll
-                        for (int tt = 3; tt < 6; ++tt)
+                        for (int tt = NT / 2; tt < NT; ++tt)
 #pragma unroll
-                            for (int j = 0; j < 6; ++j)
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], b[j][TB[tt]], acc[j], 0, 0, 0);
+                            for (int j = 0; j < 6; ++j) acc[j] = mfma16x16(a[SP::TA[tt]], b[j][SP::TB[tt]], acc[j]);
                         __builtin_amdgcn_sched_barrier(0);
                     });
                     // the next group's B reads are 18+ MFMAs away; the A prefetch below only
@@ -319,12 +323,12 @@ __global__ __launch_bounds__(MP_THREADS, X3 ? 1 : 2) void msg_pre_kernel(const M
 }
 
 inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
-    return ((size_t)2 * p.img_floats + 2 * (p.x3 ? MpEx<true>::EX : MpEx<false>::EX) + 3 * 32 * ((p.M + 31) / 32)) * 4;
+    return ((size_t)2 * p.img_floats + 2 * (p.prec ? MpEx<true>::EX : MpEx<false>::EX) + 3 * 32 * ((p.M + 31) / 32)) * 4;
 }
 
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
     if (p.V <= 0) return NBX_OK;
-    if (p.M > 128 || p.NG <= 0 || (p.x3 && p.M > 96)) {   // x3: two bf16x3 images + exchange fit LDS up to mul 96
+    if (p.M > 128 || p.NG <= 0 || (p.prec && p.M > 96)) {   // split images + exchange fit the LDS up to mul 96
         set_error("msg_pre: needs mul <= 128 and 2 <= N <= 16 (got mul %d, N %d)", p.M, p.N);
         return NBX_E_UNSUPPORTED;
     }
@@ -333,7 +337,7 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         return NBX_E_UNSUPPORTED;
     }
     p.chunks = (p.M + 15) / 16;
-    p.img_floats = 6 * ((p.M + 31) / 32) * (p.x3 ? 768 : 512);
+    p.img_floats = 6 * ((p.M + 31) / 32) * (p.prec == 1 ? 768 : 512);   // bf16x3 1.5x, fp16x2 1x fp32
     p.n_slabs = (int)((p.V + p.NG - 1) / p.NG);
     // one block per CU (LDS-bound); balance the group rounds over the chunk's blocks
     int per = num_cus / p.chunks;
@@ -350,24 +354,20 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         set_error("msg_pre: %zu bytes of LDS (> 160 KiB)", lds);
         return NBX_E_UNSUPPORTED;
     }
-    static bool attr_set = false;
-    if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)msg_pre_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
-        for (const void* k : {(const void*)msg_pre_kernel<true, 1>, (const void*)msg_pre_kernel<true, 2>,
-                              (const void*)msg_pre_kernel<true, 3>})
-            NBX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    for (const void* k : {(const void*)msg_pre_kernel<0>, (const void*)msg_pre_kernel<1, 1>,
+                          (const void*)msg_pre_kernel<1, 2>, (const void*)msg_pre_kernel<1, 3>,
+                          (const void*)msg_pre_kernel<2, 1>, (const void*)msg_pre_kernel<2, 2>,
+                          (const void*)msg_pre_kernel<2, 3>})
+        NBX_LDS_160K(k);
     const int kct = (p.M + 31) / 32;
-    if (p.x3 && kct == 3)
-        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 3>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
-    else if (p.x3 && kct == 1)
-        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 1>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
-    else if (p.x3 && kct == 2)
-        NBX_TIMED_LAUNCH((msg_pre_kernel<true, 2>), dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
-    else
-        NBX_TIMED_LAUNCH(msg_pre_kernel<false>, dim3(p.chunks * p.per_chunk), dim3(MP_THREADS), lds, st, p);
+    const dim3 grid(p.chunks * p.per_chunk);
+    if (p.prec == 2 && kct == 3) NBX_TIMED_LAUNCH((msg_pre_kernel<2, 3>), grid, dim3(MP_THREADS), lds, st, p);
+    else if (p.prec == 2 && kct == 2) NBX_TIMED_LAUNCH((msg_pre_kernel<2, 2>), grid, dim3(MP_THREADS), lds, st, p);
+    else if (p.prec == 2 && kct == 1) NBX_TIMED_LAUNCH((msg_pre_kernel<2, 1>), grid, dim3(MP_THREADS), lds, st, p);
+    else if (p.prec == 1 && kct == 3) NBX_TIMED_LAUNCH((msg_pre_kernel<1, 3>), grid, dim3(MP_THREADS), lds, st, p);
+    else if (p.prec == 1 && kct == 1) NBX_TIMED_LAUNCH((msg_pre_kernel<1, 1>), grid, dim3(MP_THREADS), lds, st, p);
+    else if (p.prec == 1 && kct == 2) NBX_TIMED_LAUNCH((msg_pre_kernel<1, 2>), grid, dim3(MP_THREADS), lds, st, p);
+    else NBX_TIMED_LAUNCH(msg_pre_kernel<0>, grid, dim3(MP_THREADS), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

@@ -35,6 +35,15 @@ int hip_error(hipError_t e, const char* where);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Raise `kernel`'s dynamic-LDS limit to 160 KiB on the current device, once per (kernel, device):
+// the attribute is per device, so a process that launches on several devices sets it on each
+// (csrc/common.hip).  Returns NBX_OK or NBX_E_HIP.
+int lds_limit_160k(const void* kernel);
+#define NBX_LDS_160K(kernel)                                                     \
+    do {                                                                         \
+        if (int _rc = ::nbx::lds_limit_160k((const void*)(kernel))) return _rc;  \
+    } while (0)
+
 // Kernel-execution timing for the *_forward_timed entry points: when a start / stop event pair is
 // armed, the next NBX_TIMED_LAUNCH records the kernel's own begin / end on them
 // (hipExtLaunchKernel: the same interval a profiler's kernel trace reports, without the

@@ -814,12 +814,7 @@ int po_ffn_launch(const FfnProb& p, hipStream_t st) {
     NBX_CHECK_ARG(p.ldi % 4 == 0 && p.ldi <= NTI * 32, "po_ffn: input stride must be a multiple of 4, <= %d", NTI * 32);
     const size_t lds = (3 * (size_t)(NTI + NTO) * nbx::LIN_X3_BLK + p.F) * 4;
     NBX_CHECK_ARG(lds <= 160 * 1024, "po_ffn: %zu bytes of LDS", lds);
-    static bool attr_set = false;
-    if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)po_ffn_kernel<NTI, NTO, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
-        attr_set = true;
-    }
+    NBX_LDS_160K((po_ffn_kernel<NTI, NTO, MODE>));
     const unsigned blocks = (unsigned)((p.rows + 32 * FFN_WAVES - 1) / (32 * FFN_WAVES));
     static const bool debug = getenv("NBX_PO_FFN_DEBUG") != nullptr;
     static unsigned long long* dbg = nullptr;

@@ -30,7 +30,6 @@
 #include "tp16.h"
 #include "tp_fused.h"
 #include "msg_pre.h"
-#include "upd_vec.h"
 
 namespace {
 
@@ -680,7 +679,6 @@ using SK_UPD1 = nbx::StatSK<12, 12, 6, 6>;
 using SK_UPD1_32 = nbx::StatSK<4, 4, 2, 2>;
 using SK_UPD1_SEG = nbx::StatSK<12, 12, 6, 6, 4>;
 using SK_UPD1_SEG_X3 = nbx::StatSKX3<12, 12, 6, 6, 4>;
-using SK_UPD1S_SEG_X3 = nbx::StatSKX3<12, 12, 6, 0, 4>;   // split form: the 0e items only (upd_vec.h)
 using SK_UPD1_32_SEG = nbx::StatSK<4, 4, 2, 2, 4>;
 using SK_UPD2 = nbx::StatSK<6, 3, 0, 3>;
 using SK_UPD2_32 = nbx::StatSK<2, 1, 0, 1>;
@@ -690,6 +688,15 @@ using SK_PP1_SEG = nbx::StatSK<6, 6, 3, 3, 2>;   // pre_pool1 reading [x_s | x_v
 using SK_PP1_32_SEG = nbx::StatSK<2, 2, 1, 1, 2>;
 using SK_MSG2_X3 = nbx::StatSKX3<6, 6, 3, 3>;
 using SK_MSG2_32_X3 = nbx::StatSKX3<2, 2, 1, 1>;
+// fp16x2 split path (include/nbx.h "fp16x2 images")
+using SK_MSG2_H2 = nbx::StatSKH2<6, 6, 3, 3>;
+using SK_MSG2_32_H2 = nbx::StatSKH2<2, 2, 1, 1>;
+using SK_UPD1_SEG_H2 = nbx::StatSKH2<12, 12, 6, 6, 4>;
+using SK_UPD1_32_SEG_H2 = nbx::StatSKH2<4, 4, 2, 2, 4>;
+using SK_UPD2_H2 = nbx::StatSKH2<6, 3, 0, 3>;
+using SK_UPD2_32_H2 = nbx::StatSKH2<2, 1, 0, 1>;
+using SK_PP1_SEG_H2 = nbx::StatSKH2<6, 6, 3, 3, 2>;
+using SK_PP1_32_SEG_H2 = nbx::StatSKH2<2, 2, 1, 1, 2>;
 
 // message_layer_2 on the split-precision MFMA path when the weights carry a bf16x3 image
 // (NBX_X3=0: fp32 MFMA path, A/B only)
@@ -702,14 +709,13 @@ bool x3_enabled() {
     return v == 1;
 }
 
-// Tuning switch for A/B runs on the GPU box (NBX_MSG_VARIANT=<waves>x<depth>, e.g. 8x3);
-// the default is the measured best.
-int msg_variant() {
+// Split-precision MFMA path of the SEGNN TPs: 2 = the fp16x2 images (default, when present),
+// 1 = the bf16x3 images, 0 = fp32 MFMA.  NBX_SPLIT=x3 / NBX_X3=0 select 1 / 0 (A/B only).
+int split_prec() {
     static int v = -1;
     if (v < 0) {
-        const char* e = getenv("NBX_MSG_VARIANT");
-        const char* x = e ? strchr(e, 'x') : nullptr;
-        v = x ? atoi(e) * 10 + atoi(x + 1) : 83;
+        const char* e = getenv("NBX_SPLIT");
+        v = !x3_enabled() ? 0 : (e && (e[0] == 'x' || e[0] == '1')) ? 1 : (e && e[0] == '0') ? 0 : 2;
     }
     return v;
 }
@@ -748,14 +754,22 @@ int tp_debug_dump(const nbx::TpProb& p, hipStream_t st, int waves) {
 }
 
 template <int NS, int NV, int EPI>
-int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3) {
+int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3, const void* img_h2,
+                   float h2_descale) {
     // message_layer_2 at mul = 96 / 32: fully unrolled static chunk schedule
     if (static_enabled()) {
-        if (img_x3 && x3_enabled()) {
+        if (img_h2 && split_prec() == 2) {
+            const float* fp32_img = p.B;
+            p.B = static_cast<const float*>(img_h2);
+            p.bscale = h2_descale;
+            if (sk_matches<SK_MSG2_H2>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_H2>(p, st, tm);
+            if (sk_matches<SK_MSG2_32_H2>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_32_H2>(p, st, tm);
+            p.B = fp32_img;
+        }
+        if (img_x3 && split_prec() == 1) {
             const float* fp32_img = p.B;
             p.B = static_cast<const float*>(img_x3);
             if (sk_matches<SK_MSG2_X3>(p, NS, NV)) {
-                if (getenv("NBX_X3_D4")) return run_tp<NS, NV, EPI, 8, 4, SK_MSG2_X3>(p, st, tm);
                 return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_X3>(p, st, tm);
             }
             if (sk_matches<SK_MSG2_32_X3>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_32_X3>(p, st, tm);
@@ -764,18 +778,15 @@ int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void*
         if (sk_matches<SK_GATE>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_GATE>(p, st, tm);
         if (sk_matches<SK_GATE_32>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_GATE_32>(p, st, tm);
     }
-    switch (msg_variant()) {
-        case 82: return run_tp<NS, NV, EPI, 8, 2>(p, st, tm);
-        case 84: return run_tp<NS, NV, EPI, 8, 4>(p, st, tm);
-        default: return run_tp<NS, NV, EPI, 8, 3>(p, st, tm);
-    }
+    return run_tp<NS, NV, EPI, 8, 3>(p, st, tm);
 }
 
 template <int NS, int NV, int EPI>
-int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3 = nullptr) {
+int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3 = nullptr,
+               const void* img_h2 = nullptr, float h2_descale = 1.f) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
     if (debug) p.dbg = tp_dbg_buf(st);
-    const int rc = run_tp_msg_sel<NS, NV, EPI>(p, st, tm, img_x3);
+    const int rc = run_tp_msg_sel<NS, NV, EPI>(p, st, tm, img_x3, img_h2, h2_descale);
     if (rc || !debug) return rc;
     return tp_debug_dump(p, st, 8);
 }
@@ -827,29 +838,13 @@ int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
     k += NV ? 3.0 * p.Kv : 0.0;
-    // the split update_layer_1 (GATE_VRAW + upd_vec_kernel) is timed as the update_layer_1 kind; its
-    // two launches count as one launch of the kind
-    constexpr int kind = EPI == nbx::TP_GATE_VRAW ? (int)nbx::TP_GATE_NODE : EPI;
+    constexpr int kind = EPI;
     tm->kind.push_back(kind);
     tm->flops[kind] += 2.0 * p.rows * 16.0 * p.chunks * k;
     tm->launches[kind] += 1;
     return NBX_OK;
 }
 
-int run_upd_vec(const nbx::UpdVecProb& p, hipStream_t st, KernelTiming* tm) {
-    if (!tm) return nbx::upd_vec_launch(p, st);
-    hipEvent_t a, b;
-    NBX_HIP(hipEventCreate(&a));
-    NBX_HIP(hipEventCreate(&b));
-    tm->ev.push_back(a);
-    tm->ev.push_back(b);
-    nbx::armed_events() = {a, b};
-    if (int rc = nbx::upd_vec_launch(p, st)) return rc;
-    NBX_HIP(nbx::disarm_events(st));
-    tm->kind.push_back(nbx::TP_GATE_NODE);
-    tm->flops[nbx::TP_GATE_NODE] += 2.0 * 3.0 * p.V * 2.0 * p.M * p.M;
-    return NBX_OK;
-}
 
 int run_msg_pre(nbx::MsgPreProb& p, hipStream_t st, KernelTiming* tm) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
@@ -1047,10 +1042,15 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             }
             // split-precision node GEMM when its two bf16x3 images and the exchange buffers fit the
             // LDS (mul <= 96); wider layers run the fp32 MFMA node GEMM
-            if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && x3_enabled() && M <= 96 && !getenv("NBX_X3_NOMP")) {
+            if (L.node_pre_s_img_h2 && L.node_pre_v_img_h2 && split_prec() == 2 && M <= 96) {
+                mp.Simg = static_cast<const float*>(L.node_pre_s_img_h2);
+                mp.Vimg = static_cast<const float*>(L.node_pre_v_img_h2);
+                mp.prec = 2;
+                mp.bscale = L.node_pre_h2_descale;
+            } else if (L.node_pre_s_img_x3 && L.node_pre_v_img_x3 && split_prec() == 1 && M <= 96) {
                 mp.Simg = static_cast<const float*>(L.node_pre_s_img_x3);
                 mp.Vimg = static_cast<const float*>(L.node_pre_v_img_x3);
-                mp.x3 = 1;
+                mp.prec = 1;
             }
             if (int rc = run_msg_pre(mp, st, tm)) return rc;
         } else if (N > 1) {
@@ -1094,7 +1094,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if (seg_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
             if (bn_atomic) p.bn_sums = sums_of(l, 0);
             if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
-                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3)) return rc;
+                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3, L.msg2_img_h2, L.msg2_h2_descale))
+                    return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
                 if (bn_atomic) {
@@ -1138,40 +1139,15 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
-            // split form (upd_vec.h; NBX_UPD1_SPLIT=1, A/B only): the 1o GEMM of all channels, then the
-            // 0e GEMM + gate.  Measured r04 (profiles/r04/segnn_upd1_split_summary.md): 10.8 + 15.0 us
-            // against 22.7-24 us for the combined kernel -- the second launch's staging and fill / drain
-            // cost more than the VALU the split saves, so the combined kernel stays the default
-            static const bool upd1_split = getenv("NBX_UPD1_SPLIT") && atoi(getenv("NBX_UPD1_SPLIT")) != 0;
-            if (M == 96 && L.upd1_img_x3 && x3_enabled() && upd1_split) {
-                const int kc_s = (4 * M + 31) / 32, kc_t = (2 * M + 31) / 32, kc_v = (2 * M + 31) / 32;
-                const int stride = (2 * kc_s + kc_t + kc_v) * 768;   // floats per bf16x3 chunk image
-                nbx::UpdVecProb vp;
-                memset(&vp, 0, sizeof(vp));
-                vp.xv = ws.X + V * M; vp.av = ws.AGG + V * M;
-                vp.img = static_cast<const float*>(L.upd1_img_x3);
-                vp.img_stride = stride; vp.vec_off = (2 * kc_s + kc_t) * 768;
-                vp.xcoef = xprev; vp.mcoef = ws.coef_msg; vp.mbn = p.mbn;
-                vp.out = ws.U1V; vp.V = V; vp.M = M;
-                if (int rc = run_upd_vec(vp, st, tm)) return rc;
-                p.B = static_cast<const float*>(L.upd1_img_x3);
-                p.img_stride = stride;
-                p.Kv = 0;
-                p.Av = ws.U1V; p.lda_v = M; p.plane_stride = V * M;
-                p.mbn = nbx::BnSrc{};   // finalised by upd_vec_kernel's block 0 into ws.coef_msg
-                if (int rc = run_tp16_w<3, 0, nbx::TP_GATE_VRAW, 1, 8, 3, 1, SK_UPD1S_SEG_X3>(p, st, tm)) return rc;
-            } else if (M == 96 && L.upd1_img_x3 && x3_enabled()) {
-                p.B = static_cast<const float*>(L.upd1_img_x3);
-                // A-ring depth (NBX_UPD1_PF, A/B): 3 = three B sets; > 3 = two B sets + the deeper ring
-                static const int upd1_pf = getenv("NBX_UPD1_PF") ? atoi(getenv("NBX_UPD1_PF")) : 3;
-                int rc;
-                switch (upd1_pf) {
-                    case 5: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 5, 1, SK_UPD1_SEG_X3>(p, st, tm); break;
-                    case 6: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 6, 1, SK_UPD1_SEG_X3>(p, st, tm); break;
-                    case 7: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 7, 1, SK_UPD1_SEG_X3>(p, st, tm); break;
-                    default: rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_X3>(p, st, tm);
-                }
+            if ((M == 96 || M == 32) && L.upd1_img_h2 && split_prec() == 2) {
+                p.B = static_cast<const float*>(L.upd1_img_h2);
+                p.bscale = L.upd1_h2_descale;
+                const int rc = M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm)
+                                       : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
                 if (rc) return rc;
+            } else if (M == 96 && L.upd1_img_x3 && split_prec() == 1) {
+                p.B = static_cast<const float*>(L.upd1_img_x3);
+                if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_X3>(p, st, tm)) return rc;
             } else if (M == 96) {
                 if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG>(p, st, tm)) return rc;
             } else {
@@ -1207,30 +1183,16 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.xcoef = xprev;
             if (seg_upd) { p.out_dot = ws.XD; }
             p.chunks = (M + 15) / 16;
-            // update_layer_2: one 16-channel chunk per wave, full K (CG 1, KS 1; measured against CG 2 / KS 2,
-            // CG 1 / KS 2, CG 2 / KS 1, CG 1 / KS 4: 15.1 vs 17.8 / 16.3 / 19.5 / 20.9 us). NBX_UPD2_VARIANT=CG*10+KS
-            static const int upd2_var = getenv("NBX_UPD2_VARIANT") ? atoi(getenv("NBX_UPD2_VARIANT")) : 11;
-            // A-ring depth (NBX_UPD2_PF, A/B): at C2 a wave owns one 16-row tile whose 15 A chunks
-            // (30 KB) stream from L2; PF = 16 issues them all before the weight staging
-            static const int upd2_pf = getenv("NBX_UPD2_PF") ? atoi(getenv("NBX_UPD2_PF")) : 3;
-            if (upd2_var == 11 && upd2_pf != 3 && M == 96 && static_enabled()) {
-                int rc;
-                switch (upd2_pf) {
-                    case 6: rc = run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 6, 1, SK_UPD2>(p, st, tm); break;
-                    case 9: rc = run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 9, 1, SK_UPD2>(p, st, tm); break;
-                    default: rc = run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 16, 1, SK_UPD2>(p, st, tm);
-                }
+            // update_layer_2: one 16-channel chunk per wave, full K (CG 1, KS 1; r02 measured it against
+            // CG 2 / KS 2, CG 1 / KS 2, CG 2 / KS 1, CG 1 / KS 4: 15.1 vs 17.8 / 16.3 / 19.5 / 20.9 us)
+            if ((M == 96 || M == 32) && L.upd2_img_h2 && split_prec() == 2 && static_enabled()) {
+                p.B = static_cast<const float*>(L.upd2_img_h2);
+                p.bscale = L.upd2_h2_descale;
+                const int rc = M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm)
+                                       : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2>(p, st, tm);
                 if (rc) return rc;
-            } else if (upd2_var == 11) {
-                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
-            } else if (upd2_var == 12) {
-                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
-            } else if (upd2_var == 21) {
-                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
-            } else if (upd2_var == 14) {
-                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 4, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             } else {
-                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 2, 2, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
+                if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             }
             wpc_feat = p.waves_per_chunk;
             if (bn_atomic) {
@@ -1272,7 +1234,13 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.B = w->pp1_img;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
-        if (M == 96) {
+        if (w->pp1_img_h2 && split_prec() == 2) {
+            p.B = static_cast<const float*>(w->pp1_img_h2);
+            p.bscale = w->pp1_h2_descale;
+            const int rc = M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2>(p, st, tm)
+                                   : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG_H2>(p, st, tm);
+            if (rc) return rc;
+        } else if (M == 96) {
             if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG>(p, st, tm)) return rc;
         } else {
             if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG>(p, st, tm)) return rc;
@@ -1287,15 +1255,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.Av = ws.U1V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
-        // pre_pool1: CG 1 / KS 1 (measured against CG 2: -0.8 % step time). NBX_PP1_VARIANT=CG*10+KS (tuning)
-        static const int pp1_var = getenv("NBX_PP1_VARIANT") ? atoi(getenv("NBX_PP1_VARIANT")) : 11;
-        if (pp1_var == 11) {
-            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
-        } else if (pp1_var == 12) {
-            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 2, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
-        } else {
-            if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 2, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
-        }
+        // pre_pool1: CG 1 / KS 1 (r02: CG 2 measured -0.8 % step time)
+        if (int rc = run_tp16_try<3, 1, nbx::TP_GATE_NODE, 1, 1, SK_GATE, SK_GATE_32>(p, st, tm)) return rc;
     }
     }
     if (upd && upd->featurize_next && !gr) {
@@ -1354,9 +1315,8 @@ extern "C" int nbx_segnn_rollout(const nbx_segnn_weights* w, float* pos, float* 
     hipLaunchKernelGGL(rollout_update_kernel, dim3(ub), dim3(256), 0, st, pos, vel, ws.out, V, (int)N, (int64_t)0,
                        num_frames, traj_pos, traj_vel);
     NBX_LAUNCH_CHECK("rollout_update");
-    // whole systems per rollout_pp2_kernel block (NBX_NO_FE_FUSE: tuning / A-B only)
-    static const bool no_fuse = getenv("NBX_NO_FE_FUSE") != nullptr;
-    const bool fuse = !no_fuse && N <= RPP2_MAX;
+    // whole systems per rollout_pp2_kernel block: the next frame's featurisation fused into pre_pool2
+    const bool fuse = N <= RPP2_MAX;
     for (int64_t f = 1; f < num_frames; ++f) {
         // the state update + trajectory write of frame f is fused into pre_pool2's epilogue, and
         // (fuse) so is the featurisation of frame f + 1's input

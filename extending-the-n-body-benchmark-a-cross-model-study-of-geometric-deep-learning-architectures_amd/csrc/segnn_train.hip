@@ -32,8 +32,8 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // contiguous dimension when VEC: 16-byte aligned operands and leading dimensions) while the current
 // one is multiplied from LDS.  The training GEMMs are small (a B=64 batch: 320-3840 rows), so the
 // grid is split along K until it holds ~256 blocks of >= 4 K steps (gemm_splits): each z writes its
-// partial tile into `part` [z][M][N] and gemm_reduce_kernel sums them in z order.  An opt-in variant
-// (T = 32, gemm_tile_size) uses 32 x 32 tiles of one wave when the 64 x 64 grid would not fill the chip.
+// partial tile into `part` [z][M][N] and gemm_reduce_kernel sums them in z order.  (32 x 32 one-wave
+// tiles for grids that would not fill the chip measured slower on every training step, r04.)
 constexpr int GB = 64, GK = 32;
 
 template <int T>
@@ -197,18 +197,12 @@ struct ReduceBatch {
     float beta[GMAXP];
     int64_t first[GMAXP + 1];   // first element of each problem in the flattened index
     int count;
-    int serial;
 };
 
 // sum_z part[z * MN + e] for z = 0 .. splits - 1, added in z order (bit-identical to the plain loop)
 // with the loads issued 8 at a time: a serial load -> add chain paid one full memory latency per split
-__device__ __forceinline__ float splitk_sum(const float* __restrict__ part, int splits, int64_t MN, int64_t e,
-                                            bool serial) {
+__device__ __forceinline__ float splitk_sum(const float* __restrict__ part, int splits, int64_t MN, int64_t e) {
     float s = 0.f;
-    if (serial) {   // NBX_SPLITK_SERIAL=1: the plain loop (A/B)
-        for (int z = 0; z < splits; ++z) s += part[(int64_t)z * MN + e];
-        return s;
-    }
     int z = 0;
     for (; z + 8 <= splits; z += 8) {
         float v[8];
@@ -236,35 +230,22 @@ __global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
         if (q < b.count && i >= b.first[q]) p = q;
     const int64_t e = i - b.first[p], N = b.N[p], MN = b.M[p] * N;
     const int64_t r = e / N, c = e - r * N;
-    const float s = splitk_sum(b.part[p], b.splits[p], MN, e, b.serial);
+    const float s = splitk_sum(b.part[p], b.splits[p], MN, e);
     float* q = b.C[p] + r * b.ldc[p] + c;
     *q = b.beta[p] != 0.f ? s + b.beta[p] * *q : s;
 }
 
 __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, int64_t M, int64_t N,
-                                   float* __restrict__ C, int64_t ldc, float beta, int serial) {
+                                   float* __restrict__ C, int64_t ldc, float beta) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= M * N) return;
     const int64_t r = i / N, c = i - r * N;
-    const float s = splitk_sum(part, splits, M * N, i, serial);
+    const float s = splitk_sum(part, splits, M * N, i);
     float* p = C + r * ldc + c;
     *p = beta != 0.f ? s + beta * *p : s;
 }
 
-bool splitk_serial() {
-    static const bool v = getenv("NBX_SPLITK_SERIAL") && atoi(getenv("NBX_SPLITK_SERIAL")) != 0;
-    return v;
-}
-
 int64_t gemm_tiles(int64_t M, int64_t N, int T) { return ((M + T - 1) / T) * ((N + T - 1) / T); }
-
-// 32 when NBX_GEMM_TILE32=1 and the launch's 64 x 64 grid (tiles64, summed over its problems) holds
-// fewer than 256 tiles.  Off by default: measured slower on every training step (r04 A/B, DESIGN
-// §3.6: a one-wave block halves the waves per CU that LDS admits, and split-K already fills the chip)
-int gemm_tile_size(int64_t tiles64) {
-    static const bool on = getenv("NBX_GEMM_TILE32") && atoi(getenv("NBX_GEMM_TILE32")) != 0;
-    return on && tiles64 < 256 ? 32 : GB;
-}
 
 int gemm_splits(int64_t M, int64_t N, int64_t K, int T) {
     const int64_t tiles = gemm_tiles(M, N, T);
@@ -663,23 +644,6 @@ __global__ __launch_bounds__(256) void segment_sum4_kernel(int64_t n, int cols, 
     }
 }
 
-// out[n][c] (+)= sum_{j in [ptr[n], ptr[n+1])} in[eid[j]][c] per plane, in CSR order
-__global__ void segment_sum_kernel(int64_t n, int cols, const int* __restrict__ ptr, const int* __restrict__ eid,
-                                   const float* __restrict__ in, int64_t ldi, int64_t psi, float* __restrict__ out,
-                                   int64_t ldo, int64_t pso, int planes, int accumulate) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n * cols) return;
-    const int64_t r = i / cols;
-    const int c = (int)(i - r * cols);
-    const int j0 = ptr[r], j1 = ptr[r + 1];
-    for (int k = 0; k < planes; ++k) {
-        float s = 0.f;
-        for (int j = j0; j < j1; ++j) s += in[k * psi + (int64_t)eid[j] * ldi + c];
-        float* o = out + k * pso + r * ldo + c;
-        *o = accumulate ? *o + s : s;
-    }
-}
-
 // ---------------------------------------------------------------- featurisation (no gradient)
 // O3Transform (o3_building_blocks.py:231-278) + catch_isolated_nodes (segnn.py:136-148) on an edge
 // list: rel = pos[src] - pos[dst]; node attribute = mean over the incoming edges (dst CSR) of
@@ -742,7 +706,7 @@ unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n
 // ======================================================================== C ABI (include/nbx.h)
 extern "C" int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes) {
     NBX_CHECK_ARG(bytes != nullptr && M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_workspace_bytes: bad arguments");
-    const int s = gemm_splits(M, N, K, gemm_tile_size(gemm_tiles(M, N, GB)));
+    const int s = gemm_splits(M, N, K, GB);
     *bytes = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
     return NBX_OK;
 }
@@ -759,7 +723,7 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     NBX_CHECK_ARG(!ones || N >= 1, "nbx_gemm_f32: NBX_GEMM_B_ONES needs N >= 1");
     NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N,
                   "nbx_gemm_f32: leading dimension too small");
-    const int T = gemm_tile_size(gemm_tiles(M, N, GB));
+    constexpr int T = GB;
     const int splits = gemm_splits(M, N, K, T);
     const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
     NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
@@ -784,12 +748,11 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
             else go(gemm_f32_kernel<false, false, false, TT>);
         }
     };
-    if (T == 32) launch(std::integral_constant<int, 32>{});
-    else launch(std::integral_constant<int, GB>{});
+    launch(std::integral_constant<int, GB>{});
     NBX_LAUNCH_CHECK("gemm_f32");
     if (splits > 1) {
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,
-                           N, C, ldc, beta, (int)splitk_serial());
+                           N, C, ldc, beta);
         NBX_LAUNCH_CHECK("gemm_reduce");
     }
     return NBX_OK;
@@ -799,9 +762,7 @@ extern "C" int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t
     NBX_CHECK_ARG(bytes != nullptr && dims != nullptr && count >= 1 && count <= GMAXP,
                   "nbx_gemm_f32_batched_workspace_bytes: bad arguments (count 1..%d)", GMAXP);
     size_t n = 0;
-    int64_t tiles64 = 0;
-    for (int i = 0; i < count; ++i) tiles64 += gemm_tiles(dims[6 * i], dims[6 * i + 1], GB);
-    const int T = gemm_tile_size(tiles64);
+    constexpr int T = GB;
     for (int i = 0; i < count; ++i) {
         const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
         NBX_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_batched_workspace_bytes: negative size");
@@ -823,9 +784,7 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
     memset(&rb, 0, sizeof(rb));
     int blocks = 0, nred = 0;
     size_t ws_off = 0;
-    int64_t tiles64 = 0;
-    for (int i = 0; i < count; ++i) tiles64 += gemm_tiles(dims[6 * i], dims[6 * i + 1], GB);
-    const int T = gemm_tile_size(tiles64);
+    constexpr int T = GB;
     for (int i = 0; i < count; ++i) {
         const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
         const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
@@ -862,12 +821,8 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
     }
     gb.count = count;
     rb.count = nred;
-    rb.serial = splitk_serial() ? 1 : 0;
     hipStream_t st = (hipStream_t)stream;
-    if (T == 32)
-        hipLaunchKernelGGL(gemm_f32_batched_kernel<32>, dim3((unsigned)blocks), dim3(GemmCfg<32>::THREADS), 0, st, gb);
-    else
-        hipLaunchKernelGGL(gemm_f32_batched_kernel<GB>, dim3((unsigned)blocks), dim3(GemmCfg<GB>::THREADS), 0, st, gb);
+    hipLaunchKernelGGL(gemm_f32_batched_kernel<GB>, dim3((unsigned)blocks), dim3(GemmCfg<GB>::THREADS), 0, st, gb);
     NBX_LAUNCH_CHECK("gemm_f32_batched");
     if (nred) {
         hipLaunchKernelGGL(gemm_reduce_batched_kernel, dim3(nblk(rb.first[nred])), dim3(256), 0, st, rb);
@@ -1005,16 +960,20 @@ extern "C" int nbx_bn_train_backward(int64_t rows, int32_t M, const float* S, co
 extern "C" int nbx_bn_train_sums(int64_t rows, int32_t M, const float* S, const float* V, const float* dOS,
                                  const float* dOV, const float* save, double* sums, void* workspace,
                                  size_t workspace_bytes, void* stream) {
-    NBX_CHECK_ARG(rows > 0 && M > 0 && sums, "nbx_bn_train_sums: need rows > 0, M > 0 and sums");
+    // rows == 0 (an empty shard of a sharded batch): zero sums and a zero count, so every rank still
+    // reaches the caller's all-reduce
+    NBX_CHECK_ARG(rows >= 0 && M > 0 && sums, "nbx_bn_train_sums: need rows >= 0, M > 0 and sums");
     NBX_CHECK_ARG(!dOS == !dOV && (!dOS || save), "nbx_bn_train_sums: the backward sums need dOS, dOV and save");
     const int nb = (int)((rows + BN_ROWS - 1) / BN_ROWS);
-    NBX_CHECK_ARG(workspace && workspace_bytes >= (size_t)(nb + 1) * 3 * M * sizeof(double),
+    NBX_CHECK_ARG(rows == 0 || (workspace && workspace_bytes >= (size_t)(nb + 1) * 3 * M * sizeof(double)),
                   "nbx_bn_train_sums: workspace too small");
     hipStream_t st = (hipStream_t)stream;
     double* part = (double*)workspace;
-    hipLaunchKernelGGL(bn_partial_kernel, dim3((unsigned)nb, (unsigned)((M + 63) / 64)), dim3(256), 0, st, rows, M, S, V,
-                       dOS, dOV, save, part);
-    NBX_LAUNCH_CHECK("bn_partial(sums)");
+    if (rows > 0) {
+        hipLaunchKernelGGL(bn_partial_kernel, dim3((unsigned)nb, (unsigned)((M + 63) / 64)), dim3(256), 0, st, rows, M,
+                           S, V, dOS, dOV, save, part);
+        NBX_LAUNCH_CHECK("bn_partial(sums)");
+    }
     hipLaunchKernelGGL(bn_sum_kernel, dim3(nblk(M)), dim3(256), 0, st, nb, rows, M, part, sums);
     NBX_LAUNCH_CHECK("bn_sum");
     return NBX_OK;
@@ -1023,11 +982,13 @@ extern "C" int nbx_bn_train_sums(int64_t rows, int32_t M, const float* S, const 
 extern "C" int nbx_bn_train_apply(int64_t rows, int32_t M, const float* S, const float* V, const float* weight,
                                   const float* bias, const double* sums, float* running_mean, float* running_var,
                                   float eps, float momentum, float* save, float* OS, float* OV, void* stream) {
-    NBX_CHECK_ARG(rows > 0 && M > 0 && sums, "nbx_bn_train_apply: need rows > 0, M > 0 and sums");
+    // rows == 0: the statistics (and the running-stat update) from the all-reduced sums, no rows to apply
+    NBX_CHECK_ARG(rows >= 0 && M > 0 && sums, "nbx_bn_train_apply: need rows >= 0, M > 0 and sums");
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk(M)), dim3(256), 0, st, 1, rows, M, sums, eps, momentum, running_mean,
                        running_var, save, sums + 3 * M);
     NBX_LAUNCH_CHECK("bn_stats(sync)");
+    if (rows == 0) return NBX_OK;
     hipLaunchKernelGGL(bn_apply_train_kernel, dim3(nblk(rows * M)), dim3(256), 0, st, rows, M, S, V, save, weight, bias,
                        OS, OV);
     NBX_LAUNCH_CHECK("bn_apply_train(sync)");
@@ -1046,7 +1007,8 @@ extern "C" int nbx_bn_train_param_grads(int32_t M, const float* save, const doub
 extern "C" int nbx_bn_train_backward_apply(int64_t rows, int32_t M, const float* S, const float* V,
                                            const float* weight, const float* save, const double* sums,
                                            const float* dOS, const float* dOV, float* dS, float* dV, void* stream) {
-    NBX_CHECK_ARG(rows > 0 && M > 0 && sums, "nbx_bn_train_backward_apply: need rows > 0, M > 0 and sums");
+    NBX_CHECK_ARG(rows >= 0 && M > 0 && sums, "nbx_bn_train_backward_apply: need rows >= 0, M > 0 and sums");
+    if (rows == 0) return NBX_OK;
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(rows * M)), dim3(256), 0, (hipStream_t)stream, rows, M, S, V, save,
                        weight, sums, dOS, dOV, dS, dV, sums + 3 * M);
     NBX_LAUNCH_CHECK("bn_bwd_apply(sync)");
@@ -1069,13 +1031,7 @@ extern "C" int nbx_segment_sum(int64_t n, int32_t cols, const int32_t* ptr, cons
                                int32_t planes, int32_t accumulate, void* stream) {
     NBX_CHECK_ARG(n >= 0 && cols >= 0 && planes >= 1 && ld_in >= cols && ld_out >= cols, "nbx_segment_sum: bad sizes");
     if (n == 0 || cols == 0) return NBX_OK;
-    // NBX_SEGSUM_SERIAL=1: the thread-per-(segment, column) sequential kernel (A/B)
-    static const bool serial = getenv("NBX_SEGSUM_SERIAL") && atoi(getenv("NBX_SEGSUM_SERIAL")) != 0;
-    if (serial)
-        hipLaunchKernelGGL(segment_sum_kernel, dim3(nblk(n * cols)), dim3(256), 0, (hipStream_t)stream, n, cols, ptr, eid,
-                           in, ld_in, plane_in, out, ld_out, plane_out, planes, accumulate);
-    else
-        hipLaunchKernelGGL(segment_sum4_kernel, dim3((unsigned)(n * ((cols + 63) / 64))), dim3(256), 0,
+    hipLaunchKernelGGL(segment_sum4_kernel, dim3((unsigned)(n * ((cols + 63) / 64))), dim3(256), 0,
                            (hipStream_t)stream, n, cols, ptr, eid, in, ld_in, plane_in, out, ld_out, plane_out, planes,
                            accumulate);
     NBX_LAUNCH_CHECK("segment_sum");

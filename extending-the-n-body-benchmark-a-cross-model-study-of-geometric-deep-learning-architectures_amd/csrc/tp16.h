@@ -211,23 +211,6 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
             // their latency hides under the MFMAs (not after the last chunk)
             float rres[EPI == TP_RESID ? CG : 1][4][4];
             float rna[4][3];
-            float rvr[EPI == TP_GATE_VRAW ? CG : 1][4][3];   // GATE_VRAW: the rows' 1o pre-gate values
-            if constexpr (EPI == TP_GATE_VRAW) {
-                const int row0p = rt * 16 + 4 * qd;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int row = row0p + jj;
-                    const bool rok = rt < row_tiles && row < P.rows;
-#pragma unroll
-                    for (int g = 0; g < CG; ++g) {
-                        const int ch = (cgroup * CG + g) * 16 + c16;
-                        const bool ok = rok && ch < P.M;
-                        const size_t o = (size_t)row * P.lda_v + ch;
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) rvr[g][jj][k] = ok ? P.Av[(size_t)k * P.plane_stride + o] : 0.f;
-                    }
-                }
-            }
             if constexpr (EPI == TP_RESID) {
                 const int row0p = rt * 16 + 4 * qd;
 #pragma unroll
@@ -404,8 +387,8 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                     }
                 }
             };
-            if (SK::PREC == 1 && rt < row_tiles) {
-                if constexpr (SK::PREC == 1) {
+            if (SK::PREC >= 1 && rt < row_tiles) {
+                if constexpr (SK::PREC >= 1) {
                     // Split-precision path (tp_fused.h StatSKX3): v_mfma_f32_16x16x32_bf16, whose A
                     // fragment (lane quarter qd: k = 8 qd + j) is exactly the chunk a lane loads.
                     // Item u's B fragments are read from LDS while item u-1's MFMAs run, into a
@@ -413,9 +396,12 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                     // issued, so no load lands on the operands of an MFMA issued just before it
                     // (the measured gfx950 hazard is a load into the SrcA of the preceding
                     // v_mfma_f32_16x16x32_bf16 at 0 wait states; build.py checks the ISA for it).
+                    // (PREC 2: the fp16x2 path, 2 parts and 3 terms on v_mfma_f32_16x16x32_f16, same structure)
+                    using SP = SplitP<SK::PREC>;
+                    using SPT = typename SP::T;
+                    constexpr int NP = SP::NP;
                     constexpr int OB[4] = {0, SK::K0, SK::K0 + SK::K1, SK::K0 + SK::K1 + SK::K2};
-                    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
-                    auto read_b = [&](auto ic, bf16x8 (&bx)[CG][NS > 1 ? NS : 1][3]) {
+                    auto read_b = [&](auto ic, SPT (&bx)[CG][NS > 1 ? NS : 1][NP]) {
                         constexpr int item = decltype(ic)::value;
                         if constexpr (item < SK::K0) {
                             static_for<0, NS>([&](auto jc) {
@@ -425,21 +411,21 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
 #pragma unroll
                                     for (int g = 0; g < CG; ++g)
 #pragma unroll
-                                        for (int p3 = 0; p3 < 3; ++p3)
-                                            bx[g][j][p3] = reinterpret_cast<const bf16x8*>(lds + g * stride_g)
-                                                [(OB[j] + item) * 192 + p3 * 64 + lane];
+                                        for (int p3 = 0; p3 < NP; ++p3)
+                                            bx[g][j][p3] = reinterpret_cast<const SPT*>(lds + g * stride_g)
+                                                [(OB[j] + item) * (NP * 64) + p3 * 64 + lane];
                             });
                         } else {
                             constexpr int kc = (item - SK::K0) % SK::KV;
 #pragma unroll
                             for (int g = 0; g < CG; ++g)
 #pragma unroll
-                                for (int p3 = 0; p3 < 3; ++p3)
-                                    bx[g][0][p3] = reinterpret_cast<const bf16x8*>(lds + g * stride_g)
-                                        [(OB[NS] + kc) * 192 + p3 * 64 + lane];
+                                for (int p3 = 0; p3 < NP; ++p3)
+                                    bx[g][0][p3] = reinterpret_cast<const SPT*>(lds + g * stride_g)
+                                        [(OB[NS] + kc) * (NP * 64) + p3 * 64 + lane];
                         }
                     };
-                    auto keep = [&](const bf16x8& v) { asm volatile("" ::"v"(v)); };
+                    auto keep = [&](const SPT& v) { asm volatile("" ::"v"(v)); };
                     // B (SrcB) fragment sets: three (item u in set u % 3, each kept live until item u+1's
                     // MFMAs issued) or, with a deep A ring (PF > 3), two: the measured gfx950 hazard is on
                     // SrcA only (a load over an MFMA's SrcB at 0 wait states is safe, tools/hazard), and
@@ -448,8 +434,8 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                     slice_call([&](auto sc_) {
                         constexpr int lo = decltype(sc_)::value * SNIT / KS;
                         constexpr int n = (decltype(sc_)::value + 1) * SNIT / KS - lo;
-                        bf16x8 bx[NBS][CG][NS > 1 ? NS : 1][3];   // item u in set u % NBS
-                        bf16x8 ax[3][3];
+                        SPT bx[NBS][CG][NS > 1 ? NS : 1][NP];   // item u in set u % NBS
+                        SPT ax[3][NP];
                         read_b(std::integral_constant<int, lo>{}, bx[0]);
                         static_for<0, n>([&](auto uc) {
                             constexpr int u = decltype(uc)::value, item = lo + u;
@@ -459,36 +445,33 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                             if constexpr (u + 1 < n) read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % NBS]);
                             float av[8];
                             item_a(std::integral_constant<int, item>{}, ring[u % PF], av);
-                            tp_split3(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]},
-                                      ax[u % 3][0], ax[u % 3][1], ax[u % 3][2]);
-                            const bf16x8 (&b)[CG][NS > 1 ? NS : 1][3] = bx[u % NBS];
-                            const bf16x8 (&a)[3] = ax[u % 3];
+                            SP::split(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]}, ax[u % 3]);
+                            const SPT (&b)[CG][NS > 1 ? NS : 1][NP] = bx[u % NBS];
+                            const SPT (&a)[NP] = ax[u % 3];
                             if constexpr (item < SK::K0) {
                                 constexpr int NA = 1 + (NS > 1 && item < SK::K1 ? 1 : 0) + (NS > 2 && item < SK::K2 ? 1 : 0);
 #pragma unroll
-                                for (int tt = 0; tt < 6; ++tt)
+                                for (int tt = 0; tt < SP::NT; ++tt)
 #pragma unroll
                                     for (int g = 0; g < CG; ++g)
 #pragma unroll
                                         for (int j = 0; j < NA; ++j)
-                                            acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[TA[tt]], b[g][j][TB[tt]],
-                                                                                                acc[g][j], 0, 0, 0);
+                                            acc[g][j] = mfma16x16(a[SP::TA[tt]], b[g][j][SP::TB[tt]], acc[g][j]);
                             } else {
                                 constexpr int plane = (item - SK::K0) / SK::KV;
 #pragma unroll
-                                for (int tt = 0; tt < 6; ++tt) {
+                                for (int tt = 0; tt < SP::NT; ++tt) {
                                     if constexpr (CG == 1) {
                                         if (tt & 1)
-                                            accv2[plane] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                                a[TA[tt]], b[0][0][TB[tt]], accv2[plane], 0, 0, 0);
+                                            accv2[plane] = mfma16x16(a[SP::TA[tt]], b[0][0][SP::TB[tt]], accv2[plane]);
                                         else
-                                            acc[0][NS + plane] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                                a[TA[tt]], b[0][0][TB[tt]], acc[0][NS + plane], 0, 0, 0);
+                                            acc[0][NS + plane] =
+                                                mfma16x16(a[SP::TA[tt]], b[0][0][SP::TB[tt]], acc[0][NS + plane]);
                                     } else {
 #pragma unroll
                                         for (int g = 0; g < CG; ++g)
-                                            acc[g][NS + plane] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                                a[TA[tt]], b[g][0][TB[tt]], acc[g][NS + plane], 0, 0, 0);
+                                            acc[g][NS + plane] =
+                                                mfma16x16(a[SP::TA[tt]], b[g][0][SP::TB[tt]], acc[g][NS + plane]);
                                     }
                                 }
                             }
@@ -499,14 +482,14 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                                                                          (NS > 2 && pitem < SK::K2 ? 1 : 0)
                                                                    : 1;
 #pragma unroll
-                                for (int p3 = 0; p3 < 3; ++p3) keep(ax[pu][p3]);
+                                for (int p3 = 0; p3 < NP; ++p3) keep(ax[pu][p3]);
                                 if constexpr (NBS == 3) {
 #pragma unroll
                                     for (int g = 0; g < CG; ++g)
 #pragma unroll
                                         for (int j = 0; j < PNA; ++j)
 #pragma unroll
-                                            for (int p3 = 0; p3 < 3; ++p3) keep(bx[pu][g][j][p3]);
+                                            for (int p3 = 0; p3 < NP; ++p3) keep(bx[pu][g][j][p3]);
                                 }
                             }
                             __builtin_amdgcn_sched_barrier(0);
@@ -587,6 +570,12 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                 }
             }
 
+            if constexpr (SK::PREC == 2) {   // undo the fp16x2 image's weight scale
+#pragma unroll
+                for (int g = 0; g < CG; ++g)
+#pragma unroll
+                    for (int j = 0; j < NS + 3 * NV; ++j) acc[g][j] *= P.bscale;
+            }
             if (P.dbg) { const unsigned long long c = clock64(); c_loop += c - c_mark; c_mark = c; }
             // ------------------------------------------------------------ epilogue
             const int row0 = rt * 16 + 4 * qd;   // rows of registers 0..3: row0 + jj
@@ -675,26 +664,6 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         const float h0 = gg * (na[1] * tt + acc[g][NS + 0][jj]);
                         const float h1 = gg * (na[2] * tt + acc[g][NS + 1][jj]);
                         const float h2 = gg * (na[3] * tt + acc[g][NS + 2][jj]);
-                        P.out_s[(size_t)row * 2 * M + ch] = hs;
-                        P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
-                        P.out_v[(size_t)row * M + ch] = h0;
-                        P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
-                        P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
-                    }
-                } else if constexpr (EPI == TP_GATE_VRAW) {
-                    const bool live = ch < M;
-                    const float ba = live ? P.bias[ch] : 0.f, bg = live ? P.bias[M + ch] : 0.f;
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const int row = row0 + jj;
-                        if (!live || row >= P.rows) continue;
-                        const float* na = P.geom + (size_t)row * 4;
-                        const float hs = kC_SILU * tp_silu(acc[g][0][jj] + ba);
-                        const float gg = kC_SIGMOID * tp_sigmoid(acc[g][1][jj] + bg);
-                        const float tt = acc[g][2][jj];
-                        const float h0 = gg * (na[1] * tt + rvr[g][jj][0]);
-                        const float h1 = gg * (na[2] * tt + rvr[g][jj][1]);
-                        const float h2 = gg * (na[3] * tt + rvr[g][jj][2]);
                         P.out_s[(size_t)row * 2 * M + ch] = hs;
                         P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
                         P.out_v[(size_t)row * M + ch] = h0;
@@ -795,7 +764,7 @@ int tp16_geom(TpProb& p, int num_cus, int* blocks, int prec = 0) {
             set_error("tp16: scalar sub-tile K must be non-increasing");
             return NBX_E_INVAL;
         }
-    p.img_floats = tp_img_floats(p, 16) * (prec ? 3 : 2) / 2;
+    p.img_floats = tp_img_floats(p, 16) * (prec == 1 ? 3 : 2) / 2;   // bf16x3: 1.5x the fp32 floats; fp16x2: the same
     p.lds_floats = p.img_floats * CG + (p.seg_s[0] ? ((10 * p.M + 3) & ~3) : 0);
     if (KS > 1) p.lds_floats += (WAVES / KS) * (KS - 1) * CG * (NS + 3 * NV) * 4 * 64;
     const size_t lds = (size_t)p.lds_floats * 4;
@@ -833,7 +802,6 @@ int tp16_check_static(const TpProb& p) {
             set_error("tp16: segmented pre_pool input needs mul %% 32 == 0 and the segment pointers");
             return NBX_E_INVAL;
         }
-        // (KV = 0: the scalar items only, update_layer_1's split form -- upd_vec.h)
         if (SK::SEG == 4 && (p.M * 4 != SK::K0 * 32 || (SK::KV && p.M * 2 != SK::KV * 32) || !p.seg_s[0] ||
                              !p.seg_s[1] || !p.seg_s[2] || !p.seg_s[3] || (SK::KV && (!p.seg_v[0] || !p.seg_v[1])) ||
                              (!p.mcoef && !p.mbn.sums))) {
@@ -876,12 +844,7 @@ int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
     if (int rc = tp16_check_static<SK>(p0)) return rc;
     if (DUAL)
         if (int rc = tp16_check_static<SK>(p1)) return rc;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    NBX_LDS_160K((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>));
     const size_t lds = (size_t)std::max(b0 ? p0.lds_floats : 0, b1 ? p1.lds_floats : 0) * 4;
     NBX_TIMED_LAUNCH((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>), dim3(b0 + b1), dim3(64 * WAVES), lds,
                      st, p0, p1, b0);

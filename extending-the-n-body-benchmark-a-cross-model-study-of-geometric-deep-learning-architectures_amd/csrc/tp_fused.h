@@ -28,10 +28,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// TP_GATE_VRAW (tp16, NV = 0): the gated node epilogue of TP_GATE_NODE with the 1o pre-gate values
-// read from Av ([3][rows][lda_v], planes plane_stride apart: upd_vec_kernel's v_raw) instead of the
-// kernel's own vector accumulators (upd_vec.h)
-enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3, TP_GATE_VRAW = 4 };
+enum TpEpi : int { TP_PLAIN = 0, TP_MSG = 1, TP_GATE_NODE = 2, TP_RESID = 3 };
 
 // BatchNorm statistics accumulated by the producing kernel with device-scope fp64 atomics
 // ([3][M]: sum s and sum s^2 over the 0e channels, sum |v|^2 over the 1o channels) and
@@ -153,6 +150,8 @@ struct TpProb {
     // [V][4]); RESID: out_dot[row][ch] = sum_k x_v,k na_k[row] of the new x
     const float* na;
     float* out_dot;
+    // fp16x2 images (StatSKH2): the factor that undoes the image's power-of-two weight scale
+    float bscale;
 };
 
 constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
@@ -213,6 +212,69 @@ __device__ inline void tp_split3(const float4& a, const float4& b, bf16x8& hi, b
     lo = __builtin_bit_cast(bf16x8, L);
 }
 
+// StatSK with the fp16x2 split path (include/nbx.h "fp16x2 images"): x = hi + lo, both fp16 (RNE,
+// v_cvt_pk_f16_f32), the residual unscaled; the weights are pre-scaled by a power of two per TP
+// (max |w s| in [2^9, 2^10), so their residuals stay normal fp16) and the accumulator is descaled
+// by TpProb::bscale = 1/s in the epilogue.  A product is the fp32 sum of hi.lo + lo.hi + hi.hi on
+// v_mfma_f32_{16x16x32,32x32x16}_f16: half the MFMAs, two thirds of the operand bytes and of the
+// split VALU of bf16x3.  Representation error <= ~2^-22 |a||b| per product (rms 7.6e-8 relative
+// on a K = 192..384 GEMM), below the fp32 accumulation error of the same GEMM.
+template <int A, int B, int C, int V, int S = 0>
+struct StatSKH2 {
+    static constexpr bool on = true;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 2;
+};
+
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 tp_h2 __attribute__((ext_vector_type(2)));
+
+// x = hi + lo (fp16 each, residual |x - hi - lo| <= 2^-22 |x| for |x| >= 2^-3; below that an
+// absolute 2^-25): v_cvt_pk_f16_f32, two v_cvt_f32_f16, two v_sub_f32, v_cvt_pk_f16_f32 per pair
+__device__ inline void tp_split_h2(const float4& a, const float4& b, h16x8& hi, h16x8& lo) {
+    const tp_f2 f[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+    tp_u4 H, L;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const tp_h2 h = __builtin_convertvector(f[i], tp_h2);
+        const tp_f2 r = tp_sub2(f[i], __builtin_convertvector(h, tp_f2));
+        H[i] = __builtin_bit_cast(unsigned, h);
+        L[i] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, tp_h2));
+    }
+    hi = __builtin_bit_cast(h16x8, H);
+    lo = __builtin_bit_cast(h16x8, L);
+}
+
+// Split-precision traits: PREC 1 = bf16x3 (3 parts, 6 terms), PREC 2 = fp16x2 (2 parts, 3 terms).
+// Term t multiplies A part TA[t] by B part TB[t]; terms run smallest first.
+template <int PREC> struct SplitP;
+template <> struct SplitP<1> {
+    using T = bf16x8;
+    static constexpr int NP = 3, NT = 6;
+    static constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+    __device__ static void split(const float4& a, const float4& b, T (&p)[3]) { tp_split3(a, b, p[0], p[1], p[2]); }
+};
+template <> struct SplitP<2> {
+    using T = h16x8;
+    static constexpr int NP = 2, NT = 3;
+    static constexpr int TA[3] = {0, 1, 0}, TB[3] = {1, 0, 0};
+    __device__ static void split(const float4& a, const float4& b, T (&p)[2]) { tp_split_h2(a, b, p[0], p[1]); }
+};
+// (PREC 0 never instantiates the split code; this keeps the templates well-formed)
+template <> struct SplitP<0> : SplitP<1> {};
+
+__device__ inline floatx4 mfma16x16(const bf16x8& a, const bf16x8& b, const floatx4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ inline floatx4 mfma16x16(const h16x8& a, const h16x8& b, const floatx4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ inline floatx16 mfma32x32(const bf16x8& a, const bf16x8& b, const floatx16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ inline floatx16 mfma32x32(const h16x8& a, const h16x8& b, const floatx16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (I < N) {
@@ -265,7 +327,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     int off[NS + 1];
     tp_img_offsets<NS>(P, 32, off);
     static_assert(SK::PREC == 0 || SK::on, "split-precision path needs a static schedule");
-    const bf16x8* ldsx = reinterpret_cast<const bf16x8*>(lds);   // PREC 1: 384 bf16x8 per 32-deep block
+    using SP = SplitP<SK::PREC>;
+    using SPT = typename SP::T;
+    constexpr int XBLK = SP::NP * 128;   // split parts x (m 2) x 64 lanes per 32-deep block (PREC 1: 384)
+    const SPT* ldsx = reinterpret_cast<const SPT*>(lds);
 
     const int ks_chunks = (P.K[0] + 31) >> 5;            // K_S = K[0] (sub-tile 0 uses all of it)
     const int kv_chunks = NV ? (P.Kv + 31) >> 5 : 0;
@@ -405,27 +470,28 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     }
                 }
             };
-            // PREC 1: item u's A chunk, split into [part][m] bf16x8 (lane (r, h) holds k = 16 h + 4 q + e
+            // PREC 1 / 2: item u's A chunk, split into [part][m] (lane (r, h) holds k = 16 h + 4 q + e
             // of the chunk; MFMA m takes k = 16 h + 8 m + j)
-            auto split_item = [&](const float4 (&cur)[4], bf16x8 (&a)[3][2]) {
-                tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
-                tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+            auto split_item = [&](const float4 (&cur)[4], SPT (&a)[SP::NP][2]) {
+                SPT p0[SP::NP], p1[SP::NP];
+                SP::split(cur[0], cur[1], p0);
+                SP::split(cur[2], cur[3], p1);
+#pragma unroll
+                for (int p = 0; p < SP::NP; ++p) { a[p][0] = p0[p]; a[p][1] = p1[p]; }
             };
-            auto mma_item_x3 = [&](auto ic, const bf16x8 (&a)[3][2]) {
+            auto mma_item_x3 = [&](auto ic, const SPT (&a)[SP::NP][2]) {
                 constexpr int item = decltype(ic)::value;
                 {
                     // block [p][m][lane][j]: smallest terms first
                     auto mma6 = [&](floatx16& c, int blk) {
-                        const bf16x8* bp = ldsx + blk * 384 + lane;
+                        const SPT* bp = ldsx + blk * XBLK + lane;
 #pragma unroll
                         for (int m = 0; m < 2; ++m) {
-                            const bf16x8 b0 = bp[m * 64], b1 = bp[(2 + m) * 64], b2 = bp[(4 + m) * 64];
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b0, c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b1, c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b2, c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b0, c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b1, c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b0, c, 0, 0, 0);
+                            SPT b[SP::NP];
+#pragma unroll
+                            for (int p = 0; p < SP::NP; ++p) b[p] = bp[(2 * p + m) * 64];
+#pragma unroll
+                            for (int tt = 0; tt < SP::NT; ++tt) c = mfma32x32(a[SP::TA[tt]][m], b[SP::TB[tt]], c);
                         }
                     };
                     // first block of each sub-tile (compile-time image offsets)
@@ -473,9 +539,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     }
                 }
             };
-            if constexpr (SK::PREC == 1) {
+            if constexpr (SK::PREC >= 1) {
                 // the split of item u + 1 runs in the shadow of item u's MFMAs (no barrier between them)
-                bf16x8 ax[2][3][2];
+                SPT ax[2][SP::NP][2];
                 split_item(buf[0], ax[0]);
                 static_for<0, SNIT>([&](auto uc) {
                     constexpr int u = decltype(uc)::value;
@@ -495,12 +561,13 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                         split_item(buf[(u + 1) % D], ax[(u + 1) % 2]);
                         // ... and its results above the next barrier (else they sink into the next block)
 #pragma unroll
-                        for (int p3 = 0; p3 < 3; ++p3)
+                        for (int p3 = 0; p3 < SP::NP; ++p3)
 #pragma unroll
                             for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(ax[(u + 1) % 2][p3][m]));
                         // spread the split's VALU over the MFMA gaps (<= ~5 per gap hide, MI355X_MICROARCH)
-                        constexpr int nm = u < SK::K0 ? 12 * ((u < SK::K2) + (u < SK::K1) + 1) : 12;
-                        constexpr int per = (120 + nm - 1) / nm;
+                        constexpr int nsub = u < SK::K0 ? (u < SK::K2) + (u < SK::K1) + 1 : 1;
+                        constexpr int nm = 2 * SP::NT * nsub;
+                        constexpr int per = ((SK::PREC == 1 ? 120 : 64) + nm - 1) / nm;
                         static_for<0, nm>([&](auto) {
                             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                             __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
@@ -541,6 +608,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                 }
             }
 
+            if constexpr (SK::PREC == 2) {   // undo the fp16x2 image's weight scale
+#pragma unroll
+                for (int j = 0; j < NS + 3 * NV; ++j) acc[j] *= P.bscale;
+            }
             if (P.dbg) c_loop = clock64();
             // ------------------------------------------------------------ epilogue
             const int ch = chunk * 32 + r;          // output channel of this lane's column
@@ -743,7 +814,7 @@ inline int tp_lds_floats(const TpProb& p) { return tp_img_floats(p, 32); }
 // (as many blocks per CU as the LDS footprint allows) without idle waves.
 // prec 1: bf16x3 image, 1.5x the floats of the fp32 one.
 inline void tp_geometry(TpProb& p, int waves = TP_WAVES, int num_cus = 256, int prec = 0) {
-    p.img_floats = tp_img_floats(p, 32) * (prec ? 3 : 2) / 2;
+    p.img_floats = tp_img_floats(p, 32) * (prec == 1 ? 3 : 2) / 2;   // bf16x3: 1.5x the fp32 floats; fp16x2: the same
     p.lds_floats = p.img_floats;
     const int lds_bytes = p.lds_floats * 4;
     int per_cu = (160 * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
@@ -771,12 +842,7 @@ int tp_launch(const TpProb& p, hipStream_t st) {
         set_error("tp_fused: weight chunk needs %zu bytes of LDS (> 160 KiB)", lds);
         return NBX_E_UNSUPPORTED;
     }
-    static bool attr_set = false;  // per instantiation
-    if (!attr_set) {
-        NBX_HIP(hipFuncSetAttribute((const void*)tp_fused_kernel<NS, NV, EPI, WAVES, D, SK>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    NBX_LDS_160K((tp_fused_kernel<NS, NV, EPI, WAVES, D, SK>));
     if constexpr (SK::on) {
         auto kc = [](int K) { return (K + 31) / 32; };
         if (!(kc(p.K[0]) == SK::K0 && (NS < 2 || kc(p.K[1]) == SK::K1) && (NS < 3 || kc(p.K[2]) == SK::K2) &&

@@ -28,7 +28,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .segnn_train import Graph, colsum, gemm, gemm_batched, _BIAS_COLSUM, _dp, _st, _ws
+from .segnn_train import Graph, colsum, gemm, gemm_batched, _dp, _st, _ws
 
 _f32 = torch.float32
 
@@ -67,9 +67,6 @@ class _LinFn(torch.autograd.Function):
                        "nbx_bias_act_backward")
         db = dW = dX = None
         want_b = b is not None and ctx.needs_input_grad[2]
-        if want_b and _BIAS_COLSUM:
-            db = colsum(dZ, rows, N, N, torch.empty(N, device=dev, dtype=_f32))
-            want_b = False
         # the weight and the input gradient GEMMs in one launch (nbx_gemm_f32_batched); the bias gradient
         # (column sums of dZ) is the last column of the weight gradient against X extended by ones
         probs = []

@@ -327,15 +327,20 @@ class SEGNN(nn.Module):
         tps = [m for m in self.modules() if isinstance(m, O3TensorProduct)]
         sizes = [m.tp.weight.numel() for m in tps]
         total = sum(sizes)
-        ids, ones, off = {}, {}, 0
+        ids, ones, perm_ids, off = {}, {}, {}, 0
+        # a third trace with the element ids permuted at random: an operand element c w_a + c w_b with
+        # equal constants would pass the id / ones traces as w_{(a+b)/2}, but not this one
+        perm = torch.randperm(total, generator=torch.Generator().manual_seed(1234)).to(torch.float64) + 1
         for m, n in zip(tps, sizes):
             ids[id(m)] = torch.arange(off + 1, off + n + 1, dtype=torch.float64)   # 1-based: 0 = no source
             ones[id(m)] = torch.ones(n, dtype=torch.float64)
+            perm_ids[id(m)] = perm[off:off + n]
             off += n
         cpu = torch.device("cpu")
         with torch.no_grad():
             Pi = self.train_matrices(cpu, ids, torch.float64)
             Po = self.train_matrices(cpu, ones, torch.float64)
+            Pp = self.train_matrices(cpu, perm_ids, torch.float64)
         keys = [k for k in Pi if not k.endswith("_bias")]
         src, scale, slots = [], [], {}
         pos = 0
@@ -346,6 +351,10 @@ class SEGNN(nn.Module):
             if not torch.equal(idx * vo, torch.where(live, vi, torch.zeros_like(vi))) and \
                     not torch.allclose(idx * vo, vi, rtol=1e-12, atol=0):
                 raise RuntimeError(f"SEGNN training operand {k} is not a scaled copy of the weights")
+            vp = Pp[k].reshape(-1)
+            want = torch.where(live, perm[(idx - 1).clamp(min=0).long()] * vo, torch.zeros_like(vo))
+            if not torch.allclose(vp, want, rtol=1e-12, atol=0):
+                raise RuntimeError(f"SEGNN training operand {k} mixes several weights")
             src.append(torch.where(live, idx - 1, torch.full_like(idx, total)).long())
             scale.append(torch.where(live, vo, torch.zeros_like(vo)))
             slots[k] = (pos, tuple(Pi[k].shape))
@@ -436,6 +445,40 @@ class SEGNN(nn.Module):
         return img.view(torch.int16)
 
     @staticmethod
+    def h2_scale(*mats) -> float:
+        """The power of two s with max |W s| in [2^9, 2^10) over the given matrices (1 if all zero):
+        the fp16x2 images' weight scale (include/nbx.h "fp16x2 images")."""
+        m = max(float(W.abs().max()) if W.numel() else 0.0 for W in mats)
+        if m == 0.0 or not math.isfinite(m):
+            return 1.0
+        return 2.0 ** (9 - math.floor(math.log2(m)))
+
+    @staticmethod
+    def frag_image_h2(subs, vec, chunks: int, cw: int, scale: float) -> torch.Tensor:
+        """fp16x2 image (include/nbx.h "fp16x2 images"): W s = hi + lo, hi = fp16(W s) (RNE),
+        lo = fp16(W s - hi); per sub-tile and 32-deep K chunk kc the bf16x3 block layout of
+        frag_image_x3 with two fp16 parts:
+          cw = 32: block [part p 2][m 2][lane 64][j 8],  cw = 16: block [part p 2][lane 64][j 8].
+        Returned as int16 bit patterns [chunks][F16]."""
+        blocks = []
+        for W, K in list(subs) + ([vec] if vec is not None else []):
+            kc = (K + 31) // 32
+            X = torch.zeros(chunks * cw, kc * 32, dtype=torch.float64, device=W.device)
+            n = min(W.shape[0], chunks * cw)
+            X[:n, :K] = W[:n, :K].double() * scale
+            X = X.float()                                   # exact: scale is a power of two
+            hi = X.half()
+            lo = (X - hi.float()).half()                    # the residual is exact in fp32
+            parts = torch.stack([hi.float(), lo.float()])   # [2][rows][kc*32]
+            if cw == 32:
+                Y = parts.reshape(2, chunks, 32, kc, 2, 2, 8).permute(1, 3, 0, 5, 4, 2, 6)
+            else:
+                Y = parts.reshape(2, chunks, 16, kc, 4, 8).permute(1, 3, 0, 4, 2, 5)
+            blocks.append(Y.reshape(chunks, -1))
+        img = torch.cat(blocks, 1).contiguous().half()
+        return img.view(torch.int16)
+
+    @staticmethod
     def tp_images(P: dict, mul: int) -> dict:
         """packed_matrices -> the device images the kernels stage (msg2: 32-channel
         chunks for the 32x32 message kernel; every other TP: 16-channel chunks, the
@@ -455,6 +498,10 @@ class SEGNN(nn.Module):
                 subs = [(B[j * M:(j + 1) * M], M) for j in range(6)]
                 out[pre + base[:-2] + "_img"] = img(subs, None, 16, c16)
                 out[pre + base[:-2] + "_img_x3"] = SEGNN.frag_image_x3(subs, None, c16, 16)
+                # one scale for both node_pre images (one kernel, one descale)
+                sc = SEGNN.h2_scale(P[pre + "node_pre_s_t"], P[pre + "node_pre_v_t"])
+                out[pre + base[:-2] + "_img_h2"] = SEGNN.frag_image_h2(subs, None, c16, 16, sc)
+                out[pre + "node_pre_h2_descale"] = 1.0 / sc
             elif base in ("msg2_s_t", "upd1_s_t", "upd2_s_t", "pp1_s_t"):
                 stem = base[:-4]
                 S, V = P[key], P[pre + stem + "_v_t"]
@@ -463,11 +510,15 @@ class SEGNN(nn.Module):
                 # the last part (t, 0e -> 1o path) only contracts the first half of K
                 Ks = [K] * (parts - 1) + [K // 2]
                 subs = [(S[j * M:(j + 1) * M], Ks[j]) for j in range(parts)]
+                sc = SEGNN.h2_scale(S, V)
+                out[pre + stem + "_h2_descale"] = 1.0 / sc
                 if stem == "msg2":
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 32, c32)
                     out[pre + stem + "_img_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c32)
+                    out[pre + stem + "_img_h2"] = SEGNN.frag_image_h2(subs, (V, V.shape[1]), c32, 32, sc)
                 else:
                     out[pre + stem + "_img"] = img(subs, (V, V.shape[1]), 16, c16)
+                    out[pre + stem + "_img_h2"] = SEGNN.frag_image_h2(subs, (V, V.shape[1]), c16, 16, sc)
                     if stem == "upd1":
                         out[pre + stem + "_img_x3"] = SEGNN.frag_image_x3(subs, (V, V.shape[1]), c16, 16)
             elif base.endswith("_v_t"):
@@ -493,15 +544,16 @@ class SEGNN(nn.Module):
         P = self.tp_images(self.packed_matrices(device), self.mul)
         W = _lib.SegnnWeights()
         W.mul, W.num_layers, W.bn_eps, W.bn_momentum = self.mul, self.num_layers, 1e-5, 0.1
-        for k in ("emb", "emb_bias", "pp1_img", "pp1_bias", "pp2"):
+        for k in ("emb", "emb_bias", "pp1_img", "pp1_bias", "pp2", "pp1_img_h2"):
             setattr(W, k, P[k].data_ptr())
+        W.pp1_h2_descale = P["pp1_h2_descale"]
         shadows = []
         for li, layer in enumerate(self.layers):
             L = W.layers[li]
             for name, _ in L._fields_:
                 key = f"layers.{li}.{name}"
                 if key in P:
-                    setattr(L, name, P[key].data_ptr())
+                    setattr(L, name, P[key] if isinstance(P[key], float) else P[key].data_ptr())
             for name, bn in (("msg", layer.message_norm), ("feat", layer.feature_norm)):
                 for stat in ("running_mean", "running_var"):
                     buf = getattr(bn, stat)

@@ -24,7 +24,6 @@ Arithmetic is fp32 (a float64 module is cast for the step, like its fp32 inferen
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -50,10 +49,6 @@ def _st(t):
 def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
-
-# NBX_BIAS_COLSUM=1: bias gradients by nbx_colsum (two launches each) instead of the ones column of the
-# weight-gradient GEMM (A/B only)
-_BIAS_COLSUM = os.environ.get("NBX_BIAS_COLSUM", "0") == "1"
 
 # bench.py's roofline: when a list, every GEMM appends (start event, stop event, flops) recorded on
 # the launch stream around its launches
@@ -157,9 +152,6 @@ class _TPFn(torch.autograd.Function):
                                           _dp(dOV), _dp(dZs), _dp(dZv), _st(dZs)), "nbx_tp_post_backward")
         dbias = None
         want_b = bias is not None and ctx.needs_input_grad[5]
-        if want_b and _BIAS_COLSUM:
-            dbias = colsum(dZs, rows, nsc, nsc + Nt, torch.empty(nsc, device=dev, dtype=_f32))
-            want_b = False
         # the (up to) four backward GEMMs -- weight gradients and input gradients -- in one launch; the
         # bias gradient (column sums of dZs[:, :NSc]) is the last column of the weight-gradient GEMM
         # against S_in extended by a column of ones (NBX_GEMM_B_ONES)

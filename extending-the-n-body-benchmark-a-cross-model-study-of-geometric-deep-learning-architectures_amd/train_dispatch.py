@@ -29,7 +29,9 @@ class NativePathWarning(UserWarning):
 
 def use_training_path(module) -> bool:
     mode = getattr(module, "native_train", "auto")
-    if mode not in MODES:
+    # by identity: 1 / 0 compare equal to True / False but are not accepted (they would fall through
+    # the `is` tests below to "auto")
+    if not any(mode is m for m in (True, False)) and not (isinstance(mode, str) and mode == "auto"):
         raise ValueError(f"native_train must be one of {MODES}, got {mode!r}")
     if mode is False or not torch.is_grad_enabled():
         return False

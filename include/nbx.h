@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 14
+#define NBX_ABI_VERSION 15
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -126,6 +126,16 @@ int nbx_ks_2samp_stat(const double* a, int64_t na, int64_t lda, const double* b,
  *            W[c = 32 chunk + (lane & 31)][k = 32 kc + 16 (lane >> 5) + 8 m + j];
  *   CW = 16: [part p 3][lane 64][j 8] bf16 = part p of
  *            W[c = 16 chunk + (lane & 15)][k = 32 kc + 8 (lane >> 4) + j].
+ *
+ * fp16x2 images (*_img_h2, ABI 15, NULL = no fp16x2 path): the weights of one TP are scaled by a
+ * power of two s (max |W s| in [2^9, 2^10)) and written as W s = hi + lo, hi = fp16(W s) (RNE),
+ * lo = fp16(W s - hi); activations are split the same way as they are loaded (unscaled).  A product
+ * accumulates in fp32 the three terms hi.lo + lo.hi + hi.hi on v_mfma_f32_32x32x16_f16 /
+ * 16x16x32_f16 and the kernel multiplies the accumulator by *_h2_descale = 1/s.  Per product the
+ * representation error is <= ~2^-22 |a||b|, below the fp32 accumulation error of the K >= 96
+ * contractions it feeds.  Layout: the bf16x3 layout above with two parts (hi, lo) of fp16:
+ *   CW = 32: [part p 2][m 2][lane 64][j 8];  CW = 16: [part p 2][lane 64][j 8]  (fp16),
+ * i.e. the same bytes per block as the fp32 image.
  */
 #define NBX_SEGNN_MAX_LAYERS 64
 
@@ -159,6 +169,17 @@ typedef struct nbx_segnn_layer {
     const float* feat_bn_bias;
     float* feat_bn_running_mean;
     float* feat_bn_running_var;
+    /* ABI 15: fp16x2 images ("fp16x2 images") of node_pre (both images share one scale, CW = 16),
+     * msg2 (CW = 32), upd1 and upd2 (CW = 16), and the factors that undo their weight scales */
+    const void* node_pre_s_img_h2;
+    const void* node_pre_v_img_h2;
+    const void* msg2_img_h2;
+    const void* upd1_img_h2;
+    const void* upd2_img_h2;
+    float node_pre_h2_descale;
+    float msg2_h2_descale;
+    float upd1_h2_descale;
+    float upd2_h2_descale;
 } nbx_segnn_layer;
 
 typedef struct nbx_segnn_weights {
@@ -192,6 +213,10 @@ typedef struct nbx_segnn_weights {
     void* bn_comm;
     int32_t deterministic;
     int32_t reserved0;
+    /* ABI 15: pre_pool1's fp16x2 image (CW = 16) and descale, or NULL */
+    const void* pp1_img_h2;
+    float pp1_h2_descale;
+    int32_t reserved1;
     nbx_segnn_layer layers[NBX_SEGNN_MAX_LAYERS];
 } nbx_segnn_weights;
 

@@ -65,13 +65,16 @@ def test_struct_layout_matches_header():
     import nbody_amd._lib as lib
     lf, layer_ptrs = _struct_fields("nbx_segnn_layer")
     assert [f for f, _ in lib.SegnnLayer._fields_] == lf
-    assert ctypes.sizeof(lib.SegnnLayer) == layer_ptrs * 8
+    layer_bytes = layer_ptrs * 8 + 4 * 4   # + the four fp16x2 descale factors (ABI 15)
+    assert ctypes.sizeof(lib.SegnnLayer) == layer_bytes
     wf, w_ptrs = _struct_fields("nbx_segnn_weights")
     assert [f for f, _ in lib.SegnnWeights._fields_] == wf
     head = 3 * 4 + 2 * 4   # mul, num_layers, training, bn_eps, bn_momentum
     head = (head + 7) // 8 * 8
-    extra = 8 + 8 + 8      # bn_allreduce (function pointer), bn_global_batch (int64), deterministic + reserved0
-    assert ctypes.sizeof(lib.SegnnWeights) == head + w_ptrs * 8 + extra + lib.MAX_LAYERS * layer_ptrs * 8
+    # bn_allreduce (function pointer), bn_global_batch (int64), deterministic + reserved0,
+    # pp1_h2_descale + reserved1
+    extra = 8 + 8 + 8 + 8
+    assert ctypes.sizeof(lib.SegnnWeights) == head + w_ptrs * 8 + extra + lib.MAX_LAYERS * layer_bytes
 
 
 def test_struct_offsets_match_the_c_compiler(tmp_path):

@@ -342,9 +342,9 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
       * over the predictable horizon (every step where the fp32 oracle itself stays within MSE 1e-7
         of the fp64 one; 5 steps here): MSE(device, oracle) <= 1e-5 (north_star) and <= 10x the
         fp32-oracle MSE;
-      * beyond it the trajectories of equally valid fp32 computations separate (chaos), so those
-        steps are printed, not asserted; test_rollout_c2_long_horizon_matches_oracle checks a
-        predictable 120-step horizon of the same model and workload.
+      * beyond it the trajectories of equally valid fp32 computations separate (chaos): there
+        MSE <= max(1e-5, 10x the fp32-oracle MSE); test_rollout_c2_long_horizon_matches_oracle checks
+        a predictable 120-step horizon of the same model and workload.
     Per-step errors are printed (measured: the device is 10-70x closer to fp64 than the fp32
     oracle over steps 1-5)."""
     import nbody_amd.segnn as S2
@@ -373,10 +373,11 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
             horizon = k
             assert mse <= 1e-5, (k, mse)
             assert mse <= 10.0 * f32 + 1e-13, (k, mse, f32)
-    # beyond the horizon the rollout is chaotic: equally valid fp32 computations separate (measured:
-    # the combined and the split update_layer_1 -- forwards equal to 1.5e-6 relative and equally
-    # close to fp64, rms 8e-7 -- reach MSE 2e-6 and 2e-4 at step 6), so those steps are only
-    # reported; the long-horizon check is test_rollout_c2_long_horizon_matches_oracle
+        else:
+            # beyond the horizon the rollout is chaotic and equally valid fp32 computations separate;
+            # the device must still stay within the north_star bound or 10x the fp32 oracle's own
+            # divergence (the long-horizon check is test_rollout_c2_long_horizon_matches_oracle)
+            assert mse <= max(1e-5, 10.0 * f32), (k, mse, f32)
     assert horizon >= 4, horizon
     assert np.isfinite(tp).all() and np.isfinite(tv).all()
     print(f"C2 predictable horizon (fp32 oracle within MSE 1e-7 of fp64): {horizon} steps")

@@ -2,6 +2,8 @@
 elements the HIP kernels read: the kernels' LDS addressing (tp16.h / tp_fused.h
 B-fragment reads) is restated here in numpy and checked against the packed
 matrices.  CPU only."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -120,3 +122,57 @@ def test_frag_image_x3_cw16_addressing():
                 k = 32 * kc + 8 * (lane // 16)[:, None] + np.arange(8)[None, :]
                 want = np.where(ch[:, None] < rows, W[np.minimum(ch, rows - 1)[:, None], k], 0.0)
                 np.testing.assert_allclose(blk.astype(np.float64).sum(0), want, rtol=2.0 ** -26, atol=0)
+
+
+@pytest.mark.parametrize("cw", [32, 16])
+def test_frag_image_h2_addressing_and_split(cw):
+    """fp16x2 image (include/nbx.h "fp16x2 images"; tp_fused.h / tp16.h StatSKH2, msg_pre PREC 2):
+    the bf16x3 addressing with two fp16 parts of W s, s = SEGNN.h2_scale; hi + lo reconstructs W s to
+    2^-22 relative (max |W s| in [2^9, 2^10)), and hi is W s rounded to fp16 (RNE)."""
+    g = torch.Generator().manual_seed(3)
+    rows, Ks = 40, (64, 40)
+    subs = [(torch.randn(rows, max(Ks), generator=g) * 10.0 ** torch.randint(-3, 1, (rows, 1), generator=g), K)
+            for K in Ks]
+    vec = (torch.randn(rows, 32, generator=g), 32)
+    s = SEGNN.h2_scale(*[W[:, :K] for W, K in subs], vec[0])
+    mx = max(float(W[:, :K].abs().max()) for W, K in subs + [vec])
+    assert 2.0 ** 9 <= mx * s < 2.0 ** 10 and math.log2(s) == int(math.log2(s))
+    chunks = -(-rows // cw)
+    img = SEGNN.frag_image_h2(subs, vec, chunks, cw, s).view(torch.float16).float().numpy()
+    kcs = [-(-K // 32) for K in Ks] + [1]
+    blk_n = 2 * 32 * cw
+    assert img.shape == (chunks, sum(kcs) * blk_n)
+    offs = np.concatenate([[0], np.cumsum(kcs)[:-1]]) * blk_n
+    mats = [(W.double().numpy() * s, K) for W, K in subs] + [(vec[0].double().numpy() * s, vec[1])]
+    lane = np.arange(64)
+    for (W, K), off, kc_n in zip(mats, offs, kcs):
+        for c in range(chunks):
+            for kc in range(kc_n):
+                blk = img[c, off + kc * blk_n:off + (kc + 1) * blk_n]
+                ms = [blk.reshape(2, 2, 64, 8)[:, m] for m in range(2)] if cw == 32 else [blk.reshape(2, 64, 8)]
+                for m, b in enumerate(ms):
+                    ch = c * cw + lane % cw
+                    k = (32 * kc + 16 * (lane // 32)[:, None] + 8 * m if cw == 32
+                         else 32 * kc + 8 * (lane // 16)[:, None]) + np.arange(8)[None, :]
+                    want = np.zeros((64, 8))
+                    ok = (ch[:, None] < W.shape[0]) & (k < K)
+                    want[ok] = W[np.broadcast_to(ch[:, None], k.shape)[ok], k[ok]]
+                    np.testing.assert_allclose(b.astype(np.float64).sum(0), want, rtol=2.0 ** -21,
+                                               atol=2.0 ** -24)
+                    np.testing.assert_array_equal(b[0], want.astype(np.float32).astype(np.float16).astype(np.float32))
+
+
+def test_tp_images_h2_entries():
+    """tp_images emits an fp16x2 image + descale for every TP the fp16x2 kernels run (node_pre pair,
+    msg2 CW 32, upd1 / upd2 / pp1 CW 16), each image the same bytes as the fp32 one."""
+    M = 96
+    m = SEGNN(hidden_features=2 * M, num_layers=2)
+    P = SEGNN.tp_images(m.packed_matrices(), M)
+    for k in ("layers.0.node_pre_s_img", "layers.0.node_pre_v_img", "layers.1.msg2_img", "layers.0.upd1_img",
+              "layers.1.upd2_img", "pp1_img"):
+        h2 = P[k + "_h2"]
+        assert h2.dtype == torch.int16 and h2.numel() * 2 == P[k].numel() * 4
+    for k in ("layers.0.node_pre_h2_descale", "layers.1.msg2_h2_descale", "layers.0.upd1_h2_descale",
+              "layers.1.upd2_h2_descale", "pp1_h2_descale"):
+        d = P[k]
+        assert isinstance(d, float) and d > 0 and math.log2(d) == int(math.log2(d))

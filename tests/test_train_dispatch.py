@@ -52,3 +52,13 @@ def test_explicit_override():
     with pytest.raises(ValueError):
         use_training_path(m)
     assert "native_train" not in m.state_dict()
+
+
+@pytest.mark.parametrize("bad", [1, 0, "Auto", None, 1.0])
+def test_native_train_rejects_lookalikes(bad):
+    """native_train is validated by identity: 1 / 0 equal True / False but would silently behave as
+    "auto" in the dispatch, so they are rejected like any other value."""
+    m = torch.nn.Linear(2, 2)
+    m.native_train = bad
+    with pytest.raises(ValueError):
+        use_training_path(m)
