@@ -58,6 +58,7 @@ def segnn_split_prec():
     return 1 if os.environ.get("NBX_SPLIT", "")[:1] in ("x", "1") else 2
 FP64_VALU_PEAK_TFLOPS = 78.6           # MI355X spec; no f64 MFMA used by the integrator
 SURVEY_GFLOP_PER_STEP = 67.73          # algorithmic work of the reference formulation
+COMPULSORY_BYTES_C2 = 8.0e6            # weights 7.79 MB + state I/O ~0.25 MB per C2 step
 
 
 def initial_states(B, N, seed0):
@@ -175,7 +176,7 @@ def bench_segnn(a, rank, world, device, P):
     def work():
         tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
         final = torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous()
-        P.all_gather_shards(final)
+        a.final_states = P.all_gather_shards(final)
         return tp
     tp, elapsed = timed_region(work, device, P)
     finite = bool(torch.isfinite(tp).all().item())
@@ -243,10 +244,28 @@ def bench_segnn(a, rank, world, device, P):
     achieved_tflops = dom_flops / dom_avg_s / 1e12
     traffic = pmc_traffic(names[dom], "segnn")
     value = a.steps / elapsed * world
+    ms_step = 1e3 * elapsed / a.steps
+    # the rocprof duration of the dominant kernel (the same run family as the PMC bytes) and the
+    # per-step HBM bytes of the whole step (report the MFMA and the HBM fractions)
+    rp_us, rp_src = rocprof_avg_us(names[dom], "segnn")
+    pp1 = (f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::{'StatSKH2' if prec == 2 else 'StatSK'}"
+           "<6, 6, 3, 3, 2> >(nbx::TpProb, nbx::TpProb, int)")
+    step_k = [(nm, LAYERS) for nm in names] + [(pp1, 1), ("(anonymous namespace)::rollout_pp2_kernel(", 1)]
+    bps, bps_src = step_bytes("segnn", step_k)
+    hbm = {"avg_launch_us_rocprof": rp_us, "rocprof_source": rp_src,
+           "frac_rocprof": round(dom_flops / (rp_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4) if rp_us else None,
+           "hbm_achieved_gbs": round(traffic / (rp_us * 1e-6) / 1e9, 1) if (rp_us and traffic) else None,
+           "hbm_frac": round(traffic / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if (rp_us and traffic) else None,
+           "bytes_per_step": bps, "bytes_per_step_source": bps_src,
+           "compulsory_bytes_per_step": COMPULSORY_BYTES_C2,
+           "bytes_over_compulsory": round(bps / COMPULSORY_BYTES_C2, 1) if bps else None,
+           "step_hbm_gbs": round(bps / (ms_step * 1e-3) / 1e9, 1) if bps else None,
+           "step_hbm_frac": round(bps / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if bps else None,
+           "compulsory_hbm_frac": round(COMPULSORY_BYTES_C2 / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
     result = {
         "metric": "self-feed rollout steps/sec, SEGNN N=5 batch=1024",
         "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (GravitySim frame-0 initial states, seeded random-init weights)",
         "config": {"workload": "C2: SEGNN lmax_h=1 hidden=192 layers=6, N=5, batch=1024 per GPU, self-feed rollout",
@@ -267,7 +286,10 @@ def bench_segnn(a, rank, world, device, P):
                      "executed_16bit_tflops": round(achieved_tflops * SPLIT_TERMS[prec], 2) if x3 else None,
                      "executed_16bit_frac": (round(achieved_tflops * SPLIT_TERMS[prec] / BF16_MFMA_PEAK_TFLOPS, 4)
                                              if x3 else None),
-                     "timing": "hipExtLaunchKernel start/stop events (kernel execution interval)",
+                     "timing": "achieved / frac: hipExtLaunchKernel start/stop events (kernel execution "
+                               "interval, this run); *_rocprof, hbm_*: the committed rocprofv3 profile's average "
+                               "duration with its PMC bytes (2 x FETCH_SIZE + WRITE_SIZE)",
+                     **hbm,
                      "fused_tp_share_of_forward": round(sum(ms_k) / fwd_ms, 3), "per_kind": per_kind},
         "finite": finite, "rollout_timing": diag,
     }
@@ -277,6 +299,43 @@ def bench_segnn(a, rank, world, device, P):
         result["cpu_baseline"] = cpu_baseline_segnn_torch(loc, vel, mass, a.cpu_torch_steps)
         result["cpu_baseline"]["numpy_oracle"] = cpu_baseline_segnn(loc, vel, mass, a.cpu_steps)
     return result
+
+
+def newest_profile(fname):
+    """The newest committed profiles/r*/<fname> (the round's HEAD profile), else None."""
+    import glob
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", fname)), reverse=True)
+    return c[0] if c else None
+
+
+def rocprof_avg_us(kernel_name, model):
+    """Average duration (us) of `kernel_name` in the newest committed rocprofv3 --stats summary
+    (profiles/r*/<model>_kernel_stats.csv, written by scripts/profile_models.sh), else None."""
+    import csv
+    path = newest_profile(f"{model}_kernel_stats.csv")
+    if path is None:
+        return None, None
+    for r in csv.DictReader(open(path)):
+        if r["Name"] == kernel_name:
+            return float(r["AverageNs"]) / 1e3, os.path.relpath(path, ROOT)
+    return None, os.path.relpath(path, ROOT)
+
+
+def step_bytes(model, step_kernels):
+    """HBM bytes per step from the newest PMC summary: sum over the step's kernels (name or name
+    prefix -> launches per step) of their PMC bytes per launch; None if any is missing."""
+    path = newest_profile(f"pmc_{model}.json")
+    if path is None:
+        return None, None
+    with open(path) as f:
+        kern = json.load(f)["kernels"]
+    total = 0
+    for name, n in step_kernels:
+        hit = [v for k, v in kern.items() if k == name or k.startswith(name)]
+        if not hit or hit[0].get("hbm_bytes_per_launch") is None:
+            return None, os.path.relpath(path, ROOT)
+        total += n * hit[0]["hbm_bytes_per_launch"]
+    return total, os.path.relpath(path, ROOT)
 
 
 def pmc_traffic(kernel_name, model=None):
@@ -319,6 +378,9 @@ def bench_ponita(a, rank, world, device, P):
     start, B = P.shard_range(B_glob, rank, world)
     torch.manual_seed(0)
     model = PONITA_NBODY(hidden_dim=128, layers=6, num_ori=20, basis_dim=128, degree=3).to(device)
+    if world > 1:   # one calibration from the moments of the whole global batch (conv.py:134-140)
+        import torch.distributed as dist
+        model.calibration_group = dist.group.WORLD
     loc, vel, mass = initial_states(B, N, start)
     t = lambda x: torch.tensor(x, dtype=torch.float32, device=device)
     loc_d, vel_d, mass_d = t(loc), t(vel), t(mass)
@@ -326,7 +388,7 @@ def bench_ponita(a, rank, world, device, P):
 
     def work():
         tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
-        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous(), B_glob)
+        a.final_states = P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous(), B_glob)
         return tp
     tp, elapsed = timed_region(work, device, P)
     finite = bool(torch.isfinite(tp).all().item())
@@ -419,7 +481,7 @@ def bench_egnn(a, rank, world, device, P):
 
     def work():
         tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1)
-        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
+        a.final_states = P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
         return tp
     tp, elapsed = timed_region(work, device, P)
     value = a.steps / elapsed * world
@@ -830,7 +892,7 @@ def bench_eqv2(a, rank, world, device, P):
 
     def work():
         tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1, seed=2)
-        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
+        a.final_states = P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
         return tp
     tp, elapsed = timed_region(work, device, P)
     finite = bool(torch.isfinite(tp).all().item())
@@ -974,7 +1036,7 @@ def bench_eqv2_l6(a, rank, world, device, P):
 
     def work():
         tp, tv = model.rollout(loc_d, vel_d, mass_d, a.steps + 1, seed=2)
-        P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
+        a.final_states = P.all_gather_shards(torch.cat([tp[:, -1], tv[:, -1]], -1).contiguous())
         return tp
     tp, elapsed = timed_region(work, device, P)
     value = a.steps / elapsed * world
@@ -1016,16 +1078,18 @@ def bench_gravity(a, rank, world, device, P):
     T = max(freq, a.steps - a.steps % freq)
     start, S = P.shard_range(S_glob, rank, world)
     sim = GravitySim(n_balls=N, interaction_strength=2, dt=0.01, softening=0.2, device=device)
-    rng = np.random.default_rng(start)
-    pos = rng.standard_normal((S, N, 3)) * np.cbrt(N / 5)
-    vel = rng.standard_normal((S, N, 3))
+    # the global batch's initial conditions from one seed, sliced per rank: system i is the same
+    # system whatever the rank count (the all-gathered final states equal a one-rank run's)
+    rng = np.random.default_rng(0)
+    pos = (rng.standard_normal((S_glob, N, 3)) * np.cbrt(N / 5))[start:start + S]
+    vel = rng.standard_normal((S_glob, N, 3))[start:start + S]
     vel -= vel.mean(1, keepdims=True)
     mass = np.ones((S, N, 1))
     sim.sample_trajectories(pos, vel, mass, max(freq, a.warmup - a.warmup % freq), freq)
 
     def work():
         ps, vs, fs = sim.sample_trajectories(pos, vel, mass, T, freq)
-        P.all_gather_shards(ps[:, -1].contiguous(), S_glob)
+        a.final_states = P.all_gather_shards(torch.cat([ps[:, -1], vs[:, -1]], -1).contiguous(), S_glob)
         return ps
     ps, elapsed = timed_region(work, device, P)
     inter = float(S_glob) * N * N * T

@@ -239,11 +239,18 @@ def run_inference(model_type, dataloader, model_path=None, model=None, save_dir=
     sync = shard and hasattr(model, "enable_sync_batchnorm") and model.training
     if sync:
         model.enable_sync_batchnorm(global_batch=batch_size)   # no per-call batch-size collective
+    # PONITA's one-time calibration (conv.py:134-140) from the moments of the whole sharded batch
+    calib = shard and hasattr(model, "calibration_group") and model.calibration_group is None
+    if calib:
+        import torch.distributed as dist
+        model.calibration_group = dist.group.WORLD
     try:
         tp, tv = model.rollout(loc0, vel0, mass0, num_steps, **kw)
     finally:
         if sync:
             model.disable_sync_batchnorm()
+        if calib:
+            model.calibration_group = None
     print("Finished prediction for all simulations")
     steps_in_actual = loc_actual.shape[1]
     loc_actual = loc_actual.reshape(count, steps_in_actual, n_nodes, output_dims)

@@ -192,6 +192,9 @@ class PONITA_NBODY(nn.Module):
             "{32, 64, 128}, basis_dim % 4 == 0, num_ori <= 24, widening * hidden <= 1024")
         self._packed = None
         self._ws = None
+        # torch.distributed group whose ranks share the one-time calibration (sharded batches: the
+        # moments of the whole global batch, as the reference's single process sees them); None = local
+        self.calibration_group = None
 
     def get_serializable_attributes(self):
         return {"lr": self.lr, "weight_decay": self.weight_decay, "warmup": self.warmup,
@@ -398,7 +401,16 @@ class PONITA_NBODY(nn.Module):
                 _lib.dev_ptr(out), _lib.dev_ptr(mom) if calib else None, _lib.dev_ptr(ws), ws.numel(),
                 _lib.stream_ptr(device)), "nbx_ponita_forward_graph")
         if calib:
-            self._callibrate(mom, V * self.num_ori * self.hidden_dim)
+            n = V * self.num_ori * self.hidden_dim
+            if self.calibration_group is not None:
+                import torch.distributed as dist
+                if dist.get_world_size(self.calibration_group) > 1:
+                    # the (sum, sum sq) moments and the element count over the group's ranks
+                    cnt = torch.tensor([float(n)], dtype=torch.float64, device=device)
+                    dist.all_reduce(mom, group=self.calibration_group)
+                    dist.all_reduce(cnt, group=self.calibration_group)
+                    n = int(cnt.item())
+            self._callibrate(mom, n)
         return out.to(pos.dtype)
 
     @torch.no_grad()

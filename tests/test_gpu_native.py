@@ -74,3 +74,29 @@ def test_gravity_batched_energy_property(hip_device):
     # first 5 frames of every system match the numpy oracle to ulp-level growth
     rp, rv, _ = ogr.sample_trajectories(pos, vel, mass, T=50, sample_freq=10, dt=0.01, G=2.0, softening=0.2)
     np.testing.assert_allclose(ps[:, :5], rp, rtol=0, atol=1e-11)
+
+
+def test_gravity_multi_system_n100_every_workgroup_slot(hip_device):
+    """C5's shape (N = 100: 10 systems per 1,000-lane workgroup, gravity.hip): 23 systems fill two
+    workgroups and leave a partial third (3 of 10 slots), so every local slot 0-9 and the partial
+    last workgroup are exercised.  Each system must match the numpy oracle (bit-exact with the
+    reference per DESIGN §2; synthetic_sim.py:357-420) over 10 frames, and equal the same system
+    integrated alone (slot 0 of a one-system launch) bit for bit."""
+    from nbody_amd.gravity import GravitySim
+    S, N, T, f = 23, 100, 100, 10
+    sim = GravitySim(n_balls=N, interaction_strength=2, dt=0.01, softening=0.2, device=hip_device)
+    ics = [sim.initial_conditions(100 + s) for s in range(S)]
+    pos = np.stack([c[0] for c in ics]); vel = np.stack([c[1] for c in ics]); mass = np.stack([c[2] for c in ics])
+    ps, vs, fs = (t.cpu().numpy() for t in sim.sample_trajectories(pos, vel, mass, T=T, sample_freq=f))
+    assert ps.shape == (S, T // f, N, 3)
+    rp, rv, rf = ogr.sample_trajectories(pos, vel, mass, T=T, sample_freq=f, dt=0.01, G=2.0, softening=0.2)
+    np.testing.assert_array_equal(ps[:, 0], pos)              # frame 0 = the initial state, bit-exact
+    np.testing.assert_allclose(ps, rp, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(vs, rv, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(fs, rf, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(ps[:, :5], rp[:, :5], rtol=0, atol=1e-11)
+    for s in range(S):
+        one = [t.cpu().numpy()[0] for t in sim.sample_trajectories(pos[s:s + 1], vel[s:s + 1], mass[s:s + 1],
+                                                                      T=T, sample_freq=f)]
+        for a, b in zip((ps[s], vs[s], fs[s]), one):
+            np.testing.assert_array_equal(a, b)

@@ -316,3 +316,68 @@ def test_syncbn_training_step_two_ranks_reproduce_full_batch(hip_device):
     for k, v in stats.items():
         for r in (0, 1):
             np.testing.assert_allclose(res[r][3][k], v, rtol=1e-5, atol=1e-7)
+
+
+def _bn_empty_worker(rank, world, port, q):
+    """Rank 0 holds every row, rank 1 none: both must reach each all-reduce of _SyncBNFn."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    from nbody_amd.segnn_train import _SyncBNFn
+    dev = torch.device("cuda:0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        S, V, w, b, dOS, dOV = _bn_inputs(dev)
+        if rank == 1:
+            S, V, dOS, dOV = S[:0], V[:, :0], dOS[:0], dOV[:, :0]
+        S.requires_grad_(True); V.requires_grad_(True); w.requires_grad_(True); b.requires_grad_(True)
+        rm, rv = torch.zeros(S.shape[1], device=dev), torch.ones(2 * S.shape[1], device=dev)
+        OS, OV = _SyncBNFn.apply(S, V, w, b, rm, rv, 1e-5, 0.1, dist.group.WORLD)
+        torch.autograd.backward([OS, OV], [dOS, dOV])
+        q.put((rank, [t.detach().cpu().numpy() for t in (OS, OV, S.grad, V.grad, w.grad, b.grad, rm, rv)]))
+    except Exception as e:
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _bn_inputs(dev, rows=200, M=32):
+    g = torch.Generator().manual_seed(5)
+    mk = lambda *s: torch.randn(*s, generator=g).to(dev)
+    return mk(rows, M), mk(3, rows, M), mk(2 * M) + 1.0, mk(M), mk(rows, M), mk(3, rows, M)
+
+
+def test_syncbn_training_bn_with_an_empty_shard(hip_device):
+    """A rank whose shard has no rows (uneven last batch, batch smaller than the world) still takes
+    part in _SyncBNFn's forward and backward all-reduces (nbx_bn_train_sums / _apply / _backward_apply
+    accept rows == 0); the rank with all rows reproduces the single-process batch-statistics
+    BatchNorm (_BNFn): outputs, input and parameter gradients, running statistics."""
+    from nbody_amd.segnn_train import _BNFn
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_empty_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert not isinstance(res[r], str), res[r]
+    S, V, w, b, dOS, dOV = _bn_inputs(hip_device)
+    for t in (S, V, w, b):
+        t.requires_grad_(True)
+    rm, rv = torch.zeros(S.shape[1], device=hip_device), torch.ones(2 * S.shape[1], device=hip_device)
+    OS, OV = _BNFn.apply(S, V, w, b, rm, rv, 1e-5, 0.1)
+    torch.autograd.backward([OS, OV], [dOS, dOV])
+    ref = [t.detach().cpu().numpy() for t in (OS, OV, S.grad, V.grad, w.grad, b.grad, rm, rv)]
+    for got, want in zip(res[0], ref):
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
+    assert res[1][0].shape == (0, S.shape[1]) and res[1][2].shape == (0, S.shape[1])
+    # the empty rank still updates its running statistics with the global batch statistics
+    np.testing.assert_allclose(res[1][6], ref[6], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(res[1][7], ref[7], rtol=1e-5, atol=1e-6)
+    # its parameter gradients are zero (no local rows); the data-parallel all-reduce sums them
+    np.testing.assert_array_equal(res[1][4], 0.0)
+    np.testing.assert_array_equal(res[1][5], 0.0)

@@ -23,9 +23,15 @@ def sig(x):
     return 1 / (1 + np.exp(-x))
 
 
-def emulate(model, pos, vel, mass, B, N, training=True):
-    """Mirror of forward_impl in csrc/segnn.hip (fp64)."""
+def emulate(model, pos, vel, mass, B, N, training=True, gemm=None):
+    """Mirror of forward_impl in csrc/segnn.hip (fp64).  ``gemm(A, key)`` (optional) replaces every
+    TP contraction A @ P[key].T, e.g. by an emulation of a reduced-operand MFMA path."""
     P = {k: v.double().numpy() for k, v in model.packed_matrices("cpu", torch.float64).items()}
+    if gemm is not None:
+        _mm = gemm
+    else:
+        def _mm(A, key):
+            return A @ P[key].T
     sd = {k: v.double().numpy().copy() for k, v in model.state_dict().items()}
     M = model.mul
     V = B * N
@@ -49,8 +55,8 @@ def emulate(model, pos, vel, mass, B, N, training=True):
                    for k in range(3)])                                    # [3, V, M]
     for li in range(model.num_layers):
         p = f"layers.{li}."
-        nps = xs @ P[p + "node_pre_s_t"].T                                # [V, 6M]
-        npv = np.stack([xv[k] @ P[p + "node_pre_v_t"].T for k in range(3)])  # [3, V, 6M]
+        nps = _mm(xs, p + "node_pre_s_t")                                # [V, 6M]
+        npv = np.stack([_mm(xv[k], p + "node_pre_v_t") for k in range(3)])  # [3, V, 6M]
         amf = np.stack([dist, pm], 1) @ P[p + "msg1_amf"]                 # [E, 3M]
         b1 = P[p + "msg1_bias"]
         sa = nps[d_of, :M] + nps[src, 3 * M:4 * M] + amf[:, :M] + b1[:M]
@@ -64,8 +70,8 @@ def emulate(model, pos, vel, mass, B, N, training=True):
         g = C_SIG * sig(sg)
         m1v = np.stack([g * vk for vk in v])
         m1s = np.concatenate([C_SILU * silu(sa), (m1v * rh.T[:, :, None]).sum(0)], 1)
-        g2s = m1s @ P[p + "msg2_s_t"].T
-        g2v = np.stack([m1v[k] @ P[p + "msg2_v_t"].T for k in range(3)])
+        g2s = _mm(m1s, p + "msg2_s_t")
+        g2v = np.stack([_mm(m1v[k], p + "msg2_v_t") for k in range(3)])
         b2 = P[p + "msg2_bias"]
         ms = C_SILU * silu(g2s[:, :M] + b2[:M])
         gg = C_SIG * sig(g2s[:, M:2 * M] + b2[M:])
@@ -88,14 +94,14 @@ def emulate(model, pos, vel, mass, B, N, training=True):
         a_s = sc_s * ags + (N - 1) * sh
         a_v = sc_v * agv
         u1s = np.concatenate([xs, a_s, (xv * na.T[:, :, None]).sum(0), (a_v * na.T[:, :, None]).sum(0)], 1)
-        g3s = u1s @ P[p + "upd1_s_t"].T
-        g3v = np.stack([np.concatenate([xv[k], a_v[k]], 1) @ P[p + "upd1_v_t"].T for k in range(3)])
+        g3s = _mm(u1s, p + "upd1_s_t")
+        g3v = np.stack([_mm(np.concatenate([xv[k], a_v[k]], 1), p + "upd1_v_t") for k in range(3)])
         b3 = P[p + "upd1_bias"]
         hs = C_SILU * silu(g3s[:, :M] + b3[:M])
         gh = C_SIG * sig(g3s[:, M:2 * M] + b3[M:])
         hv = np.stack([gh * (na[:, k, None] * g3s[:, 2 * M:] + g3v[k]) for k in range(3)])
-        g4s = np.concatenate([hs, (hv * na.T[:, :, None]).sum(0)], 1) @ P[p + "upd2_s_t"].T
-        g4v = np.stack([hv[k] @ P[p + "upd2_v_t"].T for k in range(3)])
+        g4s = _mm(np.concatenate([hs, (hv * na.T[:, :, None]).sum(0)], 1), p + "upd2_s_t")
+        g4v = np.stack([_mm(hv[k], p + "upd2_v_t") for k in range(3)])
         xs = xs + g4s[:, :M] + P[p + "upd2_bias"]
         xv = np.stack([xv[k] + na[:, k, None] * g4s[:, M:] + g4v[k] for k in range(3)])
         fw, fb = sd[p + "feature_norm.weight"], sd[p + "feature_norm.bias"]
@@ -107,8 +113,8 @@ def emulate(model, pos, vel, mass, B, N, training=True):
         sc_s, sc_v = fw[:M] / np.sqrt(var + 1e-5), fw[M:] / np.sqrt(nv + 1e-5)
         xs = sc_s * xs + (fb - sc_s * mu)
         xv = sc_v * xv
-    g = np.concatenate([xs, (xv * na.T[:, :, None]).sum(0)], 1) @ P["pp1_s_t"].T
-    gv = np.stack([xv[k] @ P["pp1_v_t"].T for k in range(3)])
+    g = _mm(np.concatenate([xs, (xv * na.T[:, :, None]).sum(0)], 1), "pp1_s_t")
+    gv = np.stack([_mm(xv[k], "pp1_v_t") for k in range(3)])
     b = P["pp1_bias"]
     hs = C_SILU * silu(g[:, :M] + b[:M])
     gh = C_SIG * sig(g[:, M:2 * M] + b[M:])
@@ -203,3 +209,54 @@ def test_train_operands_equal_train_matrices(hidden, layers, dtype):
     for n in grads[0]:
         assert grads[0][n].dtype == grads[1][n].dtype == dtype
         torch.testing.assert_close(grads[0][n], grads[1][n], rtol=1e-6, atol=1e-6)
+
+
+def _split_gemms(model):
+    """GEMM emulations over the module's packed operands: "f32" = fp32 operands, fp32 accumulation
+    (the fp32 MFMA path); "h2" = the fp16x2 path (include/nbx.h "fp16x2 images": weights scaled per
+    TP by SEGNN.h2_scale and split into fp16 hi + lo, activations split the same way unscaled, the
+    three products hi.lo + lo.hi + hi.hi accumulated in fp32)."""
+    Pt = model.packed_matrices("cpu", torch.float64)
+    P = {k: v.numpy() for k, v in Pt.items()}
+    pair = {"node_pre_s_t": "node_pre_v_t", "node_pre_v_t": "node_pre_s_t"}
+    def scale(key):
+        pre, base = key.rsplit(".", 1) if "." in key else ("", key)
+        other = pair.get(base, base[:-4] + ("_v_t" if base.endswith("_s_t") else "_s_t"))
+        okey = (pre + "." if pre else "") + other
+        return S.SEGNN.h2_scale(Pt[key], Pt[okey])
+
+    def f32(A, key):
+        return (A.astype(np.float32) @ P[key].T.astype(np.float32)).astype(np.float64)
+
+    def h2(A, key):
+        s = scale(key)
+        W = (P[key].T * s).astype(np.float32)
+        wh = W.astype(np.float16).astype(np.float32)
+        wl = (W - wh).astype(np.float16).astype(np.float32)
+        A = A.astype(np.float32)
+        ah = A.astype(np.float16).astype(np.float32)
+        al = (A - ah).astype(np.float16).astype(np.float32)
+        acc = (ah @ wl + al @ wh) + ah @ wh          # fp32 products of fp16 parts are exact
+        return acc.astype(np.float64) / s
+    return {"f32": f32, "h2": h2}
+
+
+def test_fp16x2_gemm_path_is_fp32_accurate():
+    """The fp16x2 split path (StatSKH2 kernels) on the C2 model (hidden 192, 6 layers, train-mode
+    BatchNorm): with every TP contraction emulated on its fp16x2 operands, the forward stays as close
+    to the fp64 forward as the same emulation with plain fp32 operands and fp32 accumulation (the
+    fp32 MFMA path): max error <= 2x the fp32 path's.  Measured: 1.2x (8.97e-7 vs 7.31e-7; the fp32 accumulation of
+    K = 96..384 products dominates the 2^-22 operand representation error of fp16x2)."""
+    torch.manual_seed(0)
+    model = S.SEGNN(hidden_features=192, num_layers=6)
+    rng = np.random.default_rng(3)
+    B, N = 8, 5
+    V = B * N
+    pos, vel = rng.standard_normal((V, 3)) * 1.2, rng.standard_normal((V, 3))
+    mass = np.ones(V)
+    ref = emulate(model, pos, vel, mass, B, N, True)
+    g = _split_gemms(model)
+    e = {k: np.abs(emulate(model, pos, vel, mass, B, N, True, gemm=f) - ref).max() / np.abs(ref).max()
+         for k, f in g.items()}
+    print(f"C2 forward, max error / output scale vs fp64: fp32 path {e['f32']:.2e}, fp16x2 path {e['h2']:.2e}")
+    assert e["h2"] <= 2.0 * e["f32"] and e["h2"] < 1e-5, e
