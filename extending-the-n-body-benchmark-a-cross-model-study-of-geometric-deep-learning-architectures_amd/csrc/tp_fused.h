@@ -152,7 +152,24 @@ struct TpProb {
     float* out_dot;
     // fp16x2 images (StatSKH2): the factor that undoes the image's power-of-two weight scale
     float bscale;
+    // XCD-grouped block order (set by the launchers when blocks_per_chunk % 8 == 0): the number of
+    // chunk groups G; blocks b, b + 8, ... run on one XCD, so the G chunk groups of one row range are
+    // given ids with equal b % 8 and that XCD's L2 fetches the range's A rows once for all G of them
+    // (0: chunk-major order)
+    int xcd_groups;
 };
+
+// block id -> (chunk group, row-range block): chunk-major, or XCD-grouped (TpProb::xcd_groups)
+__device__ inline void tp_block_map(const TpProb& P, int bidx, int& group, int& blk) {
+    if (P.xcd_groups > 0) {
+        const int xcd = bidx & 7, s = bidx >> 3;
+        group = s % P.xcd_groups;
+        blk = (s / P.xcd_groups) * 8 + xcd;
+    } else {
+        group = bidx / P.blocks_per_chunk;
+        blk = bidx - group * P.blocks_per_chunk;
+    }
+}
 
 constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
 
@@ -320,8 +337,8 @@ template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2, class SK = D
 __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(const TpProb P) {
     constexpr int THREADS = 64 * WAVES;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int chunk = blockIdx.x / P.blocks_per_chunk;
-    const int blk = blockIdx.x - chunk * P.blocks_per_chunk;
+    int chunk, blk;
+    tp_block_map(P, (int)blockIdx.x, chunk, blk);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
 
     int off[NS + 1];
@@ -827,6 +844,7 @@ inline void tp_geometry(TpProb& p, int waves = TP_WAVES, int num_cus = 256, int 
     if (bpc < 1) bpc = 1;
     p.blocks_per_chunk = bpc;
     p.waves_per_chunk = bpc;  // partial rows per chunk (one per block)
+    p.xcd_groups = (p.chunks > 1 && bpc % 8 == 0) ? p.chunks : 0;
 }
 
 template <int NS, int NV, int EPI, int WAVES = TP_WAVES, int D = 2, class SK = DynSK>
