@@ -17,6 +17,8 @@ constexpr int MP_THREADS = 512;
 template <bool X3> struct MpEx {   // X3: any split-precision node GEMM (bf16x3 or fp16x2)
     static constexpr int RS = X3 ? 16 : 20, PART = 16 * RS, EX = 4 * 6 * PART;
 };
+// exchange buffers: three beside the fp16x2 images (decoupled hand-off), two otherwise
+constexpr int mp_nbuf(int prec) { return prec == 2 ? 3 : 2; }
 
 // X3: the node GEMM on the split-precision path (tp_fused.h StatSKX3; bf16x3 CW = 16 images,
 // v_mfma_f32_16x16x32_bf16 whose A fragment -- lane quarter qd holds k = 8 qd + j -- is exactly
@@ -27,11 +29,16 @@ template <bool X3> struct MpEx {   // X3: any split-precision node GEMM (bf16x3 
 template <int PREC, int KCT = 0>
 __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const MsgPreProb P) {
     constexpr bool X3 = PREC != 0;
+    // fp16x2 (images the fp32 size): three exchange buffers fit, and the two roles hand them over
+    // through LDS counters instead of a block barrier per stage (DEC): the GEMM waves may run up to
+    // two groups ahead of the edge waves, so per-stage jitter of either role is absorbed
+    constexpr int NBUF = mp_nbuf(PREC);
+    constexpr bool DEC = NBUF > 2;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
     constexpr int MP_RS = MpEx<X3>::RS, MP_PART = MpEx<X3>::PART, MP_EX = MpEx<X3>::EX;
-    float* EX = lds + 2 * F;   // [2 buffers][MP_EX]
-    float* XC = EX + 2 * MP_EX;  // pending BN of X per k: [sc_s | sc_v | sh] x (KC * 32), zero past M
+    float* EX = lds + 2 * F;   // [NBUF buffers][MP_EX]
+    float* XC = EX + NBUF * MP_EX;  // pending BN of X per k: [sc_s | sc_v | sh] x (KC * 32), zero past M
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
     const bool gemm_wave = wave < 4;
     const int plane = wave & 3;
@@ -75,18 +82,31 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
             if (kc < KC) load_a(0, kc, abuf[kc]);
     }
 
+    // the previous layer's feature BatchNorm, finalised here from its sums: the inputs of one
+    // evaluation per thread (t < 2M: kind = t / M) are loaded before the image DMA, so the
+    // coefficient math waits for them only (vmcnt retires in issue order)
+    const bool bn_on = P.xbn.sums != nullptr && t < 2 * M;
+    const int bn_kind = t / M, bn_k = t % M;
+    BnPre bn_pre{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
+    if (bn_on) bn_pre = bn_pre_load(P.xbn, M, bn_kind, bn_k);
+
     // both weight images of this chunk -> LDS (DMA, verbatim)
     tp_dma_image<8>(P.Simg + (size_t)chunk * F, lds, F);
     tp_dma_image<8>(P.Vimg + (size_t)chunk * F, lds + F, F);
 
     // the previous layer's feature BatchNorm is applied to X here, as it is loaded (lazy BN:
     // X in HBM holds the pre-normalisation values); identity when xcoef is null
+    // (XC: [sc_s | sc_v | sh] x (KC * 32), zero past M)
+    if (bn_on) {
+        const float2 c = bn_pre_coef(P.xbn, bn_pre, M, bn_kind, bn_k, blockIdx.x == 0);
+        if (bn_kind == 0) { XC[bn_k] = c.x; XC[2 * KC * 32 + bn_k] = c.y; }
+        else XC[KC * 32 + bn_k] = c.x;
+    }
     for (int i = t; i < 3 * KC * 32; i += MP_THREADS) {
         const int part = i / (KC * 32), k = i - part * KC * 32;
+        if (P.xbn.sums && k < M) continue;   // written above
         float v = 0.f;
-        if (k < M)
-            v = P.xbn.sums ? bn_coef(P.xbn, M, part, k, blockIdx.x == 0)
-                           : (P.xcoef ? P.xcoef[part * M + k] : (part < 2 ? 1.f : 0.f));
+        if (k < M) v = P.xcoef ? P.xcoef[part * M + k] : (part < 2 ? 1.f : 0.f);
         XC[i] = v;
     }
 
@@ -100,8 +120,27 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
         ba = *reinterpret_cast<const float4*>(P.bias + ch0);
         bg = *reinterpret_cast<const float4*>(P.bias + M + ch0);
     }
+    // DEC hand-off counters: [0] = GEMM-wave group writes completed (4 per group), [1] = edge-wave
+    // group reads completed (4 per group)
+    int* hand = reinterpret_cast<int*>(XC + 3 * KC * 32);
+    if (DEC && t == 0) { hand[0] = 0; hand[1] = 0; }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // relaxed LDS poll (the LDS keeps each wave's operations in order; the empty asm keeps the compiler
+    // from hoisting the exchange reads above it) and no-return LDS add after this wave's LDS traffic
+    // (inline asm: no wait for the wave's global stores)
+    auto dec_wait = [&](int which, int need) {
+        while (__hip_atomic_load(hand + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+    };
+    auto dec_signal = [&](int which) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            const unsigned a = (unsigned)(uintptr_t)(hand + which);
+            asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1) : "memory");
+        }
+    };
 
     const float* img = lds + (plane ? F : 0);
     const int group_items = NG * G;
@@ -124,6 +163,8 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
     for (int i = 0; i <= my_groups; ++i) {
         floatx4 acc[6];
         auto write_ex = [&](int buf) {
+            if constexpr (DEC)   // buffer `buf` free: the edge waves are done with group i - NBUF
+                if (i >= NBUF) dec_wait(1, 4 * (i - NBUF + 1));
             float* ex = EX + buf * MP_EX + plane * 6 * MP_PART;
 #pragma unroll
             for (int j = 0; j < 6; ++j)
@@ -234,7 +275,8 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
 #pragma unroll
                 for (int kc = 0; kc < KCMAX; ++kc)
                     if (kc < KC) load_a(i + 1, kc, abuf[kc]);
-                write_ex(i & 1);
+                write_ex(i % NBUF);
+                if constexpr (DEC) dec_signal(0);
                 tick(c_gemm);
             }
         } else if (i > 0 && live && !P.diag) {
@@ -242,7 +284,8 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
             const float4 geo_cur = geo_next;
             const float pm_cur = pm_next;
             load_geo(i, geo_next, pm_next);
-            const float* exb = EX + ((i - 1) & 1) * MP_EX;
+            if constexpr (DEC) dec_wait(0, 4 * i);   // group i - 1 written by all four GEMM waves
+            const float* exb = EX + ((i - 1) % NBUF) * MP_EX;
             auto xv = [&](int pl, int part, int row) {
                 const int q = X3 ? cq ^ ((row >> 2) & 3) : cq;
                 return *reinterpret_cast<const float4*>(exb + (pl * 6 + part) * MP_PART + row * MP_RS + 4 * q);
@@ -309,11 +352,16 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
             }
             tick(c_edge);
         }
-        // LDS hand-off only: wait for this wave's LDS traffic, not for its global stores
-        // (the empty asm after each barrier keeps the compiler from hoisting LDS accesses above it)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+        if constexpr (DEC) {
+            // (every edge wave signals, dead lanes or not, so the counts stay 4 per group)
+            if (!gemm_wave && i > 0) dec_signal(1);
+        } else {
+            // LDS hand-off only: wait for this wave's LDS traffic, not for its global stores
+            // (the empty asm after each barrier keeps the compiler from hoisting LDS accesses above it)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
         tick(c_ex);
     }
     if (P.dbg && lane == 0) {
@@ -323,7 +371,8 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
 }
 
 inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
-    return ((size_t)2 * p.img_floats + 2 * (p.prec ? MpEx<true>::EX : MpEx<false>::EX) + 3 * 32 * ((p.M + 31) / 32)) * 4;
+    return ((size_t)2 * p.img_floats + mp_nbuf(p.prec) * (p.prec ? MpEx<true>::EX : MpEx<false>::EX) +
+            3 * 32 * ((p.M + 31) / 32)) * 4 + 16;   // + the hand-off counters
 }
 
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {

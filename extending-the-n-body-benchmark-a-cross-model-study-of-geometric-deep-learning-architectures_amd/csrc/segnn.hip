@@ -709,6 +709,12 @@ bool x3_enabled() {
     return v == 1;
 }
 
+// TEMPORARY A/B (r05): A-ring depth of the fp16x2 node TPs / message kernel (NBX_PF, NBX_MSG_D)
+int env_int(const char* name, int def) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : def;
+}
+
 // Split-precision MFMA path of the SEGNN TPs: 2 = the fp16x2 images (default, when present),
 // 1 = the bf16x3 images, 0 = fp32 MFMA.  NBX_SPLIT=x3 / NBX_X3=0 select 1 / 0 (A/B only).
 int split_prec() {
@@ -762,7 +768,12 @@ int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void*
             const float* fp32_img = p.B;
             p.B = static_cast<const float*>(img_h2);
             p.bscale = h2_descale;
-            if (sk_matches<SK_MSG2_H2>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_H2>(p, st, tm);
+            if (sk_matches<SK_MSG2_H2>(p, NS, NV)) {
+                static const int d = env_int("NBX_MSG_D", 3);
+                if (d == 4) return run_tp<NS, NV, EPI, 8, 4, SK_MSG2_H2>(p, st, tm);
+                if (d == 5) return run_tp<NS, NV, EPI, 8, 5, SK_MSG2_H2>(p, st, tm);
+                return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_H2>(p, st, tm);
+            }
             if (sk_matches<SK_MSG2_32_H2>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_32_H2>(p, st, tm);
             p.B = fp32_img;
         }
@@ -815,35 +826,25 @@ int tp16_debug_dump(const unsigned long long* dbg, int n, hipStream_t st, const 
     return NBX_OK;
 }
 
-// NBX_LW=1: the split-precision node TPs stage their image with a loader wave (tp16.h LW; A/B)
-bool lw_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NBX_LW");
-        v = (e && e[0] == '1') ? 1 : 0;
-    }
-    return v == 1;
-}
-
-template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, class SK = nbx::DynSK, bool LW = false>
+template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, class SK = nbx::DynSK>
 int run_tp16_w(nbx::TpProb& p, hipStream_t st, KernelTiming* tm) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
     if (debug) {
         p.dbg = tp_dbg_buf(st);
-        if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK, LW>(p, st)) return rc;
+        if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK>(p, st)) return rc;
         int n = ((p.chunks + CG - 1) / CG) * p.blocks_per_chunk * WAVES;
         char lab[32];
         snprintf(lab, sizeof lab, "tp16<%d,%d,%d,%d,KS%d>", NS, NV, EPI, CG, KS);
         return tp16_debug_dump(p.dbg, n, st, lab);
     }
-    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK, LW>(p, st);
+    if (!tm) return nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK>(p, st);
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
     NBX_HIP(hipEventCreate(&b));
     tm->ev.push_back(a);
     tm->ev.push_back(b);
     nbx::armed_events() = {a, b};   // the launch below records the kernel's own begin / end
-    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK, LW>(p, st)) return rc;
+    if (int rc = nbx::tp16_launch<NS, NV, EPI, CG, WAVES, PF, KS, SK>(p, st)) return rc;
     NBX_HIP(nbx::disarm_events(st));
     double k = 0;
     for (int j = 0; j < NS; ++j) k += p.K[j];
@@ -1152,9 +1153,10 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if ((M == 96 || M == 32) && L.upd1_img_h2 && split_prec() == 2) {
                 p.B = static_cast<const float*>(L.upd1_img_h2);
                 p.bscale = L.upd1_h2_descale;
-                const int rc = M == 96 ? (lw_enabled()
-                                              ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2, true>(p, st, tm)
-                                              : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm))
+                static const int pf = env_int("NBX_PF", 3);
+                const int rc = M == 96 ? (pf == 5 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 5, 1, SK_UPD1_SEG_H2>(p, st, tm)
+                                          : pf == 7 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 7, 1, SK_UPD1_SEG_H2>(p, st, tm)
+                                                    : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm))
                                        : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
                 if (rc) return rc;
             } else if (M == 96 && L.upd1_img_x3 && split_prec() == 1) {
@@ -1200,9 +1202,10 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if ((M == 96 || M == 32) && L.upd2_img_h2 && split_prec() == 2 && static_enabled()) {
                 p.B = static_cast<const float*>(L.upd2_img_h2);
                 p.bscale = L.upd2_h2_descale;
-                const int rc = M == 96 ? (lw_enabled()
-                                              ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2, true>(p, st, tm)
-                                              : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm))
+                static const int pf = env_int("NBX_PF", 3);
+                const int rc = M == 96 ? (pf == 5 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 5, 1, SK_UPD2_H2>(p, st, tm)
+                                          : pf == 7 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 7, 1, SK_UPD2_H2>(p, st, tm)
+                                                    : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm))
                                        : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2>(p, st, tm);
                 if (rc) return rc;
             } else {
@@ -1251,9 +1254,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         if (w->pp1_img_h2 && split_prec() == 2) {
             p.B = static_cast<const float*>(w->pp1_img_h2);
             p.bscale = w->pp1_h2_descale;
-            const int rc = M == 96 ? (lw_enabled()
-                                          ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2, true>(p, st, tm)
-                                          : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2>(p, st, tm))
+            const int rc = M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2>(p, st, tm)
                                    : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG_H2>(p, st, tm);
             if (rc) return rc;
         } else if (M == 96) {

@@ -26,31 +26,9 @@ constexpr int T16_WAVES = 8, T16_THREADS = 64 * T16_WAVES;
 
 // Two independent problems of the same shape class can share one launch (P0 for blocks below
 // `split`, P1 above): node_pre's scalar-row and vector-row GEMMs fill the chip together.
-// LW slab schedule (see tp16_kernel): blocks per slab and pieces issued after a slab
-template <class SK, int NS, int NV>
-struct LwSched {
-    static constexpr int NP = SK::PREC == 1 ? 3 : 2;   // 1 KiB pieces per 32-deep block
-    static constexpr int NSLAB = SK::K0 + (NV ? SK::KV : 0);
-    static constexpr int blocks(int s) {
-        return s < SK::K0 ? 1 + ((NS > 1 && s < SK::K1) ? 1 : 0) + ((NS > 2 && s < SK::K2) ? 1 : 0) : 1;
-    }
-    static constexpr int after(int r, int last) {
-        int n = 0;
-        for (int q = r + 1; q <= last; ++q) n += blocks(q) * NP;
-        return n;
-    }
-};
-
-// LW (loader wave): one extra wave streams the chunk image into LDS by LDS-DMA in the order the
-// static item schedule consumes it -- slab s = the blocks item s reads first -- and publishes a
-// monotonic slab counter in LDS behind its own counted vmcnt waits; the WAVES compute waves start
-// their tiles right after the prologue and wait on the counter only for blocks not yet landed, so the
-// image transfer overlaps the K loop instead of preceding it (split-precision static schedules,
-// CG = KS = 1).
 template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, bool DUAL = false,
-          class SK = DynSK, bool LW = false>
-__global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ? 1 : 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
-    static_assert(!LW || (SK::on && SK::PREC >= 1 && KS == 1 && CG == 1 && !DUAL), "loader wave: static split path only");
+          class SK = DynSK>
+__global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16_kernel(const TpProb P0, const TpProb P1, int split) {
     const bool second = DUAL && (int)blockIdx.x >= split;
     const TpProb& P = second ? P1 : P0;
     const int bidx = second ? (int)blockIdx.x - split : (int)blockIdx.x;
@@ -65,7 +43,6 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, qd = lane >> 4;
     const int slice = wave % KS, tslot = wave / KS;
     const int nchunks16 = P.chunks;                        // total 16-channel chunks
-    const bool loader = LW && wave == WAVES;               // the loader wave (LW) computes no tile
 
     int sub_off[NS + 1];
     tp_img_offsets<NS>(P, 16, sub_off);
@@ -163,55 +140,31 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
         });
     };
     if constexpr (SK::on) {
-        if (!loader)
-            slice_call([&](auto sc_) {
-                constexpr int lo = decltype(sc_)::value * SNIT / KS, hi = (decltype(sc_)::value + 1) * SNIT / KS;
-                static_for<0, PF - 1>([&](auto uc) {
-                    constexpr int u = decltype(uc)::value;
-                    if constexpr (lo + u < hi) load_item(std::integral_constant<int, lo + u>{}, rt, ring[u % PF]);
-                });
+        slice_call([&](auto sc_) {
+            constexpr int lo = decltype(sc_)::value * SNIT / KS, hi = (decltype(sc_)::value + 1) * SNIT / KS;
+            static_for<0, PF - 1>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                if constexpr (lo + u < hi) load_item(std::integral_constant<int, lo + u>{}, rt, ring[u % PF]);
             });
+        });
     } else {
 #pragma unroll
         for (int u = 0; u < PF - 1; ++u) load_a(rt, c_lo + u, ring[u]);
     }
 
-    // ---- LW: the loader wave's slab stream.  Slab s < K0 = the scalar blocks item s reads first
-    // (sub-tile j's block OB[j] + s, for the sub-tiles live at s), slab K0 + kc = vector block kc;
-    // a block is NP pieces of 1 KiB (one global_load_lds_dwordx4 each).  LWLAG slabs stay in flight.
-    using LWS = LwSched<SK, NS, NV>;
-    constexpr int LWNP = LWS::NP;
-    constexpr int NSLAB = LWS::NSLAB;
-    constexpr int LWLAG = 3;
-    int* lw_ready = reinterpret_cast<int*>(lds + P.lds_floats);   // slabs landed (LW)
-    auto lw_issue = [&](auto sc_) {
-        constexpr int s_ = decltype(sc_)::value;
-        constexpr int OB[4] = {0, SK::K0, SK::K0 + SK::K1, SK::K0 + SK::K1 + SK::K2};
-        const float* src = P.B + (size_t)cgroup * P.img_floats;
-        static_for<0, LWS::blocks(s_)>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            constexpr int blkid = s_ < SK::K0 ? OB[j] + s_ : OB[NS] + (s_ - SK::K0);
-#pragma unroll
-            for (int p = 0; p < LWNP; ++p)
-                __builtin_amdgcn_global_load_lds((const void*)(src + (blkid * LWNP + p) * 256 + lane * 4),
-                                                 (__attribute__((address_space(3))) void*)(lds + (blkid * LWNP + p) * 256),
-                                                 16, 0, 0);
-        });
-    };
-    // publish "slabs < n landed" (inline asm: a compiler-visible LDS store after LDS-DMA would get a
-    // vmcnt(0) in front of it and drain the stream)
-    auto lw_publish = [&](int n) {
-        const unsigned a = (unsigned)(uintptr_t)lw_ready;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(n) : "memory");
-    };
-    if constexpr (LW) {
-        if (t == 0) *lw_ready = 0;
-        if (loader) static_for<0, (LWLAG < NSLAB ? LWLAG : NSLAB)>([&](auto sc_) { lw_issue(sc_); });
-    }
+    // ---- segmented input: the BatchNorm coefficient inputs, loaded before the image DMA (one
+    // evaluation per thread: message BN at t < 2M, feature BN at 2M <= t < 4M; kind = which half)
+    const int bn_M = P.M;
+    const bool bn_m = SK::SEG == 4 && P.mbn.sums != nullptr;   // message BN finalised here
+    const bool bn_x = SK::SEG > 0 && P.xbn.sums != nullptr;    // pending feature BN finalised here
+    const int bn_which = t < 2 * bn_M ? 0 : 1, bn_kind = (t % (2 * bn_M)) / bn_M, bn_k = t % bn_M;
+    const bool bn_on = SK::SEG > 0 && t < 4 * bn_M && (bn_which == 0 ? bn_m : bn_x);
+    BnPre bn_pre{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
+    if (bn_on) bn_pre = bn_pre_load(bn_which == 0 ? P.mbn : P.xbn, bn_M, bn_kind, bn_k);
 
     // ---- stage the CG chunk images of this group in LDS (LDS-DMA, verbatim copy; the image
     // array holds a multiple of 4 chunks, so a group never runs past it)
-    if constexpr (!LW) {
+    {
         const int stride = P.img_stride > 0 ? P.img_stride : P.img_floats;
         if (stride == P.img_floats) {
             tp_dma_image<WAVES>(P.B + (size_t)cgroup * CG * P.img_floats, lds, CG * P.img_floats);
@@ -225,23 +178,24 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
     float* segtab = lds + CG * P.img_floats;
     if constexpr (SK::SEG > 0) {
         const int M = P.M;
-        const bool mfin = SK::SEG == 4 && P.mbn.sums != nullptr;   // message BN finalised here
-        const bool own = blockIdx.x == 0;
-        const bool xfin = P.xbn.sums != nullptr;                    // pending feature BN finalised here
-        for (int i = t; i < 10 * M && !loader; i += THREADS) {
+        const bool mfin = bn_m, xfin = bn_x;
+        // the BatchNorm parts from the preloaded inputs: message BN -> parts 1 (0e scale), 5 (shift x
+        // deg), 3 and 9 (1o scale); feature BN -> parts 0, 4, 2 and 8
+        if (bn_on) {
+            const float2 c = bn_pre_coef(bn_which == 0 ? P.mbn : P.xbn, bn_pre, M, bn_kind, bn_k, blockIdx.x == 0);
+            if (bn_which == 0) {
+                if (bn_kind == 0) { segtab[1 * M + bn_k] = c.x; segtab[5 * M + bn_k] = P.deg * c.y; }
+                else { segtab[3 * M + bn_k] = c.x; segtab[9 * M + bn_k] = c.x; }
+            } else {
+                if (bn_kind == 0) { segtab[0 * M + bn_k] = c.x; segtab[4 * M + bn_k] = c.y; }
+                else { segtab[2 * M + bn_k] = c.x; segtab[8 * M + bn_k] = c.x; }
+            }
+        }
+        for (int i = t; i < 10 * M; i += THREADS) {
             const int part = i / M, k = i - part * M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
             float v;
-            if (mfin && (part == 1 || part == 3 || part == 5 || part == 9)) {
-                const int bp = part == 1 ? 0 : part == 5 ? 2 : 1;
-                v = bn_coef(P.mbn, M, bp, k, own && part != 9);
-                segtab[i] = part == 5 ? P.deg * v : v;
-                continue;
-            }
-            if (xfin && (part == 0 || part == 2 || part == 4 || part == 8)) {
-                const int bp = part == 0 ? 0 : part == 4 ? 2 : 1;
-                segtab[i] = bn_coef(P.xbn, M, bp, k, own && part != 8);
-                continue;
-            }
+            if (mfin && (part == 1 || part == 3 || part == 5 || part == 9)) continue;
+            if (xfin && (part == 0 || part == 2 || part == 4 || part == 8)) continue;
             switch (part) {
                 case 0: v = P.xcoef ? P.xcoef[k] : 1.f; break;
                 case 1: v = SK::SEG == 4 ? P.mcoef[k] : 0.f; break;
@@ -256,49 +210,13 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
             segtab[i] = v;
         }
     }
-    if constexpr (!LW) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    } else {
-        // LDS hand-off of the table only (no fence: __syncthreads would drain the loader's DMA and
-        // the compute waves' A prefetch)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     const unsigned long long c_staged = P.dbg ? clock64() : 0ull;
     c_mark = c_staged;
-    if constexpr (LW) {
-        if (loader) {
-            // steady state: issue slab s, then publish slab s - LWLAG once it has landed
-            static_for<LWLAG, (NSLAB > LWLAG ? NSLAB : LWLAG)>([&](auto sc_) {
-                constexpr int s_ = decltype(sc_)::value;
-                lw_issue(sc_);
-                constexpr int after = LWS::after(s_ - LWLAG, s_);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(after) : "memory");
-                lw_publish(s_ - LWLAG + 1);
-            });
-            // drain
-            static_for<(NSLAB > LWLAG ? NSLAB - LWLAG : 0), NSLAB>([&](auto rc_) {
-                constexpr int r = decltype(rc_)::value;
-                constexpr int after = LWS::after(r, NSLAB - 1);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(after) : "memory");
-                lw_publish(r + 1);
-            });
-        }
-    }
-    // (LW) wait until the slab holding `item`'s first-read blocks has landed
-    auto lw_wait = [&](auto ic) {
-        if constexpr (LW) {
-            constexpr int item = decltype(ic)::value;
-            constexpr int need = (item < SK::K0 ? item : SK::K0 + (item - SK::K0) % (SK::KV > 0 ? SK::KV : 1)) + 1;
-            while (__hip_atomic_load(lw_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-                __builtin_amdgcn_s_sleep(0);
-        }
-    };
 
     float* kred = lds + P.lds_floats - (KS > 1 ? TW * (KS - 1) * NACC * 4 * 64 : 0);  // split-K partials
-    for (int it = 0; it < (loader ? 0 : iters); ++it) {
+    for (int it = 0; it < iters; ++it) {
         {
             // RESID: the epilogue's residual X rows and node attributes, loaded before the K loop so
             // their latency hides under the MFMAs (not after the last chunk)
@@ -529,17 +447,13 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
                         constexpr int n = (decltype(sc_)::value + 1) * SNIT / KS - lo;
                         SPT bx[NBS][CG][NS > 1 ? NS : 1][NP];   // item u in set u % NBS
                         SPT ax[3][NP];
-                        lw_wait(std::integral_constant<int, lo>{});
                         read_b(std::integral_constant<int, lo>{}, bx[0]);
                         static_for<0, n>([&](auto uc) {
                             constexpr int u = decltype(uc)::value, item = lo + u;
                             if constexpr (u + PF - 1 < n)
                                 load_item(std::integral_constant<int, item + PF - 1>{}, rt, ring[(u + PF - 1) % PF]);
                             __builtin_amdgcn_sched_barrier(0);
-                            if constexpr (u + 1 < n) {
-                                lw_wait(std::integral_constant<int, item + 1>{});
-                                read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % NBS]);
-                            }
+                            if constexpr (u + 1 < n) read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % NBS]);
                             float av[8];
                             item_a(std::integral_constant<int, item>{}, ring[u % PF], av);
                             SP::split(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]}, ax[u % 3]);
@@ -801,7 +715,7 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
             rt = next_rt;
         }
     }
-    if (P.dbg && lane == 0 && !loader) {
+    if (P.dbg && lane == 0) {
         unsigned long long* d = P.dbg + ((size_t)bidx * WAVES + wave) * 6;
         // [start, staged, sum over tiles of the K loop, sum over tiles of the epilogue, wall start]
         d[0] = c_start; d[1] = c_staged; d[2] = c_loop; d[3] = c_epi; d[4] = w_start;
@@ -816,7 +730,7 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
             double a = st0[g], b = st1[g], c = st2[g];
             a += __shfl_xor(a, 16); b += __shfl_xor(b, 16); c += __shfl_xor(c, 16);
             a += __shfl_xor(a, 32); b += __shfl_xor(b, 32); c += __shfl_xor(c, 32);
-            if (qd == 0 && !loader) {
+            if (qd == 0) {
                 red[((g * 3 + 0) * WAVES + wave) * 16 + c16] = a;
                 red[((g * 3 + 1) * WAVES + wave) * 16 + c16] = b;
                 red[((g * 3 + 2) * WAVES + wave) * 16 + c16] = c;
@@ -836,7 +750,7 @@ __global__ __launch_bounds__(64 * (WAVES + (LW ? 1 : 0)), (SK::PREC || PF > 4) ?
             }
         }
     }
-    if (P.dbg && lane == 0 && !loader) P.dbg[((size_t)bidx * WAVES + wave) * 6 + 5] = wall_clock64();   // wall end
+    if (P.dbg && lane == 0) P.dbg[((size_t)bidx * WAVES + wave) * 6 + 5] = wall_clock64();   // wall end
 }
 
 template <int CG>
@@ -931,7 +845,7 @@ inline int tp16_seg_prepare(TpProb& p) {
     return NBX_OK;
 }
 
-template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, bool DUAL, class SK = DynSK, bool LW = false>
+template <int NS, int NV, int EPI, int CG, int WAVES, int PF, int KS, bool DUAL, class SK = DynSK>
 int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
     if (b0 + b1 == 0) return NBX_OK;
     if constexpr (SK::SEG > 0) {
@@ -942,26 +856,20 @@ int tp16_go(TpProb& p0, TpProb& p1, int b0, int b1, hipStream_t st) {
     if (int rc = tp16_check_static<SK>(p0)) return rc;
     if (DUAL)
         if (int rc = tp16_check_static<SK>(p1)) return rc;
-    NBX_LDS_160K((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK, LW>));
-    // (LW: + the loader wave's slab counter after the image / table)
-    const size_t lds = (size_t)std::max(b0 ? p0.lds_floats : 0, b1 ? p1.lds_floats : 0) * 4 + (LW ? 16 : 0);
-    if (lds > 160 * 1024) {
-        set_error("tp16: %zu bytes of LDS (> 160 KiB)", lds);
-        return NBX_E_UNSUPPORTED;
-    }
-    NBX_TIMED_LAUNCH((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK, LW>), dim3(b0 + b1),
-                     dim3(64 * (WAVES + (LW ? 1 : 0))), lds, st, p0, p1, b0);
+    NBX_LDS_160K((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>));
+    const size_t lds = (size_t)std::max(b0 ? p0.lds_floats : 0, b1 ? p1.lds_floats : 0) * 4;
+    NBX_TIMED_LAUNCH((tp16_kernel<NS, NV, EPI, CG, WAVES, PF, KS, DUAL, SK>), dim3(b0 + b1), dim3(64 * WAVES), lds,
+                     st, p0, p1, b0);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }
 
 // p.chunks = number of 16-channel chunks; grid = ceil(chunks / CG) groups x blocks_per_chunk
-template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, class SK = DynSK,
-          bool LW = false>
+template <int NS, int NV, int EPI, int CG, int WAVES = T16_WAVES, int PF = 3, int KS = 1, class SK = DynSK>
 int tp16_launch(TpProb& p, hipStream_t st, int num_cus = 256) {
     int b = 0;
     if (int rc = tp16_geom<NS, NV, EPI, CG, WAVES, KS>(p, num_cus, &b, SK::PREC)) return rc;
-    return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, false, SK, LW>(p, p, b, 0, st);
+    return tp16_go<NS, NV, EPI, CG, WAVES, PF, KS, false, SK>(p, p, b, 0, st);
 }
 
 // two independent problems in one launch (same template shape)

@@ -85,6 +85,56 @@ __device__ inline float bn_coef(const BnSrc& b, int M, int part, int k, bool own
     return part == 0 ? sc : sh;
 }
 
+// The same arithmetic with the inputs loaded up front: a consumer prologue issues these loads before its
+// weight-image DMA (vmcnt retires in issue order, so loads issued after the DMA would wait for all of
+// it), one evaluation per thread.  kind 0 = channel k's (0e scale, 0e shift) [bn_coef parts 0, 2],
+// kind 1 = its 1o scale [part 1]; the owner (block 0) applies the running-stat update and coef_out.
+struct BnPre {
+    double s0, s1;
+    float w, b, rm, rv;
+};
+__device__ inline BnPre bn_pre_load(const BnSrc& b, int M, int kind, int k) {
+    BnPre p{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
+    if (kind == 0) {
+        if (b.training) { p.s0 = b.sums[k]; p.s1 = b.sums[M + k]; }
+        p.rm = b.rmean[k]; p.rv = b.rvar[k]; p.w = b.weight[k]; p.b = b.bias[k];
+    } else {
+        if (b.training) p.s0 = b.sums[2 * M + k];
+        p.rv = b.rvar[M + k]; p.w = b.weight[M + k];
+    }
+    return p;
+}
+__device__ inline float2 bn_pre_coef(const BnSrc& b, const BnPre& p, int M, int kind, int k, bool owner) {
+    if (kind == 1) {
+        const double n = b.training ? p.s0 / (3.0 * b.count) : (double)p.rv;
+        const float sc = (float)(1.0 / sqrt(n + (double)b.eps)) * p.w;
+        if (owner) {
+            if (b.training && b.update) b.rvar[M + k] = (1.0f - b.momentum) * p.rv + b.momentum * (float)n;
+            if (b.coef_out) b.coef_out[M + k] = sc;
+        }
+        return float2{sc, 0.f};
+    }
+    double mu, var;
+    if (b.training) {
+        mu = p.s0 / b.count;
+        var = p.s1 / b.count - mu * mu;
+        if (var < 0.0) var = 0.0;
+    } else {
+        mu = p.rm;
+        var = p.rv;
+    }
+    const float sc = (float)(1.0 / sqrt(var + (double)b.eps)) * p.w;
+    const float sh = p.b - sc * (float)mu;
+    if (owner) {
+        if (b.training && b.update) {
+            b.rmean[k] = (1.0f - b.momentum) * p.rm + b.momentum * (float)mu;
+            b.rvar[k] = (1.0f - b.momentum) * p.rv + b.momentum * (float)var;
+        }
+        if (b.coef_out) { b.coef_out[k] = sc; b.coef_out[2 * M + k] = sh; }
+    }
+    return float2{sc, sh};
+}
+
 // no-return device-scope fp64 add (executes at the memory side, so adders on every XCD agree)
 __device__ inline void bn_atomic_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
