@@ -709,12 +709,6 @@ bool x3_enabled() {
     return v == 1;
 }
 
-// TEMPORARY A/B (r05): A-ring depth of the fp16x2 node TPs / message kernel (NBX_PF, NBX_MSG_D)
-int env_int(const char* name, int def) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : def;
-}
-
 // Split-precision MFMA path of the SEGNN TPs: 2 = the fp16x2 images (default, when present),
 // 1 = the bf16x3 images, 0 = fp32 MFMA.  NBX_SPLIT=x3 / NBX_X3=0 select 1 / 0 (A/B only).
 int split_prec() {
@@ -768,12 +762,8 @@ int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void*
             const float* fp32_img = p.B;
             p.B = static_cast<const float*>(img_h2);
             p.bscale = h2_descale;
-            if (sk_matches<SK_MSG2_H2>(p, NS, NV)) {
-                static const int d = env_int("NBX_MSG_D", 3);
-                if (d == 4) return run_tp<NS, NV, EPI, 8, 4, SK_MSG2_H2>(p, st, tm);
-                if (d == 5) return run_tp<NS, NV, EPI, 8, 5, SK_MSG2_H2>(p, st, tm);
-                return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_H2>(p, st, tm);
-            }
+            // (A-ring depth 3: 4 and 5 measured no faster, r05 profiles/r05/pf)
+            if (sk_matches<SK_MSG2_H2>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_H2>(p, st, tm);
             if (sk_matches<SK_MSG2_32_H2>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_32_H2>(p, st, tm);
             p.B = fp32_img;
         }
@@ -1153,10 +1143,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if ((M == 96 || M == 32) && L.upd1_img_h2 && split_prec() == 2) {
                 p.B = static_cast<const float*>(L.upd1_img_h2);
                 p.bscale = L.upd1_h2_descale;
-                static const int pf = env_int("NBX_PF", 3);
-                const int rc = M == 96 ? (pf == 5 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 5, 1, SK_UPD1_SEG_H2>(p, st, tm)
-                                          : pf == 7 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 7, 1, SK_UPD1_SEG_H2>(p, st, tm)
-                                                    : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm))
+                // (A-ring depth 3: 5 and 7 measured slower, r05 profiles/r05/pf)
+                const int rc = M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm)
                                        : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
                 if (rc) return rc;
             } else if (M == 96 && L.upd1_img_x3 && split_prec() == 1) {
@@ -1202,10 +1190,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if ((M == 96 || M == 32) && L.upd2_img_h2 && split_prec() == 2 && static_enabled()) {
                 p.B = static_cast<const float*>(L.upd2_img_h2);
                 p.bscale = L.upd2_h2_descale;
-                static const int pf = env_int("NBX_PF", 3);
-                const int rc = M == 96 ? (pf == 5 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 5, 1, SK_UPD2_H2>(p, st, tm)
-                                          : pf == 7 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 7, 1, SK_UPD2_H2>(p, st, tm)
-                                                    : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm))
+                const int rc = M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm)
                                        : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2>(p, st, tm);
                 if (rc) return rc;
             } else {
