@@ -219,8 +219,12 @@ def bench_segnn(a, rank, world, device, P):
     # 2 = fp16x2 images (default), 1 = bf16x3 (NBX_SPLIT=x3), 0 = fp32 MFMA (NBX_X3=0)
     prec = segnn_split_prec()
     sk = {2: "StatSKH2", 1: "StatSKX3", 0: "StatSK"}[prec]
+    # message_layer_2 with the register-formed dot operand (csrc/segnn.hip msg_dv; fp16x2 only)
+    dv = prec == 2 and os.environ.get("NBX_MSG_DV", "")[:1] != "0"
+    msg2 = ("void nbx::tp_fused_kernel<3, 1, 1, 8, 2, nbx::StatSKH2<6, 6, 3, 3, 0, 1> >(nbx::TpProb)" if dv else
+            f"void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::{sk}<6, 6, 3, 3, 0> >(nbx::TpProb)")
     names = [f"void nbx::msg_pre_kernel<{prec}, {3 if prec else 0}>(nbx::MsgPreProb)",
-             f"void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::{sk}<6, 6, 3, 3, 0> >(nbx::TpProb)",
+             msg2,
              f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::{sk}<12, 12, 6, 6, 4> >(nbx::TpProb, "
              "nbx::TpProb, int)",
              f"void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, nbx::{'StatSKH2' if prec == 2 else 'StatSK'}"

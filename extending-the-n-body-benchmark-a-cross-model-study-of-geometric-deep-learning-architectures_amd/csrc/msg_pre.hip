@@ -33,7 +33,10 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
     // through LDS counters instead of a block barrier per stage (DEC): the GEMM waves may run up to
     // two groups ahead of the edge waves, so per-stage jitter of either role is absorbed
     constexpr int NBUF = mp_nbuf(PREC);
-    constexpr bool DEC = NBUF > 2;
+#ifndef NBX_MP_DEC
+#define NBX_MP_DEC 1   // 0: block barriers per stage (A/B builds only)
+#endif
+    constexpr bool DEC = NBX_MP_DEC && NBUF > 2;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = P.img_floats, M = P.M, N = P.N, G = P.G, NG = P.NG;
     constexpr int MP_RS = MpEx<X3>::RS, MP_PART = MpEx<X3>::PART, MP_EX = MpEx<X3>::EX;
@@ -61,6 +64,14 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
     const int lg = __builtin_ctz((unsigned)G);
     const float invN = 1.0f / (float)N;
     const int64_t Ep = P.V * G;
+    // M1S / M1V: 16-B buffer stores, write-through (sc1: the 39 MB edge operand leaves L2 as it is
+    // written, no end-of-kernel write-back; tp_fused.h st_out; r05 A/B +1.1 % steps/s, profiles/r05/wtdv)
+    const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void*)P.M1S, (short)0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)P.M1V, (short)0, 0x7FFFFFF0, 0x00020000);
+    auto st4 = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t off, float4 v) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 16);
+    };
 
     // GEMM waves: A = X[plane][node][k], two float4 per lane per 32-deep chunk (lane quarter qd
     // supplies k = 8 qd + s at MFMA step s), bounds-checked buffer loads (zeros past M / V)
@@ -120,24 +131,36 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
         ba = *reinterpret_cast<const float4*>(P.bias + ch0);
         bg = *reinterpret_cast<const float4*>(P.bias + M + ch0);
     }
-    // DEC hand-off counters: [0] = GEMM-wave group writes completed (4 per group), [1] = edge-wave
-    // group reads completed (4 per group)
+    // DEC hand-off counters, one per wave (the four GEMM waves and the four edge waves are not in lock
+    // step with each other: a sum over the waves could reach a stage's count while one wave is still a
+    // group behind -- r05: that race corrupted a group's edges about once per 100 forwards):
+    // hand[p] = groups GEMM wave p has written, hand[4 + q] = groups edge wave q has read
     int* hand = reinterpret_cast<int*>(XC + 3 * KC * 32);
-    if (DEC && t == 0) { hand[0] = 0; hand[1] = 0; }
+    if (DEC && t < 8) hand[t] = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // relaxed LDS poll (the LDS keeps each wave's operations in order; the empty asm keeps the compiler
-    // from hoisting the exchange reads above it) and no-return LDS add after this wave's LDS traffic
-    // (inline asm: no wait for the wave's global stores)
-    auto dec_wait = [&](int which, int need) {
-        while (__hip_atomic_load(hand + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-            __builtin_amdgcn_s_sleep(1);
+    // relaxed LDS poll until all four counters of a role reach `groups` (the LDS keeps each wave's
+    // operations in order; the empty asm keeps the compiler from hoisting the exchange accesses above
+    // it), and a no-return LDS add to the wave's own counter after its LDS traffic (inline asm: no
+    // wait for the wave's global stores)
+    auto dec_wait = [&](int role, int groups) {
+        const int* h = hand + 4 * role;
+        auto low = [&]() {
+            int m = __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+            for (int w = 1; w < 4; ++w) {
+                const int v = __hip_atomic_load(h + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                m = v < m ? v : m;
+            }
+            return m;
+        };
+        while (low() < groups) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
     };
-    auto dec_signal = [&](int which) {
+    auto dec_signal = [&](int role) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) {
-            const unsigned a = (unsigned)(uintptr_t)(hand + which);
+            const unsigned a = (unsigned)(uintptr_t)(hand + 4 * role + (wave & 3));
             asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1) : "memory");
         }
     };
@@ -164,7 +187,7 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
         floatx4 acc[6];
         auto write_ex = [&](int buf) {
             if constexpr (DEC)   // buffer `buf` free: the edge waves are done with group i - NBUF
-                if (i >= NBUF) dec_wait(1, 4 * (i - NBUF + 1));
+                if (i >= NBUF) dec_wait(1, i - NBUF + 1);
             float* ex = EX + buf * MP_EX + plane * 6 * MP_PART;
 #pragma unroll
             for (int j = 0; j < 6; ++j)
@@ -284,7 +307,7 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
             const float4 geo_cur = geo_next;
             const float pm_cur = pm_next;
             load_geo(i, geo_next, pm_next);
-            if constexpr (DEC) dec_wait(0, 4 * i);   // group i - 1 written by all four GEMM waves
+            if constexpr (DEC) dec_wait(0, i);   // group i - 1 written by all four GEMM waves
             const float* exb = EX + ((i - 1) % NBUF) * MP_EX;
             auto xv = [&](int pl, int part, int row) {
                 const int q = X3 ? cq ^ ((row >> 2) & 3) : cq;
@@ -296,15 +319,15 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
                 const int64_t dn = node0 + ld;
                 if (dn >= P.V) break;
                 const int64_t e = dn * G + q;
-                float4* m1s = reinterpret_cast<float4*>(P.M1S + e * 2 * M + ch0);
-                float4* m1v0 = reinterpret_cast<float4*>(P.M1V + e * M + ch0);
-                float4* m1v1 = reinterpret_cast<float4*>(P.M1V + (Ep + e) * M + ch0);
-                float4* m1v2 = reinterpret_cast<float4*>(P.M1V + (2 * Ep + e) * M + ch0);
+                const uint32_t os = (uint32_t)((e * 2 * M + ch0) * 4), ov = (uint32_t)((e * M + ch0) * 4);
+                const uint32_t opl = (uint32_t)(Ep * M * 4);
                 const int d = ld - N * tp_udiv_small(ld, invN);        // position in the system
                 const int sq = P.slot ? P.slot[e] : (q < N - 1 ? (q < d ? q : q + 1) : -1);
                 if (sq < 0) {   // padding slot
                     const float4 z{0.f, 0.f, 0.f, 0.f};
-                    m1s[0] = z; m1s[M / 4] = z; *m1v0 = z; *m1v1 = z; *m1v2 = z;
+                    st4(rsS, os, z);
+                    if (!P.no_dot) st4(rsS, os + 4 * M, z);
+                    st4(rsV, ov, z); st4(rsV, ov + opl, z); st4(rsV, ov + 2 * opl, z);
                     continue;
                 }
                 const int sl = ld - d + sq;                              // source node, same group
@@ -344,16 +367,16 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
                     o_v2[c] = gg * v[2];
                     o_dot[c] = fmaf(o_v2[c], hk[2], fmaf(o_v1[c], hk[1], o_v0[c] * hk[0]));
                 }
-                *m1v0 = float4{o_v0[0], o_v0[1], o_v0[2], o_v0[3]};
-                *m1v1 = float4{o_v1[0], o_v1[1], o_v1[2], o_v1[3]};
-                *m1v2 = float4{o_v2[0], o_v2[1], o_v2[2], o_v2[3]};
-                m1s[0] = float4{o_ms[0], o_ms[1], o_ms[2], o_ms[3]};
-                m1s[M / 4] = float4{o_dot[0], o_dot[1], o_dot[2], o_dot[3]};
+                st4(rsV, ov, float4{o_v0[0], o_v0[1], o_v0[2], o_v0[3]});
+                st4(rsV, ov + opl, float4{o_v1[0], o_v1[1], o_v1[2], o_v1[3]});
+                st4(rsV, ov + 2 * opl, float4{o_v2[0], o_v2[1], o_v2[2], o_v2[3]});
+                st4(rsS, os, float4{o_ms[0], o_ms[1], o_ms[2], o_ms[3]});
+                if (!P.no_dot) st4(rsS, os + 4 * M, float4{o_dot[0], o_dot[1], o_dot[2], o_dot[3]});
             }
             tick(c_edge);
         }
         if constexpr (DEC) {
-            // (every edge wave signals, dead lanes or not, so the counts stay 4 per group)
+            // (every edge wave signals, dead lanes or not)
             if (!gemm_wave && i > 0) dec_signal(1);
         } else {
             // LDS hand-off only: wait for this wave's LDS traffic, not for its global stores
@@ -372,7 +395,7 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
 
 inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
     return ((size_t)2 * p.img_floats + mp_nbuf(p.prec) * (p.prec ? MpEx<true>::EX : MpEx<false>::EX) +
-            3 * 32 * ((p.M + 31) / 32)) * 4 + 16;   // + the hand-off counters
+            3 * 32 * ((p.M + 31) / 32)) * 4 + 32;   // + the hand-off counters
 }
 
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
@@ -381,8 +404,9 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         set_error("msg_pre: needs mul <= 128 and 2 <= N <= 16 (got mul %d, N %d)", p.M, p.N);
         return NBX_E_UNSUPPORTED;
     }
-    if ((double)4 * p.V * p.M * 4.0 >= 2147483632.0) {
-        set_error("msg_pre: X spans >= 2 GiB (32-bit buffer offsets)");
+    if ((double)4 * p.V * p.M * 4.0 >= 2147483632.0 || (double)3 * p.V * p.G * p.M * 4.0 >= 2147483632.0 ||
+        (double)2 * p.V * p.G * p.M * 4.0 >= 2147483632.0) {
+        set_error("msg_pre: X / M1S / M1V span >= 2 GiB (32-bit buffer offsets)");
         return NBX_E_UNSUPPORTED;
     }
     p.chunks = (p.M + 15) / 16;

@@ -691,12 +691,19 @@ using SK_MSG2_32_X3 = nbx::StatSKX3<2, 2, 1, 1>;
 // fp16x2 split path (include/nbx.h "fp16x2 images")
 using SK_MSG2_H2 = nbx::StatSKH2<6, 6, 3, 3>;
 using SK_MSG2_32_H2 = nbx::StatSKH2<2, 2, 1, 1>;
+using SK_MSG2_H2_DV = nbx::StatSKH2<6, 6, 3, 3, 0, 1>;     // dot half of M1S formed in registers
+using SK_MSG2_32_H2_DV = nbx::StatSKH2<2, 2, 1, 1, 0, 1>;
 using SK_UPD1_SEG_H2 = nbx::StatSKH2<12, 12, 6, 6, 4>;
 using SK_UPD1_32_SEG_H2 = nbx::StatSKH2<4, 4, 2, 2, 4>;
 using SK_UPD2_H2 = nbx::StatSKH2<6, 3, 0, 3>;
 using SK_UPD2_32_H2 = nbx::StatSKH2<2, 1, 0, 1>;
 using SK_PP1_SEG_H2 = nbx::StatSKH2<6, 6, 3, 3, 2>;
 using SK_PP1_32_SEG_H2 = nbx::StatSKH2<2, 2, 1, 1, 2>;
+// (register-formed x_v . na / a_v . na chunks: tp_fused.h TpStream)
+using SK_UPD1_SEG_H2_DV = nbx::StatSKH2<12, 12, 6, 6, 4, 1>;
+using SK_UPD1_32_SEG_H2_DV = nbx::StatSKH2<4, 4, 2, 2, 4, 1>;
+using SK_PP1_SEG_H2_DV = nbx::StatSKH2<6, 6, 3, 3, 2, 1>;
+using SK_PP1_32_SEG_H2_DV = nbx::StatSKH2<2, 2, 1, 1, 2, 1>;
 
 // message_layer_2 on the split-precision MFMA path when the weights carry a bf16x3 image
 // (NBX_X3=0: fp32 MFMA path, A/B only)
@@ -753,10 +760,41 @@ int tp_debug_dump(const nbx::TpProb& p, hipStream_t st, int waves) {
     return NBX_OK;
 }
 
+// message_layer_2 forms the dot half of its scalar operand (M1S [m_s | m_v . rhat]) from M1V in
+// registers (tp_fused.h TpStream, DV) instead of reading it, and msg_pre does not write it: 20 %
+// fewer A bytes per edge.  Requires the fp16x2 static schedule (mul 96 or 32); NBX_MSG_DV=0: the
+// dot half is written and read (A/B only).
+bool msg_dv(int64_t M, int64_t N, bool h2_img) {
+    static const bool on = !(getenv("NBX_MSG_DV") && getenv("NBX_MSG_DV")[0] == '0');
+    return on && h2_img && static_enabled() && split_prec() == 2 && N > 1 && (M == 96 || M == 32);
+}
+
+// update_layer_1 and pre_pool1 form their x_v . na / a_v . na operand chunks from the vector planes
+// in registers (tp_fused.h TpStream, DV), so XD / AD are neither written (update_layer_2, message_layer_2,
+// featurisation) nor read: requires the fp16x2 segmented schedules of every layer (mul 96 or 32);
+// NBX_UPD_DV=0: XD / AD are materialised (A/B only).
+bool upd_dv(const nbx_segnn_weights* w, int64_t M, bool seg_upd) {
+    static const bool on = !(getenv("NBX_UPD_DV") && getenv("NBX_UPD_DV")[0] == '0');
+    if (!on || !seg_upd || split_prec() != 2 || !(M == 96 || M == 32) || !w->pp1_img_h2) return false;
+    for (int l = 0; l < w->num_layers; ++l)
+        if (!w->layers[l].upd1_img_h2) return false;
+    return true;
+}
+
 template <int NS, int NV, int EPI>
 int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3, const void* img_h2,
-                   float h2_descale) {
+                   float h2_descale, bool dv) {
     // message_layer_2 at mul = 96 / 32: fully unrolled static chunk schedule
+    if (dv) {   // (msg_dv: the M1S dot half was not written)
+        if constexpr (EPI == nbx::TP_MSG && NS == 3 && NV == 1) {
+            p.B = static_cast<const float*>(img_h2);
+            p.bscale = h2_descale;
+            if (sk_matches<SK_MSG2_H2_DV>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 2, SK_MSG2_H2_DV>(p, st, tm);
+            if (sk_matches<SK_MSG2_32_H2_DV>(p, NS, NV)) return run_tp<NS, NV, EPI, 8, 3, SK_MSG2_32_H2_DV>(p, st, tm);
+        }
+        nbx::set_error("message_layer_2: no register-dot schedule for this shape");
+        return NBX_E_UNSUPPORTED;
+    }
     if (static_enabled()) {
         if (img_h2 && split_prec() == 2) {
             const float* fp32_img = p.B;
@@ -784,10 +822,10 @@ int run_tp_msg_sel(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void*
 
 template <int NS, int NV, int EPI>
 int run_tp_msg(nbx::TpProb& p, hipStream_t st, KernelTiming* tm, const void* img_x3 = nullptr,
-               const void* img_h2 = nullptr, float h2_descale = 1.f) {
+               const void* img_h2 = nullptr, float h2_descale = 1.f, bool dv = false) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
     if (debug) p.dbg = tp_dbg_buf(st);
-    const int rc = run_tp_msg_sel<NS, NV, EPI>(p, st, tm, img_x3, img_h2, h2_descale);
+    const int rc = run_tp_msg_sel<NS, NV, EPI>(p, st, tm, img_x3, img_h2, h2_descale, dv);
     if (rc || !debug) return rc;
     return tp_debug_dump(p, st, 8);
 }
@@ -954,6 +992,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // (general graphs: the segmented input folds the message BN shift x a constant degree, so
     // they take the materialised path with per-node in-degrees)
     const bool seg_upd = static_enabled() && (M == 96 || M == 32) && !gr;
+    const bool dv_upd = upd_dv(w, M, seg_upd);   // x_v . na / a_v . na formed in registers, XD / AD unused
     const int* slot = gr ? ws.SLOT : nullptr;
     const float* degv = gr ? ws.DEG : nullptr;
     // block: whole multiples of the channel count (192 threads at mul = 96), >= FE_NODES
@@ -1013,7 +1052,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     if (!featurized) {
         hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st,
                            pos, vel, mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
-                           seg_upd ? ws.XD : nullptr, ws.bn_sums, nzero, slot, degv);
+                           seg_upd && !dv_upd ? ws.XD : nullptr, ws.bn_sums, nzero, slot, degv);
         NBX_LAUNCH_CHECK("embed");
     }
 
@@ -1023,10 +1062,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         if (xprev && !fused_msg && N > 1) {
             // the unfused message path reads X directly: normalise it in place first
             hipLaunchKernelGGL(bn_apply_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.coef_feat, V, M,
-                               seg_upd ? ws.XD : nullptr);
+                               seg_upd && !dv_upd ? ws.XD : nullptr);
             NBX_LAUNCH_CHECK("bn_apply");
             xprev = nullptr;
         }
+        const bool msg2_dv = msg_dv(M, N, L.msg2_img_h2 != nullptr);
         if (fused_msg) {
             // message_layer_1: node precomputation + edge combination + gate in one kernel
             nbx::MsgPreProb mp;
@@ -1053,6 +1093,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 mp.Vimg = static_cast<const float*>(L.node_pre_v_img_x3);
                 mp.prec = 1;
             }
+            mp.no_dot = msg2_dv ? 1 : 0;
             if (int rc = run_msg_pre(mp, st, tm)) return rc;
         } else if (N > 1) {
             // systems larger than a 16-row tile: node precomputation (plain GEMM, part-major
@@ -1092,10 +1133,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.bias = L.msg2_bias; p.geom = ws.EG; p.group = (int)d.G;
             p.valid_per_group = gr ? (int)d.G : (int)(N - 1);   // general graphs: padding rows have |rel| < 0
             p.out_s = ws.AGG; p.out_v = ws.AGG + V * M; p.out_plane = V * M; p.partial = ws.partial;
-            if (seg_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
+            if (seg_upd && !dv_upd) { p.na = ws.NA; p.out_dot = ws.AD; }
             if (bn_atomic) p.bn_sums = sums_of(l, 0);
             if (N > 1) {  // 32x32 tiles: edge rows are plentiful, and a tile holds whole destinations
-                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3, L.msg2_img_h2, L.msg2_h2_descale))
+                if (int rc = run_tp_msg<3, 1, nbx::TP_MSG>(p, st, tm, L.msg2_img_x3, L.msg2_img_h2, L.msg2_h2_descale,
+                                                           msg2_dv))
                     return rc;
                 wpc_msg = p.waves_per_chunk;
                 cw_msg = 32;
@@ -1144,8 +1186,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 p.B = static_cast<const float*>(L.upd1_img_h2);
                 p.bscale = L.upd1_h2_descale;
                 // (A-ring depth 3: 5 and 7 measured slower, r05 profiles/r05/pf)
-                const int rc = M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm)
-                                       : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
+                const int rc =
+                    dv_upd ? (M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2_DV>(p, st, tm)
+                                      : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2_DV>(p, st, tm))
+                    : M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm)
+                              : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
                 if (rc) return rc;
             } else if (M == 96 && L.upd1_img_x3 && split_prec() == 1) {
                 p.B = static_cast<const float*>(L.upd1_img_x3);
@@ -1183,7 +1228,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             const bool feat_atomic = bn_atomic;
             if (feat_atomic) p.bn_sums = sums_of(l, 1);
             p.xcoef = xprev;
-            if (seg_upd) { p.out_dot = ws.XD; }
+            if (seg_upd && !dv_upd) { p.out_dot = ws.XD; }
             p.chunks = (M + 15) / 16;
             // update_layer_2: one 16-channel chunk per wave, full K (CG 1, KS 1; r02 measured it against
             // CG 2 / KS 2, CG 1 / KS 2, CG 2 / KS 1, CG 1 / KS 4: 15.1 vs 17.8 / 16.3 / 19.5 / 20.9 us)
@@ -1239,8 +1284,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         if (w->pp1_img_h2 && split_prec() == 2) {
             p.B = static_cast<const float*>(w->pp1_img_h2);
             p.bscale = w->pp1_h2_descale;
-            const int rc = M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2>(p, st, tm)
-                                   : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG_H2>(p, st, tm);
+            const int rc =
+                dv_upd ? (M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2_DV>(p, st, tm)
+                                  : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG_H2_DV>(p, st, tm))
+                : M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2>(p, st, tm)
+                          : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG_H2>(p, st, tm);
             if (rc) return rc;
         } else if (M == 96) {
             if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG>(p, st, tm)) return rc;
@@ -1265,7 +1313,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         const int nb = (int)N * std::max(1, 8 / (int)N);   // whole systems, N <= RPP2_MAX
         hipLaunchKernelGGL(rollout_pp2_kernel, dim3((unsigned)nbx::ceil_div(V, nb)), dim3(64 * nb), 0, st, ws.U2S,
                            ws.U2V, ws.NA, w->pp2, V, M, out, *upd, nb, mass, (int)N, (int)d.G, w->emb, w->emb_bias,
-                           ws.EG, ws.X, seg_upd ? ws.XD : nullptr, ws.bn_sums, nzero);
+                           ws.EG, ws.X, seg_upd && !dv_upd ? ws.XD : nullptr, ws.bn_sums, nzero);
         NBX_LAUNCH_CHECK("pre_pool2 + next featurise");
         return NBX_OK;
     }

@@ -139,12 +139,21 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
             if (slice == decltype(sc_)::value) fn(sc_);
         });
     };
+    // DV (TpStream): the scalar operand's trailing dot chunks are formed from the vector chunks, not
+    // loaded; loads run in TpStream load order (the item order unless DV)
+    using TS = TpStream<SK>;
+    static_assert(!SK::DV || (KS == 1 && SK::SEG > 0 && NV == 1 && SK::PREC >= 1), "DV: segmented split-precision input");
+    constexpr int NLD = TS::NLOAD;   // DV loads (KS = 1)
     if constexpr (SK::on) {
         slice_call([&](auto sc_) {
             constexpr int lo = decltype(sc_)::value * SNIT / KS, hi = (decltype(sc_)::value + 1) * SNIT / KS;
             static_for<0, PF - 1>([&](auto uc) {
                 constexpr int u = decltype(uc)::value;
-                if constexpr (lo + u < hi) load_item(std::integral_constant<int, lo + u>{}, rt, ring[u % PF]);
+                if constexpr (SK::DV) {
+                    if constexpr (u < NLD) load_item(std::integral_constant<int, TS::item(TS::lpos(u))>{}, rt, ring[u % PF]);
+                } else if constexpr (lo + u < hi) {
+                    load_item(std::integral_constant<int, lo + u>{}, rt, ring[u % PF]);
+                }
             });
         });
     } else {
@@ -442,20 +451,46 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                     // SrcA only (a load over an MFMA's SrcB at 0 wait states is safe, tools/hazard), and
                     // the 36 VGPRs saved hold the deeper A ring
                     constexpr int NBS = PF > 3 ? 2 : 3;
+                    // DV: the node attributes of this lane's row (the dot weights) and the dot chunk being formed
+                    float yv[3] = {0.f, 0.f, 0.f};
+                    float dacc[8];
+                    if constexpr (SK::DV) {
+                        const int row = rt * 16 + c16;
+                        if (row < P.rows) {
+                            yv[0] = P.geom[(size_t)row * 4 + 1]; yv[1] = P.geom[(size_t)row * 4 + 2];
+                            yv[2] = P.geom[(size_t)row * 4 + 3];
+                        }
+                    }
                     slice_call([&](auto sc_) {
+                        // positions lo .. lo + n - 1 of the slice (TpStream; = items unless DV, where KS = 1)
                         constexpr int lo = decltype(sc_)::value * SNIT / KS;
                         constexpr int n = (decltype(sc_)::value + 1) * SNIT / KS - lo;
-                        SPT bx[NBS][CG][NS > 1 ? NS : 1][NP];   // item u in set u % NBS
+                        constexpr int nld = SK::DV ? TS::NLOAD : n;   // loads of the slice
+                        SPT bx[NBS][CG][NS > 1 ? NS : 1][NP];   // position u in set u % NBS
                         SPT ax[3][NP];
-                        read_b(std::integral_constant<int, lo>{}, bx[0]);
+                        read_b(std::integral_constant<int, TS::item(lo)>{}, bx[0]);
                         static_for<0, n>([&](auto uc) {
-                            constexpr int u = decltype(uc)::value, item = lo + u;
-                            if constexpr (u + PF - 1 < n)
-                                load_item(std::integral_constant<int, item + PF - 1>{}, rt, ring[(u + PF - 1) % PF]);
+                            constexpr int u = decltype(uc)::value, pos = lo + u, item = TS::item(pos);
+                            constexpr bool der = TS::derived(pos);
+                            constexpr int l = der ? 0 : TS::lidx(pos) - TS::lidx(lo);   // load index in the slice
+                            if constexpr (!der && l + PF - 1 < nld)
+                                load_item(std::integral_constant<int, TS::item(TS::lpos(TS::lidx(lo) + l + PF - 1))>{}, rt,
+                                          ring[(l + PF - 1) % PF]);
                             __builtin_amdgcn_sched_barrier(0);
-                            if constexpr (u + 1 < n) read_b(std::integral_constant<int, item + 1>{}, bx[(u + 1) % NBS]);
+                            if constexpr (u + 1 < n) read_b(std::integral_constant<int, TS::item(pos + 1)>{}, bx[(u + 1) % NBS]);
                             float av[8];
-                            item_a(std::integral_constant<int, item>{}, ring[u % PF], av);
+                            if constexpr (der) {
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) av[e] = dacc[e];
+                            } else {
+                                item_a(std::integral_constant<int, item>{}, ring[l % PF], av);
+                                if constexpr (SK::DV && TS::plane(pos) >= 0) {
+                                    constexpr int pl = TS::plane(pos);
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e)
+                                        dacc[e] = pl == 0 ? av[e] * yv[0] : __builtin_fmaf(av[e], yv[pl], dacc[e]);
+                                }
+                            }
                             SP::split(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]}, ax[u % 3]);
                             const SPT (&b)[CG][NS > 1 ? NS : 1][NP] = bx[u % NBS];
                             const SPT (&a)[NP] = ax[u % 3];
@@ -486,9 +521,9 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                                     }
                                 }
                             }
-                            // item u-1's operands may be reused from here on
+                            // position u-1's operands may be reused from here on
                             if constexpr (u > 0) {
-                                constexpr int pu = (u + 2) % 3, pitem = item - 1;   // item u-1's set
+                                constexpr int pu = (u + 2) % 3, pitem = TS::item(pos - 1);   // position u-1's set
                                 constexpr int PNA = pitem < SK::K0 ? 1 + (NS > 1 && pitem < SK::K1 ? 1 : 0) +
                                                                          (NS > 2 && pitem < SK::K2 ? 1 : 0)
                                                                    : 1;
@@ -511,7 +546,9 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         asm volatile("s_nop 0" ::: "memory");
                         static_for<0, PF - 1>([&](auto uc) {
                             constexpr int u = decltype(uc)::value;
-                            if constexpr (u < n) load_item(std::integral_constant<int, lo + u>{}, next_rt, ring[u % PF]);
+                            if constexpr (u < nld)
+                                load_item(std::integral_constant<int, TS::item(TS::lpos(TS::lidx(lo) + u))>{}, next_rt,
+                                          ring[u % PF]);
                         });
                     });
                     if constexpr (CG == 1 && NV)
@@ -604,7 +641,7 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         if (pm ? ch < M : col < P.ncols)
 #pragma unroll
                             for (int jj = 0; jj < 4; ++jj)
-                                if (row0 + jj < P.rows) P.C[(size_t)(row0 + jj) * P.ldc + col] = acc[g][j][jj];
+                                if (row0 + jj < P.rows) st_out<false>(&P.C[(size_t)(row0 + jj) * P.ldc + col], acc[g][j][jj]);
                     }
                 } else if constexpr (EPI == TP_MSG) {
                     const bool live = ch < M;
@@ -632,10 +669,10 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                     auto put = [&](int row, float a0, float a1, float a2, float a3) {
                         if (live && row < P.rows) {
                             const size_t o = (size_t)(row >> lg) * M + ch;
-                            P.out_s[o] = a0;
-                            P.out_v[o] = a1;
-                            P.out_v[P.out_plane + o] = a2;
-                            P.out_v[2 * P.out_plane + o] = a3;
+                            st_out<false>(&P.out_s[o], a0);
+                            st_out<false>(&P.out_v[o], a1);
+                            st_out<false>(&P.out_v[P.out_plane + o], a2);
+                            st_out<false>(&P.out_v[2 * P.out_plane + o], a3);
                         }
                     };
                     if (G <= 4) {
@@ -675,11 +712,11 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         const float h0 = gg * (na[1] * tt + acc[g][NS + 0][jj]);
                         const float h1 = gg * (na[2] * tt + acc[g][NS + 1][jj]);
                         const float h2 = gg * (na[3] * tt + acc[g][NS + 2][jj]);
-                        P.out_s[(size_t)row * 2 * M + ch] = hs;
-                        P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
-                        P.out_v[(size_t)row * M + ch] = h0;
-                        P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
-                        P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
+                        st_out<false>(&P.out_s[(size_t)row * 2 * M + ch], hs);
+                        st_out<false>(&P.out_s[(size_t)row * 2 * M + M + ch], h0 * na[1] + h1 * na[2] + h2 * na[3]);
+                        st_out<false>(&P.out_v[(size_t)row * M + ch], h0);
+                        st_out<false>(&P.out_v[P.out_plane + (size_t)row * M + ch], h1);
+                        st_out<false>(&P.out_v[2 * P.out_plane + (size_t)row * M + ch], h2);
                     }
                 } else if constexpr (EPI == TP_RESID) {
                     const bool live = ch < M;
@@ -696,15 +733,15 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         const float tt = acc[g][1][jj];
                         float* xs = P.out_s + (size_t)row * M + ch;
                         const float s = fmaf(xs_sc, rres[g][jj][0], xs_sh) + (acc[g][0][jj] + b);
-                        *xs = s;
+                        st_out<true>(xs, s);
                         float* x0 = P.out_v + (size_t)row * M + ch;
                         float* x1 = x0 + P.out_plane;
                         float* x2 = x1 + P.out_plane;
                         const float v0 = xv_sc * rres[g][jj][1] + (na[1] * tt + acc[g][NS + 0][jj]);
                         const float v1 = xv_sc * rres[g][jj][2] + (na[2] * tt + acc[g][NS + 1][jj]);
                         const float v2 = xv_sc * rres[g][jj][3] + (na[3] * tt + acc[g][NS + 2][jj]);
-                        if (P.out_dot) P.out_dot[(size_t)row * M + ch] = v0 * na[1] + v1 * na[2] + v2 * na[3];
-                        *x0 = v0; *x1 = v1; *x2 = v2;
+                        if (P.out_dot) st_out<true>(&P.out_dot[(size_t)row * M + ch], v0 * na[1] + v1 * na[2] + v2 * na[3]);
+                        st_out<true>(x0, v0); st_out<true>(x1, v1); st_out<true>(x2, v2);
                         st0[g] += (double)s;
                         st1[g] += (double)s * s;
                         st2[g] += (double)v0 * v0 + (double)v1 * v1 + (double)v2 * v2;

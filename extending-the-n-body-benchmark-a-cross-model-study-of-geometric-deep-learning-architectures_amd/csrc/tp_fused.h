@@ -18,6 +18,7 @@
 // consecutive k (lane half h supplies k = 16h + s at MFMA step s for both
 // operands: the sum is unchanged).
 #pragma once
+#include <cstdlib>
 #include <type_traits>
 
 #include "nbx_internal.h"
@@ -140,6 +141,20 @@ __device__ inline void bn_atomic_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Epilogue output stores.  WT: write-through (an agent-scope relaxed store = global_store ... sc1),
+// so the line leaves the XCD's L2 as the epilogue writes it and the kernel ends without dirty lines
+// for the end-of-kernel L2 write-back (MI355X_MICROARCH.md price list, row 'boundary': + B / 6 TB/s
+// for B dirty bytes).  Used where a wave instruction stores whole 128-B rows (message_layer_2's
+// aggregated messages: 32 lanes x 4 B) and for update_layer_2's residual update; tp16's gate
+// epilogue (16 lanes x 4 B = 64-B pieces) keeps plain stores: sc1 made it slower (one fabric write
+// per piece).  r05 A/B on one box: msg2 21.3 -> 20.0 us, upd2 12.3 -> 12.0, upd1 19.1 -> 19.7
+// (profiles/r05/wtdv).
+template <bool WT>
+__device__ inline void st_out(float* p, float v) {
+    if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 struct TpProb {
     // scalar part: NS sub-tiles, sub-tile j contracts the first K_j columns of A
     const float* As;   // [rows][lda_s]
@@ -230,12 +245,12 @@ constexpr int TP_WAVES = 8, TP_THREADS = 64 * TP_WAVES;
 // accumulator copies at control-flow merges (the dynamic loop pays ~50 v_mov per chunk for them).
 struct DynSK {
     static constexpr bool on = false;
-    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0, SEG = 0, PREC = 0;
+    static constexpr int K0 = 0, K1 = 0, K2 = 0, KV = 0, SEG = 0, PREC = 0, DV = 0;
 };
 template <int A, int B, int C, int V, int S = 0>
 struct StatSK {
     static constexpr bool on = true;
-    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 0;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 0, DV = 0;
 };
 
 // StatSK with the split-precision MFMA path (include/nbx.h "bf16x3 images"): A and B are split
@@ -245,7 +260,7 @@ struct StatSK {
 template <int A, int B, int C, int V, int S = 0>
 struct StatSKX3 {
     static constexpr bool on = true;
-    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 1;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 1, DV = 0;
 };
 
 // x = hi + mid + lo (+ <= 2^-27 |x|), each part bf16: RNE conversions (v_cvt_pk_bf16_f32, two
@@ -286,10 +301,42 @@ __device__ inline void tp_split3(const float4& a, const float4& b, bf16x8& hi, b
 // v_mfma_f32_{16x16x32,32x32x16}_f16: half the MFMAs, two thirds of the operand bytes and of the
 // split VALU of bf16x3.  Representation error <= ~2^-22 |a||b| per product (rms 7.6e-8 relative
 // on a K = 192..384 GEMM), below the fp32 accumulation error of the same GEMM.
-template <int A, int B, int C, int V, int S = 0>
+// D = 1 (TpStream): the scalar A's trailing dot chunks are formed in registers from the vector
+// planes instead of being read.
+template <int A, int B, int C, int V, int S = 0, int D = 0>
 struct StatSKH2 {
     static constexpr bool on = true;
-    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 2;
+    static constexpr int K0 = A, K1 = B, K2 = C, KV = V, SEG = S, PREC = 2, DV = D;
+};
+
+// Position stream of the static split-precision K loop.  Without DV: position u = item u (scalar
+// chunk u < K0, then vector chunk K0 + plane * KV + kc), every item loaded, in order.  With DV the
+// scalar operand ends in KV dot chunks (chunk ND + kc = sum_p y_p v_p of vector chunk kc, ND = K0 - KV):
+//   message_layer_2: [m_s | m_v . rhat] (ND = KV), update_layer_1: [x_s | a_s | x_v . na | a_v . na]
+//   (ND = KV = 6), pre_pool1: [x_s | x_v . na] (ND = KV = 3);
+// the dot chunks are not loaded but formed in registers from the three vector chunks of the same
+// channels (fmaf(v2, y2, fmaf(v1, y1, v0 * y0)), the chain their producers evaluate), so positions run
+// the ND scalar chunks, then per kc: vec(0, kc), vec(1, kc), vec(2, kc), dot(kc) -- 20 % fewer A bytes.
+template <class SK>
+struct TpStream {
+    static constexpr int KV = SK::KV, ND = SK::K0 - SK::KV;
+    static constexpr int NPOS = SK::K0 + 3 * SK::KV;
+    static constexpr int NLOAD = SK::DV ? NPOS - SK::KV : NPOS;
+    static constexpr bool derived(int u) { return SK::DV && u >= ND && (u - ND) % 4 == 3; }
+    // logical item of position u (a dot position: its scalar chunk ND + kc)
+    static constexpr int item(int u) {
+        if (!SK::DV || u < ND) return u;
+        const int w = u - ND, kc = w / 4, s = w % 4;
+        return s < 3 ? SK::K0 + s * KV + kc : ND + kc;
+    }
+    // load index of a loaded position, and the position of load index l
+    static constexpr int lidx(int u) { return (!SK::DV || u < ND) ? u : ND + (u - ND) / 4 * 3 + (u - ND) % 4; }
+    static constexpr int lpos(int l) { return (!SK::DV || l < ND) ? l : ND + (l - ND) / 3 * 4 + (l - ND) % 3; }
+    // vector plane of position u (-1: not a vector chunk)
+    static constexpr int plane(int u) {
+        const int it = item(u);
+        return (derived(u) || it < SK::K0) ? -1 : (it - SK::K0) / KV;
+    }
 };
 
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
@@ -394,6 +441,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     int off[NS + 1];
     tp_img_offsets<NS>(P, 32, off);
     static_assert(SK::PREC == 0 || SK::on, "split-precision path needs a static schedule");
+    static_assert(!SK::DV || (SK::PREC >= 1 && EPI == TP_MSG && NS == 3 && NV == 1 && SK::K0 == 2 * SK::KV &&
+                              SK::K1 == 2 * SK::KV && SK::K2 == SK::KV),
+                  "DV: message_layer_2's [m_s | m_v . rhat] scalar operand only");
     using SP = SplitP<SK::PREC>;
     using SPT = typename SP::T;
     constexpr int XBLK = SP::NP * 128;   // split parts x (m 2) x 64 lanes per 32-deep block (PREC 1: 384)
@@ -468,8 +518,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
     };
     if constexpr (SK::on) {
         static_for<0, D - 1>([&](auto uc) {
-            constexpr int u = decltype(uc)::value;
-            if constexpr (u < SNIT) load_item(std::integral_constant<int, u>{}, rt, buf[u % D]);
+            constexpr int u = decltype(uc)::value;   // load index (TpStream; = the item unless DV)
+            if constexpr (u < TpStream<SK>::NLOAD)
+                load_item(std::integral_constant<int, TpStream<SK>::item(TpStream<SK>::lpos(u))>{}, rt, buf[u % D]);
         });
     } else {
 #pragma unroll
@@ -607,32 +658,69 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                 }
             };
             if constexpr (SK::PREC >= 1) {
-                // the split of item u + 1 runs in the shadow of item u's MFMAs (no barrier between them)
+                // positions of the A stream (TpStream: with DV the dot chunks are formed, not loaded);
+                // the split of position u + 1 runs in the shadow of position u's MFMAs (no barrier
+                // between them)
+                using TS = TpStream<SK>;
+                float4 rh = make_float4(0.f, 0.f, 0.f, 0.f);   // DV: rhat of this lane's row
+                float4 dacc[4];                                 // DV: the dot chunk being formed
+                if constexpr (SK::DV) {
+                    const int grow = rt * 32 + r;
+                    if (grow < P.rows) rh = *reinterpret_cast<const float4*>(P.geom + (size_t)grow * 8);
+                }
+                auto dot_acc = [&](auto pc, const float4 (&cur)[4]) {
+                    constexpr int pl = decltype(pc)::value;
+                    const float rk = pl == 0 ? rh.x : pl == 1 ? rh.y : rh.z;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if constexpr (pl == 0) {
+                            dacc[q] = make_float4(cur[q].x * rk, cur[q].y * rk, cur[q].z * rk, cur[q].w * rk);
+                        } else {
+                            dacc[q] = make_float4(__builtin_fmaf(cur[q].x, rk, dacc[q].x), __builtin_fmaf(cur[q].y, rk, dacc[q].y),
+                                                  __builtin_fmaf(cur[q].z, rk, dacc[q].z), __builtin_fmaf(cur[q].w, rk, dacc[q].w));
+                        }
+                    }
+                };
+                auto pin4 = [&](float4 (&x)[4]) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        floatx4 v = __builtin_bit_cast(floatx4, x[q]);
+                        asm volatile("" : "+v"(v));
+                        x[q] = __builtin_bit_cast(float4, v);
+                    }
+                };
                 SPT ax[2][SP::NP][2];
-                split_item(buf[0], ax[0]);
-                static_for<0, SNIT>([&](auto uc) {
+                split_item(buf[0], ax[0]);   // position 0 = load 0 (a scalar chunk)
+                static_for<0, TS::NPOS>([&](auto uc) {
                     constexpr int u = decltype(uc)::value;
-                    if constexpr (u + D - 1 < SNIT)
-                        load_item(std::integral_constant<int, u + D - 1>{}, rt, buf[(u + D - 1) % D]);
+                    if constexpr (!TS::derived(u)) {
+                        constexpr int l = TS::lidx(u);
+                        if constexpr (l + D - 1 < TS::NLOAD)
+                            load_item(std::integral_constant<int, TS::item(TS::lpos(l + D - 1))>{}, rt, buf[(l + D - 1) % D]);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
-                    mma_item_x3(std::integral_constant<int, u>{}, ax[u % 2]);
-                    if constexpr (u + 1 < SNIT) {
+                    mma_item_x3(std::integral_constant<int, TS::item(u)>{}, ax[u % 2]);
+                    if constexpr (u + 1 < TS::NPOS) {
                         // pin the split below the barrier (its pure arithmetic would otherwise be
                         // hoisted into the previous region by instruction selection)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            floatx4 v = __builtin_bit_cast(floatx4, buf[(u + 1) % D][q]);
-                            asm volatile("" : "+v"(v));
-                            buf[(u + 1) % D][q] = __builtin_bit_cast(float4, v);
+                        if constexpr (TS::derived(u + 1)) {
+                            pin4(dacc);
+                            split_item(dacc, ax[(u + 1) % 2]);
+                        } else {
+                            constexpr int l1 = TS::lidx(u + 1);
+                            pin4(buf[l1 % D]);
+                            if constexpr (SK::DV && TS::plane(u + 1) >= 0)
+                                dot_acc(std::integral_constant<int, TS::plane(u + 1)>{}, buf[l1 % D]);
+                            split_item(buf[l1 % D], ax[(u + 1) % 2]);
                         }
-                        split_item(buf[(u + 1) % D], ax[(u + 1) % 2]);
                         // ... and its results above the next barrier (else they sink into the next block)
 #pragma unroll
                         for (int p3 = 0; p3 < SP::NP; ++p3)
 #pragma unroll
                             for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(ax[(u + 1) % 2][p3][m]));
                         // spread the split's VALU over the MFMA gaps (<= ~5 per gap hide, MI355X_MICROARCH)
-                        constexpr int nsub = u < SK::K0 ? (u < SK::K2) + (u < SK::K1) + 1 : 1;
+                        constexpr int it = TS::item(u);
+                        constexpr int nsub = it < SK::K0 ? (it < SK::K2) + (it < SK::K1) + 1 : 1;
                         constexpr int nm = 2 * SP::NT * nsub;
                         constexpr int per = ((SK::PREC == 1 ? 120 : 64) + nm - 1) / nm;
                         static_for<0, nm>([&](auto) {
@@ -643,8 +731,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     __builtin_amdgcn_sched_barrier(0);
                 });
                 static_for<0, D - 1>([&](auto uc) {
-                    constexpr int u = decltype(uc)::value;
-                    if constexpr (u < SNIT) load_item(std::integral_constant<int, u>{}, next_rt, buf[u % D]);
+                    constexpr int l = decltype(uc)::value;
+                    if constexpr (l < TS::NLOAD)
+                        load_item(std::integral_constant<int, TS::item(TS::lpos(l))>{}, next_rt, buf[l % D]);
                 });
             } else if constexpr (SK::on) {
                 static_for<0, SNIT>([&](auto uc) {
@@ -691,7 +780,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
 #pragma unroll
                         for (int e = 0; e < 16; ++e) {
                             const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                            if (row < P.rows) P.C[(size_t)row * P.ldc + col] = acc[j][e];
+                            if (row < P.rows) st_out<false>(&P.C[(size_t)row * P.ldc + col], acc[j][e]);
                         }
                     }
                 }
@@ -731,13 +820,13 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                 auto put = [&](int row, float a0, float a1, float a2, float a3) {
                     if (live && row < P.rows) {
                         const size_t o = (size_t)(row >> lg) * M + ch;
-                        P.out_s[o] = a0;
-                        P.out_v[o] = a1;
-                        P.out_v[P.out_plane + o] = a2;
-                        P.out_v[2 * P.out_plane + o] = a3;
+                        st_out<true>(&P.out_s[o], a0);
+                        st_out<true>(&P.out_v[o], a1);
+                        st_out<true>(&P.out_v[P.out_plane + o], a2);
+                        st_out<true>(&P.out_v[2 * P.out_plane + o], a3);
                         if (P.out_dot) {
                             const float4 na4 = gn[(row - row0) >> lg];
-                            P.out_dot[o] = a1 * na4.y + a2 * na4.z + a3 * na4.w;
+                            st_out<true>(&P.out_dot[o], a1 * na4.y + a2 * na4.z + a3 * na4.w);
                         }
                     }
                 };
@@ -798,11 +887,11 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     const float h0 = gg * (na[1] * tt + acc[NS + 0][e]);
                     const float h1 = gg * (na[2] * tt + acc[NS + 1][e]);
                     const float h2 = gg * (na[3] * tt + acc[NS + 2][e]);
-                    P.out_s[(size_t)row * 2 * M + ch] = hs;
-                    P.out_s[(size_t)row * 2 * M + M + ch] = h0 * na[1] + h1 * na[2] + h2 * na[3];
-                    P.out_v[(size_t)row * M + ch] = h0;
-                    P.out_v[P.out_plane + (size_t)row * M + ch] = h1;
-                    P.out_v[2 * P.out_plane + (size_t)row * M + ch] = h2;
+                    st_out<false>(&P.out_s[(size_t)row * 2 * M + ch], hs);
+                    st_out<false>(&P.out_s[(size_t)row * 2 * M + M + ch], h0 * na[1] + h1 * na[2] + h2 * na[3]);
+                    st_out<false>(&P.out_v[(size_t)row * M + ch], h0);
+                    st_out<false>(&P.out_v[P.out_plane + (size_t)row * M + ch], h1);
+                    st_out<false>(&P.out_v[2 * P.out_plane + (size_t)row * M + ch], h2);
                 }
             } else if constexpr (EPI == TP_RESID) {
                 // rows are nodes: x += update (update_layer_2 output), BN partial sums of the new x
@@ -817,14 +906,14 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                     const float tt = acc[1][e];
                     float* xs = P.out_s + (size_t)row * M + ch;
                     const float s = *xs + (acc[0][e] + b);
-                    *xs = s;
+                    st_out<false>(xs, s);
                     float* x0 = P.out_v + (size_t)row * M + ch;
                     float* x1 = x0 + P.out_plane;
                     float* x2 = x1 + P.out_plane;
                     const float v0 = *x0 + (na[1] * tt + acc[NS + 0][e]);
                     const float v1 = *x1 + (na[2] * tt + acc[NS + 1][e]);
                     const float v2 = *x2 + (na[3] * tt + acc[NS + 2][e]);
-                    *x0 = v0; *x1 = v1; *x2 = v2;
+                    st_out<false>(x0, v0); st_out<false>(x1, v1); st_out<false>(x2, v2);
                     st0 += (double)s;
                     st1 += (double)s * s;
                     st2 += (double)v0 * v0 + (double)v1 * v1 + (double)v2 * v2;

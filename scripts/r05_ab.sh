@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 A/B of the current build: SEGNN + rollout GPU tests, then the C2 bench with the default
 # settings and with each listed environment setting, interleaved, two rounds.
-# usage: bash scripts/r05_ab.sh <tag> "NBX_X=0" ["NBX_Y=1" ...]
+# usage: bash scripts/r05_ab.sh <tag> "NBX_X=0" ["NBX_Y=1 NBX_LIB=<pkg>/lib/libnbx_<build tag>.so" ...]
 set -o pipefail
 O=gpurun_out/r05/${1:-ab}
 shift
@@ -12,7 +12,7 @@ echo "tests: $(grep -c PASSED $O/tests.log) passed, $(grep -c FAILED $O/tests.lo
 grep -q "core dumped\|Segmentation fault\|HSA_STATUS_ERROR\|Memory access fault" $O/tests.log && { echo "GPU fault"; exit 1; }
 for r in 1 2; do
   for v in "" "$@"; do
-    tag=${v:-base}; tag=${tag//=/_}
+    tag=${v:-base}; tag=$(echo "$tag" | sed "s#[^ ]*/lib/libnbx_##; s#\.so##" | tr -c "A-Za-z0-9_\n" "_")
     env $v timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench_${tag}_$r.json 2> $O/bench_${tag}_$r.err || exit 1
   done
 done

@@ -1,0 +1,62 @@
+"""Diagnosis: stale reads between SEGNN C2 forwards in eval mode (no atomics on the result path):
+calls alternate a batch and a permutation of its systems, and each result must equal the permuted
+previous one bit for bit; one spawned child per path setting."""
+import multiprocessing as mp
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+REPS = int(os.environ.get("RACE_REPS", "60"))
+FIRST = os.environ.get("RACE_FIRST") == "1"   # first-call check: call 0 vs call 2 (same input)
+
+
+def child(env, q):
+    os.environ.update(env)
+    import numpy as np
+    import torch
+    import test_gpu_segnn as T
+    dev = torch.device("cuda:0")
+    model = T.make_model(192, 6, dev, perturb_bn=False).eval()
+    B, N = 1024, 5
+    pos, vel, mass = T.states(B, N, seed=4)
+    perm = np.random.default_rng(0).permutation(B)
+    idx = (perm[:, None] * N + np.arange(N)).reshape(-1)
+    # alternate the batch and a permutation of it: eval-mode outputs are per system, so every call
+    # must equal the permutation of the previous one; a read of the previous call's stale data
+    # shows up as a difference on the systems it touches
+    prev, bad = None, []
+    for r in range(REPS):
+        odd = r % 2 == 1
+        got = T.gpu_forward(model, pos[idx] if odd else pos, vel[idx] if odd else vel, mass, B, N, dev)
+        if prev is not None:
+            want = prev[idx] if odd else None
+            if not odd:   # got (natural order) vs the previous permuted result mapped back
+                want = np.empty_like(prev)
+                want[idx] = prev
+            if FIRST and r == 2:
+                want = first
+            d = np.abs(got - want)
+            if d.max() > 0:
+                rows = np.unique(np.argwhere(d > 0)[:, 0] // N)
+                bad.append((r, float(d.max()), rows[:6].tolist(), len(rows)))
+        if r == 0:
+            first = got
+        prev = got
+    q.put(bad)
+
+
+if __name__ == "__main__":
+    envs = [dict(kv.split("=") for kv in a.split(",")) if a else {} for a in sys.argv[1:]] or [{}]
+    ctx = mp.get_context("spawn")
+    for env in envs:
+        q = ctx.Queue()
+        p = ctx.Process(target=child, args=(env, q))
+        p.start()
+        bad = q.get(timeout=500)
+        p.join(timeout=60)
+        tag = {k: os.path.basename(v) for k, v in env.items()} or "default"
+        print(f"{tag}: {len(bad)} of {REPS - 1} calls differ from the permuted previous call" +
+              "".join(f"\n   rerun {r}: max diff {d:.3e}, systems {rows} ({n} systems)" for r, d, rows, n in bad[:5]),
+              flush=True)
