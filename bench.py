@@ -219,16 +219,23 @@ def bench_segnn(a, rank, world, device, P):
     # 2 = fp16x2 images (default), 1 = bf16x3 (NBX_SPLIT=x3), 0 = fp32 MFMA (NBX_X3=0)
     prec = segnn_split_prec()
     sk = {2: "StatSKH2", 1: "StatSKX3", 0: "StatSK"}[prec]
-    # message_layer_2 with the register-formed dot operand (csrc/segnn.hip msg_dv; fp16x2 only)
+    # register-formed dot operands (csrc/segnn.hip msg_dv / upd_dv; fp16x2 only): the schedule types'
+    # last parameter
     dv = prec == 2 and os.environ.get("NBX_MSG_DV", "")[:1] != "0"
-    msg2 = ("void nbx::tp_fused_kernel<3, 1, 1, 8, 2, nbx::StatSKH2<6, 6, 3, 3, 0, 1> >(nbx::TpProb)" if dv else
-            f"void nbx::tp_fused_kernel<3, 1, 1, 8, 3, nbx::{sk}<6, 6, 3, 3, 0> >(nbx::TpProb)")
+    udv = prec == 2 and os.environ.get("NBX_UPD_DV", "")[:1] != "0"
+
+    def sk_name(shape, d=0):
+        """demangled schedule type: StatSKH2 carries the DV flag as a sixth parameter"""
+        return f"nbx::StatSKH2<{shape}, {d}>" if prec == 2 else f"nbx::{sk}<{shape}>"
+
+    msg2 = (f"void nbx::tp_fused_kernel<3, 1, 1, 8, {2 if dv else 3}, {sk_name('6, 6, 3, 3, 0', int(dv))} >"
+            "(nbx::TpProb)")
     names = [f"void nbx::msg_pre_kernel<{prec}, {3 if prec else 0}>(nbx::MsgPreProb)",
              msg2,
-             f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::{sk}<12, 12, 6, 6, 4> >(nbx::TpProb, "
+             f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, {sk_name('12, 12, 6, 6, 4', int(udv))} >(nbx::TpProb, "
              "nbx::TpProb, int)",
-             f"void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, nbx::{'StatSKH2' if prec == 2 else 'StatSK'}"
-             "<6, 3, 0, 3, 0> >(nbx::TpProb, nbx::TpProb, int)"]
+             f"void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, "
+             f"{sk_name('6, 3, 0, 3, 0') if prec == 2 else 'nbx::StatSK<6, 3, 0, 3, 0>'} >(nbx::TpProb, nbx::TpProb, int)"]
     x3 = prec != 0
     roles = ["message_layer_1: node GEMM + edge combination + gate (flops: the node GEMM)",
              "message_layer_2 + gate + aggregation + BN sums",
@@ -252,8 +259,8 @@ def bench_segnn(a, rank, world, device, P):
     # the rocprof duration of the dominant kernel (the same run family as the PMC bytes) and the
     # per-step HBM bytes of the whole step (report the MFMA and the HBM fractions)
     rp_us, rp_src = rocprof_avg_us(names[dom], "segnn")
-    pp1 = (f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, nbx::{'StatSKH2' if prec == 2 else 'StatSK'}"
-           "<6, 6, 3, 3, 2> >(nbx::TpProb, nbx::TpProb, int)")
+    pp1 = (f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, "
+           f"{sk_name('6, 6, 3, 3, 2', int(udv)) if prec == 2 else 'nbx::StatSK<6, 6, 3, 3, 2>'} >(nbx::TpProb, nbx::TpProb, int)")
     step_k = [(nm, LAYERS) for nm in names] + [(pp1, 1), ("(anonymous namespace)::rollout_pp2_kernel(", 1)]
     bps, bps_src = step_bytes("segnn", step_k)
     hbm = {"avg_launch_us_rocprof": rp_us, "rocprof_source": rp_src,
