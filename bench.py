@@ -235,7 +235,7 @@ def bench_segnn(a, rank, world, device, P):
              f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, {sk_name('12, 12, 6, 6, 4', int(udv))} >(nbx::TpProb, "
              "nbx::TpProb, int)",
              f"void nbx::tp16_kernel<2, 1, 3, 1, 8, 3, 1, false, "
-             f"{sk_name('6, 3, 0, 3, 0') if prec == 2 else 'nbx::StatSK<6, 3, 0, 3, 0>'} >(nbx::TpProb, nbx::TpProb, int)"]
+             f"{sk_name('6, 3, 0, 3, 0', int(udv)) if prec == 2 else 'nbx::StatSK<6, 3, 0, 3, 0>'} >(nbx::TpProb, nbx::TpProb, int)"]
     x3 = prec != 0
     roles = ["message_layer_1: node GEMM + edge combination + gate (flops: the node GEMM)",
              "message_layer_2 + gate + aggregation + BN sums",

@@ -704,6 +704,8 @@ using SK_UPD1_SEG_H2_DV = nbx::StatSKH2<12, 12, 6, 6, 4, 1>;
 using SK_UPD1_32_SEG_H2_DV = nbx::StatSKH2<4, 4, 2, 2, 4, 1>;
 using SK_PP1_SEG_H2_DV = nbx::StatSKH2<6, 6, 3, 3, 2, 1>;
 using SK_PP1_32_SEG_H2_DV = nbx::StatSKH2<2, 2, 1, 1, 2, 1>;
+using SK_UPD2_H2_DV = nbx::StatSKH2<6, 3, 0, 3, 0, 1>;   // [h_s | h_v . na]: the dot half from U2V
+using SK_UPD2_32_H2_DV = nbx::StatSKH2<2, 1, 0, 1, 0, 1>;
 
 // message_layer_2 on the split-precision MFMA path when the weights carry a bf16x3 image
 // (NBX_X3=0: fp32 MFMA path, A/B only)
@@ -1067,6 +1069,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             xprev = nullptr;
         }
         const bool msg2_dv = msg_dv(M, N, L.msg2_img_h2 != nullptr);
+        // update_layer_2 forms the [h_v . na] half of its scalar operand from U2V (TpStream DV), so
+        // update_layer_1's gate epilogue skips writing it (same switch as dv_upd)
+        const bool upd2_dv = dv_upd && L.upd2_img_h2 != nullptr;
         if (fused_msg) {
             // message_layer_1: node precomputation + edge combination + gate in one kernel
             nbx::MsgPreProb mp;
@@ -1182,6 +1187,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             p.B = L.upd1_img;
             p.bias = L.upd1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
             p.chunks = (M + 15) / 16;
+            p.skip_gate_dot = upd2_dv ? 1 : 0;
             if ((M == 96 || M == 32) && L.upd1_img_h2 && split_prec() == 2) {
                 p.B = static_cast<const float*>(L.upd1_img_h2);
                 p.bscale = L.upd1_h2_descale;
@@ -1235,8 +1241,11 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if ((M == 96 || M == 32) && L.upd2_img_h2 && split_prec() == 2 && static_enabled()) {
                 p.B = static_cast<const float*>(L.upd2_img_h2);
                 p.bscale = L.upd2_h2_descale;
-                const int rc = M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm)
-                                       : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2>(p, st, tm);
+                const int rc =
+                    upd2_dv ? (M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2_DV>(p, st, tm)
+                                       : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2_DV>(p, st, tm))
+                    : M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm)
+                              : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2>(p, st, tm);
                 if (rc) return rc;
             } else {
                 if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;

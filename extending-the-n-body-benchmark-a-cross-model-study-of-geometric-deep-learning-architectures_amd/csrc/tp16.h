@@ -142,7 +142,8 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
     // DV (TpStream): the scalar operand's trailing dot chunks are formed from the vector chunks, not
     // loaded; loads run in TpStream load order (the item order unless DV)
     using TS = TpStream<SK>;
-    static_assert(!SK::DV || (KS == 1 && SK::SEG > 0 && NV == 1 && SK::PREC >= 1), "DV: segmented split-precision input");
+    static_assert(!SK::DV || (KS == 1 && NV == 1 && SK::PREC >= 1 && SK::K0 > SK::KV),
+                  "DV: a split-precision scalar operand ending in KV dot chunks");
     constexpr int NLD = TS::NLOAD;   // DV loads (KS = 1)
     if constexpr (SK::on) {
         slice_call([&](auto sc_) {
@@ -713,7 +714,8 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         const float h1 = gg * (na[2] * tt + acc[g][NS + 1][jj]);
                         const float h2 = gg * (na[3] * tt + acc[g][NS + 2][jj]);
                         st_out<false>(&P.out_s[(size_t)row * 2 * M + ch], hs);
-                        st_out<false>(&P.out_s[(size_t)row * 2 * M + M + ch], h0 * na[1] + h1 * na[2] + h2 * na[3]);
+                        if (!P.skip_gate_dot)
+                            st_out<false>(&P.out_s[(size_t)row * 2 * M + M + ch], h0 * na[1] + h1 * na[2] + h2 * na[3]);
                         st_out<false>(&P.out_v[(size_t)row * M + ch], h0);
                         st_out<false>(&P.out_v[P.out_plane + (size_t)row * M + ch], h1);
                         st_out<false>(&P.out_v[2 * P.out_plane + (size_t)row * M + ch], h2);

@@ -222,6 +222,8 @@ struct TpProb {
     // given ids with equal b % 8 and that XCD's L2 fetches the range's A rows once for all G of them
     // (0: chunk-major order)
     int xcd_groups;
+    // GATE_NODE: 1 = the [h_v . na] half of out_s is not written (its consumer forms it: TpStream DV)
+    int skip_gate_dot;
 };
 
 // block id -> (chunk group, row-range block): chunk-major, or XCD-grouped (TpProb::xcd_groups)
@@ -314,6 +316,7 @@ struct StatSKH2 {
 // scalar operand ends in KV dot chunks (chunk ND + kc = sum_p y_p v_p of vector chunk kc, ND = K0 - KV):
 //   message_layer_2: [m_s | m_v . rhat] (ND = KV), update_layer_1: [x_s | a_s | x_v . na | a_v . na]
 //   (ND = KV = 6), pre_pool1: [x_s | x_v . na] (ND = KV = 3);
+//   update_layer_2: [h_s | h_v . na] (ND = KV = 3);
 // the dot chunks are not loaded but formed in registers from the three vector chunks of the same
 // channels (fmaf(v2, y2, fmaf(v1, y1, v0 * y0)), the chain their producers evaluate), so positions run
 // the ND scalar chunks, then per kc: vec(0, kc), vec(1, kc), vec(2, kc), dot(kc) -- 20 % fewer A bytes.
