@@ -330,6 +330,27 @@ def test_forward_repeat_train_mode_c2(hip_device):
         assert (np.abs(o - outs[0]).max(0) <= 1e-6 * scale).all()
 
 
+def test_forward_pairs_c2(hip_device):
+    """Race guard: 150 pairs of train-mode C2 forwards, each pair on a new batch; the
+    two forwards of a pair agree per system to 1e-3 of the output scale (fp64 atomic BatchNorm sums:
+    ~1e-6).  msg_pre's summed hand-off counter corrupted one node group in about 1 % of forwards
+    (0.4-9 % errors on one or two systems); this test caught it with probability ~0.95."""
+    model = make_model(192, 6, hip_device, perturb_bn=False).train()
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    B, N = 1024, 5
+    bad = []
+    for k in range(150):
+        pos, vel, mass = states(B, N, seed=2000 + k)
+        o = []
+        for _ in range(2):
+            model.load_state_dict(sd0)
+            o.append(gpu_forward(model, pos, vel, mass, B, N, hip_device))
+        rel = (np.abs(o[0] - o[1]) / np.abs(o[0]).max(0)).reshape(B, N, -1).max(axis=(1, 2))
+        if rel.max() > 1e-3:
+            bad.append((k, float(rel.max()), np.argwhere(rel > 1e-3)[:, 0].tolist()[:4]))
+    assert not bad, bad
+
+
 def c2_fixture():
     import os
     p = os.path.join(os.path.dirname(__file__), "golden", "segnn_c2_rollout.npz")
