@@ -1290,6 +1290,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         p.B = w->pp1_img;
         p.bias = w->pp1_bias; p.geom = ws.NA; p.out_s = ws.U2S; p.out_v = ws.U2V; p.out_plane = V * M;
         p.chunks = (M + 15) / 16;
+        p.skip_gate_dot = 1;   // pre_pool2 (pp2_node) reads only the h_s half of U2S
         if (w->pp1_img_h2 && split_prec() == 2) {
             p.B = static_cast<const float*>(w->pp1_img_h2);
             p.bscale = w->pp1_h2_descale;
