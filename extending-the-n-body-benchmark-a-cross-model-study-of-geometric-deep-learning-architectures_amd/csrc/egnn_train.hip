@@ -986,16 +986,13 @@ extern "C" int nbx_egnn_train_backward(const nbx_egnn_weights* w, const float* p
     p.gpart = p.save + B * p.save_floats;
     const int G = (int)(B < TRAIN_GROUPS ? B : TRAIN_GROUPS);
     p.dbg = et_dbg_buf();
-    // NBX_ET_POISON=1 fills the slices with NaN instead (checks that every gradient element is written)
-    static const bool poison = getenv("NBX_ET_POISON") && getenv("NBX_ET_POISON")[0] == '1';
     // NBX_ET_MEMSET=1: the old hipMemsetAsync zeroing (diagnosis of the graph-replay race only,
     // tools/egnn_graph_dump.py)
     static const bool use_memset = getenv("NBX_ET_MEMSET") && getenv("NBX_ET_MEMSET")[0] == '1';
     if (use_memset) {
         NBX_HIP(hipMemsetAsync(p.gpart, 0, sizeof(float) * (size_t)G * p.blob_floats, st));
     } else {
-        hipLaunchKernelGGL(egnn_zero_kernel, dim3(4096), dim3(256), 0, st, p.gpart, (int64_t)G * p.blob_floats,
-                           poison ? __builtin_nanf("") : 0.f);
+        hipLaunchKernelGGL(egnn_zero_kernel, dim3(4096), dim3(256), 0, st, p.gpart, (int64_t)G * p.blob_floats, 0.f);
     }
     const size_t lds = train_lds_floats((int)N, w->hidden) * 4;
     if (int rc = set_lds_attr()) return rc;

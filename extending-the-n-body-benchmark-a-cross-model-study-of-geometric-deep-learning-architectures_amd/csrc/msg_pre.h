@@ -50,7 +50,6 @@ struct MsgPreProb {
     float bscale;        // fp16x2: the factor that undoes the images' power-of-two weight scale
     int xcd_group;       // block id -> (chunk, slab) so a slab's chunk blocks share one XCD (per_chunk % 8 == 0)
     unsigned long long* dbg;  // optional per-wave phase clocks (tuning only)
-    int diag;                 // tuning only: 1 = edge waves idle (timing of the GEMM side alone)
     int no_dot;               // 1: M1S's dot half is not written (message_layer_2 forms it: TpStream DV)
 };
 

@@ -302,7 +302,7 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
                 if constexpr (DEC) dec_signal(0);
                 tick(c_gemm);
             }
-        } else if (i > 0 && live && !P.diag) {
+        } else if (i > 0 && live) {
             // ---- edges of group i-1
             const float4 geo_cur = geo_next;
             const float pm_cur = pm_next;

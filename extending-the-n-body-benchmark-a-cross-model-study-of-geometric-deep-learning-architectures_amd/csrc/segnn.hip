@@ -891,7 +891,6 @@ int run_msg_pre(nbx::MsgPreProb& p, hipStream_t st, KernelTiming* tm) {
     static const bool debug = getenv("NBX_TP_DEBUG") != nullptr;
     if (debug) {
         p.dbg = tp_dbg_buf(st);
-        p.diag = getenv("NBX_MP_NOEDGE") != nullptr;
         if (int rc = nbx::msg_pre_launch(p, st)) return rc;
         const int n = p.chunks * p.per_chunk * 8;
         std::vector<unsigned long long> h((size_t)n * 4);
