@@ -12,10 +12,10 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 15
+ABI_VERSION = 16
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
-GEMM_TRANS_A, GEMM_TRANS_B, GEMM_B_ONES = 1, 2, 4
+GEMM_TRANS_A, GEMM_TRANS_B, GEMM_B_ONES, GEMM_ONES_TAIL = 1, 2, 4, 8
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_SLRELU = 0, 1, 2, 3
 MAX_LAYERS = 64
 

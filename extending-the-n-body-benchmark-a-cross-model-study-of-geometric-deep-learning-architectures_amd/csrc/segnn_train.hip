@@ -51,7 +51,15 @@ struct GemmArgs {
     int64_t kchunk;   // K range per split
     float beta;
     int ones;         // NBX_GEMM_B_ONES: op(B)'s last column (n = N - 1) is ones, not memory
+    int tail;         // NBX_GEMM_ONES_TAIL: C's last column is stored as a row after the M x (N - 1) block
 };
+
+// address of C(r, c): row-major with leading dimension ldc, except that under NBX_GEMM_ONES_TAIL the
+// last column (c = N - 1) is the contiguous vector C + M ldc (a weight gradient and its bias gradient
+// then both leave the GEMM contiguous)
+__device__ __forceinline__ float* c_at(float* C, int64_t ldc, int64_t M, int64_t N, int tail, int64_t r, int64_t c) {
+    return (tail && c == N - 1) ? C + M * ldc + r : C + r * ldc + c;
+}
 
 // one 64 x 64 output tile (bx, by) of K split bz of nz (the body of gemm_f32_kernel and of the
 // grouped gemm_f32_batched_kernel)
@@ -140,7 +148,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     for (int i = 0; i < 16; ++i) {
         const int64_t row = m0 + wm + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
         if (row >= g.M) continue;
-        float* p = out + row * ld + col;
+        float* p = split ? out + row * ld + col : c_at(out, ld, g.M, g.N, g.tail, row, col);
         *p = (!split && g.beta != 0.f) ? acc[i] + g.beta * *p : acc[i];
     }
 }
@@ -193,7 +201,7 @@ struct ReduceBatch {
     const float* part[GMAXP];
     float* C[GMAXP];
     int64_t M[GMAXP], N[GMAXP], ldc[GMAXP];
-    int splits[GMAXP];
+    int splits[GMAXP], tail[GMAXP];
     float beta[GMAXP];
     int64_t first[GMAXP + 1];   // first element of each problem in the flattened index
     int count;
@@ -231,17 +239,17 @@ __global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
     const int64_t e = i - b.first[p], N = b.N[p], MN = b.M[p] * N;
     const int64_t r = e / N, c = e - r * N;
     const float s = splitk_sum(b.part[p], b.splits[p], MN, e);
-    float* q = b.C[p] + r * b.ldc[p] + c;
+    float* q = c_at(b.C[p], b.ldc[p], b.M[p], N, b.tail[p], r, c);
     *q = b.beta[p] != 0.f ? s + b.beta[p] * *q : s;
 }
 
 __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, int64_t M, int64_t N,
-                                   float* __restrict__ C, int64_t ldc, float beta) {
+                                   float* __restrict__ C, int64_t ldc, float beta, int tail) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= M * N) return;
     const int64_t r = i / N, c = i - r * N;
     const float s = splitk_sum(part, splits, M * N, i);
-    float* p = C + r * ldc + c;
+    float* p = c_at(C, ldc, M, N, tail, r, c);
     *p = beta != 0.f ? s + beta * *p : s;
 }
 
@@ -719,16 +727,17 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     if (M == 0 || N == 0) return NBX_OK;
     NBX_CHECK_ARG(A && B && C, "nbx_gemm_f32: null operand");
     const bool ta = flags & NBX_GEMM_TRANS_A, tb = flags & NBX_GEMM_TRANS_B;
-    const int ones = (flags & NBX_GEMM_B_ONES) ? 1 : 0;
+    const int ones = (flags & NBX_GEMM_B_ONES) ? 1 : 0, tail = (flags & NBX_GEMM_ONES_TAIL) ? 1 : 0;
     NBX_CHECK_ARG(!ones || N >= 1, "nbx_gemm_f32: NBX_GEMM_B_ONES needs N >= 1");
-    NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N,
+    NBX_CHECK_ARG(!tail || ones, "nbx_gemm_f32: NBX_GEMM_ONES_TAIL needs NBX_GEMM_B_ONES");
+    NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N - tail,
                   "nbx_gemm_f32: leading dimension too small");
     constexpr int T = GB;
     const int splits = gemm_splits(M, N, K, T);
     const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
     NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
                   workspace_bytes, need);
-    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones};
+    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones, tail};
     g.kchunk = (g.kchunk + GK - 1) / GK * GK;
     const dim3 grid((unsigned)((N + T - 1) / T), (unsigned)((M + T - 1) / T), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
@@ -752,7 +761,7 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     NBX_LAUNCH_CHECK("gemm_f32");
     if (splits > 1) {
         hipLaunchKernelGGL(gemm_reduce_kernel, dim3(nblk(M * N)), dim3(256), 0, st, (const float*)workspace, splits, M,
-                           N, C, ldc, beta);
+                           N, C, ldc, beta, tail);
         NBX_LAUNCH_CHECK("gemm_reduce");
     }
     return NBX_OK;
@@ -789,11 +798,12 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
         const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
         const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
         const bool ta = flags[i] & NBX_GEMM_TRANS_A, tb = flags[i] & NBX_GEMM_TRANS_B;
-        const int ones = (flags[i] & NBX_GEMM_B_ONES) ? 1 : 0;
+        const int ones = (flags[i] & NBX_GEMM_B_ONES) ? 1 : 0, tail = (flags[i] & NBX_GEMM_ONES_TAIL) ? 1 : 0;
+        NBX_CHECK_ARG(!tail || ones, "nbx_gemm_f32_batched: NBX_GEMM_ONES_TAIL needs NBX_GEMM_B_ONES");
         NBX_CHECK_ARG(M > 0 && N > 0 && K >= 0, "nbx_gemm_f32_batched: problem %d: sizes must be positive", i);
         NBX_CHECK_ARG(beta[i] == 0.f || beta[i] == 1.f, "nbx_gemm_f32_batched: beta must be 0 or 1");
         NBX_CHECK_ARG(A[i] && B[i] && C[i], "nbx_gemm_f32_batched: null operand");
-        NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N,
+        NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N - tail,
                       "nbx_gemm_f32_batched: leading dimension too small");
         const int splits = gemm_splits(M, N, K, T);
         float* part = nullptr;
@@ -804,10 +814,10 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
             part = (float*)workspace + ws_off;
             ws_off += need;
             rb.part[nred] = part; rb.C[nred] = C[i]; rb.M[nred] = M; rb.N[nred] = N; rb.ldc[nred] = ldc;
-            rb.splits[nred] = splits; rb.beta[nred] = beta[i]; rb.first[nred + 1] = rb.first[nred] + M * N;
+            rb.splits[nred] = splits; rb.tail[nred] = tail; rb.beta[nred] = beta[i]; rb.first[nred + 1] = rb.first[nred] + M * N;
             ++nred;
         }
-        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i], ones};
+        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i], ones, tail};
         g.kchunk = (g.kchunk + GK - 1) / GK * GK;
         const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
         gb.g[i] = g;

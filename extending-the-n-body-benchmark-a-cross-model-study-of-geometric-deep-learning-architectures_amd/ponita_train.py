@@ -68,14 +68,16 @@ class _LinFn(torch.autograd.Function):
         db = dW = dX = None
         want_b = b is not None and ctx.needs_input_grad[2]
         # the weight and the input gradient GEMMs in one launch (nbx_gemm_f32_batched); the bias gradient
-        # (column sums of dZ) is the last column of the weight gradient against X extended by ones
+        # (column sums of dZ) is the last column of the weight gradient against X extended by ones, stored
+        # after it (NBX_GEMM_ONES_TAIL): both contiguous, so autograd adopts them without a copy
         probs = []
         if ctx.needs_input_grad[1] or want_b:
-            dWe = torch.empty(N, K + 1, device=dev, dtype=_f32)
-            probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES, N, K + 1, rows, dZ, N, X, ldx, dWe, K + 1, 0.0))
-            dW = dWe[:, :K] if ctx.needs_input_grad[1] else None
+            dWe = torch.empty(N * (K + 1), device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES | _lib.GEMM_ONES_TAIL, N, K + 1, rows, dZ, N, X, ldx,
+                          dWe, K, 0.0))
+            dW = dWe[:N * K].view(N, K) if ctx.needs_input_grad[1] else None
             if want_b:
-                db = dWe[:, K]
+                db = dWe[N * K:]
         if ctx.needs_input_grad[0]:
             dX = torch.zeros(rows, ldx, device=dev, dtype=_f32) if ldx != K else torch.empty(rows, K, device=dev,
                                                                                               dtype=_f32)

@@ -154,17 +154,18 @@ class _TPFn(torch.autograd.Function):
         want_b = bias is not None and ctx.needs_input_grad[5]
         # the (up to) four backward GEMMs -- weight gradients and input gradients -- in one launch; the
         # bias gradient (column sums of dZs[:, :NSc]) is the last column of the weight-gradient GEMM
-        # against S_in extended by a column of ones (NBX_GEMM_B_ONES)
+        # against S_in extended by a column of ones (NBX_GEMM_B_ONES), stored after the weight gradient
+        # (NBX_GEMM_ONES_TAIL) so that both leave contiguous (autograd adopts them without a copy)
         probs = []
         dWs = dWv = dS = None
         if ctx.needs_input_grad[3] or want_b:
-            W1 = Ks + Kv + 1
-            dWe = torch.empty(nsc + Nt, W1, device=dev, dtype=_f32)
-            probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES, nsc + Nt, W1, rows, dZs, nsc + Nt, S, Ks + Kv,
-                          dWe, W1, 0.0))
-            dWs = dWe[:, :Ks + Kv] if ctx.needs_input_grad[3] else None
+            W1, nw = Ks + Kv + 1, (nsc + Nt) * (Ks + Kv)
+            dWe = torch.empty((nsc + Nt) * W1, device=dev, dtype=_f32)
+            probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES | _lib.GEMM_ONES_TAIL, nsc + Nt, W1, rows, dZs, nsc + Nt,
+                          S, Ks + Kv, dWe, Ks + Kv, 0.0))
+            dWs = dWe[:nw].view(nsc + Nt, Ks + Kv) if ctx.needs_input_grad[3] else None
             if want_b:
-                dbias = dWe[:nsc, Ks + Kv]
+                dbias = dWe[nw:nw + nsc]
         if Kv and ctx.needs_input_grad[4]:
             dWv = torch.empty(Nt, Kv, device=dev, dtype=_f32)
             probs.append((_lib.GEMM_TRANS_A, Nt, Kv, 3 * rows, dZv, Nt, XV, Kv, dWv, Kv, 0.0))

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 15
+#define NBX_ABI_VERSION 16
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -310,6 +310,10 @@ int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, co
 /* op(B) gains a last column of ones (n = N - 1 reads 1, not memory; B holds N - 1 columns): C's last
  * column is then the row sums of op(A) -- a bias gradient from the weight-gradient GEMM (ABI 14) */
 #define NBX_GEMM_B_ONES 4
+/* with NBX_GEMM_B_ONES: C's last column (the row sums) is stored as the contiguous vector C + M ldc
+ * instead of column N - 1 (ldc >= N - 1), so a weight gradient [M][N - 1] (ldc = N - 1) and its bias
+ * gradient [M] both come out contiguous, one buffer of M N floats (ABI 16) */
+#define NBX_GEMM_ONES_TAIL 8
 int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes);
 /* ABI 12.  Up to 4 independent nbx_gemm_f32 problems in one launch (plus one launch for every split-K
  * sum): problem i has flags[i], dims[6 i ..] = (M, N, K, lda, ldb, ldc), A[i], B[i], C[i], beta[i]

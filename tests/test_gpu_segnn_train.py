@@ -69,6 +69,19 @@ def test_gemm_f32_ones_column(hip_device, flags, M, N, K, ldb_pad):
     err = (C.double().cpu() - ref).abs().max().item()
     assert err <= 2e-6 * (A.abs() @ torch.cat([B.abs(), torch.ones(K, 1, dtype=torch.float64)], 1)).max().item() + 1e-6
     assert torch.equal(C, Cb)
+    # NBX_GEMM_ONES_TAIL: the same result as one buffer [M][N - 1] (ldc = N - 1) + the row sums [M],
+    # bit-identical to the column layout, single and batched; nothing past M N floats is written
+    ft = f | _lib.GEMM_ONES_TAIL
+    for batched in (False, True):
+        Ct = torch.full((M * N + 5,), 7.0, device=hip_device)
+        if batched:
+            T.gemm_batched([(ft, M, N, K, Ad, As.shape[1], Bd, ldb, Ct, N - 1, 0.0)])
+        else:
+            T.gemm(ft, M, N, K, Ad, As.shape[1], Bd, ldb, Ct, N - 1)
+        torch.cuda.synchronize()
+        assert torch.equal(Ct[:M * (N - 1)].view(M, N - 1), C[:, :N - 1]), batched
+        assert torch.equal(Ct[M * (N - 1):M * N], C[:, N - 1]), batched
+        assert (Ct[M * N:] == 7.0).all(), batched
 
 
 def test_gemm_f32_batched_equals_single(hip_device):
