@@ -52,13 +52,22 @@ struct GemmArgs {
     float beta;
     int ones;         // NBX_GEMM_B_ONES: op(B)'s last column (n = N - 1) is ones, not memory
     int tail;         // NBX_GEMM_ONES_TAIL: C's last column is stored as a row after the M x (N - 1) block
+    // two-level rows (nbx_gemm_f32_grouped): row r of a row-major operand with outer stride o != 0 sits
+    // at (r / rdiv) o + (r % rdiv) ld -- the (2l + 1) rows of degree l of every node of an
+    // [nodes][(lmax + 1)^2][C] array as one [nodes (2l + 1)][C] operand (SO3_LinearV2)
+    int64_t rdiv, oa, ob, oc;
 };
 
-// address of C(r, c): row-major with leading dimension ldc, except that under NBX_GEMM_ONES_TAIL the
-// last column (c = N - 1) is the contiguous vector C + M ldc (a weight gradient and its bias gradient
-// then both leave the GEMM contiguous)
-__device__ __forceinline__ float* c_at(float* C, int64_t ldc, int64_t M, int64_t N, int tail, int64_t r, int64_t c) {
-    return (tail && c == N - 1) ? C + M * ldc + r : C + r * ldc + c;
+__device__ __forceinline__ int64_t row_off(int64_t r, int64_t ld, int64_t outer, int64_t rdiv) {
+    return outer ? (r / rdiv) * outer + (r % rdiv) * ld : r * ld;
+}
+
+// address of C(r, c): row-major with leading dimension ldc (two-level rows when oc != 0), except that
+// under NBX_GEMM_ONES_TAIL the last column (c = N - 1) is the contiguous vector C + M ldc (a weight
+// gradient and its bias gradient then both leave the GEMM contiguous)
+__device__ __forceinline__ float* c_at(float* C, int64_t ldc, int64_t oc, int64_t rdiv, int64_t M, int64_t N, int tail,
+                                       int64_t r, int64_t c) {
+    return (tail && c == N - 1) ? C + M * ldc + r : C + row_off(r, ldc, oc, rdiv) + c;
 }
 
 // one 64 x 64 output tile (bx, by) of K split bz of nz (the body of gemm_f32_kernel and of the
@@ -74,14 +83,16 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
     float ra[H][4], rb[H][4];
     // four consecutive elements along the contiguous dimension: (row, col) of the first, its stride
-    auto load4 = [&](const float* base, int64_t ld, int64_t r, int64_t c, int64_t rmax, int64_t cmax, float (&v)[4]) {
-        // elements base[r * ld + c + j], valid while r < rmax and c + j < cmax
+    auto load4 = [&](const float* base, int64_t ld, int64_t outer, int64_t r, int64_t c, int64_t rmax, int64_t cmax,
+                     float (&v)[4]) {
+        // elements base[row(r) + c + j], valid while r < rmax and c + j < cmax
+        const int64_t ro = row_off(r, ld, outer, g.rdiv);
         if (r < rmax && c + 3 < cmax && VEC) {
-            const float4 q = *reinterpret_cast<const float4*>(base + r * ld + c);
+            const float4 q = *reinterpret_cast<const float4*>(base + ro + c);
             v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (r < rmax && c + j < cmax) ? base[r * ld + c + j] : 0.f;
+            for (int j = 0; j < 4; ++j) v[j] = (r < rmax && c + j < cmax) ? base[ro + c + j] : 0.f;
         }
     };
     // float4 group q = t + THREADS h of a K step: [M][K] / [N][K] operands row q / 8, k 4 (q % 8);
@@ -90,11 +101,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             const int q = t + THREADS * h;
-            if (TA) load4(g.A, g.lda, k0 + q / Q4, m0 + (q % Q4) * 4, k_hi, g.M, ra[h]);   // [K][M]
-            else load4(g.A, g.lda, m0 + (q >> 3), k0 + (q & 7) * 4, g.M, k_hi, ra[h]);    // [M][K]
+            if (TA) load4(g.A, g.lda, g.oa, k0 + q / Q4, m0 + (q % Q4) * 4, k_hi, g.M, ra[h]);   // [K][M]
+            else load4(g.A, g.lda, g.oa, m0 + (q >> 3), k0 + (q & 7) * 4, g.M, k_hi, ra[h]);    // [M][K]
             const int64_t bn = TB ? n0 + (q >> 3) : n0 + (q % Q4) * 4, bk = TB ? k0 + (q & 7) * 4 : k0 + q / Q4;
-            if (TB) load4(g.B, g.ldb, bn, bk, g.N - g.ones, k_hi, rb[h]);   // [N][K]
-            else load4(g.B, g.ldb, bk, bn, k_hi, g.N - g.ones, rb[h]);      // [K][N]
+            if (TB) load4(g.B, g.ldb, g.ob, bn, bk, g.N - g.ones, k_hi, rb[h]);   // [N][K]
+            else load4(g.B, g.ldb, g.ob, bk, bn, k_hi, g.N - g.ones, rb[h]);      // [K][N]
             if (g.ones && n0 + T >= g.N) {   // the appended column of ones (block-uniform test)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -148,7 +159,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     for (int i = 0; i < 16; ++i) {
         const int64_t row = m0 + wm + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
         if (row >= g.M) continue;
-        float* p = split ? out + row * ld + col : c_at(out, ld, g.M, g.N, g.tail, row, col);
+        float* p = split ? out + row * ld + col : c_at(out, ld, g.oc, g.rdiv, g.M, g.N, g.tail, row, col);
         *p = (!split && g.beta != 0.f) ? acc[i] + g.beta * *p : acc[i];
     }
 }
@@ -163,7 +174,7 @@ __global__ __launch_bounds__(GemmCfg<T>::THREADS) void gemm_f32_kernel(GemmArgs 
 // Up to GMAXP independent GEMMs in one launch (a tensor product's scalar-row and vector-plane GEMMs,
 // its four backward GEMMs): block b belongs to the problem whose block range holds it; the operand
 // orders (TA, TB) and the float4 path are per problem (block-uniform branches).
-constexpr int GMAXP = 4;
+constexpr int GMAXP = 8;
 struct GemmBatch {
     GemmArgs g[GMAXP];
     int mode[GMAXP];      // bit 0 TA, bit 1 TB, bit 2 VEC
@@ -201,6 +212,7 @@ struct ReduceBatch {
     const float* part[GMAXP];
     float* C[GMAXP];
     int64_t M[GMAXP], N[GMAXP], ldc[GMAXP];
+    int64_t rdiv[GMAXP], oc[GMAXP];
     int splits[GMAXP], tail[GMAXP];
     float beta[GMAXP];
     int64_t first[GMAXP + 1];   // first element of each problem in the flattened index
@@ -239,7 +251,7 @@ __global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
     const int64_t e = i - b.first[p], N = b.N[p], MN = b.M[p] * N;
     const int64_t r = e / N, c = e - r * N;
     const float s = splitk_sum(b.part[p], b.splits[p], MN, e);
-    float* q = c_at(b.C[p], b.ldc[p], b.M[p], N, b.tail[p], r, c);
+    float* q = c_at(b.C[p], b.ldc[p], b.oc[p], b.rdiv[p], b.M[p], N, b.tail[p], r, c);
     *q = b.beta[p] != 0.f ? s + b.beta[p] * *q : s;
 }
 
@@ -249,7 +261,7 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, i
     if (i >= M * N) return;
     const int64_t r = i / N, c = i - r * N;
     const float s = splitk_sum(part, splits, M * N, i);
-    float* p = c_at(C, ldc, M, N, tail, r, c);
+    float* p = c_at(C, ldc, 0, 1, M, N, tail, r, c);
     *p = beta != 0.f ? s + beta * *p : s;
 }
 
@@ -737,7 +749,7 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
     NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
                   workspace_bytes, need);
-    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones, tail};
+    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones, tail, 1, 0, 0, 0};
     g.kchunk = (g.kchunk + GK - 1) / GK * GK;
     const dim3 grid((unsigned)((N + T - 1) / T), (unsigned)((M + T - 1) / T), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
@@ -767,26 +779,39 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     return NBX_OK;
 }
 
-extern "C" int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes) {
+namespace {
+// the problems of nbx_gemm_f32_batched (ds = 6 dims each) / nbx_gemm_f32_grouped (ds = 10: + rdiv and
+// the outer strides of A, B, C)
+struct GroupDims {
+    int64_t M, N, K, lda, ldb, ldc, rdiv, oa, ob, oc;
+};
+GroupDims group_dims(const int64_t* dims, int ds, int i) {
+    const int64_t* d = dims + (int64_t)ds * i;
+    GroupDims g{d[0], d[1], d[2], d[3], d[4], d[5], 1, 0, 0, 0};
+    if (ds == 10) { g.rdiv = d[6]; g.oa = d[7]; g.ob = d[8]; g.oc = d[9]; }
+    return g;
+}
+
+int gemm_group_ws(const char* name, int32_t count, const int64_t* dims, int ds, size_t* bytes) {
     NBX_CHECK_ARG(bytes != nullptr && dims != nullptr && count >= 1 && count <= GMAXP,
-                  "nbx_gemm_f32_batched_workspace_bytes: bad arguments (count 1..%d)", GMAXP);
+                  "%s_workspace_bytes: bad arguments (count 1..%d)", name, GMAXP);
     size_t n = 0;
     constexpr int T = GB;
     for (int i = 0; i < count; ++i) {
-        const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
-        NBX_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "nbx_gemm_f32_batched_workspace_bytes: negative size");
-        const int s = gemm_splits(M, N, K, T);
-        if (s > 1) n += ((size_t)s * M * N + 63) / 64 * 64;
+        const GroupDims d = group_dims(dims, ds, i);
+        NBX_CHECK_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "%s_workspace_bytes: negative size", name);
+        const int s = gemm_splits(d.M, d.N, d.K, T);
+        if (s > 1) n += ((size_t)s * d.M * d.N + 63) / 64 * 64;
     }
     *bytes = n * sizeof(float);
     return NBX_OK;
 }
 
-extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
-                                    const float* const* B, float* const* C, const float* beta, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
+int gemm_group(const char* name, int32_t count, const int32_t* flags, const int64_t* dims, int ds,
+               const float* const* A, const float* const* B, float* const* C, const float* beta, void* workspace,
+               size_t workspace_bytes, void* stream) {
     NBX_CHECK_ARG(count >= 1 && count <= GMAXP && flags && dims && A && B && C && beta,
-                  "nbx_gemm_f32_batched: bad arguments (count 1..%d)", GMAXP);
+                  "%s: bad arguments (count 1..%d)", name, GMAXP);
     GemmBatch gb;
     memset(&gb, 0, sizeof(gb));
     ReduceBatch rb;
@@ -795,31 +820,40 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
     size_t ws_off = 0;
     constexpr int T = GB;
     for (int i = 0; i < count; ++i) {
-        const int64_t M = dims[6 * i], N = dims[6 * i + 1], K = dims[6 * i + 2];
-        const int64_t lda = dims[6 * i + 3], ldb = dims[6 * i + 4], ldc = dims[6 * i + 5];
+        const GroupDims d = group_dims(dims, ds, i);
+        const int64_t M = d.M, N = d.N, K = d.K, lda = d.lda, ldb = d.ldb, ldc = d.ldc;
         const bool ta = flags[i] & NBX_GEMM_TRANS_A, tb = flags[i] & NBX_GEMM_TRANS_B;
         const int ones = (flags[i] & NBX_GEMM_B_ONES) ? 1 : 0, tail = (flags[i] & NBX_GEMM_ONES_TAIL) ? 1 : 0;
-        NBX_CHECK_ARG(!tail || ones, "nbx_gemm_f32_batched: NBX_GEMM_ONES_TAIL needs NBX_GEMM_B_ONES");
-        NBX_CHECK_ARG(M > 0 && N > 0 && K >= 0, "nbx_gemm_f32_batched: problem %d: sizes must be positive", i);
-        NBX_CHECK_ARG(beta[i] == 0.f || beta[i] == 1.f, "nbx_gemm_f32_batched: beta must be 0 or 1");
-        NBX_CHECK_ARG(A[i] && B[i] && C[i], "nbx_gemm_f32_batched: null operand");
+        NBX_CHECK_ARG(!tail || ones, "%s: NBX_GEMM_ONES_TAIL needs NBX_GEMM_B_ONES", name);
+        NBX_CHECK_ARG(M > 0 && N > 0 && K >= 0, "%s: problem %d: sizes must be positive", name, i);
+        NBX_CHECK_ARG(beta[i] == 0.f || beta[i] == 1.f, "%s: beta must be 0 or 1", name);
+        NBX_CHECK_ARG(A[i] && B[i] && C[i], "%s: null operand", name);
         NBX_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? K : N - ones) && ldc >= N - tail,
-                      "nbx_gemm_f32_batched: leading dimension too small");
+                      "%s: leading dimension too small", name);
+        // two-level rows: rdiv rows of leading dimension ld per outer step, outer >= rdiv ld (no overlap)
+        NBX_CHECK_ARG(d.rdiv >= 1 && d.oa >= 0 && d.ob >= 0 && d.oc >= 0, "%s: bad two-level row strides", name);
+        NBX_CHECK_ARG((!d.oa || d.oa >= d.rdiv * lda) && (!d.ob || d.ob >= d.rdiv * ldb) &&
+                      (!d.oc || d.oc >= d.rdiv * ldc), "%s: outer stride below rdiv x leading dimension", name);
+        NBX_CHECK_ARG(!(tail && d.oc), "%s: NBX_GEMM_ONES_TAIL with two-level C rows", name);
         const int splits = gemm_splits(M, N, K, T);
         float* part = nullptr;
         if (splits > 1) {
             const size_t need = ((size_t)splits * M * N + 63) / 64 * 64;
             NBX_CHECK_ARG(workspace && (ws_off + need) * sizeof(float) <= workspace_bytes,
-                          "nbx_gemm_f32_batched: workspace too small");
+                          "%s: workspace too small", name);
             part = (float*)workspace + ws_off;
             ws_off += need;
             rb.part[nred] = part; rb.C[nred] = C[i]; rb.M[nred] = M; rb.N[nred] = N; rb.ldc[nred] = ldc;
-            rb.splits[nred] = splits; rb.tail[nred] = tail; rb.beta[nred] = beta[i]; rb.first[nred + 1] = rb.first[nred] + M * N;
+            rb.rdiv[nred] = d.rdiv; rb.oc[nred] = d.oc;
+            rb.splits[nred] = splits; rb.tail[nred] = tail; rb.beta[nred] = beta[i];
+            rb.first[nred + 1] = rb.first[nred] + M * N;
             ++nred;
         }
-        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i], ones, tail};
+        GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i], ones, tail,
+                   d.rdiv, d.oa, d.ob, d.oc};
         g.kchunk = (g.kchunk + GK - 1) / GK * GK;
-        const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+        const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0 &&
+                         d.oa % 4 == 0 && d.ob % 4 == 0;
         gb.g[i] = g;
         gb.mode[i] = (ta ? 1 : 0) | (tb ? 2 : 0) | (vec ? 4 : 0);
         gb.tx[i] = (int)((N + T - 1) / T);
@@ -839,6 +873,27 @@ extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const i
         NBX_LAUNCH_CHECK("gemm_reduce_batched");
     }
     return NBX_OK;
+}
+}  // namespace
+
+extern "C" int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes) {
+    return gemm_group_ws("nbx_gemm_f32_batched", count, dims, 6, bytes);
+}
+
+extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
+                                    const float* const* B, float* const* C, const float* beta, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+    return gemm_group("nbx_gemm_f32_batched", count, flags, dims, 6, A, B, C, beta, workspace, workspace_bytes, stream);
+}
+
+extern "C" int nbx_gemm_f32_grouped_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes) {
+    return gemm_group_ws("nbx_gemm_f32_grouped", count, dims, 10, bytes);
+}
+
+extern "C" int nbx_gemm_f32_grouped(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
+                                    const float* const* B, float* const* C, const float* beta, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+    return gemm_group("nbx_gemm_f32_grouped", count, flags, dims, 10, A, B, C, beta, workspace, workspace_bytes, stream);
 }
 
 extern "C" int nbx_tp_prep(int64_t rows, int32_t Ks, int32_t Kv, const float* XS, int64_t ldxs, const float* XV,

@@ -8,8 +8,8 @@ separable S2 activations, rms_norm_sh) composed of libnbx operators inside ``tor
 backward passes call the same library, so ``loss.backward()`` reaches every ``nn.Parameter`` the
 reference's forward uses:
 
-* every nn.Linear / SO3_LinearV2 degree / SO(2) ``fc`` = ``ponita_train._LinFn`` (nbx_gemm_f32 +
-  nbx_bias_act), every LayerNorm = ``_LayerNormFn``, SiLU / SmoothLeakyReLU = ``_ActFn``;
+* every nn.Linear / SO(2) ``fc`` = ``ponita_train._LinFn`` (nbx_gemm_f32 + nbx_bias_act), every
+  SO3_LinearV2 = ``_SO3LinearFn`` (all degrees in one nbx_gemm_f32_grouped launch), every LayerNorm = ``_LayerNormFn``, SiLU / SmoothLeakyReLU = ``_ActFn``;
 * SO3_Rotation.rotate / rotate_inv = ``_RotateFn`` (nbx_eqv2_rotate, lmax 2 / mmax 1) or
   ``_RotateGFn`` (nbx_eqv2_rotate_general with the nbx_eqv2_wigner rows, any lmax <= 6); adjoint pairs;
 * the separable S2 activation's grid round trip = ``_S2Fn`` (nbx_eqv2_s2_act);
@@ -32,7 +32,7 @@ import torch
 
 from . import _lib, so3
 from .ponita_train import _LayerNormFn, linear
-from .segnn_train import Graph, _GatherFn, _SegSumFn, _dp, _st, colsum
+from .segnn_train import Graph, _GatherFn, _SegSumFn, _at, _dp, _st, colsum, gemm_grouped
 
 _f32 = torch.float32
 AVG_DEGREE = 23.395238876342773          # equiformer_v2_nbody.py:36
@@ -220,6 +220,62 @@ class _RMSNormGFn(torch.autograd.Function):
         return dX, dwb[:L1 * C].view(L1, C), dwb[L1 * C:], None, None
 
 
+class _SO3LinearFn(torch.autograd.Function):
+    """SO3_LinearV2 (so3.py:695-745): Y[v][i] = W[l(i)] X[v][i] (+ b on i = 0) for X [V][(lmax+1)^2][cin],
+    W [lmax+1][cout][cin].  The 2l + 1 rows of degree l of every node are one GEMM operand of V (2l + 1)
+    rows through nbx_gemm_f32_grouped's two-level rows, so all degrees run in one launch (forward: one
+    GEMM per degree; backward: the input and the weight gradient per degree and the bias gradient as
+    the row sums of the l = 0 output gradient, up to 8 per launch), with no per-degree slices, copies
+    or concatenations, and the weight gradient leaves in W's own layout."""
+
+    @staticmethod
+    def forward(ctx, X, W, b, lmax):
+        X = X.contiguous()
+        V, S, cin = X.shape
+        cout = W.shape[1]
+        Y = torch.empty(V, S, cout, device=X.device, dtype=_f32)
+        probs = [(_lib.GEMM_TRANS_B, V * (2 * l + 1), cout, cin, _at(X, l * l * cin), cin, _at(W, l * cout * cin), cin,
+                  _at(Y, l * l * cout), cout, 0.0, 2 * l + 1, S * cin, 0, S * cout) for l in range(lmax + 1)]
+        for i in range(0, len(probs), 8):
+            gemm_grouped(probs[i:i + 8], X.device)
+        if b is not None:       # the l = 0 rows, in place (each element read once, then written)
+            _lib.check(_lib.lib().nbx_bias_act(V, cout, _dp(Y), S * cout, _dp(b), _lib.ACT_NONE, _dp(Y), S * cout,
+                                               _st(Y)), "nbx_bias_act")
+        ctx.save_for_backward(X, W)
+        ctx.dims = (lmax, b is not None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        X, W = ctx.saved_tensors
+        lmax, has_b = ctx.dims
+        V, S, cin = X.shape
+        cout = W.shape[1]
+        dY = dY.contiguous()
+        dX = dWb = None
+        probs = []
+        if ctx.needs_input_grad[0]:
+            dX = torch.empty_like(X)
+            probs += [(0, V * (2 * l + 1), cin, cout, _at(dY, l * l * cout), cout, _at(W, l * cout * cin), cin,
+                       _at(dX, l * l * cin), cin, 0.0, 2 * l + 1, S * cout, 0, S * cin) for l in range(lmax + 1)]
+        want_w, want_b = ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]
+        if want_w or want_b:
+            nw = (lmax + 1) * cout * cin
+            dWb = torch.empty(nw + cout, device=X.device, dtype=_f32)
+            if want_w:
+                probs += [(_lib.GEMM_TRANS_A, cout, cin, V * (2 * l + 1), _at(dY, l * l * cout), cout,
+                           _at(X, l * l * cin), cin, _at(dWb, l * cout * cin), cin, 0.0, 2 * l + 1, S * cout, S * cin,
+                           0) for l in range(lmax + 1)]
+            if want_b:          # row sums of dY's l = 0 rows: op(B) is the column of ones alone
+                probs.append((_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES, cout, 1, V, _at(dY, 0), cout, _at(X, 0), 0,
+                              _at(dWb, nw), 1, 0.0, 1, S * cout, 0, 0))
+        for i in range(0, len(probs), 8):
+            gemm_grouped(probs[i:i + 8], X.device)
+        dW = dWb[:(lmax + 1) * cout * cin].view(lmax + 1, cout, cin) if want_w else None
+        db = dWb[(lmax + 1) * cout * cin:] if want_b else None
+        return dX, dW, db, None
+
+
 def _f(t):
     return t.to(_f32).contiguous()
 
@@ -354,18 +410,9 @@ class _Step:
         out = torch.cat(outs, 1)
         return (out if self.mprimary else out[:, self.inv_perm]), extra
 
-    def so3_linear(self, lin, x, parts=None):
-        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin];
-        ``parts``: x already split by degree."""
-        V, _, cin = x.shape
-        W = lin.weight.unbind(0)      # per-degree weights (one stack in the backward, not a select each)
-        if parts is None:
-            parts = torch.split(x, [2 * l + 1 for l in range(self.lay.lmax + 1)], dim=1)
-        ys = [linear(parts[0].reshape(V, cin), W[0], lin.bias).view(V, 1, -1)]
-        for l in range(1, self.lay.lmax + 1):
-            n = 2 * l + 1
-            ys.append(linear(parts[l].reshape(n * V, cin), W[l]).view(V, n, -1))
-        return torch.cat(ys, 1)
+    def so3_linear(self, lin, x):
+        """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on l = 0.  x [V][(lmax+1)^2][cin]."""
+        return _SO3LinearFn.apply(x, _f(lin.weight), _f(lin.bias) if lin.bias is not None else None, self.lay.lmax)
 
     def rms_norm(self, norm, x):
         if self.general:
@@ -418,10 +465,10 @@ class _Step:
 
     def ffn(self, F, x):
         """FeedForwardNetwork (transformer_block.py:473-530), separable S2 activation on SO3_Grid(lmax, lmax)."""
-        parts = torch.split(x, [2 * l + 1 for l in range(self.lay.lmax + 1)], dim=1)
-        gating = linear(parts[0].reshape(x.shape[0], -1), F.gating_linear.weight, F.gating_linear.bias,
-                        _lib.ACT_SILU)
-        h = self.so3_linear(F.so3_linear_1, x, parts)
+        V, S, C = x.shape
+        # the l = 0 columns of each node's row, read in place (leading dimension S C)
+        gating = linear(x.reshape(V, S * C), F.gating_linear.weight, F.gating_linear.bias, _lib.ACT_SILU, ldx=S * C)
+        h = self.so3_linear(F.so3_linear_1, x)
         s2 = torch.split(_S2Fn.apply(h, *self.grid_ffn), [1, h.shape[1] - 1], dim=1)[1]
         h = torch.cat([gating[:, None], s2], 1)
         return self.so3_linear(F.so3_linear_2, h)

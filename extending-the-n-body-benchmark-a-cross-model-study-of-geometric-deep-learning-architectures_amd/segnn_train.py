@@ -99,6 +99,33 @@ def gemm_batched(problems):
     return [p[8] for p in problems]
 
 
+def gemm_grouped(problems, device):
+    """Up to 8 GEMMs with two-level rows in one launch (nbx_gemm_f32_grouped): problems
+    ``(flags, M, N, K, A, lda, B, ldb, C, ldc, beta, rdiv, oa, ob, oc)`` where A / B / C are device
+    pointers (ints, e.g. ``_at(t, offset)``); outer strides 0 = plain rows."""
+    problems = [p for p in problems if p[1] > 0 and p[2] > 0]
+    if not problems:
+        return
+    L = _lib.lib()
+    n = len(problems)
+    flags = (ctypes.c_int32 * n)(*[int(p[0]) for p in problems])
+    dims = (ctypes.c_int64 * (10 * n))(*[int(v) for p in problems
+                                         for v in (p[1], p[2], p[3], p[5], p[7], p[9], p[11], p[12], p[13], p[14])])
+    ptr = lambda i: (ctypes.c_void_p * n)(*[int(p[i]) for p in problems])
+    beta = (ctypes.c_float * n)(*[float(p[10]) for p in problems])
+    nb = _lib.c_sz()
+    _lib.check(L.nbx_gemm_f32_grouped_workspace_bytes(n, dims, ctypes.byref(nb)), "nbx_gemm_f32_grouped_workspace_bytes")
+    ws = _ws(nb.value, device) if nb.value else None
+    if gemm_timer is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    _lib.check(L.nbx_gemm_f32_grouped(n, flags, dims, ptr(4), ptr(6), ptr(8), beta, _dp(ws), nb.value,
+                                      _lib.stream_ptr(device)), "nbx_gemm_f32_grouped")
+    if gemm_timer is not None:
+        ev[1].record()
+        gemm_timer.append((ev[0], ev[1], sum(2.0 * p[1] * p[2] * p[3] for p in problems)))
+
+
 def colsum(X, rows, cols, ld, out, accumulate=False):
     L = _lib.lib()
     n = _lib.c_sz()

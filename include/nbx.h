@@ -315,7 +315,7 @@ int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, co
  * gradient [M] both come out contiguous, one buffer of M N floats (ABI 16) */
 #define NBX_GEMM_ONES_TAIL 8
 int nbx_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, size_t* bytes);
-/* ABI 12.  Up to 4 independent nbx_gemm_f32 problems in one launch (plus one launch for every split-K
+/* ABI 12.  Up to 4 (ABI 16: 8) independent nbx_gemm_f32 problems in one launch (plus one launch for every split-K
  * sum): problem i has flags[i], dims[6 i ..] = (M, N, K, lda, ldb, ldc), A[i], B[i], C[i], beta[i]
  * (0 or 1), each with the operand layouts, blocking and split-K order of nbx_gemm_f32, so its result
  * is bit-identical.  Host arrays; workspace from nbx_gemm_f32_batched_workspace_bytes.  Replaces the
@@ -326,6 +326,17 @@ int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const int64_t* dim
                          size_t workspace_bytes, void* stream);
 int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
                  int64_t ldb, float* C, int64_t ldc, float beta, void* workspace, size_t workspace_bytes, void* stream);
+/* ABI 16.  nbx_gemm_f32_batched with two-level rows: dims[10 i ..] = (M, N, K, lda, ldb, ldc, rdiv, oa, ob,
+ * oc); row r of a row-major operand (A's [M][K] or [K][M] rows, B's [K][N] or [N][K] rows, C's rows)
+ * whose outer stride (oa / ob / oc) is non-zero sits at (r / rdiv) outer + (r % rdiv) ld (outer >=
+ * rdiv ld), so the 2l + 1 rows of degree l of every node of an [nodes][(lmax + 1)^2][C] array are one
+ * operand of nodes (2l + 1) rows: SO3_LinearV2 (equiformer_v2 so3.py:695-745) forward and backward for
+ * all degrees in one launch, without per-degree copies (eqv2_train.py _SO3LinearFn).  Up to 8
+ * problems (both grouped entry points since ABI 16); NBX_GEMM_ONES_TAIL needs oc = 0. */
+int nbx_gemm_f32_grouped_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes);
+int nbx_gemm_f32_grouped(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
+                         const float* const* B, float* const* C, const float* beta, void* workspace,
+                         size_t workspace_bytes, void* stream);
 
 /* S_in [rows][Ks + Kv] from XS (rows x Ks, leading dimension ldxs), XV [3][rows][Kv], Y3 [rows][3];
  * backward: dXS = dS[:, :Ks] (written when non-NULL), dXV[k] += Y3[:, k] dS[:, Ks:] (accumulated). */

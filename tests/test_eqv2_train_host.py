@@ -22,7 +22,7 @@ class _G:
 
 
 def _lin(X, W, b=None, act=0, ldx=None):
-    y = X @ W.T
+    y = X[:, :W.shape[1]] @ W.T      # ldx > K: the first K columns of each row (the operator's lda)
     return _act(y + b if b is not None else y, act)
 
 
@@ -37,6 +37,13 @@ def _act(X, k):
 
 def _fn(f):
     return type("F", (), {"apply": staticmethod(f)})
+
+
+def _so3_linear(X, W, b, lmax):
+    """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on the l = 0 row."""
+    deg = torch.tensor([l for l in range(lmax + 1) for _ in range(2 * l + 1)])
+    y = torch.einsum("vic,ioc->vio", X, W[deg])
+    return torch.cat([y[:, :1] + b, y[:, 1:]], 1) if b is not None else y
 
 
 def _rotate(X, D, inverse, rescale):
@@ -80,6 +87,7 @@ def torch_ops(monkeypatch):
     monkeypatch.setattr(T, "linear", _lin)
     monkeypatch.setattr(T, "act", _act)
     monkeypatch.setattr(T, "_LayerNormFn", _fn(lambda X, w, b, eps: EQ.layer_norm(X, w, b, eps)))
+    monkeypatch.setattr(T, "_SO3LinearFn", _fn(_so3_linear))
     monkeypatch.setattr(T, "_RotateFn", _fn(_rotate))
     monkeypatch.setattr(T, "_S2Fn", _fn(_s2))
     monkeypatch.setattr(T, "_SoftmaxFn", _fn(_softmax))

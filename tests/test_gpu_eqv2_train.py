@@ -34,6 +34,32 @@ def _close(got, ref, rel, label):
     assert err <= rel * np.abs(ref).max() + 1e-7, (label, err, np.abs(ref).max())
 
 
+@pytest.mark.parametrize("lmax,V,cin,cout", [(2, 320, 64, 64), (2, 37, 24, 40), (6, 23, 18, 33), (1, 5, 7, 3)])
+def test_so3_linear_matches_torch(hip_device, lmax, V, cin, cout):
+    """_SO3LinearFn (nbx_gemm_f32_grouped two-level rows, all degrees per launch) vs fp64 torch autograd
+    of SO3_LinearV2 (so3.py:695-745: out[v][i] = W[l(i)] x[v][i], bias on i = 0): output, input, weight
+    and bias gradients; ragged row counts, channel counts off the float4 path, lmax 6 (> 8 problems:
+    two launches in the backward)."""
+    torch.manual_seed(lmax * 100 + V)
+    S = (lmax + 1) ** 2
+    x = torch.randn(V, S, cin, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(lmax + 1, cout, cin, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(cout, dtype=torch.float64, requires_grad=True)
+    deg = torch.tensor([l for l in range(lmax + 1) for _ in range(2 * l + 1)])
+    ref = torch.einsum("vic,ioc->vio", x, W[deg]) + torch.cat([b[None], torch.zeros(S - 1, cout, dtype=torch.float64)])
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    dd = lambda t: t.detach().to(device=hip_device, dtype=torch.float32).contiguous().requires_grad_()
+    xd, Wd, bd = dd(x), dd(W), dd(b)
+    got = T._SO3LinearFn.apply(xd, Wd, bd, lmax)
+    (got * g.to(hip_device, torch.float32)).sum().backward()
+    _close(got, ref, 1e-5, "out")
+    _close(xd.grad, x.grad, 1e-5, "dx")
+    _close(Wd.grad, W.grad, 1e-5, "dW")
+    _close(bd.grad, b.grad, 1e-5, "db")
+    assert Wd.grad.is_contiguous() and Wd.grad.shape == W.shape
+
+
 def test_rotation_s2_softmax_rmsnorm_match_torch(hip_device):
     """rotate / rotate_inv (adjoint pair), the S2 grid round trip, the segment softmax and the RMS norm:
     forward and input / parameter gradients vs fp64 torch autograd of the oracle's expressions."""
