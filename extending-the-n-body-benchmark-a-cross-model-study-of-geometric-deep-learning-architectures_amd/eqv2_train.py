@@ -276,6 +276,139 @@ class _SO3LinearFn(torch.autograd.Function):
         return dX, dW, db, None
 
 
+class _SO2ConvFn(torch.autograd.Function):
+    """SO2_Convolution (so2_ops.py:78-156) on m-primary coefficients x [E][R][cin] -> (out [E][R][cout],
+    extra [E][n_extra]) in one grouped GEMM launch per direction.  meta = (n0, (n_1 .. n_mmax), n_extra)
+    (coefficients of m = 0 and per m > 0 pair); rad [E][(n0 + sum n_m) cin] or None (the radial
+    weights, one per (m, coefficient, channel), shared by the +m / -m rows); W0 / b0 = fc_m0; Wm[m - 1] =
+    so2_m_conv[m - 1].fc.weight [2 n_m cout][n_m cin] = [Wr; Wi].
+    m = 0: [extra | out0] = (x0 rad0) W0^T + b0, written straight into extra and out's m = 0 rows.
+    m > 0: the complex pair product out(+m) = x+ Wr^T - x- Wi^T, out(-m) = x- Wr^T + x+ Wi^T is one
+    GEMM of [x+ | x-] against [[Wr, -Wi], [Wi, Wr]], written straight into out's rows of the pair.
+    Backward: the weight / input gradients of every block in one launch (bias gradients as row sums,
+    NBX_GEMM_B_ONES), the radial products by torch elementwise ops into the gradient buffers."""
+
+    @staticmethod
+    def forward(ctx, meta, x, rad, W0, b0, *Wm):
+        n0, nms, n_extra = meta
+        x = x.contiguous()
+        E, R, cin = x.shape
+        cout = (W0.shape[0] - n_extra) // n0
+        dev = x.device
+        starts, roffs = [], []
+        s_, r_ = n0, n0 * cin
+        for nm in nms:
+            starts.append(s_)
+            roffs.append(r_)
+            s_ += 2 * nm
+            r_ += nm * cin
+        if rad is not None:
+            rad = rad.contiguous()
+            x0s = x[:, :n0] * rad[:, :n0 * cin].view(E, n0, cin)
+            xms = [x[:, st:st + 2 * nm].view(E, 2, nm, cin) * rad[:, ro:ro + nm * cin].view(E, 1, nm, cin)
+                   for nm, st, ro in zip(nms, starts, roffs)]
+            A0, lda0 = _at(x0s, 0), n0 * cin
+            Am = [(_at(t, 0), 2 * nm * cin) for t, nm in zip(xms, nms)]
+        else:
+            x0s, xms = None, []
+            A0, lda0 = _at(x, 0), R * cin
+            Am = [(_at(x, st * cin), R * cin) for st in starts]
+        Wb = []
+        for W, nm in zip(Wm, nms):
+            a = nm * cout
+            Wr, Wi = W[:a], W[a:]
+            Wb.append(torch.cat([torch.cat([Wr, -Wi], 1), torch.cat([Wi, Wr], 1)], 0))
+        out = torch.empty(E, R, cout, device=dev, dtype=_f32)
+        extra = torch.empty(E, n_extra, device=dev, dtype=_f32)
+        K0 = n0 * cin
+        probs = []
+        if n_extra:
+            probs.append((_lib.GEMM_TRANS_B, E, n_extra, K0, A0, lda0, _at(W0, 0), K0, _at(extra, 0), n_extra, 0.0,
+                          1, 0, 0, 0))
+        probs.append((_lib.GEMM_TRANS_B, E, n0 * cout, K0, A0, lda0, _at(W0, n_extra * K0), K0, _at(out, 0), R * cout,
+                      0.0, 1, 0, 0, 0))
+        for (ap, lda), Wbm, nm, st in zip(Am, Wb, nms, starts):
+            probs.append((_lib.GEMM_TRANS_B, E, 2 * nm * cout, 2 * nm * cin, ap, lda, _at(Wbm, 0), 2 * nm * cin,
+                          _at(out, st * cout), R * cout, 0.0, 1, 0, 0, 0))
+        for i in range(0, len(probs), 8):
+            gemm_grouped(probs[i:i + 8], dev)
+        if b0 is not None:
+            L = _lib.lib()
+            if n_extra:
+                _lib.check(L.nbx_bias_act(E, n_extra, _dp(extra), n_extra, _dp(b0), _lib.ACT_NONE, _dp(extra), n_extra,
+                                          _st(extra)), "nbx_bias_act")
+            _lib.check(L.nbx_bias_act(E, n0 * cout, _dp(out), R * cout, _at(b0, n_extra), _lib.ACT_NONE, _dp(out),
+                                      R * cout, _st(out)), "nbx_bias_act")
+        ctx.save_for_backward(x, rad, W0, x0s, *xms, *Wb)
+        ctx.meta = (n0, nms, n_extra, starts, roffs, b0 is not None, len(xms))
+        return out, extra
+
+    @staticmethod
+    def backward(ctx, dout, dextra):
+        n0, nms, n_extra, starts, roffs, has_b, nx = ctx.meta
+        saved = ctx.saved_tensors
+        x, rad, W0, x0s = saved[:4]
+        xms, Wb = saved[4:4 + nx], saved[4 + nx:]
+        E, R, cin = x.shape
+        cout = (W0.shape[0] - n_extra) // n0
+        dev = x.device
+        dout = dout.contiguous()
+        K0, M0 = n0 * cin, n_extra + n0 * cout
+        # [d extra | d out0] side by side: one operand for the m = 0 weight and input gradients
+        if n_extra:
+            G0, ldg = torch.cat([dextra.contiguous(), dout[:, :n0].reshape(E, n0 * cout)], 1), M0
+        else:
+            G0, ldg = dout, R * cout
+        if rad is not None:
+            A0, lda0 = _at(x0s, 0), K0
+            Am = [(_at(t, 0), 2 * nm * cin) for t, nm in zip(xms, nms)]
+        else:
+            A0, lda0 = _at(x, 0), R * cin
+            Am = [(_at(x, st * cin), R * cin) for st in starts]
+        need_x = ctx.needs_input_grad[1]
+        dx = torch.empty(E, R, cin, device=dev, dtype=_f32) if need_x or rad is not None else None
+        dW0b = torch.empty(M0 * (K0 + 1), device=dev, dtype=_f32)
+        dWb = [torch.empty(2 * nm * cout, 2 * nm * cin, device=dev, dtype=_f32) for nm in nms]
+        # input-side gradients land in scratch when a radial product follows, else straight in dx
+        dx0s = torch.empty(E, K0, device=dev, dtype=_f32) if rad is not None else None
+        dxms = [torch.empty(E, 2 * nm * cin, device=dev, dtype=_f32) for nm in nms] if rad is not None else []
+        probs = [(_lib.GEMM_TRANS_A | _lib.GEMM_B_ONES | _lib.GEMM_ONES_TAIL, M0, K0 + 1, E, _at(G0, 0), ldg, A0, lda0,
+                  _at(dW0b, 0), K0, 0.0, 1, 0, 0, 0)]
+        if need_x or rad is not None:
+            probs.append((0, E, K0, M0, _at(G0, 0), ldg, _at(W0, 0), K0,
+                          _at(dx0s, 0) if rad is not None else _at(dx, 0), K0 if rad is not None else R * cin, 0.0,
+                          1, 0, 0, 0))
+        for i, ((ap, lda), Wbm, nm, st) in enumerate(zip(Am, Wb, nms, starts)):
+            n2o, n2i = 2 * nm * cout, 2 * nm * cin
+            probs.append((_lib.GEMM_TRANS_A, n2o, n2i, E, _at(dout, st * cout), R * cout, ap, lda, _at(dWb[i], 0), n2i,
+                          0.0, 1, 0, 0, 0))
+            if need_x or rad is not None:
+                probs.append((0, E, n2i, n2o, _at(dout, st * cout), R * cout, _at(Wbm, 0), n2i,
+                              _at(dxms[i], 0) if rad is not None else _at(dx, st * cin),
+                              n2i if rad is not None else R * cin, 0.0, 1, 0, 0, 0))
+        for i in range(0, len(probs), 8):
+            gemm_grouped(probs[i:i + 8], dev)
+        drad = None
+        if rad is not None:
+            drad = torch.empty_like(rad)
+            torch.mul(dx0s.view(E, n0, cin), rad[:, :K0].view(E, n0, cin), out=dx[:, :n0])
+            torch.mul(dx0s.view(E, n0, cin), x[:, :n0], out=drad[:, :K0].view(E, n0, cin))
+            for nm, st, ro, g in zip(nms, starts, roffs, dxms):
+                g4 = g.view(E, 2, nm, cin)
+                torch.mul(g4, rad[:, ro:ro + nm * cin].view(E, 1, nm, cin), out=dx[:, st:st + 2 * nm].view(E, 2, nm, cin))
+                torch.sum(g4 * x[:, st:st + 2 * nm].view(E, 2, nm, cin), 1, out=drad[:, ro:ro + nm * cin].view(E, nm, cin))
+        dW0 = dW0b[:M0 * K0].view(M0, K0)
+        db0 = dW0b[M0 * K0:] if has_b else None
+        dWm = []
+        for g, nm in zip(dWb, nms):          # [[Wr, -Wi], [Wi, Wr]] -> (dWr; dWi)
+            a, b = nm * cout, nm * cin
+            d = torch.empty(2 * a, b, device=dev, dtype=_f32)
+            torch.add(g[:a, :b], g[a:, b:], out=d[:a])
+            torch.sub(g[a:, :b], g[:a, b:], out=d[a:])
+            dWm.append(d)
+        return (None, dx if need_x else None, drad, dW0, db0, *dWm)
+
+
 def _f(t):
     return t.to(_f32).contiguous()
 
@@ -382,32 +515,14 @@ class _Step:
     def so2_conv(self, conv, x, x_edge, cout, n_extra=0):
         """SO2_Convolution (so2_ops.py:78-156) of x [E][R][cin] (kept coefficients) -> ([E][R][cout], extra):
         m-primary order (CoefficientMappingModule), the m = 0 block through fc_m0, every m > 0 pair
-        (+m, -m) through its SO2_m_Convolution as a complex product.  The per-order blocks are taken
-        with one torch.split (one backward op instead of a zero-fill + copy per slice)."""
-        E, _, cin = x.shape
+        (+m, -m) through its SO2_m_Convolution as a complex product (_SO2ConvFn)."""
         lay = self.lay
         xm = x if self.mprimary else x[:, self.perm]
-        n0 = lay.m_size[0]
-        parts = torch.split(xm, [n0] + [2 * lay.m_size[m] for m in range(1, lay.mmax + 1)], dim=1)
         rad = self.rad_func(conv.rad_func, x_edge) if x_edge is not None else None
-        rparts = torch.split(rad, [n0 * cin] + [lay.m_size[m] * cin for m in range(1, lay.mmax + 1)], dim=1) \
-            if rad is not None else None
-        x0 = parts[0].reshape(E, n0 * cin)
-        if rad is not None:
-            x0 = x0 * rparts[0]
-        y0 = linear(x0, conv.fc_m0.weight, conv.fc_m0.bias)
-        extra, y0 = torch.split(y0, [n_extra, n0 * cout], dim=1)
-        outs = [y0.reshape(E, n0, cout)]
-        for m in range(1, lay.mmax + 1):
-            nm = lay.m_size[m]
-            xmm = parts[m].reshape(E, 2, nm * cin)
-            if rad is not None:
-                xmm = xmm * rparts[m][:, None]
-            y = linear(xmm.reshape(2 * E, nm * cin), conv.so2_m_conv[m - 1].fc.weight).view(E, 2, 2, nm * cout)
-            xr, xi = y.unbind(2)         # [E][row (+m, -m)][nm cout]: real / imaginary halves of fc
-            # (+m, -m) outputs = (xr[+m] - xi[-m], xr[-m] + xi[+m])
-            outs.append((xr + xi.flip(1) * self.sign).reshape(E, 2 * nm, cout))
-        out = torch.cat(outs, 1)
+        meta = (lay.m_size[0], tuple(lay.m_size[m] for m in range(1, lay.mmax + 1)), n_extra)
+        b0 = _f(conv.fc_m0.bias) if conv.fc_m0.bias is not None else None
+        out, extra = _SO2ConvFn.apply(meta, xm, rad, _f(conv.fc_m0.weight), b0,
+                                      *[_f(c.fc.weight) for c in conv.so2_m_conv])
         return (out if self.mprimary else out[:, self.inv_perm]), extra
 
     def so3_linear(self, lin, x):

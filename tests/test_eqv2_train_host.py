@@ -39,6 +39,31 @@ def _fn(f):
     return type("F", (), {"apply": staticmethod(f)})
 
 
+def _so2conv(meta, x, rad, W0, b0, *Wm):
+    """SO2_Convolution (so2_ops.py:78-156) on m-primary rows, as torch ops: m = 0 block through fc_m0,
+    each m > 0 pair (+m, -m) through fc as the complex product (xr[+m] - xi[-m], xr[-m] + xi[+m])."""
+    n0, nms, n_extra = meta
+    E, R, cin = x.shape
+    parts = torch.split(x, [n0] + [2 * nm for nm in nms], 1)
+    rparts = torch.split(rad, [n0 * cin] + [nm * cin for nm in nms], 1) if rad is not None else None
+    x0 = parts[0].reshape(E, n0 * cin)
+    if rad is not None:
+        x0 = x0 * rparts[0]
+    y0 = x0 @ W0.T + (b0 if b0 is not None else 0.0)
+    extra, y0 = y0[:, :n_extra], y0[:, n_extra:]
+    cout = y0.shape[1] // n0
+    outs = [y0.reshape(E, n0, cout)]
+    sign = torch.tensor([-1.0, 1.0], dtype=x.dtype, device=x.device).view(1, 2, 1)
+    for i, nm in enumerate(nms):
+        xmm = parts[i + 1].reshape(E, 2, nm * cin)
+        if rad is not None:
+            xmm = xmm * rparts[i + 1][:, None]
+        y = (xmm.reshape(2 * E, nm * cin) @ Wm[i].T).view(E, 2, 2, nm * cout)
+        xr, xi = y.unbind(2)
+        outs.append((xr + xi.flip(1) * sign).reshape(E, 2 * nm, cout))
+    return torch.cat(outs, 1), extra
+
+
 def _so3_linear(X, W, b, lmax):
     """SO3_LinearV2 (so3.py:695-745): per-degree weight, bias on the l = 0 row."""
     deg = torch.tensor([l for l in range(lmax + 1) for _ in range(2 * l + 1)])
@@ -88,6 +113,7 @@ def torch_ops(monkeypatch):
     monkeypatch.setattr(T, "act", _act)
     monkeypatch.setattr(T, "_LayerNormFn", _fn(lambda X, w, b, eps: EQ.layer_norm(X, w, b, eps)))
     monkeypatch.setattr(T, "_SO3LinearFn", _fn(_so3_linear))
+    monkeypatch.setattr(T, "_SO2ConvFn", _fn(_so2conv))
     monkeypatch.setattr(T, "_RotateFn", _fn(_rotate))
     monkeypatch.setattr(T, "_S2Fn", _fn(_s2))
     monkeypatch.setattr(T, "_SoftmaxFn", _fn(_softmax))

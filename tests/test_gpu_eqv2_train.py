@@ -34,6 +34,48 @@ def _close(got, ref, rel, label):
     assert err <= rel * np.abs(ref).max() + 1e-7, (label, err, np.abs(ref).max())
 
 
+@pytest.mark.parametrize("n0,nms,n_extra,cin,cout,E,radial,bias", [
+    (3, (2,), 40, 128, 64, 1280, True, True),     # C4 so2_conv_1 (lmax 2 / mmax 1; extra = alpha + gating)
+    (3, (2,), 0, 64, 16, 1280, False, True),      # C4 so2_conv_2 (no radial weights)
+    (7, (6, 5), 9, 24, 20, 301, True, True),      # lmax 6 / mmax 2, ragged sizes
+    (4, (3, 2, 1), 0, 12, 8, 77, True, False),    # lmax 3 / mmax 3, no bias
+])
+def test_so2_conv_matches_torch(hip_device, n0, nms, n_extra, cin, cout, E, radial, bias):
+    """_SO2ConvFn (one grouped GEMM launch per direction; the complex pair product as one GEMM against
+    [[Wr, -Wi], [Wi, Wr]]) vs fp64 torch autograd of SO2_Convolution's composition (so2_ops.py:78-156):
+    outputs and the gradients of x, the radial weights, fc_m0 and every m > 0 fc."""
+    from test_eqv2_train_host import _so2conv
+    torch.manual_seed(E + cin)
+    R = n0 + 2 * sum(nms)
+    x = torch.randn(E, R, cin, dtype=torch.float64, requires_grad=True)
+    rad = torch.randn(E, (n0 + sum(nms)) * cin, dtype=torch.float64, requires_grad=True) if radial else None
+    W0 = torch.randn(n_extra + n0 * cout, n0 * cin, dtype=torch.float64, requires_grad=True)
+    b0 = torch.randn(n_extra + n0 * cout, dtype=torch.float64, requires_grad=True) if bias else None
+    Wm = [torch.randn(2 * nm * cout, nm * cin, dtype=torch.float64, requires_grad=True) for nm in nms]
+    meta = (n0, tuple(nms), n_extra)
+    out, extra = _so2conv(meta, x, rad, W0, b0, *Wm)
+    go, ge = torch.randn_like(out), torch.randn_like(extra)
+    ((out * go).sum() + (extra * ge).sum()).backward()
+    dd = lambda t: t.detach().to(device=hip_device, dtype=torch.float32).contiguous().requires_grad_() \
+        if t is not None else None
+    xd, radd, W0d, b0d = dd(x), dd(rad), dd(W0), dd(b0)
+    Wmd = [dd(w) for w in Wm]
+    o, e = T._SO2ConvFn.apply(meta, xd, radd, W0d, b0d, *Wmd)
+    cu = lambda t: t.to(hip_device, torch.float32)
+    ((o * cu(go)).sum() + (e * cu(ge)).sum()).backward()
+    _close(o, out, 1e-5, "out")
+    if n_extra:
+        _close(e, extra, 1e-5, "extra")
+    _close(xd.grad, x.grad, 1e-5, "dx")
+    if radial:
+        _close(radd.grad, rad.grad, 1e-5, "drad")
+    _close(W0d.grad, W0.grad, 1e-5, "dW0")
+    if bias:
+        _close(b0d.grad, b0.grad, 1e-5, "db0")
+    for i, (g, r) in enumerate(zip(Wmd, Wm)):
+        _close(g.grad, r.grad, 1e-5, f"dW{i + 1}")
+
+
 @pytest.mark.parametrize("lmax,V,cin,cout", [(2, 320, 64, 64), (2, 37, 24, 40), (6, 23, 18, 33), (1, 5, 7, 3)])
 def test_so3_linear_matches_torch(hip_device, lmax, V, cin, cout):
     """_SO3LinearFn (nbx_gemm_f32_grouped two-level rows, all degrees per launch) vs fp64 torch autograd
