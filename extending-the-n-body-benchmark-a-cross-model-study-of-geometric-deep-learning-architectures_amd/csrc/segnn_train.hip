@@ -609,27 +609,25 @@ __global__ void bn_param_grad_kernel(int nb, int M, const double* __restrict__ p
 }
 
 // ---------------------------------------------------------------- gathers and segment sums
-// out[r][c] = in[idx[r]][c] per plane
+// out[r][c] = in[idx[r]][c] per plane (plane = blockIdx.y)
 __global__ void gather_rows_kernel(int64_t n, int cols, const int* __restrict__ idx, const float* __restrict__ in,
-                                   int64_t ldi, int64_t psi, float* __restrict__ out, int64_t ldo, int64_t pso,
-                                   int planes) {
+                                   int64_t ldi, int64_t psi, float* __restrict__ out, int64_t ldo, int64_t pso) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n * cols) return;
-    const int64_t r = i / cols;
+    const int64_t r = i / cols, k = blockIdx.y;
     const int c = (int)(i - r * cols);
-    const int64_t s = idx[r];
-    for (int k = 0; k < planes; ++k) out[k * pso + r * ldo + c] = in[k * psi + s * ldi + c];
+    out[k * pso + r * ldo + c] = in[k * psi + (int64_t)idx[r] * ldi + c];
 }
 
 // out[n][c] (+)= sum_{j in [ptr[n], ptr[n+1])} in[eid[j]][c] per plane, fixed order: one block of 4
 // waves per (segment, 64-column slice), lane = column; wave w sums the w-th quarter of the segment
 // in CSR order with its row loads issued 8 at a time (long segments -- an embedding-table gradient
 // has ~E / #elements rows per segment -- were a serial chain of dependent L2 round trips), then
-// the 4 partials are added in wave order through LDS
+// the 4 partials are added in wave order through LDS; one grid row (blockIdx.y) per plane
 __global__ __launch_bounds__(256) void segment_sum4_kernel(int64_t n, int cols, const int* __restrict__ ptr,
                                                           const int* __restrict__ eid, const float* __restrict__ in,
                                                           int64_t ldi, int64_t psi, float* __restrict__ out,
-                                                          int64_t ldo, int64_t pso, int planes, int accumulate) {
+                                                          int64_t ldo, int64_t pso, int accumulate) {
     __shared__ float part[4][64];
     const int slices = (cols + 63) >> 6;
     const int64_t r = blockIdx.x / slices;
@@ -637,7 +635,8 @@ __global__ __launch_bounds__(256) void segment_sum4_kernel(int64_t n, int cols, 
     const int j0 = ptr[r], j1 = ptr[r + 1], len = j1 - j0, q = (len + 3) >> 2;
     const int a = j0 + min(len, w * q), b = j0 + min(len, (w + 1) * q);
     const bool live = c < cols;
-    for (int k = 0; k < planes; ++k) {
+    {
+        const int64_t k = blockIdx.y;
         const float* src = in + k * psi + (live ? c : 0);
         float s = 0.f;
         int j = a;
@@ -660,7 +659,6 @@ __global__ __launch_bounds__(256) void segment_sum4_kernel(int64_t n, int cols, 
             float* o = out + k * pso + r * ldo + c;
             *o = accumulate ? *o + t : t;
         }
-        __syncthreads();
     }
 }
 
@@ -1085,8 +1083,8 @@ extern "C" int nbx_gather_rows(int64_t n, int32_t cols, const int32_t* idx, cons
                                void* stream) {
     NBX_CHECK_ARG(n >= 0 && cols >= 0 && planes >= 1 && ld_in >= cols && ld_out >= cols, "nbx_gather_rows: bad sizes");
     if (n == 0 || cols == 0) return NBX_OK;
-    hipLaunchKernelGGL(gather_rows_kernel, dim3(nblk(n * cols)), dim3(256), 0, (hipStream_t)stream, n, cols, idx, in,
-                       ld_in, plane_in, out, ld_out, plane_out, planes);
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(nblk(n * cols), (unsigned)planes), dim3(256), 0, (hipStream_t)stream, n,
+                       cols, idx, in, ld_in, plane_in, out, ld_out, plane_out);
     NBX_LAUNCH_CHECK("gather_rows");
     return NBX_OK;
 }
@@ -1096,9 +1094,8 @@ extern "C" int nbx_segment_sum(int64_t n, int32_t cols, const int32_t* ptr, cons
                                int32_t planes, int32_t accumulate, void* stream) {
     NBX_CHECK_ARG(n >= 0 && cols >= 0 && planes >= 1 && ld_in >= cols && ld_out >= cols, "nbx_segment_sum: bad sizes");
     if (n == 0 || cols == 0) return NBX_OK;
-    hipLaunchKernelGGL(segment_sum4_kernel, dim3((unsigned)(n * ((cols + 63) / 64))), dim3(256), 0,
-                           (hipStream_t)stream, n, cols, ptr, eid, in, ld_in, plane_in, out, ld_out, plane_out, planes,
-                           accumulate);
+    hipLaunchKernelGGL(segment_sum4_kernel, dim3((unsigned)(n * ((cols + 63) / 64)), (unsigned)planes), dim3(256), 0,
+                       (hipStream_t)stream, n, cols, ptr, eid, in, ld_in, plane_in, out, ld_out, plane_out, accumulate);
     NBX_LAUNCH_CHECK("segment_sum");
     return NBX_OK;
 }

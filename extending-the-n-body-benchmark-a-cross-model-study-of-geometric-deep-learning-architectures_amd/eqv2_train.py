@@ -424,6 +424,43 @@ def gather(X, idx_graph, which):
     return out.view(idx.shape[0], *shape[1:])
 
 
+class _GatherPairFn(torch.autograd.Function):
+    """[X[src] | X[dst]] per coefficient: X [V][S][C] -> [E][S][2C] (the attention's
+    torch.cat([x[edge_index[0]], x[edge_index[1]]], 2), transformer_block.py:281-289) as two strided
+    gathers into the halves of one buffer; backward: two segment sums over the source / destination
+    CSRs reading the halves in place, the second accumulating (no concatenation, copy or add)."""
+
+    @staticmethod
+    def forward(ctx, X, g):
+        X = X.contiguous()
+        V, S, C = X.shape
+        E = g.src.shape[0]
+        out = torch.empty(E, S, 2 * C, device=X.device, dtype=_f32)
+        L = _lib.lib()
+        for h, idx in enumerate((g.src, g.dst)):
+            _lib.check(L.nbx_gather_rows(E, C, _dp(idx), _dp(X), S * C, C, _at(out, h * C), 2 * S * C, 2 * C, S,
+                                         _st(X)), "nbx_gather_rows")
+        ctx.g = g
+        ctx.shape = (V, S, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        g = ctx.g
+        V, S, C = ctx.shape
+        dout = dout.contiguous()
+        dX = torch.empty(V, S, C, device=dout.device, dtype=_f32)
+        L = _lib.lib()
+        for h, (ptr, eid) in enumerate(((g.sptr, g.seid), (g.dptr, g.deid))):
+            _lib.check(L.nbx_segment_sum(V, C, _dp(ptr), _dp(eid), _at(dout, h * C), 2 * S * C, 2 * C, _dp(dX), S * C,
+                                         C, S, h, _st(dout)), "nbx_segment_sum")
+        return dX, None
+
+
+def gather_pair(X, g):
+    return _GatherPairFn.apply(X, g)
+
+
 class _Step:
     """Per-forward state: the graph, edge frames, distance expansion and dropout settings."""
 
@@ -558,8 +595,7 @@ class _Step:
         m, g, E, V = self.m, self.g, self.E, self.V
         nh, na, nv, H = m.num_heads, m.attn_alpha_channels, m.attn_value_channels, m.attn_hidden_channels
         x_edge = self.x_edge(A)
-        xs, xd = gather(x, g, "s"), gather(x, g, "d")
-        msg = self.rotate(torch.cat([xs, xd], 2))
+        msg = self.rotate(gather_pair(x, g))
         msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
         a_in, gating = torch.split(extra, [nh * na, H], dim=1)
         s2 = torch.split(_S2Fn.apply(msg, *self.grid_attn), [1, msg.shape[1] - 1], dim=1)[1]

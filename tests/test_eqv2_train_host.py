@@ -109,6 +109,7 @@ def torch_ops(monkeypatch):
     monkeypatch.setattr(T, "_f32", torch.float64)
     monkeypatch.setattr(T, "_f", lambda t: t.double())
     monkeypatch.setattr(T, "gather", lambda X, g, w: X[g.src if w == "s" else g.dst])
+    monkeypatch.setattr(T, "gather_pair", lambda X, g: torch.cat([X[g.src], X[g.dst]], 2))
     monkeypatch.setattr(T, "linear", _lin)
     monkeypatch.setattr(T, "act", _act)
     monkeypatch.setattr(T, "_LayerNormFn", _fn(lambda X, w, b, eps: EQ.layer_norm(X, w, b, eps)))
