@@ -1001,8 +1001,9 @@ def bench_eqv2_train(a, rank, world, device, P):
                    "parallelism": f"dp{world}",
                    "execution": "one HIP graph replay per step (forward, backward, clip, fused AdamW)" if graph
                                 else "eager"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_f32_kernel (nbx_gemm_f32: every linear layer of the forward "
-                                               "and backward)",
+        "roofline": {"bound": "mfma", "kernel": "gemm_f32 / gemm_f32_batched kernels (nbx_gemm_f32 / _batched / "
+                                               "_grouped: every linear layer, SO3_LinearV2 and SO2_Convolution of "
+                                               "the forward and backward, each grouped launch timed whole)",
                      "achieved": round(ach, 3) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None, "traffic": None,
                      "avg_launch_us": round(1e3 * gemm_ms / max(n_gemm, 1), 3), "launches_per_step": n_gemm,
