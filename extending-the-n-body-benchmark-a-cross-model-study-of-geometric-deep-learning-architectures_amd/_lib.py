@@ -129,7 +129,7 @@ _SIGNATURES = {
     "nbx_gemm_f32_batched_workspace_bytes": (ctypes.c_int, [c_i32, c_p, ctypes.POINTER(c_sz)]),
     "nbx_gemm_f32_batched": (ctypes.c_int, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_gemm_f32_grouped_workspace_bytes": (ctypes.c_int, [c_i32, c_p, ctypes.POINTER(c_sz)]),
-    "nbx_gemm_f32_grouped": (ctypes.c_int, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_gemm_f32_grouped": (ctypes.c_int, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_tp_prep": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "nbx_tp_prep_backward": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p, c_p]),
     "nbx_tp_post": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),

@@ -56,6 +56,7 @@ struct GemmArgs {
     // at (r / rdiv) o + (r % rdiv) ld -- the (2l + 1) rows of degree l of every node of an
     // [nodes][(lmax + 1)^2][C] array as one [nodes (2l + 1)][C] operand (SO3_LinearV2)
     int64_t rdiv, oa, ob, oc;
+    const float* bias;   // nbx_gemm_f32_grouped: C(r, n) += bias[n] (NULL: none)
 };
 
 __device__ __forceinline__ int64_t row_off(int64_t r, int64_t ld, int64_t outer, int64_t rdiv) {
@@ -160,7 +161,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         const int64_t row = m0 + wm + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
         if (row >= g.M) continue;
         float* p = split ? out + row * ld + col : c_at(out, ld, g.oc, g.rdiv, g.M, g.N, g.tail, row, col);
-        *p = (!split && g.beta != 0.f) ? acc[i] + g.beta * *p : acc[i];
+        const float v = (!split && g.bias) ? acc[i] + g.bias[col] : acc[i];
+        *p = (!split && g.beta != 0.f) ? v + g.beta * *p : v;
     }
 }
 
@@ -213,6 +215,7 @@ struct ReduceBatch {
     float* C[GMAXP];
     int64_t M[GMAXP], N[GMAXP], ldc[GMAXP];
     int64_t rdiv[GMAXP], oc[GMAXP];
+    const float* bias[GMAXP];
     int splits[GMAXP], tail[GMAXP];
     float beta[GMAXP];
     int64_t first[GMAXP + 1];   // first element of each problem in the flattened index
@@ -250,7 +253,8 @@ __global__ void gemm_reduce_batched_kernel(ReduceBatch b) {
         if (q < b.count && i >= b.first[q]) p = q;
     const int64_t e = i - b.first[p], N = b.N[p], MN = b.M[p] * N;
     const int64_t r = e / N, c = e - r * N;
-    const float s = splitk_sum(b.part[p], b.splits[p], MN, e);
+    const float s0 = splitk_sum(b.part[p], b.splits[p], MN, e);
+    const float s = b.bias[p] ? s0 + b.bias[p][c] : s0;
     float* q = c_at(b.C[p], b.ldc[p], b.oc[p], b.rdiv[p], b.M[p], N, b.tail[p], r, c);
     *q = b.beta[p] != 0.f ? s + b.beta[p] * *q : s;
 }
@@ -747,7 +751,8 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     const size_t need = splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
     NBX_CHECK_ARG(workspace_bytes >= need && (need == 0 || workspace), "nbx_gemm_f32: workspace too small (%zu < %zu)",
                   workspace_bytes, need);
-    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones, tail, 1, 0, 0, 0};
+    GemmArgs g{A, B, C, (float*)workspace, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta, ones, tail, 1, 0, 0, 0,
+               nullptr};
     g.kchunk = (g.kchunk + GK - 1) / GK * GK;
     const dim3 grid((unsigned)((N + T - 1) / T), (unsigned)((M + T - 1) / T), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
@@ -806,8 +811,8 @@ int gemm_group_ws(const char* name, int32_t count, const int64_t* dims, int ds, 
 }
 
 int gemm_group(const char* name, int32_t count, const int32_t* flags, const int64_t* dims, int ds,
-               const float* const* A, const float* const* B, float* const* C, const float* beta, void* workspace,
-               size_t workspace_bytes, void* stream) {
+               const float* const* A, const float* const* B, float* const* C, const float* beta,
+               const float* const* bias, void* workspace, size_t workspace_bytes, void* stream) {
     NBX_CHECK_ARG(count >= 1 && count <= GMAXP && flags && dims && A && B && C && beta,
                   "%s: bad arguments (count 1..%d)", name, GMAXP);
     GemmBatch gb;
@@ -833,6 +838,8 @@ int gemm_group(const char* name, int32_t count, const int32_t* flags, const int6
         NBX_CHECK_ARG((!d.oa || d.oa >= d.rdiv * lda) && (!d.ob || d.ob >= d.rdiv * ldb) &&
                       (!d.oc || d.oc >= d.rdiv * ldc), "%s: outer stride below rdiv x leading dimension", name);
         NBX_CHECK_ARG(!(tail && d.oc), "%s: NBX_GEMM_ONES_TAIL with two-level C rows", name);
+        const float* bi = bias ? bias[i] : nullptr;
+        NBX_CHECK_ARG(!(bi && ones), "%s: a bias with NBX_GEMM_B_ONES", name);
         const int splits = gemm_splits(M, N, K, T);
         float* part = nullptr;
         if (splits > 1) {
@@ -842,13 +849,13 @@ int gemm_group(const char* name, int32_t count, const int32_t* flags, const int6
             part = (float*)workspace + ws_off;
             ws_off += need;
             rb.part[nred] = part; rb.C[nred] = C[i]; rb.M[nred] = M; rb.N[nred] = N; rb.ldc[nred] = ldc;
-            rb.rdiv[nred] = d.rdiv; rb.oc[nred] = d.oc;
+            rb.rdiv[nred] = d.rdiv; rb.oc[nred] = d.oc; rb.bias[nred] = bi;
             rb.splits[nred] = splits; rb.tail[nred] = tail; rb.beta[nred] = beta[i];
             rb.first[nred + 1] = rb.first[nred] + M * N;
             ++nred;
         }
         GemmArgs g{A[i], B[i], C[i], part, M, N, K, lda, ldb, ldc, (K + splits - 1) / splits, beta[i], ones, tail,
-                   d.rdiv, d.oa, d.ob, d.oc};
+                   d.rdiv, d.oa, d.ob, d.oc, bi};
         g.kchunk = (g.kchunk + GK - 1) / GK * GK;
         const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0 &&
                          d.oa % 4 == 0 && d.ob % 4 == 0;
@@ -864,8 +871,24 @@ int gemm_group(const char* name, int32_t count, const int32_t* flags, const int6
     gb.count = count;
     rb.count = nred;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(gemm_f32_batched_kernel<GB>, dim3((unsigned)blocks), dim3(GemmCfg<GB>::THREADS), 0, st, gb);
-    NBX_LAUNCH_CHECK("gemm_f32_batched");
+    if (count == 1) {   // one problem: the storage-order-specialised kernel (fewer registers than the grouped one)
+        const dim3 grid((unsigned)gb.tx[0], (unsigned)gb.ty[0], (unsigned)gb.nz[0]), blk(GemmCfg<GB>::THREADS);
+        const GemmArgs& g = gb.g[0];
+        switch (gb.mode[0]) {
+            case 0: hipLaunchKernelGGL((gemm_f32_kernel<false, false, false, GB>), grid, blk, 0, st, g); break;
+            case 1: hipLaunchKernelGGL((gemm_f32_kernel<true, false, false, GB>), grid, blk, 0, st, g); break;
+            case 2: hipLaunchKernelGGL((gemm_f32_kernel<false, true, false, GB>), grid, blk, 0, st, g); break;
+            case 3: hipLaunchKernelGGL((gemm_f32_kernel<true, true, false, GB>), grid, blk, 0, st, g); break;
+            case 4: hipLaunchKernelGGL((gemm_f32_kernel<false, false, true, GB>), grid, blk, 0, st, g); break;
+            case 5: hipLaunchKernelGGL((gemm_f32_kernel<true, false, true, GB>), grid, blk, 0, st, g); break;
+            case 6: hipLaunchKernelGGL((gemm_f32_kernel<false, true, true, GB>), grid, blk, 0, st, g); break;
+            default: hipLaunchKernelGGL((gemm_f32_kernel<true, true, true, GB>), grid, blk, 0, st, g); break;
+        }
+        NBX_LAUNCH_CHECK("gemm_f32");
+    } else {
+        hipLaunchKernelGGL(gemm_f32_batched_kernel<GB>, dim3((unsigned)blocks), dim3(GemmCfg<GB>::THREADS), 0, st, gb);
+        NBX_LAUNCH_CHECK("gemm_f32_batched");
+    }
     if (nred) {
         hipLaunchKernelGGL(gemm_reduce_batched_kernel, dim3(nblk(rb.first[nred])), dim3(256), 0, st, rb);
         NBX_LAUNCH_CHECK("gemm_reduce_batched");
@@ -881,7 +904,8 @@ extern "C" int nbx_gemm_f32_batched_workspace_bytes(int32_t count, const int64_t
 extern "C" int nbx_gemm_f32_batched(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
                                     const float* const* B, float* const* C, const float* beta, void* workspace,
                                     size_t workspace_bytes, void* stream) {
-    return gemm_group("nbx_gemm_f32_batched", count, flags, dims, 6, A, B, C, beta, workspace, workspace_bytes, stream);
+    return gemm_group("nbx_gemm_f32_batched", count, flags, dims, 6, A, B, C, beta, nullptr, workspace, workspace_bytes,
+                      stream);
 }
 
 extern "C" int nbx_gemm_f32_grouped_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes) {
@@ -889,9 +913,10 @@ extern "C" int nbx_gemm_f32_grouped_workspace_bytes(int32_t count, const int64_t
 }
 
 extern "C" int nbx_gemm_f32_grouped(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
-                                    const float* const* B, float* const* C, const float* beta, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
-    return gemm_group("nbx_gemm_f32_grouped", count, flags, dims, 10, A, B, C, beta, workspace, workspace_bytes, stream);
+                                    const float* const* B, float* const* C, const float* beta, const float* const* bias,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+    return gemm_group("nbx_gemm_f32_grouped", count, flags, dims, 10, A, B, C, beta, bias, workspace, workspace_bytes,
+                      stream);
 }
 
 extern "C" int nbx_tp_prep(int64_t rows, int32_t Ks, int32_t Kv, const float* XS, int64_t ldxs, const float* XV,

@@ -234,13 +234,12 @@ class _SO3LinearFn(torch.autograd.Function):
         V, S, cin = X.shape
         cout = W.shape[1]
         Y = torch.empty(V, S, cout, device=X.device, dtype=_f32)
+        # the bias in the l = 0 GEMM's epilogue
         probs = [(_lib.GEMM_TRANS_B, V * (2 * l + 1), cout, cin, _at(X, l * l * cin), cin, _at(W, l * cout * cin), cin,
-                  _at(Y, l * l * cout), cout, 0.0, 2 * l + 1, S * cin, 0, S * cout) for l in range(lmax + 1)]
+                  _at(Y, l * l * cout), cout, 0.0, 2 * l + 1, S * cin, 0, S * cout, _dp(b) if l == 0 else None)
+                 for l in range(lmax + 1)]
         for i in range(0, len(probs), 8):
             gemm_grouped(probs[i:i + 8], X.device)
-        if b is not None:       # the l = 0 rows, in place (each element read once, then written)
-            _lib.check(_lib.lib().nbx_bias_act(V, cout, _dp(Y), S * cout, _dp(b), _lib.ACT_NONE, _dp(Y), S * cout,
-                                               _st(Y)), "nbx_bias_act")
         ctx.save_for_backward(X, W)
         ctx.dims = (lmax, b is not None)
         return Y
@@ -321,24 +320,17 @@ class _SO2ConvFn(torch.autograd.Function):
         out = torch.empty(E, R, cout, device=dev, dtype=_f32)
         extra = torch.empty(E, n_extra, device=dev, dtype=_f32)
         K0 = n0 * cin
-        probs = []
+        probs = []      # fc_m0's bias in the epilogues of its two GEMMs
         if n_extra:
             probs.append((_lib.GEMM_TRANS_B, E, n_extra, K0, A0, lda0, _at(W0, 0), K0, _at(extra, 0), n_extra, 0.0,
-                          1, 0, 0, 0))
+                          1, 0, 0, 0, _dp(b0)))
         probs.append((_lib.GEMM_TRANS_B, E, n0 * cout, K0, A0, lda0, _at(W0, n_extra * K0), K0, _at(out, 0), R * cout,
-                      0.0, 1, 0, 0, 0))
+                      0.0, 1, 0, 0, 0, _at(b0, n_extra) if b0 is not None else None))
         for (ap, lda), Wbm, nm, st in zip(Am, Wb, nms, starts):
             probs.append((_lib.GEMM_TRANS_B, E, 2 * nm * cout, 2 * nm * cin, ap, lda, _at(Wbm, 0), 2 * nm * cin,
                           _at(out, st * cout), R * cout, 0.0, 1, 0, 0, 0))
         for i in range(0, len(probs), 8):
             gemm_grouped(probs[i:i + 8], dev)
-        if b0 is not None:
-            L = _lib.lib()
-            if n_extra:
-                _lib.check(L.nbx_bias_act(E, n_extra, _dp(extra), n_extra, _dp(b0), _lib.ACT_NONE, _dp(extra), n_extra,
-                                          _st(extra)), "nbx_bias_act")
-            _lib.check(L.nbx_bias_act(E, n0 * cout, _dp(out), R * cout, _at(b0, n_extra), _lib.ACT_NONE, _dp(out),
-                                      R * cout, _st(out)), "nbx_bias_act")
         ctx.save_for_backward(x, rad, W0, x0s, *xms, *Wb)
         ctx.meta = (n0, nms, n_extra, starts, roffs, b0 is not None, len(xms))
         return out, extra

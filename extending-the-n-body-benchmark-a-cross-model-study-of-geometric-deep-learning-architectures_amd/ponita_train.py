@@ -28,13 +28,15 @@ import ctypes
 import torch
 
 from . import _lib
-from .segnn_train import Graph, colsum, gemm, gemm_batched, _dp, _st, _ws
+from .segnn_train import Graph, colsum, gemm, gemm_batched, gemm_grouped, _at, _dp, _st, _ws
 
 _f32 = torch.float32
 
 
 class _LinFn(torch.autograd.Function):
-    """Y = act(X W^T + b): X [rows][K] (ld = ldx), W [N][K] (nn.Linear layout), b [N] or None."""
+    """Y = act(X W^T + b): X [rows][K] (ld = ldx), W [N][K] (nn.Linear layout), b [N] or None.  The bias
+    is added in the GEMM's epilogue (nbx_gemm_f32_grouped), so Z = X W^T + b leaves the GEMM and only an
+    activation takes a second launch."""
 
     @staticmethod
     def forward(ctx, X, W, b, act, ldx):
@@ -42,12 +44,14 @@ class _LinFn(torch.autograd.Function):
         rows = X.shape[0]
         N, K = W.shape
         Z = torch.empty(rows, N, device=X.device, dtype=_f32)
-        gemm(_lib.GEMM_TRANS_B, rows, N, K, X, ldx, W, K, Z, N)
-        if b is None and act == _lib.ACT_NONE:
+        if rows and N:
+            gemm_grouped([(_lib.GEMM_TRANS_B, rows, N, K, _at(X, 0), ldx, _at(W, 0), K, _at(Z, 0), N, 0.0, 1, 0, 0, 0,
+                           _dp(b))], X.device)
+        if act == _lib.ACT_NONE:
             Y = Z
         else:
             Y = torch.empty_like(Z)
-            _lib.check(L.nbx_bias_act(rows, N, _dp(Z), N, _dp(b), act, _dp(Y), N, _st(Z)), "nbx_bias_act")
+            _lib.check(L.nbx_bias_act(rows, N, _dp(Z), N, None, act, _dp(Y), N, _st(Z)), "nbx_bias_act")
         ctx.save_for_backward(X, W, b, Z if act != _lib.ACT_NONE else None)
         ctx.dims = (rows, N, K, act, ldx)
         return Y
@@ -63,7 +67,7 @@ class _LinFn(torch.autograd.Function):
             dZ = dY
         else:
             dZ = torch.empty(rows, N, device=dev, dtype=_f32)
-            _lib.check(L.nbx_bias_act_backward(rows, N, _dp(Z), N, _dp(b), act, _dp(dY), _dp(dZ), _st(dZ)),
+            _lib.check(L.nbx_bias_act_backward(rows, N, _dp(Z), N, None, act, _dp(dY), _dp(dZ), _st(dZ)),
                        "nbx_bias_act_backward")
         db = dW = dX = None
         want_b = b is not None and ctx.needs_input_grad[2]

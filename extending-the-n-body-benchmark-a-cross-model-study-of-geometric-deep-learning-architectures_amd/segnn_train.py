@@ -101,8 +101,8 @@ def gemm_batched(problems):
 
 def gemm_grouped(problems, device):
     """Up to 8 GEMMs with two-level rows in one launch (nbx_gemm_f32_grouped): problems
-    ``(flags, M, N, K, A, lda, B, ldb, C, ldc, beta, rdiv, oa, ob, oc)`` where A / B / C are device
-    pointers (ints, e.g. ``_at(t, offset)``); outer strides 0 = plain rows."""
+    ``(flags, M, N, K, A, lda, B, ldb, C, ldc, beta, rdiv, oa, ob, oc[, bias])`` where A / B / C / bias
+    are device pointers (ints, e.g. ``_at(t, offset)``; bias None = none); outer strides 0 = plain rows."""
     problems = [p for p in problems if p[1] > 0 and p[2] > 0]
     if not problems:
         return
@@ -113,13 +113,14 @@ def gemm_grouped(problems, device):
                                          for v in (p[1], p[2], p[3], p[5], p[7], p[9], p[11], p[12], p[13], p[14])])
     ptr = lambda i: (ctypes.c_void_p * n)(*[int(p[i]) for p in problems])
     beta = (ctypes.c_float * n)(*[float(p[10]) for p in problems])
+    bias = (ctypes.c_void_p * n)(*[(int(p[15]) if len(p) > 15 and p[15] else None) for p in problems])
     nb = _lib.c_sz()
     _lib.check(L.nbx_gemm_f32_grouped_workspace_bytes(n, dims, ctypes.byref(nb)), "nbx_gemm_f32_grouped_workspace_bytes")
     ws = _ws(nb.value, device) if nb.value else None
     if gemm_timer is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    _lib.check(L.nbx_gemm_f32_grouped(n, flags, dims, ptr(4), ptr(6), ptr(8), beta, _dp(ws), nb.value,
+    _lib.check(L.nbx_gemm_f32_grouped(n, flags, dims, ptr(4), ptr(6), ptr(8), beta, bias, _dp(ws), nb.value,
                                       _lib.stream_ptr(device)), "nbx_gemm_f32_grouped")
     if gemm_timer is not None:
         ev[1].record()

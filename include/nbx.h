@@ -332,11 +332,13 @@ int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, const float* A,
  * rdiv ld), so the 2l + 1 rows of degree l of every node of an [nodes][(lmax + 1)^2][C] array are one
  * operand of nodes (2l + 1) rows: SO3_LinearV2 (equiformer_v2 so3.py:695-745) forward and backward for
  * all degrees in one launch, without per-degree copies (eqv2_train.py _SO3LinearFn).  Up to 8
- * problems (both grouped entry points since ABI 16); NBX_GEMM_ONES_TAIL needs oc = 0. */
+ * problems (both grouped entry points since ABI 16); NBX_GEMM_ONES_TAIL needs oc = 0.  bias (host array of
+ * count device pointers, or NULL): C(r, n) = op(A) op(B) + bias[i][n] (+ C), the nn.Linear bias in the
+ * GEMM's epilogue / split-K sum (not with NBX_GEMM_B_ONES). */
 int nbx_gemm_f32_grouped_workspace_bytes(int32_t count, const int64_t* dims, size_t* bytes);
 int nbx_gemm_f32_grouped(int32_t count, const int32_t* flags, const int64_t* dims, const float* const* A,
-                         const float* const* B, float* const* C, const float* beta, void* workspace,
-                         size_t workspace_bytes, void* stream);
+                         const float* const* B, float* const* C, const float* beta, const float* const* bias,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* S_in [rows][Ks + Kv] from XS (rows x Ks, leading dimension ldxs), XV [3][rows][Kv], Y3 [rows][3];
  * backward: dXS = dS[:, :Ks] (written when non-NULL), dXV[k] += Y3[:, k] dS[:, Ks:] (accumulated). */

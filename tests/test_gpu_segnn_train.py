@@ -84,6 +84,38 @@ def test_gemm_f32_ones_column(hip_device, flags, M, N, K, ldb_pad):
         assert (Ct[M * N:] == 7.0).all(), batched
 
 
+@pytest.mark.parametrize("M,N,K", [(320, 64, 64), (70, 33, 45), (96, 65, 1280), (5, 7, 3840)])
+def test_gemm_f32_grouped_bias_and_two_level_rows(hip_device, M, N, K):
+    """nbx_gemm_f32_grouped: the epilogue bias (unsplit and split-K shapes) equals the GEMM plus the bias
+    added afterwards bit for bit, and two-level rows (rdiv 3 over an [M/3][5][K] array) equal the
+    same rows copied out."""
+    from nbody_amd.segnn_train import _at
+    g = torch.Generator().manual_seed(M + N + K)
+    d = lambda x: x.to(hip_device).contiguous()
+    A, W, b = d(torch.randn(M, K, generator=g)), d(torch.randn(N, K, generator=g)), d(torch.randn(N, generator=g))
+    C = torch.empty(M, N, device=hip_device)
+    T.gemm_grouped([(_lib.GEMM_TRANS_B, M, N, K, _at(A, 0), K, _at(W, 0), K, _at(C, 0), N, 0.0, 1, 0, 0, 0,
+                     _at(b, 0))], hip_device)
+    C0 = torch.empty(M, N, device=hip_device)
+    T.gemm_grouped([(_lib.GEMM_TRANS_B, M, N, K, _at(A, 0), K, _at(W, 0), K, _at(C0, 0), N, 0.0, 1, 0, 0, 0)],
+                   hip_device)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C0 + b)
+    Mr = (M // 3) * 3
+    if Mr:
+        X = d(torch.randn(M // 3, 5, K, generator=g))          # rows 1..3 of every group of 5
+        Y = torch.full((M // 3, 5, N), 7.0, device=hip_device)
+        T.gemm_grouped([(_lib.GEMM_TRANS_B, Mr, N, K, _at(X, K), K, _at(W, 0), K, _at(Y, N), N, 0.0, 3, 5 * K, 0,
+                         5 * N)], hip_device)
+        Xc = X[:, 1:4].reshape(Mr, K).contiguous()
+        Yc = torch.empty(Mr, N, device=hip_device)
+        T.gemm_grouped([(_lib.GEMM_TRANS_B, Mr, N, K, _at(Xc, 0), K, _at(W, 0), K, _at(Yc, 0), N, 0.0, 1, 0, 0, 0)],
+                       hip_device)
+        torch.cuda.synchronize()
+        assert torch.equal(Y[:, 1:4].reshape(Mr, N), Yc)
+        assert (Y[:, 0] == 7.0).all() and (Y[:, 4] == 7.0).all()
+
+
 def test_gemm_f32_batched_equals_single(hip_device):
     """nbx_gemm_f32_batched (up to 4 GEMMs in one launch + one split-K sum launch) is bit-identical to
     nbx_gemm_f32 on each problem: mixed storage orders, split and unsplit shapes, beta 0 and 1."""
