@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 16
+ABI_VERSION = 17
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B, GEMM_B_ONES, GEMM_ONES_TAIL = 1, 2, 4, 8
@@ -202,6 +202,8 @@ _SIGNATURES = {
                                                c_i64, c_p, c_p, c_sz, c_p]),
     "nbx_segnn_rollout_knn": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
                                              c_i32, c_i64, c_p, c_p, c_p, c_sz, c_p]),
+    "nbx_segnn_range_check": (ctypes.c_int, [c_p, c_sz, c_i64, c_i64, c_i32, c_p]),
+    "nbx_debug_msg_pre_check": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_i32]),
     "nbx_ponita_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_i64, c_i64,
                                                   ctypes.POINTER(c_sz)]),
     "nbx_ponita_forward": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_p, c_p, c_i64, c_i64, c_p, c_p,

@@ -51,6 +51,8 @@ struct MsgPreProb {
     int xcd_group;       // block id -> (chunk, slab) so a slab's chunk blocks share one XCD (per_chunk % 8 == 0)
     unsigned long long* dbg;  // optional per-wave phase clocks (tuning only)
     int no_dot;               // 1: M1S's dot half is not written (message_layer_2 forms it: TpStream DV)
+    int* range_flag;          // fp16x2 range guard (tp_fused.h tp_range_flag), null: off
+    unsigned* check;          // NBX_MP_CHECK builds: hand-off invariant violations are counted here
 };
 
 // helpers (defined in msg_pre.hip, compiled with packed-fp32 VALU disabled: the edge step's

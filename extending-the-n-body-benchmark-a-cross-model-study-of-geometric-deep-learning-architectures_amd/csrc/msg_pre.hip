@@ -26,7 +26,12 @@ constexpr int mp_nbuf(int prec) { return prec == 2 ? 3 : 2; }
 // (X3 runs a static schedule over KCT = ceil(M / 32) K chunks)
 // (PREC 2: the fp16x2 images and v_mfma_f32_16x16x32_f16, 3 terms instead of 6; the node GEMM
 // results are descaled by P.bscale as they are parked in the exchange)
-template <int PREC, int KCT = 0>
+// CHK (NBX_MP_CHECK=1, diagnosis builds of the hand-off; tests/test_gpu_segnn_paths.py): every wave
+// checks the stage tag of the exchange buffer it is about to consume -- the group the four GEMM waves
+// last wrote into it (edge waves) or the group the four edge waves last read from it (GEMM waves) --
+// against the group its counters promised, and counts / printfs each mismatch (block, wave, group).
+// CHK 2 also drops the edge waves' wait (fault injection: shows the check detects a broken hand-off).
+template <int PREC, int KCT = 0, int CHK = 0>
 __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const MsgPreProb P) {
     constexpr bool X3 = PREC != 0;
     // fp16x2 (images the fp32 size): three exchange buffers fit, and the two roles hand them over
@@ -137,6 +142,17 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
     // hand[p] = groups GEMM wave p has written, hand[4 + q] = groups edge wave q has read
     int* hand = reinterpret_cast<int*>(XC + 3 * KC * 32);
     if (DEC && t < 8) hand[t] = 0;
+    // CHK: stage tags gtag[buf][p] = last group GEMM wave p wrote into buffer buf, etag[buf][q] = last
+    // group edge wave q read from it
+    int* gtag = hand + 8;
+    int* etag = gtag + 4 * NBUF;
+    if (CHK && t < 8 * NBUF) gtag[t] = -1;
+    auto chk_fail = [&](int group, int buf, int who, int expect, int got) {
+        const unsigned n = __hip_atomic_fetch_add(P.check, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n < 8)   // the first few of a run
+            printf("msg_pre hand-off mismatch: block %d wave %d group %d buffer %d: tag of wave %d is %d, expected %d\n",
+               (int)blockIdx.x, wave, group, buf, who, got, expect);
+    };
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // relaxed LDS poll until all four counters of a role reach `groups` (the LDS keeps each wave's
@@ -188,14 +204,24 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
         auto write_ex = [&](int buf) {
             if constexpr (DEC)   // buffer `buf` free: the edge waves are done with group i - NBUF
                 if (i >= NBUF) dec_wait(1, i - NBUF + 1);
+            if constexpr (CHK != 0 && DEC) {
+                if (i >= NBUF && lane == 0)
+                    for (int q = 0; q < 4; ++q) {
+                        const int g = __hip_atomic_load(etag + 4 * buf + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (g != i - NBUF) chk_fail(i, buf, 4 + q, i - NBUF, g);
+                    }
+            }
             float* ex = EX + buf * MP_EX + plane * 6 * MP_PART;
+            float z = 0.f;   // fp16x2 range guard (tp_fused.h tp_range_flag)
 #pragma unroll
             for (int j = 0; j < 6; ++j)
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int col = X3 ? (c16 & 3) | (((c16 >> 2) ^ qd) << 2) : c16;   // row (4 qd + jj) >> 2 = qd
                     ex[j * MP_PART + (4 * qd + jj) * MP_RS + col] = PREC == 2 ? acc[j][jj] * P.bscale : acc[j][jj];
+                    if constexpr (PREC == 2) z = tp_nonfinite_fold(z, acc[j][jj]);
                 }
+            if constexpr (PREC == 2) tp_range_flag(P.range_flag, z);
         };
         if (gemm_wave) {
             if (i < my_groups) {
@@ -299,6 +325,10 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
                 for (int kc = 0; kc < KCMAX; ++kc)
                     if (kc < KC) load_a(i + 1, kc, abuf[kc]);
                 write_ex(i % NBUF);
+                if constexpr (CHK != 0 && DEC) {   // stage tag after the data (the LDS keeps a wave's order)
+                    if (lane == 0) __hip_atomic_store(gtag + 4 * (i % NBUF) + plane, i, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
                 if constexpr (DEC) dec_signal(0);
                 tick(c_gemm);
             }
@@ -307,7 +337,16 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
             const float4 geo_cur = geo_next;
             const float pm_cur = pm_next;
             load_geo(i, geo_next, pm_next);
-            if constexpr (DEC) dec_wait(0, i);   // group i - 1 written by all four GEMM waves
+            if constexpr (DEC && CHK != 2) dec_wait(0, i);   // group i - 1 written by all four GEMM waves
+            if constexpr (CHK != 0 && DEC) {
+                if ((t & 63) == 0)
+                    for (int p = 0; p < 4; ++p) {
+                        const int g = __hip_atomic_load(gtag + 4 * ((i - 1) % NBUF) + p, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (g != i - 1) chk_fail(i - 1, (i - 1) % NBUF, p, i - 1, g);
+                    }
+                asm volatile("" ::: "memory");
+            }
             const float* exb = EX + ((i - 1) % NBUF) * MP_EX;
             auto xv = [&](int pl, int part, int row) {
                 const int q = X3 ? cq ^ ((row >> 2) & 3) : cq;
@@ -376,6 +415,13 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
             tick(c_edge);
         }
         if constexpr (DEC) {
+            if constexpr (CHK != 0) {   // this edge wave is done reading group i - 1
+                if (!gemm_wave && i > 0 && (t & 63) == 0) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __hip_atomic_store(etag + 4 * ((i - 1) % NBUF) + (wave & 3), i - 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
             // (every edge wave signals, dead lanes or not)
             if (!gemm_wave && i > 0) dec_signal(1);
         } else {
@@ -395,7 +441,19 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
 
 inline size_t msg_pre_lds_bytes(const MsgPreProb& p) {
     return ((size_t)2 * p.img_floats + mp_nbuf(p.prec) * (p.prec ? MpEx<true>::EX : MpEx<false>::EX) +
-            3 * 32 * ((p.M + 31) / 32)) * 4 + 32;   // + the hand-off counters
+            3 * 32 * ((p.M + 31) / 32)) * 4 + 32 + 4 * 8 * 3;   // + the hand-off counters and stage tags
+}
+
+// NBX_MP_CHECK: the device word the check kernels count hand-off mismatches into (allocated once)
+unsigned* mp_check_word() {
+    static unsigned* w = nullptr;
+    if (!w) {
+        if (hipMalloc(&w, sizeof(unsigned)) != hipSuccess || hipMemset(w, 0, sizeof(unsigned)) != hipSuccess) {
+            set_error("msg_pre: cannot allocate the NBX_MP_CHECK counter");
+            w = nullptr;
+        }
+    }
+    return w;
 }
 
 int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
@@ -434,6 +492,22 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
         NBX_LDS_160K(k);
     const int kct = (p.M + 31) / 32;
     const dim3 grid(p.chunks * p.per_chunk);
+    // NBX_MP_CHECK=1 / 2: the hand-off invariant check (2: with the fault injection) on the fp16x2 path,
+    // counted into a device word read by nbx_debug_msg_pre_check (diagnosis and tests only)
+    static const int chk = getenv("NBX_MP_CHECK") ? atoi(getenv("NBX_MP_CHECK")) : 0;
+    if (chk && p.prec == 2 && p.M % 16 == 0) {
+        p.check = mp_check_word();
+        if (!p.check) return NBX_E_HIP;
+        for (const void* k : {(const void*)msg_pre_kernel<2, 1, 1>, (const void*)msg_pre_kernel<2, 2, 1>,
+                              (const void*)msg_pre_kernel<2, 3, 1>, (const void*)msg_pre_kernel<2, 3, 2>})
+            NBX_LDS_160K(k);
+        if (kct == 3 && chk == 2) hipLaunchKernelGGL((msg_pre_kernel<2, 3, 2>), grid, dim3(MP_THREADS), lds, st, p);
+        else if (kct == 3) hipLaunchKernelGGL((msg_pre_kernel<2, 3, 1>), grid, dim3(MP_THREADS), lds, st, p);
+        else if (kct == 2) hipLaunchKernelGGL((msg_pre_kernel<2, 2, 1>), grid, dim3(MP_THREADS), lds, st, p);
+        else hipLaunchKernelGGL((msg_pre_kernel<2, 1, 1>), grid, dim3(MP_THREADS), lds, st, p);
+        NBX_HIP(hipGetLastError());
+        return NBX_OK;
+    }
     if (p.prec == 2 && kct == 3) NBX_TIMED_LAUNCH((msg_pre_kernel<2, 3>), grid, dim3(MP_THREADS), lds, st, p);
     else if (p.prec == 2 && kct == 2) NBX_TIMED_LAUNCH((msg_pre_kernel<2, 2>), grid, dim3(MP_THREADS), lds, st, p);
     else if (p.prec == 2 && kct == 1) NBX_TIMED_LAUNCH((msg_pre_kernel<2, 1>), grid, dim3(MP_THREADS), lds, st, p);
@@ -446,3 +520,17 @@ int msg_pre_launch(MsgPreProb& p, hipStream_t st, int num_cus) {
 }
 
 }  // namespace nbx
+
+// NBX_MP_CHECK diagnosis: the number of hand-off invariant violations counted so far (0 when the check is off)
+extern "C" int nbx_debug_msg_pre_check(uint32_t* mismatches, int32_t reset) {
+    NBX_CHECK_ARG(mismatches != nullptr, "nbx_debug_msg_pre_check: null output");
+    *mismatches = 0;
+    static const int chk = getenv("NBX_MP_CHECK") ? atoi(getenv("NBX_MP_CHECK")) : 0;
+    if (!chk) return NBX_OK;
+    unsigned* w = nbx::mp_check_word();
+    if (!w) return NBX_E_HIP;
+    NBX_HIP(hipDeviceSynchronize());
+    NBX_HIP(hipMemcpy(mismatches, w, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (reset) NBX_HIP(hipMemset(w, 0, sizeof(unsigned)));
+    return NBX_OK;
+}

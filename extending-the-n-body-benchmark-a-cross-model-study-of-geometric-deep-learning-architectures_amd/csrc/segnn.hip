@@ -168,9 +168,12 @@ __global__ void featurize_embed_kernel(const float* __restrict__ pos, const floa
                                        const float* __restrict__ emb, const float* __restrict__ emb_b, int M,
                                        float* __restrict__ NA, float* __restrict__ EG, float* __restrict__ X,
                                        float* __restrict__ XD, double* __restrict__ zsum, int nzero,
-                                       const int* __restrict__ slot, const float* __restrict__ degv) {
-    // zero the forward's atomic BatchNorm sums (nzero = 0: not in use)
+                                       const int* __restrict__ slot, const float* __restrict__ degv,
+                                       int* __restrict__ range_flag) {
+    // zero the forward's atomic BatchNorm sums (nzero = 0: not in use) and, at the first frame of a call,
+    // its fp16x2 range flag (null: a later frame, which accumulates into the call's flag)
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += gridDim.x * blockDim.x) zsum[i] = 0.0;
+    if (range_flag && blockIdx.x == 0 && threadIdx.x == 0) *range_flag = 0;
     const int64_t n0 = (int64_t)blockIdx.x * FE_NODES;
     const int nn = (int)(V - n0 < FE_NODES ? V - n0 : FE_NODES);
     featurize_nodes<FE_NODES>(pos, vel, 0, mass, V, N, G, emb, emb_b, M, NA, EG, X, XD, n0, nn, slot, degv);
@@ -555,6 +558,7 @@ struct Workspace {
     float* DEG;       // general graphs: [V] in-degree
     unsigned long long* ADJ;   // general graphs: [V] source bit masks
     int* ERR;         // general graphs: [64] validation flags
+    int* RANGE;       // fp16x2 range flag of the call (tp_fused.h tp_range_flag), zeroed by its first featurisation
     double* partial;
     double* bn_sums;  // atomic-mode BatchNorm sums: [2 x NBX_SEGNN_MAX_LAYERS][3][M] (message, feature per layer)
     size_t bytes;
@@ -593,6 +597,7 @@ size_t carve(Workspace* ws, void* base, int64_t B, int64_t N, int M) {
     w.DEG = (float*)take(V, 4);
     w.ADJ = (unsigned long long*)take(V, 8);
     w.ERR = (int*)take(64, 4);
+    w.RANGE = (int*)take(64, 4);
     w.bytes = (off + 255) & ~size_t(255);
     if (ws) *ws = w;
     return w.bytes;
@@ -986,6 +991,12 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     const Dims d = dims_of(B, N, M);
     const int64_t V = d.V, Ep = d.Ep;
     const dim3 ewb(EW_X, EW_Y);
+    // every tensor-product problem of the forward raises the call's fp16x2 range flag
+    auto tp_flagged = [&](int rows, const Dims& dd) {
+        nbx::TpProb p = tp_base(rows, dd);
+        p.range_flag = ws.RANGE;
+        return p;
+    };
 
 
     // update_layer_1 reads its [x | BN(agg)] input straight from X / AGG and the two dot buffers
@@ -1053,7 +1064,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     if (!featurized) {
         hipLaunchKernelGGL(featurize_embed_kernel, dim3((unsigned)nbx::ceil_div(V, FE_NODES)), dim3(fe_threads), 0, st,
                            pos, vel, mass, V, (int)N, (int)d.G, w->emb, w->emb_bias, M, ws.NA, ws.EG, ws.X,
-                           seg_upd && !dv_upd ? ws.XD : nullptr, ws.bn_sums, nzero, slot, degv);
+                           seg_upd && !dv_upd ? ws.XD : nullptr, ws.bn_sums, nzero, slot, degv,
+                           upd == nullptr || upd->frame <= 1 ? ws.RANGE : nullptr);
         NBX_LAUNCH_CHECK("embed");
     }
 
@@ -1098,6 +1110,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 mp.prec = 1;
             }
             mp.no_dot = msg2_dv ? 1 : 0;
+            mp.range_flag = ws.RANGE;
             if (int rc = run_msg_pre(mp, st, tm)) return rc;
         } else if (N > 1) {
             // systems larger than a 16-row tile: node precomputation (plain GEMM, part-major
@@ -1108,7 +1121,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 nbx::TpProb pp[2];
                 for (int part = 0; part < 2; ++part) {
                     nbx::TpProb& p = pp[part];
-                    p = tp_base(part == 0 ? (int)V : (int)(3 * V), d);
+                    p = tp_flagged(part == 0 ? (int)V : (int)(3 * V), d);
                     p.As = ws.X + (part ? V * M : 0);
                     p.lda_s = M;
                     p.B = (part ? L.node_pre_v_img : L.node_pre_s_img) + half * 3 * KC * 512;
@@ -1130,7 +1143,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         int wpc_msg = 1, cw_msg = 16;
         {
             // message_layer_2 + gate + aggregation + message-BN partial sums
-            nbx::TpProb p = tp_base((int)Ep, d);
+            nbx::TpProb p = tp_flagged((int)Ep, d);
             p.As = ws.M1S; p.lda_s = 2 * M; p.B = L.msg2_img;
             p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
             p.Av = ws.M1V; p.lda_v = M; p.plane_stride = Ep * M; p.Kv = M;
@@ -1173,7 +1186,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             // update_layer_1 + gate, input segments [x_s | a_s | x_v.na | a_v.na] and [x_v | a_v]
             // read from X / AGG / XD / AD with the pending feature BN and the message BN applied
             // per (segment, channel) as the A chunks are consumed
-            nbx::TpProb p = tp_base((int)V, d);
+            nbx::TpProb p = tp_flagged((int)V, d);
             p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M; p.Kv = 2 * M;
             p.lda_s = 4 * M; p.lda_v = 2 * M;
             p.seg_s[0] = ws.X; p.seg_s[1] = ws.AGG; p.seg_s[2] = ws.XD; p.seg_s[3] = ws.AD;
@@ -1211,7 +1224,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             NBX_LAUNCH_CHECK("upd_pre");
             {
                 // update_layer_1 + gate -> inputs of update_layer_2
-                nbx::TpProb p = tp_base((int)V, d);
+                nbx::TpProb p = tp_flagged((int)V, d);
                 p.As = ws.U1S; p.lda_s = 4 * M; p.B = L.upd1_img;
                 p.K[0] = 4 * M; p.K[1] = 4 * M; p.K[2] = 2 * M;
                 p.Av = ws.U1V; p.lda_v = 2 * M; p.plane_stride = V * 2 * M;
@@ -1224,7 +1237,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
         int wpc_feat;
         {
             // update_layer_2 + residual + feature-BN partial sums
-            nbx::TpProb p = tp_base((int)V, d);
+            nbx::TpProb p = tp_flagged((int)V, d);
             p.As = ws.U2S; p.lda_s = 2 * M; p.B = L.upd2_img;
             p.K[0] = 2 * M; p.K[1] = M;
             p.Av = ws.U2V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
@@ -1275,7 +1288,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     // segment from X and XD (x_v . na) with the scale / shift applied as the A chunks are consumed
     // (static schedules at mul 96 / 32), else materialised by pp_pre_kernel
     if (seg_upd) {
-        nbx::TpProb p = tp_base((int)V, d);
+        nbx::TpProb p = tp_flagged((int)V, d);
         p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M; p.Kv = M;
         p.lda_s = 2 * M; p.lda_v = M;
         p.seg_s[0] = ws.X; p.seg_s[1] = ws.XD; p.seg_v[0] = ws.X + V * M; p.seg_vplane = V * M;
@@ -1308,7 +1321,7 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
     hipLaunchKernelGGL(pp_pre_kernel, ew_grid(V, M), ewb, 0, st, ws.X, ws.NA,
                        w->num_layers > 0 ? ws.coef_feat : nullptr, V, M, ws.U1S, ws.U1V);
     {
-        nbx::TpProb p = tp_base((int)V, d);
+        nbx::TpProb p = tp_flagged((int)V, d);
         p.As = ws.U1S; p.lda_s = 2 * M; p.B = w->pp1_img;
         p.K[0] = 2 * M; p.K[1] = 2 * M; p.K[2] = M;
         p.Av = ws.U1V; p.lda_v = M; p.plane_stride = V * M; p.Kv = M;
@@ -1440,6 +1453,24 @@ extern "C" int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, flo
         const RolloutUpdate upd{pos, vel, traj_pos, traj_vel, f, num_frames, (int)N, 0,
                                 (flags & NBX_ROLLOUT_ABSOLUTE) ? 1 : 0};
         if (int rc = forward_impl(w, pos, vel, mass, B, N, ws.out, ws, st, nullptr, &upd, false, &gr)) return rc;
+    }
+    return NBX_OK;
+}
+
+extern "C" int nbx_segnn_range_check(const void* workspace, size_t workspace_bytes, int64_t B, int64_t N, int32_t mul,
+                                     void* stream) {
+    NBX_CHECK_ARG(workspace != nullptr && B >= 1 && N >= 1 && mul > 0, "nbx_segnn_range_check: bad arguments");
+    Workspace ws;
+    const size_t need = carve(&ws, const_cast<void*>(workspace), B, N, mul);
+    NBX_CHECK_ARG(workspace_bytes >= need, "nbx_segnn_range_check: workspace too small (%zu < %zu bytes)",
+                  workspace_bytes, need);
+    int flag = 0;
+    NBX_HIP(hipMemcpyAsync(&flag, ws.RANGE, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    NBX_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (flag) {
+        nbx::set_error("segnn: a tensor-product operand left the fp16 range of the fp16x2 split path (|a| >= 65520) "
+                       "or the input is not finite; the bf16x3 path (NBX_SPLIT=x3) keeps the fp32 exponent range");
+        return NBX_E_RANGE;
     }
     return NBX_OK;
 }

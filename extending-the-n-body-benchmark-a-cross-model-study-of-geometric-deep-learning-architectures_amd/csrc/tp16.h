@@ -481,15 +481,23 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                             if constexpr (u + 1 < n) read_b(std::integral_constant<int, TS::item(pos + 1)>{}, bx[(u + 1) % NBS]);
                             float av[8];
                             if constexpr (der) {
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) av[e] = dacc[e];
+                                // the dot chunk, then its segment's BatchNorm scale: the same arithmetic as
+                                // the materialised operand (producer dot of the stored values, scale applied
+                                // by item_a as the chunk is consumed), so both paths give identical bits
+                                const float4 dc[2] = {float4{dacc[0], dacc[1], dacc[2], dacc[3]},
+                                                      float4{dacc[4], dacc[5], dacc[6], dacc[7]}};
+                                item_a(std::integral_constant<int, item>{}, dc, av);
                             } else {
                                 item_a(std::integral_constant<int, item>{}, ring[l % PF], av);
                                 if constexpr (SK::DV && TS::plane(pos) >= 0) {
+                                    // dot of the stored (unscaled) values, in the producers' fmaf order
                                     constexpr int pl = TS::plane(pos);
+                                    const float4 (&cb)[2] = ring[l % PF];
+                                    const float raw[8] = {cb[0].x, cb[0].y, cb[0].z, cb[0].w,
+                                                          cb[1].x, cb[1].y, cb[1].z, cb[1].w};
 #pragma unroll
                                     for (int e = 0; e < 8; ++e)
-                                        dacc[e] = pl == 0 ? av[e] * yv[0] : __builtin_fmaf(av[e], yv[pl], dacc[e]);
+                                        dacc[e] = pl == 0 ? raw[e] * yv[0] : __builtin_fmaf(raw[e], yv[pl], dacc[e]);
                                 }
                             }
                             SP::split(float4{av[0], av[1], av[2], av[3]}, float4{av[4], av[5], av[6], av[7]}, ax[u % 3]);
@@ -619,11 +627,17 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                 }
             }
 
-            if constexpr (SK::PREC == 2) {   // undo the fp16x2 image's weight scale
+            if constexpr (SK::PREC == 2) {   // undo the fp16x2 image's weight scale; range guard
+                float z = 0.f;
 #pragma unroll
                 for (int g = 0; g < CG; ++g)
 #pragma unroll
-                    for (int j = 0; j < NS + 3 * NV; ++j) acc[g][j] *= P.bscale;
+                    for (int j = 0; j < NS + 3 * NV; ++j) {
+                        acc[g][j] *= P.bscale;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) z = tp_nonfinite_fold(z, acc[g][j][e]);
+                    }
+                tp_range_flag(P.range_flag, z);
             }
             if (P.dbg) { const unsigned long long c = clock64(); c_loop += c - c_mark; c_mark = c; }
             // ------------------------------------------------------------ epilogue
@@ -715,7 +729,7 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         const float h2 = gg * (na[3] * tt + acc[g][NS + 2][jj]);
                         st_out<false>(&P.out_s[(size_t)row * 2 * M + ch], hs);
                         if (!P.skip_gate_dot)
-                            st_out<false>(&P.out_s[(size_t)row * 2 * M + M + ch], h0 * na[1] + h1 * na[2] + h2 * na[3]);
+                            st_out<false>(&P.out_s[(size_t)row * 2 * M + M + ch], fmaf(h2, na[3], fmaf(h1, na[2], h0 * na[1])));
                         st_out<false>(&P.out_v[(size_t)row * M + ch], h0);
                         st_out<false>(&P.out_v[P.out_plane + (size_t)row * M + ch], h1);
                         st_out<false>(&P.out_v[2 * P.out_plane + (size_t)row * M + ch], h2);
@@ -742,7 +756,7 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                         const float v0 = xv_sc * rres[g][jj][1] + (na[1] * tt + acc[g][NS + 0][jj]);
                         const float v1 = xv_sc * rres[g][jj][2] + (na[2] * tt + acc[g][NS + 1][jj]);
                         const float v2 = xv_sc * rres[g][jj][3] + (na[3] * tt + acc[g][NS + 2][jj]);
-                        if (P.out_dot) st_out<true>(&P.out_dot[(size_t)row * M + ch], v0 * na[1] + v1 * na[2] + v2 * na[3]);
+                        if (P.out_dot) st_out<true>(&P.out_dot[(size_t)row * M + ch], fmaf(v2, na[3], fmaf(v1, na[2], v0 * na[1])));
                         st_out<true>(x0, v0); st_out<true>(x1, v1); st_out<true>(x2, v2);
                         st0[g] += (double)s;
                         st1[g] += (double)s * s;

@@ -224,7 +224,19 @@ struct TpProb {
     int xcd_groups;
     // GATE_NODE: 1 = the [h_v . na] half of out_s is not written (its consumer forms it: TpStream DV)
     int skip_gate_dot;
+    // fp16x2 range guard (tp_range_flag): set to 1 when a tile's accumulators are not finite; null: off
+    int* range_flag;
 };
+
+// fp16x2 operand range guard.  An A operand with |a| >= 65520 rounds to an fp16 infinity (the split
+// keeps fp32 accuracy everywhere below that), and every product it enters is then inf
+// or NaN.  z = the sum over a tile's accumulators of acc * 0 is NaN exactly when one of them is not
+// finite; the lane raises the call's flag (a vector store of a constant: racing lanes agree), which
+// the host reads after the call and reports as NBX_E_RANGE instead of returning non-finite values.
+__device__ inline float tp_nonfinite_fold(float z, float a) { return __builtin_fmaf(a, 0.f, z); }
+__device__ inline void tp_range_flag(int* flag, float z) {
+    if (flag != nullptr && !(z == 0.f)) *flag = 1;
+}
 
 // block id -> (chunk group, row-range block): chunk-major, or XCD-grouped (TpProb::xcd_groups)
 __device__ inline void tp_block_map(const TpProb& P, int bidx, int& group, int& blk) {
@@ -768,8 +780,14 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
             }
 
             if constexpr (SK::PREC == 2) {   // undo the fp16x2 image's weight scale
+                float z = 0.f;
 #pragma unroll
-                for (int j = 0; j < NS + 3 * NV; ++j) acc[j] *= P.bscale;
+                for (int j = 0; j < NS + 3 * NV; ++j) {
+                    acc[j] *= P.bscale;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) z = tp_nonfinite_fold(z, acc[j][e]);
+                }
+                tp_range_flag(P.range_flag, z);
             }
             if (P.dbg) c_loop = clock64();
             // ------------------------------------------------------------ epilogue
@@ -829,7 +847,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void tp_fused_kernel(c
                         st_out<true>(&P.out_v[2 * P.out_plane + o], a3);
                         if (P.out_dot) {
                             const float4 na4 = gn[(row - row0) >> lg];
-                            st_out<true>(&P.out_dot[o], a1 * na4.y + a2 * na4.z + a3 * na4.w);
+                            st_out<true>(&P.out_dot[o], fmaf(a3, na4.w, fmaf(a2, na4.z, a1 * na4.y)));
                         }
                     }
                 };

@@ -186,6 +186,9 @@ class SEGNN(nn.Module):
         # rollout semantics, infer_self_feed.py never calls eval()); "batch" / "running" force
         # batch statistics (running stats updated) / the running statistics
         self.bn_mode = None
+        # fp16x2 range guard after every native forward / rollout (include/nbx.h nbx_segnn_range_check):
+        # NbxError instead of non-finite results when an operand leaves the fp16 range of the split path
+        self.range_check = True
 
     # ------------------------------------------------------------ reference API
     def get_model_size(self):
@@ -751,6 +754,7 @@ class SEGNN(nn.Module):
                 _lib.dev_ptr(out), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
                 "nbx_segnn_forward_graph")
         self._bn_sync_out()
+        self._range_check(B, N, device)
         return out.to(out_dtype)
 
     @torch.no_grad()
@@ -783,4 +787,18 @@ class SEGNN(nn.Module):
                 int(num_neighbors), _lib.dev_ptr(tp), _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(),
                 _lib.stream_ptr(device)), "nbx_segnn_rollout_knn")
         self._bn_sync_out()
+        self._range_check(B, N, device)
         return tp, tv
+
+    def _range_check(self, B, N, device):
+        """fp16x2 range guard (include/nbx.h nbx_segnn_range_check): NbxError when a tensor-product operand
+        of the call left the fp16 range of the split path (or an input was not finite) instead of returning
+        non-finite values.  One stream synchronisation per call; skipped while a HIP graph is being
+        captured (call ``check_range`` after a replay) and when ``range_check`` is False."""
+        if self.range_check and not torch.cuda.is_current_stream_capturing():
+            self.check_range(B, N, device)
+
+    def check_range(self, B, N, device=None):
+        device = device if device is not None else self._ws.device
+        _lib.check(_lib.lib().nbx_segnn_range_check(_lib.dev_ptr(self._ws), self._ws.numel(), B, N, self.mul,
+                                                    _lib.stream_ptr(device)), "segnn")

@@ -22,13 +22,14 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 16
+#define NBX_ABI_VERSION 17
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
 #define NBX_E_UNSUPPORTED 2 /* configuration outside the native path */
 #define NBX_E_HIP 3        /* HIP runtime error (message has details) */
 #define NBX_E_WORKSPACE 4  /* workspace too small */
+#define NBX_E_RANGE 5      /* an fp16x2 tensor-product operand left the fp16 range (nbx_segnn_range_check) */
 
 /* rollout flags */
 #define NBX_ROLLOUT_ABSOLUTE 1 /* the model predicts absolute positions: pos = pred[:, :3] (every dataset target
@@ -287,6 +288,25 @@ int nbx_segnn_rollout_knn(const nbx_segnn_weights* w, float* pos, float* vel, co
                           int64_t batch_size, int64_t num_nodes, int64_t num_frames, int32_t flags,
                           int64_t num_neighbors, float* traj_pos, float* traj_vel, void* workspace,
                           size_t workspace_bytes, void* stream);
+
+/* fp16x2 range guard (ABI 17).  The fp16x2 split tensor products (include/nbx.h "fp16x2 images", the
+ * default SEGNN path) represent an fp32 operand a as hi + lo, both fp16: fp32-accurate for |a| < 65504,
+ * while an operand at |a| >= 65520 rounds to an fp16 infinity.  Every split-precision kernel of a
+ * nbx_segnn_forward / _forward_graph / _rollout / _rollout_knn call raises a flag in the call's
+ * workspace when one of its output tiles is not finite (such an operand, or a non-finite input);
+ * the flag covers every frame of a rollout.  This call waits for `stream`, reads the flag of the last
+ * call made with `workspace` and returns NBX_E_RANGE (with a message) if it is set, NBX_OK otherwise.
+ * The fp32 MFMA and bf16x3 paths (NBX_X3=0, NBX_SPLIT=x3) have the fp32 exponent range.  Synchronises. */
+int nbx_segnn_range_check(const void* workspace, size_t workspace_bytes, int64_t batch_size, int64_t num_nodes,
+                          int32_t mul, void* stream);
+
+/* Diagnosis of msg_pre's exchange-buffer hand-off (ABI 17).  With the environment variable
+ * NBX_MP_CHECK=1 set before the first SEGNN call, the fp16x2 message_layer_1 kernel runs an instantiation in
+ * which every wave checks the stage tag of the exchange buffer it consumes (the group its hand-off
+ * counters promise) and counts and printfs each mismatch; NBX_MP_CHECK=2 also drops the edge waves' wait
+ * (fault injection, for the test that the check fires).  Writes the count so far (0 when the check is
+ * off) and resets it if `reset`.  Synchronises the device. */
+int nbx_debug_msg_pre_check(uint32_t* mismatches, int32_t reset);
 
 
 /* ------------------------------------------------------------------------

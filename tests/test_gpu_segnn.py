@@ -357,64 +357,95 @@ def c2_fixture():
     return np.load(p)
 
 
+def c2_ensemble():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "segnn_c2_ensemble.npz"))
+
+
+def ensemble_agreement(sys_err, k):
+    """Per-system agreement at step k: the threshold tau_k = 10 x the median over the ensemble members
+    of each member's median per-system error; returns (tau_k, each member's fraction of systems
+    within tau_k)."""
+    tau = 10.0 * float(np.median(np.median(sys_err[:, k, :], axis=1)))
+    return tau, (sys_err[:, k, :] <= tau).mean(1)
+
+
+def c2_rollout_envelope_check(tp, tv, rl, rv, ens, label="device"):
+    """Places a C2 rollout (positions tp, velocities tv [B, T, N, 3]) in the ensemble of equally valid
+    fp32 computations (tests/golden/make_segnn_c2_ensemble.py).  Returns the list of failed checks:
+    at every step k >= 1, pos and vel MSE vs the fp64 oracle <= the ensemble's largest, and the
+    fraction of systems within the step's agreement threshold >= the ensemble's smallest."""
+    B, T = tp.shape[0], tp.shape[1]
+    bad = []
+    for k in range(1, T):
+        ml = float(((tp[:, k] - rl[:, k]) ** 2).mean())
+        mv = float(((tv[:, k] - rv[:, k]) ** 2).mean())
+        se = np.abs(tp[:, k] - rl[:, k]).reshape(B, -1).max(1) / np.abs(rl[:, k]).max()
+        tau, fr_ens = ensemble_agreement(ens["sys_err"], k)
+        fr = float((se <= tau).mean())
+        el, ev = ens["mse_loc"][:, k], ens["mse_vel"][:, k]
+        rank = int((el < ml).sum())
+        print(f"C2 rollout step {k} ({label}): pos MSE {ml:.2e} (ensemble {el.min():.1e}..{el.max():.1e}, "
+              f"{rank} of {len(el)} members closer) vel MSE {mv:.2e} (ensemble max {ev.max():.1e}) | systems "
+              f"within {tau:.1e}: {fr:.4f} (ensemble min {fr_ens.min():.4f}, median {np.median(fr_ens):.4f})")
+        if ml > el.max():
+            bad.append((k, "pos MSE above the ensemble", ml, float(el.max())))
+        if mv > ev.max():
+            bad.append((k, "vel MSE above the ensemble", mv, float(ev.max())))
+        if fr < fr_ens.min():
+            bad.append((k, "per-system agreement below the ensemble", fr, float(fr_ens.min())))
+    return bad
+
+
 def test_rollout_c2_matches_oracle_fixture(hip_device):
     """north_star: rollout MSE <= 1e-5 vs the reference at C2 (hidden 192, 6 layers, N=5,
     B=1024, train-mode BatchNorm, GravitySim initial states), against the fp64 oracle rollout
-    of tests/golden/make_segnn_c2.py.
+    of tests/golden/make_segnn_c2.py, over 10 steps.
 
-    With random-init weights this rollout turns chaotic within a few steps (bodies are flung to
+    With random-init weights this rollout turns chaotic after ~5 steps (bodies are flung to
     |pos| ~ 50-75 and pairs pass within ~1e-3 of each other, where r-hat is ill-conditioned;
-    train-mode BatchNorm couples every system to the outliers).  The fixture therefore also holds
-    the same oracle rollout computed entirely in fp32 arithmetic (the divergence fp32 rounding
-    alone produces) and from states one fp32 ulp away (the reference's own sensitivity).
-    Checks, per step k:
-      * over the predictable horizon (every step where the fp32 oracle itself stays within MSE 1e-7
-        of the fp64 one; 5 steps here): MSE(device, oracle) <= 1e-5 (north_star) and <= 10x the
-        fp32-oracle MSE;
-      * beyond it the trajectories of equally valid fp32 computations separate (chaos): system 595
-        passes a near-collision at step 6 and train-mode BatchNorm spreads its divergence to every
-        system.  Measured step-6 MSE vs fp64 (profiles/r05/roll/rollout_paths.txt): fp32-MFMA path
-        (NBX_X3=0) 2.6e-4, fp16x2 with register-formed dot operands (default) 1.9e-4, bf16x3 and the
-        materialised-dot fp16x2 path 2.4e-6, the all-fp32 oracle 3.7e-7 -- an accuracy bound there
-        would rank rounding orders, not correctness.  Past the horizon the test checks that the
-        trajectories stay finite and physical (|pos| within 4x the oracle's largest); the predictable
-        120-step horizon of the same model and workload is test_rollout_c2_long_horizon_matches_oracle.
-    Per-step errors are printed (measured: the device is 1.5-80x closer to fp64 than the fp32
-    oracle over steps 1-5)."""
+    system 595 passes a near-collision at step 6 and train-mode BatchNorm couples every system to it).
+    Past that point one fp32 sample cannot separate "another valid rounding" from "worse", so the
+    check is against an ENSEMBLE of 41 equally valid fp32 computations of the same rollout
+    (tests/golden/make_segnn_c2_ensemble.py: the numpy and torch fp32 restatements, systems permuted,
+    edge lists shuffled, every GEMM's contraction order permuted, a quarter of the systems rounded to
+    the neighbouring fp32 value, and fp64 rollouts from such states).  At step 6 the ensemble's pos MSE
+    spans 7.1e-9 .. 3.7e-4 (the torch fp32 restatement in its natural order: 1.7e-4).
+    Checks, per step k = 1..10:
+      * pos and vel MSE(device, fp64 oracle) <= the largest of the ensemble;
+      * the fraction of systems whose error (max over its bodies / max |pos| of the frame) is within
+        tau_k = 10 x the ensemble's median per-system error >= the smallest fraction of any member;
+      * over the predictable horizon (every step where the numpy fp32 oracle stays within MSE 1e-7 of
+        the fp64 one; 5 steps here): MSE <= 1e-5 (north_star) and <= 10x the fp32-oracle MSE.
+    Where the kernel paths fall in the ensemble: DESIGN.md §3.5c (scripts/rollout_paths.py)."""
     import nbody_amd.segnn as S2
     fx = c2_fixture()
+    ens = c2_ensemble()
+    assert float(ens["weight_checksum"]) == float(fx["weight_checksum"])
     torch.manual_seed(0)
     model = S2.SEGNN(hidden_features=192, num_layers=6)
     cs = float(sum(t.double().abs().sum().item() for t in model.state_dict().values()))
     assert abs(cs - float(fx["weight_checksum"])) <= 1e-9 * abs(cs), "C2 weights differ from the fixture's"
     model = model.to(hip_device).train()
     rl, rv = fx["traj_loc"].astype(np.float64), fx["traj_vel"].astype(np.float64)
-    fl, pl = fx["f32_loc"].astype(np.float64), fx["pert_loc"].astype(np.float64)
+    fl = fx["f32_loc"].astype(np.float64)
     T = rl.shape[1]
     t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
     tp, tv = model.rollout(t(fx["loc0"]), t(fx["vel0"]), t(np.ones(fx["loc0"].shape[:2] + (1,))), T)
     tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
+    assert np.isfinite(tp).all() and np.isfinite(tv).all()
+    bad = c2_rollout_envelope_check(tp, tv, rl, rv, ens)
     horizon = 0
     for k in range(1, T):
         mse = float(((tp[:, k] - rl[:, k]) ** 2).mean())
         f32 = float(((fl[:, k] - rl[:, k]) ** 2).mean())
-        sens = float(((pl[:, k] - rl[:, k]) ** 2).mean())
-        sys_err = np.abs(tp[:, k] - rl[:, k]).reshape(tp.shape[0], -1).max(1) / np.abs(rl[:, k]).max()
-        print(f"C2 rollout step {k}: pos MSE {mse:.3e} (fp32 oracle {f32:.3e}, one-ulp input change {sens:.3e}), "
-              f"max rel err pos {sys_err.max():.3e} (median over systems {np.median(sys_err):.3e}), vel "
-              f"{np.abs(tv[:, k] - rv[:, k]).max() / np.abs(rv[:, k]).max():.3e}")
         if f32 <= 1e-7 and horizon == k - 1:
             horizon = k
-            assert mse <= 1e-5, (k, mse)
-            assert mse <= 10.0 * f32 + 1e-13, (k, mse, f32)
-        else:
-            # beyond the horizon the rollout is chaotic and equally valid fp32 computations separate
-            # (docstring); the trajectory must stay physical
-            assert np.abs(tp[:, k]).max() <= 4.0 * np.abs(rl[:, k]).max(), k
-    assert horizon >= 4, horizon
-    assert np.isfinite(tp).all() and np.isfinite(tv).all()
+            if mse > 1e-5 or mse > 10.0 * f32 + 1e-13:
+                bad.append((k, "horizon MSE", mse, f32))
     print(f"C2 predictable horizon (fp32 oracle within MSE 1e-7 of fp64): {horizon} steps")
-    assert horizon >= 4
+    assert horizon >= 4, horizon
+    assert not bad, bad
 
 
 def test_forward_mul128_repeats_and_matches_oracle(hip_device):
