@@ -2,6 +2,7 @@
 #include <mutex>
 #include <set>
 #include <utility>
+#include <vector>
 
 #include "nbx_internal.h"
 
@@ -26,12 +27,19 @@ int hip_error(hipError_t e, const char* where) {
 int lds_limit_160k(const void* kernel) {
     static std::mutex mu;
     static std::set<std::pair<const void*, int>> done;
+    // lock-free fast path on every launch after the first: this thread's cache of the (kernel, device)
+    // pairs already raised (a few dozen entries, scanned linearly)
+    thread_local std::vector<std::pair<const void*, int>> seen;
     int dev = 0;
     NBX_HIP(hipGetDevice(&dev));
+    for (const auto& e : seen)
+        if (e.first == kernel && e.second == dev) return NBX_OK;
     std::lock_guard<std::mutex> lk(mu);
-    if (done.count({kernel, dev})) return NBX_OK;
-    NBX_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    done.insert({kernel, dev});
+    if (!done.count({kernel, dev})) {
+        NBX_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        done.insert({kernel, dev});
+    }
+    seen.emplace_back(kernel, dev);
     return NBX_OK;
 }
 

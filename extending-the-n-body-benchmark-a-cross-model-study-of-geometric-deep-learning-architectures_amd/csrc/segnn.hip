@@ -1210,6 +1210,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                     : M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm)
                               : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
                 if (rc) return rc;
+            } else if (dv_upd) {   // (upd_dv implies the branch above; XD / AD were not written)
+                nbx::set_error("segnn: internal: register-dot update_layer_1 decision without its schedule");
+                return NBX_E_INVAL;
             } else if (M == 96 && L.upd1_img_x3 && split_prec() == 1) {
                 p.B = static_cast<const float*>(L.upd1_img_x3);
                 if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_X3>(p, st, tm)) return rc;
@@ -1259,6 +1262,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                     : M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2>(p, st, tm)
                               : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2>(p, st, tm);
                 if (rc) return rc;
+            } else if (upd2_dv) {   // (update_layer_1 skipped the [h_v . na] half this consumer would read)
+                nbx::set_error("segnn: internal: register-dot update_layer_2 decision without its schedule");
+                return NBX_E_INVAL;
             } else {
                 if (int rc = run_tp16_try<2, 1, nbx::TP_RESID, 1, 1, SK_UPD2, SK_UPD2_32>(p, st, tm)) return rc;
             }
@@ -1312,6 +1318,9 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 : M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG_H2>(p, st, tm)
                           : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_32_SEG_H2>(p, st, tm);
             if (rc) return rc;
+        } else if (dv_upd) {   // (upd_dv implies the branch above; XD was not written)
+            nbx::set_error("segnn: internal: register-dot pre_pool1 decision without its schedule");
+            return NBX_E_INVAL;
         } else if (M == 96) {
             if (int rc = run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_PP1_SEG>(p, st, tm)) return rc;
         } else {

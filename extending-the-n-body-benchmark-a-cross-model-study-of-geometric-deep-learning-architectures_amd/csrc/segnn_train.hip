@@ -517,6 +517,14 @@ __global__ void bn_stats_kernel(int nb, int64_t rows_arg, int M, const double* _
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= M) return;
     const double rows = count ? *count : (double)rows_arg;   // SyncBN: the all-reduced row count
+    if (!(rows > 0.0)) {
+        // no row anywhere (an empty batch without an all-reduced count): no statistics exist; the
+        // running statistics stay as they are and the saved coefficients are the identity
+        save[c] = 0.f;
+        save[M + c] = 1.f;
+        save[2 * M + c] = 1.f;
+        return;
+    }
     double a = 0.0, b = 0.0, e = 0.0;
 #pragma unroll 8
     for (int i = 0; i < nb; ++i) {

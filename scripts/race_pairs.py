@@ -2,7 +2,7 @@
 runs K pairs of forwards, every pair on a new seeded batch, and compares the two results of a pair:
 train-mode reruns agree to ~1e-6 relative (fp64 atomic BatchNorm sums), so a system off by more than
 1e-3 of the output scale in either call is a corrupted forward.
-usage: python scripts/r05_pairs.py K "<env>" ["<env>" ...]   (env: A=1,B=2; '' = defaults)
+usage: python scripts/race_pairs.py K "<env>" ["<env>" ...]   (env: A=1,B=2; '' = defaults)
 PAIRS_EVAL=1: eval-mode BatchNorm."""
 import multiprocessing as mp
 import os

@@ -3,7 +3,7 @@ setting) runs K eval-mode forwards on K different seeded batches in one process;
 every forward with the fp32-MFMA path (NBX_X3=0: no split precision, no decoupled msg_pre hand-off)
 computed the same way in its own child.  Paths differ by float rounding only (<= ~1e-5 relative);
 a system off by more than 1e-3 of the output scale is reported.
-usage: python scripts/r05_xcheck.py K "<env>" ["<env>" ...]   (env: A=1,B=2; '' = defaults)
+usage: python scripts/race_xcheck.py K "<env>" ["<env>" ...]   (env: A=1,B=2; '' = defaults)
 XCHECK_TRAIN=1: train-mode BatchNorm (batch statistics over the 1024 systems)."""
 import multiprocessing as mp
 import os

@@ -20,14 +20,12 @@ def child(env, q):
     try:
         import torch
         import nbody_amd.segnn as S
-        fx = np.load(os.path.join(ROOT, "tests", "golden", "segnn_c2_rollout.npz"))
+        import test_gpu_segnn as TG
         torch.manual_seed(0)
         dev = torch.device("cuda:0")
         model = S.SEGNN(hidden_features=192, num_layers=6).to(dev).train()
-        t = lambda a: torch.tensor(a, dtype=torch.float32, device=dev)
-        T = fx["traj_loc"].shape[1]
-        tp, tv = model.rollout(t(fx["loc0"]), t(fx["vel0"]), t(np.ones(fx["loc0"].shape[:2] + (1,))), T)
-        q.put((tp.double().cpu().numpy(), tv.double().cpu().numpy()))
+        samples, _ = TG.c2_device_samples(model, TG.c2_fixture(), TG.c2_ensemble(), dev)
+        q.put(samples)
     except Exception as e:  # surfaced by the parent
         import traceback
         q.put(repr(e) + traceback.format_exc())
@@ -36,9 +34,7 @@ def child(env, q):
 if __name__ == "__main__":
     import test_gpu_segnn as TG
     envs = [dict(kv.split("=", 1) for kv in a.split(",")) if a else {} for a in sys.argv[1:]] or [{}]
-    fx = TG.c2_fixture()
     ens = TG.c2_ensemble()
-    rl, rv = fx["traj_loc"].astype(np.float64), fx["traj_vel"].astype(np.float64)
     ctx = mp.get_context("spawn")
     for env in envs:
         q = ctx.Queue()
@@ -50,5 +46,8 @@ if __name__ == "__main__":
         if isinstance(r, str):
             print(f"{tag}: FAILED {r}", flush=True)
             continue
-        bad = TG.c2_rollout_envelope_check(r[0], r[1], rl, rv, ens, label=tag)
+        for i, smp in enumerate(r):   # each sample alone: where single draws land
+            single = TG.c2_rollout_envelope_check(smp[None], ens, label=f"{tag} sample {i}", q=1.0)
+            print(f"-- {tag} sample {i}: {'inside' if not single else f'{len(single)} checks outside'}", flush=True)
+        bad = TG.c2_rollout_envelope_check(r, ens, label=tag)
         print(f"== {tag}: {'inside the ensemble at every step' if not bad else bad}", flush=True)
