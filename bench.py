@@ -366,12 +366,14 @@ def pmc_traffic(kernel_name, model=None):
 
 
 # ---------------------------------------------------------------- C3 PONITA
-# rocprofv3 names at C3 with the bf16x3 images (ponita.hip lin_auto: PREC = 1, NT by the image's LDS size;
-# the ConvNext MLP fused into po_ffn_kernel; kind 2 (linear_2 alone) only runs on the unfused path)
-PONITA_KIND_NAMES = ["void nbx::lin_kernel<4, 0, 1, 1>(nbx::LinProb)",
-                     "void (anonymous namespace)::po_ffn_kernel<4, 4, 0>((anonymous namespace)::FfnProb)",
+# rocprofv3 names at C3 (ponita.hip lin_auto: PREC = 2 with the fp16x2 images, the default since r06, 1 with
+# the bf16x3 ones (NBX_PO_SPLIT=x3); NT by the image's LDS size; the ConvNext MLP fused into po_ffn_kernel;
+# kind 2 (linear_2 alone) only runs on the unfused path)
+_PO_PREC = "1" if os.environ.get("NBX_PO_SPLIT", "")[:1] in ("x", "1") else "2"
+PONITA_KIND_NAMES = [f"void nbx::lin_kernel<4, 0, 1, {_PO_PREC}>(nbx::LinProb)",
+                     f"void (anonymous namespace)::po_ffn_kernel<4, 4, 0, {_PO_PREC}>((anonymous namespace)::FfnProb)",
                      "void nbx::lin_rp_kernel<4, 0>(nbx::LinRpProb)",
-                     "void (anonymous namespace)::po_ffn_kernel<1, 4, 1>((anonymous namespace)::FfnProb)",
+                     f"void (anonymous namespace)::po_ffn_kernel<1, 4, 1, {_PO_PREC}>((anonymous namespace)::FfnProb)",
                      "void (anonymous namespace)::po_fiber_ln1_kernel<20, 4, 512>(float const*, float const*, int, "
                      "float const*, float const*, float const*, long, int, int, int, int, float*, double*)"]
 PONITA_KIND_ROLES = ["FiberBundleConv spatial kernel GEMM + gather/aggregate epilogue",

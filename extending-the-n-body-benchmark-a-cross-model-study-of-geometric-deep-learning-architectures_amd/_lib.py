@@ -72,14 +72,16 @@ PONITA_MAX_LAYERS = 64
 class PonitaLayer(ctypes.Structure):
     _fields_ = [(n, c_p) for n in ("kernel_t", "conv_bias", "norm_w", "norm_b", "lin1_t", "lin1_b", "lin2_t",
                                    "lin2_b", "layer_scale", "readout_w", "readout_b", "kernel_img_x3",
-                                   "lin1_img_x3", "lin2_img_x3", "ffn_img_x3")]
+                                   "lin1_img_x3", "lin2_img_x3", "ffn_img_x3", "ffn_img_h2", "kernel_img_h2")] + [
+        (n, c_f) for n in ("ffn_h2_s1inv", "ffn_h2_s2inv", "kernel_h2_sinv", "h2_pad")]
 
 
 class PonitaWeights(ctypes.Structure):
     _fields_ = [(n, c_i32) for n in ("hidden", "basis_dim", "widening", "num_layers", "num_ori")] + [
         (n, c_p) for n in ("ori_grid", "basis1_t", "basis1_b", "basis2_t", "basis2_b", "fbasis1_t", "fbasis1_b",
-                           "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w", "basis2_img_x3", "basis_ffn_img_x3")] + [
-        ("layers", PonitaLayer * PONITA_MAX_LAYERS)]
+                           "fbasis2_t", "fbasis2_b", "fiber_t", "embed_w", "basis2_img_x3", "basis_ffn_img_x3",
+                           "basis_ffn_img_h2")] + [
+        ("basis_ffn_h2_s1inv", c_f), ("basis_ffn_h2_s2inv", c_f), ("layers", PonitaLayer * PONITA_MAX_LAYERS)]
 
 
 EQV2_MAX_LAYERS = 32
@@ -93,7 +95,8 @@ class Eqv2Radial(ctypes.Structure):
 class Eqv2Attn(ctypes.Structure):
     _fields_ = [("rad", Eqv2Radial)] + [(n, c_p) for n in (
         "fc0_x3", "fc0_b", "fc1_x3", "c20_x3", "c20_b", "c21_x3", "alpha_norm_w", "alpha_norm_b", "alpha_dot",
-        "proj_t", "proj_b")]
+        "proj_t", "proj_b", "w2_h2", "fc0_h2", "fc1_h2", "c20_h2", "c21_h2")] + [
+        (n, c_f) for n in ("w2_sinv", "fc0_sinv", "fc1_sinv", "c20_sinv", "c21_sinv", "h2_pad")]
 
 
 class Eqv2Block(ctypes.Structure):
@@ -203,6 +206,8 @@ _SIGNATURES = {
     "nbx_segnn_rollout_knn": (ctypes.c_int, [ctypes.POINTER(SegnnWeights), c_p, c_p, c_p, c_i64, c_i64, c_i64,
                                              c_i32, c_i64, c_p, c_p, c_p, c_sz, c_p]),
     "nbx_segnn_range_check": (ctypes.c_int, [c_p, c_sz, c_i64, c_i64, c_i32, c_p]),
+    "nbx_ponita_range_check": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_p, c_sz, c_i64, c_i64, c_p]),
+    "nbx_eqv2_range_check": (ctypes.c_int, [ctypes.POINTER(Eqv2Weights), c_p, c_sz, c_i64, c_i64, c_p]),
     "nbx_debug_msg_pre_check": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_i32]),
     "nbx_ponita_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(PonitaWeights), c_i64, c_i64,
                                                   ctypes.POINTER(c_sz)]),

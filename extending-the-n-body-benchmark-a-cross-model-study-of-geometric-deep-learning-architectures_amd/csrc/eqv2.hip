@@ -763,6 +763,7 @@ __global__ __launch_bounds__(64) void eqv2_node_block_kernel(const NodeArgs A, i
 struct EqWs {
     float *rot, *H2, *A0, *A1, *Y0, *Y1, *Z0, *Z1, *L, *V0, *V1, *X, *XN, *out;
     int* zn;
+    int* RANGE;   // [64]: the call's fp16x2 range flag (tp_fused.h tp_range_flag)
     int ld0, ldv0, ldv1;
 };
 
@@ -831,6 +832,7 @@ size_t eqv2_carve(EqWs* ws, void* base, const nbx_eqv2_weights* w, int64_t B, in
     s.X = (float*)take(V * 9 * C, 4);
     s.XN = (float*)take(V * 9 * C, 4);
     s.out = (float*)take(V * 6, 4);
+    s.RANGE = (int*)take(64, 4);
     if (ws) *ws = s;
     return (off + 255) & ~size_t(255);
 }
@@ -855,27 +857,45 @@ int radial(const nbx_eqv2_weights* w, const nbx_eqv2_radial& R, const EqWs& ws, 
     return nbx::lin_launch<1, nbx::ACT_NONE, nbx::LIN_LNSILU>(p, st);
 }
 
-// x3 GEMM: Y[rows][ldy] = A[rows][K] W^T (+ bias), N padded to 32
-int gemm_x3(const float* A, int K, int rows, const void* Wx3, int N, const float* bias, float* Y, int ldy,
-            hipStream_t st) {
+// the fp16x2 images when the weights carry them (NBX_EQ_SPLIT=x3: the bf16x3 images, A/B only)
+bool eq_h2_enabled() {
+    static const bool on = !(getenv("NBX_EQ_SPLIT") && (getenv("NBX_EQ_SPLIT")[0] == 'x' || getenv("NBX_EQ_SPLIT")[0] == '1'));
+    return on;
+}
+
+// split-precision GEMM: Y[rows][ldy] = A[rows][K] W^T (+ bias), N padded to 32; on the fp16x2 image (Wh2,
+// descaled by sinv, raising `flag` on a non-finite tile) when given and enabled, else the bf16x3 one
+int gemm_x3(const float* A, int K, int rows, const void* Wx3, const void* Wh2, float sinv, int* flag, int N,
+            const float* bias, float* Y, int ldy, hipStream_t st) {
     nbx::LinProb p = nbx::lin_dense(A, K, K, rows, nullptr, K, N, bias, Y, ldy);
     p.Wx3 = Wx3;
+    if (Wh2 && eq_h2_enabled()) {
+        p.Wh2 = Wh2;
+        p.h2_sinv = sinv;
+        p.range_flag = flag;
+        return nbx::lin_launch<2, nbx::ACT_NONE, nbx::LIN_STORE, 2>(p, st);
+    }
     return nbx::lin_launch<2, nbx::ACT_NONE, nbx::LIN_STORE, 1>(p, st);
 }
 
-// row-panel x3 GEMM over all N = 32 ntiles columns (chunk-major image; lin.h lin_rp_kernel)
-int gemm_rp(const float* A, int K, int rows, const void* Wx3, int ntiles, const float* bias, float* Y, int ldy,
-            hipStream_t st) {
-    nbx::LinRpProb p{A, K, rows, K, Wx3, bias, Y, ldy, 32 * ntiles, nullptr, 0, nullptr};
+// row-panel split-precision GEMM over all N = 32 ntiles columns (chunk-major image; lin.h lin_rp_kernel)
+template <int PREC>
+int gemm_rp_p(const nbx::LinRpProb& p, int ntiles, hipStream_t st) {
     switch (ntiles) {
-        case 4: return nbx::lin_rp_launch<4, nbx::ACT_NONE>(p, st);
-        case 5: return nbx::lin_rp_launch<5, nbx::ACT_NONE>(p, st);
-        case 8: return nbx::lin_rp_launch<8, nbx::ACT_NONE>(p, st);
-        case 9: return nbx::lin_rp_launch<9, nbx::ACT_NONE>(p, st);
+        case 4: return nbx::lin_rp_launch<4, nbx::ACT_NONE, PREC>(p, st);
+        case 5: return nbx::lin_rp_launch<5, nbx::ACT_NONE, PREC>(p, st);
+        case 8: return nbx::lin_rp_launch<8, nbx::ACT_NONE, PREC>(p, st);
+        case 9: return nbx::lin_rp_launch<9, nbx::ACT_NONE, PREC>(p, st);
         default:
             nbx::set_error("eqv2: no row-panel GEMM for %d column tiles", ntiles);
             return NBX_E_UNSUPPORTED;
     }
+}
+int gemm_rp(const float* A, int K, int rows, const void* Wx3, const void* Wh2, float sinv, int* flag, int ntiles,
+            const float* bias, float* Y, int ldy, hipStream_t st) {
+    const bool h2 = Wh2 && eq_h2_enabled();
+    nbx::LinRpProb p{A, K, rows, K, h2 ? Wh2 : Wx3, bias, Y, ldy, 32 * ntiles, nullptr, 0, nullptr, sinv, flag};
+    return h2 ? gemm_rp_p<2>(p, ntiles, st) : gemm_rp_p<1>(p, ntiles, st);
 }
 
 // SO2EquivariantGraphAttention (transformer_block.py:226-370) up to the per-edge values and logits
@@ -895,22 +915,31 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
         TScope ts(1, st, 2.0 * e * He * 10 * C, f4 * e * (He + 14 * C + 25));
         nbx::LinProb p = nbx::lin_dense(ws.H2, He, He, iE, nullptr, He, 10 * C, Aw.rad.b2, nullptr, 0);
         p.Wx3 = Aw.rad.w2_x3;
+        p.Wh2 = Aw.w2_h2;
+        p.h2_sinv = Aw.w2_sinv;
+        p.range_flag = ws.RANGE;
         p.eq_x = ws.XN;
         p.eq_rot = ws.rot;
         p.eq_a0 = ws.A0;
         p.eq_a1 = ws.A1;
         p.eq_C = C;
         p.eq_nodes = N;
-        if (int rc = nbx::lin_launch<5, nbx::ACT_NONE, nbx::LIN_EQMSG, 1>(p, st)) return rc;
+        const int rc = p.Wh2 && eq_h2_enabled() ? nbx::lin_launch<5, nbx::ACT_NONE, nbx::LIN_EQMSG, 2>(p, st)
+                                                : nbx::lin_launch<5, nbx::ACT_NONE, nbx::LIN_EQMSG, 1>(p, st);
+        if (rc) return rc;
     }
     const int n0 = ceil32(nh * w->alpha_channels + 4 * H);
     {
         TScope ts(2, st, 2.0 * e * 6 * C * n0r, f4 * e * (6 * C + n0r));
-        if (int rc = gemm_rp(ws.A0, 6 * C, iE, Aw.fc0_x3, n0 / 32, Aw.fc0_b, ws.Y0, ws.ld0, st)) return rc;
+        if (int rc = gemm_rp(ws.A0, 6 * C, iE, Aw.fc0_x3, Aw.fc0_h2, Aw.fc0_sinv, ws.RANGE, n0 / 32, Aw.fc0_b, ws.Y0,
+                             ws.ld0, st))
+            return rc;
     }
     {
         TScope ts(3, st, 2.0 * 2 * e * 4 * C * 4 * H, f4 * 2 * e * (4 * C + 4 * H));
-        if (int rc = gemm_rp(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, 4 * H / 32, nullptr, ws.Y1, 4 * H, st)) return rc;
+        if (int rc = gemm_rp(ws.A1, 4 * C, 2 * iE, Aw.fc1_x3, Aw.fc1_h2, Aw.fc1_sinv, ws.RANGE, 4 * H / 32, nullptr,
+                             ws.Y1, 4 * H, st))
+            return rc;
     }
     S2Args s{ws.Y0, ws.ld0, ws.Y1, w->grid_attn_to, w->grid_attn_from, Aw.alpha_norm_w, Aw.alpha_norm_b,
              Aw.alpha_dot, nh, w->alpha_channels, H, E, ws.Z0, ws.Z1, ws.L};
@@ -928,8 +957,12 @@ int attention_edges(const nbx_eqv2_weights* w, const nbx_eqv2_attn& Aw, const Eq
     }
     {
         TScope ts(5, st, 2.0 * e * (3 * H * 3 * KV + 2 * 2 * H * 4 * KV), f4 * e * (7 * H + 11 * KV));
-        if (int rc = gemm_x3(ws.Z0, 3 * H, iE, Aw.c20_x3, ws.ldv0, Aw.c20_b, ws.V0, ws.ldv0, st)) return rc;
-        if (int rc = gemm_x3(ws.Z1, 2 * H, 2 * iE, Aw.c21_x3, ws.ldv1, nullptr, ws.V1, ws.ldv1, st)) return rc;
+        if (int rc = gemm_x3(ws.Z0, 3 * H, iE, Aw.c20_x3, Aw.c20_h2, Aw.c20_sinv, ws.RANGE, ws.ldv0, Aw.c20_b, ws.V0,
+                             ws.ldv0, st))
+            return rc;
+        if (int rc = gemm_x3(ws.Z1, 2 * H, 2 * iE, Aw.c21_x3, Aw.c21_h2, Aw.c21_sinv, ws.RANGE, ws.ldv1, nullptr, ws.V1,
+                             ws.ldv1, st))
+            return rc;
     }
     (void)KV;
     return NBX_OK;
@@ -1081,6 +1114,7 @@ extern "C" int nbx_eqv2_forward(const nbx_eqv2_weights* w, const float* pos, con
                                 size_t workspace_bytes, void* stream) {
     EqWs ws;
     if (int rc = eqv2_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), (hipStream_t)stream));
     return eqv2_forward_impl(w, pos, vel, mass, B, N, gauge, seed, 0, out, ws, (hipStream_t)stream);
 }
 
@@ -1092,6 +1126,7 @@ extern "C" int nbx_eqv2_forward_timed(const nbx_eqv2_weights* w, const float* po
     EqWs ws;
     if (int rc = eqv2_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     hipStream_t st = (hipStream_t)stream;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), st));
     static EqTimer T;
     static bool made = false;
     if (!made) {
@@ -1131,6 +1166,7 @@ extern "C" int nbx_eqv2_rollout(const nbx_eqv2_weights* w, float* pos, float* ve
     if (int rc = eqv2_prepare(w, B, N, workspace, workspace_bytes, &ws)) return rc;
     NBX_CHECK_ARG(num_frames >= 1, "nbx_eqv2_rollout: frames >= 1");
     hipStream_t st = (hipStream_t)stream;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), st));
     const int64_t V = B * N;
     hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
                        (int64_t)0, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
@@ -1171,5 +1207,20 @@ extern "C" int nbx_eqv2_edges(int64_t B, int64_t N, const float* pos, const floa
     NBX_LAUNCH_CHECK("eqv2 edges");
     hipLaunchKernelGGL(eqv2_dsel_kernel, dim3(g1(E)), dim3(256), 0, st, E, rot_scratch, nullptr, dist);
     NBX_LAUNCH_CHECK("eqv2 edge distances");
+    return NBX_OK;
+}
+
+extern "C" int nbx_eqv2_range_check(const nbx_eqv2_weights* w, const void* workspace, size_t workspace_bytes, int64_t B,
+                                    int64_t N, void* stream) {
+    EqWs ws;
+    if (int rc = eqv2_prepare(w, B, N, const_cast<void*>(workspace), workspace_bytes, &ws)) return rc;
+    int flag = 0;
+    NBX_HIP(hipMemcpyAsync(&flag, ws.RANGE, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    NBX_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (flag) {
+        nbx::set_error("eqv2: a GEMM operand left the fp16 range of the fp16x2 split path (|a| >= 65520) or the "
+                       "input is not finite; the bf16x3 path (NBX_EQ_SPLIT=x3) keeps the fp32 exponent range");
+        return NBX_E_RANGE;
+    }
     return NBX_OK;
 }

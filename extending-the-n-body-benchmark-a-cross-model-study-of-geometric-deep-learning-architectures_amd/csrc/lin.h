@@ -39,6 +39,12 @@ struct LinProb {
     // sub-tile): [N/32 column tiles][Ktot/32 chunks][part 3][m 2][lane 64][8] bf16; when set (and N %
     // 32 == 0) lin_auto runs the PREC = 1 kernel: fp32-accurate products on v_mfma_f32_32x32x16_bf16
     const void* Wx3;
+    // optional fp16x2 image of Wt (include/nbx.h "fp16x2 images", the Wx3 layout with two fp16 parts,
+    // W s = hi + lo) with h2_sinv = 1 / s: lin_auto runs the PREC = 2 kernel (three fp16 products per fp32
+    // product); range_flag: the call's fp16x2 range flag (tp_fused.h tp_range_flag), or null
+    const void* Wh2;
+    float h2_sinv;
+    int* range_flag;
     const float* bias;  // [N] or null
     float* Y;           // [rows][ldy] (may be null when only the row dot is wanted)
     int ldy;
@@ -95,6 +101,7 @@ __device__ inline float lin_act(float x, int act) {
 // the fp32 sum of the six leading cross products on v_mfma_f32_32x32x16_bf16 (12 x 32 cycles
 // instead of 16 x 64).
 constexpr int LIN_X3_BLK = 1536;   // floats of one (column tile, 32-deep chunk) bf16x3 block
+constexpr int LIN_H2_BLK = 1024;   // the same block of an fp16x2 image (two fp16 parts)
 
 template <int NT, int ACT, int EPI = LIN_STORE, int PREC = 0>
 __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
@@ -107,11 +114,12 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     const int n0 = chunk * NT * 32;
     const int n_chunks = P.Ktot >> 5;
 
-    if constexpr (PREC == 1) {
-        // ---- stage the block's column tiles of the bf16x3 image (contiguous) in LDS
+    constexpr int BLK = PREC == 2 ? LIN_H2_BLK : LIN_X3_BLK;
+    if constexpr (PREC >= 1) {
+        // ---- stage the block's column tiles of the bf16x3 / fp16x2 image (contiguous) in LDS
         const int tiles = min(NT, (P.N >> 5) - chunk * NT);
-        tp_dma_image<LIN_WAVES>(reinterpret_cast<const float*>(P.Wx3) + (size_t)chunk * NT * n_chunks * LIN_X3_BLK,
-                                lds, tiles * n_chunks * LIN_X3_BLK);
+        tp_dma_image<LIN_WAVES>(reinterpret_cast<const float*>(PREC == 2 ? P.Wh2 : P.Wx3) + (size_t)chunk * NT * n_chunks * BLK,
+                                lds, tiles * n_chunks * BLK);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
         // ---- stage Wt[n0 : n0 + NT*32, :] in LDS
@@ -196,25 +204,30 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
         auto consume = [&](const float4 (&cur)[4], int k0) {
-            if constexpr (PREC == 1) {
+            if constexpr (PREC >= 1) {
                 // lane (r, h) holds k = 16 h + 4 q + e of the chunk; MFMA m takes k = 16 h + 8 m + j
-                bf16x8 a[3][2];
-                tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
-                tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
-                const bf16x8* ldsx = reinterpret_cast<const bf16x8*>(lds);
+                using SP = SplitP<PREC>;
+                using SPT = typename SP::T;
+                SPT a[SP::NP][2];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    SPT t3[SP::NP];
+                    SP::split(cur[2 * m], cur[2 * m + 1], t3);
+#pragma unroll
+                    for (int p3 = 0; p3 < SP::NP; ++p3) a[p3][m] = t3[p3];
+                }
+                const SPT* ldsx = reinterpret_cast<const SPT*>(lds);
                 const int kc = k0 >> 5;
 #pragma unroll
                 for (int j = 0; j < NT; ++j) {
-                    const bf16x8* bp = ldsx + (j * n_chunks + kc) * (LIN_X3_BLK / 4) + lane;
+                    const SPT* bp = ldsx + (j * n_chunks + kc) * (BLK / 4) + lane;
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {   // block [part p][m][lane][8]: smallest terms first
-                        const bf16x8 b0 = bp[m * 64], b1 = bp[(2 + m) * 64], b2 = bp[(4 + m) * 64];
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b0, acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b1, acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b2, acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b0, acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b1, acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b0, acc[j], 0, 0, 0);
+                        SPT b[SP::NP];
+#pragma unroll
+                        for (int p3 = 0; p3 < SP::NP; ++p3) b[p3] = bp[(2 * p3 + m) * 64];
+#pragma unroll
+                        for (int tt = 0; tt < SP::NT; ++tt) acc[j] = mfma32x32(a[SP::TA[tt]][m], b[SP::TB[tt]], acc[j]);
                     }
                 }
                 return;
@@ -259,6 +272,21 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
                 tile_rows(nrt, n0r, n1r, n2r, nok);
                 load_a(n0r, n1r, n2r, nok, 0, bA);
             }
+        }
+        if constexpr (PREC == 2) {   // undo the image's weight scale; fp16x2 range guard
+            float z = 0.f;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                // (a column tile past N was not staged: its accumulators hold whatever the LDS held and
+                // are never stored, so they stay out of the guard)
+                const bool live_tile = n0 + 32 * j < P.N;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    acc[j][e] *= P.h2_sinv;
+                    if (live_tile) z = tp_nonfinite_fold(z, acc[j][e]);
+                }
+            }
+            tp_range_flag(P.range_flag, z);
         }
         // ---- epilogue: col = n0 + 32 j + r; row = rt*32 + (e&3) + 8(e>>2) + 4h
         if constexpr (EPI == LIN_EQMSG) {
@@ -437,9 +465,10 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
     }
 }
 
-// LDS bytes of a block's weight slice: fp32 rows with pitch, or NT bf16x3 column tiles
+// LDS bytes of a block's weight slice: fp32 rows with pitch, or NT bf16x3 / fp16x2 column tiles
 inline size_t lin_lds_bytes(int nt, int Ktot, int prec) {
-    return prec ? (size_t)nt * (Ktot >> 5) * LIN_X3_BLK * 4 : (size_t)nt * 32 * (((Ktot + 31) & ~31) + 4) * 4;
+    return prec ? (size_t)nt * (Ktot >> 5) * (prec == 2 ? LIN_H2_BLK : LIN_X3_BLK) * 4
+                : (size_t)nt * 32 * (((Ktot + 31) & ~31) + 4) * 4;
 }
 
 template <int NT, int ACT, int EPI = LIN_STORE, int PREC = 0>
@@ -449,8 +478,8 @@ int lin_launch(LinProb& p, hipStream_t st, int num_cus = 256) {
         set_error("lin: Ktot must be a multiple of 32 (got %d)", p.Ktot);
         return NBX_E_INVAL;
     }
-    if (PREC == 1 && (!p.Wx3 || p.N % 32)) {
-        set_error("lin: the split-precision path needs a bf16x3 image and N %% 32 == 0");
+    if ((PREC == 1 && !p.Wx3) || (PREC == 2 && !p.Wh2) || (PREC && p.N % 32)) {
+        set_error("lin: the split-precision path needs its image and N %% 32 == 0");
         return NBX_E_INVAL;
     }
     for (int s = 0; s < p.nseg; ++s)   // buffer-load offsets are 32-bit, OOB sentinel at 2 GiB
@@ -502,14 +531,21 @@ struct LinRpProb {
     const float* resid; // optional: Y = R + scale (.) act(...)  (R may alias Y)
     int ldr;
     const float* scale; // optional per-column scale (layer_scale)
+    // PREC 2 (an fp16x2 image in Wx3's place, W s = hi + lo): h2_sinv = 1 / s; the call's range flag
+    float h2_sinv;
+    int* range_flag;
 };
 
 constexpr int RP_WAVES = 8;
 
-template <int NTILES, int ACT>
+// PREC 1: bf16x3 image blocks (six products per fp32 product); PREC 2: fp16x2 blocks (three)
+template <int NTILES, int ACT, int PREC = 1>
 __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpProb P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    constexpr int SLAB = NTILES * LIN_X3_BLK;          // floats of one K chunk of every column tile
+    using SP = SplitP<PREC>;
+    using SPT = typename SP::T;
+    constexpr int BLK = PREC == 2 ? LIN_H2_BLK : LIN_X3_BLK;
+    constexpr int SLAB = NTILES * BLK;                 // floats of one K chunk of every column tile
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
     const int nk = P.K >> 5;
     const int rt = blockIdx.x * RP_WAVES + wave;
@@ -529,22 +565,29 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
     for (int j = 0; j < NTILES; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    // one A register buffer: a chunk is split into hi / mid / lo bf16 first, then the next chunk's A
-    // load is issued into the same registers and lands while this chunk's MFMAs run
-    auto mfmas = [&](const bf16x8 (&a)[3][2], const float* buf) {
-        const bf16x8* ldsx = reinterpret_cast<const bf16x8*>(buf);
+    // one A register buffer: a chunk is split into its parts first, then the next chunk's A load is
+    // issued into the same registers and lands while this chunk's MFMAs run
+    auto split_a = [&](const float4 (&cur)[4], SPT (&a)[SP::NP][2]) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            SPT t3[SP::NP];
+            SP::split(cur[2 * m], cur[2 * m + 1], t3);
+#pragma unroll
+            for (int p3 = 0; p3 < SP::NP; ++p3) a[p3][m] = t3[p3];
+        }
+    };
+    auto mfmas = [&](const SPT (&a)[SP::NP][2], const float* buf) {
+        const SPT* ldsx = reinterpret_cast<const SPT*>(buf);
 #pragma unroll
         for (int j = 0; j < NTILES; ++j) {
-            const bf16x8* bp = ldsx + j * (LIN_X3_BLK / 4) + lane;
+            const SPT* bp = ldsx + j * (BLK / 4) + lane;
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {   // smallest terms first (as lin_kernel PREC 1)
-                const bf16x8 b0 = bp[m * 64], b1 = bp[(2 + m) * 64], b2 = bp[(4 + m) * 64];
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b0, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b1, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b2, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b0, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b1, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b0, acc[j], 0, 0, 0);
+            for (int m = 0; m < 2; ++m) {   // smallest terms first (as lin_kernel)
+                SPT b[SP::NP];
+#pragma unroll
+                for (int p3 = 0; p3 < SP::NP; ++p3) b[p3] = bp[(2 * p3 + m) * 64];
+#pragma unroll
+                for (int tt = 0; tt < SP::NT; ++tt) acc[j] = mfma32x32(a[SP::TA[tt]][m], b[SP::TB[tt]], acc[j]);
             }
         }
     };
@@ -552,8 +595,8 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
         // small panels (N <= 160): three LDS slabs and two A register buffers, both streams issued two
         // chunks ahead.  At the end of chunk kc only chunk kc + 2's slab pieces and A loads may still be
         // in flight: vmcnt(this wave's slab pieces + 4) (the slab pieces per wave are counted so the
-        // immediate is exact).
-        const int ndma = (6 * NTILES - wave + RP_WAVES - 1) / RP_WAVES;
+        // immediate is exact; a slab is BLK / 256 pieces per column tile).
+        const int ndma = ((BLK / 256) * NTILES - wave + RP_WAVES - 1) / RP_WAVES;
         auto wait_all_but_one_chunk = [&]() {
             switch (ndma) {
                 case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
@@ -575,9 +618,8 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
         }
         __builtin_amdgcn_s_barrier();
         auto step = [&](int kc, float4 (&cur)[4]) {
-            bf16x8 a[3][2];
-            tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
-            tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+            SPT a[SP::NP][2];
+            split_a(cur, a);
             const bool ahead = kc + 2 < nk;
             if (ahead) {
                 tp_dma_image<RP_WAVES>(W + (size_t)(kc + 2) * SLAB, lds + ((kc + 2) % 3) * SLAB, SLAB);
@@ -602,9 +644,8 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         for (int kc = 0; kc < nk; ++kc) {
-            bf16x8 a[3][2];
-            tp_split3(cur[0], cur[1], a[0][0], a[1][0], a[2][0]);
-            tp_split3(cur[2], cur[3], a[0][1], a[1][1], a[2][1]);
+            SPT a[SP::NP][2];
+            split_a(cur, a);
             if (kc + 1 < nk) {
                 load_a(kc + 1, cur);
                 tp_dma_image<RP_WAVES>(W + (size_t)(kc + 1) * SLAB, lds + ((kc + 1) & 1) * SLAB, SLAB);
@@ -614,6 +655,17 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
         }
+    }
+    if constexpr (PREC == 2) {   // undo the image's weight scale; fp16x2 range guard
+        float z = 0.f;
+#pragma unroll
+        for (int j = 0; j < NTILES; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                acc[j][e] *= P.h2_sinv;
+                z = tp_nonfinite_fold(z, acc[j][e]);
+            }
+        tp_range_flag(P.range_flag, z);
     }
 #pragma unroll
     for (int j = 0; j < NTILES; ++j) {
@@ -640,7 +692,7 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
     }
 }
 
-template <int NTILES, int ACT>
+template <int NTILES, int ACT, int PREC = 1>
 int lin_rp_launch(const LinRpProb& p, hipStream_t st) {
     if (p.rows <= 0) return NBX_OK;
     if (p.K % 32 || !p.Wx3 || p.N > NTILES * 32) {
@@ -651,10 +703,10 @@ int lin_rp_launch(const LinRpProb& p, hipStream_t st) {
         set_error("lin_rp: A spans >= 2 GiB");
         return NBX_E_UNSUPPORTED;
     }
-    const size_t lds = (NTILES <= 5 ? 3 : 2) * (size_t)NTILES * LIN_X3_BLK * 4;
-    NBX_LDS_160K((lin_rp_kernel<NTILES, ACT>));
+    const size_t lds = (NTILES <= 5 ? 3 : 2) * (size_t)NTILES * (PREC == 2 ? LIN_H2_BLK : LIN_X3_BLK) * 4;
+    NBX_LDS_160K((lin_rp_kernel<NTILES, ACT, PREC>));
     const unsigned blocks = (unsigned)((p.rows + 32 * RP_WAVES - 1) / (32 * RP_WAVES));
-    hipLaunchKernelGGL((lin_rp_kernel<NTILES, ACT>), dim3(blocks), dim3(64 * RP_WAVES), lds, st, p);
+    hipLaunchKernelGGL((lin_rp_kernel<NTILES, ACT, PREC>), dim3(blocks), dim3(64 * RP_WAVES), lds, st, p);
     NBX_HIP(hipGetLastError());
     return NBX_OK;
 }

@@ -378,6 +378,7 @@ struct PoWs {
     float* DEG;                // [V] in-degree (unused by the model: FiberBundleConv sums)
     unsigned long long* ADJ;   // [V]
     int* ERR;                  // [64]
+    int* RANGE;                // [64]: the call's fp16x2 range flag (tp_fused.h tp_range_flag)
 };
 
 int next_pow2(int x) {
@@ -421,6 +422,7 @@ size_t po_carve(PoWs* ws, void* base, const PoDims& d) {
     w.DEG = take((size_t)d.V);
     w.ADJ = (unsigned long long*)take((size_t)d.V * 2);
     w.ERR = (int*)take(64);
+    w.RANGE = (int*)take(64);
     if (ws) *ws = w;
     return (off + 255) & ~size_t(255);
 }
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(256) void po_basis1_kernel(const float* __restrict_
 struct FfnProb {
     const float* XN;      // [rows][ldi] GEMM 1 input: the LayerNorm output (ConvNext), P16 (kernel basis)
     float* X;             // [rows][C] residual in, layer output (in place); the kernel basis KB (FFN_BASIS)
-    const void* img;      // [F/32] slabs [W1 chunk | W2 chunk] (include/nbx.h ffn_img_x3)
+    const void* img;      // [F/32] slabs [W1 chunk | W2 chunk] (include/nbx.h ffn_img_x3 / ffn_img_h2)
     const float* b1;      // [F]
     const float* b2;      // [C]
     const float* scale;   // [C] layer_scale or null
@@ -520,6 +522,10 @@ struct FfnProb {
     int F;                // hidden width (multiple of 32, <= FFN_FMAX)
     int ldi;              // GEMM 1 input row stride (floats); input columns >= ldi read as zeros
     unsigned long long* dbg;   // tuning only (NBX_PO_FFN_DEBUG): per-wave phase clocks [4]
+    // fp16x2 images (PREC 2): the factors undoing the images' power-of-two weight scales (W1, W2), and the
+    // call's range flag (tp_fused.h tp_range_flag; null: off)
+    float s1inv, s2inv;
+    int* range_flag;
 };
 constexpr int FFN_FMAX = 1024;
 
@@ -529,14 +535,20 @@ constexpr int FFN_FMAX = 1024;
 // columns 16-31 read as zeros against zero weights), output Bk = NTO 32 columns stored, so the [E O][C]
 // hidden activation (839 MB at C3) never reaches HBM.
 constexpr int FFN_CONVNEXT = 0, FFN_BASIS = 1;
-template <int NTI, int NTO, int MODE>
+// PREC 1: bf16x3 images (six bf16 products per fp32 product); PREC 2: fp16x2 images (three fp16 products,
+// tp_fused.h StatSKH2; the accumulators are descaled by s1inv / s2inv).  Block of one (column tile, chunk):
+// [part][m 2][lane 64][8] with 3 (bf16x3) or 2 (fp16x2) parts.
+template <int NTI, int NTO, int MODE, int PREC = 1>
 __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb P) {
-    using nbx::bf16x8;
     using nbx::floatx16;
+    using SP = nbx::SplitP<PREC>;
+    using SPT = typename SP::T;
+    constexpr int NP = SP::NP, NTRM = SP::NT;
+    constexpr int BLK = PREC == 2 ? nbx::LIN_H2_BLK : nbx::LIN_X3_BLK;
     constexpr int NT = NTO;               // output column tiles (the scheduling groups' unit)
     constexpr int C = NTO * 32;           // output width
-    constexpr int PART1 = NTI * nbx::LIN_X3_BLK;   // floats of one chunk's W1 blocks
-    constexpr int PART = NTO * nbx::LIN_X3_BLK;    // floats of one chunk's W2 blocks
+    constexpr int PART1 = NTI * BLK;      // floats of one chunk's W1 blocks
+    constexpr int PART = NTO * BLK;       // floats of one chunk's W2 blocks
     constexpr int NP1 = PART1 / 256;               // W1 DMA pieces (1 KiB each) per chunk
     constexpr int PW1 = (NP1 + FFN_WAVES - 1) / FFN_WAVES;
     constexpr int PW = PART / 256 / FFN_WAVES;    // W2 DMA pieces per wave per part
@@ -558,7 +570,7 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
 
     // prologue: input rows (lane (row, h) holds k = 32 kc + 16 h + 8 m + i, the image K order), b1,
     // W1 chunks 0-2 and W2 chunk 0; W2 chunk 1 then goes in flight
-    bf16x8 ax[NTI][3][2];
+    SPT ax[NTI][NP][2];
     {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.XN, (short)0, 0x7FFFFFF0, 0x00020000);
         const uint32_t base = (uint32_t)(((ok ? row : 0) * P.ldi + 16 * h) * 4);
@@ -586,16 +598,20 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
             if (i < P.F) b1s[i] = bv[u];
         }
 #pragma unroll
-        for (int kc = 0; kc < NTI; ++kc) {
-            nbx::tp_split3(a[kc][0], a[kc][1], ax[kc][0][0], ax[kc][1][0], ax[kc][2][0]);
-            nbx::tp_split3(a[kc][2], a[kc][3], ax[kc][0][1], ax[kc][1][1], ax[kc][2][1]);
-        }
+        for (int kc = 0; kc < NTI; ++kc)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                SPT t3[NP];
+                SP::split(a[kc][2 * m], a[kc][2 * m + 1], t3);
+#pragma unroll
+                for (int p3 = 0; p3 < NP; ++p3) ax[kc][p3][m] = t3[p3];
+            }
         // the input operands live in AGPRs for the whole loop (MFMA reads A/B from either file), which
         // leaves the architectural VGPRs to the weight fragments and the GELU arithmetic
 #pragma unroll
         for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
-            for (int p3 = 0; p3 < 3; ++p3)
+            for (int p3 = 0; p3 < NP; ++p3)
 #pragma unroll
                 for (int m = 0; m < 2; ++m) asm volatile("" : "+a"(ax[kc][p3][m]));
     }
@@ -611,63 +627,59 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     // issues at full rate; the first MFMA takes an inline 0 accumulator)
     auto gemm1 = [&](const float* buf) {
         // all of the chunk's fragments are read first (one LDS latency per chunk, not per 6 MFMAs)
-        const bf16x8* w1 = reinterpret_cast<const bf16x8*>(buf) + lane;
-        bf16x8 b[NTI][2][3];
+        const SPT* w1 = reinterpret_cast<const SPT*>(buf) + lane;
+        SPT b[NTI][2][NP];
 #pragma unroll
         for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
             for (int m = 0; m < 2; ++m)
 #pragma unroll
-                for (int p3 = 0; p3 < 3; ++p3) b[kc][m][p3] = w1[kc * (nbx::LIN_X3_BLK / 4) + m * 64 + p3 * 128];
+                for (int p3 = 0; p3 < NP; ++p3) b[kc][m][p3] = w1[kc * (BLK / 4) + m * 64 + p3 * 128];
         floatx16 g;
 #pragma unroll
         for (int kc = 0; kc < NTI; ++kc)
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                const bf16x8(&a)[3][2] = ax[kc];
-                const bf16x8(&w)[3] = b[kc][m];
-                if (kc == 0 && m == 0)
-                    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[2][m], floatx16{}, 0, 0, 0);
-                else
-                    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[2][m], g, 0, 0, 0);
-                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a[1][m], g, 0, 0, 0);
-                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], a[0][m], g, 0, 0, 0);
-                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[1][m], g, 0, 0, 0);
-                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a[0][m], g, 0, 0, 0);
-                g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a[0][m], g, 0, 0, 0);
+                const SPT(&a)[NP][2] = ax[kc];
+                const SPT(&w)[NP] = b[kc][m];
+#pragma unroll
+                for (int tt = 0; tt < NTRM; ++tt)   // smallest terms first; the weights are the MFMA's A
+                    g = nbx::mfma32x32(w[SP::TB[tt]], a[SP::TA[tt]][m], (kc == 0 && m == 0 && tt == 0) ? floatx16{} : g);
             }
+        if constexpr (PREC == 2) g *= P.s1inv;
         return g;
     };
     // b1 + GELU of chunk j's GEMM 1 result, split into the GEMM 2 A operand (registers 8m..8m+7 ->
     // MFMA step m)
-    auto gelu_split = [&](int j, const floatx16& g, bf16x8 (&hx)[3][2]) {
+    auto gelu_split = [&](int j, const floatx16& g, SPT (&hx)[NP][2]) {
         float hv[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) hv[e] = gelu_nb(g[e] + b1s[32 * j + (e & 3) + 8 * (e >> 2) + 4 * h]);
-        nbx::tp_split3(float4{hv[0], hv[1], hv[2], hv[3]}, float4{hv[4], hv[5], hv[6], hv[7]}, hx[0][0], hx[1][0], hx[2][0]);
-        nbx::tp_split3(float4{hv[8], hv[9], hv[10], hv[11]}, float4{hv[12], hv[13], hv[14], hv[15]}, hx[0][1], hx[1][1],
-                       hx[2][1]);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            SPT t3[NP];
+            SP::split(float4{hv[8 * m], hv[8 * m + 1], hv[8 * m + 2], hv[8 * m + 3]},
+                      float4{hv[8 * m + 4], hv[8 * m + 5], hv[8 * m + 6], hv[8 * m + 7]}, t3);
+#pragma unroll
+            for (int p3 = 0; p3 < NP; ++p3) hx[p3][m] = t3[p3];
+        }
     };
-    auto gemm2 = [&](const float* buf, const bf16x8 (&hx)[3][2]) {
-        const bf16x8* w2 = reinterpret_cast<const bf16x8*>(buf) + lane;
-        bf16x8 b[NT][2][3];
+    auto gemm2 = [&](const float* buf, const SPT (&hx)[NP][2]) {
+        const SPT* w2 = reinterpret_cast<const SPT*>(buf) + lane;
+        SPT b[NT][2][NP];
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
             for (int m = 0; m < 2; ++m)
 #pragma unroll
-                for (int p3 = 0; p3 < 3; ++p3) b[tt][m][p3] = w2[tt * (nbx::LIN_X3_BLK / 4) + m * 64 + p3 * 128];
+                for (int p3 = 0; p3 < NP; ++p3) b[tt][m][p3] = w2[tt * (BLK / 4) + m * 64 + p3 * 128];
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                const bf16x8(&w)[3] = b[tt][m];
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[2][m], w[0], acc[tt], 0, 0, 0);
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[1][m], w[1], acc[tt], 0, 0, 0);
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[0][m], w[2], acc[tt], 0, 0, 0);
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[1][m], w[0], acc[tt], 0, 0, 0);
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[0][m], w[1], acc[tt], 0, 0, 0);
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hx[0][m], w[0], acc[tt], 0, 0, 0);
+                const SPT(&w)[NP] = b[tt][m];
+#pragma unroll
+                for (int t3 = 0; t3 < NTRM; ++t3) acc[tt] = nbx::mfma32x32(hx[SP::TA[t3]][m], w[SP::TB[t3]], acc[tt]);
             }
     };
     // Two-deep software pipeline: iteration j issues GEMM 1 of chunk j + 2 and GEMM 2 of chunk j
@@ -676,7 +688,7 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     // Rings: iteration j reads W1 chunk j + 2 and W2 chunk j; it refills W1 slot j % 3 with chunk
     // j + 3 (needed next iteration) and W2 slot (j + 2) % 3 with chunk j + 2.
     floatx16 gq[2];
-    bf16x8 hq[2][3][2];
+    SPT hq[2][NP][2];
     gq[0] = gemm1(ring1);                               // chunk 0
     if (nj > 1) gq[1] = gemm1(ring1 + PART1);          // chunk 1
     gelu_split(0, gq[0], hq[0]);
@@ -720,20 +732,22 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
         if (FULL || j + 2 < nj) gq[cur] = gemm1(ring1 + s2 * PART1);
         gemm2(ring2 + s0 * PART, hq[cur]);
         if constexpr (FULL) {
-            // GEMM 1's fragment reads first; its 12 NT MFMAs each followed by ~5 vector instructions
-            // (the GELU of chunk j + 1) with GEMM 2's fragment reads spread among them, so every
-            // read lands long before its MFMA; then GEMM 2's MFMAs with the remaining vector work
-            __builtin_amdgcn_sched_group_barrier(0x100, 6 * NT, 0);
+            // GEMM 1's fragment reads first; its 2 NTRM NT MFMAs each followed by ~5 (bf16x3) / ~10
+            // (fp16x2: half the MFMAs for the same GELU) vector instructions (the GELU of chunk j + 1)
+            // with GEMM 2's fragment reads spread among them, so every read lands long before its MFMA;
+            // then GEMM 2's MFMAs with the remaining vector work
+            constexpr int VA = PREC == 2 ? 10 : 5, VB = PREC == 2 ? 8 : 4;
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * NP * NT, 0);
 #pragma unroll
-            for (int i = 0; i < 12 * NT; ++i) {
+            for (int i = 0; i < 2 * NTRM * NT; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-                if (i & 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, VA, 0);
+                if (PREC == 2 || (i & 1)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
 #pragma unroll
-            for (int i = 0; i < 12 * NT; ++i) {
+            for (int i = 0; i < 2 * NTRM * NT; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, VB, 0);
             }
         }
         // the next iteration reads W1 chunk j + 3 (issued above) and W2 chunk j + 1 (issued in j - 1):
@@ -774,6 +788,15 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
             const int col = 32 * tt + r;
             const float b = P.b2[col];
             const float sc = P.scale ? P.scale[col] : 1.f;
+            if constexpr (PREC == 2) {   // undo W2's image scale; fp16x2 range guard
+                float z = 0.f;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    acc[tt][e] *= P.s2inv;
+                    z = nbx::tp_nonfinite_fold(z, acc[tt][e]);
+                }
+                nbx::tp_range_flag(P.range_flag, z);
+            }
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const float v = MODE == FFN_BASIS ? gelu_nb(acc[tt][e] + b) : sc * (acc[tt][e] + b);
@@ -805,16 +828,20 @@ __global__ __launch_bounds__(64 * FFN_WAVES, 1) void po_ffn_kernel(const FfnProb
     }
 }
 
-template <int NTI, int NTO, int MODE>
+template <int NTI, int NTO, int MODE, int PREC = 1>
 int po_ffn_launch(const FfnProb& p, hipStream_t st) {
     if (p.rows <= 0) return NBX_OK;
     NBX_CHECK_ARG(p.F % 32 == 0 && p.F >= 32 && p.F <= FFN_FMAX && p.img && p.b1 && p.b2,
                   "po_ffn: 32 <= F <= %d, F %% 32 == 0, an image, b1 and b2 required", FFN_FMAX);
     NBX_CHECK_ARG((double)p.rows * p.ldi * 4.0 < 2147483632.0, "po_ffn: XN spans >= 2 GiB");
     NBX_CHECK_ARG(p.ldi % 4 == 0 && p.ldi <= NTI * 32, "po_ffn: input stride must be a multiple of 4, <= %d", NTI * 32);
-    const size_t lds = (3 * (size_t)(NTI + NTO) * nbx::LIN_X3_BLK + p.F) * 4;
+    // the rings + b1, and at least the epilogue's transpose tiles (FFN_WAVES x 32 rows x (C + 8) floats), which
+    // reuse the ring space: with the smaller fp16x2 blocks and one input chunk (FFN_BASIS) the tiles are the
+    // larger of the two
+    const size_t lds = std::max<size_t>((3 * (size_t)(NTI + NTO) * (PREC == 2 ? nbx::LIN_H2_BLK : nbx::LIN_X3_BLK) + p.F) * 4,
+                                        (size_t)FFN_WAVES * 32 * (NTO * 32 + 8) * 4);
     NBX_CHECK_ARG(lds <= 160 * 1024, "po_ffn: %zu bytes of LDS", lds);
-    NBX_LDS_160K((po_ffn_kernel<NTI, NTO, MODE>));
+    NBX_LDS_160K((po_ffn_kernel<NTI, NTO, MODE, PREC>));
     const unsigned blocks = (unsigned)((p.rows + 32 * FFN_WAVES - 1) / (32 * FFN_WAVES));
     static const bool debug = getenv("NBX_PO_FFN_DEBUG") != nullptr;
     static unsigned long long* dbg = nullptr;
@@ -822,7 +849,7 @@ int po_ffn_launch(const FfnProb& p, hipStream_t st) {
     const size_t nw = (size_t)blocks * FFN_WAVES;
     if (debug && !dbg) NBX_HIP(hipMalloc(&dbg, nw * 4 * sizeof(unsigned long long)));
     q.dbg = debug ? dbg : nullptr;
-    hipLaunchKernelGGL((po_ffn_kernel<NTI, NTO, MODE>), dim3(blocks), dim3(64 * FFN_WAVES), lds, st, q);
+    hipLaunchKernelGGL((po_ffn_kernel<NTI, NTO, MODE, PREC>), dim3(blocks), dim3(64 * FFN_WAVES), lds, st, q);
     NBX_HIP(hipGetLastError());
     if (debug) {   // tuning only: average clocks per wave of prologue / loop / loop-end waits / epilogue
         std::vector<unsigned long long> hb(nw * 4);
@@ -848,9 +875,25 @@ bool po_x3_enabled() {
     return v == 1;
 }
 
+// the fp16x2 images when the weights carry them (NBX_PO_SPLIT=x3: the bf16x3 images, A/B only)
+bool po_h2_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NBX_PO_SPLIT");
+        v = (po_x3_enabled() && !(e && (e[0] == 'x' || e[0] == '1'))) ? 1 : 0;
+    }
+    return v == 1;
+}
+
 template <int ACT, int EPI = nbx::LIN_STORE>
 int lin_auto(nbx::LinProb& p, hipStream_t st) {
     const int need = (p.N + 31) / 32;
+    if (p.Wh2 && po_h2_enabled() && p.N % 32 == 0) {
+        auto lds = [&](int nt) { return nbx::lin_lds_bytes(nt, p.Ktot, 2); };
+        if (need >= 3 && lds(4) <= 160 * 1024) return nbx::lin_launch<4, ACT, EPI, 2>(p, st);
+        if (need >= 2 && lds(2) <= 160 * 1024) return nbx::lin_launch<2, ACT, EPI, 2>(p, st);
+        if (lds(1) <= 160 * 1024) return nbx::lin_launch<1, ACT, EPI, 2>(p, st);
+    }
     if (p.Wx3 && po_x3_enabled() && p.N % 32 == 0) {
         auto lds = [&](int nt) { return nbx::lin_lds_bytes(nt, p.Ktot, 1); };
         if (need >= 3 && lds(4) <= 160 * 1024) return nbx::lin_launch<4, ACT, EPI, 1>(p, st);
@@ -885,9 +928,14 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
     // both kernel-basis layers in one kernel when the weights carry the fused image (NBX_PO_BASIS_FUSED=0:
     // the two-kernel path, A/B only)
     static const bool basis_fused = !(getenv("NBX_PO_BASIS_FUSED") && getenv("NBX_PO_BASIS_FUSED")[0] == '0');
-    if (w->basis_ffn_img_x3 && basis_fused && (Bk == 128 || Bk == 64) && C % 32 == 0 && C <= FFN_FMAX) {
-        const FfnProb fb{ws.P16, ws.KB, w->basis_ffn_img_x3, w->basis1_b, w->basis2_b, nullptr, d.R, C, 16, nullptr};
+    const bool basis_h2 = w->basis_ffn_img_h2 && po_h2_enabled();
+    if ((basis_h2 || w->basis_ffn_img_x3) && basis_fused && (Bk == 128 || Bk == 64) && C % 32 == 0 && C <= FFN_FMAX) {
+        const FfnProb fb{ws.P16, ws.KB, basis_h2 ? w->basis_ffn_img_h2 : w->basis_ffn_img_x3, w->basis1_b,
+                         w->basis2_b, nullptr, d.R, C, 16, nullptr, w->basis_ffn_h2_s1inv, w->basis_ffn_h2_s2inv,
+                         ws.RANGE};
         if (int rc = nbx::timed(tm, st, PK_BASIS, 2.0 * Ev * (14 * C + C * Bk), Ev * f4 * (16 + Bk), [&] {
+                if (basis_h2)
+                    return Bk == 128 ? po_ffn_launch<1, 4, FFN_BASIS, 2>(fb, st) : po_ffn_launch<1, 2, FFN_BASIS, 2>(fb, st);
                 return Bk == 128 ? po_ffn_launch<1, 4, FFN_BASIS>(fb, st) : po_ffn_launch<1, 2, FFN_BASIS>(fb, st);
             }))
             return rc;
@@ -926,6 +974,9 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
         {   // spatial conv: X1[(d,o)] = sum_q (KB Wk')[(d,o,q)] * X[(src,o)]
             LinProb p = nbx::lin_dense(ws.KB, Bk, Bk, (int)d.R, Ly.kernel_t, kp(Bk), C, nullptr, ws.X1, C);
             p.Wx3 = Ly.kernel_img_x3;
+            p.Wh2 = Ly.kernel_img_h2;
+            p.h2_sinv = Ly.kernel_h2_sinv;
+            p.range_flag = ws.RANGE;
             p.conv_G = (int)d.G;
             p.conv_O = O;
             p.conv_nodes = (int)d.N;
@@ -1007,11 +1058,17 @@ int po_forward_impl(const nbx_ponita_weights* w, const float* pos, const float* 
             }
         fiber_done:;
         }
-        if (Ly.ffn_img_x3 && po_x3_enabled() && (C == 64 || C == 128) && d.mlp % 32 == 0 && d.mlp <= FFN_FMAX) {
+        const bool ffn_h2 = Ly.ffn_img_h2 && po_h2_enabled();
+        if ((ffn_h2 || Ly.ffn_img_x3) && po_x3_enabled() && (C == 64 || C == 128) && d.mlp % 32 == 0 &&
+            d.mlp <= FFN_FMAX) {
             // ConvNext MLP fused (linear_1 + GELU + linear_2 + layer_scale + residual): the hidden
-            // activation stays in registers (po_ffn_kernel)
-            const FfnProb fp{ws.XN, ws.X, Ly.ffn_img_x3, Ly.lin1_b, Ly.lin2_b, Ly.layer_scale, VO, d.mlp, C, nullptr};
+            // activation stays in registers (po_ffn_kernel), on the fp16x2 image when present
+            const FfnProb fp{ws.XN, ws.X, ffn_h2 ? Ly.ffn_img_h2 : Ly.ffn_img_x3, Ly.lin1_b, Ly.lin2_b, Ly.layer_scale, VO,
+                             d.mlp, C, nullptr, Ly.ffn_h2_s1inv, Ly.ffn_h2_s2inv, ws.RANGE};
             if (int rc = nbx::timed(tm, st, PK_LIN1, 2.0 * 2.0 * VO * C * d.mlp, (double)VO * f4 * 3 * C, [&] {
+                    if (ffn_h2)
+                        return C == 128 ? po_ffn_launch<4, 4, FFN_CONVNEXT, 2>(fp, st)
+                                        : po_ffn_launch<2, 2, FFN_CONVNEXT, 2>(fp, st);
                     return C == 128 ? po_ffn_launch<4, 4, FFN_CONVNEXT>(fp, st) : po_ffn_launch<2, 2, FFN_CONVNEXT>(fp, st);
                 }))
                 return rc;
@@ -1094,6 +1151,7 @@ extern "C" int nbx_ponita_forward(const nbx_ponita_weights* w, const float* pos,
     PoDims d;
     PoWs ws;
     if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), (hipStream_t)stream));
     return po_forward_impl(w, pos, vel, mass, d, out, calib_moments, ws, (hipStream_t)stream);
 }
 
@@ -1106,6 +1164,7 @@ extern "C" int nbx_ponita_forward_timed(const nbx_ponita_weights* w, const float
     PoWs ws;
     if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
     hipStream_t st = (hipStream_t)stream;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), st));
     nbx::LaunchTimer tm;
     hipEvent_t a, b;
     NBX_HIP(hipEventCreate(&a));
@@ -1134,6 +1193,7 @@ extern "C" int nbx_ponita_rollout(const nbx_ponita_weights* w, float* pos, float
     if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
     NBX_CHECK_ARG(num_frames >= 1, "nbx_ponita_rollout: num_frames >= 1");
     hipStream_t st = (hipStream_t)stream;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), st));
     const int64_t V = d.V;
     hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
                        (int64_t)0, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
@@ -1155,6 +1215,7 @@ extern "C" int nbx_ponita_forward_graph(const nbx_ponita_weights* w, const float
     if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
     NBX_CHECK_ARG(num_edges >= 0 && (num_edges == 0 || edge_index), "nbx_ponita_forward_graph: bad edge_index");
     hipStream_t st = (hipStream_t)stream;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), st));
     if (int rc = nbx::graph_slots_from_edges(edge_index, num_edges, d.V, (int)N, (int)d.G, ws.ADJ, ws.SLOT, ws.DEG,
                                              ws.ERR, st))
         return rc;
@@ -1176,6 +1237,7 @@ extern "C" int nbx_ponita_rollout_knn(const nbx_ponita_weights* w, float* pos, f
     if (int rc = po_prepare(w, B, N, workspace, workspace_bytes, &d, &ws)) return rc;
     NBX_CHECK_ARG(num_frames >= 1, "nbx_ponita_rollout_knn: num_frames >= 1");
     hipStream_t st = (hipStream_t)stream;
+    NBX_HIP(hipMemsetAsync(ws.RANGE, 0, sizeof(int), st));
     const int64_t V = d.V;
     hipLaunchKernelGGL(nbx::rollout_state_kernel, dim3(g1(3 * V)), dim3(256), 0, st, pos, vel, ws.out, V, (int)N,
                        (int64_t)0, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
@@ -1189,5 +1251,21 @@ extern "C" int nbx_ponita_rollout_knn(const nbx_ponita_weights* w, float* pos, f
                            f, num_frames, traj_pos, traj_vel, flags & NBX_ROLLOUT_ABSOLUTE);
     }
     NBX_LAUNCH_CHECK("ponita rollout");
+    return NBX_OK;
+}
+
+extern "C" int nbx_ponita_range_check(const nbx_ponita_weights* w, const void* workspace, size_t workspace_bytes,
+                                      int64_t B, int64_t N, void* stream) {
+    PoDims d;
+    PoWs ws;
+    if (int rc = po_prepare(w, B, N, const_cast<void*>(workspace), workspace_bytes, &d, &ws)) return rc;
+    int flag = 0;
+    NBX_HIP(hipMemcpyAsync(&flag, ws.RANGE, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    NBX_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (flag) {
+        nbx::set_error("ponita: a GEMM operand left the fp16 range of the fp16x2 split path (|a| >= 65520) or the "
+                       "input is not finite; the bf16x3 path (NBX_PO_SPLIT=x3) keeps the fp32 exponent range");
+        return NBX_E_RANGE;
+    }
     return NBX_OK;
 }

@@ -1204,9 +1204,12 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
                 p.B = static_cast<const float*>(L.upd1_img_h2);
                 p.bscale = L.upd1_h2_descale;
                 // (A-ring depth 3: 5 and 7 measured slower, r05 profiles/r05/pf)
+                // (r06 A/B, profiles/r06/upd_variants: two 16-channel chunks per 4-wave block, ring 3 or 5,
+                // 17.5-18.1 us against 17.8 us and fewer steps/s -- the single-tile latency chain, not the
+                // 6x L2 re-read, bounds this kernel)
                 const int rc =
                     dv_upd ? (M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2_DV>(p, st, tm)
-                                      : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2_DV>(p, st, tm))
+                                        : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2_DV>(p, st, tm))
                     : M == 96 ? run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_SEG_H2>(p, st, tm)
                               : run_tp16_w<3, 1, nbx::TP_GATE_NODE, 1, 8, 3, 1, SK_UPD1_32_SEG_H2>(p, st, tm);
                 if (rc) return rc;
@@ -1256,6 +1259,8 @@ int forward_impl(const nbx_segnn_weights* w, const float* pos, const float* vel,
             if ((M == 96 || M == 32) && L.upd2_img_h2 && split_prec() == 2 && static_enabled()) {
                 p.B = static_cast<const float*>(L.upd2_img_h2);
                 p.bscale = L.upd2_h2_descale;
+                // (r06 A/B, profiles/r06/upd_variants: CG 2 / 4 waves with ring 3 or 5: 12.3-12.4 us against
+                // 11.5 us; CG 3 / 2 waves needs a 144-thread BN reduction and was not kept)
                 const int rc =
                     upd2_dv ? (M == 96 ? run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_H2_DV>(p, st, tm)
                                        : run_tp16_w<2, 1, nbx::TP_RESID, 1, 8, 3, 1, SK_UPD2_32_H2_DV>(p, st, tm))

@@ -164,13 +164,21 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
 
     // ---- segmented input: the BatchNorm coefficient inputs, loaded before the image DMA (one
     // evaluation per thread: message BN at t < 2M, feature BN at 2M <= t < 4M; kind = which half)
+    // (evaluation index i = t + e THREADS over the 4M evaluations: NEV per thread for blocks smaller
+    // than 4M threads; the segmented paths have M <= 96)
     const int bn_M = P.M;
     const bool bn_m = SK::SEG == 4 && P.mbn.sums != nullptr;   // message BN finalised here
     const bool bn_x = SK::SEG > 0 && P.xbn.sums != nullptr;    // pending feature BN finalised here
-    const int bn_which = t < 2 * bn_M ? 0 : 1, bn_kind = (t % (2 * bn_M)) / bn_M, bn_k = t % bn_M;
-    const bool bn_on = SK::SEG > 0 && t < 4 * bn_M && (bn_which == 0 ? bn_m : bn_x);
-    BnPre bn_pre{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
-    if (bn_on) bn_pre = bn_pre_load(bn_which == 0 ? P.mbn : P.xbn, bn_M, bn_kind, bn_k);
+    constexpr int NEV = SK::SEG > 0 ? (4 * 96 + THREADS - 1) / THREADS : 1;
+    BnPre bn_pre[NEV];
+#pragma unroll
+    for (int e = 0; e < NEV; ++e) {
+        bn_pre[e] = BnPre{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
+        const int i = t + e * THREADS;
+        const int which = i < 2 * bn_M ? 0 : 1, kind = (i % (2 * bn_M)) / bn_M, k = i % bn_M;
+        if (SK::SEG > 0 && i < 4 * bn_M && (which == 0 ? bn_m : bn_x))
+            bn_pre[e] = bn_pre_load(which == 0 ? P.mbn : P.xbn, bn_M, kind, k);
+    }
 
     // ---- stage the CG chunk images of this group in LDS (LDS-DMA, verbatim copy; the image
     // array holds a multiple of 4 chunks, so a group never runs past it)
@@ -191,8 +199,12 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
         const bool mfin = bn_m, xfin = bn_x;
         // the BatchNorm parts from the preloaded inputs: message BN -> parts 1 (0e scale), 5 (shift x
         // deg), 3 and 9 (1o scale); feature BN -> parts 0, 4, 2 and 8
-        if (bn_on) {
-            const float2 c = bn_pre_coef(bn_which == 0 ? P.mbn : P.xbn, bn_pre, M, bn_kind, bn_k, blockIdx.x == 0);
+#pragma unroll
+        for (int e = 0; e < NEV; ++e) {
+            const int i = t + e * THREADS;
+            const int bn_which = i < 2 * M ? 0 : 1, bn_kind = (i % (2 * M)) / M, bn_k = i % M;
+            if (!(i < 4 * M && (bn_which == 0 ? bn_m : bn_x))) continue;
+            const float2 c = bn_pre_coef(bn_which == 0 ? P.mbn : P.xbn, bn_pre[e], M, bn_kind, bn_k, blockIdx.x == 0);
             if (bn_which == 0) {
                 if (bn_kind == 0) { segtab[1 * M + bn_k] = c.x; segtab[5 * M + bn_k] = P.deg * c.y; }
                 else { segtab[3 * M + bn_k] = c.x; segtab[9 * M + bn_k] = c.x; }

@@ -383,6 +383,20 @@ class EquiformerV2_nbody(nn.Module):
         nt, kc = img.shape[0], W.shape[1] // 32
         return img.reshape(nt, kc, -1).transpose(0, 1).contiguous()
 
+    @staticmethod
+    def _image_h2(W, chunk_major=False):
+        """fp16x2 image of W (include/nbx.h "fp16x2 images", the _image block order, optionally chunk-major)
+        and its descale 1 / s as a 0-d float64 tensor."""
+        from .segnn import SEGNN
+        W = W.float()
+        s = SEGNN.h2_scale(W)
+        rows = W.shape[0]
+        img = SEGNN.frag_image_h2([(W, W.shape[1])], None, -(-rows // 32), 32, s)
+        if chunk_major:
+            nt, kc = img.shape[0], W.shape[1] // 32
+            img = img.reshape(nt, kc, -1).transpose(0, 1).contiguous()
+        return img, torch.tensor(1.0 / s, dtype=torch.float64)
+
     def packed_tensors(self, device):
         """Every device tensor the C-ABI weight struct points at, keyed by struct path."""
         C, He = self.sphere_channels, self.edge_channels
@@ -412,11 +426,21 @@ class EquiformerV2_nbody(nn.Module):
                 perm = g * 2 * C + 32 * cb + i
                 P[prefix + "w2_x3"] = self._image(W2[perm].to(device)).to(device)
                 P[prefix + "b2"] = v(b2[perm])
-            else:
-                P[prefix + "w2"], P[prefix + "b2"] = v(W2), v(b2)
+                return W2[perm]
+            P[prefix + "w2"], P[prefix + "b2"] = v(W2), v(b2)
+            return None
 
         def attn(prefix, A):
-            radial(prefix + "rad.", A.so2_conv_1.rad_func, A.source_embedding, A.target_embedding, True)
+            W2p = radial(prefix + "rad.", A.so2_conv_1.rad_func, A.source_embedding, A.target_embedding, True)
+            # fp16x2 images of the five split-precision GEMMs (include/nbx.h nbx_eqv2_attn "fp16x2 images")
+            P[prefix + "w2_h2"], P[prefix + "w2_sinv"] = self._image_h2(W2p.to(device))
+            P[prefix + "fc0_h2"], P[prefix + "fc0_sinv"] = self._image_h2(
+                A.so2_conv_1.fc_m0.weight.detach().to(device), chunk_major=True)
+            P[prefix + "fc1_h2"], P[prefix + "fc1_sinv"] = self._image_h2(
+                A.so2_conv_1.so2_m_conv[0].fc.weight.detach().to(device), chunk_major=True)
+            P[prefix + "c20_h2"], P[prefix + "c20_sinv"] = self._image_h2(A.so2_conv_2.fc_m0.weight.detach().to(device))
+            P[prefix + "c21_h2"], P[prefix + "c21_sinv"] = self._image_h2(
+                A.so2_conv_2.so2_m_conv[0].fc.weight.detach().to(device))
             fc0 = A.so2_conv_1.fc_m0
             n0 = c32(fc0.out_features)
             P[prefix + "fc0_x3"] = self._image_chunk_major(fc0.weight.detach().to(device))
@@ -464,6 +488,8 @@ class EquiformerV2_nbody(nn.Module):
             for name, typ in struct._fields_:
                 if isinstance(getattr(struct, name), ctypes_struct_types()):
                     fill(getattr(struct, name), prefix + name + ".")
+                elif typ is _lib.c_f:   # the fp16x2 images' descale factors
+                    setattr(struct, name, float(P.get(prefix + name, 1.0)))
                 elif prefix + name in P:
                     setattr(struct, name, P[prefix + name].data_ptr())
 
@@ -556,7 +582,16 @@ class EquiformerV2_nbody(nn.Module):
                                                _lib.dev_ptr(g) if g is not None else None, seed, _lib.dev_ptr(out),
                                                _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(device)),
                    "nbx_eqv2_forward")
+        self._range_check(W, ws, B, N, device)
         return out.to(pos.dtype)
+
+    def _range_check(self, W, ws, B, N, device):
+        """fp16x2 range guard (include/nbx.h nbx_eqv2_range_check): NbxError instead of non-finite results when a
+        GEMM operand leaves the fp16 range of the split path; one stream synchronisation per call, skipped while a
+        HIP graph is captured and when ``range_check`` is False."""
+        if getattr(self, "range_check", True) and not torch.cuda.is_current_stream_capturing():
+            _lib.check(_lib.lib().nbx_eqv2_range_check(W, _lib.dev_ptr(ws), ws.numel(), B, N, _lib.stream_ptr(device)),
+                       "eqv2")
 
     @torch.no_grad()
     def rollout(self, loc, vel, mass, num_frames: int, absolute: bool = False, seed=None):
@@ -589,6 +624,7 @@ class EquiformerV2_nbody(nn.Module):
                                                _lib.ROLLOUT_ABSOLUTE if absolute else 0, int(seed), _lib.dev_ptr(tp),
                                                _lib.dev_ptr(tv), _lib.dev_ptr(ws), ws.numel(),
                                                _lib.stream_ptr(device)), "nbx_eqv2_rollout")
+        self._range_check(W, ws, B, N, device)
         return tp, tv
 
 

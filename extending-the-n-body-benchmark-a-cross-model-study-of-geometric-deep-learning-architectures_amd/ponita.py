@@ -256,11 +256,45 @@ class PONITA_NBODY(nn.Module):
         # the kernel-basis MLP as one fused kernel (csrc/ponita.hip po_ffn_kernel FFN_BASIS)
         if C % 32 == 0 and C <= 1024 and m.basis_dim in (64, 128) and P["basis1_t"].shape[1] == 32:
             P["basis_ffn_img_x3"] = self._ffn_image(P["basis1_t"], P["basis2_t"])
+            P["basis_ffn_img_h2"], P["basis_ffn_h2_s1inv"], P["basis_ffn_h2_s2inv"] = self._ffn_image_h2(
+                P["basis1_t"], P["basis2_t"])
         for i in range(len(m.interaction_layers)):
             p = f"layers.{i}."
             if C in (64, 128) and P[p + "lin1_t"].shape[0] % 32 == 0:
                 P[p + "ffn_img_x3"] = self._ffn_image(P[p + "lin1_t"], P[p + "lin2_t"])
+                P[p + "ffn_img_h2"], P[p + "ffn_h2_s1inv"], P[p + "ffn_h2_s2inv"] = self._ffn_image_h2(
+                    P[p + "lin1_t"], P[p + "lin2_t"])
+            Wk = P[p + "kernel_t"]
+            if Wk.shape[0] % 32 == 0:   # the spatial conv (LIN_CONV) on fp16x2 (include/nbx.h "fp16x2 images")
+                s = self.h2_scale(Wk)
+                P[p + "kernel_img_h2"] = self.lin_image_h2(Wk, s)
+                P[p + "kernel_h2_sinv"] = torch.tensor(1.0 / s, dtype=torch.float64)
         return P
+
+    @staticmethod
+    def h2_scale(*mats):
+        from .segnn import SEGNN
+        return SEGNN.h2_scale(*mats)
+
+    @classmethod
+    def _ffn_image_h2(cls, W1, W2):
+        """include/nbx.h nbx_ponita_layer.ffn_img_h2: the _ffn_image slabs with fp16x2 blocks, W1 scaled by
+        s1 and W2 by s2 (powers of two, max |W s| in [2^9, 2^10)); returns (image, 1 / s1, 1 / s2)."""
+        F, C = W1.shape[0], W2.shape[0]
+        nj = F // 32
+        s1, s2 = cls.h2_scale(W1), cls.h2_scale(W2[:, :F])
+        img1 = cls.lin_image_h2(W1, s1).reshape(nj, -1)
+        perm = torch.tensor([32 * j + q for j in range(nj) for q in cls.FFN_PERM], device=W2.device)
+        W2p = W2[:, :F][:, perm].contiguous()
+        img2 = cls.lin_image_h2(W2p, s2).reshape(C // 32, nj, -1).transpose(0, 1).reshape(nj, -1)
+        inv = lambda x: torch.tensor(1.0 / x, dtype=torch.float64)   # exact: powers of two
+        return torch.cat([img1, img2], 1).contiguous(), inv(s1), inv(s2)
+
+    @staticmethod
+    def lin_image_h2(W, scale):
+        """[N][Kp] -> int16 fp16x2 image [N/32][Kp/32][2][2][64][8] of W * scale (include/nbx.h "fp16x2 images")."""
+        from .segnn import SEGNN
+        return SEGNN.frag_image_h2([(W, W.shape[1])], None, W.shape[0] // 32, 32, scale)
 
     # hidden index held by image K slot q = 16 h + 8 m + i of a 32-wide chunk in the fused ConvNext MLP:
     # the register order of the 32x32 MFMA result that becomes GEMM 2's A operand (csrc/ponita.hip
@@ -296,11 +330,17 @@ class PONITA_NBODY(nn.Module):
             setattr(W, name, P[name].data_ptr())
         W.basis2_img_x3 = P["basis2_img_x3"].data_ptr() if "basis2_img_x3" in P else None
         W.basis_ffn_img_x3 = P["basis_ffn_img_x3"].data_ptr() if "basis_ffn_img_x3" in P else None
+        W.basis_ffn_img_h2 = P["basis_ffn_img_h2"].data_ptr() if "basis_ffn_img_h2" in P else None
+        W.basis_ffn_h2_s1inv = float(P.get("basis_ffn_h2_s1inv", 1.0))
+        W.basis_ffn_h2_s2inv = float(P.get("basis_ffn_h2_s2inv", 1.0))
         for i in range(W.num_layers):
             L = W.layers[i]
-            for name, _ in L._fields_:
+            for name, ctype in L._fields_:
                 t = P.get(f"layers.{i}.{name}")
-                setattr(L, name, t.data_ptr() if t is not None else None)
+                if ctype is _lib.c_f:   # the fp16x2 images' descale factors
+                    setattr(L, name, float(t) if t is not None else 1.0)
+                else:
+                    setattr(L, name, t.data_ptr() if t is not None else None)
         self._packed = (self._param_version(), W, P)
         return W
 
@@ -400,6 +440,7 @@ class PONITA_NBODY(nn.Module):
                 W, _lib.dev_ptr(p), _lib.dev_ptr(v), _lib.dev_ptr(m), B, N, _lib.dev_ptr(e), e.shape[1],
                 _lib.dev_ptr(out), _lib.dev_ptr(mom) if calib else None, _lib.dev_ptr(ws), ws.numel(),
                 _lib.stream_ptr(device)), "nbx_ponita_forward_graph")
+        self._range_check(W, ws, B, N, device)
         if calib:
             n = V * self.num_ori * self.hidden_dim
             if self.calibration_group is not None:
@@ -459,6 +500,7 @@ class PONITA_NBODY(nn.Module):
         ws = self._workspace(W, B, N, device)
         if first is None:
             run(p, v, num_frames, tp, tv)
+            self._range_check(W, ws, B, N, device)
             return tp, tv
         # frame 1 came from the calibrating forward; the rest from the calibrated weights
         tp[:, 0], tv[:, 0] = p, v
@@ -469,5 +511,14 @@ class PONITA_NBODY(nn.Module):
         rp = torch.empty(B, num_frames - 1, N, 3, device=device, dtype=torch.float32)
         rv = torch.empty_like(rp)
         run(p, v, num_frames - 1, rp, rv)
+        self._range_check(W, ws, B, N, device)
         tp[:, 1:], tv[:, 1:] = rp, rv
         return tp, tv
+
+    def _range_check(self, W, ws, B, N, device):
+        """fp16x2 range guard (include/nbx.h nbx_ponita_range_check): NbxError instead of non-finite results
+        when a GEMM operand leaves the fp16 range of the split path; one stream synchronisation per call,
+        skipped while a HIP graph is captured and when ``range_check`` is False."""
+        if getattr(self, "range_check", True) and not torch.cuda.is_current_stream_capturing():
+            _lib.check(_lib.lib().nbx_ponita_range_check(W, _lib.dev_ptr(ws), ws.numel(), B, N,
+                                                         _lib.stream_ptr(device)), "ponita")

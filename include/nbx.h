@@ -709,6 +709,14 @@ typedef struct nbx_ponita_layer {
      * 16 h + 8 m + i holds hidden unit (i & 3) + 16 m + 8 (i >> 2) + 4 h]; used when hidden C is 64
      * or 128 and 4C <= 1024 (ponita.py _ffn_image); lin1_b / lin2_b / layer_scale as above */
     const void* ffn_img_x3;
+    /* optional (ABI 17): fp16x2 images ("fp16x2 images": W s = hi + lo, both fp16, s a power of two per
+     * matrix; block [part 2][m 2][lane 64][8] fp16 in place of the bf16x3 block) of the fused ConvNext MLP
+     * (the ffn_img_x3 layout; linear_1 scaled by 1 / ffn_h2_s1inv, linear_2 by 1 / ffn_h2_s2inv) and of
+     * kernel_t (the kernel_img_x3 layout, scaled by 1 / kernel_h2_sinv); used in place of the bf16x3 images
+     * when present (NBX_PO_SPLIT=x3: the bf16x3 images) */
+    const void* ffn_img_h2;
+    const void* kernel_img_h2;
+    float ffn_h2_s1inv, ffn_h2_s2inv, kernel_h2_sinv, h2_pad;
 } nbx_ponita_layer;
 
 typedef struct nbx_ponita_weights {
@@ -726,10 +734,21 @@ typedef struct nbx_ponita_weights {
      * chunk, K order permuted], the ffn_img_x3 layout with one 32-deep input chunk; the [E O][hidden]
      * activation between the layers never reaches HBM */
     const void* basis_ffn_img_x3;
+    /* optional (ABI 17): the fp16x2 image of the fused kernel-basis MLP (basis_ffn_img_x3 layout, the
+     * ffn_img_h2 scales) */
+    const void* basis_ffn_img_h2;
+    float basis_ffn_h2_s1inv, basis_ffn_h2_s2inv;
     nbx_ponita_layer layers[NBX_PONITA_MAX_LAYERS];
 } nbx_ponita_weights;
 
 int nbx_ponita_workspace_bytes(const nbx_ponita_weights* w, int64_t batch_size, int64_t num_nodes, size_t* bytes);
+
+/* fp16x2 range guard of the PONITA calls (ABI 17), as nbx_segnn_range_check: waits for `stream`, reads the
+ * flag the fp16x2 kernels of the last nbx_ponita_forward / _forward_graph / _rollout / _rollout_knn call made
+ * with `workspace` raised, and returns NBX_E_RANGE if an operand left the fp16 range (or an input was not
+ * finite).  Synchronises. */
+int nbx_ponita_range_check(const nbx_ponita_weights* w, const void* workspace, size_t workspace_bytes,
+                           int64_t batch_size, int64_t num_nodes, void* stream);
 
 /* PONITA_NBODY.forward on the graph of infer_self_feed.py:131-147
  * (x = mass, vec = vel, rel_pos = pos[src] - pos[dst]): out [B*N, 6].
@@ -823,6 +842,12 @@ typedef struct nbx_eqv2_attn {             /* SO2EquivariantGraphAttention */
     const float* alpha_norm_w; const float* alpha_norm_b;   /* [na] */
     const float* alpha_dot;                  /* [nh][na] */
     const float* proj_t; const float* proj_b;  /* proj (SO3_LinearV2) [3][nh nv][Cout], [Cout] */
+    /* optional (ABI 17): fp16x2 images (W s = hi + lo, both fp16, s a power of two per matrix; block
+     * [part 2][m 2][lane 64][8] fp16 in place of the bf16x3 block, same orders: fc0 / fc1 chunk-major)
+     * of rad.w2, fc0, fc1, c20, c21 with their 1 / s; used in place of the bf16x3 images when present
+     * (NBX_EQ_SPLIT=x3: the bf16x3 images) */
+    const void* w2_h2; const void* fc0_h2; const void* fc1_h2; const void* c20_h2; const void* c21_h2;
+    float w2_sinv, fc0_sinv, fc1_sinv, c20_sinv, c21_sinv, h2_pad;
 } nbx_eqv2_attn;
 
 typedef struct nbx_eqv2_block {            /* TransBlockV2 */
@@ -873,6 +898,12 @@ int nbx_eqv2_forward_timed(const nbx_eqv2_weights* w, const float* pos, const fl
 int nbx_eqv2_rollout(const nbx_eqv2_weights* w, float* pos, float* vel, const float* mass, int64_t batch_size,
                      int64_t num_nodes, int64_t num_frames, int32_t flags, uint64_t seed, float* traj_pos,
                      float* traj_vel, void* workspace, size_t workspace_bytes, void* stream);
+
+/* fp16x2 range guard of the EquiformerV2 calls (ABI 17), as nbx_segnn_range_check: waits for `stream`, reads
+ * the flag of the last nbx_eqv2_forward / _forward_timed / _rollout call made with `workspace`; NBX_E_RANGE
+ * if an operand of an fp16x2 GEMM left the fp16 range (or an input was not finite).  Synchronises. */
+int nbx_eqv2_range_check(const nbx_eqv2_weights* w, const void* workspace, size_t workspace_bytes, int64_t batch_size,
+                         int64_t num_nodes, void* stream);
 
 #ifdef __cplusplus
 }

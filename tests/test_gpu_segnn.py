@@ -3,10 +3,12 @@
 Tolerances (north_star: "a stated fp32 tolerance"):
 * one forward at C2 size (B = 1024): per output column c, max |gpu - oracle| <= 1e-5 * max|oracle[:, c]| + 1e-7
   (measured 1.6e-6 on the fp16x2 path, 1.1e-6 bf16x3, 1.2e-6 fp32 MFMA);
-* the small parametrized configurations (20-160 nodes, up to 3 layers): 2e-5 per column.  Their
-  batch statistics come from a few dozen nodes and amplify the fp32 rounding of every path alike:
-  measured worst 7.1e-6 with the fp32 MFMA kernels (NBX_X3=0), 8.6e-6 bf16x3, 1.04e-5 fp16x2
-  (profiles/r05/xcd/acc_*.log); the bound is 2-3x the fp32 path's own error;
+* the small parametrized configurations (10-160 nodes, up to 3 layers), keyed on the path (small_rel):
+  1e-5 per column for the fp32-MFMA and bf16x3 paths, 1.5e-5 for the default fp16x2 path.  Measured
+  worst (profiles/r05/xcd/acc_*.log, at hidden 32 / B 4 = 20 nodes): 7.1e-6 fp32 MFMA, 8.6e-6 bf16x3,
+  1.04e-5 fp16x2.  The same configurations computed by the torch fp32 restatement in 12 summation
+  orders reach 0.4-2.7e-6 (tests/golden/segnn_small_ensemble.json): every native path is 3-5x that
+  on these few-node batches, fp16x2 1.4x the fp32-MFMA path (DESIGN.md §3.5c);
 * rollouts: per-frame relative error budget growing with the horizon (fp32 rounding is
   amplified by the autoregressive feedback) and north_star's rollout MSE <= 1e-5, checked
   at the C2 configuration (hidden 192, 6 layers, B=1024) over 10 steps against the fixture
@@ -78,7 +80,17 @@ def assert_close(got, ref, rel=2e-4, abs_=1e-5):
     assert err <= rel * scale + abs_, f"max err {err:.3e} vs scale {scale:.3e}"
 
 
-SMALL_REL = 2e-5   # the small parametrized configurations (module docstring)
+def small_rel(env=None):
+    """Per-column tolerance of the small parametrized configurations (module docstring), keyed on the
+    kernel path the library runs: 1e-5 for the fp32-MFMA (NBX_X3=0) and bf16x3 (NBX_SPLIT=x3) paths,
+    1.5e-5 for the default fp16x2 path."""
+    import os
+    env = os.environ if env is None else env
+    fp32_like = env.get("NBX_X3") == "0" or env.get("NBX_SPLIT", "")[:1] in ("x", "1", "0")
+    return 1e-5 if fp32_like else 1.5e-5
+
+
+SMALL_REL = small_rel()
 
 
 def assert_close_cols(got, ref, rel=1e-5, abs_=1e-7):
@@ -370,31 +382,77 @@ def ensemble_agreement(sys_err, k):
     return tau, (sys_err[:, k, :] <= tau).mean(1)
 
 
-def c2_rollout_envelope_check(tp, tv, rl, rv, ens, label="device"):
-    """Places a C2 rollout (positions tp, velocities tv [B, T, N, 3]) in the ensemble of equally valid
-    fp32 computations (tests/golden/make_segnn_c2_ensemble.py).  Returns the list of failed checks:
-    at every step k >= 1, pos and vel MSE vs the fp64 oracle <= the ensemble's largest, and the
-    fraction of systems within the step's agreement threshold >= the ensemble's smallest."""
+def rollout_sample_stats(tp, tv, rl, rv, ens):
+    """Per step k >= 1 of one rollout: (pos MSE, vel MSE, fraction of systems within tau_k) vs the fp64
+    oracle; the per-system error is max over the system's bodies of |pos - fp64| / max |fp64| of the frame."""
     B, T = tp.shape[0], tp.shape[1]
-    bad = []
+    out = []
     for k in range(1, T):
-        ml = float(((tp[:, k] - rl[:, k]) ** 2).mean())
-        mv = float(((tv[:, k] - rv[:, k]) ** 2).mean())
         se = np.abs(tp[:, k] - rl[:, k]).reshape(B, -1).max(1) / np.abs(rl[:, k]).max()
-        tau, fr_ens = ensemble_agreement(ens["sys_err"], k)
-        fr = float((se <= tau).mean())
+        tau, _ = ensemble_agreement(ens["sys_err"], k)
+        out.append((float(((tp[:, k] - rl[:, k]) ** 2).mean()), float(((tv[:, k] - rv[:, k]) ** 2).mean()),
+                    float((se <= tau).mean())))
+    return np.array(out)   # [T - 1, 3]
+
+
+ENS_Q = 1.0   # the device samples' median must lie inside the ensemble's range (its max MSE, its min agreement)
+
+
+def c2_rollout_envelope_check(samples, ens, label="device", q=None):
+    """Compares a set of device rollouts of the C2 fixture (samples: [S, T - 1, 3] from rollout_sample_stats,
+    S equally valid device computations: the same batch with its systems permuted) with the ensemble of
+    equally valid fp32 computations of tests/golden/make_segnn_c2_ensemble.py, per step k >= 1:
+      * median over the device samples of the pos MSE and of the vel MSE <= the ensemble's largest;
+      * median over the device samples of the per-system agreement fraction >= the ensemble's smallest
+    (q < 1: the ensemble's q-quantile instead).  The median of several draws is compared because past the
+    predictable horizon (5 steps) one rollout is one draw from a heavy-tailed distribution (the ensemble's
+    step-6 pos MSE spans 7e-9 .. 4e-4): measured, 3-4 of 8 single draws of the default, the bf16x3 and the
+    materialised-dot paths land beyond the ensemble's extremes at some step, and which ones changes with
+    any rounding-order change.  Returns the failed checks; prints the placement."""
+    q = ENS_Q if q is None else q   # q = 1: the ensemble's extremes (a single draw against max / min)
+    bad = []
+    T1 = samples.shape[1]
+    for j in range(T1):
+        k = j + 1
         el, ev = ens["mse_loc"][:, k], ens["mse_vel"][:, k]
-        rank = int((el < ml).sum())
-        print(f"C2 rollout step {k} ({label}): pos MSE {ml:.2e} (ensemble {el.min():.1e}..{el.max():.1e}, "
-              f"{rank} of {len(el)} members closer) vel MSE {mv:.2e} (ensemble max {ev.max():.1e}) | systems "
-              f"within {tau:.1e}: {fr:.4f} (ensemble min {fr_ens.min():.4f}, median {np.median(fr_ens):.4f})")
-        if ml > el.max():
-            bad.append((k, "pos MSE above the ensemble", ml, float(el.max())))
-        if mv > ev.max():
-            bad.append((k, "vel MSE above the ensemble", mv, float(ev.max())))
-        if fr < fr_ens.min():
-            bad.append((k, "per-system agreement below the ensemble", fr, float(fr_ens.min())))
+        _, fr_ens = ensemble_agreement(ens["sys_err"], k)
+        ml, mv, fr = (float(np.median(samples[:, j, c])) for c in range(3))
+        ql, qv, qf = float(np.quantile(el, q)), float(np.quantile(ev, q)), float(np.quantile(fr_ens, 1 - q))
+        print(f"C2 rollout step {k} ({label}, {samples.shape[0]} samples): pos MSE median {ml:.2e} "
+              f"[{samples[:, j, 0].min():.1e} .. {samples[:, j, 0].max():.1e}] (ensemble p50 {np.median(el):.1e} "
+              f"q{q:g} {ql:.1e} max {el.max():.1e}) | vel MSE median {mv:.2e} (ensemble q{q:g} {qv:.1e}) | systems within "
+              f"tau: median {fr:.4f} (ensemble q{1 - q:g} {qf:.4f}, min {fr_ens.min():.4f})")
+        if ml > ql:
+            bad.append((k, f"pos MSE median above the ensemble's q{q:g}", ml, ql))
+        if mv > qv:
+            bad.append((k, f"vel MSE median above the ensemble's q{q:g}", mv, qv))
+        if fr < qf:
+            bad.append((k, f"agreement median below the ensemble's q{1 - q:g}", fr, qf))
     return bad
+
+
+def c2_device_samples(model, fx, ens, device, n_samples=8):
+    """n_samples device rollouts of the C2 fixture: the batch as given, then with its systems permuted
+    (a permutation of the batch is the same problem; train-mode BatchNorm is permutation invariant)
+    -- every kernel sums in another order; trajectories permuted back.  Returns (stats [S, T - 1, 3],
+    the first rollout's (tp, tv))."""
+    rl, rv = fx["traj_loc"].astype(np.float64), fx["traj_vel"].astype(np.float64)
+    T = rl.shape[1]
+    B = rl.shape[0]
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=device)
+    stats, first = [], None
+    for s in range(n_samples):
+        perm = np.arange(B) if s == 0 else np.random.default_rng(7000 + s).permutation(B)
+        inv = np.argsort(perm)
+        model.load_state_dict(sd0)
+        tp, tv = model.rollout(t(fx["loc0"][perm]), t(fx["vel0"][perm]), t(np.ones((B,) + fx["loc0"].shape[1:2] + (1,))), T)
+        tp, tv = tp.double().cpu().numpy()[inv], tv.double().cpu().numpy()[inv]
+        assert np.isfinite(tp).all() and np.isfinite(tv).all()
+        if s == 0:
+            first = (tp, tv)
+        stats.append(rollout_sample_stats(tp, tv, rl, rv, ens))
+    return np.stack(stats), first
 
 
 def test_rollout_c2_matches_oracle_fixture(hip_device):
@@ -405,19 +463,18 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
     With random-init weights this rollout turns chaotic after ~5 steps (bodies are flung to
     |pos| ~ 50-75 and pairs pass within ~1e-3 of each other, where r-hat is ill-conditioned;
     system 595 passes a near-collision at step 6 and train-mode BatchNorm couples every system to it).
-    Past that point one fp32 sample cannot separate "another valid rounding" from "worse", so the
-    check is against an ENSEMBLE of 41 equally valid fp32 computations of the same rollout
+    Past that point a rollout is one draw from a heavy-tailed distribution, so the check compares
+    distributions: 8 device rollouts (the batch with its systems permuted: every kernel sums in another
+    order) against an ENSEMBLE of 41 equally valid fp32 computations of the same rollout
     (tests/golden/make_segnn_c2_ensemble.py: the numpy and torch fp32 restatements, systems permuted,
     edge lists shuffled, every GEMM's contraction order permuted, a quarter of the systems rounded to
     the neighbouring fp32 value, and fp64 rollouts from such states).  At step 6 the ensemble's pos MSE
     spans 7.1e-9 .. 3.7e-4 (the torch fp32 restatement in its natural order: 1.7e-4).
-    Checks, per step k = 1..10:
-      * pos and vel MSE(device, fp64 oracle) <= the largest of the ensemble;
-      * the fraction of systems whose error (max over its bodies / max |pos| of the frame) is within
-        tau_k = 10 x the ensemble's median per-system error >= the smallest fraction of any member;
-      * over the predictable horizon (every step where the numpy fp32 oracle stays within MSE 1e-7 of
-        the fp64 one; 5 steps here): MSE <= 1e-5 (north_star) and <= 10x the fp32-oracle MSE.
-    Where the kernel paths fall in the ensemble: DESIGN.md §3.5c (scripts/rollout_paths.py)."""
+    Checks, per step k = 1..10 (c2_rollout_envelope_check): the device samples' median pos / vel MSE
+    <= the ensemble's largest, their median per-system agreement >= the ensemble's smallest; and
+    over the predictable horizon (every step where the numpy fp32 oracle stays within MSE 1e-7 of the
+    fp64 one; 5 steps here), on the unpermuted rollout: MSE <= 1e-5 (north_star) and <= 10x the
+    fp32-oracle MSE.  Where the kernel paths fall: DESIGN.md §3.5c (scripts/rollout_paths.py)."""
     import nbody_amd.segnn as S2
     fx = c2_fixture()
     ens = c2_ensemble()
@@ -427,14 +484,11 @@ def test_rollout_c2_matches_oracle_fixture(hip_device):
     cs = float(sum(t.double().abs().sum().item() for t in model.state_dict().values()))
     assert abs(cs - float(fx["weight_checksum"])) <= 1e-9 * abs(cs), "C2 weights differ from the fixture's"
     model = model.to(hip_device).train()
-    rl, rv = fx["traj_loc"].astype(np.float64), fx["traj_vel"].astype(np.float64)
+    rl = fx["traj_loc"].astype(np.float64)
     fl = fx["f32_loc"].astype(np.float64)
     T = rl.shape[1]
-    t = lambda a: torch.tensor(a, dtype=torch.float32, device=hip_device)
-    tp, tv = model.rollout(t(fx["loc0"]), t(fx["vel0"]), t(np.ones(fx["loc0"].shape[:2] + (1,))), T)
-    tp, tv = tp.double().cpu().numpy(), tv.double().cpu().numpy()
-    assert np.isfinite(tp).all() and np.isfinite(tv).all()
-    bad = c2_rollout_envelope_check(tp, tv, rl, rv, ens)
+    samples, (tp, _) = c2_device_samples(model, fx, ens, hip_device)
+    bad = c2_rollout_envelope_check(samples, ens)
     horizon = 0
     for k in range(1, T):
         mse = float(((tp[:, k] - rl[:, k]) ** 2).mean())

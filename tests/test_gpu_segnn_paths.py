@@ -74,7 +74,7 @@ def test_segnn_path_switch_matches_oracle(env, oracle_outputs):
     assert not isinstance(outs, str), outs
     for (hidden, layers, B, N), got, ref in zip(CONFIGS, outs, oracle_outputs):
         print(f"[{env or 'default'}] hidden {hidden} layers {layers} B {B}")
-        T.assert_close_cols(got, ref, rel=T.SMALL_REL)
+        T.assert_close_cols(got, ref, rel=T.small_rel(env))
 
 
 def _child_c2(env, q):

@@ -25,6 +25,7 @@ sys.path.insert(0, HERE)
 # setting -> families it touches
 SWITCHES = [
     ({"NBX_PO_X3": "0"}, ["ponita"]),
+    ({"NBX_PO_SPLIT": "x3"}, ["ponita"]),
     ({"NBX_PO_BASIS1": "0"}, ["ponita"]),
     ({"NBX_PO_BASIS_FUSED": "0"}, ["ponita"]),
     ({"NBX_PO_FIB_ONEPASS": "0"}, ["ponita"]),
@@ -37,6 +38,7 @@ SWITCHES = [
     ({"NBX_ET_MEMSET": "1"}, ["egnn_grad"]),
     ({"NBX_ET_DEBUG": "1"}, ["egnn_grad"]),
     ({"NBX_EQ_NPW": "1"}, ["eqv2"]),
+    ({"NBX_EQ_SPLIT": "x3"}, ["eqv2"]),
     ({"NBX_EQ_NB": "4"}, ["eqv2"]),
     ({"NBX_EQV2_S2_NA0": "1"}, ["eqv2"]),
     ({"NBX_EQV2_SPECIALISED": "1"}, ["eqv2_grad"]),
