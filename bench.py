@@ -372,7 +372,7 @@ def pmc_traffic(kernel_name, model=None):
 _PO_PREC = "1" if os.environ.get("NBX_PO_SPLIT", "")[:1] in ("x", "1") else "2"
 PONITA_KIND_NAMES = [f"void nbx::lin_kernel<4, 0, 1, {_PO_PREC}>(nbx::LinProb)",
                      f"void (anonymous namespace)::po_ffn_kernel<4, 4, 0, {_PO_PREC}>((anonymous namespace)::FfnProb)",
-                     "void nbx::lin_rp_kernel<4, 0>(nbx::LinRpProb)",
+                     "void nbx::lin_rp_kernel<4, 0, 1>(nbx::LinRpProb)",
                      f"void (anonymous namespace)::po_ffn_kernel<1, 4, 1, {_PO_PREC}>((anonymous namespace)::FfnProb)",
                      "void (anonymous namespace)::po_fiber_ln1_kernel<20, 4, 512>(float const*, float const*, int, "
                      "float const*, float const*, float const*, long, int, int, int, int, float*, double*)"]
@@ -440,6 +440,10 @@ def bench_ponita(a, rank, world, device, P):
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
     roof.update({"traffic": pmc_traffic(PONITA_KIND_NAMES[dom], "ponita"), "kernel": PONITA_KIND_NAMES[dom],
                  "role": PONITA_KIND_ROLES[dom], "avg_launch_us": round(dom_s * 1e6, 2), "per_kind": per_kind})
+    if dom in (0, 1, 3):   # a split-precision GEMM kernel: the 16-bit MFMA products actually issued
+        roof.update({"mfma_path": ("fp16x2 split (fp32-accurate), v_mfma_f32_32x32x16_f16" if _PO_PREC == "2" else
+                                   "bf16x3 split (fp32-accurate), v_mfma_f32_32x32x16_bf16"),
+                     "executed_16bit_frac": round(ach * SPLIT_TERMS[int(_PO_PREC)] / BF16_MFMA_PEAK_TFLOPS, 4)})
     value = a.steps / elapsed
     result = {
         "metric": "self-feed rollout steps/sec, PONITA N=5 batch=4096", "value": round(value, 3), "unit": "steps/s",
@@ -887,9 +891,12 @@ EQV2_KINDS = ["radial hidden layers (per-edge layer + GEMM with LayerNorm/SiLU e
               "radial output GEMM + rotated-message epilogue (A0/A1)", "SO(2) conv 1, m=0 GEMM",
               "SO(2) conv 1, m=1 GEMM", "separable S2 activation + attention logits", "SO(2) conv 2 GEMMs",
               "node kernels (softmax, inverse rotation, proj, FFN, norms)", "edge frame + edge-degree embedding"]
-# rocprofv3 names of the one-launch GEMM kinds at C4 (eqv2.hip gemm_rp: row-panel bf16x3, all output
-# columns per workgroup; 288 = 32 alpha + 4 x 64 hidden m=0 outputs -> 9 tiles, 4 x 64 m=1 outputs -> 8)
-EQV2_GEMM_NAMES = {2: "void nbx::lin_rp_kernel<9, 0>(nbx::LinRpProb)", 3: "void nbx::lin_rp_kernel<8, 0>(nbx::LinRpProb)"}
+# rocprofv3 names of the one-launch GEMM kinds at C4 (eqv2.hip gemm_rp: row-panel split-precision GEMM, all
+# output columns per workgroup; 288 = 32 alpha + 4 x 64 hidden m=0 outputs -> 9 tiles, 4 x 64 m=1 outputs -> 8;
+# PREC 2 on the fp16x2 images, the default since r06, 1 on the bf16x3 ones with NBX_EQ_SPLIT=x3)
+_EQ_PREC = "1" if os.environ.get("NBX_EQ_SPLIT", "")[:1] in ("x", "1") else "2"
+EQV2_GEMM_NAMES = {2: f"void nbx::lin_rp_kernel<9, 0, {_EQ_PREC}>(nbx::LinRpProb)",
+                   3: f"void nbx::lin_rp_kernel<8, 0, {_EQ_PREC}>(nbx::LinRpProb)"}
 
 
 def bench_eqv2(a, rank, world, device, P):
@@ -941,9 +948,11 @@ def bench_eqv2(a, rank, world, device, P):
             "traffic": pmc_traffic(EQV2_GEMM_NAMES[dom], "eqv2"), "avg_launch_us": round(g_avg_s * 1e6, 2),
             "gflop_per_launch": round(acc[2, dom] / acc[1, dom] / 1e9, 4),
             "algorithmic_mb_per_launch": round(acc[3, dom] / acc[1, dom] / 1e6, 3),
-            "mfma_path": "bf16x3 split (fp32-accurate), v_mfma_f32_32x32x16_bf16",
-            "executed_bf16_tflops": round(ach * X3_TERMS, 2),
-            "executed_bf16_frac": round(ach * X3_TERMS / BF16_MFMA_PEAK_TFLOPS, 4),
+            "mfma_path": ("fp16x2 split (fp32-accurate), v_mfma_f32_32x32x16_f16" if _EQ_PREC == "2" else
+                          "bf16x3 split (fp32-accurate), v_mfma_f32_32x32x16_bf16"),
+            # the 16-bit MFMA products actually issued (bf16x3: 6, fp16x2: 3 per fp32 product)
+            "executed_16bit_tflops": round(ach * SPLIT_TERMS[int(_EQ_PREC)], 2),
+            "executed_16bit_frac": round(ach * SPLIT_TERMS[int(_EQ_PREC)] / BF16_MFMA_PEAK_TFLOPS, 4),
             "timing": "HIP event pairs around each launch group on the launch stream",
             "gemm_share_of_forward": round(gemm_ms / fwd, 3), "per_kind": per_kind}
     value = a.steps / elapsed * world
