@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 17
+ABI_VERSION = 18
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B, GEMM_B_ONES, GEMM_ONES_TAIL = 1, 2, 4, 8
@@ -89,7 +89,7 @@ EQV2_MAX_LAYERS = 32
 
 class Eqv2Radial(ctypes.Structure):
     _fields_ = [(n, c_p) for n in ("a", "c", "us", "ut", "ln1_w", "ln1_b", "w1", "b1", "ln2_w", "ln2_b", "w2_x3", "w2",
-                                   "b2")]
+                                   "b2", "w1_h2", "w2_h2")] + [(n, c_f) for n in ("w1_sinv", "w2_sinv")]
 
 
 class Eqv2Attn(ctypes.Structure):

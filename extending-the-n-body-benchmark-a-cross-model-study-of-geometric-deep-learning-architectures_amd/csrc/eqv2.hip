@@ -152,6 +152,152 @@ __global__ __launch_bounds__(256) void eqv2_radial_kernel(const float* __restric
     }
 }
 
+// ---- both RadialFunction hidden layers in one launch on the fp16x2 path (net.3 image W.w1_h2): a wave
+// owns a 32-edge tile.  Lane (r, h) forms the first layer of edge r at k = 32 c + 16 h + [0, 16) (chunk
+// c) in registers -- the A-fragment layout of v_mfma_f32_32x32x16_f16 (lin.h lin_kernel: lane (r, h)
+// holds k = 16 h + 4 q + e of a 32-deep chunk) -- with the row's LayerNorm statistics from the lane's
+// values plus one shuffle with its partner half; then net.3 on the fp16x2 image in LDS and the
+// LIN_LNSILU epilogue (bias, LayerNorm over the He columns, SiLU).  H1 never leaves registers.
+constexpr int RAD_WAVES = 4;
+template <int HE>
+__global__ __launch_bounds__(64 * RAD_WAVES, 2) void eqv2_radial_h2_kernel(const float* __restrict__ rot,
+                                                                       const int* __restrict__ zn,
+                                                                       const nbx_eqv2_radial W, int64_t E, int N,
+                                                                       float* __restrict__ H2, int* range_flag) {
+    constexpr int NC = HE / 32;                  // K chunks = output column tiles
+    constexpr int BLK = nbx::LIN_H2_BLK;
+    using SP = nbx::SplitP<2>;
+    using SPT = SP::T;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* cst = lds + NC * NC * BLK;            // a | c | ln1_w | ln1_b, HE floats each
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+    nbx::tp_dma_image<RAD_WAVES>(static_cast<const float*>(W.w1_h2), lds, NC * NC * BLK);
+    for (int i = t; i < 4 * HE; i += 64 * RAD_WAVES) {
+        const int q = i / HE, k = i - q * HE;
+        cst[i] = (q == 0 ? W.a : q == 1 ? W.c : q == 2 ? W.ln1_w : W.ln1_b)[k];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float bb[NC], gw[NC], gb[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        bb[j] = W.b1[32 * j + r];
+        gw[j] = W.ln2_w[32 * j + r];
+        gb[j] = W.ln2_b[32 * j + r];
+    }
+    const float inv = 1.0f / HE;
+    const SPT* ldsx = reinterpret_cast<const SPT*>(lds);
+    const __amdgpu_buffer_rsrc_t rsH2 = __builtin_amdgcn_make_buffer_rsrc((void*)H2, (short)0, 0x7FFFFFF0, 0x00020000);
+    const int64_t tiles = (E + 31) >> 5;
+    float zguard = 0.f;
+    for (int64_t tile = (int64_t)blockIdx.x * RAD_WAVES + wave; tile < tiles; tile += (int64_t)gridDim.x * RAD_WAVES) {
+        const int64_t e = tile * 32 + r;
+        const int64_t ee = e < E ? e : E - 1;
+        int64_t s, tt;
+        edge_nodes(ee, N, s, tt);
+        const float d = rot[ee * ROT + 24];
+        const float* us = W.us + (size_t)zn[s] * HE + 16 * h;
+        const float* ut = W.ut + (size_t)zn[tt] * HE + 16 * h;
+        // first layer: v = d a + c + us[z_src] + ut[z_dst] (eqv2_radial_kernel's order)
+        float v[NC][16];
+        float sum = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 u = *reinterpret_cast<const float4*>(us + 32 * c + 4 * q);
+                const float4 w = *reinterpret_cast<const float4*>(ut + 32 * c + 4 * q);
+                const float4 a = *reinterpret_cast<const float4*>(cst + 32 * c + 16 * h + 4 * q);
+                const float4 cc = *reinterpret_cast<const float4*>(cst + HE + 32 * c + 16 * h + 4 * q);
+                v[c][4 * q + 0] = d * a.x + cc.x + u.x + w.x;
+                v[c][4 * q + 1] = d * a.y + cc.y + u.y + w.y;
+                v[c][4 * q + 2] = d * a.z + cc.z + u.z + w.z;
+                v[c][4 * q + 3] = d * a.w + cc.w + u.w + w.w;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sum += v[c][4 * q + i];
+                if (q == 3) __builtin_amdgcn_sched_barrier(0);   // one chunk's loads live at a time (VGPR budget)
+            }
+        sum += __shfl_xor(sum, 32);
+        const float mu = sum * inv;
+        float sq = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                v[c][i] -= mu;
+                sq += v[c][i] * v[c][i];
+            }
+        sq += __shfl_xor(sq, 32);
+        const float rsd = 1.0f / sqrtf(sq * inv + 1e-5f);
+        nbx::floatx16 acc[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            float hv[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 g = *reinterpret_cast<const float4*>(cst + 2 * HE + 32 * c + 16 * h + 4 * q);
+                const float4 b = *reinterpret_cast<const float4*>(cst + 3 * HE + 32 * c + 16 * h + 4 * q);
+                hv[4 * q + 0] = silu(v[c][4 * q + 0] * rsd * g.x + b.x);
+                hv[4 * q + 1] = silu(v[c][4 * q + 1] * rsd * g.y + b.y);
+                hv[4 * q + 2] = silu(v[c][4 * q + 2] * rsd * g.z + b.z);
+                hv[4 * q + 3] = silu(v[c][4 * q + 3] * rsd * g.w + b.w);
+            }
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {   // MFMA m takes k = 16 h + 8 m + [0, 8)
+                SPT a[SP::NP];
+                SP::split(make_float4(hv[8 * m], hv[8 * m + 1], hv[8 * m + 2], hv[8 * m + 3]),
+                          make_float4(hv[8 * m + 4], hv[8 * m + 5], hv[8 * m + 6], hv[8 * m + 7]), a);
+#pragma unroll
+                for (int j = 0; j < NC; ++j) {
+                    const SPT* bp = ldsx + (j * NC + c) * (BLK / 4) + lane;
+                    SPT b[SP::NP];
+#pragma unroll
+                    for (int p3 = 0; p3 < SP::NP; ++p3) b[p3] = bp[(2 * p3 + m) * 64];
+#pragma unroll
+                    for (int tt3 = 0; tt3 < SP::NT; ++tt3) acc[j] = nbx::mfma32x32(a[SP::TA[tt3]], b[SP::TB[tt3]], acc[j]);
+                }
+            }
+        }
+        // epilogue (lin.h LIN_LNSILU): undo the weight scale, guard, bias, LayerNorm over HE, SiLU
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                acc[j][i] *= W.w1_sinv;
+                zguard = nbx::tp_nonfinite_fold(zguard, acc[j][i]);
+            }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int64_t row = tile * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            float y[NC], sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                y[j] = acc[j][i] + bb[j];
+                sm += y[j];
+            }
+            for (int o = 16; o > 0; o >>= 1) sm += __shfl_xor(sm, o);   // the 32 lanes of this row
+            const float m2 = sm * inv;
+            float q2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) q2 += (y[j] - m2) * (y[j] - m2);
+            for (int o = 16; o > 0; o >>= 1) q2 += __shfl_xor(q2, o);
+            const float rs = 1.0f / sqrtf(q2 * inv + 1e-5f);
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {   // 32-bit offsets (E HE < 2^29, eqv2_prepare), rows past E dropped
+                const float z = (y[j] - m2) * rs * gw[j] + gb[j];
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, z * __builtin_amdgcn_rcpf(1.0f + __expf(-z))), rsH2,
+                                                      row < E ? (uint32_t)((row * HE + 32 * j + r) * 4) : 0x7FFFFFF0u,
+                                                      0, 0);
+            }
+        }
+    }
+    nbx::tp_range_flag(range_flag, zguard);
+}
+
 // softmax over a node's deg incoming edges for head `lane` (segment softmax + 1e-16, PyG): alpha[q] ->
 // sal[q * 8 + lane].  Up to 32 edges the logits are loaded in one predicated batch into registers (the
 // loop form waited one memory latency per edge, twice); the arithmetic and its order are unchanged.
@@ -842,8 +988,24 @@ unsigned gwave(int64_t n) { return (unsigned)std::min<int64_t>(nbx::ceil_div(n >
 
 // H2 = SiLU(LN(W1 SiLU(LN(h1_pre)) + b1)): the per-edge first layer, then an MFMA GEMM with the
 // LayerNorm + SiLU epilogue (He = 32 or 64 columns: one column chunk).  H1 lives in the A0 buffer.
+bool eq_h2_enabled();
+
 int radial(const nbx_eqv2_weights* w, const nbx_eqv2_radial& R, const EqWs& ws, int64_t E, int N, hipStream_t st) {
     const int He = w->edge_channels;
+    static const bool two = getenv("NBX_EQ_RAD2") && getenv("NBX_EQ_RAD2")[0] == '1';   // A/B: the two-launch form
+    if (R.w1_h2 && eq_h2_enabled() && !two) {   // one launch (eqv2_radial_h2_kernel)
+        const int64_t tiles = (E + 31) / 32;
+        const unsigned blocks = (unsigned)std::min<int64_t>(nbx::ceil_div(tiles, RAD_WAVES), 4096);
+        const size_t lds = ((size_t)(He / 32) * (He / 32) * nbx::LIN_H2_BLK + 4 * He) * 4;
+        if (He == 64)
+            hipLaunchKernelGGL(eqv2_radial_h2_kernel<64>, dim3(blocks), dim3(64 * RAD_WAVES), lds, st, ws.rot, ws.zn, R,
+                               E, N, ws.H2, ws.RANGE);
+        else
+            hipLaunchKernelGGL(eqv2_radial_h2_kernel<32>, dim3(blocks), dim3(64 * RAD_WAVES), lds, st, ws.rot, ws.zn, R,
+                               E, N, ws.H2, ws.RANGE);
+        NBX_LAUNCH_CHECK("eqv2 radial (fp16x2, one launch)");
+        return NBX_OK;
+    }
     float* H1 = ws.A0;
     if (He == 64)
         hipLaunchKernelGGL(eqv2_radial_kernel<64>, dim3(gwave(E)), dim3(256), 0, st, ws.rot, ws.zn, R, E, N, H1);
@@ -1000,7 +1162,14 @@ int eqv2_forward_impl(const nbx_eqv2_weights* w, const float* pos, const float* 
     {
         nbx::LinProb p = nbx::lin_dense(ws.H2, He, He, (int)E, w->edge_degree.w2, He, 3 * C, w->edge_degree.b2, ws.Y0,
                                         3 * C);
-        if (int rc = nbx::lin_launch<2, nbx::ACT_NONE>(p, st)) return rc;
+        if (w->edge_degree.w2_h2 && eq_h2_enabled()) {   // fp16x2 (3C % 32 == 0: C is 32 or 64)
+            p.Wh2 = w->edge_degree.w2_h2;
+            p.h2_sinv = w->edge_degree.w2_sinv;
+            p.range_flag = ws.RANGE;
+            if (int rc = nbx::lin_launch<2, nbx::ACT_NONE, nbx::LIN_STORE, 2>(p, st)) return rc;
+        } else if (int rc = nbx::lin_launch<2, nbx::ACT_NONE>(p, st)) {
+            return rc;
+        }
     }
     {
         NodeArgs a = node_args(w, ws, N);

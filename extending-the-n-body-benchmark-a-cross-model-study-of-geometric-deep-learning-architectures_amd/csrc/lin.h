@@ -185,18 +185,30 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
         }
     };
 
+    // A streams in steps of SUP 32-deep chunks: two chunks for the fp16x2 gathering convolution (8 KB per
+    // wave in flight behind the step being consumed instead of 4 KB: C3's spatial conv 500 -> 478 us,
+    // profiles/r06/lin_sup), otherwise one (EquiformerV2's so2_conv_2 GEMMs measured 64 -> 70 us with
+    // two).  A step past the last chunk loads zeros (out-of-range offsets) and is not consumed.
+    constexpr int SUP = (PREC == 2 && EPI == LIN_CONV) ? 2 : 1;
+    const int n_steps = (n_chunks + SUP - 1) / SUP;
+    auto load_s = [&](int64_t s0, int64_t s1, int64_t s2, bool ok, int st, float4 (&a)[4 * SUP]) {
+#pragma unroll
+        for (int u = 0; u < SUP; ++u)
+            load_a(s0, s1, s2, ok, SUP * st + u, *reinterpret_cast<float4(*)[4]>(&a[4 * u]));
+    };
+
     int rt = blk * LIN_WAVES + wave;
     if (rt >= row_tiles) return;
-    // A is double-buffered with the two buffers' roles fixed by an unroll-by-2 of the chunk
-    // loop (bA <- even chunks, bB <- odd chunks), the next tile's chunk 0 always landing in bA
-    // during the current tile's last chunk.  No register move ever reads a load still in
-    // flight, so the waitcnt pass waits only for the chunk about to be consumed (a
-    // cur <- nxt <- nx2 shuffle would force vmcnt(0) on every chunk).
-    float4 bA[4], bB[4];
+    // A is double-buffered with the two buffers' roles fixed by an unroll-by-2 of the step
+    // loop (bA <- even steps, bB <- odd steps), the next tile's step 0 always landing in bA
+    // during the current tile's last step.  No register move ever reads a load still in
+    // flight, so the waitcnt pass waits only for the step about to be consumed (a
+    // cur <- nxt <- nx2 shuffle would force vmcnt(0) on every step).
+    float4 bA[4 * SUP], bB[4 * SUP];
     int64_t r0, r1, r2;
     bool rok;
     tile_rows(rt, r0, r1, r2, rok);
-    load_a(r0, r1, r2, rok, 0, bA);
+    load_s(r0, r1, r2, rok, 0, bA);
     while (true) {
         floatx16 acc[NT];
 #pragma unroll
@@ -248,29 +260,36 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
                 for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q].w, b4[j].w, acc[j], 0, 0, 0);
             }
         };
+        // the chunks of step st (a step's second chunk past the last is skipped, wave-uniform)
+        auto consume_s = [&](const float4 (&cur)[4 * SUP], int st) {
+#pragma unroll
+            for (int u = 0; u < SUP; ++u)
+                if (u == 0 || SUP * st + u < n_chunks)
+                    consume(*reinterpret_cast<const float4(*)[4]>(&cur[4 * u]), (SUP * st + u) * 32);
+        };
         const int nrt = rt + wstride;       // next tile of this wave
         int i = 0;
         int64_t n0r, n1r, n2r;              // next tile's source rows
         bool nok = false;
         // sched_barrier keeps each prefetch issued ahead of the MFMAs that follow it
-        for (; i + 1 < n_chunks; i += 2) {
-            load_a(r0, r1, r2, rok, i + 1, bB);
+        for (; i + 1 < n_steps; i += 2) {
+            load_s(r0, r1, r2, rok, i + 1, bB);
             __builtin_amdgcn_sched_barrier(0);
-            consume(bA, i * 32);
-            if (i + 2 < n_chunks) {
-                load_a(r0, r1, r2, rok, i + 2, bA);
+            consume_s(bA, i);
+            if (i + 2 < n_steps) {
+                load_s(r0, r1, r2, rok, i + 2, bA);
             } else if (nrt < row_tiles) {
                 tile_rows(nrt, n0r, n1r, n2r, nok);
-                load_a(n0r, n1r, n2r, nok, 0, bA);
+                load_s(n0r, n1r, n2r, nok, 0, bA);
             }
             __builtin_amdgcn_sched_barrier(0);
-            consume(bB, (i + 1) * 32);
+            consume_s(bB, i + 1);
         }
-        if (i < n_chunks) {                 // odd chunk count: the last chunk sits in bA
-            consume(bA, i * 32);
+        if (i < n_steps) {                  // odd step count: the last step sits in bA
+            consume_s(bA, i);
             if (nrt < row_tiles) {
                 tile_rows(nrt, n0r, n1r, n2r, nok);
-                load_a(n0r, n1r, n2r, nok, 0, bA);
+                load_s(n0r, n1r, n2r, nok, 0, bA);
             }
         }
         if constexpr (PREC == 2) {   // undo the image's weight scale; fp16x2 range guard
@@ -591,9 +610,9 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
             }
         }
     };
-    if constexpr (NTILES <= 5) {
-        // small panels (N <= 160): three LDS slabs and two A register buffers, both streams issued two
-        // chunks ahead.  At the end of chunk kc only chunk kc + 2's slab pieces and A loads may still be
+    if constexpr (NTILES <= 5 || PREC == 2) {
+        // small panels (N <= 160), and any panel on fp16x2 images (2/3 of the bf16x3 slab): three LDS
+        // slabs and two A register buffers, both streams issued two chunks ahead.  At the end of chunk kc only chunk kc + 2's slab pieces and A loads may still be
         // in flight: vmcnt(this wave's slab pieces + 4) (the slab pieces per wave are counted so the
         // immediate is exact; a slab is BLK / 256 pieces per column tile).
         const int ndma = ((BLK / 256) * NTILES - wave + RP_WAVES - 1) / RP_WAVES;
@@ -603,6 +622,7 @@ __global__ __launch_bounds__(64 * RP_WAVES, 1) void lin_rp_kernel(const LinRpPro
                 case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
                 case 3: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
                 case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+                case 5: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
                 default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
             }
         };
@@ -703,7 +723,7 @@ int lin_rp_launch(const LinRpProb& p, hipStream_t st) {
         set_error("lin_rp: A spans >= 2 GiB");
         return NBX_E_UNSUPPORTED;
     }
-    const size_t lds = (NTILES <= 5 ? 3 : 2) * (size_t)NTILES * (PREC == 2 ? LIN_H2_BLK : LIN_X3_BLK) * 4;
+    const size_t lds = ((NTILES <= 5 || PREC == 2) ? 3 : 2) * (size_t)NTILES * (PREC == 2 ? LIN_H2_BLK : LIN_X3_BLK) * 4;
     NBX_LDS_160K((lin_rp_kernel<NTILES, ACT, PREC>));
     const unsigned blocks = (unsigned)((p.rows + 32 * RP_WAVES - 1) / (32 * RP_WAVES));
     hipLaunchKernelGGL((lin_rp_kernel<NTILES, ACT, PREC>), dim3(blocks), dim3(64 * RP_WAVES), lds, st, p);

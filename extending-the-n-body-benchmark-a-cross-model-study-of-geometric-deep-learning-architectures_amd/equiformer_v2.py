@@ -419,6 +419,7 @@ class EquiformerV2_nbody(nn.Module):
             P[prefix + "ln1_w"], P[prefix + "ln1_b"] = v(net[1].weight), v(net[1].bias)
             P[prefix + "w1"], P[prefix + "b1"] = v(net[3].weight), v(net[3].bias)
             P[prefix + "ln2_w"], P[prefix + "ln2_b"] = v(net[4].weight), v(net[4].bias)
+            P[prefix + "w1_h2"], P[prefix + "w1_sinv"] = self._image_h2(net[3].weight.detach().to(device))
             W2, b2 = net[6].weight.detach(), net[6].bias.detach()
             if permute:
                 n = torch.arange(10 * C)
@@ -428,6 +429,7 @@ class EquiformerV2_nbody(nn.Module):
                 P[prefix + "b2"] = v(b2[perm])
                 return W2[perm]
             P[prefix + "w2"], P[prefix + "b2"] = v(W2), v(b2)
+            P[prefix + "w2_h2"], P[prefix + "w2_sinv"] = self._image_h2(W2.to(device))
             return None
 
         def attn(prefix, A):

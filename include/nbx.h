@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 17
+#define NBX_ABI_VERSION 18
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -828,6 +828,12 @@ typedef struct nbx_eqv2_radial {
     const void* w2_x3;                     /* net.6 image (attention radials, permuted), or NULL */
     const float* w2;                       /* net.6 [R][He] fp32 (edge-degree radial) */
     const float* b2;                       /* [R] */
+    /* optional (ABI 18): fp16x2 images (nbx_eqv2_attn "fp16x2 images", the lin_kernel block order) of
+     * net.3 -- with it the hidden layers run as one launch: the first layer formed in the GEMM's operand
+     * registers, net.3 on fp16x2 MFMA, LayerNorm + SiLU in its epilogue -- and, edge-degree radial only,
+     * of net.6 (the attention radials' net.6 image is nbx_eqv2_attn.w2_h2); with their 1 / s */
+    const void* w1_h2; const void* w2_h2;
+    float w1_sinv, w2_sinv;
 } nbx_eqv2_radial;
 
 typedef struct nbx_eqv2_attn {             /* SO2EquivariantGraphAttention */

@@ -1,5 +1,6 @@
 """EquiformerV2 product module on the CPU: reference-compatible state dict, seeded initialisation,
 constant buffers and the weight packing the C-ABI reads (no device call)."""
+import math
 import json
 import os
 import sys
@@ -106,10 +107,14 @@ def test_pack_weights_fills_every_pointer():
                               "ffn_hidden", "edge_channels", "num_layers", "num_elements", "h2_pad"):
                 yield path + name, v
     nulls = [k for k, v in walk(W) if not v]
-    # the attention radials use the bf16x3 image, the edge-degree radial the fp32 matrix
-    assert sorted(nulls) == ["edge_degree.w2_x3", "force.rad.w2"], nulls
+    # the attention radials use the bf16x3 / fp16x2 images of nbx_eqv2_attn, the edge-degree radial the fp32
+    # matrix and its own fp16x2 image (ABI 18)
+    assert sorted(nulls) == ["edge_degree.w2_x3", "force.rad.w2", "force.rad.w2_h2"], nulls
     for i in range(4):
-        assert [k for k, v in walk(W.blocks[i]) if not v] == ["ga.rad.w2"]
+        assert [k for k, v in walk(W.blocks[i]) if not v] == ["ga.rad.w2", "ga.rad.w2_h2"]
+    # the fp16x2 descale factors are powers of two
+    for s in (W.edge_degree.w1_sinv, W.edge_degree.w2_sinv, W.force.rad.w1_sinv, W.blocks[0].ga.rad.w1_sinv):
+        assert s > 0 and math.frexp(s)[0] == 0.5, s
 
 
 def test_unsupported_configuration_fails_loudly():
