@@ -1063,6 +1063,24 @@ def bench_eqv2_l6(a, rank, world, device, P):
         return tp
     tp, elapsed = timed_region(work, device, P)
     value = a.steps / elapsed * world
+    # roofline: every GEMM launch of one composed forward (a 2-frame rollout after the timed region),
+    # event-timed on the launch stream, as the training lines do
+    import nbody_amd.segnn_train as ST
+    ST.gemm_timer = []
+    model.rollout(loc_d, vel_d, mass_d, 2, seed=3)
+    torch.cuda.synchronize(device)
+    g_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ST.gemm_timer)
+    g_fl, n_g = sum(f for _, _, f in ST.gemm_timer), len(ST.gemm_timer)
+    ST.gemm_timer = None
+    ach = g_fl / (g_ms * 1e-3) / 1e12 if g_ms > 0 else None
+    roof = {"bound": "mfma", "kernel": "gemm_f32 / gemm_f32_batched / grouped (nbx_gemm_f32 family: every SO3_LinearV2, "
+                                       "SO(2) convolution and radial linear of the composed forward, each launch timed whole)",
+            "achieved": round(ach, 3) if ach else None, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None, "traffic": None,
+            "avg_launch_us": round(1e3 * g_ms / max(n_g, 1), 3), "launches_per_forward": n_g,
+            "gflop_per_forward": round(g_fl / 1e9, 4),
+            "gemm_share_of_step": round(g_ms * 1e-3 / (elapsed / a.steps), 4),
+            "timing": "torch.cuda.Event pairs around every GEMM launch of one forward, launch stream"}
     result = {
         "metric": "self-feed rollout steps/sec, EquiformerV2 lmax 6 / mmax 2 N=20 batch=64", "value": round(value, 3),
         "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -1073,7 +1091,7 @@ def bench_eqv2_l6(a, rank, world, device, P):
                                "(4 layers, sphere 64, attn hidden 64, 4 heads, ffn 64, edge 64), N=20, batch 64 per GPU, "
                                "composed native operators",
                    "model": "EquiformerV2", "global_batch": B * world, "seq_len": a.steps, "parallelism": f"dp{world}"},
-        "trajectory_steps_per_s": round(value * B, 1), "roofline": None,
+        "trajectory_steps_per_s": round(value * B, 1), "roofline": roof,
         "finite": bool(torch.isfinite(tp).all().item())}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_eqv2(model, B, B_s=8, cfg=cfg)
