@@ -230,7 +230,8 @@ def bench_segnn(a, rank, world, device, P):
 
     msg2 = (f"void nbx::tp_fused_kernel<3, 1, 1, 8, {2 if dv else 3}, {sk_name('6, 6, 3, 3, 0', int(dv))} >"
             "(nbx::TpProb)")
-    names = [f"void nbx::msg_pre_kernel<{prec}, {3 if prec else 0}>(nbx::MsgPreProb)",
+    # (msg_pre's third parameter: the NBX_MP_CHECK hand-off invariant build, 0 unless that switch is set)
+    names = [f"void nbx::msg_pre_kernel<{prec}, {3 if prec else 0}, {mp_check_level()}>(nbx::MsgPreProb)",
              msg2,
              f"void nbx::tp16_kernel<3, 1, 2, 1, 8, 3, 1, false, {sk_name('12, 12, 6, 6, 4', int(udv))} >(nbx::TpProb, "
              "nbx::TpProb, int)",
@@ -317,6 +318,12 @@ def newest_profile(fname):
     import glob
     c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", fname)), reverse=True)
     return c[0] if c else None
+
+
+def mp_check_level():
+    """msg_pre's CHK template argument (csrc/msg_pre.hip mp_check_word: NBX_MP_CHECK=1 check, 2 fault injection)."""
+    v = os.environ.get("NBX_MP_CHECK", "")
+    return int(v) if v in ("1", "2") else 0
 
 
 def rocprof_avg_us(kernel_name, model):
