@@ -1,5 +1,5 @@
-// EquiformerV2 N-body forward + device-resident self-feed rollout (fp32; GEMMs on the bf16x3
-// split-precision MFMA path of lin.h).
+// EquiformerV2 N-body forward + device-resident self-feed rollout (fp32; GEMMs on the fp16x2
+// split-precision MFMA path of lin.h, the bf16x3 images with NBX_EQ_SPLIT=x3).
 //
 // Reference (models/equiformer_v2/architecture/): equiformer_v2_nbody.py:428-575 (forward),
 // edge_rot_mat.py:6-63, so3.py:30-185 / 485-531 / 695-745, so2_ops.py:13-238,
@@ -16,7 +16,8 @@
 //   Z0/Z1  [E][3H] / [2E][2H]       separable-S2-activated message (so2_conv_2 input, m-primary)
 //   L      [E][nh]                  attention logits
 //   V0/V1  [E][ldv0] / [2E][ldv1]   so2_conv_2 outputs (values)
-// Per attention: radial MLP kernel -> radial GEMM with the message-building epilogue (LIN_EQMSG)
+// Per attention: radial MLP (one fp16x2 launch, eqv2_radial_h2_kernel) -> radial GEMM with the
+// message-building epilogue (LIN_EQMSG)
 // -> two SO(2) GEMMs -> S2 activation + alpha kernel -> two GEMMs -> per-system node kernel
 // (segment softmax over the N-1 incoming edges, inverse rotation, sum, projection, residual, norm,
 // the whole FFN and the next norm), so node features make one HBM round trip per block.

@@ -39,6 +39,7 @@ SWITCHES = [
     ({"NBX_ET_DEBUG": "1"}, ["egnn_grad"]),
     ({"NBX_EQ_NPW": "1"}, ["eqv2"]),
     ({"NBX_EQ_SPLIT": "x3"}, ["eqv2"]),
+    ({"NBX_EQ_RAD2": "1"}, ["eqv2"]),
     ({"NBX_EQ_NB": "4"}, ["eqv2"]),
     ({"NBX_EQV2_S2_NA0": "1"}, ["eqv2"]),
     ({"NBX_EQV2_SPECIALISED": "1"}, ["eqv2_grad"]),
