@@ -103,8 +103,7 @@ __global__ __launch_bounds__(MP_THREADS, PREC ? 1 : 2) void msg_pre_kernel(const
     // coefficient math waits for them only (vmcnt retires in issue order)
     const bool bn_on = P.xbn.sums != nullptr && t < 2 * M;
     const int bn_kind = t / M, bn_k = t % M;
-    BnPre bn_pre{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
-    if (bn_on) bn_pre = bn_pre_load(P.xbn, M, bn_kind, bn_k);
+    const BnPre bn_pre = bn_pre_load(P.xbn, M, bn_kind & 1, bn_on ? bn_k : 0, bn_on, P.X);
 
     // both weight images of this chunk -> LDS (DMA, verbatim)
     tp_dma_image<8>(P.Simg + (size_t)chunk * F, lds, F);

@@ -173,11 +173,32 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
     BnPre bn_pre[NEV];
 #pragma unroll
     for (int e = 0; e < NEV; ++e) {
-        bn_pre[e] = BnPre{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
         const int i = t + e * THREADS;
-        const int which = i < 2 * bn_M ? 0 : 1, kind = (i % (2 * bn_M)) / bn_M, k = i % bn_M;
-        if (SK::SEG > 0 && i < 4 * bn_M && (which == 0 ? bn_m : bn_x))
-            bn_pre[e] = bn_pre_load(which == 0 ? P.mbn : P.xbn, bn_M, kind, k);
+        const int which = i < 2 * bn_M ? 0 : 1, kind = (i % (2 * bn_M)) / bn_M, k = i < 4 * bn_M ? i % bn_M : 0;
+        const bool on = SK::SEG > 0 && i < 4 * bn_M && (which == 0 ? bn_m : bn_x);
+        bn_pre[e] = bn_pre_load(bn_src_sel(P.mbn, P.xbn, which == 1), bn_M, kind, k, on,
+                                SK::SEG > 0 ? (const void*)P.seg_base : (const void*)P.As);
+    }
+
+    // ---- segmented input: the per-(segment, k) coefficients the table takes from an earlier kernel
+    // (xcoef: the pending feature BN finalised by message_layer_1's block 0; mcoef: a finalised message
+    // BN), loaded here, before the image DMA, into registers (branch-free, a dummy address for table
+    // entries that need none): loaded after the DMA they cost one more memory round trip behind it
+    constexpr int NSEG_IT = SK::SEG > 0 ? (10 * 96 + THREADS - 1) / THREADS : 1;
+    float seg_raw[NSEG_IT];
+#pragma unroll
+    for (int j = 0; j < NSEG_IT; ++j) {
+        const int i = t + j * THREADS;
+        const int part = i / bn_M, k = i - part * bn_M;
+        const bool isx = part == 0 || part == 2 || part == 4 || part == 8;
+        const bool ism = SK::SEG == 4 && (part == 1 || part == 3 || part == 5 || part == 9);
+        const bool need = SK::SEG > 0 && i < 10 * bn_M &&
+                          ((isx && !bn_x && P.xcoef != nullptr) || (ism && !bn_m && P.mcoef != nullptr));
+        const int idx = (part == 0 || part == 1) ? k : (part == 4 || part == 5) ? 2 * bn_M + k : bn_M + k;
+        const float* src = need ? (isx ? P.xcoef : P.mcoef)
+                                : static_cast<const float*>(SK::SEG > 0 ? (const void*)P.seg_base : (const void*)P.As);
+        const float raw = src[need ? idx : 0];
+        seg_raw[j] = need ? raw : 0.f;
     }
 
     // ---- stage the CG chunk images of this group in LDS (LDS-DMA, verbatim copy; the image
@@ -213,20 +234,20 @@ __global__ __launch_bounds__(64 * WAVES, (SK::PREC || PF > 4) ? 1 : 2) void tp16
                 else { segtab[2 * M + bn_k] = c.x; segtab[8 * M + bn_k] = c.x; }
             }
         }
-        for (int i = t; i < 10 * M; i += THREADS) {
-            const int part = i / M, k = i - part * M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
-            float v;
+#pragma unroll
+        for (int j = 0; j < NSEG_IT; ++j) {
+            const int i = t + j * THREADS;
+            if (i >= 10 * M) continue;
+            const int part = i / M;   // part 0-3 scales, 4-7 shifts, 8-9 vector scales
             if (mfin && (part == 1 || part == 3 || part == 5 || part == 9)) continue;
             if (xfin && (part == 0 || part == 2 || part == 4 || part == 8)) continue;
+            const float raw = seg_raw[j];   // xcoef / mcoef entry of this part (preloaded)
+            float v;
             switch (part) {
-                case 0: v = P.xcoef ? P.xcoef[k] : 1.f; break;
-                case 1: v = SK::SEG == 4 ? P.mcoef[k] : 0.f; break;
-                case 2: v = P.xcoef ? P.xcoef[M + k] : 1.f; break;
-                case 3: v = SK::SEG == 4 ? P.mcoef[M + k] : 0.f; break;
-                case 4: v = P.xcoef ? P.xcoef[2 * M + k] : 0.f; break;
-                case 5: v = SK::SEG == 4 ? P.deg * P.mcoef[2 * M + k] : 0.f; break;
-                case 8: v = P.xcoef ? P.xcoef[M + k] : 1.f; break;
-                case 9: v = SK::SEG == 4 ? P.mcoef[M + k] : 0.f; break;
+                case 0: case 2: case 8: v = P.xcoef ? raw : 1.f; break;
+                case 4: v = P.xcoef ? raw : 0.f; break;
+                case 1: case 3: case 9: v = SK::SEG == 4 ? raw : 0.f; break;
+                case 5: v = SK::SEG == 4 ? P.deg * raw : 0.f; break;
                 default: v = 0.f;
             }
             segtab[i] = v;

@@ -94,16 +94,49 @@ struct BnPre {
     double s0, s1;
     float w, b, rm, rv;
 };
-__device__ inline BnPre bn_pre_load(const BnSrc& b, int M, int kind, int k) {
-    BnPre p{0.0, 0.0, 0.f, 0.f, 0.f, 0.f};
-    if (kind == 0) {
-        if (b.training) { p.s0 = b.sums[k]; p.s1 = b.sums[M + k]; }
-        p.rm = b.rmean[k]; p.rv = b.rvar[k]; p.w = b.weight[k]; p.b = b.bias[k];
-    } else {
-        if (b.training) p.s0 = b.sums[2 * M + k];
-        p.rv = b.rvar[M + k]; p.w = b.weight[M + k];
-    }
+// The inputs of one coefficient evaluation (kind 0: 0e mean / variance, kind 1: 1o norm; `on`: this
+// thread evaluates one).  Branch-free: every thread issues the same six loads -- an unused slot reads
+// `dummy`, any readable address with 3 M doubles behind it -- into registers of their own and selects
+// afterwards.  Loads under a divergent branch made the waitcnt pass drain every load in flight, the A
+// ring's first chunks included, before the weight-image DMA was issued: one memory latency added to
+// the staging of update_layer_1, pre_pool1 and msg_pre.
+__device__ inline BnPre bn_pre_load(const BnSrc& b, int M, int kind, int k, bool on, const void* dummy) {
+    const double* dd = static_cast<const double*>(dummy);
+    const float* df = static_cast<const float*>(dummy);
+    const bool tr = on && b.training && b.sums;
+    const bool k0 = kind == 0;
+    const double* sums = tr ? b.sums : dd;
+    const float* rmean = on && b.rmean ? b.rmean : df;
+    const float* rvar = on && b.rvar ? b.rvar : df;
+    const float* weight = on && b.weight ? b.weight : df;
+    const float* bias = on && b.bias ? b.bias : df;
+    const int iv = k0 ? k : M + k;
+    const double s0 = sums[k0 ? k : 2 * M + k], s1 = sums[M + k];
+    const float rm = rmean[k], rv = rvar[iv], w = weight[iv], bb = bias[k];
+    BnPre p;
+    p.s0 = tr ? s0 : 0.0;
+    p.s1 = tr && k0 ? s1 : 0.0;
+    p.rm = on && k0 ? rm : 0.f;
+    p.rv = on ? rv : 0.f;
+    p.w = on ? w : 0.f;
+    p.b = on && k0 ? bb : 0.f;
     return p;
+}
+// one of two sources, selected per lane field by field (no pointer to either struct is formed)
+__device__ inline BnSrc bn_src_sel(const BnSrc& a, const BnSrc& b, bool use_b) {
+    BnSrc s;
+    s.sums = use_b ? b.sums : a.sums;
+    s.weight = use_b ? b.weight : a.weight;
+    s.bias = use_b ? b.bias : a.bias;
+    s.rmean = use_b ? b.rmean : a.rmean;
+    s.rvar = use_b ? b.rvar : a.rvar;
+    s.coef_out = use_b ? b.coef_out : a.coef_out;
+    s.count = use_b ? b.count : a.count;
+    s.eps = use_b ? b.eps : a.eps;
+    s.momentum = use_b ? b.momentum : a.momentum;
+    s.training = use_b ? b.training : a.training;
+    s.update = use_b ? b.update : a.update;
+    return s;
 }
 __device__ inline float2 bn_pre_coef(const BnSrc& b, const BnPre& p, int M, int kind, int k, bool owner) {
     if (kind == 1) {
