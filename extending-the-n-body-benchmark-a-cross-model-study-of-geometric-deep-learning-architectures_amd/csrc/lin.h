@@ -317,7 +317,9 @@ __global__ __launch_bounds__(LIN_THREADS, 2) void lin_kernel(const LinProb P) {
             float bb[5];
 #pragma unroll
             for (int j = 0; j < 5; ++j) bb[j] = P.bias[n0 + 32 * j + r];
-#pragma unroll 2
+            // fully unrolled: every row's gathers (9 x values, 24 rotation entries) can be in flight together
+            // (unroll 2 / 4 / 16: 154 / 148 / 137 us per launch at C4, profiles/r06/eqmsg_unroll)
+#pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int row = rt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 if (row >= P.rows) continue;
