@@ -17,6 +17,7 @@
 #include <cstring>
 
 #include "nbx_internal.h"
+#include "tp_fused.h"   // bf16x3 split helpers (tp_split3, SplitP, mfma32x32)
 
 namespace {
 
@@ -269,7 +270,144 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ part, int splits, i
     *p = beta != 0.f ? s + beta * *p : s;
 }
 
+// ---------------------------------------------------------------- GEMM on the bf16x3 split MFMA
+// The large C = A B^T products (NBX_GEMM_TRANS_B on plain rows, one K split: EquiformerV2 lmax 6's
+// SO(2) convolutions, 24 320 edge rows, K 448..1536).  Each fp32 operand fragment is split into three
+// bf16 parts as it leaves the LDS (tp_fused.h tp_split3: x = hi + mid + lo within 2^-27 |x|) and a
+// product is the fp32 sum of the six leading cross terms on v_mfma_f32_32x32x16_bf16 (SplitP<1>,
+// smallest first): fp32-level accuracy at up to 2.7x the fp32 MFMA rate (12 x 32 cycles per
+// 32 x 32 x 32 step against 16 x 64).  Tile 128 x 128, K step 32, four waves of 64 x 64 (2 x 2 MFMA
+// tiles, 24 MFMAs per 16-deep step against 8 fragment splits); both operands are K-contiguous, so the
+// LDS holds fp32 rows [row][X3P] (144-byte pitch: a lane's 8 consecutive k are two conflict-free
+// ds_read_b128), one buffer, 36 KB.  The 128-wide tile halves the operand re-reads of a 64-wide one,
+// which bound it (profiles/r06/gemm_x3/: SO(2) conv 1 group 1 328 us fp32, 1 092 us at 64 x 64, 868 us
+// here; splitting once while staging into [part][row] bf16 rows needed 60 KB and ran 1 781 us).
+// NBX_GEMM_X3=0 keeps every problem on the fp32 kernel (A/B).
+constexpr int X3P = GK + 4;
+constexpr int X3T = 128;   // block tile X3T x X3T, four waves of 64 x 64 (2 x 2 MFMA tiles each)
+
+__device__ __forceinline__ void gemm_x3_tile(const GemmArgs& g, int bx, int by, float (&As)[X3T][X3P],
+                                             float (&Bs)[X3T][X3P]) {
+    using SP = nbx::SplitP<1>;
+    constexpr int S = X3T / 64, L = X3T / 32;   // MFMA tiles per wave and dimension; float4s per operand
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t m0 = (int64_t)by * X3T, n0 = (int64_t)bx * X3T;
+    const int wm = (wave & 1) * (X3T / 2), wn = (wave >> 1) * (X3T / 2);
+    const int r = t >> 3, k4 = (t & 7) * 4;   // this thread stages rows r + 32 h, k4 .. k4 + 3
+    float4 a[L], b[L];
+    auto ld4 = [&](const float* base, int64_t ld, int64_t row, int64_t rmax, int64_t k, float4& v) {
+        if (row < rmax && k + 3 < g.K) {
+            v = *reinterpret_cast<const float4*>(base + row * ld + k);
+        } else {
+            float e[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[j] = (row < rmax && k + j < g.K) ? base[row * ld + k + j] : 0.f;
+            v = make_float4(e[0], e[1], e[2], e[3]);
+        }
+    };
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int h = 0; h < L; ++h) {
+            ld4(g.A, g.lda, m0 + r + 32 * h, g.M, k0 + k4, a[h]);
+            ld4(g.B, g.ldb, n0 + r + 32 * h, g.N, k0 + k4, b[h]);
+        }
+    };
+    floatx16 acc[S][S];
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    const int64_t nk = (g.K + GK - 1) / GK;
+    if (nk > 0) load(0);
+    // one LDS buffer: stage K step it, barrier, request step it + 1, multiply, barrier.  (Two steps in
+    // flight: 236 VGPRs under launch bounds (256, 2) and 1.33x slower; profiles/r06/gemm_x3/.)
+    for (int64_t it = 0; it < nk; ++it) {
+#pragma unroll
+        for (int h = 0; h < L; ++h) {
+            *reinterpret_cast<float4*>(&As[r + 32 * h][k4]) = a[h];
+            *reinterpret_cast<float4*>(&Bs[r + 32 * h][k4]) = b[h];
+        }
+        __syncthreads();
+        if (it + 1 < nk) load((it + 1) * GK);
+#pragma unroll
+        for (int kk = 0; kk < GK; kk += 16) {
+            const int kr = kk + 8 * (lane >> 5);
+            nbx::bf16x8 fa[S][3], fb[S][3];
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                const float* pa = &As[wm + 32 * i + (lane & 31)][kr];
+                const float* pb = &Bs[wn + 32 * i + (lane & 31)][kr];
+                nbx::tp_split3(*reinterpret_cast<const float4*>(pa), *reinterpret_cast<const float4*>(pa + 4),
+                               fa[i][0], fa[i][1], fa[i][2]);
+                nbx::tp_split3(*reinterpret_cast<const float4*>(pb), *reinterpret_cast<const float4*>(pb + 4),
+                               fb[i][0], fb[i][1], fb[i][2]);
+            }
+#pragma unroll
+            for (int u = 0; u < SP::NT; ++u)
+#pragma unroll
+                for (int i = 0; i < S; ++i)
+#pragma unroll
+                    for (int j = 0; j < S; ++j) acc[i][j] = nbx::mfma32x32(fa[i][SP::TA[u]], fb[j][SP::TB[u]], acc[i][j]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const int64_t col = n0 + wn + 32 * j + (lane & 31);
+        if (col >= g.N) continue;
+        const float bias = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t row = m0 + wm + 32 * i + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+                if (row >= g.M) continue;
+                float* p = g.C + row * g.ldc + col;
+                const float v = g.bias ? acc[i][j][e] + bias : acc[i][j][e];
+                *p = g.beta != 0.f ? v + g.beta * *p : v;
+            }
+    }
+}
+
+// the problems of a GemmBatch that are all bf16x3-eligible (gemm_x3_ok; tx / ty count X3T tiles); the
+// row blocks of each problem are dealt to the XCDs in groups (block l runs on XCD l % 8 under
+// round-robin dispatch): XCD x owns row blocks x, x + 8, ... and walks each one's column tiles, so its
+// L2 fetches those A rows once
+__global__ __launch_bounds__(256) void gemm_x3_batched_kernel(GemmBatch b) {
+    __shared__ float As[X3T][X3P];
+    __shared__ float Bs[X3T][X3P];
+    const int blk = (int)blockIdx.x;
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < GMAXP; ++i)
+        if (i < b.count && blk >= b.first[i]) p = i;
+    const int l = blk - b.first[p], tx = b.tx[p], ty = b.ty[p];
+    const int full = (ty / 8) * 8 * tx;   // blocks of the complete 8-row-block groups
+    int by, bx;
+    if (l < full) {
+        const int x = l % 8, j = l / 8;
+        by = (j / tx) * 8 + x;
+        bx = j % tx;
+    } else {
+        by = (ty / 8) * 8 + (l - full) / tx;
+        bx = (l - full) % tx;
+    }
+    gemm_x3_tile(b.g[p], bx, by, As, Bs);
+}
+
 int64_t gemm_tiles(int64_t M, int64_t N, int T) { return ((M + T - 1) / T) * ((N + T - 1) / T); }
+
+// bf16x3 kernel eligibility: C = A B^T on plain rows, float4-aligned operands, one K split, and large
+// enough for the MFMA rate to matter (K >= 256, >= 2^30 multiply-adds; no training-step GEMM qualifies),
+// and at least 96 columns (a 64-column problem would leave half of each 128-wide tile idle: the radial
+// output layer 24 320 x 64 x 1152 ran 69 -> 91 us)
+bool gemm_x3_ok(int32_t flags, const GemmArgs& g, int splits, bool vec) {
+    static const bool on = !(getenv("NBX_GEMM_X3") && getenv("NBX_GEMM_X3")[0] == '0');
+    return on && flags == NBX_GEMM_TRANS_B && splits == 1 && vec && g.rdiv == 1 && !g.oa && !g.ob && !g.oc &&
+           !g.ones && !g.tail && g.K >= 256 && g.N >= 96 && (double)g.M * g.N * g.K >= 1073741824.0;
+}
 
 int gemm_splits(int64_t M, int64_t N, int64_t K, int T) {
     const int64_t tiles = gemm_tiles(M, N, T);
@@ -765,6 +903,19 @@ extern "C" int nbx_gemm_f32(int32_t flags, int64_t M, int64_t N, int64_t K, cons
     const dim3 grid((unsigned)((N + T - 1) / T), (unsigned)((M + T - 1) / T), (unsigned)splits);
     hipStream_t st = (hipStream_t)stream;
     const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+    if (gemm_x3_ok(flags, g, splits, vec)) {
+        GemmBatch gb;
+        memset(&gb, 0, sizeof(gb));
+        gb.g[0] = g;
+        gb.tx[0] = (int)((N + X3T - 1) / X3T);
+        gb.ty[0] = (int)((M + X3T - 1) / X3T);
+        gb.nz[0] = 1;
+        gb.first[1] = gb.tx[0] * gb.ty[0];
+        gb.count = 1;
+        hipLaunchKernelGGL(gemm_x3_batched_kernel, dim3((unsigned)gb.first[1]), dim3(256), 0, st, gb);
+        NBX_LAUNCH_CHECK("gemm_x3");
+        return NBX_OK;
+    }
     auto launch = [&](auto tile) {
         constexpr int TT = decltype(tile)::value;
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(GemmCfg<TT>::THREADS), 0, st, g); };
@@ -828,6 +979,7 @@ int gemm_group(const char* name, int32_t count, const int32_t* flags, const int6
     ReduceBatch rb;
     memset(&rb, 0, sizeof(rb));
     int blocks = 0, nred = 0;
+    bool x3 = true;   // every problem on the bf16x3 kernel
     size_t ws_off = 0;
     constexpr int T = GB;
     for (int i = 0; i < count; ++i) {
@@ -868,6 +1020,7 @@ int gemm_group(const char* name, int32_t count, const int32_t* flags, const int6
         const bool vec = ((uintptr_t)A[i] % 16 == 0) && ((uintptr_t)B[i] % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0 &&
                          d.oa % 4 == 0 && d.ob % 4 == 0;
         gb.g[i] = g;
+        x3 = x3 && gemm_x3_ok(flags[i], g, splits, vec);
         gb.mode[i] = (ta ? 1 : 0) | (tb ? 2 : 0) | (vec ? 4 : 0);
         gb.tx[i] = (int)((N + T - 1) / T);
         gb.ty[i] = (int)((M + T - 1) / T);
@@ -879,6 +1032,19 @@ int gemm_group(const char* name, int32_t count, const int32_t* flags, const int6
     gb.count = count;
     rb.count = nred;
     hipStream_t st = (hipStream_t)stream;
+    if (x3) {   // (x3 implies no split problem: nred == 0); the grid in X3T x X3T tiles
+        int xb = 0;
+        for (int i = 0; i < count; ++i) {
+            gb.tx[i] = (int)((gb.g[i].N + X3T - 1) / X3T);
+            gb.ty[i] = (int)((gb.g[i].M + X3T - 1) / X3T);
+            gb.first[i] = xb;
+            xb += gb.tx[i] * gb.ty[i];
+            gb.first[i + 1] = xb;
+        }
+        hipLaunchKernelGGL(gemm_x3_batched_kernel, dim3((unsigned)xb), dim3(256), 0, st, gb);
+        NBX_LAUNCH_CHECK("gemm_x3_batched");
+        return NBX_OK;
+    }
     if (count == 1) {   // one problem: the storage-order-specialised kernel (fewer registers than the grouped one)
         const dim3 grid((unsigned)gb.tx[0], (unsigned)gb.ty[0], (unsigned)gb.nz[0]), blk(GemmCfg<GB>::THREADS);
         const GemmArgs& g = gb.g[0];

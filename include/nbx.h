@@ -324,7 +324,11 @@ int nbx_debug_msg_pre_check(uint32_t* mismatches, int32_t reset);
 /* C = op(A) op(B) (+ C if beta = 1), C [M][N] (ldc); op(A) [M][K]: A stored [M][K] (lda) or, with
  * NBX_GEMM_TRANS_A, [K][M]; op(B) [K][N]: B stored [K][N] (ldb) or, with NBX_GEMM_TRANS_B, [N][K].
  * fp32 MFMA (v_mfma_f32_32x32x2_f32), 64 x 64 tiles; small-M N, long-K products (weight gradients)
- * split K over the workspace (nbx_gemm_f32_workspace_bytes) and sum the splits in order. */
+ * split K over the workspace (nbx_gemm_f32_workspace_bytes) and sum the splits in order.  Large
+ * C = A B^T products (flags exactly NBX_GEMM_TRANS_B, plain rows, no K split, K >= 256, N >= 96, >= 2^30
+ * multiply-adds, 16-byte aligned operands; in a batched / grouped launch: when every problem qualifies)
+ * run on the bf16x3 split MFMA since r06: six bf16 products per fp32 product, fp32 accumulation,
+ * fp32-level accuracy but not bitwise the fp32-MFMA result; NBX_GEMM_X3=0 keeps them on fp32 MFMA. */
 #define NBX_GEMM_TRANS_A 1
 #define NBX_GEMM_TRANS_B 2
 /* op(B) gains a last column of ones (n = N - 1 reads 1, not memory; B holds N - 1 columns): C's last

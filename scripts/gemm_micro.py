@@ -23,12 +23,17 @@ GROUPS = {
                     (1, 64, 64, 1600), (5, 64, 1, 320)],
     "segnn_bwd": [(13, 288, 387, 1280), (1, 96, 192, 3840), (0, 1280, 386, 288), (0, 3840, 192, 96)],
     "segnn_fwd": [(2, 1280, 288, 386), (2, 3840, 96, 192)],
+    # EquiformerV2 lmax 6 forward (N = 20, B = 64: 24 320 edges): SO(2) conv 1 / conv 2, radial output
+    "l6_conv1": [(2, 24320, 96, 896), (2, 24320, 448, 896), (2, 24320, 768, 1536), (2, 24320, 640, 1280)],
+    "l6_conv2": [(2, 24320, 112, 448), (2, 24320, 192, 768), (2, 24320, 160, 640)],
+    "l6_rad1152": [(2, 24320, 64, 1152)],
 }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--only", help="comma-separated group names")
     ap.add_argument("--check", action="store_true", help="compare each problem with torch fp64")
     ap.add_argument("--dump", help="save every C to this .npz (bit-identity checks between builds / modes)")
     a = ap.parse_args()
@@ -39,6 +44,8 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     dump = {}
     for name, probs in GROUPS.items():
+        if a.only and name not in a.only.split(","):
+            continue
         ps, ref = [], []
         for fl, M, N, K in probs:
             ta, tb, ones, tail = fl & 1, fl & 2, fl & 4, fl & 8

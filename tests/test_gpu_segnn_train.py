@@ -116,6 +116,34 @@ def test_gemm_f32_grouped_bias_and_two_level_rows(hip_device, M, N, K):
         assert (Y[:, 0] == 7.0).all() and (Y[:, 4] == 7.0).all()
 
 
+@pytest.mark.parametrize("M,N,K,beta", [(8190, 160, 1000, 0.0), (8192, 128, 1024, 1.0), (4100, 452, 900, 0.0)])
+def test_gemm_x3_large_products_match_fp64(hip_device, M, N, K, beta):
+    """The bf16x3 kernel (gemm_x3_ok: C = A B^T on plain rows, >= 2^30 multiply-adds, K >= 256, N >= 96;
+    tails in M, N and K) against fp64 torch at the fp32 kernels' bound, with the epilogue bias; one
+    problem through nbx_gemm_f32 and the same problem in a two-problem nbx_gemm_f32_grouped launch agree
+    bit for bit."""
+    from nbody_amd.segnn_train import _at
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    W = torch.randn(N, K, generator=g, dtype=torch.float64)
+    b = torch.randn(N, generator=g, dtype=torch.float64)
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    d = lambda x: x.to(device=hip_device, dtype=torch.float32).contiguous()
+    Ad, Wd, bd = d(A), d(W), d(b)
+    bound = 2e-6 * (A.abs() @ W.abs().t()).max().item() + 1e-6
+    C = d(C0)
+    T.gemm(_lib.GEMM_TRANS_B, M, N, K, Ad, K, Wd, K, C, N, beta)
+    ref = A @ W.t() + beta * C0
+    assert (C.double().cpu() - ref).abs().max().item() <= bound
+    Cg, C2 = d(C0), torch.empty(M, N, device=hip_device)
+    T.gemm_grouped([(_lib.GEMM_TRANS_B, M, N, K, _at(Ad, 0), K, _at(Wd, 0), K, _at(Cg, 0), N, beta, 1, 0, 0, 0),
+                    (_lib.GEMM_TRANS_B, M, N, K, _at(Ad, 0), K, _at(Wd, 0), K, _at(C2, 0), N, 0.0, 1, 0, 0, 0,
+                     _at(bd, 0))], hip_device)
+    torch.cuda.synchronize()
+    assert torch.equal(Cg, C)
+    assert (C2.double().cpu() - (A @ W.t() + b)).abs().max().item() <= bound
+
+
 def test_gemm_f32_batched_equals_single(hip_device):
     """nbx_gemm_f32_batched (up to 4 GEMMs in one launch + one split-K sum launch) is bit-identical to
     nbx_gemm_f32 on each problem: mixed storage orders, split and unsplit shapes, beta 0 and 1."""

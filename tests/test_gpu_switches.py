@@ -43,10 +43,11 @@ SWITCHES = [
     ({"NBX_EQ_NB": "4"}, ["eqv2"]),
     ({"NBX_EQV2_S2_NA0": "1"}, ["eqv2"]),
     ({"NBX_EQV2_SPECIALISED": "1"}, ["eqv2_grad"]),
+    ({"NBX_GEMM_X3": "0"}, ["eqv2_l6"]),
     ({"NBX_GRAV_OCC": "1"}, ["gravity"]),
     ({"NBX_TP_DEBUG": "1"}, ["segnn"]),
 ]
-FAMILIES = ["ponita", "egnn", "egnn_grad", "eqv2", "eqv2_grad", "gravity", "segnn"]
+FAMILIES = ["ponita", "egnn", "egnn_grad", "eqv2", "eqv2_l6", "eqv2_grad", "gravity", "segnn"]
 
 
 class _Graph:
@@ -105,6 +106,19 @@ def _eqv2(torch, dev):
     return {"out": TQ.run(TQ.make_model("c4", dev), loc, vel, mass, gauge, dev)}
 
 
+def _eqv2_l6(torch, dev):
+    """The lmax 6 / mmax 2 bench model (bench.py eqv2_l6) at B = 64, N = 20: its SO(2) convolution
+    GEMMs (24 320 edge rows) run on the bf16x3 kernel by default, on fp32 MFMA under NBX_GEMM_X3=0."""
+    import bench
+    from nbody_amd.equiformer_v2 import EquiformerV2_nbody
+    torch.manual_seed(0)
+    m = EquiformerV2_nbody(**dict(bench.EQV2_C4, lmax_list=[6], mmax_list=[2])).to(dev).eval()
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
+    loc, vel, mass = bench.initial_states(64, 20, 0)
+    tp, tv = m.rollout(t(loc), t(vel), t(mass), 3, seed=1)
+    return {"pos": tp.double().cpu().numpy(), "vel": tv.double().cpu().numpy()}
+
+
 def _eqv2_grad(torch, dev):
     import test_gpu_eqv2_train as TT
     m = TT._model(TT.SMALL, dev)
@@ -137,8 +151,8 @@ def _child(env, fams, q):
     try:
         import torch
         dev = torch.device("cuda:0")
-        fn = {"ponita": _ponita, "egnn": _egnn, "egnn_grad": _egnn_grad, "eqv2": _eqv2, "eqv2_grad": _eqv2_grad,
-              "gravity": _gravity, "segnn": _segnn}
+        fn = {"ponita": _ponita, "egnn": _egnn, "egnn_grad": _egnn_grad, "eqv2": _eqv2, "eqv2_l6": _eqv2_l6,
+              "eqv2_grad": _eqv2_grad, "gravity": _gravity, "segnn": _segnn}
         q.put({f: fn[f](torch, dev) for f in fams})
     except Exception as e:  # surfaced by the parent
         import traceback
@@ -167,7 +181,7 @@ def _compare(fam, got, ref, exact):
         assert g.shape == r.shape, (fam, k)
         if exact:
             np.testing.assert_array_equal(g, r, err_msg=f"{fam} {k}")
-        elif fam == "eqv2":
+        elif fam in ("eqv2", "eqv2_l6"):
             err = np.abs(g - r)
             assert (err <= 2e-5 + 2e-5 * np.abs(r)).all(), (fam, k, err.max())
         elif k.startswith("g/"):
