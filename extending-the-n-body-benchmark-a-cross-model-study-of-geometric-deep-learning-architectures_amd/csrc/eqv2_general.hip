@@ -125,14 +125,17 @@ __device__ __forceinline__ float inv_rescale(int l, int mmax) {
 // MODE 0 (rotate):     out [E][R][C]          = D_sel in (x rescale), in [E][(lmax+1)^2][C] (ld_in per edge)
 // MODE 1 (rotate_inv): out [E][(lmax+1)^2][C] = D_sel^T in (x rescale), in [E][R][C] (ld_in per edge)
 // order (nullable): the edge-side row of kept coefficient k (l-primary) is order[k] -- e.g. the
-// m-primary order of SO2_Convolution, so the SO(2) blocks read contiguous rows without a permutation
-template <int MODE>
+// m-primary order of SO2_Convolution, so the SO(2) blocks read contiguous rows without a permutation.
+// UNI (C a multiple of 64): a wave's lanes share one edge, made explicit with readfirstlane, so the
+// edge's Wigner block and the row order are read once per wave through the scalar cache instead of
+// once per lane (455 per-lane loads per output channel at lmax 6 / mmax 2)
+template <int MODE, bool UNI>
 __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax, int S, int R,
                                            const float* __restrict__ D, const float* __restrict__ in, int64_t ld_in,
                                            float* __restrict__ out, int rescale, const int* __restrict__ order) {
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (t >= E * C) return;
-    const int64_t e = t / C;
+    const int64_t e = UNI ? (int64_t)__builtin_amdgcn_readfirstlane((int)(t / C)) : t / C;
     const int c = (int)(t - e * C);
     const float* d = D + e * S;
     const float* x = in + e * ld_in + c;
@@ -320,12 +323,14 @@ extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32
     NBX_CHECK_ARG(dsel && in && out, "nbx_eqv2_rotate_general: null operand");
     hipStream_t st = (hipStream_t)stream;
     const int S = dsel_floats(lmax, mmax);
-    if (inverse)
-        hipLaunchKernelGGL(eqv2_rotate_general_kernel<1>, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R,
-                           dsel, in, ld_in, out, rescale, order);
-    else
-        hipLaunchKernelGGL(eqv2_rotate_general_kernel<0>, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R,
-                           dsel, in, ld_in, out, rescale, order);
+    NBX_CHECK_ARG(E * C < ((int64_t)1 << 31), "nbx_eqv2_rotate_general: E C >= 2^31");
+    const bool uni = C % 64 == 0;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R, dsel, in, ld_in, out,
+                           rescale, order);
+    };
+    if (inverse) uni ? go(eqv2_rotate_general_kernel<1, true>) : go(eqv2_rotate_general_kernel<1, false>);
+    else uni ? go(eqv2_rotate_general_kernel<0, true>) : go(eqv2_rotate_general_kernel<0, false>);
     NBX_LAUNCH_CHECK("eqv2_rotate_general");
     return NBX_OK;
 }
