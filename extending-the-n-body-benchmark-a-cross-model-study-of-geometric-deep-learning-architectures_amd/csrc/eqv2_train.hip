@@ -77,8 +77,8 @@ constexpr int S2_MAXI = 49, S2_MAXP = 240;   // LDS: 2 x 240 x 52 floats = 99.8 
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-template <int MAXI, bool BWD>
-__global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P, int H, const float* __restrict__ T,
+template <int MAXI, bool BWD, int NT>
+__global__ __launch_bounds__(NT) void eqv2_s2_kernel(int64_t rows, int I, int P, int H, const float* __restrict__ T,
                                                       const float* __restrict__ F, const float* __restrict__ X,
                                                       const float* __restrict__ dOut, float* __restrict__ out) {
     // T / F rows padded to a multiple of 4 coefficients with zeros and read as float4: the lanes of a
@@ -110,13 +110,17 @@ __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P
     for (int p = 0; p < P; ++p) {
         const float4* tp = sT + p * I4;
         const float4* fp = sF + p * I4;
-        float t = 0.f;
+        // four independent chains (one per float4 component): a single chain of I dependent FMAs per
+        // grid point was latency bound at the one or two waves per SIMD the LDS footprint allows
+        float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
 #pragma unroll
         for (int q = 0; q < M4; ++q)
             if (q < I4) {
                 const float4 v = tp[q];
-                t += v.x * x[4 * q] + v.y * x[4 * q + 1] + v.z * x[4 * q + 2] + v.w * x[4 * q + 3];
+                t0 = fmaf(v.x, x[4 * q], t0); t1 = fmaf(v.y, x[4 * q + 1], t1);
+                t2 = fmaf(v.z, x[4 * q + 2], t2); t3 = fmaf(v.w, x[4 * q + 3], t3);
             }
+        const float t = (t0 + t1) + (t2 + t3);
         const float s = sigm(t);
         if (!BWD) {
             const float a = t * s;
@@ -127,13 +131,15 @@ __global__ __launch_bounds__(256) void eqv2_s2_kernel(int64_t rows, int I, int P
                     o[4 * q] += v.x * a; o[4 * q + 1] += v.y * a; o[4 * q + 2] += v.z * a; o[4 * q + 3] += v.w * a;
                 }
         } else {
-            float gsum = 0.f;
+            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
 #pragma unroll
             for (int q = 0; q < M4; ++q)
                 if (q < I4) {
                     const float4 v = fp[q];
-                    gsum += v.x * d[4 * q] + v.y * d[4 * q + 1] + v.z * d[4 * q + 2] + v.w * d[4 * q + 3];
+                    g0 = fmaf(v.x, d[4 * q], g0); g1 = fmaf(v.y, d[4 * q + 1], g1);
+                    g2 = fmaf(v.z, d[4 * q + 2], g2); g3 = fmaf(v.w, d[4 * q + 3], g3);
                 }
+            const float gsum = (g0 + g1) + (g2 + g3);
             const float dt = gsum * (s + t * s * (1.0f - s));
 #pragma unroll
             for (int q = 0; q < M4; ++q)
@@ -153,9 +159,14 @@ int s2_launch(int64_t rows, int I, int P, int H, const float* T, const float* F,
               float* out, hipStream_t st) {
     const size_t lds = 2 * (size_t)P * ((I + 3) / 4 * 4) * sizeof(float);
     const int which = I <= 9 ? 0 : I <= 32 ? 1 : 2;
-    auto kern = which == 0 ? eqv2_s2_kernel<9, BWD> : which == 1 ? eqv2_s2_kernel<32, BWD> : eqv2_s2_kernel<S2_MAXI, BWD>;
+    // one copy of the grid matrices per block: the large-I forms take 512 / 1024 threads, so the LDS
+    // that limits a CU to one or two blocks still holds 2 / 4 waves per SIMD (VGPRs allow it up to I 49 /
+    // 32); the lmax 2 form keeps 256
+    const int nt = which == 0 ? 256 : which == 1 ? 1024 : 512;
+    auto kern = which == 0 ? eqv2_s2_kernel<9, BWD, 256>
+              : which == 1 ? eqv2_s2_kernel<32, BWD, 1024> : eqv2_s2_kernel<S2_MAXI, BWD, 512>;
     if (lds > 64 * 1024) NBX_LDS_160K(kern);
-    hipLaunchKernelGGL(kern, dim3(nblk(rows * H)), dim3(256), lds, st, rows, I, P, H, T, F, X, dOut, out);
+    hipLaunchKernelGGL(kern, dim3(nblk(rows * H, nt)), dim3(nt), lds, st, rows, I, P, H, T, F, X, dOut, out);
     return NBX_OK;
 }
 
