@@ -1089,7 +1089,7 @@ def bench_eqv2_l6(a, rank, world, device, P):
             "gemm_share_of_step": round(g_ms * 1e-3 / (elapsed / a.steps), 4),
             "mfma_path": "fp32 MFMA (NBX_GEMM_X3=0)" if os.environ.get("NBX_GEMM_X3", "1")[:1] == "0" else
                          "bf16x3 split MFMA (six bf16 products per fp32 product, fp32 accumulate) for the SO(2) "
-                         "convolutions' grouped GEMMs (gemm_x3_ok: >= 2^30 multiply-adds, K >= 256, N >= 96), fp32 "
+                         "convolutions' grouped GEMMs (gemm_x3_ok: >= 2^30 multiply-adds, K >= 64, N >= 96), fp32 "
                          "MFMA for the rest; achieved counts fp32-equivalent flops",
             "timing": "torch.cuda.Event pairs around every GEMM launch of one forward, launch stream"}
     result = {

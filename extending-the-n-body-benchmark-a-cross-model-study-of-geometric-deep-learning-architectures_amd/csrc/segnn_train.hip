@@ -400,13 +400,14 @@ __global__ __launch_bounds__(256) void gemm_x3_batched_kernel(GemmBatch b) {
 int64_t gemm_tiles(int64_t M, int64_t N, int T) { return ((M + T - 1) / T) * ((N + T - 1) / T); }
 
 // bf16x3 kernel eligibility: C = A B^T on plain rows, float4-aligned operands, one K split, and large
-// enough for the MFMA rate to matter (K >= 256, >= 2^30 multiply-adds; no training-step GEMM qualifies),
+// enough for the MFMA rate to matter (K >= 64, >= 2^30 multiply-adds; no training-step GEMM qualifies;
+// the radial layer 24 320 x 2 304 x 64 143 -> 126 us),
 // and at least 96 columns (a 64-column problem would leave half of each 128-wide tile idle: the radial
 // output layer 24 320 x 64 x 1152 ran 69 -> 91 us)
 bool gemm_x3_ok(int32_t flags, const GemmArgs& g, int splits, bool vec) {
     static const bool on = !(getenv("NBX_GEMM_X3") && getenv("NBX_GEMM_X3")[0] == '0');
     return on && flags == NBX_GEMM_TRANS_B && splits == 1 && vec && g.rdiv == 1 && !g.oa && !g.ob && !g.oc &&
-           !g.ones && !g.tail && g.K >= 256 && g.N >= 96 && (double)g.M * g.N * g.K >= 1073741824.0;
+           !g.ones && !g.tail && g.K >= 64 && g.N >= 96 && (double)g.M * g.N * g.K >= 1073741824.0;
 }
 
 int gemm_splits(int64_t M, int64_t N, int64_t K, int T) {

@@ -325,7 +325,7 @@ int nbx_debug_msg_pre_check(uint32_t* mismatches, int32_t reset);
  * NBX_GEMM_TRANS_A, [K][M]; op(B) [K][N]: B stored [K][N] (ldb) or, with NBX_GEMM_TRANS_B, [N][K].
  * fp32 MFMA (v_mfma_f32_32x32x2_f32), 64 x 64 tiles; small-M N, long-K products (weight gradients)
  * split K over the workspace (nbx_gemm_f32_workspace_bytes) and sum the splits in order.  Large
- * C = A B^T products (flags exactly NBX_GEMM_TRANS_B, plain rows, no K split, K >= 256, N >= 96, >= 2^30
+ * C = A B^T products (flags exactly NBX_GEMM_TRANS_B, plain rows, no K split, K >= 64, N >= 96, >= 2^30
  * multiply-adds, 16-byte aligned operands; in a batched / grouped launch: when every problem qualifies)
  * run on the bf16x3 split MFMA since r06: six bf16 products per fp32 product, fp32 accumulation,
  * fp32-level accuracy but not bitwise the fp32-MFMA result; NBX_GEMM_X3=0 keeps them on fp32 MFMA. */

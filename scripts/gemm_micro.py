@@ -27,6 +27,8 @@ GROUPS = {
     "l6_conv1": [(2, 24320, 96, 896), (2, 24320, 448, 896), (2, 24320, 768, 1536), (2, 24320, 640, 1280)],
     "l6_conv2": [(2, 24320, 112, 448), (2, 24320, 192, 768), (2, 24320, 160, 640)],
     "l6_rad1152": [(2, 24320, 64, 1152)],
+    "l6_rad2304": [(2, 24320, 2304, 64)],
+    "l6_rad448": [(2, 24320, 448, 64)],
 }
 
 

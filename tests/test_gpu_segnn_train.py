@@ -118,7 +118,7 @@ def test_gemm_f32_grouped_bias_and_two_level_rows(hip_device, M, N, K):
 
 @pytest.mark.parametrize("M,N,K,beta", [(8190, 160, 1000, 0.0), (8192, 128, 1024, 1.0), (4100, 452, 900, 0.0)])
 def test_gemm_x3_large_products_match_fp64(hip_device, M, N, K, beta):
-    """The bf16x3 kernel (gemm_x3_ok: C = A B^T on plain rows, >= 2^30 multiply-adds, K >= 256, N >= 96;
+    """The bf16x3 kernel (gemm_x3_ok: C = A B^T on plain rows, >= 2^30 multiply-adds, K >= 64, N >= 96;
     tails in M, N and K) against fp64 torch at the fp32 kernels' bound, with the epilogue bias; one
     problem through nbx_gemm_f32 and the same problem in a two-problem nbx_gemm_f32_grouped launch agree
     bit for bit."""
