@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBX_LIB") or os.path.join(_HERE, "lib", "libnbx.so")  # NBX_LIB: A/B builds only
-ABI_VERSION = 18
+ABI_VERSION = 19
 COMM_ID_BYTES = 128
 ROLLOUT_ABSOLUTE = 1   # NBX_ROLLOUT_ABSOLUTE
 GEMM_TRANS_A, GEMM_TRANS_B, GEMM_B_ONES, GEMM_ONES_TAIL = 1, 2, 4, 8
@@ -178,6 +178,8 @@ _SIGNATURES = {
     "nbx_eqv2_wigner": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "nbx_eqv2_rotate_general": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p,
                                                 c_p]),
+    "nbx_eqv2_rotate_gather": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_p, c_p, c_i32,
+                                               c_p, c_p]),
     "nbx_eqv2_rms_norm_general": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "nbx_eqv2_rms_norm_general_backward": (ctypes.c_int, [c_i64, c_i32, c_i32] + [c_p] * 7),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),

@@ -128,17 +128,25 @@ __device__ __forceinline__ float inv_rescale(int l, int mmax) {
 // m-primary order of SO2_Convolution, so the SO(2) blocks read contiguous rows without a permutation.
 // UNI (C a multiple of 64): a wave's lanes share one edge, made explicit with readfirstlane, so the
 // edge's Wigner block and the row order are read once per wave through the scalar cache instead of
-// once per lane (455 per-lane loads per output channel at lmax 6 / mmax 2)
-template <int MODE, bool UNI>
+// once per lane (455 per-lane loads per output channel at lmax 6 / mmax 2).
+// GATHER (MODE 0): in is the node array [V][(lmax+1)^2][C / 2] (ld_in floats per node) and edge e's
+// input is [in[src[e]] | in[dst[e]]] per coefficient -- the attention's gathered message, read in
+// place instead of materialised (nbx_eqv2_rotate_gather)
+template <int MODE, bool UNI, bool GATHER = false>
 __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax, int S, int R,
                                            const float* __restrict__ D, const float* __restrict__ in, int64_t ld_in,
-                                           float* __restrict__ out, int rescale, const int* __restrict__ order) {
+                                           float* __restrict__ out, int rescale, const int* __restrict__ order,
+                                           const int* __restrict__ src = nullptr,
+                                           const int* __restrict__ dst = nullptr) {
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (t >= E * C) return;
     const int64_t e = UNI ? (int64_t)__builtin_amdgcn_readfirstlane((int)(t / C)) : t / C;
     const int c = (int)(t - e * C);
     const float* d = D + e * S;
-    const float* x = in + e * ld_in + c;
+    const int half = C >> 1;
+    const float* x = GATHER ? (c < half ? in + (int64_t)src[e] * ld_in + c : in + (int64_t)dst[e] * ld_in + (c - half))
+                            : in + e * ld_in + c;
+    const int xs = GATHER ? half : C;   // stride between the coefficient rows of x
     const int K = (lmax + 1) * (lmax + 1);
     float* o = out + e * (int64_t)(MODE == 0 ? R : K) * C + c;
     int doff = 0, roff = 0;
@@ -148,7 +156,7 @@ __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax,
         if (MODE == 0) {
             float v[GN_MAX];
 #pragma unroll
-            for (int j = 0; j < GN_MAX; ++j) v[j] = j < n ? x[(int64_t)(l * l + j) * C] : 0.f;
+            for (int j = 0; j < GN_MAX; ++j) v[j] = j < n ? x[(int64_t)(l * l + j) * xs] : 0.f;
             for (int i = 0; i < kl; ++i) {
                 const float* di = d + doff + i * n;
                 float a = 0.f;
@@ -327,11 +335,33 @@ extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32
     const bool uni = C % 64 == 0;
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R, dsel, in, ld_in, out,
-                           rescale, order);
+                           rescale, order, (const int*)nullptr, (const int*)nullptr);
     };
     if (inverse) uni ? go(eqv2_rotate_general_kernel<1, true>) : go(eqv2_rotate_general_kernel<1, false>);
     else uni ? go(eqv2_rotate_general_kernel<0, true>) : go(eqv2_rotate_general_kernel<0, false>);
     NBX_LAUNCH_CHECK("eqv2_rotate_general");
+    return NBX_OK;
+}
+
+extern "C" int nbx_eqv2_rotate_gather(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel,
+                                      const float* X, int64_t ld_x, const int32_t* src, const int32_t* dst, float* out,
+                                      int32_t rescale, const int32_t* order, void* stream) {
+    NBX_CHECK_ARG(E >= 0 && C >= 1 && mmax >= 0 && mmax <= lmax && lmax <= GL_MAX,
+                  "nbx_eqv2_rotate_gather: need C >= 1, 0 <= mmax <= lmax <= %d", GL_MAX);
+    const int R = kept_rows(lmax, mmax), K = (lmax + 1) * (lmax + 1);
+    NBX_CHECK_ARG(ld_x >= (int64_t)K * C, "nbx_eqv2_rotate_gather: ld_x too small");
+    if (E == 0) return NBX_OK;
+    NBX_CHECK_ARG(dsel && X && src && dst && out, "nbx_eqv2_rotate_gather: null operand");
+    NBX_CHECK_ARG(2 * E * C < ((int64_t)1 << 31), "nbx_eqv2_rotate_gather: 2 E C >= 2^31");
+    hipStream_t st = (hipStream_t)stream;
+    const int S = dsel_floats(lmax, mmax), C2 = 2 * C;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(nblk(E * C2)), dim3(256), 0, st, E, C2, lmax, mmax, S, R, dsel, X, ld_x, out,
+                           rescale, order, src, dst);
+    };
+    if (C % 64 == 0) go(eqv2_rotate_general_kernel<0, true, true>);
+    else go(eqv2_rotate_general_kernel<0, false, true>);
+    NBX_LAUNCH_CHECK("eqv2_rotate_gather");
     return NBX_OK;
 }
 

@@ -453,6 +453,43 @@ def gather_pair(X, g):
     return _GatherPairFn.apply(X, g)
 
 
+class _RotateGatherFn(torch.autograd.Function):
+    """General degrees: rotate(gather_pair(X, g)) in one pass (nbx_eqv2_rotate_gather): X [V][(lmax+1)^2][C]
+    -> [E][R][2C], the [E][(lmax+1)^2][2C] gathered message never written.  Backward: the rotation's
+    adjoint (nbx_eqv2_rotate_general, inverse = 1) into the gathered layout, then the gather's two
+    segment sums (as _GatherPairFn)."""
+
+    @staticmethod
+    def forward(ctx, X, g, D, lay, order):
+        X = X.contiguous()
+        V, K, C = X.shape
+        E = g.src.shape[0]
+        out = torch.empty(E, lay.n_red, 2 * C, device=X.device, dtype=_f32)
+        _lib.check(_lib.lib().nbx_eqv2_rotate_gather(E, C, lay.lmax, lay.mmax, _dp(D), _dp(X), K * C, _dp(g.src),
+                                                     _dp(g.dst), _dp(out), 0, _dp(order), _st(X)),
+                   "nbx_eqv2_rotate_gather")
+        ctx.save_for_backward(D, order)
+        ctx.g, ctx.lay, ctx.shape = g, lay, (V, K, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, dY):
+        D, order = ctx.saved_tensors
+        lay, g = ctx.lay, ctx.g
+        V, K, C = ctx.shape
+        dY = dY.contiguous()
+        E = dY.shape[0]
+        dG = torch.empty(E, K, 2 * C, device=dY.device, dtype=_f32)
+        L = _lib.lib()
+        _lib.check(L.nbx_eqv2_rotate_general(E, 2 * C, lay.lmax, lay.mmax, _dp(D), _dp(dY), dY.shape[1] * 2 * C,
+                                             _dp(dG), 1, 0, _dp(order), _st(dY)), "nbx_eqv2_rotate_general")
+        dX = torch.empty(V, K, C, device=dY.device, dtype=_f32)
+        for h, (ptr, eid) in enumerate(((g.sptr, g.seid), (g.dptr, g.deid))):
+            _lib.check(L.nbx_segment_sum(V, C, _dp(ptr), _dp(eid), _at(dG, h * C), 2 * K * C, 2 * C, _dp(dX), K * C,
+                                         C, K, h, _st(dG)), "nbx_segment_sum")
+        return dX, None, None, None, None
+
+
 class _Step:
     """Per-forward state: the graph, edge frames, distance expansion and dropout settings."""
 
@@ -587,7 +624,8 @@ class _Step:
         m, g, E, V = self.m, self.g, self.E, self.V
         nh, na, nv, H = m.num_heads, m.attn_alpha_channels, m.attn_value_channels, m.attn_hidden_channels
         x_edge = self.x_edge(A)
-        msg = self.rotate(gather_pair(x, g))
+        msg = _RotateGatherFn.apply(x, g, self.D, self.lay, self.order) if self.general \
+            else self.rotate(gather_pair(x, g))
         msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
         a_in, gating = torch.split(extra, [nh * na, H], dim=1)
         s2 = torch.split(_S2Fn.apply(msg, *self.grid_attn), [1, msg.shape[1] - 1], dim=1)[1]

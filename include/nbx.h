@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NBX_ABI_VERSION 18
+#define NBX_ABI_VERSION 19
 
 #define NBX_OK 0
 #define NBX_E_INVAL 1      /* bad argument (shape, size, pointer) */
@@ -564,6 +564,16 @@ int nbx_eqv2_wigner(int64_t E, int32_t lmax, int32_t mmax, const float* rot, int
 int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel, const float* in,
                             int64_t ld_in, float* out, int32_t inverse, int32_t rescale, const int32_t* order,
                             void* stream);
+
+/* ABI 19.  The attention's gathered message rotated in one pass (transformer_block.py:281-289 then
+ * SO3_Rotation.rotate): out [E][R][2C] = rotate of in'[e] = [X[src[e]] | X[dst[e]]] per coefficient,
+ * X [V][(lmax+1)^2][C] with ld_x floats per node, src / dst int32 [E]; rescale and order as
+ * nbx_eqv2_rotate_general with inverse = 0, and bit-identical to it on the materialised in' (which is
+ * never written).  Its adjoint is nbx_eqv2_rotate_general (inverse = 1) followed by the segment sums of
+ * the gather. */
+int nbx_eqv2_rotate_gather(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel, const float* X,
+                           int64_t ld_x, const int32_t* src, const int32_t* dst, float* out, int32_t rescale,
+                           const int32_t* order, void* stream);
 
 /* EquivariantRMSNormArraySphericalHarmonicsV2 (layer_norm.py:327-441) of X [V][(lmax+1)^2][C], any C:
  * weight [lmax+1][C], bias [C], balance weights float32(1/(2l+1)) / (lmax+1); save [2][V]; backward

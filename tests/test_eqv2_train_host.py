@@ -121,6 +121,8 @@ def torch_ops(monkeypatch):
     monkeypatch.setattr(T, "_RMSNormFn", _fn(lambda X, w, b, eps: EQ.rms_norm_sh(
         {"n.affine_weight": w, "n.affine_bias": b}, "n", X, 2, eps)))
     monkeypatch.setattr(T, "_RotateGFn", _fn(_rotate_general))
+    monkeypatch.setattr(T, "_RotateGatherFn", _fn(lambda X, g, D, lay, order: _rotate_general(
+        torch.cat([X[g.src], X[g.dst]], 2), D, lay, 0, 0, order)))
     monkeypatch.setattr(T, "_RMSNormGFn", _fn(lambda X, w, b, eps, lmax: EQ.rms_norm_sh(
         {"n.affine_weight": w, "n.affine_bias": b}, "n", X, lmax, eps)))
     monkeypatch.setattr(T, "_SegSumFn", _fn(lambda X, idx, p, e, V: torch.zeros(V, X.shape[1], dtype=X.dtype)

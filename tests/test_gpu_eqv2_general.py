@@ -162,6 +162,40 @@ def test_general_operators_match_torch(hip_device, lmax, mmax):
             _close(a.grad, r.grad, 1e-4, f"rms norm {name} C={Cn}")
 
 
+@pytest.mark.parametrize("C", [24, 64])
+def test_rotate_gather_equals_gather_then_rotate(hip_device, C):
+    """nbx_eqv2_rotate_gather (ABI 19; the attention's [x[src] | x[dst]] rotated without materialising
+    it) is bit-identical to gather_pair followed by the rotation, forward and input gradient, on the
+    m-primary row order, at C = 24 (per-lane Wigner reads) and C = 64 (wave-uniform edge, scalar
+    reads: that rotation path is also checked against fp64 torch here)."""
+    from nbody_amd.graph import fc_edge_index
+    from nbody_amd.segnn_train import Graph
+    dev = hip_device
+    lmax, mmax, B, N = 6, 2, 2, 6
+    V = B * N
+    g = Graph(fc_edge_index(B, N, dev), V, dev)
+    E = g.src.shape[0]
+    lay = so3.Layout(lmax, mmax)
+    R = _rotations(E, 17)
+    D = _wigner_rows(R, lmax, mmax, dev)
+    order = torch.tensor(lay.inv_perm, dtype=torch.int32, device=dev)
+    X = torch.randn(V, lay.n_full, C, generator=torch.Generator().manual_seed(C), dtype=torch.float64)
+    dy = torch.randn(E, lay.n_red, 2 * C, generator=torch.Generator().manual_seed(C + 1)).to(dev)
+    xa = X.float().to(dev).requires_grad_()
+    xb = X.float().to(dev).requires_grad_()
+    fused = T._RotateGatherFn.apply(xa, g, D, lay, order)
+    ref = T._RotateGFn.apply(T.gather_pair(xb, g), D, lay, 0, 0, order)
+    (fused * dy).sum().backward()
+    (ref * dy).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(fused, ref)
+    assert torch.equal(xa.grad, xb.grad)
+    src, dst = g.src.long().cpu(), g.dst.long().cpu()
+    Dd = EQ.wigner(R, lmax)[:, lay.sel, :]
+    want = torch.bmm(Dd, torch.cat([X[src], X[dst]], 2))[:, lay.perm]
+    _close(fused, want, 1e-5, f"rotate gather C={C}")
+
+
 def _fixture_model(tag, device):
     torch.manual_seed(0)
     m = EquiformerV2_nbody(**STATE6[tag]["config"])
