@@ -154,17 +154,23 @@ __global__ __launch_bounds__(NT) void eqv2_s2_kernel(int64_t rows, int I, int P,
         if (i < I) out[base + (int64_t)i * H] = o[i];
 }
 
+#ifndef NBX_S2_NT32
+#define NBX_S2_NT32 512
+#endif
+// block threads of the I <= 32 form (-DNBX_S2_NT32 A/B builds): eqv2_l6 63.3 steps/s at 512 against 63.1 at
+// 256 and 62.0 at 1 024, same box (profiles/r06/s2_l6/nt_*)
+constexpr int S2_NT32 = NBX_S2_NT32;
+
 template <bool BWD>
 int s2_launch(int64_t rows, int I, int P, int H, const float* T, const float* F, const float* X, const float* dOut,
               float* out, hipStream_t st) {
     const size_t lds = 2 * (size_t)P * ((I + 3) / 4 * 4) * sizeof(float);
     const int which = I <= 9 ? 0 : I <= 32 ? 1 : 2;
-    // one copy of the grid matrices per block: the large-I forms take 512 / 1024 threads, so the LDS
-    // that limits a CU to one or two blocks still holds 2 / 4 waves per SIMD (VGPRs allow it up to I 49 /
-    // 32); the lmax 2 form keeps 256
-    const int nt = which == 0 ? 256 : which == 1 ? 1024 : 512;
+    // one copy of the grid matrices per block: the large-I forms take 512 threads, so the LDS that
+    // limits a CU to one or two blocks still holds 2+ waves per SIMD; the lmax 2 form keeps 256
+    const int nt = which == 0 ? 256 : which == 1 ? S2_NT32 : 512;
     auto kern = which == 0 ? eqv2_s2_kernel<9, BWD, 256>
-              : which == 1 ? eqv2_s2_kernel<32, BWD, 1024> : eqv2_s2_kernel<S2_MAXI, BWD, 512>;
+              : which == 1 ? eqv2_s2_kernel<32, BWD, S2_NT32> : eqv2_s2_kernel<S2_MAXI, BWD, 512>;
     if (lds > 64 * 1024) NBX_LDS_160K(kern);
     hipLaunchKernelGGL(kern, dim3(nblk(rows * H, nt)), dim3(nt), lds, st, rows, I, P, H, T, F, X, dOut, out);
     return NBX_OK;
