@@ -179,7 +179,7 @@ _SIGNATURES = {
     "nbx_eqv2_rotate_general": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p,
                                                 c_p]),
     "nbx_eqv2_rotate_gather": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_p, c_p, c_i32,
-                                               c_p, c_p]),
+                                               c_p, c_p, c_i64, c_p, c_p]),
     "nbx_eqv2_rms_norm_general": (ctypes.c_int, [c_i64, c_i32, c_i32, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "nbx_eqv2_rms_norm_general_backward": (ctypes.c_int, [c_i64, c_i32, c_i32] + [c_p] * 7),
     "nbx_segnn_workspace_bytes": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_sz)]),

@@ -132,12 +132,17 @@ __device__ __forceinline__ float inv_rescale(int l, int mmax) {
 // GATHER (MODE 0): in is the node array [V][(lmax+1)^2][C / 2] (ld_in floats per node) and edge e's
 // input is [in[src[e]] | in[dst[e]]] per coefficient -- the attention's gathered message, read in
 // place instead of materialised (nbx_eqv2_rotate_gather)
+// rad (GATHER, nullable): output row j of edge e is multiplied by rad[e ld_rad + radrow[j] C + c], the
+// SO(2) convolution's radial weights applied in the epilogue (inference; the same single rounding as
+// the separate product)
 template <int MODE, bool UNI, bool GATHER = false>
 __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax, int S, int R,
                                            const float* __restrict__ D, const float* __restrict__ in, int64_t ld_in,
                                            float* __restrict__ out, int rescale, const int* __restrict__ order,
                                            const int* __restrict__ src = nullptr,
-                                           const int* __restrict__ dst = nullptr) {
+                                           const int* __restrict__ dst = nullptr,
+                                           const float* __restrict__ rad = nullptr, int64_t ld_rad = 0,
+                                           const int* __restrict__ radrow = nullptr) {
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (t >= E * C) return;
     const int64_t e = UNI ? (int64_t)__builtin_amdgcn_readfirstlane((int)(t / C)) : t / C;
@@ -163,7 +168,9 @@ __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax,
 #pragma unroll
                 for (int j = 0; j < GN_MAX; ++j)
                     if (j < n) a += di[j] * v[j];
-                o[(int64_t)(order ? order[roff + i] : roff + i) * C] = s * a;
+                const int j = order ? order[roff + i] : roff + i;
+                const float y = s * a;
+                o[(int64_t)j * C] = (GATHER && rad) ? y * rad[e * ld_rad + (int64_t)radrow[j] * C + c] : y;
             }
         } else {
             float v[GN_MAX];
@@ -335,7 +342,8 @@ extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32
     const bool uni = C % 64 == 0;
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R, dsel, in, ld_in, out,
-                           rescale, order, (const int*)nullptr, (const int*)nullptr);
+                           rescale, order, (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, (int64_t)0,
+                           (const int*)nullptr);
     };
     if (inverse) uni ? go(eqv2_rotate_general_kernel<1, true>) : go(eqv2_rotate_general_kernel<1, false>);
     else uni ? go(eqv2_rotate_general_kernel<0, true>) : go(eqv2_rotate_general_kernel<0, false>);
@@ -345,19 +353,21 @@ extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32
 
 extern "C" int nbx_eqv2_rotate_gather(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel,
                                       const float* X, int64_t ld_x, const int32_t* src, const int32_t* dst, float* out,
-                                      int32_t rescale, const int32_t* order, void* stream) {
+                                      int32_t rescale, const int32_t* order, const float* rad, int64_t ld_rad,
+                                      const int32_t* radrow, void* stream) {
     NBX_CHECK_ARG(E >= 0 && C >= 1 && mmax >= 0 && mmax <= lmax && lmax <= GL_MAX,
                   "nbx_eqv2_rotate_gather: need C >= 1, 0 <= mmax <= lmax <= %d", GL_MAX);
     const int R = kept_rows(lmax, mmax), K = (lmax + 1) * (lmax + 1);
     NBX_CHECK_ARG(ld_x >= (int64_t)K * C, "nbx_eqv2_rotate_gather: ld_x too small");
     if (E == 0) return NBX_OK;
     NBX_CHECK_ARG(dsel && X && src && dst && out, "nbx_eqv2_rotate_gather: null operand");
+    NBX_CHECK_ARG(!rad || (radrow && ld_rad >= 2 * C), "nbx_eqv2_rotate_gather: rad needs radrow and ld_rad >= 2 C");
     NBX_CHECK_ARG(2 * E * C < ((int64_t)1 << 31), "nbx_eqv2_rotate_gather: 2 E C >= 2^31");
     hipStream_t st = (hipStream_t)stream;
     const int S = dsel_floats(lmax, mmax), C2 = 2 * C;
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nblk(E * C2)), dim3(256), 0, st, E, C2, lmax, mmax, S, R, dsel, X, ld_x, out,
-                           rescale, order, src, dst);
+                           rescale, order, src, dst, rad, ld_rad, radrow);
     };
     if (C % 64 == 0) go(eqv2_rotate_general_kernel<0, true, true>);
     else go(eqv2_rotate_general_kernel<0, false, true>);

@@ -453,6 +453,31 @@ def gather_pair(X, g):
     return _GatherPairFn.apply(X, g)
 
 
+def radial_rows(lay):
+    """Radial block row of each m-primary coefficient row (SO2_Convolution, so2_ops.py:118-121): the m = 0
+    rows one each, then per m > 0 the +m and the -m rows of its n_m coefficients sharing one row each."""
+    rows, r0 = list(range(lay.m_size[0])), lay.m_size[0]
+    for mm in range(1, lay.mmax + 1):
+        nm = lay.m_size[mm]
+        rows += [r0 + i for i in range(nm)] * 2
+        r0 += nm
+    return rows
+
+
+def rotate_gather_radial(X, g, D, lay, order, rad, radrow):
+    """Inference only (no autograd): _RotateGatherFn's output times SO2_Convolution's radial weights rad
+    [E][(n0 + sum n_m) 2C], fused in the rotation's epilogue (nbx_eqv2_rotate_gather with rad): the
+    x * rad product of the convolution (so2_ops.py:118-121) never materialises separately."""
+    X, rad = X.contiguous(), rad.contiguous()
+    V, K, C = X.shape
+    E = g.src.shape[0]
+    out = torch.empty(E, lay.n_red, 2 * C, device=X.device, dtype=_f32)
+    _lib.check(_lib.lib().nbx_eqv2_rotate_gather(E, C, lay.lmax, lay.mmax, _dp(D), _dp(X), K * C, _dp(g.src),
+                                                 _dp(g.dst), _dp(out), 0, _dp(order), _dp(rad), rad.shape[1],
+                                                 _dp(radrow), _st(X)), "nbx_eqv2_rotate_gather")
+    return out
+
+
 class _RotateGatherFn(torch.autograd.Function):
     """General degrees: rotate(gather_pair(X, g)) in one pass (nbx_eqv2_rotate_gather): X [V][(lmax+1)^2][C]
     -> [E][R][2C], the [E][(lmax+1)^2][2C] gathered message never written.  Backward: the rotation's
@@ -466,7 +491,7 @@ class _RotateGatherFn(torch.autograd.Function):
         E = g.src.shape[0]
         out = torch.empty(E, lay.n_red, 2 * C, device=X.device, dtype=_f32)
         _lib.check(_lib.lib().nbx_eqv2_rotate_gather(E, C, lay.lmax, lay.mmax, _dp(D), _dp(X), K * C, _dp(g.src),
-                                                     _dp(g.dst), _dp(out), 0, _dp(order), _st(X)),
+                                                     _dp(g.dst), _dp(out), 0, _dp(order), None, 0, None, _st(X)),
                    "nbx_eqv2_rotate_gather")
         ctx.save_for_backward(D, order)
         ctx.g, ctx.lay, ctx.shape = g, lay, (V, K, C)
@@ -540,6 +565,12 @@ class _Step:
                 + (torch.tensor(lay.inv_perm, device=dev, dtype=torch.int32),
                    torch.tensor([-1.0, 1.0], device=dev, dtype=_f32).view(1, 2, 1))
         self.perm, self.inv_perm, self.m0, self.order, self.sign = cache[dev]
+        # the radial block row of each m-primary row (SO2_Convolution: the m = 0 rows, then per m the +m and
+        # -m rows of its n_m coefficients sharing one radial row each); rotate_gather_radial
+        rcache = model.__dict__.setdefault("_eqv2_radrow_cache", {})
+        if dev not in rcache:
+            rcache[dev] = torch.tensor(radial_rows(lay), device=dev, dtype=torch.int32)
+        self.radrow = rcache[dev]
         # general operators: edge irreps stay in the m-primary order of the SO(2) convolutions end to end
         # (the rotation writes / reads rows through `order`, the attention grid's columns are permuted
         # once), so no feature permutation runs per convolution; the lmax-2 operators work l-primary
@@ -624,9 +655,14 @@ class _Step:
         m, g, E, V = self.m, self.g, self.E, self.V
         nh, na, nv, H = m.num_heads, m.attn_alpha_channels, m.attn_value_channels, m.attn_hidden_channels
         x_edge = self.x_edge(A)
-        msg = _RotateGatherFn.apply(x, g, self.D, self.lay, self.order) if self.general \
-            else self.rotate(gather_pair(x, g))
-        msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
+        if self.general and not torch.is_grad_enabled():   # inference: radial product in the rotation
+            rad = self.rad_func(A.so2_conv_1.rad_func, x_edge)
+            msg = rotate_gather_radial(x, g, self.D, self.lay, self.order, rad, self.radrow)
+            msg, extra = self.so2_conv(A.so2_conv_1, msg, None, H, n_extra=nh * na + H)
+        else:
+            msg = _RotateGatherFn.apply(x, g, self.D, self.lay, self.order) if self.general \
+                else self.rotate(gather_pair(x, g))
+            msg, extra = self.so2_conv(A.so2_conv_1, msg, x_edge, H, n_extra=nh * na + H)
         a_in, gating = torch.split(extra, [nh * na, H], dim=1)
         s2 = torch.split(_S2Fn.apply(msg, *self.grid_attn), [1, msg.shape[1] - 1], dim=1)[1]
         msg = torch.cat([act(gating.contiguous(), _lib.ACT_SILU)[:, None], s2], 1)

@@ -570,10 +570,14 @@ int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32_t mmax, co
  * X [V][(lmax+1)^2][C] with ld_x floats per node, src / dst int32 [E]; rescale and order as
  * nbx_eqv2_rotate_general with inverse = 0, and bit-identical to it on the materialised in' (which is
  * never written).  Its adjoint is nbx_eqv2_rotate_general (inverse = 1) followed by the segment sums of
- * the gather. */
+ * the gather.  rad (nullable, inference): out[e][j][c] is multiplied by rad[e ld_rad + radrow[j] 2C + c],
+ * SO2_Convolution's radial weights (so2_ops.py:118-121, one per (m, coefficient, channel), shared by the
+ * +m / -m rows; radrow int32 [R] maps each output row to its radial block row), bit-identical to the
+ * separate product. */
 int nbx_eqv2_rotate_gather(int64_t E, int32_t C, int32_t lmax, int32_t mmax, const float* dsel, const float* X,
                            int64_t ld_x, const int32_t* src, const int32_t* dst, float* out, int32_t rescale,
-                           const int32_t* order, void* stream);
+                           const int32_t* order, const float* rad, int64_t ld_rad, const int32_t* radrow,
+                           void* stream);
 
 /* EquivariantRMSNormArraySphericalHarmonicsV2 (layer_norm.py:327-441) of X [V][(lmax+1)^2][C], any C:
  * weight [lmax+1][C], bias [C], balance weights float32(1/(2l+1)) / (lmax+1); save [2][V]; backward

@@ -123,6 +123,9 @@ def torch_ops(monkeypatch):
     monkeypatch.setattr(T, "_RotateGFn", _fn(_rotate_general))
     monkeypatch.setattr(T, "_RotateGatherFn", _fn(lambda X, g, D, lay, order: _rotate_general(
         torch.cat([X[g.src], X[g.dst]], 2), D, lay, 0, 0, order)))
+    monkeypatch.setattr(T, "rotate_gather_radial", lambda X, g, D, lay, order, rad, radrow: _rotate_general(
+        torch.cat([X[g.src], X[g.dst]], 2), D, lay, 0, 0, order) * rad.view(rad.shape[0], -1, 2 * X.shape[2])[
+        :, radrow.long()])
     monkeypatch.setattr(T, "_RMSNormGFn", _fn(lambda X, w, b, eps, lmax: EQ.rms_norm_sh(
         {"n.affine_weight": w, "n.affine_bias": b}, "n", X, lmax, eps)))
     monkeypatch.setattr(T, "_SegSumFn", _fn(lambda X, idx, p, e, V: torch.zeros(V, X.shape[1], dtype=X.dtype)
@@ -138,6 +141,7 @@ def torch_ops(monkeypatch):
         self.perm, self.inv_perm, self.m0 = (torch.tensor(v) for v in (lay.perm, lay.inv_perm, lay.m0))
         self.order = torch.tensor(lay.inv_perm, dtype=torch.int32)
         self.sign = torch.tensor([-1.0, 1.0], dtype=torch.float64).view(1, 2, 1)
+        self.radrow = torch.tensor(T.radial_rows(lay))
         self.mprimary = self.general
         z = ctx.z
         self.g = _G(torch.stack([ctx.src, ctx.dst]), self.V)
@@ -154,6 +158,28 @@ def torch_ops(monkeypatch):
             ta, fa = ta[:, self.perm], fa[:, self.perm]
         self.grid_attn, self.grid_ffn = (ta, fa), (tf.reshape(-1, nf), ff.reshape(-1, nf))
     monkeypatch.setattr(T._Step, "__init__", step_init)
+
+
+@pytest.mark.parametrize("lmax,mmax", [(6, 2), (4, 3), (2, 1)])
+def test_inference_forward_radial_rows_match_oracle(torch_ops, lmax, mmax):
+    """Under no_grad the general path applies SO2_Convolution's radial product inside the gathered
+    rotation (rotate_gather_radial) through radial_rows' row map; with that map in a torch stand-in the
+    composed forward equals the oracle."""
+    torch.manual_seed(1)
+    cfg = dict(CFG, lmax_list=[lmax], mmax_list=[mmax])
+    m = EquiformerV2_nbody(**cfg, alpha_drop=0.0, drop_path_rate=0.0).double().eval()
+    m.specialised_ops = False
+    B, N = 2, 4
+    rng = np.random.default_rng(1)
+    loc = torch.tensor(rng.standard_normal((B * N, 3)))
+    vel = torch.tensor(rng.standard_normal((B * N, 3))) * 0.3
+    mass = torch.tensor(rng.integers(1, 4, B * N).astype(np.float64))
+    gauge = torch.tensor(rng.uniform(0, 1, (B * N * (N - 1), 3)))
+    with torch.no_grad():
+        got = T.train_forward(m, loc, vel, mass, B, N, gauge, 0)
+        P = {k: p.detach().clone() for k, p in m.named_parameters()}
+        ref = EQ.forward(cfg, P, loc, vel, mass, B, N, gauge)
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-13)
 
 
 @pytest.mark.parametrize("lmax,mmax,general", [(2, 1, False), (2, 1, True), (6, 2, True), (4, 3, True), (3, 0, True)])

@@ -196,6 +196,24 @@ def test_rotate_gather_equals_gather_then_rotate(hip_device, C):
     _close(fused, want, 1e-5, f"rotate gather C={C}")
 
 
+def test_inference_radial_in_rotation_is_bit_identical(hip_device):
+    """Under no_grad the attention applies SO2_Convolution's radial product in the gathered rotation's
+    epilogue (rotate_gather_radial); in grad mode it stays a separate product.  Both round the same
+    product once, so the lmax 6 fixture model's forward is bit-identical either way."""
+    m = _fixture_model("l6", hip_device)
+    loc, vel, mass = Z6["l6/loc"], Z6["l6/vel"], Z6["l6/mass"]
+    B, N = loc.shape[:2]
+    pos = _t(loc, B, N, hip_device)
+    batch = torch.arange(B, device=hip_device).repeat_interleave(N)
+    data = (pos, _t(vel, B, N, hip_device), torch.zeros_like(pos), _t(mass, B, N, hip_device), pos)
+    gauge = torch.as_tensor(Z6["l6/gauge"], dtype=torch.float32, device=hip_device)
+    with torch.no_grad():
+        fused = m(data, batch, gauge=gauge)
+    plain = m(data, batch, gauge=gauge)
+    assert plain.requires_grad
+    assert torch.equal(fused, plain.detach())
+
+
 def _fixture_model(tag, device):
     torch.manual_seed(0)
     m = EquiformerV2_nbody(**STATE6[tag]["config"])
