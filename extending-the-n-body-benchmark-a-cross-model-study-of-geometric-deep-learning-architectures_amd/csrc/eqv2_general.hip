@@ -135,7 +135,9 @@ __device__ __forceinline__ float inv_rescale(int l, int mmax) {
 // rad (GATHER, nullable): output row j of edge e is multiplied by rad[e ld_rad + radrow[j] C + c], the
 // SO(2) convolution's radial weights applied in the epilogue (inference; the same single rounding as
 // the separate product)
-template <int MODE, bool UNI, bool GATHER = false>
+// LDSD (C < 64 dividing the 256-thread block, not UNI): the block's 256 / C edges share a wave, so their
+// Wigner blocks are staged once in the LDS (coalesced) and read from there, not per lane from memory
+template <int MODE, bool UNI, bool GATHER = false, bool LDSD = false>
 __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax, int S, int R,
                                            const float* __restrict__ D, const float* __restrict__ in, int64_t ld_in,
                                            float* __restrict__ out, int rescale, const int* __restrict__ order,
@@ -143,11 +145,20 @@ __global__ void eqv2_rotate_general_kernel(int64_t E, int C, int lmax, int mmax,
                                            const int* __restrict__ dst = nullptr,
                                            const float* __restrict__ rad = nullptr, int64_t ld_rad = 0,
                                            const int* __restrict__ radrow = nullptr) {
+    extern __shared__ float rot_lds[];
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * (blockDim.x / C);   // LDSD: the block's first edge
+    if constexpr (LDSD) {
+        const int64_t n = std::min<int64_t>(blockDim.x / C, E - e0) * S;
+        for (int64_t k = threadIdx.x; k < n; k += blockDim.x) rot_lds[k] = D[e0 * S + k];
+        __syncthreads();
+    }
     if (t >= E * C) return;
     const int64_t e = UNI ? (int64_t)__builtin_amdgcn_readfirstlane((int)(t / C)) : t / C;
     const int c = (int)(t - e * C);
-    const float* d = D + e * S;
+    const float* d;
+    if constexpr (LDSD) d = rot_lds + (e - e0) * S;
+    else d = D + e * S;
     const int half = C >> 1;
     const float* x = GATHER ? (c < half ? in + (int64_t)src[e] * ld_in + c : in + (int64_t)dst[e] * ld_in + (c - half))
                             : in + e * ld_in + c;
@@ -340,13 +351,22 @@ extern "C" int nbx_eqv2_rotate_general(int64_t E, int32_t C, int32_t lmax, int32
     const int S = dsel_floats(lmax, mmax);
     NBX_CHECK_ARG(E * C < ((int64_t)1 << 31), "nbx_eqv2_rotate_general: E C >= 2^31");
     const bool uni = C % 64 == 0;
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(nblk(E * C)), dim3(256), 0, st, E, C, lmax, mmax, S, R, dsel, in, ld_in, out,
+    const size_t lds = (size_t)(256 / C) * S * sizeof(float);
+    const bool ldsd = !uni && 256 % C == 0 && lds <= 64 * 1024;
+    auto go = [&](auto kern, size_t shm) {
+        hipLaunchKernelGGL(kern, dim3(nblk(E * C)), dim3(256), shm, st, E, C, lmax, mmax, S, R, dsel, in, ld_in, out,
                            rescale, order, (const int*)nullptr, (const int*)nullptr, (const float*)nullptr, (int64_t)0,
                            (const int*)nullptr);
     };
-    if (inverse) uni ? go(eqv2_rotate_general_kernel<1, true>) : go(eqv2_rotate_general_kernel<1, false>);
-    else uni ? go(eqv2_rotate_general_kernel<0, true>) : go(eqv2_rotate_general_kernel<0, false>);
+    if (inverse) {
+        if (uni) go(eqv2_rotate_general_kernel<1, true>, 0);
+        else if (ldsd) go(eqv2_rotate_general_kernel<1, false, false, true>, lds);
+        else go(eqv2_rotate_general_kernel<1, false>, 0);
+    } else {
+        if (uni) go(eqv2_rotate_general_kernel<0, true>, 0);
+        else if (ldsd) go(eqv2_rotate_general_kernel<0, false, false, true>, lds);
+        else go(eqv2_rotate_general_kernel<0, false>, 0);
+    }
     NBX_LAUNCH_CHECK("eqv2_rotate_general");
     return NBX_OK;
 }

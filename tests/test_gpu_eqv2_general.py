@@ -162,6 +162,29 @@ def test_general_operators_match_torch(hip_device, lmax, mmax):
             _close(a.grad, r.grad, 1e-4, f"rms norm {name} C={Cn}")
 
 
+@pytest.mark.parametrize("C", [8, 16, 32])
+def test_rotate_small_channel_counts_stage_wigner_in_lds(hip_device, C):
+    """rotate / rotate_inv at channel counts dividing the 256-thread block (the attention's nh nv = 16 at
+    C4 widths): the block's Wigner blocks are staged in the LDS; E = 37 leaves a partial last block.
+    Against fp64 torch, with the m-primary order and the inverse rescale."""
+    dev, lmax, mmax, E = hip_device, 6, 2, 37
+    lay, olay = so3.Layout(lmax, mmax), EQ.Layout(lmax, mmax)
+    R = _rotations(E, 23)
+    Dfull = EQ.wigner(R, lmax)
+    D = _wigner_rows(R, lmax, mmax, dev)
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(E, lay.n_full, C, generator=g, dtype=torch.float64)
+    y = torch.randn(E, lay.n_red, C, generator=g, dtype=torch.float64)
+    order = torch.tensor(lay.inv_perm, dtype=torch.int32, device=dev)
+    perm = torch.tensor(lay.perm)
+    with torch.no_grad():
+        got_r = T._RotateGFn.apply(x.float().to(dev), D, lay, 0, 0, order)
+        got_i = T._RotateGFn.apply(y[:, perm].float().to(dev).contiguous(), D, lay, 1, 1, order)
+    _close(got_r, torch.bmm(Dfull[:, lay.sel, :], x)[:, perm], 1e-5, f"rotate C={C}")
+    _close(got_i, torch.bmm(Dfull.transpose(1, 2)[:, :, lay.sel] * olay.rescale[None], y), 1e-5,
+           f"rotate_inv C={C}")
+
+
 @pytest.mark.parametrize("C", [24, 64])
 def test_rotate_gather_equals_gather_then_rotate(hip_device, C):
     """nbx_eqv2_rotate_gather (ABI 19; the attention's [x[src] | x[dst]] rotated without materialising
